@@ -1,0 +1,195 @@
+"""bench.py — device-resident FedAvg reduce on MI355X (BASELINE.json metric).
+
+One "step" = one complete FedAvg aggregation of K client updates (default 64 x 100 M
+fp32, all resident in HBM) into a fresh aggregate: fedavg.py's fold loop
+``x <- x + (n_k*(y_k - x))/N_k`` over k = 1..K-1 in queue order, as ONE libfedagg
+launch. value = aggregated client-params/s = n_gpus * K * P / t_step.
+
+Multi-GPU (torchrun, one process per GPU): every rank aggregates its own parameter
+slice of P params (the global model is n_gpus * P params sharded by contiguous slice);
+no collective is on the data path ("scaling": "weak"). The RCCL all-gather that would
+reassemble the model on every GPU is timed separately and reported beside the line
+(``allgather``), not folded into ``value``.
+
+Also measured in the same run:
+  roofline      algorithmic bytes (K*P*4 + P*4 per launch) / average kernel time (HIP events
+                on the launch stream) vs the 8.0 TB/s HBM3E peak; ``traffic`` = HBM bytes per
+                launch from rocprofv3 PMC counters (profiles/pmc_*.json, collected by
+                tools/pmc_traffic.py), or null if not collected for this workload
+  cpu_baseline  the numpy restatement of numpyhelper.increment_average (oracle/, bit-equal to
+                FEDn) on a bounded sample (K clients x S params) on one host core; its result is
+                also compared bit-for-bit with the GPU aggregate of the same elements.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "aggregated params/sec (device-resident) — FedAvg 64-client reduce, 100M fp32"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--clients", type=int, default=64)
+    ap.add_argument("--params", type=int, default=100_000_000, help="params per GPU")
+    ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32")
+    ap.add_argument("--cpu-sample", type=int, default=25_000_000,
+                    help="params per client in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+def make_updates(K, P, dtype, device, seed):
+    """Synthetic client updates: base ~ N(0,1), client k = base + 0.01 N(0,1)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    base = torch.randn(P, generator=g, device=device)
+    ups = []
+    for _ in range(K):
+        u = torch.randn(P, generator=g, device=device).mul_(0.01).add_(base)
+        ups.append(u.to(torch.bfloat16) if dtype == "bf16" else u)
+    del base
+    torch.cuda.synchronize(device)
+    return ups
+
+
+def pmc_traffic(workload):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(workload)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(ups, ns, agg, S):
+    """Time the oracle (numpy, 1 core) on a K x S sample and check the GPU result on it."""
+    from oracle import numpy_ref as ref  # test infrastructure: the baseline/checker only
+
+    S = min(S, agg.numel())
+    sample = [u[:S].float().cpu().numpy() for u in ups]
+    t0 = time.perf_counter()
+    want = ref.fedavg_flat(sample, ns)
+    dt = time.perf_counter() - t0
+    got = agg[:S].cpu().numpy()
+    exact = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+    return {"value": len(ups) * S / dt, "unit": "params/s", "cores": 1, "kind": "port",
+            "sample": f"{len(ups)} clients x {S} fp32 params (first {S} of each client buffer); "
+                      f"numpy {np.__version__} oracle/numpy_ref.fedavg_flat, single-threaded, "
+                      f"{os.cpu_count()} host cores present", "seconds": dt,
+            "gpu_bit_exact_on_sample": exact}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from fedn_amd import _abi, ops
+    _abi.load()
+
+    K, P = a.clients, a.params
+    ups = make_updates(K, P, a.dtype, device, a.seed + 1000 * rank)
+    ns = [int(v) for v in np.random.default_rng(a.seed).integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
+    agg = torch.empty(P, dtype=torch.float32, device=device)
+    stream = torch.cuda.current_stream(device)
+
+    def step():
+        ops.fedavg_fold(agg, ups, ns, Ns, init=True, stream=stream)
+
+    for _ in range(a.warmup):
+        step()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        step()
+        e.record(stream)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(s.elapsed_time(e) for s, e in ev) / a.steps
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+
+    in_bytes = 2 if a.dtype == "bf16" else 4
+    alg_bytes = K * P * in_bytes + P * 4           # read every update once, write the aggregate once
+    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+    workload = f"fedavg_k{K}_p{P}_{a.dtype}"
+
+    allgather = None
+    if world > 1 and not a.no_allgather:
+        full = torch.empty(P * world, dtype=torch.float32, device=device)
+        for _ in range(2):
+            dist.all_gather_into_tensor(full, agg)
+        torch.cuda.synchronize(device)
+        dist.barrier()
+        t1 = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            dist.all_gather_into_tensor(full, agg)
+        torch.cuda.synchronize(device)
+        ag = torch.tensor([(time.perf_counter() - t1) / reps], dtype=torch.float64, device=device)
+        dist.all_reduce(ag, op=dist.ReduceOp.MAX)
+        ag_s = float(ag[0])
+        allgather = {"ms": ag_s * 1e3, "bytes_in_per_rank": (world - 1) * P * 4,
+                     "algbw_GBps": world * P * 4 / ag_s / 1e9,
+                     "busbw_GBps": (world - 1) * P * 4 / ag_s / 1e9, "backend": "rccl"}
+        del full
+
+    base = None
+    if rank == 0 and world == 1 and a.cpu_sample > 0:
+        base = cpu_baseline(ups, ns, agg, a.cpu_sample)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": world * K * P / (elapsed / a.steps), "unit": "params/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+            "data": "synthetic: base~N(0,1), client=base+0.01*N(0,1), num_examples~U{1..5000}, device-resident",
+            "config": {"workload": f"FedAvg {K} clients x {P} params {a.dtype} per GPU (BASELINE configs[1]/north "
+                                   "star; device-resident, one fused fold launch per aggregation)",
+                       "clients": K, "params_per_gpu": P, "global_params": P * world,
+                       "parallelism": f"param-slice shards x{world}, no data-path collective"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(workload),
+                         "kernel": "k_fedavg<float,float,CF32,4,INIT>", "kernel_ms": kern_ms,
+                         "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": base,
+        }
+        if allgather:
+            line["allgather"] = allgather
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,123 @@
+"""ctypes binding of ``libfedagg.so`` (C ABI declared in ``include/fedagg.h``).
+
+The library is the product path: if it is missing or fails to load, every entry
+point raises :class:`FedAggLibraryError`. There is no CPU fallback.
+
+``torch`` is imported before the library is opened so the HIP runtime that
+PyTorch-ROCm already loaded (SONAME ``libamdhip64.so.7``) is the one the library
+binds to; streams and device pointers handed over from torch are then valid in it.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libfedagg.so"
+LIB_PATH = os.path.join(_HERE, LIB_NAME)
+
+# element type codes (enum fa_dtype)
+FA_NONE, FA_F32, FA_F64, FA_BF16, FA_F16, FA_I32, FA_I64 = -1, 0, 1, 2, 3, 4, 5
+# status codes (enum fa_status)
+FA_OK, FA_EINVAL, FA_EDTYPE, FA_EHIP = 0, 1, 2, 3
+# server optimizers (enum fa_serveropt)
+FA_ADAM, FA_YOGI, FA_ADAGRAD = 0, 1, 2
+FA_PG_FIRST, FA_PG_FINAL = 1, 2
+
+EXPORTS = {
+    # name: (restype, argtypes)
+    "fa_abi_version": (ctypes.c_int, []),
+    "fa_last_error": (ctypes.c_char_p, []),
+    "fa_promote": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "fa_fedavg_fold": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_int,                       # agg, agg_dtype
+        ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,       # updates, upd_dtype
+        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int,  # n, N, K
+        ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),     # P, init, stream
+    "fa_fedopt_step": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_int,                       # old, old_dtype
+        ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,       # updates, upd_dtype
+        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int,  # n, N, K
+        ctypes.c_void_p, ctypes.c_int,                       # pg, flags
+        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,      # m_in, m_in_dtype, m_out
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,   # v_in, v_out, out
+        ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,  # opt, lr, b1, b2, tau
+        ctypes.c_int64, ctypes.c_void_p]),                   # P, stream
+    "fa_stream_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "fa_stream_read_blocks": (ctypes.c_int64, [ctypes.c_int64]),
+    "fa_stream_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+}
+
+ABI_VERSION = 1
+
+
+class FedAggLibraryError(ImportError):
+    """libfedagg.so is missing or unusable: the HIP path cannot run (no fallback)."""
+
+
+class FedAggError(RuntimeError):
+    """A libfedagg entry point returned a nonzero status."""
+
+    def __init__(self, status, message):
+        super().__init__(f"libfedagg status {status}: {message}")
+        self.status = status
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib_path():
+    return os.environ.get("FEDN_AMD_LIB", LIB_PATH)
+
+
+def load():
+    """Open libfedagg.so once (thread-safe) and attach the C signatures."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  (binds the library to torch's HIP runtime)
+
+        path = lib_path()
+        if not os.path.exists(path):
+            raise FedAggLibraryError(
+                f"{path} not found: build it first (python -c 'import __graft_entry__ as g; g.build()' "
+                "or python -m fedn_amd.build). The HIP library is required; there is no CPU fallback.")
+        try:
+            lib = ctypes.CDLL(path)
+        except OSError as e:
+            raise FedAggLibraryError(f"cannot load {path}: {e}") from e
+        for name, (res, args) in EXPORTS.items():
+            try:
+                fn = getattr(lib, name)
+            except AttributeError as e:
+                raise FedAggLibraryError(f"{path} does not export {name}") from e
+            fn.restype = res
+            fn.argtypes = args
+        ver = lib.fa_abi_version()
+        if ver != ABI_VERSION:
+            raise FedAggLibraryError(f"{path}: ABI version {ver}, expected {ABI_VERSION}; rebuild it")
+        _lib = lib
+        return lib
+
+
+def check(status):
+    if status != FA_OK:
+        msg = load().fa_last_error()
+        raise FedAggError(status, msg.decode(errors="replace") if msg else "")
+
+
+def ptr_array(ptrs):
+    arr = (ctypes.c_void_p * max(1, len(ptrs)))()
+    for i, p in enumerate(ptrs):
+        arr[i] = ctypes.c_void_p(int(p))
+    return arr
+
+
+def double_array(vals):
+    arr = (ctypes.c_double * max(1, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = float(v)
+    return arr

@@ -1,0 +1,82 @@
+"""FedAvg aggregator plug-in — drop-in for fedn/network/combiner/aggregators/fedavg.py.
+
+Same contract and observable behaviour as fedavg.py:8-83:
+  * drains ``update_handler.model_updates`` in FIFO order (fedavg.py:109-112);
+  * ``total_examples`` grows BEFORE the fold (fedavg.py:124), so an update whose fold
+    fails is skipped but still counted; a load failure is skipped uncounted;
+  * the first update is the model (fedavg.py:127-128): K = 1 returns it unchanged;
+  * returns ``(model, data)`` with ``time_model_load``, ``time_model_aggregation``,
+    ``nr_aggregated_models`` (fedavg.py:99-101, 142), ``(None, data)`` if nothing folded.
+The fold ``x + (n*(y-x))/N`` (numpyhelper.py:32) runs in libfedagg on the GPU, bit-exact;
+updates are staged through pinned memory and folded on arrival (fedn_amd/staging.py).
+Extra ``data`` keys: ``time_h2d`` / ``time_kernel`` (HIP events), ``time_pack``, ``time_d2h``.
+"""
+import logging
+import os
+import time
+import traceback
+
+import torch
+
+from ..staging import FedAvgPipeline
+from .aggregatorbase import AggregatorBase
+
+logger = logging.getLogger("fedn")
+
+
+def default_device():
+    dev = os.environ.get("FEDN_AMD_DEVICE")
+    if dev:
+        return torch.device(dev)
+    if not torch.cuda.is_available():
+        raise RuntimeError("fedn_amd aggregators need a HIP device (torch.cuda.is_available() is False)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class Aggregator(AggregatorBase):
+    """Federated Averaging on MI355X (weighted incremental mean of client updates)."""
+
+    def __init__(self, update_handler, device=None):
+        super().__init__(update_handler)
+        self.name = "fedavg"
+        self.device = torch.device(device) if device is not None else None
+
+    def combine_models(self, helper=None, delete_models=True, parameters=None):
+        data = {"time_model_load": 0.0, "time_model_aggregation": 0.0}
+        model = None
+        nr_aggregated_models = 0
+        total_examples = 0
+        pipe = None
+
+        logger.info("AGGREGATOR({}): Aggregating model updates... ".format(self.name))
+        while not self.update_handler.model_updates.empty():
+            try:
+                model_update = self.update_handler.next_model_update()
+                tic = time.time()
+                model_next, metadata = self.update_handler.load_model_update(model_update, helper)
+                data["time_model_load"] += time.time() - tic
+
+                total_examples += metadata["num_examples"]
+
+                tic = time.time()
+                if nr_aggregated_models == 0:
+                    pipe = FedAvgPipeline(self.device or default_device(), model_next)
+                else:
+                    pipe.add(model_next, metadata["num_examples"], total_examples)
+                data["time_model_aggregation"] += time.time() - tic
+
+                nr_aggregated_models += 1
+                if delete_models:
+                    self.update_handler.delete_model(model_update)
+            except Exception as e:  # noqa: BLE001 — fedavg.py:137-140: log and continue
+                logger.error(f"AGGREGATOR({self.name}): Error encoutered while processing model update: {e}")
+                logger.error(traceback.format_exc())
+
+        data["nr_aggregated_models"] = nr_aggregated_models
+        if pipe is not None:
+            tic = time.time()
+            model = pipe.result()
+            data["time_model_aggregation"] += time.time() - tic
+            data.update(pipe.timings())
+        logger.info("AGGREGATOR({}): Aggregation completed, aggregated {} models.".format(self.name, nr_aggregated_models))
+        return model, data

@@ -1,0 +1,109 @@
+"""FedOpt aggregator plug-in (FedAdam / FedYogi / FedAdaGrad) — drop-in for
+fedn/network/combiner/aggregators/fedopt.py.
+
+Same contract and observable behaviour as fedopt.py:13-258:
+  * hyper-parameters: defaults {serveropt: adam, learning_rate: 1e-3, beta1: 0.9,
+    beta2: 0.99, tau: 1e-4} merged with validated user kwargs; invalid ones return
+    ``(None, data)`` without touching the queue (fedopt.py:52-66, 123-137);
+  * the pseudo-gradient is the running weighted mean of ``update - model_old``, where
+    ``model_old`` is the model the first folded update names (fedopt.py:89-94);
+  * server step without bias correction; ``m``, ``v`` persist on the instance across the
+    rounds of a session (fedopt.py:36-38) — here they stay resident in HBM;
+  * an unknown ``serveropt`` drains the queue and returns ``(None, data)`` (fedopt.py:110-116);
+  * output dtype float64 (``v`` starts as ``np.ones(...) * tau**2``, numpyhelper.py:141).
+The whole reduction runs in libfedagg (bit-exact to the numpy reference).
+"""
+import logging
+import time
+import traceback
+
+from ..exceptions import InvalidParameterError
+from ..parameters import Parameters
+from ..staging import FedOptPipeline, FedOptState
+from .aggregatorbase import AggregatorBase
+from .fedavg import default_device
+
+logger = logging.getLogger("fedn")
+
+import torch  # noqa: E402
+
+DEFAULT_PARAMETERS = {"serveropt": "adam", "learning_rate": 1e-3, "beta1": 0.9, "beta2": 0.99, "tau": 1e-4}
+PARAMETER_SCHEMA = {"serveropt": str, "learning_rate": float, "beta1": float, "beta2": float, "tau": float}
+
+
+class Aggregator(AggregatorBase):
+    """Federated Optimization (FedOpt) on MI355X."""
+
+    def __init__(self, update_handler, device=None):
+        super().__init__(update_handler)
+        self.name = "fedopt"
+        self.device = torch.device(device) if device is not None else None
+        self.state = FedOptState()
+
+    # reference attribute names (fedopt.py:37-38): host copies of the HBM-resident state
+    @property
+    def m(self):
+        return self.state.m_host()
+
+    @property
+    def v(self):
+        return self.state.v_host()
+
+    def combine_models(self, helper=None, delete_models=True, parameters=None):
+        data = {"time_model_load": 0.0, "time_model_aggregation": 0.0}
+        try:
+            parameters = self._validate_and_merge_parameters(parameters, DEFAULT_PARAMETERS)
+        except InvalidParameterError as e:
+            logger.error(f"Aggregator {self.name} received invalid parameters: {e}")
+            return None, data
+
+        pipe = None
+        nr_aggregated_models, total_examples = 0, 0
+        while not self.update_handler.model_updates.empty():
+            try:
+                model_update = self.update_handler.next_model_update()
+                tic = time.time()
+                model_next, metadata = self.update_handler.load_model_update(model_update, helper)
+                data["time_model_load"] += time.time() - tic
+
+                total_examples += metadata["num_examples"]
+                tic = time.time()
+                if nr_aggregated_models == 0:
+                    model_old = self.update_handler.load_model(helper, model_update.model_id)
+                    pipe = FedOptPipeline(self.device or default_device(), model_old, model_next)
+                pipe.add(model_next, metadata["num_examples"], total_examples)
+                data["time_model_aggregation"] += time.time() - tic
+
+                nr_aggregated_models += 1
+                if delete_models:
+                    self.update_handler.delete_model(model_update)
+            except Exception as e:  # noqa: BLE001 — fedopt.py:103-106
+                logger.error(f"Error processing model update: {e}. Skipping this update.")
+                logger.error(traceback.format_exc())
+                if nr_aggregated_models == 0:
+                    pipe = None
+                continue
+
+        data["nr_aggregated_models"] = nr_aggregated_models
+        if pipe is None or nr_aggregated_models == 0:
+            return None, data
+        try:
+            tic = time.time()
+            model = pipe.server_step(self.state, parameters)
+            data["time_model_aggregation"] += time.time() - tic
+            data.update(pipe.timings())
+        except Exception as e:  # noqa: BLE001 — fedopt.py:111-116
+            logger.error(f"Error during model aggregation: {e}")
+            logger.error(traceback.format_exc())
+            return None, data
+        logger.info(f"Aggregator {self.name} completed. Aggregated {nr_aggregated_models} models.")
+        return model, data
+
+    def _validate_and_merge_parameters(self, parameters, default_parameters):
+        """fedopt.py:123-137."""
+        if parameters:
+            Parameters(parameters).validate(PARAMETER_SCHEMA)
+            parameters = dict(parameters)
+        else:
+            parameters = {}
+        return {**default_parameters, **parameters}

@@ -1,0 +1,41 @@
+"""Build libfedagg.so (gfx950) in-tree with hipcc. ``python -m fedn_amd.build [--force]``."""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "fedagg.hip")
+HDR = os.path.join(ROOT, "include", "fedagg.h")
+OUT = os.path.join(HERE, "libfedagg.so")
+ARCH = os.environ.get("FEDN_AMD_ARCH", "gfx950")
+
+# -ffp-contract=off: numpy never fuses a*b+c, so neither may we (bit-exact parity).
+# hipcc's defaults keep f32 denormals and correctly rounded f32/f64 division and sqrt.
+FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall", f"--offload-arch={ARCH}"]
+
+
+def hipcc():
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def build(force=False, verbose=True):
+    if not force and os.path.exists(OUT):
+        t = os.path.getmtime(OUT)
+        if t >= os.path.getmtime(SRC) and t >= os.path.getmtime(HDR):
+            return OUT
+    tmp = OUT + ".tmp"
+    cmd = [hipcc()] + FLAGS + ["-I", os.path.join(ROOT, "include"), "-o", tmp, SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

@@ -1,0 +1,724 @@
+// fedagg.hip — gfx950 (MI355X) kernels + C ABI for FEDn's combiner-side aggregation.
+//
+// The hot path is an elementwise, HBM-bound recurrence over K client buffers:
+//   FedAvg  (numpyhelper.py:32, fedavg.py:109-133):   x <- x + (n_k*(y_k - x))/N_k
+//   FedOpt  (fedopt.py:74-118):  pg <- running mean of (y_k - old), then one
+//           Adam/Yogi/AdaGrad server step (fedopt.py:151-258) over (old, m, v).
+// Every output element depends only on the same element of the inputs, and the
+// client order is fixed by FEDn's FIFO queue, so parallelism is across elements:
+// one lane owns a 16-byte strip of elements, keeps the running aggregate in
+// registers for all K clients (no LDS round trip: nothing is shared between
+// lanes), issues the K strip loads U at a time so every wave has U x 1 KiB in
+// flight, and stores once. Bit-exact parity with numpy requires replaying the
+// op order with IEEE rounding at every step: this file is compiled with
+// -ffp-contract=off and relies on hipcc's correctly rounded f32/f64 `/` and
+// f64 sqrt (checked against the golden fixtures).
+//
+// Client tables (pointer, n_k, N_k) travel in the kernarg segment (<= 64 clients
+// per launch, ~1.5 KiB): they are read by scalar loads, need no H2D copy and keep
+// launches graph-capturable. K > 64 is chunked by the host code below; the chunks
+// continue from the stored aggregate, which replays the same recurrence exactly.
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <type_traits>
+
+#include "../../include/fedagg.h"
+
+namespace {
+
+// ----------------------------------------------------------------------------
+// error plumbing
+// ----------------------------------------------------------------------------
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(FA_EHIP, "%s: %s", what, hipGetErrorString(e));
+    return FA_OK;
+}
+
+constexpr int kMaxK = 64;     // clients per launch (kernarg table)
+constexpr int kBlock = 256;   // 4 waves
+constexpr int kUnroll = 8;    // client strips in flight per lane
+
+size_t dt_size(int dt) {
+    switch (dt) {
+        case FA_F32: return 4;
+        case FA_F64: return 8;
+        case FA_BF16: return 2;
+        case FA_F16: return 2;
+        case FA_I32: return 4;
+        case FA_I64: return 8;
+        default: return 0;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// element types and exact conversions
+// ----------------------------------------------------------------------------
+struct bf16 { uint16_t bits; };
+struct f16 { uint16_t bits; };
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t b) { return __uint_as_float(static_cast<uint32_t>(b) << 16); }
+__device__ __forceinline__ float f16_to_f32(uint16_t b) {
+    __half h;
+    __builtin_memcpy(&h, &b, 2);
+    return __half2float(h);
+}
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+    __half h = __float2half_rn(f);
+    uint16_t b;
+    __builtin_memcpy(&b, &h, 2);
+    return b;
+}
+
+// ----------------------------------------------------------------------------
+// compute policies: the arithmetic numpy performs for each dtype
+// ----------------------------------------------------------------------------
+struct CF32 {            // float32 ufunc loops
+    using V = float;     // register type
+    using S = float;     // scalar (n, N) type
+    __device__ static __forceinline__ V fold(V x, V y, S n, S N) {
+        V t = y - x;
+        t = n * t;
+        t = t / N;
+        return x + t;
+    }
+};
+struct CF64 {            // float64 ufunc loops
+    using V = double;
+    using S = double;
+    __device__ static __forceinline__ V fold(V x, V y, S n, S N) {
+        V t = y - x;
+        t = n * t;
+        t = t / N;
+        return x + t;
+    }
+};
+struct CF16 {            // numpy half loops: op in float, round to half after every op
+    using V = float;     // holds a value exactly representable in f16
+    using S = float;     // n, N pre-rounded to f16 on the host
+    __device__ static __forceinline__ V rh(float a) { return f16_to_f32(f32_to_f16(a)); }
+    __device__ static __forceinline__ V fold(V x, V y, S n, S N) {
+        V t = rh(y - x);
+        t = rh(n * t);
+        t = rh(t / N);
+        return rh(x + t);
+    }
+};
+
+// load one element of storage type T, widened to the compute register type V
+template <typename T, typename V> __device__ __forceinline__ V widen(T v) { return static_cast<V>(v); }
+template <> __device__ __forceinline__ float widen<bf16, float>(bf16 v) { return bf16_to_f32(v.bits); }
+template <> __device__ __forceinline__ double widen<bf16, double>(bf16 v) { return (double)bf16_to_f32(v.bits); }
+template <> __device__ __forceinline__ float widen<f16, float>(f16 v) { return f16_to_f32(v.bits); }
+
+template <typename T, typename V> __device__ __forceinline__ T narrow(V v) { return static_cast<T>(v); }
+template <> __device__ __forceinline__ f16 narrow<f16, float>(float v) { return f16{f32_to_f16(v)}; }
+
+// ----------------------------------------------------------------------------
+// 16-byte strip loads/stores (E elements of T). NT = non-temporal (read-once data)
+// ----------------------------------------------------------------------------
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T, int E, bool NT>
+__device__ __forceinline__ void strip_load(const T* __restrict__ p, T (&r)[E]) {
+    constexpr int bytes = E * (int)sizeof(T);
+    if constexpr (bytes % 16 == 0) {
+        const u32x4* q = reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+        for (int j = 0; j < bytes / 16; ++j) {
+            u32x4 w = NT ? __builtin_nontemporal_load(q + j) : q[j];
+            __builtin_memcpy(reinterpret_cast<char*>(r) + 16 * j, &w, 16);
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) r[e] = p[e];
+    }
+}
+
+template <typename T, int E>
+__device__ __forceinline__ void strip_store(T* __restrict__ p, const T (&r)[E]) {
+    constexpr int bytes = E * (int)sizeof(T);
+    if constexpr (bytes % 16 == 0) {
+        u32x4* q = reinterpret_cast<u32x4*>(p);
+#pragma unroll
+        for (int j = 0; j < bytes / 16; ++j) {
+            u32x4 w;
+            __builtin_memcpy(&w, reinterpret_cast<const char*>(r) + 16 * j, 16);
+            q[j] = w;
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) p[e] = r[e];
+    }
+}
+
+// ----------------------------------------------------------------------------
+// FedAvg fold kernel
+// ----------------------------------------------------------------------------
+template <typename S>
+struct ClientTable {
+    const void* ptr[kMaxK];
+    S n[kMaxK];
+    S N[kMaxK];
+};
+
+// MODE_INIT: x starts from updates[0]; MODE_CONT: x starts from agg.
+// INT_FIRST: integer updates, first fold in integer arithmetic (numpy int64/int32
+//            subtract + multiply wrap, then true_divide to f64), fedavg.py:127-130.
+template <typename Y, typename X, class CP, int E, bool INIT, bool INT_FIRST, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedavg(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P) {
+    using V = typename CP::V;
+    const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * E;
+    if (i0 >= P) return;
+    const int rem = (P - i0) < E ? (int)(P - i0) : E;
+
+    V x[E];
+    int k = 0;
+    if constexpr (INIT) {
+        const Y* y0p = static_cast<const Y*>(tab.ptr[0]) + i0;
+        Y y0[E];
+        if (rem == E) strip_load<Y, E, NT>(y0p, y0);
+        else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) y0[e] = e < rem ? y0p[e] : Y{};
+        }
+        if constexpr (INT_FIRST) {
+            // k = 1 in integer arithmetic (K >= 2 guaranteed by the host)
+            const Y* y1p = static_cast<const Y*>(tab.ptr[1]) + i0;
+            using U = typename std::make_unsigned<Y>::type;
+            const U n1 = (U)(int64_t)tab.n[1];
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                Y y1 = e < rem ? y1p[e] : Y{};
+                U t = (U)y1 - (U)y0[e];              // wrapping subtract
+                t = n1 * t;                          // wrapping multiply
+                double q = (double)(Y)t / (double)tab.N[1];
+                x[e] = (double)y0[e] + q;
+            }
+            k = 2;
+        } else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) x[e] = widen<Y, V>(y0[e]);
+            k = 1;
+        }
+    } else {
+        X xa[E];
+        if (rem == E) strip_load<X, E, false>(agg + i0, xa);
+        else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) xa[e] = e < rem ? agg[i0 + e] : X{};
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) x[e] = widen<X, V>(xa[e]);
+    }
+
+    if (rem == E) {
+        // steady state: U strips in flight, then U dependent folds
+        for (; k + kUnroll <= K; k += kUnroll) {
+            Y y[kUnroll][E];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u)
+                strip_load<Y, E, NT>(static_cast<const Y*>(tab.ptr[k + u]) + i0, y[u]);
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const typename CP::S n = tab.n[k + u], N = tab.N[k + u];
+#pragma unroll
+                for (int e = 0; e < E; ++e) x[e] = CP::fold(x[e], widen<Y, V>(y[u][e]), n, N);
+            }
+        }
+        for (; k < K; ++k) {
+            Y y[E];
+            strip_load<Y, E, NT>(static_cast<const Y*>(tab.ptr[k]) + i0, y);
+            const typename CP::S n = tab.n[k], N = tab.N[k];
+#pragma unroll
+            for (int e = 0; e < E; ++e) x[e] = CP::fold(x[e], widen<Y, V>(y[e]), n, N);
+        }
+        X xo[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) xo[e] = narrow<X, V>(x[e]);
+        strip_store<X, E>(agg + i0, xo);
+    } else {
+        // ragged tail strip (at most one lane per launch)
+        for (; k < K; ++k) {
+            const Y* yp = static_cast<const Y*>(tab.ptr[k]) + i0;
+            const typename CP::S n = tab.n[k], N = tab.N[k];
+            for (int e = 0; e < rem; ++e) x[e] = CP::fold(x[e], widen<Y, V>(yp[e]), n, N);
+        }
+        for (int e = 0; e < rem; ++e) agg[i0 + e] = narrow<X, V>(x[e]);
+    }
+}
+
+// ----------------------------------------------------------------------------
+// FedOpt kernel: pseudo-gradient fold + server step, fused
+// ----------------------------------------------------------------------------
+struct OptScalars {
+    // python-float constants exactly as fedopt.py computes them
+    double lr, b1, b2, tau, tau2, c1, c2, nc2;   // c1 = 1-b1, c2 = 1-b2, nc2 = -(1-b2)
+    float b1f, c1f, c2f;                         // the same cast to f32 (numpy weak-scalar rule)
+    int opt;
+};
+
+struct OptBuffers {
+    const void* old;
+    void* pg;
+    const void* m_in;
+    void* m_out;
+    const double* v_in;
+    double* v_out;
+    double* out;
+    int m_in_f64;    // 0: f32, 1: f64, -1: None
+    int m_out_f64;
+};
+
+// multiply an array element held as PG by a python float constant (numpy weak scalar)
+template <class PG> __device__ __forceinline__ double mul_pg(double a, double c, float cf);
+template <> __device__ __forceinline__ double mul_pg<CF32>(double a, double, float cf) { return (double)((float)a * cf); }
+template <> __device__ __forceinline__ double mul_pg<CF64>(double a, double c, float) { return a * c; }
+
+__device__ __forceinline__ double np_sign(double d) {
+    // numpy sign: 1 / -1 / 0 (for +-0), NaN propagates
+    return d > 0.0 ? 1.0 : (d < 0.0 ? -1.0 : (d == 0.0 ? 0.0 : d));
+}
+
+template <typename Y, typename OLD, class PG, int E, bool FIRST, bool FINAL, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
+    using V = typename PG::V;   // float or double
+    const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * E;
+    if (i0 >= P) return;
+    const int rem = (P - i0) < E ? (int)(P - i0) : E;
+    const bool full = rem == E;
+
+    OLD old[E];
+    const OLD* oldp = static_cast<const OLD*>(b.old) + i0;
+    if (full) strip_load<OLD, E, false>(oldp, old);
+    else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) old[e] = e < rem ? oldp[e] : OLD{};
+    }
+    V ov[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) ov[e] = widen<OLD, V>(old[e]);
+
+    // ---- pseudo-gradient: pg = y0 - old ; pg = pg + (n*((y_k - old) - pg))/N (fedopt.py:89-94)
+    V pg[E];
+    int k = 0;
+    if constexpr (FIRST) {
+        Y y[E];
+        const Y* yp = static_cast<const Y*>(tab.ptr[0]) + i0;
+        if (full) strip_load<Y, E, NT>(yp, y);
+        else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) y[e] = e < rem ? yp[e] : Y{};
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) pg[e] = widen<Y, V>(y[e]) - ov[e];
+        k = 1;
+    } else {
+        V* pgp = static_cast<V*>(b.pg) + i0;
+        if (full) strip_load<V, E, false>(pgp, pg);
+        else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) pg[e] = e < rem ? pgp[e] : V{};
+        }
+    }
+    if (full) {
+        for (; k + kUnroll / 2 <= K; k += kUnroll / 2) {
+            Y y[kUnroll / 2][E];
+#pragma unroll
+            for (int u = 0; u < kUnroll / 2; ++u)
+                strip_load<Y, E, NT>(static_cast<const Y*>(tab.ptr[k + u]) + i0, y[u]);
+#pragma unroll
+            for (int u = 0; u < kUnroll / 2; ++u) {
+                const typename PG::S n = tab.n[k + u], N = tab.N[k + u];
+#pragma unroll
+                for (int e = 0; e < E; ++e) pg[e] = PG::fold(pg[e], widen<Y, V>(y[u][e]) - ov[e], n, N);
+            }
+        }
+    }
+    for (; k < K; ++k) {
+        const Y* yp = static_cast<const Y*>(tab.ptr[k]) + i0;
+        const typename PG::S n = tab.n[k], N = tab.N[k];
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+            if (e < rem) pg[e] = PG::fold(pg[e], widen<Y, V>(yp[e]) - ov[e], n, N);
+    }
+
+    if constexpr (!FINAL) {
+        V* pgp = static_cast<V*>(b.pg) + i0;
+        if (full) strip_store<V, E>(pgp, pg);
+        else
+            for (int e = 0; e < rem; ++e) pgp[e] = pg[e];
+        return;
+    } else {
+        constexpr bool PG32 = std::is_same<PG, CF32>::value;
+        // ---- m (fedopt.py:173-176 and the two twins)
+        double m[E];
+        if (b.m_in_f64 < 0) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) m[e] = mul_pg<PG>((double)pg[e], s.c1, s.c1f);
+        } else if (b.m_in_f64 == 0) {
+            float mi[E];
+            const float* mp = static_cast<const float*>(b.m_in) + i0;
+            if (full) strip_load<float, E, false>(mp, mi);
+            else
+                for (int e = 0; e < E; ++e) mi[e] = e < rem ? mp[e] : 0.f;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float a = mi[e] * s.b1f;                               // m*beta1 in f32
+                if constexpr (PG32) m[e] = (double)(a + (float)pg[e] * s.c1f);  // f32 + f32
+                else m[e] = (double)a + (double)pg[e] * s.c1;                   // f32 -> f64 add
+            }
+        } else {
+            double mi[E];
+            const double* mp = static_cast<const double*>(b.m_in) + i0;
+            if (full) strip_load<double, E, false>(mp, mi);
+            else
+                for (int e = 0; e < E; ++e) mi[e] = e < rem ? mp[e] : 0.0;
+#pragma unroll
+            for (int e = 0; e < E; ++e) m[e] = mi[e] * s.b1 + mul_pg<PG>((double)pg[e], s.c1, s.c1f);
+        }
+        // ---- v (fedopt.py:170-171, 178-179 / 214-217 / 251-252)
+        double v[E];
+        if (b.v_in) {
+            const double* vp = b.v_in + i0;
+            if (full) strip_load<double, E, false>(vp, v);
+            else
+                for (int e = 0; e < E; ++e) v[e] = e < rem ? vp[e] : 0.0;
+        } else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) v[e] = s.tau2;
+        }
+        double o[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const V pv = pg[e];
+            const double p = (double)(V)(pv * pv);   // power(pg, 2) in the pg dtype
+            if (s.opt == FA_ADAM) {
+                v[e] = v[e] * s.b2 + mul_pg<PG>(p, s.c2, s.c2f);
+            } else if (s.opt == FA_YOGI) {
+                const double sg = np_sign(v[e] - p);
+                v[e] = v[e] + (sg * p) * s.nc2;
+            } else {
+                v[e] = v[e] + p;
+            }
+            const double sv = __builtin_sqrt(v[e]) + s.tau;
+            const double t = m[e] / sv;
+            o[e] = widen<OLD, double>(old[e]) + t * s.lr;
+        }
+        // ---- stores
+        if (full) {
+            strip_store<double, E>(b.v_out + i0, v);
+            strip_store<double, E>(b.out + i0, o);
+            if (b.m_out_f64) strip_store<double, E>(static_cast<double*>(b.m_out) + i0, m);
+            else {
+                float mf[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) mf[e] = (float)m[e];
+                strip_store<float, E>(static_cast<float*>(b.m_out) + i0, mf);
+            }
+        } else {
+            for (int e = 0; e < rem; ++e) {
+                b.v_out[i0 + e] = v[e];
+                b.out[i0 + e] = o[e];
+                if (b.m_out_f64) static_cast<double*>(b.m_out)[i0 + e] = m[e];
+                else static_cast<float*>(b.m_out)[i0 + e] = (float)m[e];
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// measurement kernels
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_stream_copy(u32x4* __restrict__ dst, const u32x4* __restrict__ src, int64_t n16) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n16) dst[i] = __builtin_nontemporal_load(src + i);
+}
+
+constexpr int kReadPerLane = 16;
+__global__ void __launch_bounds__(kBlock) k_stream_read(const u32x4* __restrict__ src, int64_t n16, u32x4* __restrict__ sink) {
+    const int64_t base = (int64_t)blockIdx.x * kBlock * kReadPerLane + threadIdx.x;
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < kReadPerLane; ++j) {
+        const int64_t i = base + (int64_t)j * kBlock;
+        if (i < n16) acc ^= __builtin_nontemporal_load(src + i);
+    }
+    // wave xor-reduce is unnecessary for a bandwidth probe: one lane's word per block
+    __shared__ u32x4 red[kBlock];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u32x4 r = red[0];
+        for (int t = 1; t < kBlock; ++t) r ^= red[t];
+        sink[blockIdx.x] = r;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// host side
+// ----------------------------------------------------------------------------
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template <typename S>
+void fill_table(ClientTable<S>& t, const void* const* ptrs, const double* n, const double* N, int k0, int cnt) {
+    for (int j = 0; j < cnt; ++j) {
+        t.ptr[j] = ptrs[k0 + j];
+        t.n[j] = (S)n[k0 + j];
+        t.N[j] = (S)N[k0 + j];
+    }
+    for (int j = cnt; j < kMaxK; ++j) {
+        t.ptr[j] = nullptr;
+        t.n[j] = 0;
+        t.N[j] = 0;
+    }
+}
+
+// numpy's conversion of a python int to float16 (round-to-nearest-even), kept in f32
+float to_half_value(double v) {
+    __half h = __float2half_rn((float)v);
+    return __half2float(h);
+}
+
+int64_t grid_for(int64_t P, int E) {
+    const int64_t strips = (P + E - 1) / E;
+    return (strips + kBlock - 1) / kBlock;
+}
+
+template <typename Y, typename X, class CP>
+int launch_fedavg(void* agg, const void* const* ups, const double* n, const double* N, int K, int64_t P,
+                  int init, bool int_first, hipStream_t st) {
+    constexpr int E16 = 16 / (int)sizeof(Y) > 0 ? 16 / (int)sizeof(Y) : 1;
+    bool vec = aligned16(agg);
+    for (int k = 0; k < K && vec; ++k) vec = aligned16(ups[k]);
+    // byte-exact strip stores of X also need 16-B alignment of the agg strip
+    using S = typename CP::S;
+    ClientTable<S> tab;
+    int k0 = 0;
+    bool first = init != 0;
+    while (k0 < K) {
+        const int cnt = (K - k0) < kMaxK ? (K - k0) : kMaxK;
+        fill_table<S>(tab, ups, n, N, k0, cnt);
+        if (std::is_same<CP, CF16>::value) {
+            for (int j = 0; j < cnt; ++j) {
+                tab.n[j] = (S)to_half_value(n[k0 + j]);
+                tab.N[j] = (S)to_half_value(N[k0 + j]);
+            }
+        }
+        X* a = static_cast<X*>(agg);
+        if (vec) {
+            const dim3 grid((unsigned)grid_for(P, E16));
+            if (first && int_first) {
+                if constexpr (std::is_integral<Y>::value)
+                    hipLaunchKernelGGL((k_fedavg<Y, X, CP, E16, true, true, true>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+            } else if (first)
+                hipLaunchKernelGGL((k_fedavg<Y, X, CP, E16, true, false, true>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+            else
+                hipLaunchKernelGGL((k_fedavg<Y, X, CP, E16, false, false, true>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+        } else {
+            const dim3 grid((unsigned)grid_for(P, 1));
+            if (first && int_first) {
+                if constexpr (std::is_integral<Y>::value)
+                    hipLaunchKernelGGL((k_fedavg<Y, X, CP, 1, true, true, false>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+            } else if (first)
+                hipLaunchKernelGGL((k_fedavg<Y, X, CP, 1, true, false, false>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+            else
+                hipLaunchKernelGGL((k_fedavg<Y, X, CP, 1, false, false, false>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+        }
+        int rc = check_launch("fa_fedavg_fold: kernel launch");
+        if (rc) return rc;
+        first = false;
+        k0 += cnt;
+    }
+    return FA_OK;
+}
+
+template <typename Y, typename OLD, class PG, int E, bool NT>
+int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTable<typename PG::S>& tab, int cnt,
+                      int64_t P, bool first, bool final_, hipStream_t st) {
+    const dim3 grid((unsigned)grid_for(P, E));
+    if (first && final_) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+    else if (first) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, false, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+    else if (final_) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, false, true, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+    else hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, false, false, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+    return check_launch("fa_fedopt_step: kernel launch");
+}
+
+template <typename Y, typename OLD, class PG>
+int launch_fedopt(const OptBuffers& b, const OptScalars& s, const void* const* ups, const double* n, const double* N,
+                  int K, int64_t P, int flags, hipStream_t st) {
+    bool vec = aligned16(b.old) && aligned16(b.pg) && aligned16(b.m_in) && aligned16(b.m_out) && aligned16(b.v_in) &&
+               aligned16(b.v_out) && aligned16(b.out);
+    for (int k = 0; k < K && vec; ++k) vec = aligned16(ups[k]);
+    using S = typename PG::S;
+    ClientTable<S> tab;
+    bool first = (flags & FA_PG_FIRST) != 0;
+    const bool final_all = (flags & FA_PG_FINAL) != 0;
+    int k0 = 0;
+    do {
+        const int cnt = (K - k0) < kMaxK ? (K - k0) : kMaxK;
+        fill_table<S>(tab, ups, n, N, k0, cnt);
+        const bool last = k0 + cnt >= K;
+        const bool fin = last && final_all;
+        int rc = vec ? launch_fedopt_one<Y, OLD, PG, 4, true>(b, s, tab, cnt, P, first, fin, st)
+                     : launch_fedopt_one<Y, OLD, PG, 1, false>(b, s, tab, cnt, P, first, fin, st);
+        if (rc) return rc;
+        first = false;
+        k0 += cnt;
+    } while (k0 < K);
+    return FA_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int fa_abi_version(void) { return FA_ABI_VERSION; }
+
+const char* fa_last_error(void) { return g_err; }
+
+int fa_promote(int a, int b) {
+    auto fl = [](int d) { return d == FA_BF16 ? FA_F32 : d; };
+    if (a == FA_NONE) return fl(b);
+    if (b == FA_NONE) return fl(a);
+    a = fl(a);
+    b = fl(b);
+    if (a == b) return a;
+    if (a == FA_F64 || b == FA_F64) return FA_F64;
+    if ((a == FA_F32 && b == FA_F16) || (a == FA_F16 && b == FA_F32)) return FA_F32;
+    return FA_NONE;
+}
+
+int fa_fedavg_fold(void* agg, int agg_dtype, const void* const* updates, int upd_dtype, const double* n, const double* N,
+                   int K, int64_t P, int init, void* stream) {
+    g_err[0] = 0;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (P < 0 || K < 0) return fail(FA_EINVAL, "fa_fedavg_fold: negative size (P=%lld, K=%d)", (long long)P, K);
+    if (init && K < 1) return fail(FA_EINVAL, "fa_fedavg_fold: init requires K >= 1");
+    if (K == 0 || P == 0) return FA_OK;
+    if (!agg || !updates || !n || !N) return fail(FA_EINVAL, "fa_fedavg_fold: null pointer argument");
+    for (int k = 0; k < K; ++k)
+        if (!updates[k]) return fail(FA_EINVAL, "fa_fedavg_fold: updates[%d] is NULL", k);
+    for (int k = init ? 1 : 0; k < K; ++k)
+        if (!(N[k] != 0.0)) return fail(FA_EINVAL, "fa_fedavg_fold: N[%d] == 0", k);
+    if (init && K == 1) {
+        if (agg_dtype != upd_dtype) return fail(FA_EDTYPE, "fa_fedavg_fold: K=1 init is a copy; dtypes must match");
+        hipError_t e = hipMemcpyAsync(agg, updates[0], (size_t)P * dt_size(upd_dtype), hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return fail(FA_EHIP, "fa_fedavg_fold: hipMemcpyAsync: %s", hipGetErrorString(e));
+        return FA_OK;
+    }
+    const bool int_first = init && (upd_dtype == FA_I64 || upd_dtype == FA_I32);
+    if (upd_dtype == FA_F32 && agg_dtype == FA_F32) return launch_fedavg<float, float, CF32>(agg, updates, n, N, K, P, init, false, st);
+    if (upd_dtype == FA_BF16 && agg_dtype == FA_F32) return launch_fedavg<bf16, float, CF32>(agg, updates, n, N, K, P, init, false, st);
+    if (upd_dtype == FA_F16 && agg_dtype == FA_F16) return launch_fedavg<f16, f16, CF16>(agg, updates, n, N, K, P, init, false, st);
+    if (upd_dtype == FA_F64 && agg_dtype == FA_F64) return launch_fedavg<double, double, CF64>(agg, updates, n, N, K, P, init, false, st);
+    if (upd_dtype == FA_F32 && agg_dtype == FA_F64) return launch_fedavg<float, double, CF64>(agg, updates, n, N, K, P, init, false, st);
+    if (upd_dtype == FA_I64 && agg_dtype == FA_F64) return launch_fedavg<int64_t, double, CF64>(agg, updates, n, N, K, P, init, int_first, st);
+    if (upd_dtype == FA_I32 && agg_dtype == FA_F64) return launch_fedavg<int32_t, double, CF64>(agg, updates, n, N, K, P, init, int_first, st);
+    return fail(FA_EDTYPE, "fa_fedavg_fold: unsupported dtype pair (update %d, aggregate %d)", upd_dtype, agg_dtype);
+}
+
+int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, int upd_dtype, const double* n,
+                   const double* N, int K, void* pg, int flags, const void* m_in, int m_in_dtype, void* m_out,
+                   const double* v_in, double* v_out, double* out, int serveropt, double lr, double beta1,
+                   double beta2, double tau, int64_t P, void* stream) {
+    g_err[0] = 0;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (P < 0 || K < 0) return fail(FA_EINVAL, "fa_fedopt_step: negative size");
+    if (P == 0) return FA_OK;
+    const bool first = flags & FA_PG_FIRST, final_ = flags & FA_PG_FINAL;
+    if (first && K < 1) return fail(FA_EINVAL, "fa_fedopt_step: FA_PG_FIRST requires K >= 1");
+    if (!old) return fail(FA_EINVAL, "fa_fedopt_step: old is NULL");
+    if (K > 0 && (!updates || !n || !N)) return fail(FA_EINVAL, "fa_fedopt_step: null client table");
+    for (int k = 0; k < K; ++k)
+        if (!updates[k]) return fail(FA_EINVAL, "fa_fedopt_step: updates[%d] is NULL", k);
+    for (int k = first ? 1 : 0; k < K; ++k)
+        if (!(N[k] != 0.0)) return fail(FA_EINVAL, "fa_fedopt_step: N[%d] == 0", k);
+    if ((!first || !final_ || K > kMaxK) && !pg) return fail(FA_EINVAL, "fa_fedopt_step: pg workspace required");
+    if (final_ && (!m_out || !v_out || !out)) return fail(FA_EINVAL, "fa_fedopt_step: null output buffer");
+    if (serveropt < FA_ADAM || serveropt > FA_ADAGRAD) return fail(FA_EINVAL, "fa_fedopt_step: unsupported serveropt %d", serveropt);
+    if (old_dtype != FA_F32 && old_dtype != FA_F64) return fail(FA_EDTYPE, "fa_fedopt_step: old dtype %d", old_dtype);
+    if (upd_dtype != FA_F32 && upd_dtype != FA_F64 && upd_dtype != FA_BF16)
+        return fail(FA_EDTYPE, "fa_fedopt_step: update dtype %d", upd_dtype);
+    const int pg_dt = fa_promote(upd_dtype, old_dtype);
+    if (m_in && m_in_dtype != FA_F32 && m_in_dtype != FA_F64) return fail(FA_EDTYPE, "fa_fedopt_step: m dtype %d", m_in_dtype);
+    if (!m_in) m_in_dtype = FA_NONE;
+    const int m_out_dt = fa_promote(m_in_dtype, pg_dt);
+
+    OptBuffers b{old, pg, m_in, m_out, v_in, v_out, out, m_in_dtype == FA_NONE ? -1 : (m_in_dtype == FA_F64 ? 1 : 0),
+                 m_out_dt == FA_F64 ? 1 : 0};
+    OptScalars s;
+    s.lr = lr;
+    s.b1 = beta1;
+    s.b2 = beta2;
+    s.tau = tau;
+    s.tau2 = std::pow(tau, 2.0);   // math.pow(tau, 2)
+    s.c1 = 1.0 - beta1;
+    s.c2 = 1.0 - beta2;
+    s.nc2 = -(1.0 - beta2);
+    s.b1f = (float)beta1;
+    s.c1f = (float)s.c1;
+    // fedopt adam: p*(1-beta2); p has the pg dtype
+    s.c2f = (float)s.c2;
+    s.opt = serveropt;
+
+    if (upd_dtype == FA_F32 && old_dtype == FA_F32) return launch_fedopt<float, float, CF32>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_BF16 && old_dtype == FA_F32) return launch_fedopt<bf16, float, CF32>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_F32 && old_dtype == FA_F64) return launch_fedopt<float, double, CF64>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_F64 && old_dtype == FA_F64) return launch_fedopt<double, double, CF64>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_BF16 && old_dtype == FA_F64) return launch_fedopt<bf16, double, CF64>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_F64 && old_dtype == FA_F32) return launch_fedopt<double, float, CF64>(b, s, updates, n, N, K, P, flags, st);
+    return fail(FA_EDTYPE, "fa_fedopt_step: unsupported dtype pair (update %d, old %d)", upd_dtype, old_dtype);
+}
+
+int fa_stream_copy(void* dst, const void* src, int64_t bytes, void* stream) {
+    g_err[0] = 0;
+    if (bytes < 0 || (bytes & 15) || !aligned16(dst) || !aligned16(src))
+        return fail(FA_EINVAL, "fa_stream_copy: bytes must be a multiple of 16 and buffers 16-B aligned");
+    const int64_t n16 = bytes / 16;
+    if (!n16) return FA_OK;
+    hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)((n16 + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       static_cast<hipStream_t>(stream), static_cast<u32x4*>(dst), static_cast<const u32x4*>(src), n16);
+    return check_launch("fa_stream_copy");
+}
+
+int64_t fa_stream_read_blocks(int64_t bytes) {
+    const int64_t n16 = bytes / 16;
+    const int64_t per = (int64_t)kBlock * kReadPerLane;
+    return (n16 + per - 1) / per;
+}
+
+int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream) {
+    g_err[0] = 0;
+    if (bytes < 0 || (bytes & 15) || !aligned16(src) || !aligned16(sink))
+        return fail(FA_EINVAL, "fa_stream_read: bytes must be a multiple of 16 and buffers 16-B aligned");
+    const int64_t blocks = fa_stream_read_blocks(bytes);
+    if (!blocks) return FA_OK;
+    hipLaunchKernelGGL(k_stream_read, dim3((unsigned)blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const u32x4*>(src), bytes / 16, static_cast<u32x4*>(sink));
+    return check_launch("fa_stream_read");
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+"""Flat device layout of a FEDn model (``list[np.ndarray]``, numpyhelper's model format).
+
+A model is a list of per-layer arrays (numpyhelper.py:171-189 loads them from an npz
+in key order "0", "1", ...). The kernels work on flat buffers, so a model is packed
+into ONE contiguous byte buffer with one region per element dtype ("group"): every
+fp32 tensor back to back, then (if any) the int64 tensors, etc. Each region starts
+on a 256-byte boundary so every group base is 16-B aligned for the vector path.
+One H2D copy moves a whole update; one kernel launch per group folds it.
+"""
+import numpy as np
+
+ALIGN = 256
+
+
+def _round_up(x, a):
+    return (x + a - 1) // a * a
+
+
+class Layout:
+    """Shapes, dtypes and group offsets of a model."""
+
+    def __init__(self, shapes, dtypes):
+        self.shapes = [tuple(s) for s in shapes]
+        self.dtypes = [np.dtype(d) for d in dtypes]
+        self.sizes = [int(np.prod(s, dtype=np.int64)) for s in self.shapes]
+        # group key = dtype, in first-appearance order
+        self.groups = []          # list of dtype
+        self.members = {}         # dtype -> list of (tensor index, element offset)
+        self.group_elems = {}     # dtype -> elements
+        for i, (dt, sz) in enumerate(zip(self.dtypes, self.sizes)):
+            if dt not in self.members:
+                self.groups.append(dt)
+                self.members[dt] = []
+                self.group_elems[dt] = 0
+            self.members[dt].append((i, self.group_elems[dt]))
+            self.group_elems[dt] += sz
+        self.group_byte_offset = {}
+        off = 0
+        for dt in self.groups:
+            self.group_byte_offset[dt] = off
+            off = _round_up(off + self.group_elems[dt] * dt.itemsize, ALIGN)
+        self.nbytes = max(off, ALIGN)
+        self.nparams = sum(self.sizes)
+
+    @classmethod
+    def of(cls, arrays):
+        arrays = [np.asarray(a) for a in arrays]
+        return cls([a.shape for a in arrays], [a.dtype for a in arrays])
+
+    def signature(self):
+        return (tuple(self.shapes), tuple(str(d) for d in self.dtypes))
+
+    def check(self, arrays):
+        """Raise (as numpy would, on a non-broadcastable mismatch) if ``arrays`` does not match."""
+        if len(arrays) != len(self.shapes):
+            raise ValueError(f"model has {len(arrays)} tensors, expected {len(self.shapes)}")
+        for i, a in enumerate(arrays):
+            a = np.asarray(a)
+            if tuple(a.shape) != self.shapes[i]:
+                raise ValueError(f"operands could not be combined: tensor {i} has shape {a.shape}, "
+                                 f"expected {self.shapes[i]}")
+            if a.dtype != self.dtypes[i]:
+                raise TypeError(f"tensor {i} has dtype {a.dtype}, expected {self.dtypes[i]} "
+                                "(mixed dtypes across client updates are not supported)")
+
+    def group_view(self, buf_np_u8, dt):
+        """numpy view of group ``dt`` inside a uint8 host buffer."""
+        off = self.group_byte_offset[dt]
+        n = self.group_elems[dt]
+        return buf_np_u8[off:off + n * dt.itemsize].view(dt)
+
+    def pack(self, arrays, buf_np_u8):
+        """Copy the tensors of ``arrays`` into their group regions of a host uint8 buffer."""
+        for dt in self.groups:
+            g = self.group_view(buf_np_u8, dt)
+            for i, off in self.members[dt]:
+                sz = self.sizes[i]
+                if sz:
+                    np.copyto(g[off:off + sz], np.ascontiguousarray(arrays[i]).reshape(-1), casting="no")
+
+    def unpack_group(self, flat, dt, out):
+        """Scatter a group's flat host array back into per-tensor arrays (new, owned)."""
+        for i, off in self.members[dt]:
+            sz = self.sizes[i]
+            out[i] = np.array(flat[off:off + sz]).reshape(self.shapes[i])
+        return out

@@ -1,0 +1,203 @@
+"""Tensor-level entry points over the C ABI (device buffers are PyTorch-ROCm tensors).
+
+These are thin: validate shapes/devices, collect raw pointers, call libfedagg on the
+tensors' current HIP stream, raise :class:`FedAggError` on a nonzero status.
+
+dtype rules mirror numpy's for the reference expressions:
+see :func:`fold_result_dtype` and :func:`fedopt_dtypes`.
+"""
+import numpy as np
+import torch
+
+from . import _abi
+
+_TORCH_TO_FA = {
+    torch.float32: _abi.FA_F32,
+    torch.float64: _abi.FA_F64,
+    torch.bfloat16: _abi.FA_BF16,
+    torch.float16: _abi.FA_F16,
+    torch.int32: _abi.FA_I32,
+    torch.int64: _abi.FA_I64,
+}
+_FA_TO_TORCH = {v: k for k, v in _TORCH_TO_FA.items()}
+_NP_TO_TORCH = {
+    np.dtype(np.float32): torch.float32,
+    np.dtype(np.float64): torch.float64,
+    np.dtype(np.float16): torch.float16,
+    np.dtype(np.int32): torch.int32,
+    np.dtype(np.int64): torch.int64,
+}
+_TORCH_TO_NP = {v: k for k, v in _NP_TO_TORCH.items()}
+
+
+def fa_dtype(t):
+    dt = t.dtype if isinstance(t, torch.Tensor) else t
+    if isinstance(dt, np.dtype) or (isinstance(dt, type) and issubclass(dt, np.generic)):
+        dt = torch_dtype(dt)
+    try:
+        return _TORCH_TO_FA[dt]
+    except KeyError:
+        raise TypeError(f"dtype {dt} is not supported by libfedagg") from None
+
+
+def torch_dtype(np_dtype):
+    try:
+        return _NP_TO_TORCH[np.dtype(np_dtype)]
+    except KeyError:
+        raise TypeError(f"numpy dtype {np_dtype} is not supported by libfedagg") from None
+
+
+def numpy_dtype(torch_dt):
+    if torch_dt == torch.bfloat16:
+        raise TypeError("bfloat16 has no numpy dtype")
+    return _TORCH_TO_NP[torch_dt]
+
+
+def fold_result_dtype(agg_dt, upd_dt, nfolds=1):
+    """dtype of ``np.add(x, n*(y-x)/N)`` for x: agg_dt, y: upd_dt (torch dtypes).
+
+    bf16 (no numpy counterpart) accumulates in f32. Integer inputs become f64 on the
+    first fold (numpy true_divide). ``nfolds == 0`` means "no fold yet" (plain alias).
+    """
+    if nfolds == 0:
+        return upd_dt
+    ints = (torch.int32, torch.int64)
+    if agg_dt in ints or upd_dt in ints:
+        return torch.float64
+    if torch.float64 in (agg_dt, upd_dt):
+        return torch.float64
+    if agg_dt == torch.float16 and upd_dt == torch.float16:
+        return torch.float16
+    return torch.float32
+
+
+def _stream_handle(t, stream):
+    if stream is None:
+        stream = torch.cuda.current_stream(t.device)
+    return ctypes_stream(stream)
+
+
+def ctypes_stream(stream):
+    return int(stream.cuda_stream) if stream is not None else 0
+
+
+def _check_dev(name, t, P, device):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must be a device (cuda/hip) tensor, got {t.device}")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if t.numel() != P:
+        raise ValueError(f"{name} has {t.numel()} elements, expected {P}")
+
+
+def fedavg_fold(agg, updates, n, N, init, stream=None):
+    """FedAvg fold on device (``fa_fedavg_fold``): numpyhelper.py:32 replayed in queue order.
+
+    agg      flat device tensor (running model; written)
+    updates  sequence of flat device tensors of the same length
+    n, N     per-update num_examples and running totals (python numbers)
+    init     True: agg := updates[0] then fold updates[1:]; False: fold all into agg
+    """
+    lib = _abi.load()
+    K = len(updates)
+    if len(n) != K or len(N) != K:
+        raise ValueError("n and N must have one entry per update")
+    P = agg.numel()
+    dev = agg.device
+    _check_dev("agg", agg, P, None)
+    upd_dt = updates[0].dtype if K else agg.dtype
+    for i, u in enumerate(updates):
+        _check_dev(f"updates[{i}]", u, P, dev)
+        if u.dtype != upd_dt:
+            raise TypeError("all updates in one fold call must share a dtype")
+    with torch.cuda.device(dev):
+        st = _stream_handle(agg, stream)
+    rc = lib.fa_fedavg_fold(agg.data_ptr(), fa_dtype(agg), _abi.ptr_array([u.data_ptr() for u in updates]),
+                            fa_dtype(upd_dt), _abi.double_array(n), _abi.double_array(N), K, P, int(bool(init)), st)
+    _abi.check(rc)
+    return agg
+
+
+_OPTS = {"adam": _abi.FA_ADAM, "yogi": _abi.FA_YOGI, "adagrad": _abi.FA_ADAGRAD}
+
+
+def promote(a, b):
+    """numpy result dtype for the FedOpt elementwise pairs (torch dtypes; None = absent)."""
+    if a is None:
+        a, b = b, None
+    if b is None:
+        return torch.float32 if a == torch.bfloat16 else a
+    a = torch.float32 if a == torch.bfloat16 else a
+    b = torch.float32 if b == torch.bfloat16 else b
+    if a == b:
+        return a
+    if torch.float64 in (a, b):
+        return torch.float64
+    return torch.float32
+
+
+def fedopt_dtypes(upd_dt, old_dt, m_dt):
+    """(pg dtype, m_out dtype) for fedopt.py's expressions; v and out are always f64."""
+    pg = promote(upd_dt, old_dt)
+    return pg, promote(m_dt, pg)
+
+
+def fedopt_step(old, updates, n, N, *, first, final, pg=None, m_in=None, m_out=None, v_in=None, v_out=None,
+                out=None, serveropt="adam", learning_rate=1e-3, beta1=0.9, beta2=0.99, tau=1e-4, stream=None):
+    """Fused FedOpt step on device (``fa_fedopt_step``), fedopt.py:74-118 + 151-258."""
+    lib = _abi.load()
+    if serveropt not in _OPTS:
+        raise ValueError(f"Unsupported server optimizer: {serveropt}")
+    K = len(updates)
+    P = old.numel()
+    dev = old.device
+    _check_dev("old", old, P, None)
+    upd_dt = updates[0].dtype if K else old.dtype
+    for i, u in enumerate(updates):
+        _check_dev(f"updates[{i}]", u, P, dev)
+        if u.dtype != upd_dt:
+            raise TypeError("all updates in one call must share a dtype")
+    for name, t in (("pg", pg), ("m_in", m_in), ("m_out", m_out), ("v_in", v_in), ("v_out", v_out), ("out", out)):
+        if t is not None:
+            _check_dev(name, t, P, dev)
+    if v_in is not None and v_in.dtype != torch.float64:
+        raise TypeError("v must be float64 (fedopt.py:171: np.ones(...) * tau**2)")
+    if final:
+        if m_out is None or v_out is None or out is None:
+            raise ValueError("final step needs m_out, v_out and out")
+        pg_dt, m_dt = fedopt_dtypes(upd_dt, old.dtype, None if m_in is None else m_in.dtype)
+        if m_out.dtype != m_dt or v_out.dtype != torch.float64 or out.dtype != torch.float64:
+            raise TypeError(f"output dtypes: m_out {m_dt}, v_out/out float64 required")
+    flags = (_abi.FA_PG_FIRST if first else 0) | (_abi.FA_PG_FINAL if final else 0)
+    ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+    with torch.cuda.device(dev):
+        st = _stream_handle(old, stream)
+    rc = lib.fa_fedopt_step(
+        old.data_ptr(), fa_dtype(old), _abi.ptr_array([u.data_ptr() for u in updates]), fa_dtype(upd_dt),
+        _abi.double_array(n), _abi.double_array(N), K, ptr(pg), flags,
+        ptr(m_in), _abi.FA_NONE if m_in is None else fa_dtype(m_in), ptr(m_out),
+        ptr(v_in), ptr(v_out), ptr(out), _OPTS[serveropt], float(learning_rate), float(beta1), float(beta2),
+        float(tau), P, st)
+    _abi.check(rc)
+
+
+def stream_copy(dst, src, stream=None):
+    lib = _abi.load()
+    st = _stream_handle(src, stream)
+    _abi.check(lib.fa_stream_copy(dst.data_ptr(), src.data_ptr(), src.numel() * src.element_size(), st))
+
+
+def stream_read(src, sink, stream=None):
+    lib = _abi.load()
+    st = _stream_handle(src, stream)
+    _abi.check(lib.fa_stream_read(src.data_ptr(), src.numel() * src.element_size(), sink.data_ptr(), st))
+
+
+def stream_read_sink(src):
+    lib = _abi.load()
+    blocks = lib.fa_stream_read_blocks(src.numel() * src.element_size())
+    return torch.empty(max(1, blocks) * 16, dtype=torch.uint8, device=src.device)

@@ -1,0 +1,91 @@
+"""In-process stand-in for FEDn's combiner UpdateHandler (fedn/network/combiner/updatehandler.py).
+
+Exposes exactly the surface the aggregator plug-ins consume:
+``model_updates`` (a FIFO ``queue.Queue``), ``next_model_update()``,
+``load_model_update(mu, helper) -> (arrays, training_metadata)``, ``load_model(helper,
+model_id)`` and ``delete_model(mu)``. Models live in a dict instead of the combiner's
+temp-file store + npz codec, so tests and benchmarks can drive the plug-ins without
+gRPC. Behaviour mirrors updatehandler.py:35-117: metadata must carry
+``training_metadata.num_examples`` (else the update is rejected at ingest, :72-88) and
+``round_id`` is copied from the config (:106-116).
+"""
+import json
+import queue
+import uuid
+from dataclasses import dataclass
+
+
+@dataclass
+class ModelUpdate:
+    """The fields of fedn.proto ``ModelUpdate`` (fedn.proto:67-76) the aggregators read."""
+
+    model_id: str
+    model_update_id: str
+    meta: str
+    config: str = "{}"
+
+
+class MemoryModelStore:
+    def __init__(self):
+        self.models = {}
+
+    def put(self, model_id, arrays):
+        self.models[model_id] = arrays
+
+    def get(self, model_id):
+        return self.models.get(model_id)
+
+    def delete(self, model_id):
+        return self.models.pop(model_id, None) is not None
+
+
+class MemoryUpdateHandler:
+    def __init__(self, store=None):
+        self.model_updates = queue.Queue()
+        self.store = store or MemoryModelStore()
+
+    # --- producer side (what Combiner.SendModelUpdate -> on_model_update does) ----------
+    def put_global_model(self, arrays, model_id=None):
+        model_id = model_id or str(uuid.uuid4())
+        self.store.put(model_id, arrays)
+        return model_id
+
+    def submit(self, arrays, num_examples, model_id="global", round_id="1"):
+        """Store an update and enqueue its ModelUpdate (on_model_update, updatehandler.py:46-70)."""
+        uid = str(uuid.uuid4())
+        self.store.put(uid, arrays)
+        meta = json.dumps({"training_metadata": {"num_examples": num_examples},
+                           "config": json.dumps({"round_id": round_id})})
+        mu = ModelUpdate(model_id=model_id, model_update_id=uid, meta=meta)
+        self.on_model_update(mu)
+        return mu
+
+    def on_model_update(self, model_update):
+        try:
+            json.loads(model_update.meta)["training_metadata"]["num_examples"]
+        except (KeyError, TypeError, ValueError):
+            return False
+        self.model_updates.put(model_update)
+        return True
+
+    # --- consumer side (what the aggregators call) -------------------------------------
+    def next_model_update(self):
+        return self.model_updates.get(block=False)
+
+    def load_model(self, helper, model_id):
+        model = self.store.get(model_id)
+        if model is None:
+            raise RuntimeError(f"Failed to load model {model_id}.")
+        return model
+
+    def load_model_update(self, model_update, helper):
+        model = self.load_model(helper, model_update.model_update_id)
+        metadata = json.loads(model_update.meta)
+        config = json.loads(metadata["config"]) if "config" in metadata else json.loads(model_update.config)
+        training_metadata = metadata["training_metadata"]
+        if "round_id" in config:
+            training_metadata["round_id"] = config["round_id"]
+        return model, training_metadata
+
+    def delete_model(self, model_update):
+        self.store.delete(model_update.model_update_id)

@@ -1,0 +1,141 @@
+/*
+ * fedagg.h — C ABI of the MI355X (gfx950) aggregation library `libfedagg.so`.
+ *
+ * This is the drop-in boundary for FEDn's combiner-side aggregation hot path
+ * (SURVEY.md §8(b)). Every entry point takes plain pointers, sizes and a
+ * hipStream_t passed as `void*`; no torch or numpy types cross it. Buffers are
+ * owned by the caller (device memory, e.g. PyTorch-ROCm tensors); the library
+ * allocates nothing persistent. Every function returns 0 on success or a
+ * positive FA_E* status; `fa_last_error()` then holds a message (thread-local).
+ *
+ * Reference interfaces each entry point replaces (paths relative to the FEDn
+ * checkout, v0.33.0):
+ *   fa_fedavg_fold   numpyhelper.Helper.increment_average
+ *                    fedn/utils/helpers/plugins/numpyhelper.py:18-32, applied in
+ *                    queue order by fedavg.Aggregator.combine_models
+ *                    fedn/network/combiner/aggregators/fedavg.py:109-133, and by
+ *                    Control.reduce fedn/network/controller/control.py:678-682
+ *   fa_fedopt_step   the pseudo-gradient loop + server optimizer of
+ *                    fedopt.Aggregator.combine_models
+ *                    fedn/network/combiner/aggregators/fedopt.py:74-118 with
+ *                    serveropt_adam   fedopt.py:151-185
+ *                    serveropt_yogi   fedopt.py:187-223
+ *                    serveropt_adagrad fedopt.py:225-258
+ *                    and the helper primitives numpyhelper.py:34-142 they call.
+ *
+ * Numerics contract: results are bit-identical to the numpy reference for the
+ * dtypes it defines (IEEE-754 op-by-op replay of the same expression order, no
+ * FMA contraction, correctly rounded division and square root). bf16 inputs have
+ * no numpy counterpart: they are defined as the fp32 path on the exactly
+ * upcast values.
+ */
+#ifndef FEDAGG_H
+#define FEDAGG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FA_ABI_VERSION 1
+
+/* element type codes */
+enum fa_dtype {
+    FA_NONE = -1, /* "array is None" (FedOpt state before the first round) */
+    FA_F32 = 0,
+    FA_F64 = 1,
+    FA_BF16 = 2,
+    FA_F16 = 3,
+    FA_I32 = 4,
+    FA_I64 = 5
+};
+
+/* status codes */
+enum fa_status {
+    FA_OK = 0,
+    FA_EINVAL = 1,  /* bad argument (null pointer, negative size, K out of range) */
+    FA_EDTYPE = 2,  /* unsupported dtype combination */
+    FA_EHIP = 3     /* a HIP runtime call or kernel launch failed */
+};
+
+/* server optimizers, fedopt.py:141-145 */
+enum fa_serveropt { FA_ADAM = 0, FA_YOGI = 1, FA_ADAGRAD = 2 };
+
+/* fa_fedopt_step flags */
+#define FA_PG_FIRST 1 /* pseudo-gradient starts from updates[0] - old (fedopt.py:89-91); else read from pg */
+#define FA_PG_FINAL 2 /* apply the server step and write m_out, v_out, out; else write pg   */
+
+int fa_abi_version(void);
+const char* fa_last_error(void);
+
+/*
+ * FedAvg incremental weighted fold (numpyhelper.py:32):
+ *     x <- x + (n_k * (y_k - x)) / N_k        for k in queue order
+ *
+ * agg      device buffer, P elements of agg_dtype (the running model)
+ * updates  HOST array of K DEVICE pointers, each P elements of upd_dtype
+ * n, N     HOST arrays of K doubles: num_examples of update k and the running
+ *          total including it (fedavg.py:124), exact integers
+ * init     1: agg := updates[0] (the `model = model_next` alias, fedavg.py:127-128),
+ *             then fold k = 1..K-1;  0: fold k = 0..K-1 into the existing agg
+ * stream   hipStream_t (NULL = default stream)
+ *
+ * dtype pairs (upd, agg) and the compute type numpy would use:
+ *   (F32,F32)->f32  (BF16,F32)->f32  (F16,F16)->f16  (F64,F64)->f64
+ *   (F32,F64)->f64  (I64,F64)/(I32,F64)->int then f64 (numpy true_divide)
+ * With init=1 and K=1 the result is a plain copy and agg_dtype must equal upd_dtype.
+ */
+int fa_fedavg_fold(void* agg, int agg_dtype,
+                   const void* const* updates, int upd_dtype,
+                   const double* n, const double* N, int K,
+                   int64_t P, int init, void* stream);
+
+/*
+ * FedOpt (fedopt.py:74-118, 151-258), fused: pseudo-gradient running mean over the
+ * K updates followed (FA_PG_FINAL) by one Adam / Yogi / AdaGrad server step.
+ *
+ * old       device, P elements of old_dtype (F32 | F64): the global model the
+ *           clients trained from (fedopt.py:90)
+ * updates   HOST array of K DEVICE pointers (F32 | BF16 | F64)
+ * n, N      HOST arrays of K doubles (num_examples, running total)
+ * pg        device workspace, P elements of pg dtype = promote(upd, old); read when
+ *           !FA_PG_FIRST, written when !FA_PG_FINAL (and used internally when
+ *           K exceeds one launch); may be NULL when FIRST|FINAL and K <= 64
+ * m_in      device, P elements of m_in_dtype, or NULL with m_in_dtype = FA_NONE
+ * m_out     device, dtype promote(m_in, pg) (pg dtype when m is None); may alias m_in
+ *           when the dtypes are equal
+ * v_in      device f64, or NULL (v is None -> ones * tau**2, fedopt.py:170-171)
+ * v_out     device f64; may alias v_in
+ * out       device f64 (the new global model, fedopt.py:183)
+ * serveropt FA_ADAM | FA_YOGI | FA_ADAGRAD; lr, beta1, beta2, tau as in fedopt.py:53-59
+ */
+int fa_fedopt_step(const void* old, int old_dtype,
+                   const void* const* updates, int upd_dtype,
+                   const double* n, const double* N, int K,
+                   void* pg, int flags,
+                   const void* m_in, int m_in_dtype, void* m_out,
+                   const double* v_in, double* v_out, double* out,
+                   int serveropt, double lr, double beta1, double beta2, double tau,
+                   int64_t P, void* stream);
+
+/* dtype promotion used by the two entry points above (numpy result_type for the
+ * pairs this library supports; bf16 promotes as f32). Returns FA_NONE if unsupported. */
+int fa_promote(int a, int b);
+
+/*
+ * Measurement helpers (not part of the reference interface): achievable-peak
+ * reference kernels for the roofline section of bench.py.
+ *   fa_stream_copy  dst[i] = src[i], 16 B per lane
+ *   fa_stream_read  reads `bytes` and writes one 16-B word per workgroup to `sink`
+ *                   (sink must hold >= 16 * fa_stream_read_blocks(bytes) bytes)
+ */
+int fa_stream_copy(void* dst, const void* src, int64_t bytes, void* stream);
+int64_t fa_stream_read_blocks(int64_t bytes);
+int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FEDAGG_H */

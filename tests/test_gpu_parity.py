@@ -1,0 +1,247 @@
+"""GPU parity: libfedagg on an MI355X vs the CPU oracle (itself pinned to the reference).
+
+Bar: bit-exact values AND dtypes (NaN payloads excepted) — the kernels replay numpy's
+op order with IEEE rounding (SURVEY.md §0 parity findings 1-3).
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import assert_lists_identical, case_names, load_case
+from oracle import numpy_ref as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    from fedn_amd import _abi
+    _abi.load()
+
+
+def _plugin(name):
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    uh = MemoryUpdateHandler()
+    return uh, get_aggregator(name, uh)
+
+
+# ------------------------------------------------------------------------- golden, plug-in level
+@pytest.mark.parametrize("name", case_names("fedavg"))
+def test_fedavg_plugin_golden(name):
+    rd = load_case(name)["rounds"][0]
+    uh, agg = _plugin("fedavg")
+    for arrays, n in rd["updates"]:
+        uh.submit(arrays, n)
+    model, data = agg.combine_models(helper=None, delete_models=True, parameters=None)
+    assert data["nr_aggregated_models"] == rd["nr"]
+    assert uh.model_updates.qsize() == rd["qsize"]
+    for k in rd["data_keys"]:
+        assert k in data
+    assert_lists_identical(model, rd["out"], name)
+
+
+@pytest.mark.parametrize("name", case_names("fedopt"))
+def test_fedopt_plugin_golden(name):
+    case = load_case(name)
+    uh, agg = _plugin("fedopt")
+    for r, rd in enumerate(case["rounds"]):
+        gid = uh.put_global_model(rd["old"], f"global-{r}")
+        for arrays, n in rd["updates"]:
+            uh.submit(arrays, n, model_id=gid)
+        model, data = agg.combine_models(helper=None, delete_models=True, parameters=case["params"])
+        assert_lists_identical(model, rd["out"], f"{name} r{r} out")
+        assert data.get("nr_aggregated_models", -1) == rd["nr"]
+        assert uh.model_updates.qsize() == rd["qsize"]
+        if rd["m"] is not None:
+            assert_lists_identical(agg.m, rd["m"], f"{name} r{r} m")
+            assert_lists_identical(agg.v, rd["v"], f"{name} r{r} v")
+        else:
+            assert agg.m is None and agg.v is None
+
+
+# ------------------------------------------------------------------------- ops level, random
+def _updates(rng, K, P, dtype=np.float32, offset=0):
+    base = rng.standard_normal(P)
+    ups = [(base + 0.01 * rng.standard_normal(P)).astype(dtype) for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    return ups, ns
+
+
+def _to_dev(a, offset=0):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if offset:
+        big = torch.empty(t.numel() + offset, dtype=t.dtype, device=DEV)
+        d = big[offset:]
+        d.copy_(t.to(DEV))
+        return d
+    return t.to(DEV)
+
+
+def _fold_dev(ups_dev, ns, agg_dtype, chunks=None):
+    from fedn_amd import ops
+    Ns = list(np.cumsum(ns))
+    agg = torch.empty(ups_dev[0].numel(), dtype=agg_dtype, device=DEV)
+    if chunks is None:
+        ops.fedavg_fold(agg, ups_dev, ns, Ns, init=True)
+    else:
+        k0, first = 0, True
+        for c in chunks:
+            ops.fedavg_fold(agg, ups_dev[k0:k0 + c], ns[k0:k0 + c], Ns[k0:k0 + c], init=first)
+            first = False
+            k0 += c
+    torch.cuda.synchronize()
+    return agg.cpu().numpy()
+
+
+@pytest.mark.parametrize("K", [2, 3, 8, 9, 63, 64, 65, 130])
+@pytest.mark.parametrize("P", [1, 5, 4099, 1 << 16])
+def test_fedavg_ops_vs_oracle(K, P):
+    rng = np.random.default_rng(K * 1000 + P)
+    ups, ns = _updates(rng, K, P)
+    want = ref.fedavg_flat(ups, ns)
+    got = _fold_dev([_to_dev(u) for u in ups], ns, torch.float32)
+    assert_lists_identical([got], [want], f"K={K} P={P}")
+
+
+@pytest.mark.parametrize("offset", [1, 2, 3])
+def test_fedavg_misaligned_scalar_path(offset):
+    rng = np.random.default_rng(offset)
+    ups, ns = _updates(rng, 5, 1001)
+    want = ref.fedavg_flat(ups, ns)
+    got = _fold_dev([_to_dev(u, offset) for u in ups], ns, torch.float32)
+    assert_lists_identical([got], [want], "misaligned")
+
+
+def test_fedavg_streaming_chunks_equal_single_pass():
+    rng = np.random.default_rng(7)
+    ups, ns = _updates(rng, 20, 12345)
+    dev = [_to_dev(u) for u in ups]
+    a = _fold_dev(dev, ns, torch.float32)
+    b = _fold_dev(dev, ns, torch.float32, chunks=[1, 2, 5, 1, 11])
+    assert_lists_identical([b], [a], "waves")
+    assert_lists_identical([a], [ref.fedavg_flat(ups, ns)], "oracle")
+
+
+@pytest.mark.parametrize("dt,agg_dt", [(np.float64, torch.float64), (np.float16, torch.float16),
+                                        (np.int64, torch.float64), (np.int32, torch.float64)])
+def test_fedavg_other_dtypes(dt, agg_dt):
+    rng = np.random.default_rng(11)
+    if np.dtype(dt).kind == "i":
+        ups = [rng.integers(-10**6, 10**6, 3001).astype(dt) for _ in range(6)]
+        ns = [int(v) for v in rng.integers(1, 5001, 6)]
+    else:
+        ups, ns = _updates(rng, 6, 3001, dt)
+    want = ref.fedavg_flat(ups, ns)
+    got = _fold_dev([_to_dev(u) for u in ups], ns, agg_dt)
+    assert_lists_identical([got], [want], str(dt))
+
+
+def test_fedavg_f32_updates_into_f64_aggregate():
+    rng = np.random.default_rng(12)
+    ups, ns = _updates(rng, 5, 777)
+    first = ups[0].astype(np.float64)
+    want = ref.fedavg_flat([first] + ups[1:], ns)
+    from fedn_amd import ops
+    agg = _to_dev(first)
+    ops.fedavg_fold(agg, [_to_dev(u) for u in ups[1:]], ns[1:], list(np.cumsum(ns))[1:], init=False)
+    torch.cuda.synchronize()
+    assert_lists_identical([agg.cpu().numpy()], [want], "f32->f64")
+
+
+def test_fedavg_bf16_defined_as_fp32_on_upcast():
+    """bf16 has no numpy reference: parity = fp32 oracle on the exactly upcast values."""
+    rng = np.random.default_rng(13)
+    ups, ns = _updates(rng, 9, 10001)
+    bf = [torch.from_numpy(u).to(torch.bfloat16) for u in ups]
+    up32 = [b.to(torch.float32).numpy() for b in bf]
+    want = ref.fedavg_flat(up32, ns)
+    got = _fold_dev([b.to(DEV) for b in bf], ns, torch.float32)
+    assert_lists_identical([got], [want], "bf16")
+
+
+def test_fedavg_special_values():
+    """zeros, signed zeros, denormals, huge values, inf and NaN follow IEEE like numpy."""
+    vals = np.array([0.0, -0.0, 1e-45, -1e-45, 1e-40, 3e38, -3e38, np.inf, -np.inf, np.nan, 1.0, -2.5],
+                    dtype=np.float32)
+    rng = np.random.default_rng(5)
+    ups = [rng.permutation(np.tile(vals, 11)).astype(np.float32) for _ in range(7)]
+    ns = [3, 1, 4000, 1, 5, 9, 2]
+    with np.errstate(all="ignore"):
+        want = ref.fedavg_flat(ups, ns)
+    got = _fold_dev([_to_dev(u) for u in ups], ns, torch.float32)
+    assert_lists_identical([got], [want], "special")
+
+
+# ------------------------------------------------------------------------- FedOpt ops level
+@pytest.mark.parametrize("opt", ["adam", "yogi", "adagrad"])
+@pytest.mark.parametrize("K", [1, 4, 70])
+@pytest.mark.parametrize("old_dt,upd_dt", [(np.float32, np.float32), (np.float64, np.float32),
+                                           (np.float64, np.float64)])
+def test_fedopt_ops_two_rounds(opt, K, old_dt, upd_dt):
+    from fedn_amd import ops
+    rng = np.random.default_rng(K + len(opt))
+    P = 2053
+    old = rng.standard_normal(P).astype(old_dt)
+    params = {"serveropt": opt, "learning_rate": 1e-2, "beta1": 0.9, "beta2": 0.99, "tau": 1e-3}
+    st = ref.FedOptState()
+    m_dev = v_dev = None
+    for r in range(2):
+        ups = [(old + 0.01 * rng.standard_normal(P)).astype(upd_dt) for _ in range(K)]
+        ns = [int(v) for v in rng.integers(1, 5001, K)]
+        want, _ = ref.fedopt_combine(st, [([u], n) for u, n in zip(ups, ns)], [old], params)
+        old_d = _to_dev(old)
+        pg_dt, m_dt = ops.fedopt_dtypes(ops.torch_dtype(upd_dt), old_d.dtype, None if m_dev is None else m_dev.dtype)
+        pg = torch.empty(P, dtype=pg_dt, device=DEV)
+        m_out = torch.empty(P, dtype=m_dt, device=DEV)
+        v_out = torch.empty(P, dtype=torch.float64, device=DEV)
+        out = torch.empty(P, dtype=torch.float64, device=DEV)
+        ops.fedopt_step(old_d, [_to_dev(u) for u in ups], ns, list(np.cumsum(ns)), first=True, final=True, pg=pg,
+                        m_in=m_dev, m_out=m_out, v_in=v_dev, v_out=v_out, out=out, **params)
+        torch.cuda.synchronize()
+        assert_lists_identical([out.cpu().numpy()], want, f"r{r} out")
+        assert_lists_identical([m_out.cpu().numpy()], st.m, f"r{r} m")
+        assert_lists_identical([v_out.cpu().numpy()], st.v, f"r{r} v")
+        m_dev, v_dev, old = m_out, v_out, want[0]
+
+
+def test_fedopt_bf16_updates():
+    from fedn_amd import ops
+    rng = np.random.default_rng(21)
+    P, K = 4099, 5
+    old = rng.standard_normal(P).astype(np.float32)
+    bf = [torch.from_numpy(old + 0.01 * rng.standard_normal(P).astype(np.float32)).to(torch.bfloat16) for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    st = ref.FedOptState()
+    want, _ = ref.fedopt_combine(st, [([b.float().numpy()], n) for b, n in zip(bf, ns)], [old], {"serveropt": "yogi"})
+    out = torch.empty(P, dtype=torch.float64, device=DEV)
+    m_out = torch.empty(P, dtype=torch.float32, device=DEV)
+    v_out = torch.empty(P, dtype=torch.float64, device=DEV)
+    ops.fedopt_step(_to_dev(old), [b.to(DEV) for b in bf], ns, list(np.cumsum(ns)), first=True, final=True,
+                    m_out=m_out, v_out=v_out, out=out, serveropt="yogi")
+    torch.cuda.synchronize()
+    assert_lists_identical([out.cpu().numpy()], want, "bf16 fedopt")
+
+
+# ------------------------------------------------------------------------- full size, sampled
+@pytest.mark.slow
+def test_fedavg_full_size_sampled():
+    """100 M fp32 x 8 clients (BASELINE config 2) on the GPU; the oracle checks 3 slices.
+    Elementwise independence makes any slice a complete check of the elements in it."""
+    from fedn_amd import ops
+    P, K = 100_000_000, 8
+    g = torch.Generator(device=DEV).manual_seed(0)
+    base = torch.randn(P, generator=g, device=DEV)
+    ups = [base + 0.01 * torch.randn(P, generator=g, device=DEV) for _ in range(K)]
+    ns = [int(v) for v in np.random.default_rng(0).integers(1, 5001, K)]
+    agg = torch.empty(P, device=DEV)
+    ops.fedavg_fold(agg, ups, ns, list(np.cumsum(ns)), init=True)
+    torch.cuda.synchronize()
+    for lo in (0, P // 2 - 12345, P - 1_000_003):
+        sl = slice(lo, lo + 1_000_003)
+        want = ref.fedavg_flat([u[sl].cpu().numpy() for u in ups], ns)
+        assert_lists_identical([agg[sl].cpu().numpy()], [want], f"slice {lo}")

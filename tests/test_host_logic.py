@@ -1,0 +1,91 @@
+"""Host-side logic of the plug-ins that needs no GPU: layout, parameters, loader, empty rounds."""
+import numpy as np
+import pytest
+import torch
+
+from fedn_amd import ops
+from fedn_amd.aggregators import get_aggregator
+from fedn_amd.exceptions import InvalidParameterError
+from fedn_amd.layout import ALIGN, Layout
+from fedn_amd.parameters import Parameters
+from fedn_amd.updatehandler import MemoryUpdateHandler
+
+
+def test_layout_groups_alignment_roundtrip():
+    rng = np.random.default_rng(0)
+    arrays = [rng.standard_normal((3, 5)).astype(np.float32), np.arange(7, dtype=np.int64),
+              rng.standard_normal(11).astype(np.float32), np.float32(2.5) * np.ones((), np.float32),
+              rng.standard_normal((2, 2)).astype(np.float64)]
+    lay = Layout.of(arrays)
+    assert [str(d) for d in lay.groups] == ["float32", "int64", "float64"]
+    for dt in lay.groups:
+        assert lay.group_byte_offset[dt] % ALIGN == 0
+    assert lay.group_elems[np.dtype(np.float32)] == 15 + 11 + 1
+    buf = np.zeros(lay.nbytes, np.uint8)
+    lay.pack(arrays, buf)
+    out = [None] * len(arrays)
+    for dt in lay.groups:
+        lay.unpack_group(lay.group_view(buf, dt), dt, out)
+    for a, b in zip(arrays, out):
+        assert a.dtype == b.dtype and a.shape == b.shape
+        np.testing.assert_array_equal(a, b)
+
+
+def test_layout_check_mismatch():
+    lay = Layout.of([np.zeros((3,), np.float32)])
+    with pytest.raises(ValueError):
+        lay.check([np.zeros((4,), np.float32)])
+    with pytest.raises(ValueError):
+        lay.check([np.zeros((3,), np.float32)] * 2)
+    with pytest.raises(TypeError):
+        lay.check([np.zeros((3,), np.float64)])
+
+
+def test_parameters_validate_mirror():
+    schema = {"serveropt": str, "learning_rate": float}
+    assert Parameters({"serveropt": "adam", "learning_rate": 0.1}).validate(schema)
+    with pytest.raises(InvalidParameterError):
+        Parameters({"learning_rate": 1}).validate(schema)     # int rejected, like FEDn
+    with pytest.raises(InvalidParameterError):
+        Parameters({"momentum": 0.1}).validate(schema)
+    assert not issubclass(InvalidParameterError, Exception)   # BaseException, fedn/common/exceptions.py:9
+
+
+def test_result_dtype_rules():
+    f32, f64, f16, bf, i64 = torch.float32, torch.float64, torch.float16, torch.bfloat16, torch.int64
+    assert ops.fold_result_dtype(f32, f32) == f32
+    assert ops.fold_result_dtype(f32, f64) == f64
+    assert ops.fold_result_dtype(f16, f16) == f16
+    assert ops.fold_result_dtype(f32, bf) == f32
+    assert ops.fold_result_dtype(i64, i64) == f64
+    assert ops.fedopt_dtypes(f32, f32, None) == (f32, f32)
+    assert ops.fedopt_dtypes(f32, f64, f32) == (f64, f64)
+    assert ops.fedopt_dtypes(bf, f32, None) == (f32, f32)
+
+
+@pytest.mark.parametrize("name", ["fedavg", "fedopt"])
+def test_get_aggregator_and_empty_round(name):
+    uh = MemoryUpdateHandler()
+    agg = get_aggregator(name, uh)
+    assert agg.name == name and agg.update_handler is uh
+    model, data = agg.combine_models(helper=None, delete_models=True, parameters=None)
+    assert model is None
+    assert data["nr_aggregated_models"] == 0
+    assert data["time_model_load"] == 0.0 and data["time_model_aggregation"] == 0.0
+
+
+@pytest.mark.parametrize("params", [{"learning_rate": 1}, {"momentum": 0.5}])
+def test_fedopt_bad_parameters_leave_queue(params):
+    """fedopt.py:62-66: invalid kwargs -> (None, data) before the queue is touched."""
+    uh = MemoryUpdateHandler()
+    uh.submit([np.zeros(3, np.float32)], 10)
+    model, data = get_aggregator("fedopt", uh).combine_models(parameters=params)
+    assert model is None and "nr_aggregated_models" not in data
+    assert uh.model_updates.qsize() == 1
+
+
+def test_update_handler_rejects_missing_metadata():
+    from fedn_amd.updatehandler import ModelUpdate
+    uh = MemoryUpdateHandler()
+    assert not uh.on_model_update(ModelUpdate("g", "u", '{"training_metadata": {}}'))
+    assert uh.model_updates.empty()

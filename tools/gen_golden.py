@@ -1,0 +1,260 @@
+"""Generate the golden parity fixtures under ``tests/golden/`` by running FEDn ITSELF.
+
+THIS SCRIPT IS TEST INFRASTRUCTURE. It runs only in the build container where the
+read-only reference checkout exists at ``/root/reference``; it refuses to run anywhere
+else (the GPU box has no reference). Only its OUTPUT (small ``.npz`` data files:
+inputs + expected outputs) is committed and shipped; no reference source travels.
+
+What it drives (all real reference code, imported from /root/reference):
+  * ``fedn/utils/helpers/plugins/numpyhelper.py``   Helper (increment_average, add, ...)
+  * ``fedn/network/combiner/aggregators/fedavg.py``  Aggregator.combine_models
+  * ``fedn/network/combiner/aggregators/fedopt.py``  Aggregator.combine_models (adam/yogi/adagrad)
+  * ``fedn/network/combiner/updatehandler.py``       UpdateHandler (FIFO queue, load_model_update)
+  * ``fedn/network/combiner/modelservice.py``        ModelService (npz wire codec, temp storage)
+Updates are pushed exactly as the combiner receives them: npz bytes uploaded through
+``ModelService.set_model`` and a ``fedn_pb2.ModelUpdate`` proto with
+``meta = {"training_metadata": {"num_examples": n}, "config": ...}`` handed to
+``UpdateHandler.on_model_update``.
+
+Import workaround: ``fedn/__init__.py`` and ``fedn/common/log_config.py``
+pull in opentelemetry (not installed). We pre-register a bare ``fedn`` package and a stub
+``fedn.common.log_config`` exposing ``logger``; nothing else is stubbed.
+
+Usage:  python tools/gen_golden.py            (writes tests/golden/*.npz + manifest.json)
+"""
+import json
+import logging
+import os
+import sys
+import tempfile
+import types
+import uuid
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "..", "tests", "golden")
+
+
+def _import_reference():
+    if not os.path.isdir(os.path.join(REF, "fedn")):
+        raise SystemExit("gen_golden: /root/reference is absent; fixtures are generated only in the build container")
+    sys.dont_write_bytecode = True  # /root/reference is read-only
+    os.environ.setdefault("FEDN_MODEL_DIR", tempfile.mkdtemp(prefix="fedn_models_"))
+    pkg = types.ModuleType("fedn")
+    pkg.__path__ = [os.path.join(REF, "fedn")]
+    sys.modules["fedn"] = pkg
+    common = types.ModuleType("fedn.common")
+    common.__path__ = [os.path.join(REF, "fedn", "common")]
+    sys.modules["fedn.common"] = common
+    lc = types.ModuleType("fedn.common.log_config")
+    lg = logging.getLogger("fedn")
+    lg.setLevel(logging.CRITICAL)
+    lc.logger = lg
+    sys.modules["fedn.common.log_config"] = lc
+    from fedn.network.combiner.aggregators import fedavg, fedopt  # noqa: E402
+    from fedn.network.combiner.modelservice import ModelService  # noqa: E402
+    from fedn.network.combiner.updatehandler import UpdateHandler  # noqa: E402
+    from fedn.network.grpc import fedn_pb2  # noqa: E402
+    from fedn.utils.helpers.plugins.numpyhelper import Helper  # noqa: E402
+    from fedn.utils.parameters import Parameters  # noqa: E402
+
+    return dict(fedavg=fedavg, fedopt=fedopt, ModelService=ModelService, UpdateHandler=UpdateHandler,
+                pb2=fedn_pb2, Helper=Helper, Parameters=Parameters)
+
+
+class Harness:
+    """One combiner-side session: ModelService + UpdateHandler + an aggregator instance."""
+
+    def __init__(self, ref, agg_name):
+        self.ref = ref
+        self.ms = ref["ModelService"]()
+        self.uh = ref["UpdateHandler"](self.ms)
+        self.helper = ref["Helper"]()
+        self.agg = ref[agg_name].Aggregator(self.uh)
+
+    def put_model(self, arrays, model_id):
+        self.ms.set_model(arrays, model_id)
+
+    def push_update(self, arrays, n, global_model_id):
+        uid = str(uuid.uuid4())
+        self.put_model(arrays, uid)
+        meta = json.dumps({"training_metadata": {"num_examples": n, "batch_size": 32, "epochs": 1},
+                           "config": json.dumps({"round_id": "1"})})
+        mu = self.ref["pb2"].ModelUpdate(model_id=global_model_id, model_update_id=uid, meta=meta)
+        self.uh.on_model_update(mu)
+
+    def combine(self, parameters=None):
+        return self.agg.combine_models(helper=self.helper, delete_models=True, parameters=parameters)
+
+
+def _store_list(d, prefix, arrays):
+    for t, a in enumerate(arrays):
+        d[f"{prefix}_t{t}"] = np.asarray(a)
+    d[f"{prefix}_len"] = np.array(len(arrays))
+
+
+def _rng_model(rng, shapes, dtype):
+    return [rng.standard_normal(s).astype(dtype) for s in shapes]
+
+
+def _perturb(rng, model, dtype, scale=0.01):
+    return [(np.asarray(w, dtype=np.float64) + scale * rng.standard_normal(np.shape(w))).astype(dtype) for w in model]
+
+
+ODD_SHAPES = [(7,), (3, 5, 11), (1,), (129, 3), ()]
+MNIST_SHAPES = [(64, 784), (64,), (32, 64), (32,), (10, 32), (10,)]  # examples/mnist-pytorch/client/model.py:18-32
+
+
+def fedavg_case(ref, name, rng, shapes, dtype, nks, bad_index=None, special=None, int_vals=False):
+    h = Harness(ref, "fedavg")
+    d = {"kind": np.array("fedavg"), "name": np.array(name)}
+    base = _rng_model(rng, shapes, np.float64)
+    if special == "tiny":
+        base = [w * np.float64(1e-41) for w in base]  # fp32 denormal range
+    ups = []
+    for k, n in enumerate(nks):
+        if int_vals:
+            u = [rng.integers(-1000, 1000, size=s).astype(dtype) for s in shapes]
+        else:
+            scale = 1e-41 if special == "tiny" else 0.01
+            u = _perturb(rng, base, dtype, scale)
+            if special == "wide":
+                u = [w * np.asarray(10.0 ** rng.integers(-30, 30, size=np.shape(w)), dtype=dtype) for w in u]
+                for w in u:
+                    if w.size > 2:
+                        w.flat[0] = 0.0
+                        w.flat[1] = -0.0
+        if bad_index is not None and k == bad_index:
+            u = [np.zeros((s[0] + 1,) + tuple(s[1:]) if len(s) else (2,), dtype) for s in shapes]
+        ups.append(u)
+        h.push_update(u, int(n), "global-0")
+        _store_list(d, f"r0_u{k}", u)
+    d["r0_n"] = np.array(nks, dtype=np.int64)
+    d["r0_K"] = np.array(len(nks))
+    model, data = h.combine()
+    d["r0_nr"] = np.array(data["nr_aggregated_models"])
+    d["r0_data_keys"] = np.array(json.dumps(sorted(data)))
+    d["r0_qsize"] = np.array(h.uh.model_updates.qsize())
+    d["r0_out_none"] = np.array(model is None)
+    if model is not None:
+        _store_list(d, "r0_out", model)
+    d["rounds"] = np.array(1)
+    return d
+
+
+def fedopt_case(ref, name, rng, shapes, nks_per_round, params=None, old_dtype=np.float32, upd_dtype=np.float32):
+    h = Harness(ref, "fedopt")
+    d = {"kind": np.array("fedopt"), "name": np.array(name)}
+    d["params"] = np.array(json.dumps(params if params is not None else None))
+    old = _rng_model(rng, shapes, old_dtype)
+    for r, nks in enumerate(nks_per_round):
+        gid = f"global-{r}"
+        h.put_model(old, gid)
+        _store_list(d, f"r{r}_old", old)
+        for k, n in enumerate(nks):
+            u = _perturb(rng, old, upd_dtype)
+            h.push_update(u, int(n), gid)
+            _store_list(d, f"r{r}_u{k}", u)
+        d[f"r{r}_n"] = np.array(nks, dtype=np.int64)
+        d[f"r{r}_K"] = np.array(len(nks))
+        p = ref["Parameters"](params) if params is not None else None
+        model, data = h.combine(p)
+        d[f"r{r}_nr"] = np.array(data.get("nr_aggregated_models", -1))
+        d[f"r{r}_data_keys"] = np.array(json.dumps(sorted(data)))
+        d[f"r{r}_qsize"] = np.array(h.uh.model_updates.qsize())
+        d[f"r{r}_out_none"] = np.array(model is None)
+        if model is not None:
+            _store_list(d, f"r{r}_out", model)
+        d[f"r{r}_m_none"] = np.array(h.agg.m is None)
+        d[f"r{r}_v_none"] = np.array(h.agg.v is None)
+        if h.agg.m is not None:
+            _store_list(d, f"r{r}_m", h.agg.m)
+        if h.agg.v is not None:
+            _store_list(d, f"r{r}_v", h.agg.v)
+        if model is not None:
+            old = model  # next round's global model is this round's output (fp64), as in FEDn
+    d["rounds"] = np.array(len(nks_per_round))
+    return d
+
+
+def helper_kat(ref):
+    """numpyhelper known-answer test, fedn/utils/helpers/tests/test_numpyhelper.py:20-29."""
+    h = ref["Helper"]()
+    res = h.increment_average([np.array([1, 2, 3])], [np.array([4, 5, 6])], 10, 20)
+    return {"kind": np.array("helper_kat"), "name": np.array("kat_int64"), "m1_t0": np.array([1, 2, 3]),
+            "m2_t0": np.array([4, 5, 6]), "a": np.array(10), "W": np.array(20), "out_t0": res[0]}
+
+
+def helper_ops(ref, rng):
+    """Elementwise helper primitives a9 (numpyhelper.py:34-142) on mixed dtypes."""
+    h = ref["Helper"]()
+    x32 = rng.standard_normal(257).astype(np.float32)
+    y32 = rng.standard_normal(257).astype(np.float32)
+    x64 = rng.standard_normal(257)
+    d = {"kind": np.array("helper_ops"), "name": np.array("helper_ops"), "x32": x32, "y32": y32, "x64": x64}
+    d["add_32_32"] = h.add([x32], [y32], 0.9, 0.1)[0]
+    d["add_64_32"] = h.add([x64], [y32], 0.99, 1.0 - 0.99)[0]
+    d["sub_32_64"] = h.subtract([x32], [x64])[0]
+    d["mul_32_s"] = h.multiply([x32], [1.0 - 0.9])[0]
+    d["pow_32"] = h.power([x32], 2)[0]
+    d["sqrt_64"] = h.sqrt([np.abs(x64)])[0]
+    d["div_32_64"] = h.divide([x32], [np.abs(x64) + 1.0])[0]
+    d["sign_64"] = h.sign([np.concatenate([x64, [0.0, -0.0]])])[0]
+    d["ones_32"] = h.ones([x32], 1e-4 ** 2)[0]
+    d["norm_32"] = np.array(h.norm([x32, y32]))
+    return d
+
+
+def main():
+    ref = _import_reference()
+    os.makedirs(OUT, exist_ok=True)
+    cases = []
+    cases.append(helper_kat(ref))
+    rng = np.random.default_rng(1)
+    cases.append(helper_ops(ref, rng))
+    # FedAvg ------------------------------------------------------------------------
+    rng = np.random.default_rng(2)
+    cases.append(fedavg_case(ref, "fedavg_mnist_k2", rng, MNIST_SHAPES, np.float32, rng.integers(1, 5001, 2)))
+    for K in (1, 2, 3, 8, 17):
+        cases.append(fedavg_case(ref, f"fedavg_odd_k{K}", rng, ODD_SHAPES, np.float32, rng.integers(1, 5001, K)))
+    cases.append(fedavg_case(ref, "fedavg_f64_k3", rng, ODD_SHAPES, np.float64, rng.integers(1, 5001, 3)))
+    cases.append(fedavg_case(ref, "fedavg_bigN_k5", rng, ODD_SHAPES, np.float32,
+                             rng.integers(5_000_000, 20_000_000, 5)))
+    cases.append(fedavg_case(ref, "fedavg_int64_k3", rng, ODD_SHAPES, np.int64, rng.integers(1, 5001, 3), int_vals=True))
+    cases.append(fedavg_case(ref, "fedavg_int32_k3", rng, ODD_SHAPES, np.int32, rng.integers(1, 5001, 3), int_vals=True))
+    cases.append(fedavg_case(ref, "fedavg_skipbad_k4", rng, ODD_SHAPES, np.float32, rng.integers(1, 5001, 4), bad_index=2))
+    cases.append(fedavg_case(ref, "fedavg_empty", rng, ODD_SHAPES, np.float32, []))
+    cases.append(fedavg_case(ref, "fedavg_tiny_k6", rng, [(1000,)], np.float32, rng.integers(1, 5001, 6), special="tiny"))
+    cases.append(fedavg_case(ref, "fedavg_wide_k6", rng, [(1000,)], np.float32, rng.integers(1, 5001, 6), special="wide"))
+    cases.append(fedavg_case(ref, "fedavg_flat_k8", rng, [(4099,)], np.float32, rng.integers(1, 5001, 8)))
+    # FedOpt ------------------------------------------------------------------------
+    rng = np.random.default_rng(3)
+    for opt in ("adam", "yogi", "adagrad"):
+        params = None if opt == "adam" else {"serveropt": opt}
+        cases.append(fedopt_case(ref, f"fedopt_{opt}_3r", rng, ODD_SHAPES,
+                                 [list(rng.integers(1, 5001, 3)) for _ in range(3)], params))
+        cases.append(fedopt_case(ref, f"fedopt_{opt}_lr1e-2_k8", rng, [(2053,)],
+                                 [list(rng.integers(1, 5001, 8)), list(rng.integers(1, 5001, 5))],
+                                 {"serveropt": opt, "learning_rate": 1e-2, "beta1": 0.9, "beta2": 0.99, "tau": 1e-3}))
+    cases.append(fedopt_case(ref, "fedopt_adam_k1", rng, ODD_SHAPES, [[17], [4000]]))
+    cases.append(fedopt_case(ref, "fedopt_adam_f64old", rng, ODD_SHAPES, [list(rng.integers(1, 5001, 4))],
+                             None, old_dtype=np.float64))
+    cases.append(fedopt_case(ref, "fedopt_badparam_int_lr", rng, ODD_SHAPES, [[10, 20]], {"learning_rate": 1}))
+    cases.append(fedopt_case(ref, "fedopt_badparam_key", rng, ODD_SHAPES, [[10, 20]], {"momentum": 0.5}))
+    cases.append(fedopt_case(ref, "fedopt_badopt", rng, ODD_SHAPES, [[10, 20]], {"serveropt": "sgd"}))
+
+    manifest = []
+    for c in cases:
+        name = str(c["name"])
+        np.savez(os.path.join(OUT, name + ".npz"), **c)
+        manifest.append(name)
+    with open(os.path.join(OUT, "manifest.json"), "w") as f:
+        json.dump({"generator": "tools/gen_golden.py", "numpy": np.__version__, "cases": manifest}, f, indent=1)
+    total = sum(os.path.getsize(os.path.join(OUT, n + ".npz")) for n in manifest)
+    print(f"wrote {len(manifest)} fixtures, {total / 1e6:.2f} MB")
+
+
+if __name__ == "__main__":
+    main()
