@@ -93,17 +93,53 @@ __device__ __forceinline__ uint16_t f32_to_f16(float f) {
 struct CF32 {            // float32 ufunc loops
     using V = float;     // register type
     using S = float;     // scalar (n, N) type
-    __device__ static __forceinline__ V fold(V x, V y, S n, S N) {
-        V t = y - x;
-        t = n * t;
-        t = t / N;
-        return x + t;
+    __device__ static __forceinline__ V fold(V x, V y, S n, S N, double r) {
+        V t[1] = {x}, yy[1] = {y};
+        fold_strip<1>(t, yy, n, N, r);
+        return t[0];
+    }
+    // One client step over E elements: x <- x + (n*(y-x))/N.
+    // t/N is correctly rounded. N is the same for every element of a client step, so
+    // the host supplies r = RN64(1/N) and the quotient is RN32(RN64(t * r)): its
+    // relative error is < 2^-52, while t/N (t, N binary32, N's odd part < 2^24) is
+    // never closer than 2^-49 (relative) to a binary32 rounding midpoint in the normal
+    // range, so the final rounding lands where IEEE division does (DESIGN.md has the
+    // argument; tests/test_gpu_divide.py checks every binary32 t exhaustively).
+    // r == 0 (host: N == 0, |N| >= 2^28, or fa_tune) selects IEEE division; lanes with
+    // 0 < |t| < 2^-98 (a subnormal quotient is possible) redo it with IEEE division.
+    template <int E>
+    __device__ static __forceinline__ void fold_strip(V (&x)[E], const V (&y)[E], S n, S N, double r) {
+        V t[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            t[e] = y[e] - x[e];
+            t[e] = n * t[e];
+        }
+        if (r != 0.0) {
+            V q[E];
+            bool tiny = false;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                q[e] = (float)((double)t[e] * r);
+                tiny |= __builtin_fabsf(t[e]) < 0x1p-98f && t[e] != 0.0f;
+            }
+            if (__builtin_expect(tiny, 0)) {
+#pragma unroll
+                for (int e = 0; e < E; ++e)
+                    if (__builtin_fabsf(t[e]) < 0x1p-98f) q[e] = t[e] / N;
+            }
+#pragma unroll
+            for (int e = 0; e < E; ++e) x[e] = x[e] + q[e];
+        } else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) x[e] = x[e] + t[e] / N;
+        }
     }
 };
 struct CF64 {            // float64 ufunc loops
     using V = double;
     using S = double;
-    __device__ static __forceinline__ V fold(V x, V y, S n, S N) {
+    __device__ static __forceinline__ V fold(V x, V y, S n, S N, double) {
         V t = y - x;
         t = n * t;
         t = t / N;
@@ -114,13 +150,25 @@ struct CF16 {            // numpy half loops: op in float, round to half after e
     using V = float;     // holds a value exactly representable in f16
     using S = float;     // n, N pre-rounded to f16 on the host
     __device__ static __forceinline__ V rh(float a) { return f16_to_f32(f32_to_f16(a)); }
-    __device__ static __forceinline__ V fold(V x, V y, S n, S N) {
+    __device__ static __forceinline__ V fold(V x, V y, S n, S N, double) {
         V t = rh(y - x);
         t = rh(n * t);
         t = rh(t / N);
         return rh(x + t);
     }
 };
+
+// element-wise client step for policies without a strip-level shortcut
+template <class CP, int E>
+__device__ __forceinline__ void fold_strip(typename CP::V (&x)[E], const typename CP::V (&y)[E], typename CP::S n,
+                                           typename CP::S N, double r) {
+    if constexpr (std::is_same<CP, CF32>::value) {
+        CP::template fold_strip<E>(x, y, n, N, r);
+    } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) x[e] = CP::fold(x[e], y[e], n, N, r);
+    }
+}
 
 // load one element of storage type T, widened to the compute register type V
 template <typename T, typename V> __device__ __forceinline__ V widen(T v) { return static_cast<V>(v); }
@@ -177,21 +225,18 @@ struct ClientTable {
     const void* ptr[kMaxK];
     S n[kMaxK];
     S N[kMaxK];
+    double r[kMaxK];   // RN64(1/N) for CF32's division shortcut, 0 = use IEEE division
 };
 
-// MODE_INIT: x starts from updates[0]; MODE_CONT: x starts from agg.
-// INT_FIRST: integer updates, first fold in integer arithmetic (numpy int64/int32
-//            subtract + multiply wrap, then true_divide to f64), fedavg.py:127-130.
+// Start one strip's running value. INIT: x := updates[0] (the `model = model_next`
+// alias, fedavg.py:127-128); else x := agg (continuing a chunked / streamed fold).
+// INT_FIRST: integer updates; the first fold runs in integer arithmetic (numpy int
+// subtract + multiply wrap), then true_divide to f64 (numpyhelper.py:32 on int arrays).
+// Returns the first client index still to fold.
 template <typename Y, typename X, class CP, int E, bool INIT, bool INT_FIRST, bool NT>
-__global__ void __launch_bounds__(kBlock)
-k_fedavg(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P) {
+__device__ __forceinline__ int strip_start(typename CP::V (&x)[E], const X* __restrict__ agg,
+                                           const ClientTable<typename CP::S>& tab, int64_t i0, int rem) {
     using V = typename CP::V;
-    const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * E;
-    if (i0 >= P) return;
-    const int rem = (P - i0) < E ? (int)(P - i0) : E;
-
-    V x[E];
-    int k = 0;
     if constexpr (INIT) {
         const Y* y0p = static_cast<const Y*>(tab.ptr[0]) + i0;
         Y y0[E];
@@ -201,23 +246,21 @@ k_fedavg(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K
             for (int e = 0; e < E; ++e) y0[e] = e < rem ? y0p[e] : Y{};
         }
         if constexpr (INT_FIRST) {
-            // k = 1 in integer arithmetic (K >= 2 guaranteed by the host)
-            const Y* y1p = static_cast<const Y*>(tab.ptr[1]) + i0;
+            const Y* y1p = static_cast<const Y*>(tab.ptr[1]) + i0;   // K >= 2 guaranteed by the host
             using U = typename std::make_unsigned<Y>::type;
             const U n1 = (U)(int64_t)tab.n[1];
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                Y y1 = e < rem ? y1p[e] : Y{};
-                U t = (U)y1 - (U)y0[e];              // wrapping subtract
-                t = n1 * t;                          // wrapping multiply
-                double q = (double)(Y)t / (double)tab.N[1];
-                x[e] = (double)y0[e] + q;
+                const Y y1 = e < rem ? y1p[e] : Y{};
+                U t = (U)y1 - (U)y0[e];   // wrapping subtract
+                t = n1 * t;               // wrapping multiply
+                x[e] = (double)y0[e] + (double)(Y)t / (double)tab.N[1];
             }
-            k = 2;
+            return 2;
         } else {
 #pragma unroll
             for (int e = 0; e < E; ++e) x[e] = widen<Y, V>(y0[e]);
-            k = 1;
+            return 1;
         }
     } else {
         X xa[E];
@@ -228,41 +271,84 @@ k_fedavg(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K
         }
 #pragma unroll
         for (int e = 0; e < E; ++e) x[e] = widen<X, V>(xa[e]);
+        return 0;
     }
+}
 
-    if (rem == E) {
-        // steady state: U strips in flight, then U dependent folds
-        for (; k + kUnroll <= K; k += kUnroll) {
-            Y y[kUnroll][E];
+// One lane owns S strips of E elements (strip s at lane + s*kBlock within the block's
+// span, so every wave instruction stays a contiguous 1 KiB). U clients' strips are
+// loaded before any of them is folded, so a lane keeps U*S 16-B loads in flight.
+template <typename Y, typename X, class CP, int E, int S, int U, bool INIT, bool INT_FIRST, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedavg(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P) {
+    using V = typename CP::V;
+    using Sc = typename CP::S;
+    const int64_t strip0 = (int64_t)blockIdx.x * (kBlock * S) + threadIdx.x;
+    if ((strip0 + (int64_t)(S - 1) * kBlock) * E + E <= P) {
+        V x[S][E];
+        int k = 0;
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u)
-                strip_load<Y, E, NT>(static_cast<const Y*>(tab.ptr[k + u]) + i0, y[u]);
+        for (int s = 0; s < S; ++s)
+            k = strip_start<Y, X, CP, E, INIT, INT_FIRST, NT>(x[s], agg, tab, (strip0 + s * kBlock) * E, E);
+        for (; k + U <= K; k += U) {
+            Y y[U][S][E];
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const typename CP::S n = tab.n[k + u], N = tab.N[k + u];
+            for (int u = 0; u < U; ++u) {
+                const Y* yp = static_cast<const Y*>(tab.ptr[k + u]);
 #pragma unroll
-                for (int e = 0; e < E; ++e) x[e] = CP::fold(x[e], widen<Y, V>(y[u][e]), n, N);
+                for (int s = 0; s < S; ++s) strip_load<Y, E, NT>(yp + (strip0 + s * kBlock) * E, y[u][s]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const Sc n = tab.n[k + u], N = tab.N[k + u];
+                const double r = tab.r[k + u];
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    V yv[E];
+#pragma unroll
+                    for (int e = 0; e < E; ++e) yv[e] = widen<Y, V>(y[u][s][e]);
+                    fold_strip<CP, E>(x[s], yv, n, N, r);
+                }
             }
         }
         for (; k < K; ++k) {
-            Y y[E];
-            strip_load<Y, E, NT>(static_cast<const Y*>(tab.ptr[k]) + i0, y);
-            const typename CP::S n = tab.n[k], N = tab.N[k];
+            const Y* yp = static_cast<const Y*>(tab.ptr[k]);
+            Y y[S][E];
 #pragma unroll
-            for (int e = 0; e < E; ++e) x[e] = CP::fold(x[e], widen<Y, V>(y[e]), n, N);
+            for (int s = 0; s < S; ++s) strip_load<Y, E, NT>(yp + (strip0 + s * kBlock) * E, y[s]);
+            const Sc n = tab.n[k], N = tab.N[k];
+            const double r = tab.r[k];
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                V yv[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) yv[e] = widen<Y, V>(y[s][e]);
+                fold_strip<CP, E>(x[s], yv, n, N, r);
+            }
         }
-        X xo[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) xo[e] = narrow<X, V>(x[e]);
-        strip_store<X, E>(agg + i0, xo);
+        for (int s = 0; s < S; ++s) {
+            X xo[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) xo[e] = narrow<X, V>(x[s][e]);
+            strip_store<X, E>(agg + (strip0 + s * kBlock) * E, xo);
+        }
     } else {
-        // ragged tail strip (at most one lane per launch)
-        for (; k < K; ++k) {
-            const Y* yp = static_cast<const Y*>(tab.ptr[k]) + i0;
-            const typename CP::S n = tab.n[k], N = tab.N[k];
-            for (int e = 0; e < rem; ++e) x[e] = CP::fold(x[e], widen<Y, V>(yp[e]), n, N);
+        // the grid's last block: strips may be ragged or past the end
+        for (int s = 0; s < S; ++s) {
+            const int64_t i0 = (strip0 + s * kBlock) * E;
+            if (i0 >= P) break;
+            const int rem = (P - i0) < E ? (int)(P - i0) : E;
+            V x[E];
+            int k = strip_start<Y, X, CP, E, INIT, INT_FIRST, false>(x, agg, tab, i0, rem);
+            for (; k < K; ++k) {
+                const Y* yp = static_cast<const Y*>(tab.ptr[k]) + i0;
+                const Sc n = tab.n[k], N = tab.N[k];
+            const double r = tab.r[k];
+                for (int e = 0; e < rem; ++e) x[e] = CP::fold(x[e], widen<Y, V>(yp[e]), n, N, r);
+            }
+            for (int e = 0; e < rem; ++e) agg[i0 + e] = narrow<X, V>(x[e]);
         }
-        for (int e = 0; e < rem; ++e) agg[i0 + e] = narrow<X, V>(x[e]);
     }
 }
 
@@ -349,17 +435,21 @@ k_fedopt(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::
 #pragma unroll
             for (int u = 0; u < kUnroll / 2; ++u) {
                 const typename PG::S n = tab.n[k + u], N = tab.N[k + u];
+                const double r = tab.r[k + u];
+                V d[E];
 #pragma unroll
-                for (int e = 0; e < E; ++e) pg[e] = PG::fold(pg[e], widen<Y, V>(y[u][e]) - ov[e], n, N);
+                for (int e = 0; e < E; ++e) d[e] = widen<Y, V>(y[u][e]) - ov[e];   // subtract(next, old)
+                fold_strip<PG, E>(pg, d, n, N, r);
             }
         }
     }
     for (; k < K; ++k) {
         const Y* yp = static_cast<const Y*>(tab.ptr[k]) + i0;
         const typename PG::S n = tab.n[k], N = tab.N[k];
+        const double r = tab.r[k];
 #pragma unroll
         for (int e = 0; e < E; ++e)
-            if (e < rem) pg[e] = PG::fold(pg[e], widen<Y, V>(yp[e]) - ov[e], n, N);
+            if (e < rem) pg[e] = PG::fold(pg[e], widen<Y, V>(yp[e]) - ov[e], n, N, r);
     }
 
     if constexpr (!FINAL) {
@@ -479,17 +569,24 @@ __global__ void __launch_bounds__(kBlock) k_stream_read(const u32x4* __restrict_
 // ----------------------------------------------------------------------------
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+int g_fastdiv = 1;
+
 template <typename S>
 void fill_table(ClientTable<S>& t, const void* const* ptrs, const double* n, const double* N, int k0, int cnt) {
     for (int j = 0; j < cnt; ++j) {
         t.ptr[j] = ptrs[k0 + j];
         t.n[j] = (S)n[k0 + j];
         t.N[j] = (S)N[k0 + j];
+        // reciprocal for CF32's division shortcut: only for N that keep every normal-range
+        // quotient normal (|N| < 2^28) and only when enabled
+        const float Nf = (float)N[k0 + j];
+        t.r[j] = (g_fastdiv && Nf != 0.0f && std::fabs(Nf) < 0x1p28f) ? 1.0 / (double)Nf : 0.0;
     }
     for (int j = cnt; j < kMaxK; ++j) {
         t.ptr[j] = nullptr;
         t.n[j] = 0;
         t.N[j] = 0;
+        t.r[j] = 0.0;
     }
 }
 
@@ -504,17 +601,58 @@ int64_t grid_for(int64_t P, int E) {
     return (strips + kBlock - 1) / kBlock;
 }
 
+// FedAvg launch geometry (fa_tune): strips per lane, clients in flight, non-temporal loads.
+struct FedAvgCfg {
+    int strips = 1;
+    int unroll = 8;
+    int nt = 0;   // measured: cached loads beat non-temporal ones by ~3% (profiles/)
+};
+FedAvgCfg g_cfg;
+
+template <typename Y, typename X, class CP, int E, int S, int U, bool NT>
+void launch_fedavg_geom(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
+                        hipStream_t st) {
+    const int64_t strips = (P + E - 1) / E;
+    const dim3 grid((unsigned)((strips + (int64_t)kBlock * S - 1) / ((int64_t)kBlock * S)));
+    if (first && int_first) {
+        if constexpr (std::is_integral<Y>::value)
+            hipLaunchKernelGGL((k_fedavg<Y, X, CP, E, S, U, true, true, NT>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+    } else if (first)
+        hipLaunchKernelGGL((k_fedavg<Y, X, CP, E, S, U, true, false, NT>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+    else
+        hipLaunchKernelGGL((k_fedavg<Y, X, CP, E, S, U, false, false, NT>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+}
+
+// The tunable geometries are instantiated for the fp32 hot path only; other dtypes use the default.
+template <typename Y, typename X, class CP, int E>
+void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
+                       hipStream_t st) {
+    constexpr bool tunable = std::is_same<Y, float>::value && std::is_same<X, float>::value;
+    if constexpr (tunable) {
+        const int key = g_cfg.strips * 100 + g_cfg.unroll * 2 + g_cfg.nt;
+        switch (key) {
+#define FA_GEOM(S_, U_, NT_) \
+    case S_ * 100 + U_ * 2 + NT_: return launch_fedavg_geom<Y, X, CP, E, S_, U_, NT_>(a, tab, cnt, P, first, int_first, st);
+            FA_GEOM(1, 4, 1) FA_GEOM(1, 8, 1) FA_GEOM(1, 16, 1) FA_GEOM(2, 4, 1) FA_GEOM(2, 8, 1) FA_GEOM(2, 16, 1)
+            FA_GEOM(1, 4, 0) FA_GEOM(1, 8, 0) FA_GEOM(1, 16, 0) FA_GEOM(2, 4, 0) FA_GEOM(2, 8, 0) FA_GEOM(2, 16, 0)
+#undef FA_GEOM
+            default: break;
+        }
+    }
+    launch_fedavg_geom<Y, X, CP, E, 1, kUnroll, false>(a, tab, cnt, P, first, int_first, st);
+}
+
 template <typename Y, typename X, class CP>
 int launch_fedavg(void* agg, const void* const* ups, const double* n, const double* N, int K, int64_t P,
                   int init, bool int_first, hipStream_t st) {
     constexpr int E16 = 16 / (int)sizeof(Y) > 0 ? 16 / (int)sizeof(Y) : 1;
     bool vec = aligned16(agg);
     for (int k = 0; k < K && vec; ++k) vec = aligned16(ups[k]);
-    // byte-exact strip stores of X also need 16-B alignment of the agg strip
     using S = typename CP::S;
     ClientTable<S> tab;
     int k0 = 0;
     bool first = init != 0;
+    X* a = static_cast<X*>(agg);
     while (k0 < K) {
         const int cnt = (K - k0) < kMaxK ? (K - k0) : kMaxK;
         fill_table<S>(tab, ups, n, N, k0, cnt);
@@ -524,26 +662,8 @@ int launch_fedavg(void* agg, const void* const* ups, const double* n, const doub
                 tab.N[j] = (S)to_half_value(N[k0 + j]);
             }
         }
-        X* a = static_cast<X*>(agg);
-        if (vec) {
-            const dim3 grid((unsigned)grid_for(P, E16));
-            if (first && int_first) {
-                if constexpr (std::is_integral<Y>::value)
-                    hipLaunchKernelGGL((k_fedavg<Y, X, CP, E16, true, true, true>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
-            } else if (first)
-                hipLaunchKernelGGL((k_fedavg<Y, X, CP, E16, true, false, true>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
-            else
-                hipLaunchKernelGGL((k_fedavg<Y, X, CP, E16, false, false, true>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
-        } else {
-            const dim3 grid((unsigned)grid_for(P, 1));
-            if (first && int_first) {
-                if constexpr (std::is_integral<Y>::value)
-                    hipLaunchKernelGGL((k_fedavg<Y, X, CP, 1, true, true, false>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
-            } else if (first)
-                hipLaunchKernelGGL((k_fedavg<Y, X, CP, 1, true, false, false>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
-            else
-                hipLaunchKernelGGL((k_fedavg<Y, X, CP, 1, false, false, false>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
-        }
+        if (vec) launch_fedavg_vec<Y, X, CP, E16>(a, tab, cnt, P, first, int_first, st);
+        else launch_fedavg_geom<Y, X, CP, 1, 1, kUnroll, false>(a, tab, cnt, P, first, int_first, st);
         int rc = check_launch("fa_fedavg_fold: kernel launch");
         if (rc) return rc;
         first = false;
@@ -621,8 +741,6 @@ int fa_fedavg_fold(void* agg, int agg_dtype, const void* const* updates, int upd
     if (!agg || !updates || !n || !N) return fail(FA_EINVAL, "fa_fedavg_fold: null pointer argument");
     for (int k = 0; k < K; ++k)
         if (!updates[k]) return fail(FA_EINVAL, "fa_fedavg_fold: updates[%d] is NULL", k);
-    for (int k = init ? 1 : 0; k < K; ++k)
-        if (!(N[k] != 0.0)) return fail(FA_EINVAL, "fa_fedavg_fold: N[%d] == 0", k);
     if (init && K == 1) {
         if (agg_dtype != upd_dtype) return fail(FA_EDTYPE, "fa_fedavg_fold: K=1 init is a copy; dtypes must match");
         hipError_t e = hipMemcpyAsync(agg, updates[0], (size_t)P * dt_size(upd_dtype), hipMemcpyDeviceToDevice, st);
@@ -654,8 +772,6 @@ int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, i
     if (K > 0 && (!updates || !n || !N)) return fail(FA_EINVAL, "fa_fedopt_step: null client table");
     for (int k = 0; k < K; ++k)
         if (!updates[k]) return fail(FA_EINVAL, "fa_fedopt_step: updates[%d] is NULL", k);
-    for (int k = first ? 1 : 0; k < K; ++k)
-        if (!(N[k] != 0.0)) return fail(FA_EINVAL, "fa_fedopt_step: N[%d] == 0", k);
     if ((!first || !final_ || K > kMaxK) && !pg) return fail(FA_EINVAL, "fa_fedopt_step: pg workspace required");
     if (final_ && (!m_out || !v_out || !out)) return fail(FA_EINVAL, "fa_fedopt_step: null output buffer");
     if (serveropt < FA_ADAM || serveropt > FA_ADAGRAD) return fail(FA_EINVAL, "fa_fedopt_step: unsupported serveropt %d", serveropt);
@@ -691,6 +807,28 @@ int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, i
     if (upd_dtype == FA_BF16 && old_dtype == FA_F64) return launch_fedopt<bf16, double, CF64>(b, s, updates, n, N, K, P, flags, st);
     if (upd_dtype == FA_F64 && old_dtype == FA_F32) return launch_fedopt<double, float, CF64>(b, s, updates, n, N, K, P, flags, st);
     return fail(FA_EDTYPE, "fa_fedopt_step: unsupported dtype pair (update %d, old %d)", upd_dtype, old_dtype);
+}
+
+int fa_tune(int knob, int value) {
+    g_err[0] = 0;
+    switch (knob) {
+        case FA_TUNE_STRIPS:
+            if (value != 1 && value != 2) return fail(FA_EINVAL, "fa_tune: strips must be 1 or 2");
+            g_cfg.strips = value;
+            return FA_OK;
+        case FA_TUNE_UNROLL:
+            if (value != 4 && value != 8 && value != 16) return fail(FA_EINVAL, "fa_tune: unroll must be 4, 8 or 16");
+            g_cfg.unroll = value;
+            return FA_OK;
+        case FA_TUNE_NT:
+            g_cfg.nt = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_FASTDIV:
+            g_fastdiv = value ? 1 : 0;
+            return FA_OK;
+        default:
+            return fail(FA_EINVAL, "fa_tune: unknown knob %d", knob);
+    }
 }
 
 int fa_stream_copy(void* dst, const void* src, int64_t bytes, void* stream) {

@@ -201,3 +201,14 @@ def stream_read_sink(src):
     lib = _abi.load()
     blocks = lib.fa_stream_read_blocks(src.numel() * src.element_size())
     return torch.empty(max(1, blocks) * 16, dtype=torch.uint8, device=src.device)
+
+
+_KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _abi.FA_TUNE_NT,
+          "fastdiv": _abi.FA_TUNE_FASTDIV}
+
+
+def tune(**knobs):
+    """Set fp32 FedAvg launch knobs (fa_tune): strips, unroll, nt, fastdiv. Results never change."""
+    lib = _abi.load()
+    for k, v in knobs.items():
+        _abi.check(lib.fa_tune(_KNOBS[k], int(v)))

@@ -131,6 +131,16 @@ int fa_promote(int a, int b);
  *                   (sink must hold >= 16 * fa_stream_read_blocks(bytes) bytes)
  */
 int fa_stream_copy(void* dst, const void* src, int64_t bytes, void* stream);
+
+/* Launch-geometry knobs of the fp32 FedAvg kernel (process-global; measurement and
+ * tuning only, results are identical for every setting):
+ *   FA_TUNE_STRIPS  16-B strips per lane (1 | 2)
+ *   FA_TUNE_UNROLL  client strips loaded before folding (4 | 8 | 16)
+ *   FA_TUNE_NT      non-temporal loads of the client buffers (0 | 1)
+ *   FA_TUNE_FASTDIV fp32 t/N via the exact RN64(1/N) product (1, default) or IEEE
+ *                   division (0); both are correctly rounded                        */
+enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_TUNE_FASTDIV = 3 };
+int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);
 

@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprof kernel stats.
+# Every GPU step has its own time limit; a crash / abort / timeout stops the session.
+# Usage: bash tools/gpu_session.sh [tag] [steps...]   (steps: test smoke bench prof)
+set -u
+TAG=${1:-r01}; shift || true
+STEPS=${*:-test smoke bench prof}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+fatal() { case $1 in 0|1) return 1;; *) return 0;; esac; }   # 0 ok, 1 test failures; else stop
+python -c "import fedn_amd.build as b; b.build()" > "$OUT/build.log" 2>&1 || { echo "build failed"; exit 2; }
+for s in $STEPS; do
+  case $s in
+    test)
+      timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+      echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu.log"; if fatal $rc; then exit $rc; fi ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$?
+      echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"; [ $rc -eq 0 ] || exit $rc ;;
+    bench)
+      timeout -k 10 600 python bench.py > "$OUT/bench.log" 2>&1; rc=$?
+      echo "bench rc=$rc"; tail -3 "$OUT/bench.log"; [ $rc -eq 0 ] || exit $rc ;;
+    micro)
+      timeout -k 10 600 python tools/microbench.py > "$OUT/micro.log" 2>&1; rc=$?
+      echo "micro rc=$rc"; cat "$OUT/micro.log" | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc ;;
+    prof)
+      cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- \
+        python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 --cpu-sample 0 > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1; rc=$?
+      cd "$GRAFT_REPO_ROOT"; echo "prof rc=$rc"; tail -2 "$OUT/prof.log"; [ $rc -eq 0 ] || exit $rc ;;
+  esac
+done
