@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--clients", type=int, default=64)
     ap.add_argument("--params", type=int, default=100_000_000, help="params per GPU")
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32")
-    ap.add_argument("--cpu-sample", type=int, default=25_000_000,
+    ap.add_argument("--cpu-sample", type=int, default=100_000_000,
                     help="params per client in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
@@ -66,12 +66,14 @@ def make_updates(K, P, dtype, device, seed):
 
 
 def pmc_traffic(workload):
+    """HBM bytes per launch measured by rocprofv3 PMC (tools/pmc_traffic.py), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(workload)
+            ent = json.load(f).get(workload)
     except (OSError, ValueError):
         return None
+    return None if ent is None else ent["bytes"]
 
 
 def cpu_baseline(ups, ns, agg, S):
@@ -180,7 +182,7 @@ def main():
                        "parallelism": f"param-slice shards x{world}, no data-path collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(workload),
-                         "kernel": "k_fedavg<float,float,CF32,4,INIT>", "kernel_ms": kern_ms,
+                         "kernel": "k_fedavg_pipe (fp32, 4 x 16-B strips per lane, next client prefetched)", "kernel_ms": kern_ms,
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": base,
         }

@@ -22,7 +22,7 @@ FA_OK, FA_EINVAL, FA_EDTYPE, FA_EHIP = 0, 1, 2, 3
 # server optimizers (enum fa_serveropt)
 FA_ADAM, FA_YOGI, FA_ADAGRAD = 0, 1, 2
 FA_PG_FIRST, FA_PG_FINAL = 1, 2
-FA_TUNE_STRIPS, FA_TUNE_UNROLL, FA_TUNE_NT, FA_TUNE_FASTDIV = 0, 1, 2, 3
+FA_TUNE_STRIPS, FA_TUNE_UNROLL, FA_TUNE_NT, FA_TUNE_FASTDIV, FA_TUNE_LANETAB = 0, 1, 2, 3, 4
 
 EXPORTS = {
     # name: (restype, argtypes)

@@ -275,6 +275,27 @@ __device__ __forceinline__ int strip_start(typename CP::V (&x)[E], const X* __re
     }
 }
 
+// The grid's last block: its strips may be ragged or past the end of the buffers.
+template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST>
+__device__ __forceinline__ void k_fedavg_tail(X* __restrict__ agg, const ClientTable<typename CP::S>& tab, const int K,
+                                           const int64_t P, const int64_t strip0) {
+    using V = typename CP::V;
+    for (int s = 0; s < S; ++s) {
+        const int64_t i0 = (strip0 + s * kBlock) * E;
+        if (i0 >= P) break;
+        const int rem = (P - i0) < E ? (int)(P - i0) : E;
+        V x[E];
+        int k = strip_start<Y, X, CP, E, INIT, INT_FIRST, false>(x, agg, tab, i0, rem);
+        for (; k < K; ++k) {
+            const Y* yp = static_cast<const Y*>(tab.ptr[k]) + i0;
+            const typename CP::S n = tab.n[k], N = tab.N[k];
+            const double r = tab.r[k];
+            for (int e = 0; e < rem; ++e) x[e] = CP::fold(x[e], widen<Y, V>(yp[e]), n, N, r);
+        }
+        for (int e = 0; e < rem; ++e) agg[i0 + e] = narrow<X, V>(x[e]);
+    }
+}
+
 // One lane owns S strips of E elements (strip s at lane + s*kBlock within the block's
 // span, so every wave instruction stays a contiguous 1 KiB). U clients' strips are
 // loaded before any of them is folded, so a lane keeps U*S 16-B loads in flight.
@@ -334,21 +355,96 @@ k_fedavg(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K
             strip_store<X, E>(agg + (strip0 + s * kBlock) * E, xo);
         }
     } else {
-        // the grid's last block: strips may be ragged or past the end
-        for (int s = 0; s < S; ++s) {
-            const int64_t i0 = (strip0 + s * kBlock) * E;
-            if (i0 >= P) break;
-            const int rem = (P - i0) < E ? (int)(P - i0) : E;
-            V x[E];
-            int k = strip_start<Y, X, CP, E, INIT, INT_FIRST, false>(x, agg, tab, i0, rem);
-            for (; k < K; ++k) {
-                const Y* yp = static_cast<const Y*>(tab.ptr[k]) + i0;
-                const Sc n = tab.n[k], N = tab.N[k];
-            const double r = tab.r[k];
-                for (int e = 0; e < rem; ++e) x[e] = CP::fold(x[e], widen<Y, V>(yp[e]), n, N, r);
-            }
-            for (int e = 0; e < rem; ++e) agg[i0 + e] = narrow<X, V>(x[e]);
+        k_fedavg_tail<Y, X, CP, E, S, INIT, INT_FIRST>(agg, tab, K, P, strip0);
+    }
+}
+
+// Software-pipelined variant: while client k's S strips are folded, client k+1's are
+// already in flight (two register buffers, explicit ping-pong), so a lane never waits
+// for a whole batch to drain before issuing the next.
+// Client-table access from registers: lane j of every wave holds client j's pointer,
+// n, N and r (K <= 64 = wave size), and a client step reads them with v_readlane
+// (uniform index -> SGPR) instead of a scalar-memory load + lgkmcnt wait.
+template <class CP>
+struct LaneTable {
+    uint64_t p;
+    typename CP::S n, N;
+    double r;
+    __device__ __forceinline__ explicit LaneTable(const ClientTable<typename CP::S>& tab) {
+        const int lane = threadIdx.x & 63;
+        p = reinterpret_cast<uint64_t>(tab.ptr[lane]);
+        n = tab.n[lane];
+        N = tab.N[lane];
+        r = tab.r[lane];
+    }
+    template <typename T>
+    __device__ __forceinline__ static T rl(T v, int k) {
+        static_assert(sizeof(T) == 4 || sizeof(T) == 8, "readlane of 4/8-byte values");
+        if constexpr (sizeof(T) == 4) {
+            int i;
+            __builtin_memcpy(&i, &v, 4);
+            i = __builtin_amdgcn_readlane(i, k);
+            __builtin_memcpy(&v, &i, 4);
+            return v;
+        } else {
+            int i[2];
+            __builtin_memcpy(i, &v, 8);
+            i[0] = __builtin_amdgcn_readlane(i[0], k);
+            i[1] = __builtin_amdgcn_readlane(i[1], k);
+            __builtin_memcpy(&v, i, 8);
+            return v;
         }
+    }
+};
+
+template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT>
+__global__ void __launch_bounds__(kBlock)
+k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P) {
+    using V = typename CP::V;
+    const int64_t strip0 = (int64_t)blockIdx.x * (kBlock * S) + threadIdx.x;
+    if ((strip0 + (int64_t)(S - 1) * kBlock) * E + E > P) {
+        k_fedavg_tail<Y, X, CP, E, S, INIT, INT_FIRST>(agg, tab, K, P, strip0);
+        return;
+    }
+    V x[S][E];
+    int k = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+        k = strip_start<Y, X, CP, E, INIT, INT_FIRST, NT>(x[s], agg, tab, (strip0 + s * kBlock) * E, E);
+    const LaneTable<CP> lt(tab);
+    auto load = [&](int kk, Y (&y)[S][E]) {
+        const Y* yp = LT ? reinterpret_cast<const Y*>(LaneTable<CP>::rl(lt.p, kk)) : static_cast<const Y*>(tab.ptr[kk]);
+#pragma unroll
+        for (int s = 0; s < S; ++s) strip_load<Y, E, NT>(yp + (strip0 + s * kBlock) * E, y[s]);
+    };
+    auto fold = [&](int kk, const Y (&y)[S][E]) {
+        const typename CP::S n = LT ? LaneTable<CP>::rl(lt.n, kk) : tab.n[kk];
+        const typename CP::S N = LT ? LaneTable<CP>::rl(lt.N, kk) : tab.N[kk];
+        const double r = LT ? LaneTable<CP>::rl(lt.r, kk) : tab.r[kk];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            V yv[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) yv[e] = widen<Y, V>(y[s][e]);
+            fold_strip<CP, E>(x[s], yv, n, N, r);
+        }
+    };
+    Y a[S][E], b[S][E];
+    if (k < K) load(k, a);
+    while (k + 1 < K) {
+        load(k + 1, b);
+        fold(k, a);
+        if (k + 2 < K) load(k + 2, a);
+        fold(k + 1, b);
+        k += 2;
+    }
+    if (k < K) fold(k, a);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        X xo[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) xo[e] = narrow<X, V>(x[s][e]);
+        strip_store<X, E>(agg + (strip0 + s * kBlock) * E, xo);
     }
 }
 
@@ -603,11 +699,26 @@ int64_t grid_for(int64_t P, int E) {
 
 // FedAvg launch geometry (fa_tune): strips per lane, clients in flight, non-temporal loads.
 struct FedAvgCfg {
-    int strips = 1;
-    int unroll = 8;
+    int strips = 4;   // measured best on MI355X (profiles/r01_microbench.md): 4 strips per lane,
+    int unroll = 0;   // software-pipelined one client ahead
+    int lanetab = 0;
     int nt = 0;   // measured: cached loads beat non-temporal ones by ~3% (profiles/)
 };
 FedAvgCfg g_cfg;
+
+template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT>
+void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
+                        hipStream_t st) {
+    const int64_t strips = (P + E - 1) / E;
+    const dim3 grid((unsigned)((strips + (int64_t)kBlock * S - 1) / ((int64_t)kBlock * S)));
+    if (first && int_first) {
+        if constexpr (std::is_integral<Y>::value)
+            hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, true, NT, LT>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+    } else if (first)
+        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, false, NT, LT>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+    else
+        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, false, false, NT, LT>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+}
 
 template <typename Y, typename X, class CP, int E, int S, int U, bool NT>
 void launch_fedavg_geom(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
@@ -627,14 +738,22 @@ void launch_fedavg_geom(X* a, const ClientTable<typename CP::S>& tab, int cnt, i
 template <typename Y, typename X, class CP, int E>
 void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
                        hipStream_t st) {
-    constexpr bool tunable = std::is_same<Y, float>::value && std::is_same<X, float>::value;
+    constexpr bool tunable = (std::is_same<Y, float>::value || std::is_same<Y, bf16>::value) && std::is_same<X, float>::value;
     if constexpr (tunable) {
-        const int key = g_cfg.strips * 100 + g_cfg.unroll * 2 + g_cfg.nt;
+        const int key = g_cfg.lanetab * 10000 + g_cfg.strips * 100 + g_cfg.unroll * 2 + g_cfg.nt;
         switch (key) {
 #define FA_GEOM(S_, U_, NT_) \
     case S_ * 100 + U_ * 2 + NT_: return launch_fedavg_geom<Y, X, CP, E, S_, U_, NT_>(a, tab, cnt, P, first, int_first, st);
-            FA_GEOM(1, 4, 1) FA_GEOM(1, 8, 1) FA_GEOM(1, 16, 1) FA_GEOM(2, 4, 1) FA_GEOM(2, 8, 1) FA_GEOM(2, 16, 1)
             FA_GEOM(1, 4, 0) FA_GEOM(1, 8, 0) FA_GEOM(1, 16, 0) FA_GEOM(2, 4, 0) FA_GEOM(2, 8, 0) FA_GEOM(2, 16, 0)
+            FA_GEOM(4, 1, 0) FA_GEOM(4, 2, 0) FA_GEOM(4, 4, 0) FA_GEOM(8, 1, 0) FA_GEOM(8, 2, 0) FA_GEOM(16, 1, 0)
+            FA_GEOM(1, 8, 1) FA_GEOM(4, 2, 1) FA_GEOM(8, 1, 1)
+            case 2 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 2, false, false>(a, tab, cnt, P, first, int_first, st);
+            case 4 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 4, false, false>(a, tab, cnt, P, first, int_first, st);
+            case 8 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 8, false, false>(a, tab, cnt, P, first, int_first, st);
+            case 4 * 100 + 1: return launch_fedavg_pipe<Y, X, CP, E, 4, true, false>(a, tab, cnt, P, first, int_first, st);
+            case 10000 + 2 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 2, false, true>(a, tab, cnt, P, first, int_first, st);
+            case 10000 + 4 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 4, false, true>(a, tab, cnt, P, first, int_first, st);
+            case 10000 + 8 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 8, false, true>(a, tab, cnt, P, first, int_first, st);
 #undef FA_GEOM
             default: break;
         }
@@ -813,15 +932,20 @@ int fa_tune(int knob, int value) {
     g_err[0] = 0;
     switch (knob) {
         case FA_TUNE_STRIPS:
-            if (value != 1 && value != 2) return fail(FA_EINVAL, "fa_tune: strips must be 1 or 2");
+            if (value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
+                return fail(FA_EINVAL, "fa_tune: strips must be 1, 2, 4, 8 or 16");
             g_cfg.strips = value;
             return FA_OK;
         case FA_TUNE_UNROLL:
-            if (value != 4 && value != 8 && value != 16) return fail(FA_EINVAL, "fa_tune: unroll must be 4, 8 or 16");
+            if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
+                return fail(FA_EINVAL, "fa_tune: unroll must be 0 (pipelined), 1, 2, 4, 8 or 16");
             g_cfg.unroll = value;
             return FA_OK;
         case FA_TUNE_NT:
             g_cfg.nt = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_LANETAB:
+            g_cfg.lanetab = value ? 1 : 0;
             return FA_OK;
         case FA_TUNE_FASTDIV:
             g_fastdiv = value ? 1 : 0;

@@ -204,7 +204,7 @@ def stream_read_sink(src):
 
 
 _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _abi.FA_TUNE_NT,
-          "fastdiv": _abi.FA_TUNE_FASTDIV}
+          "fastdiv": _abi.FA_TUNE_FASTDIV, "lanetab": _abi.FA_TUNE_LANETAB}
 
 
 def tune(**knobs):

@@ -134,12 +134,15 @@ int fa_stream_copy(void* dst, const void* src, int64_t bytes, void* stream);
 
 /* Launch-geometry knobs of the fp32 FedAvg kernel (process-global; measurement and
  * tuning only, results are identical for every setting):
- *   FA_TUNE_STRIPS  16-B strips per lane (1 | 2)
- *   FA_TUNE_UNROLL  client strips loaded before folding (4 | 8 | 16)
+ *   FA_TUNE_STRIPS  16-B strips per lane (1 | 2 | 4 | 8 | 16)
+ *   FA_TUNE_UNROLL  clients loaded before folding (1 | 2 | 4 | 8 | 16)
+ *   (instantiated pairs: see launch_fedavg_vec; other pairs fall back to 1 x 8)
  *   FA_TUNE_NT      non-temporal loads of the client buffers (0 | 1)
  *   FA_TUNE_FASTDIV fp32 t/N via the exact RN64(1/N) product (1, default) or IEEE
- *                   division (0); both are correctly rounded                        */
-enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_TUNE_FASTDIV = 3 };
+ *                   division (0); both are correctly rounded
+ *   FA_TUNE_LANETAB pipelined kernel (unroll 0) reads the client table from registers
+ *                   via v_readlane (1) or by scalar loads (0)                      */
+enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_TUNE_FASTDIV = 3, FA_TUNE_LANETAB = 4 };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);

@@ -24,6 +24,12 @@ for s in $STEPS; do
     micro)
       timeout -k 10 600 python tools/microbench.py > "$OUT/micro.log" 2>&1; rc=$?
       echo "micro rc=$rc"; cat "$OUT/micro.log" | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc ;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc_$c" -o run -- \
+          python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 > "$GRAFT_REPO_ROOT/$OUT/pmc_$c.log" 2>&1; rc=$?
+        cd "$GRAFT_REPO_ROOT"; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done ;;
     prof)
       cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- \
         python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 --cpu-sample 0 > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1; rc=$?
