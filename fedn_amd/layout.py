@@ -7,9 +7,36 @@ fp32 tensor back to back, then (if any) the int64 tensors, etc. Each region star
 on a 256-byte boundary so every group base is 16-B aligned for the vector path.
 One H2D copy moves a whole update; one kernel launch per group folds it.
 """
+import os
+from concurrent.futures import ThreadPoolExecutor
+
 import numpy as np
 
 ALIGN = 256
+# host pack: large tensors are copied into the pinned staging buffer by several threads
+# (np.copyto releases the GIL), so the host memcpy keeps up with PCIe Gen5 H2D
+PACK_THREADS = int(os.environ.get("FEDN_AMD_PACK_THREADS", "8"))
+PACK_CHUNK = 16 << 20   # bytes per copy task
+_pool = None
+
+
+def _executor():
+    global _pool
+    if _pool is None:
+        _pool = ThreadPoolExecutor(max_workers=PACK_THREADS, thread_name_prefix="fedn_amd_pack")
+    return _pool
+
+
+def parallel_copy(dst, src):
+    """dst[:] = src for 1-D arrays of one dtype, split over the pack thread pool."""
+    n = src.size
+    step = max(1, PACK_CHUNK // max(1, src.itemsize))
+    if PACK_THREADS <= 1 or n <= 2 * step:
+        np.copyto(dst, src, casting="no")
+        return
+    futs = [_executor().submit(np.copyto, dst[i:i + step], src[i:i + step], casting="no") for i in range(0, n, step)]
+    for f in futs:
+        f.result()
 
 
 def _round_up(x, a):
@@ -76,11 +103,13 @@ class Layout:
             for i, off in self.members[dt]:
                 sz = self.sizes[i]
                 if sz:
-                    np.copyto(g[off:off + sz], np.ascontiguousarray(arrays[i]).reshape(-1), casting="no")
+                    parallel_copy(g[off:off + sz], np.ascontiguousarray(arrays[i]).reshape(-1))
 
-    def unpack_group(self, flat, dt, out):
-        """Scatter a group's flat host array back into per-tensor arrays (new, owned)."""
+    def unpack_group(self, flat, dt, out, copy=True):
+        """Scatter a group's flat host array back into per-tensor arrays. With copy=False
+        the tensors are views of ``flat`` (the caller hands over ownership of it)."""
         for i, off in self.members[dt]:
             sz = self.sizes[i]
-            out[i] = np.array(flat[off:off + sz]).reshape(self.shapes[i])
+            v = flat[off:off + sz]
+            out[i] = (np.array(v) if copy else v).reshape(self.shapes[i])
         return out

@@ -1,0 +1,94 @@
+"""Parameter-slice sharding of the aggregation across the GPUs of one node.
+
+Every output element depends only on the same element of the K client buffers (and of
+old / m / v for FedOpt), so the flat parameter vector splits into contiguous slices with
+no exchange during the reduce: rank r folds slice r of every update with the same kernel
+and the same (n_k, N_k) table, which is bit-identical to the single-GPU result.
+
+Slices are aligned to 4 KiB (1024 fp32) so every shard starts on the kernels' 16-B vector
+boundary and on its own DRAM pages. One process per GPU (torch.distributed, backend
+"nccl" = RCCL on ROCm). The only collective is optional and outside the reduce: an
+all-gather that reassembles the model on every rank (``allgather``), or a gather of the
+slices to the host of one rank (``gather_to_host``), which is what FEDn needs because
+the combiner serialises the model on the host (roundhandler.py:465-468).
+"""
+import torch
+import torch.distributed as dist
+
+ALIGN_ELEMS = 1024
+
+
+def shard_bounds(P, nshards, align=ALIGN_ELEMS):
+    """Contiguous [lo, hi) slices of P elements, each a multiple of ``align`` except the last."""
+    if nshards < 1:
+        raise ValueError("nshards must be >= 1")
+    per = -(-P // nshards)
+    per = -(-per // align) * align
+    out = []
+    for r in range(nshards):
+        lo = min(r * per, P)
+        out.append((lo, min(lo + per, P)))
+    return out
+
+
+class ShardedFedAvg:
+    """One rank's share of a FedAvg over a P-element flat model.
+
+    ``fold_fn(agg, updates, n, N, init)`` defaults to the libfedagg kernel
+    (:func:`fedn_amd.ops.fedavg_fold`); it is a parameter so the sharding and exchange
+    logic can be exercised on CPU-only ranks (gloo) by tests with a reference fold.
+    """
+
+    def __init__(self, P, group=None, fold_fn=None, align=ALIGN_ELEMS):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.P = P
+        self.bounds = shard_bounds(P, self.world, align)
+        self.lo, self.hi = self.bounds[self.rank]
+        self.shard = self.bounds[0][1] - self.bounds[0][0]   # padded per-rank length
+        if fold_fn is None:
+            from .ops import fedavg_fold as fold_fn
+        self.fold_fn = fold_fn
+
+    def local(self, flat):
+        """This rank's slice of a full flat buffer (a view)."""
+        return flat[self.lo:self.hi]
+
+    def fold(self, agg_local, updates_local, n, N, init):
+        return self.fold_fn(agg_local, updates_local, n, N, init)
+
+    def allgather(self, agg_local):
+        """Reassemble the full P-element model on every rank (RCCL all-gather over xGMI)."""
+        if self.world == 1:
+            return agg_local
+        buf = agg_local
+        if agg_local.numel() != self.shard:
+            buf = torch.zeros(self.shard, dtype=agg_local.dtype, device=agg_local.device)
+            buf[:agg_local.numel()].copy_(agg_local)
+        full = torch.empty(self.shard * self.world, dtype=agg_local.dtype, device=agg_local.device)
+        if dist.get_backend(self.group) == "gloo":
+            dist.all_gather(list(full.chunk(self.world)), buf, group=self.group)
+        else:
+            dist.all_gather_into_tensor(full, buf, group=self.group)
+        return full[:self.P]
+
+    def gather_to_host(self, agg_local, dst=0):
+        """Collect every slice into one host tensor on rank ``dst`` (None elsewhere)."""
+        host = agg_local.to("cpu")
+        if self.world == 1:
+            return host
+        buf = torch.zeros(self.shard, dtype=host.dtype)
+        buf[:host.numel()] = host
+        parts = [torch.empty_like(buf) for _ in range(self.world)] if self.rank == dst else None
+        if dist.get_backend(self.group) == "gloo":
+            dist.gather(buf, parts, dst=dst, group=self.group)
+        else:
+            # RCCL gathers device tensors; stage through the device and bring the result back
+            dbuf = buf.to(agg_local.device)
+            dparts = [torch.empty_like(dbuf) for _ in range(self.world)] if self.rank == dst else None
+            dist.gather(dbuf, dparts, dst=dst, group=self.group)
+            parts = [p.cpu() for p in dparts] if self.rank == dst else None
+        if self.rank != dst:
+            return None
+        return torch.cat(parts)[:self.P]

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from . import ops
-from .layout import Layout
+from .layout import Layout, parallel_copy
 
 
 class _Slot:
@@ -91,10 +91,19 @@ class _Pipeline:
         self._kern.append((a, b))
 
     def _to_host(self, t):
+        """D2H through pinned memory (PCIe rate), then one threaded copy into a fresh,
+        caller-owned pageable array (the returned model must not alias reused staging)."""
         tic = time.perf_counter()
-        h = t.to("cpu")                         # synchronizes the compute stream
+        pinned = torch.empty(t.numel(), dtype=t.dtype, pin_memory=True)
+        pinned.copy_(t, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        out = torch.empty(t.numel(), dtype=t.dtype)
+        if t.dtype == torch.bfloat16:
+            out.copy_(pinned)
+        else:
+            parallel_copy(out.numpy(), pinned.numpy())
         self.time_d2h += time.perf_counter() - tic
-        return h
+        return out
 
     def timings(self):
         """GPU-side H2D and kernel time (s, HIP events) plus host pack and D2H wall time."""
@@ -146,7 +155,7 @@ class FedAvgPipeline(_Pipeline):
         out = [None] * len(self.layout.shapes)
         for dt in self.layout.groups:
             h = self._to_host(self.agg[dt])
-            self.layout.unpack_group(h.numpy(), dt, out)
+            self.layout.unpack_group(h.numpy(), dt, out, copy=False)
         return out
 
 
@@ -258,9 +267,7 @@ class FedOptPipeline(_Pipeline):
         model = [None] * len(self.layout.shapes)
         for dt in self.layout.groups:
             h = self._to_host(outs[dt])
-            for i, off in self.layout.members[dt]:
-                sz = self.layout.sizes[i]
-                model[i] = np.array(h.numpy()[off:off + sz]).reshape(self.layout.shapes[i])
+            self.layout.unpack_group(h.numpy(), dt, model, copy=False)
         return model
 
 

@@ -1,0 +1,87 @@
+"""N>1 path on CPU: world_size-2 (and 3) gloo ranks shard a FedAvg by parameter slice,
+fold their slices, and reassemble by all-gather / gather; the result must be bit-identical
+to the single-process oracle (elementwise independence makes sharding exact).
+The per-slice fold here is the oracle (test infrastructure) — the GPU runs libfedagg."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from fedn_amd.sharded import ALIGN_ELEMS, ShardedFedAvg, shard_bounds
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_fold(agg, updates, n, N, init):
+    from oracle import numpy_ref as ref
+    ups = [u.numpy() for u in updates]
+    if init:
+        out = ref.fedavg_flat(ups, n)    # N recomputed from n in order: same totals
+    else:
+        raise NotImplementedError
+    agg.copy_(torch.from_numpy(out))
+    return agg
+
+
+def _worker(rank, world, port, P, K, seed, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(seed)
+        base = rng.standard_normal(P).astype(np.float32)
+        ups = [torch.from_numpy((base + 0.01 * rng.standard_normal(P)).astype(np.float32)) for _ in range(K)]
+        ns = [int(v) for v in rng.integers(1, 5001, K)]
+        Ns = list(np.cumsum(ns))
+        sh = ShardedFedAvg(P, fold_fn=_oracle_fold)
+        agg = torch.empty(sh.hi - sh.lo, dtype=torch.float32)
+        sh.fold(agg, [sh.local(u) for u in ups], ns, Ns, init=True)
+        full = sh.allgather(agg)
+        host = sh.gather_to_host(agg, dst=0)
+        if rank == 0:
+            q.put((full.numpy().copy(), host.numpy().copy(), sh.bounds))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,P", [(2, 10_000), (2, 4096), (3, 5_003)])
+def test_sharded_fedavg_gloo(world, P):
+    from oracle import numpy_ref as ref
+    K, seed = 5, 17
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    pc = mp.start_processes(_worker, args=(world, port, P, K, seed, q), nprocs=world, join=False,
+                            start_method="spawn")
+    full, host, bounds = q.get(timeout=120)   # drain before joining (queue feeder would block exit)
+    while not pc.join(timeout=60):
+        pass
+    rng = np.random.default_rng(seed)
+    base = rng.standard_normal(P).astype(np.float32)
+    ups = [(base + 0.01 * rng.standard_normal(P)).astype(np.float32) for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    want = ref.fedavg_flat(ups, ns)
+    assert np.array_equal(full.view(np.uint32), want.view(np.uint32))
+    assert np.array_equal(host.view(np.uint32), want.view(np.uint32))
+    assert bounds[0][0] == 0 and bounds[-1][1] == P
+
+
+def test_shard_bounds_cover_and_align():
+    for P in (1, 1023, 1024, 100_000_000, 12_345_679):
+        for n in (1, 2, 4, 8):
+            b = shard_bounds(P, n)
+            assert b[0][0] == 0 and b[-1][1] == P
+            for (lo, hi), (lo2, _) in zip(b, b[1:]):
+                assert hi == lo2 and (lo % ALIGN_ELEMS == 0 or lo == P) and (lo2 % ALIGN_ELEMS == 0 or lo2 == P)
+            assert all(lo <= hi for lo, hi in b)

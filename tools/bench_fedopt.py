@@ -1,0 +1,132 @@
+"""FedOpt benchmarks (BASELINE.json configs[3] and configs[4]); results go to DESIGN.md.
+
+config4  350 M fp32 params, 32 device-resident client updates, FedAdam. One fused launch
+         (pseudo-gradient fold + server step). Round 1 (old fp32, m/v None) and steady state
+         (old/m/v fp64, the dtype flow fedopt.py produces), bytes P*(4K+48) per step.
+config5  1 B bf16 params, 128 client updates streamed from pinned host memory in waves of W,
+         FedYogi, H2D of wave i+1 overlapped with the fold of wave i (fa_fedopt_step without
+         FINAL keeps the running pseudo-gradient in HBM), then the server step. The host pool
+         holds `pool` distinct pinned updates reused cyclically (256 GB of distinct bf16
+         updates does not fit the box's host memory); every update still crosses PCIe.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fedn_amd import _abi, ops  # noqa: E402
+
+PEAK = 8000.0
+
+
+def timed(fn, reps=5, warm=2):
+    for _ in range(warm):
+        fn()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for s, e in ev:
+        s.record()
+        fn()
+        e.record()
+    torch.cuda.synchronize()
+    return sorted(s.elapsed_time(e) for s, e in ev)[reps // 2]
+
+
+def config4(P, K, opt):
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(4)
+    old32 = torch.randn(P, generator=g, device=dev)
+    ups = [torch.randn(P, generator=g, device=dev).mul_(0.01).add_(old32) for _ in range(K)]
+    ns = [int(v) for v in np.random.default_rng(4).integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
+    out = torch.empty(P, dtype=torch.float64, device=dev)
+    v = torch.empty(P, dtype=torch.float64, device=dev)
+    m32 = torch.empty(P, dtype=torch.float32, device=dev)
+    # round 1: old fp32, m/v None -> m fp32, v fp64
+    r1 = lambda: ops.fedopt_step(old32, ups, ns, Ns, first=True, final=True, m_out=m32, v_out=v, out=out,  # noqa: E731
+                                 serveropt=opt)
+    ms1 = timed(r1)
+    b1 = K * P * 4 + P * 4 + P * (4 + 8 + 8)
+    old64 = out.clone()
+    m64 = m32.double()
+    r2 = lambda: ops.fedopt_step(old64, ups, ns, Ns, first=True, final=True, m_in=m64, m_out=m64, v_in=v, v_out=v,  # noqa: E731
+                                 out=out, serveropt=opt)
+    ms2 = timed(r2)
+    b2 = P * (4 * K + 48)
+    for name, ms, b in (("round1", ms1, b1), ("steady", ms2, b2)):
+        print(json.dumps({"config": "config4", "opt": opt, "phase": name, "params": P, "clients": K, "ms": ms,
+                          "params_per_s": K * P / ms * 1e3, "GBps": b / ms / 1e6, "frac_hbm": b / ms / 1e6 / PEAK,
+                          "alg_bytes": b}), flush=True)
+
+
+def config5(P, K, W, pool, opt):
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(5)
+    old = torch.randn(P, generator=g, device=dev, dtype=torch.float64)
+    host = []
+    for _ in range(pool):
+        h = torch.empty(P, dtype=torch.bfloat16, pin_memory=True)
+        h.copy_((old + 0.01 * torch.randn(P, generator=g, device=dev, dtype=torch.float64)).to(torch.bfloat16))
+        host.append(h)
+    ns = [int(v) for v in np.random.default_rng(5).integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
+    slots = [[torch.empty(P, dtype=torch.bfloat16, device=dev) for _ in range(W)] for _ in range(2)]
+    pg = torch.empty(P, dtype=torch.float64, device=dev)
+    m = torch.empty(P, dtype=torch.float64, device=dev)
+    v = torch.empty(P, dtype=torch.float64, device=dev)
+    out = torch.empty(P, dtype=torch.float64, device=dev)
+    comp = torch.cuda.current_stream(dev)
+    copy = torch.cuda.Stream(dev)
+    loaded = [torch.cuda.Event() for _ in range(2)]
+    used = [torch.cuda.Event() for _ in range(2)]
+    waves = (K + W - 1) // W
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for w in range(waves):
+        b = w % 2
+        ks = list(range(w * W, min(K, (w + 1) * W)))
+        if w >= 2:
+            copy.wait_event(used[b])
+        with torch.cuda.stream(copy):
+            for j, k in enumerate(ks):
+                slots[b][j].copy_(host[k % pool], non_blocking=True)
+            loaded[b].record(copy)
+        comp.wait_event(loaded[b])
+        ops.fedopt_step(old, slots[b][:len(ks)], [ns[k] for k in ks], [Ns[k] for k in ks], first=(w == 0),
+                        final=False, pg=pg, stream=comp)
+        used[b].record(comp)
+    ops.fedopt_step(old, [], [], [], first=False, final=True, pg=pg, m_out=m, v_out=v, out=out, serveropt=opt,
+                    stream=comp)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    print(json.dumps({"config": "config5", "opt": opt, "params": P, "clients": K, "wave": W, "s": t,
+                      "params_per_s": K * P / t, "h2d_GBps": K * P * 2 / t / 1e9,
+                      "note": f"{pool} distinct pinned bf16 updates reused cyclically"}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--which", default="4,5")
+    ap.add_argument("--p4", type=int, default=350_000_000)
+    ap.add_argument("--k4", type=int, default=32)
+    ap.add_argument("--p5", type=int, default=1_000_000_000)
+    ap.add_argument("--k5", type=int, default=128)
+    ap.add_argument("--wave", type=int, default=8)
+    ap.add_argument("--pool", type=int, default=16)
+    a = ap.parse_args()
+    _abi.load()
+    torch.cuda.set_device(0)
+    if "4" in a.which:
+        for opt in ("adam", "yogi", "adagrad"):
+            config4(a.p4, a.k4, opt)
+            torch.cuda.empty_cache()
+    if "5" in a.which:
+        config5(a.p5, a.k5, a.wave, a.pool, "yogi")
+
+
+if __name__ == "__main__":
+    main()

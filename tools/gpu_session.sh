@@ -24,6 +24,12 @@ for s in $STEPS; do
     micro)
       timeout -k 10 600 python tools/microbench.py > "$OUT/micro.log" 2>&1; rc=$?
       echo "micro rc=$rc"; cat "$OUT/micro.log" | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc ;;
+    e2e)
+      timeout -k 10 600 python tools/bench_e2e.py > "$OUT/e2e.log" 2>&1; rc=$?
+      echo "e2e rc=$rc"; grep -v amdgpu.ids "$OUT/e2e.log" | tail -5; [ $rc -eq 0 ] || exit $rc ;;
+    fedopt)
+      timeout -k 10 900 python tools/bench_fedopt.py > "$OUT/fedopt.log" 2>&1; rc=$?
+      echo "fedopt rc=$rc"; grep -v amdgpu.ids "$OUT/fedopt.log" | tail -8; [ $rc -eq 0 ] || exit $rc ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc_$c" -o run -- \
