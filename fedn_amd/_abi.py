@@ -22,7 +22,7 @@ FA_OK, FA_EINVAL, FA_EDTYPE, FA_EHIP = 0, 1, 2, 3
 # server optimizers (enum fa_serveropt)
 FA_ADAM, FA_YOGI, FA_ADAGRAD = 0, 1, 2
 FA_PG_FIRST, FA_PG_FINAL = 1, 2
-FA_TUNE_STRIPS, FA_TUNE_UNROLL, FA_TUNE_NT, FA_TUNE_FASTDIV, FA_TUNE_LANETAB = 0, 1, 2, 3, 4
+FA_TUNE_STRIPS, FA_TUNE_UNROLL, FA_TUNE_NT, FA_TUNE_FASTDIV, FA_TUNE_LANETAB, FA_TUNE_GRID = 0, 1, 2, 3, 4, 5
 
 EXPORTS = {
     # name: (restype, argtypes)
@@ -44,6 +44,8 @@ EXPORTS = {
         ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,  # opt, lr, b1, b2, tau
         ctypes.c_int64, ctypes.c_void_p]),                   # P, stream
     "fa_tune": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "fa_stream_sum": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int64,
+                                     ctypes.c_void_p]),
     "fa_stream_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "fa_stream_read_blocks": (ctypes.c_int64, [ctypes.c_int64]),
     "fa_stream_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),

@@ -26,8 +26,10 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <type_traits>
+#include <vector>
 
 #include "../../include/fedagg.h"
 
@@ -156,6 +158,12 @@ struct CF16 {            // numpy half loops: op in float, round to half after e
         t = rh(t / N);
         return rh(x + t);
     }
+};
+
+struct CADD {            // measurement only: x <- x + y (same traversal as the fold, minimal VALU)
+    using V = float;
+    using S = float;
+    __device__ static __forceinline__ V fold(V x, V y, S, S, double) { return x + y; }
 };
 
 // element-wise client step for policies without a strip-level shortcut
@@ -401,50 +409,55 @@ template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FI
 __global__ void __launch_bounds__(kBlock)
 k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P) {
     using V = typename CP::V;
-    const int64_t strip0 = (int64_t)blockIdx.x * (kBlock * S) + threadIdx.x;
-    if ((strip0 + (int64_t)(S - 1) * kBlock) * E + E > P) {
-        k_fedavg_tail<Y, X, CP, E, S, INIT, INT_FIRST>(agg, tab, K, P, strip0);
-        return;
-    }
-    V x[S][E];
-    int k = 0;
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-        k = strip_start<Y, X, CP, E, INIT, INT_FIRST, NT>(x[s], agg, tab, (strip0 + s * kBlock) * E, E);
     const LaneTable<CP> lt(tab);
-    auto load = [&](int kk, Y (&y)[S][E]) {
-        const Y* yp = LT ? reinterpret_cast<const Y*>(LaneTable<CP>::rl(lt.p, kk)) : static_cast<const Y*>(tab.ptr[kk]);
+    const int64_t ntiles = ((P + E - 1) / E + (int64_t)kBlock * S - 1) / ((int64_t)kBlock * S);
+    // one tile per block (gridDim == ntiles), or a persistent grid sweeping tiles in grid
+    // order so the tiles read concurrently from one client buffer are adjacent
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t strip0 = tile * (kBlock * S) + threadIdx.x;
+        if ((strip0 + (int64_t)(S - 1) * kBlock) * E + E > P) {
+            k_fedavg_tail<Y, X, CP, E, S, INIT, INT_FIRST>(agg, tab, K, P, strip0);
+            continue;
+        }
+        V x[S][E];
+        int k = 0;
 #pragma unroll
-        for (int s = 0; s < S; ++s) strip_load<Y, E, NT>(yp + (strip0 + s * kBlock) * E, y[s]);
-    };
-    auto fold = [&](int kk, const Y (&y)[S][E]) {
-        const typename CP::S n = LT ? LaneTable<CP>::rl(lt.n, kk) : tab.n[kk];
-        const typename CP::S N = LT ? LaneTable<CP>::rl(lt.N, kk) : tab.N[kk];
-        const double r = LT ? LaneTable<CP>::rl(lt.r, kk) : tab.r[kk];
+        for (int s = 0; s < S; ++s)
+            k = strip_start<Y, X, CP, E, INIT, INT_FIRST, NT>(x[s], agg, tab, (strip0 + s * kBlock) * E, E);
+        auto load = [&](int kk, Y (&y)[S][E]) {
+            const Y* yp = LT ? reinterpret_cast<const Y*>(LaneTable<CP>::rl(lt.p, kk)) : static_cast<const Y*>(tab.ptr[kk]);
+#pragma unroll
+            for (int s = 0; s < S; ++s) strip_load<Y, E, NT>(yp + (strip0 + s * kBlock) * E, y[s]);
+        };
+        auto fold = [&](int kk, const Y (&y)[S][E]) {
+            const typename CP::S n = LT ? LaneTable<CP>::rl(lt.n, kk) : tab.n[kk];
+            const typename CP::S N = LT ? LaneTable<CP>::rl(lt.N, kk) : tab.N[kk];
+            const double r = LT ? LaneTable<CP>::rl(lt.r, kk) : tab.r[kk];
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                V yv[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) yv[e] = widen<Y, V>(y[s][e]);
+                fold_strip<CP, E>(x[s], yv, n, N, r);
+            }
+        };
+        Y a[S][E], b[S][E];
+        if (k < K) load(k, a);
+        while (k + 1 < K) {
+            load(k + 1, b);
+            fold(k, a);
+            if (k + 2 < K) load(k + 2, a);
+            fold(k + 1, b);
+            k += 2;
+        }
+        if (k < K) fold(k, a);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            V yv[E];
+            X xo[E];
 #pragma unroll
-            for (int e = 0; e < E; ++e) yv[e] = widen<Y, V>(y[s][e]);
-            fold_strip<CP, E>(x[s], yv, n, N, r);
+            for (int e = 0; e < E; ++e) xo[e] = narrow<X, V>(x[s][e]);
+            strip_store<X, E>(agg + (strip0 + s * kBlock) * E, xo);
         }
-    };
-    Y a[S][E], b[S][E];
-    if (k < K) load(k, a);
-    while (k + 1 < K) {
-        load(k + 1, b);
-        fold(k, a);
-        if (k + 2 < K) load(k + 2, a);
-        fold(k + 1, b);
-        k += 2;
-    }
-    if (k < K) fold(k, a);
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-        X xo[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) xo[e] = narrow<X, V>(x[s][e]);
-        strip_store<X, E>(agg + (strip0 + s * kBlock) * E, xo);
     }
 }
 
@@ -702,15 +715,26 @@ struct FedAvgCfg {
     int strips = 4;   // measured best on MI355X (profiles/r01_microbench.md): 4 strips per lane,
     int unroll = 0;   // software-pipelined one client ahead
     int lanetab = 0;
+    int grid_per_cu = 0;   // 0: one tile per block; n: persistent grid of n blocks per CU
     int nt = 0;   // measured: cached loads beat non-temporal ones by ~3% (profiles/)
 };
 FedAvgCfg g_cfg;
+
+int device_cus() {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    return cus > 0 ? cus : 256;
+}
 
 template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT>
 void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
                         hipStream_t st) {
     const int64_t strips = (P + E - 1) / E;
-    const dim3 grid((unsigned)((strips + (int64_t)kBlock * S - 1) / ((int64_t)kBlock * S)));
+    int64_t ntiles = (strips + (int64_t)kBlock * S - 1) / ((int64_t)kBlock * S);
+    if (g_cfg.grid_per_cu > 0) ntiles = std::min<int64_t>(ntiles, (int64_t)g_cfg.grid_per_cu * device_cus());
+    const dim3 grid((unsigned)ntiles);
     if (first && int_first) {
         if constexpr (std::is_integral<Y>::value)
             hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, true, NT, LT>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
@@ -944,6 +968,10 @@ int fa_tune(int knob, int value) {
         case FA_TUNE_NT:
             g_cfg.nt = value ? 1 : 0;
             return FA_OK;
+        case FA_TUNE_GRID:
+            if (value < 0 || value > 64) return fail(FA_EINVAL, "fa_tune: grid blocks per CU must be 0..64");
+            g_cfg.grid_per_cu = value;
+            return FA_OK;
         case FA_TUNE_LANETAB:
             g_cfg.lanetab = value ? 1 : 0;
             return FA_OK;
@@ -953,6 +981,19 @@ int fa_tune(int knob, int value) {
         default:
             return fail(FA_EINVAL, "fa_tune: unknown knob %d", knob);
     }
+}
+
+int fa_stream_sum(float* out, const float* const* bufs, int K, int64_t P, void* stream) {
+    g_err[0] = 0;
+    if (K < 1 || K > kMaxK || P < 0 || !out || !bufs) return fail(FA_EINVAL, "fa_stream_sum: bad arguments");
+    bool vec = aligned16(out);
+    for (int k = 0; k < K; ++k) vec = vec && bufs[k] && aligned16(bufs[k]);
+    if (!vec) return fail(FA_EINVAL, "fa_stream_sum: buffers must be 16-B aligned");
+    ClientTable<float> tab;
+    std::vector<double> ones(K, 1.0);
+    fill_table<float>(tab, reinterpret_cast<const void* const*>(bufs), ones.data(), ones.data(), 0, K);
+    launch_fedavg_pipe<float, float, CADD, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
+    return check_launch("fa_stream_sum");
 }
 
 int fa_stream_copy(void* dst, const void* src, int64_t bytes, void* stream) {

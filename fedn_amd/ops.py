@@ -191,6 +191,14 @@ def stream_copy(dst, src, stream=None):
     _abi.check(lib.fa_stream_copy(dst.data_ptr(), src.data_ptr(), src.numel() * src.element_size(), st))
 
 
+def stream_sum(out, bufs, stream=None):
+    """Measurement: out = sum of bufs (fp32) with the FedAvg kernel's traversal."""
+    lib = _abi.load()
+    st = _stream_handle(out, stream)
+    _abi.check(lib.fa_stream_sum(out.data_ptr(), _abi.ptr_array([b.data_ptr() for b in bufs]), len(bufs),
+                                 out.numel(), st))
+
+
 def stream_read(src, sink, stream=None):
     lib = _abi.load()
     st = _stream_handle(src, stream)
@@ -204,7 +212,8 @@ def stream_read_sink(src):
 
 
 _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _abi.FA_TUNE_NT,
-          "fastdiv": _abi.FA_TUNE_FASTDIV, "lanetab": _abi.FA_TUNE_LANETAB}
+          "fastdiv": _abi.FA_TUNE_FASTDIV, "lanetab": _abi.FA_TUNE_LANETAB,
+          "grid": _abi.FA_TUNE_GRID}
 
 
 def tune(**knobs):

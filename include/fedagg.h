@@ -131,6 +131,9 @@ int fa_promote(int a, int b);
  *                   (sink must hold >= 16 * fa_stream_read_blocks(bytes) bytes)
  */
 int fa_stream_copy(void* dst, const void* src, int64_t bytes, void* stream);
+/* out[i] = sum_k bufs[k][i] (fp32, K <= 64) with exactly the traversal of the FedAvg fold
+ * kernel but one add per element: the access-pattern ceiling of fa_fedavg_fold.        */
+int fa_stream_sum(float* out, const float* const* bufs, int K, int64_t P, void* stream);
 
 /* Launch-geometry knobs of the fp32 FedAvg kernel (process-global; measurement and
  * tuning only, results are identical for every setting):
@@ -141,8 +144,11 @@ int fa_stream_copy(void* dst, const void* src, int64_t bytes, void* stream);
  *   FA_TUNE_FASTDIV fp32 t/N via the exact RN64(1/N) product (1, default) or IEEE
  *                   division (0); both are correctly rounded
  *   FA_TUNE_LANETAB pipelined kernel (unroll 0) reads the client table from registers
- *                   via v_readlane (1) or by scalar loads (0)                      */
-enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_TUNE_FASTDIV = 3, FA_TUNE_LANETAB = 4 };
+ *                   via v_readlane (1) or by scalar loads (0)
+ *   FA_TUNE_GRID    pipelined kernel: 0 = one 16-KiB-per-client tile per workgroup,
+ *                   n = persistent grid of n workgroups per CU sweeping tiles        */
+enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_TUNE_FASTDIV = 3, FA_TUNE_LANETAB = 4,
+                    FA_TUNE_GRID = 5 };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);

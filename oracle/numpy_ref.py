@@ -207,3 +207,23 @@ def fedopt_combine(state, updates, old, parameters=None):
         return _server_step(state, pg, old, p), nr
     except Exception:  # noqa: BLE001  (fedopt.py:113-116)
         return None, nr
+
+
+# --------------------------------------------------------------------------------------
+# Control.reduce — fedn/network/controller/control.py:648-693
+# --------------------------------------------------------------------------------------
+def control_reduce(fetched):
+    """``fetched`` = per combiner, the loaded model or None (fetch failed). control.py:662-690:
+    the first model is taken after increment_average(None, ...) raises, later ones fold with
+    n = 1.0, N = i; a fold that raises REPLACES the running model; i counts fetched models."""
+    i, model = 1, None
+    for data in fetched:
+        if data is not None:
+            try:
+                if model is None:
+                    raise TypeError("'NoneType' object is not iterable")
+                model = increment_average(model, data, 1.0, i)
+            except Exception:  # noqa: BLE001
+                model = data
+            i += 1
+    return model

@@ -31,6 +31,11 @@ def load_case(name):
     with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
         z = {k: z[k] for k in z.files}
     case = {"name": name, "kind": str(z["kind"]), "raw": z}
+    if case["kind"] == "reduce":
+        plan = json.loads(str(z["plan"]))
+        case["plan"] = plan
+        case["models"] = [_list(z, f"c{c}") for c in range(len(plan))]
+        case["out"] = None if bool(z["out_none"]) else _list(z, "out")
     if case["kind"] in ("fedavg", "fedopt"):
         case["params"] = json.loads(str(z["params"])) if "params" in z else None
         rounds = []

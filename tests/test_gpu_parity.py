@@ -245,3 +245,23 @@ def test_fedavg_full_size_sampled():
         sl = slice(lo, lo + 1_000_003)
         want = ref.fedavg_flat([u[sl].cpu().numpy() for u in ups], ns)
         assert_lists_identical([agg[sl].cpu().numpy()], [want], f"slice {lo}")
+
+
+# ------------------------------------------------------------------------- Control.reduce
+@pytest.mark.parametrize("name", case_names("reduce"))
+def test_control_reduce_golden(name):
+    from fedn_amd.reduce import reduce_models
+    case = load_case(name)
+    store = {f"m{c}": m for c, (m, kind) in enumerate(zip(case["models"], case["plan"])) if kind != "missing"}
+    deleted = []
+
+    def fetch(mid):
+        if mid not in store:
+            raise KeyError(mid)
+        return store[mid]
+
+    combiners = [{"name": f"c{c}", "model_id": f"m{c}"} for c in range(len(case["plan"]))]
+    model, meta = reduce_models(combiners, fetch=fetch, load=lambda d: d, delete=deleted.append)
+    assert_lists_identical(model, case["out"], name)
+    assert deleted == [c["model_id"] for c in combiners]
+    assert set(meta) == {"time_fetch_model", "time_load_model", "time_aggregate_model"}

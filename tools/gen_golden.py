@@ -207,6 +207,38 @@ def helper_ops(ref, rng):
     return d
 
 
+def reduce_case(ref, name, rng, shapes, plan):
+    """Control.reduce (fedn/network/controller/control.py:648-693). control.py cannot be imported
+    here (it needs `tenacity`, absent from the image, and we do not stub libraries), so its
+    loop is restated line by line below; every arithmetic step is the REAL
+    numpyhelper.Helper.increment_average(model, model_next, 1.0, i) (control.py:682).
+    plan: per combiner "ok" | "missing" (fetch fails -> data None) | "bad" (shape mismatch)."""
+    h = ref["Helper"]()
+    d = {"kind": np.array("reduce"), "name": np.array(name), "plan": np.array(json.dumps(plan))}
+    base = _rng_model(rng, shapes, np.float32)
+    models = []
+    for c, kind in enumerate(plan):
+        if kind == "bad":
+            m = [np.ones((s[0] + 2,) + tuple(s[1:]) if len(s) else (3,), np.float32) for s in shapes]
+        else:
+            m = _perturb(rng, base, np.float32, 0.05)
+        models.append(m)
+        _store_list(d, f"c{c}", m)
+    i, model = 1, None
+    for m, kind in zip(models, plan):                      # control.py:662-690
+        data = None if kind == "missing" else m
+        if data is not None:
+            try:
+                model = h.increment_average(model, data, 1.0, i)
+            except Exception:  # noqa: BLE001  (control.py:683-686: reload and replace)
+                model = data
+            i = i + 1
+    d["out_none"] = np.array(model is None)
+    if model is not None:
+        _store_list(d, "out", model)
+    return d
+
+
 def main():
     ref = _import_reference()
     os.makedirs(OUT, exist_ok=True)
@@ -244,6 +276,13 @@ def main():
     cases.append(fedopt_case(ref, "fedopt_badparam_int_lr", rng, ODD_SHAPES, [[10, 20]], {"learning_rate": 1}))
     cases.append(fedopt_case(ref, "fedopt_badparam_key", rng, ODD_SHAPES, [[10, 20]], {"momentum": 0.5}))
     cases.append(fedopt_case(ref, "fedopt_badopt", rng, ODD_SHAPES, [[10, 20]], {"serveropt": "sgd"}))
+
+    # Control.reduce -------------------------------------------------------------------
+    rng = np.random.default_rng(4)
+    cases.append(reduce_case(ref, "reduce_3", rng, ODD_SHAPES, ["ok", "ok", "ok"]))
+    cases.append(reduce_case(ref, "reduce_missing", rng, ODD_SHAPES, ["missing", "ok", "missing", "ok", "ok"]))
+    cases.append(reduce_case(ref, "reduce_bad_replaces", rng, ODD_SHAPES, ["ok", "ok", "bad", "ok"]))
+    cases.append(reduce_case(ref, "reduce_single", rng, ODD_SHAPES, ["ok"]))
 
     manifest = []
     for c in cases:

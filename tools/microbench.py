@@ -63,28 +63,33 @@ def main():
     agg = torch.empty(P, device=dev)
     ref_out = None
     alg = K * P * 4 + P * 4
-    combos = [(S, U, 0, 1, 0) for S, U in ((1, 8), (2, 4), (4, 1), (4, 2), (8, 1))]
-    combos += [(S, 0, 0, 1, L) for S in (2, 4, 8) for L in (0, 1)]
-    for S, U, NT, F, L in combos:
-                ops.tune(strips=S, unroll=U, nt=NT, fastdiv=F, lanetab=L)
+    med, best = timed(lambda: ops.stream_sum(agg, ups))
+    print(json.dumps({"kernel": "stream_sum (fold traversal, 1 add)", "ms": med, "GBps": alg / med / 1e6,
+                      "best_GBps": alg / best / 1e6}), flush=True)
+    combos = [(S, U, 0, 1, 0, 0) for S, U in ((1, 8), (4, 1))]
+    combos += [(S, 0, 0, 1, 0, G) for S in (2, 4) for G in (0, 2, 4, 6, 8)]
+    for S, U, NT, F, L, G in combos:
+                ops.tune(strips=S, unroll=U, nt=NT, fastdiv=F, lanetab=L, grid=G)
                 med, best = timed(lambda: ops.fedavg_fold(agg, ups, ns, Ns, init=True))
                 torch.cuda.synchronize()
                 if ref_out is None:
                     ref_out = agg.clone()
                 same = bool(torch.equal(agg.view(torch.int32), ref_out.view(torch.int32)))
-                print(json.dumps({"kernel": "fedavg", "strips": S, "unroll": U, "nt": NT, "fastdiv": F, "lanetab": L, "K": K, "P": P, "ms": med,
+                print(json.dumps({"kernel": "fedavg", "strips": S, "unroll": U, "nt": NT, "fastdiv": F, "lanetab": L, "grid": G, "K": K, "P": P, "ms": med,
                                   "GBps": alg / med / 1e6, "best_GBps": alg / best / 1e6, "identical": same}), flush=True)
     # one contiguous [K, P] slab instead of K separate allocations
     slab = torch.stack(ups)
     rows = list(slab.unbind(0))
-    for S, U, L in ((4, 1, 0), (4, 0, 1), (1, 8, 0)):
+    med, _ = timed(lambda: ops.stream_sum(agg, rows))
+    print(json.dumps({"kernel": "stream_sum_slab", "ms": med, "GBps": alg / med / 1e6}), flush=True)
+    for S, U, L in ((4, 0, 0),):
         ops.tune(strips=S, unroll=U, lanetab=L)
         med, best = timed(lambda: ops.fedavg_fold(agg, rows, ns, Ns, init=True))
         print(json.dumps({"kernel": "fedavg_slab", "strips": S, "unroll": U, "lanetab": L, "ms": med,
                           "GBps": alg / med / 1e6}), flush=True)
     del slab, rows
     # reset defaults
-    ops.tune(strips=1, unroll=8, nt=0, fastdiv=1)
+    ops.tune(strips=4, unroll=0, nt=0, fastdiv=1, lanetab=0, grid=0)
     # K = 8 (BASELINE config 2) and bf16 inputs
     med, _ = timed(lambda: ops.fedavg_fold(agg, ups[:8], ns[:8], Ns[:8], init=True))
     b8 = 8 * P * 4 + P * 4
