@@ -23,7 +23,36 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
+NPZ_SRC = os.path.join(HERE, "csrc", "npz_codec.cpp")
+NPZ_HDR = os.path.join(ROOT, "include", "fednpz.h")
+NPZ_OUT = os.path.join(HERE, "libfednpz.so")
+
+
+def _stale(out, *deps):
+    return not os.path.exists(out) or any(os.path.getmtime(out) < os.path.getmtime(d) for d in deps)
+
+
+def build_codec(force=False, verbose=True):
+    """Host-side npz codec (C++17 + zlib, no GPU code)."""
+    if not force and not _stale(NPZ_OUT, NPZ_SRC, NPZ_HDR):
+        return NPZ_OUT
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
+    tmp = NPZ_OUT + ".tmp"
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", "-I", os.path.join(ROOT, "include"),
+           "-o", tmp, NPZ_SRC, "-lz"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, NPZ_OUT)
+    return NPZ_OUT
+
+
 def build(force=False, verbose=True):
+    build_codec(force, verbose)
+    return build_hip(force, verbose)
+
+
+def build_hip(force=False, verbose=True):
     if not force and os.path.exists(OUT):
         t = os.path.getmtime(OUT)
         if t >= os.path.getmtime(SRC) and t >= os.path.getmtime(HDR):
@@ -38,4 +67,4 @@ def build(force=False, verbose=True):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
+    print(build(force="--force" in sys.argv), NPZ_OUT)

@@ -1,0 +1,182 @@
+"""Native .npz codec (``libfednpz.so``, include/fednpz.h) — FEDn's model wire format.
+
+FEDn serialises every model with ``np.savez_compressed`` and reads it back through a temp
+file and ``np.load`` (numpyhelper.py:144-189, modelservice.py:57-75, 110-146). This module
+decodes an archive held in memory straight into caller buffers — optionally one pinned
+host buffer in the grouped flat layout the GPU pipelines stage from (layout.py) — and
+encodes with a block-parallel deflate. Decoded arrays are byte-identical to ``np.load``;
+written archives are valid npz files (``np.load``/``zipfile`` read them, CRCs checked).
+"""
+import ctypes
+import io
+import os
+import threading
+
+import numpy as np
+
+from .layout import Layout
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfednpz.so")
+MAX_DIMS = 16
+THREADS = int(os.environ.get("FEDN_AMD_CODEC_THREADS", str(min(16, os.cpu_count() or 1))))
+
+
+class Entry(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 256), ("descr", ctypes.c_char * 32), ("fortran_order", ctypes.c_int32),
+                ("ndim", ctypes.c_int32), ("shape", ctypes.c_int64 * MAX_DIMS), ("nbytes", ctypes.c_int64),
+                ("npy_header", ctypes.c_int64), ("data_offset", ctypes.c_int64), ("comp_size", ctypes.c_int64),
+                ("uncomp_size", ctypes.c_int64), ("crc32", ctypes.c_uint32), ("method", ctypes.c_int32),
+                ("index_offset", ctypes.c_int64), ("index_count", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class CodecError(ValueError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load_lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(f"{LIB_PATH} not found: run python -m fedn_amd.build")
+            lib = ctypes.CDLL(LIB_PATH)
+            lib.fnpz_abi_version.restype = ctypes.c_int
+            lib.fnpz_last_error.restype = ctypes.c_char_p
+            lib.fnpz_open.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(Entry), ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_int)]
+            lib.fnpz_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(Entry), ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]
+            lib.fnpz_write_bound.restype = ctypes.c_int64
+            lib.fnpz_write_bound.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+                                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]
+            lib.fnpz_write.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_void_p),
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_void_p),
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                       ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+            if lib.fnpz_abi_version() != 1:
+                raise ImportError("libfednpz.so ABI mismatch; rebuild")
+            _lib = lib
+    return _lib
+
+
+def _check(rc):
+    if rc:
+        raise CodecError(f"fednpz status {rc}: {load_lib().fnpz_last_error().decode(errors='replace')}")
+
+
+def _as_u8(buf):
+    """A contiguous uint8 numpy view of bytes / bytearray / memoryview / ndarray (no copy)."""
+    if isinstance(buf, np.ndarray):
+        a = buf.reshape(-1).view(np.uint8)
+    else:
+        a = np.frombuffer(buf, dtype=np.uint8)
+    return np.ascontiguousarray(a)
+
+
+def open_archive(buf):
+    """Parse an npz archive; returns (uint8 view, list of Entry) in archive order."""
+    lib = load_lib()
+    a = _as_u8(buf)
+    n = ctypes.c_int(0)
+    cap = 64
+    while True:
+        ents = (Entry * cap)()
+        rc = lib.fnpz_open(a.ctypes.data, a.size, ents, cap, ctypes.byref(n))
+        if rc == 4 and n.value > cap:     # FNPZ_ENOSPC: retry with room for every member
+            cap = n.value
+            continue
+        _check(rc)
+        return a, list(ents[:n.value])
+
+
+def _dtype(e):
+    dt = np.dtype(e.descr.decode())
+    if dt.hasobject:
+        raise CodecError("object arrays are not supported")
+    return dt
+
+
+def _shape(e):
+    return tuple(e.shape[i] for i in range(e.ndim))
+
+
+def read_entries(a, ents, dsts, threads=None):
+    lib = load_lib()
+    arr = (Entry * max(1, len(ents)))(*ents)
+    ptrs = (ctypes.c_void_p * max(1, len(ents)))(*[d.ctypes.data if d.size else 0 for d in dsts])
+    _check(lib.fnpz_read(a.ctypes.data, a.size, arr, len(ents), ptrs, threads or THREADS))
+
+
+def _ordered(ents):
+    """numpyhelper.load order: keys "0", "1", ... (numpyhelper.py:180-182); KeyError otherwise."""
+    by_name = {e.name.decode(): e for e in ents}
+    return [by_name[str(i)] for i in range(len(ents))]
+
+
+def load_npz(buf, threads=None):
+    """Decode an npz archive to the list numpyhelper.Helper.load returns (new arrays)."""
+    a, ents = open_archive(buf)
+    ents = _ordered(ents)
+    outs = []
+    for e in ents:
+        dt = _dtype(e)
+        outs.append(np.empty(_shape(e), dtype=dt, order="F" if e.fortran_order else "C"))
+    read_entries(a, ents, [o.reshape(-1, order="A").view(np.uint8) if o.size else o.view(np.uint8).reshape(-1)
+                           for o in outs], threads)
+    return outs
+
+
+def load_npz_into_layout(buf, alloc, threads=None):
+    """Decode straight into ONE buffer in the grouped flat layout of layout.py.
+
+    ``alloc(nbytes)`` returns a uint8 host tensor/array to decode into (e.g. pinned
+    memory); returns (layout, buffer). Fortran-ordered members are not supported here."""
+    a, ents = open_archive(buf)
+    ents = _ordered(ents)
+    if any(e.fortran_order for e in ents):
+        raise CodecError("fortran-ordered members cannot be decoded into the flat layout")
+    layout = Layout([_shape(e) for e in ents], [_dtype(e) for e in ents])
+    out = alloc(layout.nbytes)
+    base = out.numpy() if hasattr(out, "numpy") else out
+    dsts = []
+    for i, e in enumerate(ents):
+        dt = layout.dtypes[i]
+        off = dict(layout.members[dt])[i] * dt.itemsize + layout.group_byte_offset[dt]
+        dsts.append(base[off:off + e.nbytes])
+    read_entries(a, ents, dsts, threads)
+    return layout, out
+
+
+def save_npz(arrays, level=6, threads=None, block=0):
+    """Encode ``arrays`` like numpyhelper.Helper.save (keys "0", "1", ...); returns bytes."""
+    lib = load_lib()
+    arrays = [np.asarray(x) for x in arrays]
+    n = len(arrays)
+    names, hdrs, datas = [], [], []
+    for i, x in enumerate(arrays):
+        if x.dtype.hasobject:
+            raise CodecError("object arrays are not supported")
+        bio = io.BytesIO()
+        np.lib.format.write_array_header_1_0(bio, np.lib.format.header_data_from_array_1_0(x))
+        hdrs.append(np.frombuffer(bio.getvalue(), dtype=np.uint8))
+        data = x if x.flags.c_contiguous or x.flags.f_contiguous else np.ascontiguousarray(x)
+        datas.append(data)
+        names.append(str(i).encode())
+    hl = (ctypes.c_int64 * max(1, n))(*[h.size for h in hdrs])
+    nb = (ctypes.c_int64 * max(1, n))(*[d.nbytes for d in datas])
+    nl = (ctypes.c_int32 * max(1, n))(*[len(s) for s in names])
+    cap = lib.fnpz_write_bound(n, hl, nb, nl)
+    out = np.empty(cap, dtype=np.uint8)
+    out_len = ctypes.c_int64(0)
+    _check(lib.fnpz_write(n, (ctypes.c_char_p * max(1, n))(*names),
+                          (ctypes.c_void_p * max(1, n))(*[h.ctypes.data for h in hdrs]), hl,
+                          (ctypes.c_void_p * max(1, n))(*[d.ctypes.data if d.size else 0 for d in datas]), nb,
+                          level, threads or THREADS, block, out.ctypes.data, cap, ctypes.byref(out_len)))
+    return out[:out_len.value].tobytes()

@@ -1,0 +1,648 @@
+// npz_codec.cpp — native .npz codec for FEDn's model wire format (see include/fednpz.h).
+//
+// Reader: ZIP / ZIP64 central directory -> per member local header -> raw-inflate the
+// .npy preamble + header dict (parsed for descr / fortran_order / shape), then inflate the
+// payload straight into the caller's buffer (no temp file, no intermediate bytes object,
+// no copy), CRC-32 checked; members decode in parallel.
+// Writer: every member's uncompressed stream (npy header + payload) is cut into blocks
+// that deflate independently and in parallel (no shared window; non-final blocks end in
+// Z_SYNC_FLUSH, the last in Z_FINISH), so their concatenation is one valid deflate stream;
+// block CRC-32s are combined, and a block index in a private extra field lets fnpz_read
+// inflate the blocks in parallel too. Container layout follows numpy's savez_compressed
+// (ZIP64 extras on every member, names "<key>.npy").
+
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/fednpz.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+uint32_t rd32(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }
+uint64_t rd64(const uint8_t* p) { return (uint64_t)rd32(p) | ((uint64_t)rd32(p + 4) << 32); }
+void wr16(uint8_t* p, uint16_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); }
+void wr32(uint8_t* p, uint32_t v) { for (int i = 0; i < 4; ++i) p[i] = (uint8_t)(v >> (8 * i)); }
+void wr64(uint8_t* p, uint64_t v) { for (int i = 0; i < 8; ++i) p[i] = (uint8_t)(v >> (8 * i)); }
+
+constexpr uint32_t kLocalSig = 0x04034b50, kCentralSig = 0x02014b50, kEocdSig = 0x06054b50;
+constexpr uint32_t kZ64EocdSig = 0x06064b50, kZ64LocSig = 0x07064b50;
+constexpr uInt kChunk = 1u << 30;   // zlib's avail_* are 32-bit
+
+// ---------------------------------------------------------------------------------------
+// inflate helper: a raw-deflate stream consumed in pieces into successive outputs
+// ---------------------------------------------------------------------------------------
+struct Inflater {
+    z_stream zs{};
+    const uint8_t* src;
+    int64_t left;
+    bool ok = false;
+    Inflater(const uint8_t* s, int64_t n) : src(s), left(n) { ok = inflateInit2(&zs, -MAX_WBITS) == Z_OK; }
+    ~Inflater() {
+        if (ok) inflateEnd(&zs);
+    }
+    // fill exactly `n` bytes of out; returns false on a corrupt / short stream
+    bool fill(uint8_t* out, int64_t n) {
+        while (n > 0) {
+            if (zs.avail_in == 0 && left > 0) {
+                zs.next_in = const_cast<Bytef*>(src);
+                zs.avail_in = (uInt)std::min<int64_t>(left, kChunk);
+                src += zs.avail_in;
+                left -= zs.avail_in;
+            }
+            zs.next_out = out;
+            zs.avail_out = (uInt)std::min<int64_t>(n, kChunk);
+            const uInt before = zs.avail_out;
+            const int rc = inflate(&zs, Z_NO_FLUSH);
+            const uInt got = before - zs.avail_out;
+            out += got;
+            n -= got;
+            if (rc == Z_STREAM_END) return n == 0;
+            if (rc != Z_OK && !(rc == Z_BUF_ERROR && got > 0)) return false;
+            if (got == 0 && zs.avail_in == 0 && left == 0) return false;
+        }
+        return true;
+    }
+};
+
+// source of a member's uncompressed bytes: stored or deflated
+struct MemberReader {
+    const uint8_t* data;
+    int64_t comp;
+    int method;
+    int64_t pos = 0;
+    Inflater* inf = nullptr;
+    MemberReader(const uint8_t* d, int64_t c, int m) : data(d), comp(c), method(m) {
+        if (method == 8) inf = new Inflater(d, c);
+    }
+    ~MemberReader() { delete inf; }
+    bool ready() const { return method == 0 || (inf && inf->ok); }
+    bool read(uint8_t* out, int64_t n) {
+        if (method == 0) {
+            if (pos + n > comp) return false;
+            std::memcpy(out, data + pos, (size_t)n);
+            pos += n;
+            return true;
+        }
+        return inf->fill(out, n);
+    }
+};
+
+// ---------------------------------------------------------------------------------------
+// .npy header dict parser: {'descr': '<f4', 'fortran_order': False, 'shape': (3, 4), }
+// ---------------------------------------------------------------------------------------
+bool parse_npy_dict(const std::string& h, fnpz_entry* e) {
+    auto key = [&](const char* k) -> size_t {
+        size_t p = h.find(std::string("'") + k + "'");
+        if (p == std::string::npos) return p;
+        p = h.find(':', p);
+        return p == std::string::npos ? p : p + 1;
+    };
+    size_t p = key("descr");
+    if (p == std::string::npos) return false;
+    while (p < h.size() && h[p] == ' ') ++p;
+    if (p >= h.size() || (h[p] != '\'' && h[p] != '"')) return false;   // structured dtypes (lists) unsupported
+    const char q = h[p];
+    const size_t end = h.find(q, p + 1);
+    if (end == std::string::npos || end - p - 1 >= sizeof(e->descr)) return false;
+    std::memcpy(e->descr, h.data() + p + 1, end - p - 1);
+    e->descr[end - p - 1] = 0;
+    p = key("fortran_order");
+    if (p == std::string::npos) return false;
+    while (p < h.size() && h[p] == ' ') ++p;
+    e->fortran_order = h.compare(p, 4, "True") == 0 ? 1 : 0;
+    p = key("shape");
+    if (p == std::string::npos) return false;
+    p = h.find('(', p);
+    const size_t close = h.find(')', p);
+    if (p == std::string::npos || close == std::string::npos) return false;
+    e->ndim = 0;
+    size_t i = p + 1;
+    while (i < close) {
+        while (i < close && (h[i] == ' ' || h[i] == ',')) ++i;
+        if (i >= close) break;
+        if (h[i] < '0' || h[i] > '9') return false;
+        int64_t v = 0;
+        while (i < close && h[i] >= '0' && h[i] <= '9') v = v * 10 + (h[i++] - '0');
+        if (e->ndim >= FNPZ_MAX_DIMS) return false;
+        e->shape[e->ndim++] = v;
+    }
+    return true;
+}
+
+int64_t descr_itemsize(const char* d) {
+    // '<f4', '|u1', '<c16', '|S5', '<U6' ...: the digits after the kind letter are bytes,
+    // except for 'U' (UCS-4 characters: 4 bytes each)
+    const char* p = d;
+    char kind = 0;
+    while (*p && (*p < '0' || *p > '9')) kind = *p++;
+    const int64_t n = *p ? std::atoll(p) : 0;
+    return kind == 'U' ? 4 * n : n;
+}
+
+// ---------------------------------------------------------------------------------------
+// central directory
+// ---------------------------------------------------------------------------------------
+struct CdEntry {
+    std::string name;
+    int method;
+    uint32_t crc;
+    uint64_t comp, uncomp, local_off;
+};
+
+// Block index extra field written by fnpz_write (ID 0x5046, "FP"): u32 count, u32 pad,
+// u64 raw block size, then count + 1 u64 offsets of each independently deflated block
+// inside the member's compressed data. Readers that do not know the ID skip it (APPNOTE
+// 4.5.2); fnpz_read uses it to inflate the blocks of one member in parallel.
+constexpr uint16_t kIndexId = 0x5046;
+constexpr int kMaxIndexBlocks = 8000;   // keeps the local extra field < 64 KiB
+
+int read_central(const uint8_t* a, int64_t len, std::vector<CdEntry>& out) {
+    if (len < 22) return fail(FNPZ_EFORMAT, "not a zip archive (too short)");
+    int64_t eocd = -1;
+    for (int64_t p = len - 22; p >= std::max<int64_t>(0, len - 22 - 65535); --p)
+        if (rd32(a + p) == kEocdSig) {
+            eocd = p;
+            break;
+        }
+    if (eocd < 0) return fail(FNPZ_EFORMAT, "no end-of-central-directory record");
+    uint64_t n = rd16(a + eocd + 10), cd_size = rd32(a + eocd + 12), cd_off = rd32(a + eocd + 16);
+    if (eocd >= 20 && rd32(a + eocd - 20) == kZ64LocSig) {
+        const uint64_t z64 = rd64(a + eocd - 20 + 8);
+        if (z64 + 56 > (uint64_t)len || rd32(a + z64) != kZ64EocdSig) return fail(FNPZ_EFORMAT, "bad ZIP64 EOCD");
+        n = rd64(a + z64 + 32);
+        cd_size = rd64(a + z64 + 40);
+        cd_off = rd64(a + z64 + 48);
+    }
+    if (cd_off + cd_size > (uint64_t)len) return fail(FNPZ_EFORMAT, "central directory out of range");
+    const uint8_t* p = a + cd_off;
+    const uint8_t* end = p + cd_size;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (p + 46 > end || rd32(p) != kCentralSig) return fail(FNPZ_EFORMAT, "bad central directory entry %llu", (unsigned long long)i);
+        CdEntry e;
+        const uint16_t flags = rd16(p + 8);
+        if (flags & 1) return fail(FNPZ_EFORMAT, "encrypted members are not supported");
+        e.method = rd16(p + 10);
+        e.crc = rd32(p + 16);
+        e.comp = rd32(p + 20);
+        e.uncomp = rd32(p + 24);
+        const uint16_t nl = rd16(p + 28), xl = rd16(p + 30), cl = rd16(p + 32);
+        e.local_off = rd32(p + 42);
+        if (p + 46 + nl + xl + cl > end) return fail(FNPZ_EFORMAT, "truncated central directory");
+        e.name.assign(reinterpret_cast<const char*>(p + 46), nl);
+        const uint8_t* x = p + 46 + nl;
+        const uint8_t* xe = x + xl;
+        while (x + 4 <= xe) {
+            const uint16_t id = rd16(x), sz = rd16(x + 2);
+            if (id == 1) {
+                const uint8_t* f = x + 4;
+                if (e.uncomp == 0xFFFFFFFFu && f + 8 <= x + 4 + sz) { e.uncomp = rd64(f); f += 8; }
+                if (e.comp == 0xFFFFFFFFu && f + 8 <= x + 4 + sz) { e.comp = rd64(f); f += 8; }
+                if (e.local_off == 0xFFFFFFFFu && f + 8 <= x + 4 + sz) { e.local_off = rd64(f); f += 8; }
+            }
+            x += 4 + sz;
+        }
+        out.push_back(e);
+        p += 46 + nl + xl + cl;
+    }
+    return FNPZ_OK;
+}
+
+int resolve_entry(const uint8_t* a, int64_t len, const CdEntry& c, fnpz_entry* e) {
+    std::memset(e, 0, sizeof(*e));
+    if (c.method != 0 && c.method != 8) return fail(FNPZ_EFORMAT, "%s: compression method %d unsupported", c.name.c_str(), c.method);
+    if (c.local_off + 30 > (uint64_t)len || rd32(a + c.local_off) != kLocalSig) return fail(FNPZ_EFORMAT, "%s: bad local header", c.name.c_str());
+    const uint16_t lnl = rd16(a + c.local_off + 26), lxl = rd16(a + c.local_off + 28);
+    const uint64_t data = c.local_off + 30 + lnl + lxl;
+    if (data + c.comp > (uint64_t)len) return fail(FNPZ_EFORMAT, "%s: member data out of range", c.name.c_str());
+    std::string nm = c.name;
+    if (nm.size() >= 4 && nm.compare(nm.size() - 4, 4, ".npy") == 0) nm.resize(nm.size() - 4);
+    if (nm.size() >= sizeof(e->name)) return fail(FNPZ_EFORMAT, "member name too long");
+    std::memcpy(e->name, nm.data(), nm.size());
+    e->method = c.method;
+    e->crc32 = c.crc;
+    e->comp_size = (int64_t)c.comp;
+    e->uncomp_size = (int64_t)c.uncomp;
+    e->data_offset = (int64_t)data;
+    e->index_offset = 0;
+    e->index_count = 0;
+    if (data <= (uint64_t)len) {
+        const uint8_t* x = a + c.local_off + 30 + lnl;
+        const uint8_t* xe = x + lxl;
+        while (x + 4 <= xe) {
+            const uint16_t id = rd16(x), sz = rd16(x + 2);
+            if (id == kIndexId && sz >= 16 && x + 4 + sz <= xe) {
+                const uint32_t cnt = rd32(x + 4);
+                if (cnt > 0 && (uint64_t)sz == 16 + 8ull * (cnt + 1) && rd64(x + 4 + 16 + 8ull * cnt) == c.comp) {
+                    e->index_offset = (int64_t)(x + 4 - a);
+                    e->index_count = (int32_t)cnt;
+                }
+            }
+            x += 4 + sz;
+        }
+    }
+    // .npy preamble: magic(6) major minor len (2 or 4) then the header dict
+    MemberReader r(a + data, e->comp_size, c.method);
+    if (!r.ready()) return fail(FNPZ_ECORRUPT, "%s: inflate init failed", c.name.c_str());
+    uint8_t pre[12];
+    if (!r.read(pre, 10) || std::memcmp(pre, "\x93NUMPY", 6) != 0) return fail(FNPZ_EFORMAT, "%s: not a .npy member", c.name.c_str());
+    int64_t hlen, hoff;
+    if (pre[6] == 1) {
+        hlen = rd16(pre + 8);
+        hoff = 10;
+    } else if (pre[6] == 2 || pre[6] == 3) {
+        if (!r.read(pre + 10, 2)) return fail(FNPZ_ECORRUPT, "%s: short header", c.name.c_str());
+        hlen = rd32(pre + 8);
+        hoff = 12;
+    } else {
+        return fail(FNPZ_EFORMAT, "%s: .npy version %d unsupported", c.name.c_str(), pre[6]);
+    }
+    std::string h((size_t)hlen, '\0');
+    if (!r.read(reinterpret_cast<uint8_t*>(&h[0]), hlen)) return fail(FNPZ_ECORRUPT, "%s: short header", c.name.c_str());
+    if (!parse_npy_dict(h, e)) return fail(FNPZ_EFORMAT, "%s: unsupported .npy header %s", c.name.c_str(), h.c_str());
+    e->npy_header = hoff + hlen;
+    int64_t count = 1;
+    for (int d = 0; d < e->ndim; ++d) count *= e->shape[d];
+    e->nbytes = count * descr_itemsize(e->descr);
+    if (e->npy_header + e->nbytes != e->uncomp_size)
+        return fail(FNPZ_EFORMAT, "%s: size mismatch (header says %lld payload bytes, member holds %lld)", c.name.c_str(),
+                    (long long)e->nbytes, (long long)(e->uncomp_size - e->npy_header));
+    return FNPZ_OK;
+}
+
+int decode_one(const uint8_t* a, const fnpz_entry& e, void* dst, char* err, size_t errlen) {
+    MemberReader r(a + e.data_offset, e.comp_size, e.method);
+    if (!r.ready()) return snprintf(err, errlen, "%s: inflate init failed", e.name), FNPZ_ECORRUPT;
+    std::vector<uint8_t> hdr((size_t)e.npy_header);
+    if (!r.read(hdr.data(), e.npy_header)) return snprintf(err, errlen, "%s: corrupt header", e.name), FNPZ_ECORRUPT;
+    uLong crc = crc32(0L, hdr.data(), (uInt)hdr.size());
+    uint8_t* out = static_cast<uint8_t*>(dst);
+    int64_t left = e.nbytes;
+    while (left > 0) {
+        const int64_t n = std::min<int64_t>(left, kChunk);
+        if (!r.read(out, n)) return snprintf(err, errlen, "%s: corrupt or truncated payload", e.name), FNPZ_ECORRUPT;
+        crc = crc32(crc, out, (uInt)n);
+        out += n;
+        left -= n;
+    }
+    if ((uint32_t)crc != e.crc32) return snprintf(err, errlen, "%s: CRC-32 mismatch", e.name), FNPZ_ECORRUPT;
+    return FNPZ_OK;
+}
+
+template <class F>
+void parallel_for(int n, int threads, F&& f) {
+    threads = std::max(1, std::min(threads, n));
+    if (threads == 1) {
+        for (int i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; ++t)
+        pool.emplace_back([&] {
+            for (int i; (i = next.fetch_add(1)) < n;) f(i);
+        });
+    for (auto& th : pool) th.join();
+}
+
+// ---------------------------------------------------------------------------------------
+// writer
+// ---------------------------------------------------------------------------------------
+struct Block {
+    int member;
+    int64_t begin, len;          // range in the member's virtual stream (header + payload)
+    bool last;
+    std::vector<uint8_t> out;
+    uLong crc = 0;
+    int rc = Z_OK;
+};
+
+struct MemberSrc {
+    const uint8_t* header;
+    int64_t hlen;
+    const uint8_t* data;
+    int64_t nbytes;
+    // copy virtual-stream range [b, b+n) into dst
+    void gather(int64_t b, int64_t n, uint8_t* dst) const {
+        if (b < hlen) {
+            const int64_t k = std::min(n, hlen - b);
+            std::memcpy(dst, header + b, (size_t)k);
+            dst += k;
+            b += k;
+            n -= k;
+        }
+        if (n > 0) std::memcpy(dst, data + (b - hlen), (size_t)n);
+    }
+    const uint8_t* direct(int64_t b, int64_t n) const { return b >= hlen ? data + (b - hlen) : (b + n <= hlen ? header + b : nullptr); }
+};
+
+void deflate_block(const MemberSrc& m, Block& blk, int level) {
+    std::vector<uint8_t> tmp;
+    const uint8_t* in = m.direct(blk.begin, blk.len);
+    if (!in) {
+        tmp.resize((size_t)blk.len);
+        m.gather(blk.begin, blk.len, tmp.data());
+        in = tmp.data();
+    }
+    blk.crc = crc32(0L, in, (uInt)blk.len);
+    z_stream zs{};
+    if (deflateInit2(&zs, level, Z_DEFLATED, -MAX_WBITS, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+        blk.rc = Z_STREAM_ERROR;
+        return;
+    }
+    blk.out.resize(deflateBound(&zs, (uLong)blk.len) + 64);
+    zs.next_in = const_cast<Bytef*>(in);
+    zs.avail_in = (uInt)blk.len;
+    zs.next_out = blk.out.data();
+    zs.avail_out = (uInt)blk.out.size();
+    const int rc = deflate(&zs, blk.last ? Z_FINISH : Z_SYNC_FLUSH);
+    blk.rc = (blk.last ? rc == Z_STREAM_END : (rc == Z_OK && zs.avail_in == 0)) ? Z_OK : Z_BUF_ERROR;
+    blk.out.resize(blk.out.size() - zs.avail_out);
+    deflateEnd(&zs);
+}
+
+}  // namespace
+
+extern "C" {
+
+int fnpz_abi_version(void) { return FNPZ_ABI_VERSION; }
+const char* fnpz_last_error(void) { return g_err; }
+
+int fnpz_open(const uint8_t* archive, int64_t len, fnpz_entry* entries, int max_entries, int* n_entries) {
+    g_err[0] = 0;
+    if (!archive || len < 0 || !n_entries || (max_entries > 0 && !entries)) return fail(FNPZ_EINVAL, "fnpz_open: bad arguments");
+    std::vector<CdEntry> cd;
+    int rc = read_central(archive, len, cd);
+    if (rc) return rc;
+    *n_entries = (int)cd.size();
+    if ((int)cd.size() > max_entries) return fail(FNPZ_ENOSPC, "fnpz_open: archive has %d members, room for %d", (int)cd.size(), max_entries);
+    for (size_t i = 0; i < cd.size(); ++i)
+        if ((rc = resolve_entry(archive, len, cd[i], &entries[i]))) return rc;
+    return FNPZ_OK;
+}
+
+int fnpz_read(const uint8_t* archive, int64_t len, const fnpz_entry* entries, int n, void* const* dsts, int threads) {
+    g_err[0] = 0;
+    if (!archive || n < 0 || (n > 0 && (!entries || !dsts))) return fail(FNPZ_EINVAL, "fnpz_read: bad arguments");
+    for (int i = 0; i < n; ++i) {
+        if (entries[i].data_offset + entries[i].comp_size > len) return fail(FNPZ_EINVAL, "fnpz_read: entry %d out of range", i);
+        if (entries[i].nbytes > 0 && !dsts[i]) return fail(FNPZ_EINVAL, "fnpz_read: dsts[%d] is NULL", i);
+    }
+    // tasks: one per member, or one per block of members that carry a block index
+    struct Task { int member, block; };
+    std::vector<Task> tasks;
+    for (int i = 0; i < n; ++i) {
+        if (entries[i].method == 8 && entries[i].index_count > 0)
+            for (int b = 0; b < entries[i].index_count; ++b) tasks.push_back({i, b});
+        else
+            tasks.push_back({i, -1});
+    }
+    std::vector<int> rcs(tasks.size(), FNPZ_OK);
+    std::vector<uLong> bcrc(tasks.size(), 0);
+    std::vector<std::string> errs(tasks.size());
+    parallel_for((int)tasks.size(), threads, [&](int t) {
+        const fnpz_entry& e = entries[tasks[t].member];
+        void* dst = dsts[tasks[t].member];
+        char msg[300] = "";
+        if (tasks[t].block < 0) {
+            rcs[t] = decode_one(archive, e, dst, msg, sizeof(msg));
+        } else {
+            const uint8_t* ix = archive + e.index_offset;
+            const uint64_t B = rd64(ix + 8);
+            const int b = tasks[t].block;
+            const uint64_t c0 = rd64(ix + 16 + 8ull * b), c1 = rd64(ix + 16 + 8ull * (b + 1));
+            const uint64_t r0 = B * (uint64_t)b, r1 = std::min<uint64_t>(r0 + B, (uint64_t)e.uncomp_size);
+            if (c1 < c0 || c1 > (uint64_t)e.comp_size || r0 >= r1) {
+                rcs[t] = FNPZ_ECORRUPT;
+                snprintf(msg, sizeof(msg), "%s: bad block index", e.name);
+            } else {
+                Inflater inf(archive + e.data_offset + c0, (int64_t)(c1 - c0));
+                uLong crc = 0;
+                bool ok = inf.ok;
+                uint64_t pos = r0;
+                if (ok && pos < (uint64_t)e.npy_header) {          // block 0 starts with the .npy header
+                    std::vector<uint8_t> hdr((size_t)(e.npy_header - pos));
+                    ok = inf.fill(hdr.data(), (int64_t)hdr.size());
+                    crc = crc32(crc, hdr.data(), (uInt)hdr.size());
+                    pos = (uint64_t)e.npy_header;
+                }
+                uint8_t* out = static_cast<uint8_t*>(dst) + (pos - (uint64_t)e.npy_header);
+                while (ok && pos < r1) {
+                    const int64_t k = (int64_t)std::min<uint64_t>(r1 - pos, kChunk);
+                    ok = inf.fill(out, k);
+                    crc = crc32(crc, out, (uInt)k);
+                    out += k;
+                    pos += (uint64_t)k;
+                }
+                if (!ok) {
+                    rcs[t] = FNPZ_ECORRUPT;
+                    snprintf(msg, sizeof(msg), "%s: corrupt block %d", e.name, b);
+                }
+                bcrc[t] = crc;
+            }
+        }
+        errs[t] = msg;
+    });
+    for (size_t t = 0; t < tasks.size(); ++t)
+        if (rcs[t]) return fail(rcs[t], "%s", errs[t].c_str());
+    // combine the block CRCs of indexed members, in order
+    for (size_t t = 0; t < tasks.size();) {
+        const int i = tasks[t].member;
+        if (tasks[t].block < 0) {
+            ++t;
+            continue;
+        }
+        const fnpz_entry& e = entries[i];
+        const uint64_t B = rd64(archive + e.index_offset + 8);
+        uLong crc = 0;
+        for (int b = 0; b < e.index_count; ++b, ++t) {
+            const uint64_t r0 = B * (uint64_t)b, r1 = std::min<uint64_t>(r0 + B, (uint64_t)e.uncomp_size);
+            crc = b == 0 ? bcrc[t] : crc32_combine(crc, bcrc[t], (z_off_t)(r1 - r0));
+        }
+        if ((uint32_t)crc != e.crc32) return fail(FNPZ_ECORRUPT, "%s: CRC-32 mismatch", e.name);
+    }
+    return FNPZ_OK;
+}
+
+int64_t fnpz_write_bound(int n, const int64_t* header_lens, const int64_t* nbytes, const int32_t* name_lens) {
+    int64_t total = 22 + 56 + 20;
+    for (int i = 0; i < n; ++i) {
+        const int64_t raw = header_lens[i] + nbytes[i];
+        // stored-block worst case of deflate: 5 bytes per 16 KiB, plus per-block flush markers
+        total += raw + raw / 16000 * 5 + (raw / 65536 + 2) * 72 + 2 * (30 + 46 + name_lens[i] + 4 + 20 + 28) + 64;
+    }
+    return total;
+}
+
+int fnpz_write(int n, const char* const* names, const uint8_t* const* headers, const int64_t* header_lens,
+               const void* const* datas, const int64_t* nbytes, int level, int threads, int64_t block,
+               uint8_t* out, int64_t out_cap, int64_t* out_len) {
+    g_err[0] = 0;
+    if (n < 0 || !out || !out_len || (n > 0 && (!names || !headers || !header_lens || !datas || !nbytes)))
+        return fail(FNPZ_EINVAL, "fnpz_write: bad arguments");
+    if (level < 0 || level > 9) return fail(FNPZ_EINVAL, "fnpz_write: level must be 0..9");
+    if (block <= 0) block = 4 << 20;
+    block = std::min<int64_t>(std::max<int64_t>(block, 64 << 10), 1 << 30);
+    std::vector<MemberSrc> src((size_t)n);
+    std::vector<Block> blocks;
+    std::vector<int64_t> mblock((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        src[i] = MemberSrc{headers[i], header_lens[i], static_cast<const uint8_t*>(datas[i]), nbytes[i]};
+        const int64_t total = header_lens[i] + nbytes[i];
+        const int64_t B = std::max<int64_t>(block, (total + kMaxIndexBlocks - 1) / kMaxIndexBlocks);
+        mblock[i] = B;
+        for (int64_t b = 0; b < total || b == 0; b += B) {
+            Block blk;
+            blk.member = i;
+            blk.begin = b;
+            blk.len = std::min(B, total - b);
+            blk.last = b + B >= total;
+            blocks.push_back(std::move(blk));
+            if (total == 0) break;
+        }
+    }
+    parallel_for((int)blocks.size(), threads, [&](int j) { deflate_block(src[blocks[j].member], blocks[j], level); });
+    for (auto& b : blocks)
+        if (b.rc != Z_OK) return fail(FNPZ_ECORRUPT, "fnpz_write: deflate failed on member %d", b.member);
+
+    uint8_t* p = out;
+    uint8_t* const lim = out + out_cap;
+    std::vector<uint64_t> offs((size_t)n), comps((size_t)n);
+    std::vector<uint32_t> crcs((size_t)n);
+    size_t bi = 0;
+    for (int i = 0; i < n; ++i) {
+        const size_t nl = std::strlen(names[i]) + 4;
+        uint64_t comp = 0;
+        uLong crc = 0;
+        size_t bj = bi;
+        for (; bj < blocks.size() && blocks[bj].member == i; ++bj) {
+            comp += blocks[bj].out.size();
+            crc = bj == bi ? blocks[bj].crc : crc32_combine(crc, blocks[bj].crc, (z_off_t)blocks[bj].len);
+        }
+        const uint64_t raw = (uint64_t)(header_lens[i] + nbytes[i]);
+        const int nblk = (int)(bj - bi);
+        const int xl = 20 + 4 + 16 + 8 * (nblk + 1);
+        if (p + 30 + nl + xl + comp > lim) return fail(FNPZ_ENOSPC, "fnpz_write: output buffer too small");
+        offs[i] = (uint64_t)(p - out);
+        comps[i] = comp;
+        crcs[i] = (uint32_t)crc;
+        wr32(p, kLocalSig);
+        wr16(p + 4, 45);
+        wr16(p + 6, 0);
+        wr16(p + 8, 8);
+        wr16(p + 10, 0);        // DOS time 00:00
+        wr16(p + 12, 0x21);     // DOS date 1980-01-01
+        wr32(p + 14, (uint32_t)crc);
+        wr32(p + 18, 0xFFFFFFFFu);
+        wr32(p + 22, 0xFFFFFFFFu);
+        wr16(p + 26, (uint16_t)nl);
+        wr16(p + 28, (uint16_t)xl);
+        std::memcpy(p + 30, names[i], nl - 4);
+        std::memcpy(p + 30 + nl - 4, ".npy", 4);
+        uint8_t* x = p + 30 + nl;
+        wr16(x, 1);
+        wr16(x + 2, 16);
+        wr64(x + 4, raw);
+        wr64(x + 12, comp);
+        x += 20;
+        wr16(x, kIndexId);
+        wr16(x + 2, (uint16_t)(16 + 8 * (nblk + 1)));
+        wr32(x + 4, (uint32_t)nblk);
+        wr32(x + 8, 0);
+        wr64(x + 12, (uint64_t)mblock[i]);
+        uint64_t off = 0;
+        for (int b = 0; b <= nblk; ++b) {
+            wr64(x + 20 + 8 * b, off);
+            if (b < nblk) off += blocks[bi + b].out.size();
+        }
+        p = x + 20 + 8 * (nblk + 1);
+        for (; bi < bj; ++bi) {
+            std::memcpy(p, blocks[bi].out.data(), blocks[bi].out.size());
+            p += blocks[bi].out.size();
+            std::vector<uint8_t>().swap(blocks[bi].out);
+        }
+    }
+    const uint64_t cd_off = (uint64_t)(p - out);
+    for (int i = 0; i < n; ++i) {
+        const size_t nl = std::strlen(names[i]) + 4;
+        if (p + 46 + nl + 28 > lim) return fail(FNPZ_ENOSPC, "fnpz_write: output buffer too small");
+        const uint64_t raw = (uint64_t)(header_lens[i] + nbytes[i]);
+        wr32(p, kCentralSig);
+        wr16(p + 4, 45);
+        wr16(p + 6, 45);
+        wr16(p + 8, 0);
+        wr16(p + 10, 8);
+        wr16(p + 12, 0);
+        wr16(p + 14, 0x21);
+        wr32(p + 16, crcs[i]);
+        wr32(p + 20, 0xFFFFFFFFu);
+        wr32(p + 24, 0xFFFFFFFFu);
+        wr16(p + 28, (uint16_t)nl);
+        wr16(p + 30, 28);
+        wr16(p + 32, 0);
+        wr16(p + 34, 0);
+        wr16(p + 36, 0);
+        wr32(p + 38, 0x01800000u);   // -rw------- (what zipfile writes for numpy)
+        wr32(p + 42, 0xFFFFFFFFu);
+        std::memcpy(p + 46, names[i], nl - 4);
+        std::memcpy(p + 46 + nl - 4, ".npy", 4);
+        uint8_t* x = p + 46 + nl;
+        wr16(x, 1);
+        wr16(x + 2, 24);
+        wr64(x + 4, raw);
+        wr64(x + 12, comps[i]);
+        wr64(x + 20, offs[i]);
+        p = x + 28;
+    }
+    const uint64_t cd_size = (uint64_t)(p - out) - cd_off;
+    if (p + 56 + 20 + 22 > lim) return fail(FNPZ_ENOSPC, "fnpz_write: output buffer too small");
+    const uint64_t z64 = (uint64_t)(p - out);
+    wr32(p, kZ64EocdSig);
+    wr64(p + 4, 44);
+    wr16(p + 12, 45);
+    wr16(p + 14, 45);
+    wr32(p + 16, 0);
+    wr32(p + 20, 0);
+    wr64(p + 24, (uint64_t)n);
+    wr64(p + 32, (uint64_t)n);
+    wr64(p + 40, cd_size);
+    wr64(p + 48, cd_off);
+    p += 56;
+    wr32(p, kZ64LocSig);
+    wr32(p + 4, 0);
+    wr64(p + 8, z64);
+    wr32(p + 16, 1);
+    p += 20;
+    wr32(p, kEocdSig);
+    wr16(p + 4, 0);
+    wr16(p + 6, 0);
+    wr16(p + 8, (uint16_t)std::min(n, 0xFFFF));
+    wr16(p + 10, (uint16_t)std::min(n, 0xFFFF));
+    wr32(p + 12, (uint32_t)std::min<uint64_t>(cd_size, 0xFFFFFFFFu));
+    wr32(p + 16, (uint32_t)std::min<uint64_t>(cd_off, 0xFFFFFFFFu));
+    wr16(p + 20, 0);
+    p += 22;
+    *out_len = (int64_t)(p - out);
+    return FNPZ_OK;
+}
+
+}  // extern "C"

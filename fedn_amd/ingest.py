@@ -1,0 +1,175 @@
+"""Streaming ingest: stage client updates into HBM when they
+ARRIVE, not when the round aggregates.
+
+In FEDn an update reaches the combiner through ``ModelService.Upload`` (modelservice.py:
+198-221) and ``UpdateHandler.on_model_update`` (updatehandler.py:46-70), which only
+validates and enqueues it; decoding (npz inflate, updatehandler.py:90-117) and all
+arithmetic happen later, serially, inside ``combine_models`` (fedavg.py:118, 130). Here
+:class:`StagingUpdateHandler` wraps the combiner's UpdateHandler: ``on_model_update``
+enqueues the update in arrival order exactly as before AND hands it to a worker pool
+that decodes it (the wrapped handler's own ``load_model_update`` with the round's
+helper) and copies it into a device buffer on its own HIP stream. When the aggregator
+later calls ``load_model_update`` it receives a :class:`StagedModel` (already in HBM),
+which the pipelines in staging.py fold without any host work. FIFO order, metadata
+handling and error semantics are unchanged: a decode that fails re-raises from
+``load_model_update``, where the aggregator's per-update error handling (fedavg.py:
+137-140) logs and skips it, as FEDn would.
+"""
+import json
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import torch
+
+from .layout import Layout
+
+
+class StagedModel:
+    """One decoded client update resident in HBM: flat grouped layout (layout.py) in
+    ``dev`` (uint8), ready once ``ready`` (an event on the staging stream) has fired.
+    ``host`` returns the update as host arrays (needed only when it is the round's sole
+    update, fedavg.py:127-128): the decoded arrays if they were kept, else a D2H copy."""
+
+    __slots__ = ("layout", "dev", "ready", "_host")
+
+    def __init__(self, layout, dev, ready, host=None):
+        self.layout, self.dev, self.ready, self._host = layout, dev, ready, host
+
+    @property
+    def host(self):
+        if self._host is None:
+            self.ready.synchronize()
+            flat = self.dev.to("cpu").numpy()
+            out = [None] * len(self.layout.shapes)
+            for dt in self.layout.groups:
+                self.layout.unpack_group(self.layout.group_view(flat, dt), dt, out, copy=False)
+            self._host = out
+        return self._host
+
+    # list-like access to the host arrays, so code written for list[np.ndarray] still works
+    def __len__(self):
+        return len(self.layout.shapes)
+
+    def __getitem__(self, i):
+        return self.host[i]
+
+    def __iter__(self):
+        return iter(self.host)
+
+
+def stage_arrays(arrays, device, stream):
+    """Pack host ``arrays`` into pinned memory and copy them to a new device buffer on
+    ``stream``; returns a :class:`StagedModel` (the H2D may still be in flight)."""
+    arrays = [np.asarray(a) for a in arrays]
+    layout = Layout.of(arrays)
+    pinned = torch.empty(layout.nbytes, dtype=torch.uint8, pin_memory=True)
+    layout.pack(arrays, pinned.numpy())
+    dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
+    ready = torch.cuda.Event()
+    with torch.cuda.stream(stream):
+        dev.copy_(pinned, non_blocking=True)
+        ready.record(stream)
+    # the pinned block returns to torch's caching host allocator only after the copy
+    ready.synchronize()
+    del pinned
+    return StagedModel(layout, dev, ready, arrays)
+
+
+def stage_npz(data, device, stream):
+    """Inflate an npz update (native codec) straight into a pinned buffer laid out for the
+    pipelines, then copy it to HBM on ``stream``: no temp file, no numpy arrays, no pack."""
+    from . import codec
+
+    layout, pinned = codec.load_npz_into_layout(
+        data, lambda nbytes: torch.empty(nbytes, dtype=torch.uint8, pin_memory=True))
+    dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
+    ready = torch.cuda.Event()
+    with torch.cuda.stream(stream):
+        dev.copy_(pinned, non_blocking=True)
+        ready.record(stream)
+    ready.synchronize()
+    return StagedModel(layout, dev, ready)
+
+
+class StagingUpdateHandler:
+    """Drop-in wrapper of a FEDn ``UpdateHandler`` that decodes + stages updates on arrival.
+
+    helper   the round's helper (FEDn: ``get_helper(config["helper_type"])``); used for decoding
+             when the update is not available as raw npz bytes
+    workers  decode/H2D threads (each with its own HIP stream)
+    native_decode  take the raw npz bytes (UpdateHandler.load_model_update_byte,
+             updatehandler.py:119-144) and inflate them with fedn_amd.codec straight into
+             pinned memory in the pipelines' layout
+    Every attribute not defined here (``model_updates``, ``next_model_update``, ``load_model``,
+    ``waitforit``, ...) is the wrapped handler's.
+    """
+
+    def __init__(self, inner, helper=None, device=None, workers=4, native_decode=True):
+        self.inner = inner
+        self.native_decode = native_decode
+        self.helper = helper
+        self.device = torch.device(device) if device is not None else None
+        self._pool = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="fedn_amd_ingest")
+        self._streams = {}
+        self._lock = threading.Lock()
+        self._staged = {}
+
+    def __getattr__(self, name):
+        return getattr(self.inner, name)
+
+    def _device(self):
+        if self.device is None:
+            from .aggregators.fedavg import default_device
+            self.device = default_device()
+        return self.device
+
+    def _stream(self):
+        tid = threading.get_ident()
+        with self._lock:
+            st = self._streams.get(tid)
+            if st is None:
+                st = self._streams[tid] = torch.cuda.Stream(self._device())
+        return st
+
+    def _stage(self, model_update):
+        dev = self._device()
+        if self.native_decode and hasattr(self.inner, "load_model_update_byte"):
+            try:
+                data, metadata = self.inner.load_model_update_byte(model_update)
+            except Exception:  # noqa: BLE001 — not held as bytes: decode through the helper
+                data = None
+            if data is not None:
+                with torch.cuda.device(dev):
+                    return stage_npz(data, dev, self._stream()), metadata
+        arrays, metadata = self.inner.load_model_update(model_update, self.helper)
+        with torch.cuda.device(dev):
+            return stage_arrays(arrays, dev, self._stream()), metadata
+
+    def on_model_update(self, model_update):
+        """Validate as FEDn does (updatehandler.py:72-88), start staging, then enqueue."""
+        try:
+            json.loads(model_update.meta)["training_metadata"]["num_examples"]
+            valid = True
+        except (KeyError, TypeError, ValueError):
+            valid = False
+        if valid:
+            self._device()
+            with self._lock:
+                self._staged[model_update.model_update_id] = self._pool.submit(self._stage, model_update)
+        return self.inner.on_model_update(model_update)
+
+    def load_model_update(self, model_update, helper):
+        with self._lock:
+            fut = self._staged.pop(model_update.model_update_id, None)
+        if fut is None:                       # arrived before the wrapper was installed
+            return self.inner.load_model_update(model_update, helper)
+        return fut.result()
+
+    def delete_model(self, model_update):
+        with self._lock:
+            self._staged.pop(model_update.model_update_id, None)
+        return self.inner.delete_model(model_update)
+
+    def close(self):
+        self._pool.shutdown(wait=True)

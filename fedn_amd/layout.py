@@ -90,6 +90,19 @@ class Layout:
                 raise TypeError(f"tensor {i} has dtype {a.dtype}, expected {self.dtypes[i]} "
                                 "(mixed dtypes across client updates are not supported)")
 
+    def check_layout(self, other):
+        """Like :meth:`check` for an already-laid-out update (a staged model's Layout)."""
+        if other.signature() == self.signature():
+            return
+        if len(other.shapes) != len(self.shapes):
+            raise ValueError(f"model has {len(other.shapes)} tensors, expected {len(self.shapes)}")
+        for i, (s, d) in enumerate(zip(other.shapes, other.dtypes)):
+            if s != self.shapes[i]:
+                raise ValueError(f"operands could not be combined: tensor {i} has shape {s}, expected {self.shapes[i]}")
+            if d != self.dtypes[i]:
+                raise TypeError(f"tensor {i} has dtype {d}, expected {self.dtypes[i]} "
+                                "(mixed dtypes across client updates are not supported)")
+
     def group_view(self, buf_np_u8, dt):
         """numpy view of group ``dt`` inside a uint8 host buffer."""
         off = self.group_byte_offset[dt]

@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from . import ops
+from .ingest import StagedModel
 from .layout import Layout, parallel_copy
 
 
@@ -40,15 +41,19 @@ class _Pipeline:
         self.layout = layout
         self.compute = torch.cuda.current_stream(self.device)
         self.copy = torch.cuda.Stream(self.device)
-        self.slots = [_Slot(layout.nbytes, self.device) for _ in range(nslots)]
+        self.nslots = nslots
+        self.slots = []                          # created on first use (staged inputs need none)
         self._next = 0
         self._h2d = []
         self._kern = []
         self.time_pack = 0.0
         self.time_d2h = 0.0
+        self._hold = []
 
     # ---- staging ---------------------------------------------------------------------
     def _take_slot(self):
+        if not self.slots:
+            self.slots = [_Slot(self.layout.nbytes, self.device) for _ in range(self.nslots)]
         for _ in range(len(self.slots)):
             s = self.slots[self._next]
             self._next = (self._next + 1) % len(self.slots)
@@ -73,6 +78,17 @@ class _Pipeline:
         self.compute.wait_event(s.h2d_done)
         s.used = True
         return s
+
+    def acquire(self, arrays):
+        """Device-resident source for ``arrays``: a StagedModel is used in place (the compute
+        stream waits for its H2D); host arrays are packed into a ring slot."""
+        if isinstance(arrays, StagedModel):
+            self.layout.check_layout(arrays.layout)      # raises the numpy-like error
+            self.compute.wait_event(arrays.ready)
+            self._hold.append(arrays)                    # keep HBM alive until the round ends
+            return arrays
+        self.layout.check(arrays)
+        return self.stage(arrays)
 
     def group(self, slot, dt):
         """Device view (flat, torch dtype) of group ``dt`` inside a staged slot."""
@@ -117,20 +133,25 @@ class FedAvgPipeline(_Pipeline):
     """Streaming FedAvg on one device: fedavg.py:109-133 with the fold on the GPU."""
 
     def __init__(self, device, first_arrays, nslots=3):
-        super().__init__(device, Layout.of(first_arrays), nslots)
-        self.first_arrays = first_arrays
-        self.first = self.stage(first_arrays)
-        self.first.reserved = True
+        staged = isinstance(first_arrays, StagedModel)
+        super().__init__(device, first_arrays.layout if staged else Layout.of(first_arrays), nslots)
+        self.first_arrays = first_arrays         # a StagedModel materialises host arrays only if needed
+        self.first = self.acquire(first_arrays) if staged else self.stage(first_arrays)
+        if not staged:
+            self.first.reserved = True
         self.n0 = None
         self.nfolds = 0
         self.agg = {}
 
     def add(self, arrays, n, N):
         """Fold one more update (n = its num_examples, N = running total including it)."""
-        self.layout.check(arrays)
+        if isinstance(arrays, StagedModel):
+            self.layout.check_layout(arrays.layout)
+        else:
+            self.layout.check(arrays)
         for dt in self.layout.groups:           # refuse before touching device state
             ops.fa_dtype(ops.torch_dtype(dt))
-        slot = self.stage(arrays)
+        slot = self.acquire(arrays)
         span = self._kernel_span()
         for dt in self.layout.groups:
             y = self.group(slot, dt)
@@ -142,8 +163,9 @@ class FedAvgPipeline(_Pipeline):
             else:
                 ops.fedavg_fold(self.agg[dt], [y], [n], [N], init=False, stream=self.compute)
         self._end_span(span)
-        slot.consumed.record(self.compute)
-        if self.nfolds == 0:
+        if isinstance(slot, _Slot):
+            slot.consumed.record(self.compute)
+        if self.nfolds == 0 and isinstance(self.first, _Slot):
             self.first.consumed.record(self.compute)
             self.first.reserved = False
         self.nfolds += 1
@@ -151,7 +173,8 @@ class FedAvgPipeline(_Pipeline):
     def result(self):
         """The aggregated model as a new host ``list[np.ndarray]`` (fedavg.py:145)."""
         if self.nfolds == 0:
-            return self.first_arrays            # `model = model_next` alias (fedavg.py:127-128)
+            first = self.first_arrays           # `model = model_next` alias (fedavg.py:127-128)
+            return first.host if isinstance(first, StagedModel) else first
         out = [None] * len(self.layout.shapes)
         for dt in self.layout.groups:
             h = self._to_host(self.agg[dt])
@@ -198,7 +221,7 @@ class FedOptPipeline(_Pipeline):
     GPU (pg resident in HBM), then the fused server step (fedopt.py:151-258)."""
 
     def __init__(self, device, old_arrays, first_arrays, nslots=2):
-        layout = Layout.of(first_arrays)
+        layout = first_arrays.layout if isinstance(first_arrays, StagedModel) else Layout.of(first_arrays)
         super().__init__(device, layout, nslots)
         if len(old_arrays) != len(layout.shapes):
             raise ValueError("global model and update have different tensor counts")
@@ -221,11 +244,14 @@ class FedOptPipeline(_Pipeline):
         self.nfolds = 0
 
     def add(self, arrays, n, N):
-        self.layout.check(arrays)
+        if isinstance(arrays, StagedModel):
+            self.layout.check_layout(arrays.layout)
+        else:
+            self.layout.check(arrays)
         for dt in self.layout.groups:
             if ops.torch_dtype(dt) not in (torch.float32, torch.float64):
                 raise TypeError(f"FedOpt supports float32/float64 updates, got {dt}")
-        slot = self.stage(arrays)
+        slot = self.acquire(arrays)
         span = self._kernel_span()
         first = self.nfolds == 0
         for dt in self.layout.groups:
@@ -236,7 +262,8 @@ class FedOptPipeline(_Pipeline):
                 self.pg[dt] = torch.empty(y.numel(), dtype=pg_dt, device=self.device)
             ops.fedopt_step(old, [y], [n], [N], first=first, final=False, pg=self.pg[dt], stream=self.compute)
         self._end_span(span)
-        slot.consumed.record(self.compute)
+        if isinstance(slot, _Slot):
+            slot.consumed.record(self.compute)
         self.nfolds += 1
 
     def server_step(self, state, params):

@@ -13,6 +13,14 @@ import json
 import queue
 import uuid
 from dataclasses import dataclass
+from io import BytesIO
+
+
+class _NpzBytes:
+    __slots__ = ("data",)
+
+    def __init__(self, data):
+        self.data = data
 
 
 @dataclass
@@ -50,14 +58,19 @@ class MemoryUpdateHandler:
         self.store.put(model_id, arrays)
         return model_id
 
-    def submit(self, arrays, num_examples, model_id="global", round_id="1"):
-        """Store an update and enqueue its ModelUpdate (on_model_update, updatehandler.py:46-70)."""
+    def submit_bytes(self, npz_bytes, num_examples, model_id="global", round_id="1", via=None):
+        """Enqueue an update held as npz bytes (what ModelService.Upload stores, modelservice.py:198-221)."""
+        return self.submit(_NpzBytes(bytes(npz_bytes)), num_examples, model_id, round_id, via)
+
+    def submit(self, arrays, num_examples, model_id="global", round_id="1", via=None):
+        """Store an update and enqueue its ModelUpdate (on_model_update, updatehandler.py:46-70).
+        ``via``: a wrapper (e.g. ingest.StagingUpdateHandler) whose on_model_update to call."""
         uid = str(uuid.uuid4())
         self.store.put(uid, arrays)
         meta = json.dumps({"training_metadata": {"num_examples": num_examples},
                            "config": json.dumps({"round_id": round_id})})
         mu = ModelUpdate(model_id=model_id, model_update_id=uid, meta=meta)
-        self.on_model_update(mu)
+        (via or self).on_model_update(mu)
         return mu
 
     def on_model_update(self, model_update):
@@ -76,7 +89,23 @@ class MemoryUpdateHandler:
         model = self.store.get(model_id)
         if model is None:
             raise RuntimeError(f"Failed to load model {model_id}.")
+        if isinstance(model, _NpzBytes):        # load_model_from_bytes(..., helper) (modelservice.py:110-125)
+            if helper is None:
+                raise RuntimeError("an npz-encoded update needs a helper to decode it")
+            return helper.load(BytesIO(model.data))
         return model
+
+    def load_model_update_byte(self, model_update):
+        """(raw npz bytes, training_metadata) — updatehandler.py:119-144."""
+        model = self.store.get(model_update.model_update_id)
+        if not isinstance(model, _NpzBytes):
+            raise RuntimeError("update is not held as bytes")
+        metadata = json.loads(model_update.meta)
+        config = json.loads(metadata["config"]) if "config" in metadata else json.loads(model_update.config)
+        training_metadata = metadata["training_metadata"]
+        if "round_id" in config:
+            training_metadata["round_id"] = config["round_id"]
+        return model.data, training_metadata
 
     def load_model_update(self, model_update, helper):
         model = self.load_model(helper, model_update.model_update_id)

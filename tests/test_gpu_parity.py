@@ -265,3 +265,76 @@ def test_control_reduce_golden(name):
     assert_lists_identical(model, case["out"], name)
     assert deleted == [c["model_id"] for c in combiners]
     assert set(meta) == {"time_fetch_model", "time_load_model", "time_aggregate_model"}
+
+
+# ------------------------------------------------------------------------- streaming ingest
+@pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k17", "fedavg_skipbad_k4", "fedavg_int64_k3",
+                                  "fedavg_odd_k1"])
+def test_staging_ingest_fedavg_golden(name):
+    """Updates staged into HBM on arrival (ingest.StagingUpdateHandler) give the same result."""
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rd = load_case(name)["rounds"][0]
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=None, device=DEV, workers=3)
+    for arrays, n in rd["updates"]:
+        uh.submit(arrays, n, via=st)
+    model, data = get_aggregator("fedavg", st).combine_models(helper=None)
+    st.close()
+    assert data["nr_aggregated_models"] == rd["nr"]
+    assert_lists_identical(model, rd["out"], name)
+
+
+@pytest.mark.parametrize("name", ["fedopt_adam_3r", "fedopt_yogi_lr1e-2_k8"])
+def test_staging_ingest_fedopt_golden(name):
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    case = load_case(name)
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=None, device=DEV, workers=2)
+    agg = get_aggregator("fedopt", st)
+    for r, rd in enumerate(case["rounds"]):
+        gid = uh.put_global_model(rd["old"], f"global-{r}")
+        for arrays, n in rd["updates"]:
+            uh.submit(arrays, n, model_id=gid, via=st)
+        model, _ = agg.combine_models(helper=None, parameters=case["params"])
+        assert_lists_identical(model, rd["out"], f"{name} r{r}")
+    st.close()
+
+
+@pytest.mark.parametrize("native", [True, False])
+@pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k8", "fedavg_int32_k3", "fedavg_skipbad_k4"])
+def test_staging_ingest_npz_bytes(name, native):
+    """Updates arriving as npz bytes (numpy savez_compressed, as FEDn clients upload them):
+    inflated by the native codec straight into pinned memory (native=True) or decoded by
+    the helper (native=False), staged into HBM on arrival, folded bit-exactly."""
+    import io
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.helper import Helper
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rd = load_case(name)["rounds"][0]
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=Helper(), device=DEV, workers=3, native_decode=native)
+    for arrays, n in rd["updates"]:
+        b = io.BytesIO()
+        np.savez_compressed(b, **{str(i): a for i, a in enumerate(arrays)})
+        uh.submit_bytes(b.getvalue(), n, via=st)
+    model, data = get_aggregator("fedavg", st).combine_models(helper=Helper())
+    st.close()
+    assert data["nr_aggregated_models"] == rd["nr"]
+    assert_lists_identical(model, rd["out"], name)
+
+
+def test_helper_increment_average_gpu():
+    """fedn_amd.helper.Helper.increment_average == numpyhelper's (the reference KAT + random)."""
+    from fedn_amd.helper import Helper
+    c = load_case("kat_int64")["raw"]
+    out = Helper().increment_average([c["m1_t0"]], [c["m2_t0"]], int(c["a"]), int(c["W"]))
+    assert_lists_identical(out, [c["out_t0"]], "kat")
+    rng = np.random.default_rng(9)
+    m1 = [rng.standard_normal((7, 3)).astype(np.float32), rng.standard_normal(5).astype(np.float32)]
+    m2 = [rng.standard_normal((7, 3)).astype(np.float32), rng.standard_normal(5).astype(np.float32)]
+    assert_lists_identical(Helper().increment_average(m1, m2, 37, 1234), ref.increment_average(m1, m2, 37, 1234), "rnd")
