@@ -284,12 +284,12 @@ __device__ __forceinline__ int strip_start(typename CP::V (&x)[E], const X* __re
 }
 
 // The grid's last block: its strips may be ragged or past the end of the buffers.
-template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST>
+template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, int BLK = kBlock>
 __device__ __forceinline__ void k_fedavg_tail(X* __restrict__ agg, const ClientTable<typename CP::S>& tab, const int K,
                                            const int64_t P, const int64_t strip0) {
     using V = typename CP::V;
     for (int s = 0; s < S; ++s) {
-        const int64_t i0 = (strip0 + s * kBlock) * E;
+        const int64_t i0 = (strip0 + s * BLK) * E;
         if (i0 >= P) break;
         const int rem = (P - i0) < E ? (int)(P - i0) : E;
         V x[E];
@@ -405,29 +405,29 @@ struct LaneTable {
     }
 };
 
-template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT>
-__global__ void __launch_bounds__(kBlock)
+template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK = kBlock>
+__global__ void __launch_bounds__(BLK)
 k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P) {
     using V = typename CP::V;
     const LaneTable<CP> lt(tab);
-    const int64_t ntiles = ((P + E - 1) / E + (int64_t)kBlock * S - 1) / ((int64_t)kBlock * S);
+    const int64_t ntiles = ((P + E - 1) / E + (int64_t)BLK * S - 1) / ((int64_t)BLK * S);
     // one tile per block (gridDim == ntiles), or a persistent grid sweeping tiles in grid
     // order so the tiles read concurrently from one client buffer are adjacent
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t strip0 = tile * (kBlock * S) + threadIdx.x;
-        if ((strip0 + (int64_t)(S - 1) * kBlock) * E + E > P) {
-            k_fedavg_tail<Y, X, CP, E, S, INIT, INT_FIRST>(agg, tab, K, P, strip0);
+        const int64_t strip0 = tile * (BLK * S) + threadIdx.x;
+        if ((strip0 + (int64_t)(S - 1) * BLK) * E + E > P) {
+            k_fedavg_tail<Y, X, CP, E, S, INIT, INT_FIRST, BLK>(agg, tab, K, P, strip0);
             continue;
         }
         V x[S][E];
         int k = 0;
 #pragma unroll
         for (int s = 0; s < S; ++s)
-            k = strip_start<Y, X, CP, E, INIT, INT_FIRST, NT>(x[s], agg, tab, (strip0 + s * kBlock) * E, E);
+            k = strip_start<Y, X, CP, E, INIT, INT_FIRST, NT>(x[s], agg, tab, (strip0 + s * BLK) * E, E);
         auto load = [&](int kk, Y (&y)[S][E]) {
             const Y* yp = LT ? reinterpret_cast<const Y*>(LaneTable<CP>::rl(lt.p, kk)) : static_cast<const Y*>(tab.ptr[kk]);
 #pragma unroll
-            for (int s = 0; s < S; ++s) strip_load<Y, E, NT>(yp + (strip0 + s * kBlock) * E, y[s]);
+            for (int s = 0; s < S; ++s) strip_load<Y, E, NT>(yp + (strip0 + s * BLK) * E, y[s]);
         };
         auto fold = [&](int kk, const Y (&y)[S][E]) {
             const typename CP::S n = LT ? LaneTable<CP>::rl(lt.n, kk) : tab.n[kk];
@@ -456,7 +456,7 @@ k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const 
             X xo[E];
 #pragma unroll
             for (int e = 0; e < E; ++e) xo[e] = narrow<X, V>(x[s][e]);
-            strip_store<X, E>(agg + (strip0 + s * kBlock) * E, xo);
+            strip_store<X, E>(agg + (strip0 + s * BLK) * E, xo);
         }
     }
 }
@@ -654,15 +654,16 @@ __global__ void __launch_bounds__(kBlock) k_stream_copy(u32x4* __restrict__ dst,
 }
 
 constexpr int kReadPerLane = 16;
+template <int RPL>
 __global__ void __launch_bounds__(kBlock) k_stream_read(const u32x4* __restrict__ src, int64_t n16, u32x4* __restrict__ sink) {
-    const int64_t base = (int64_t)blockIdx.x * kBlock * kReadPerLane + threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * kBlock * RPL + threadIdx.x;
     u32x4 acc = {0, 0, 0, 0};
 #pragma unroll
-    for (int j = 0; j < kReadPerLane; ++j) {
+    for (int j = 0; j < RPL; ++j) {
         const int64_t i = base + (int64_t)j * kBlock;
         if (i < n16) acc ^= __builtin_nontemporal_load(src + i);
     }
-    // wave xor-reduce is unnecessary for a bandwidth probe: one lane's word per block
+    // one 16-B word per block keeps the loads alive; the bandwidth probe needs no exact reduction
     __shared__ u32x4 red[kBlock];
     red[threadIdx.x] = acc;
     __syncthreads();
@@ -715,7 +716,9 @@ struct FedAvgCfg {
     int strips = 4;   // measured best on MI355X (profiles/r01_microbench.md): 4 strips per lane,
     int unroll = 0;   // software-pipelined one client ahead
     int lanetab = 0;
-    int grid_per_cu = 0;   // 0: one tile per block; n: persistent grid of n blocks per CU
+    int grid_per_cu = 0;
+    int read_per_lane = 16;   // fa_stream_read probe only
+    int block_log = 8;        // pipelined kernel workgroup size 2^block_log (8, 9, 10)   // 0: one tile per block; n: persistent grid of n blocks per CU
     int nt = 0;   // measured: cached loads beat non-temporal ones by ~3% (profiles/)
 };
 FedAvgCfg g_cfg;
@@ -728,20 +731,20 @@ int device_cus() {
     return cus > 0 ? cus : 256;
 }
 
-template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT>
+template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT, int BLK = kBlock>
 void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
                         hipStream_t st) {
     const int64_t strips = (P + E - 1) / E;
-    int64_t ntiles = (strips + (int64_t)kBlock * S - 1) / ((int64_t)kBlock * S);
+    int64_t ntiles = (strips + (int64_t)BLK * S - 1) / ((int64_t)BLK * S);
     if (g_cfg.grid_per_cu > 0) ntiles = std::min<int64_t>(ntiles, (int64_t)g_cfg.grid_per_cu * device_cus());
     const dim3 grid((unsigned)ntiles);
     if (first && int_first) {
         if constexpr (std::is_integral<Y>::value)
-            hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, true, NT, LT>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+            hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, true, NT, LT, BLK>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
     } else if (first)
-        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, false, NT, LT>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, false, NT, LT, BLK>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
     else
-        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, false, false, NT, LT>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
+        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, false, false, NT, LT, BLK>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
 }
 
 template <typename Y, typename X, class CP, int E, int S, int U, bool NT>
@@ -764,7 +767,8 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
                        hipStream_t st) {
     constexpr bool tunable = (std::is_same<Y, float>::value || std::is_same<Y, bf16>::value) && std::is_same<X, float>::value;
     if constexpr (tunable) {
-        const int key = g_cfg.lanetab * 10000 + g_cfg.strips * 100 + g_cfg.unroll * 2 + g_cfg.nt;
+        const int key = (g_cfg.block_log == 9 ? 20000 : g_cfg.block_log == 10 ? 30000 : 0) + g_cfg.lanetab * 10000 +
+                        g_cfg.strips * 100 + g_cfg.unroll * 2 + g_cfg.nt;
         switch (key) {
 #define FA_GEOM(S_, U_, NT_) \
     case S_ * 100 + U_ * 2 + NT_: return launch_fedavg_geom<Y, X, CP, E, S_, U_, NT_>(a, tab, cnt, P, first, int_first, st);
@@ -775,6 +779,10 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
             case 4 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 4, false, false>(a, tab, cnt, P, first, int_first, st);
             case 8 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 8, false, false>(a, tab, cnt, P, first, int_first, st);
             case 4 * 100 + 1: return launch_fedavg_pipe<Y, X, CP, E, 4, true, false>(a, tab, cnt, P, first, int_first, st);
+            case 20000 + 4 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, 512>(a, tab, cnt, P, first, int_first, st);
+            case 30000 + 4 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, 1024>(a, tab, cnt, P, first, int_first, st);
+            case 20000 + 8 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 8, false, false, 512>(a, tab, cnt, P, first, int_first, st);
+            case 30000 + 2 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 2, false, false, 1024>(a, tab, cnt, P, first, int_first, st);
             case 10000 + 2 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 2, false, true>(a, tab, cnt, P, first, int_first, st);
             case 10000 + 4 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 4, false, true>(a, tab, cnt, P, first, int_first, st);
             case 10000 + 8 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 8, false, true>(a, tab, cnt, P, first, int_first, st);
@@ -968,6 +976,14 @@ int fa_tune(int knob, int value) {
         case FA_TUNE_NT:
             g_cfg.nt = value ? 1 : 0;
             return FA_OK;
+        case FA_TUNE_BLOCK:
+            if (value != 256 && value != 512 && value != 1024) return fail(FA_EINVAL, "fa_tune: block 256, 512 or 1024");
+            g_cfg.block_log = value == 256 ? 8 : value == 512 ? 9 : 10;
+            return FA_OK;
+        case FA_TUNE_READ:
+            if (value != 4 && value != 8 && value != 16) return fail(FA_EINVAL, "fa_tune: read probe depth 4, 8 or 16");
+            g_cfg.read_per_lane = value;
+            return FA_OK;
         case FA_TUNE_GRID:
             if (value < 0 || value > 64) return fail(FA_EINVAL, "fa_tune: grid blocks per CU must be 0..64");
             g_cfg.grid_per_cu = value;
@@ -1019,8 +1035,17 @@ int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream) {
         return fail(FA_EINVAL, "fa_stream_read: bytes must be a multiple of 16 and buffers 16-B aligned");
     const int64_t blocks = fa_stream_read_blocks(bytes);
     if (!blocks) return FA_OK;
-    hipLaunchKernelGGL(k_stream_read, dim3((unsigned)blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
-                       static_cast<const u32x4*>(src), bytes / 16, static_cast<u32x4*>(sink));
+    const int64_t n16 = bytes / 16;
+    const dim3 blk(kBlock);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const u32x4* s4 = static_cast<const u32x4*>(src);
+    u32x4* k4 = static_cast<u32x4*>(sink);
+    // loads in flight per lane (fa_tune FA_TUNE_UNROLL reused for this probe: 4, 8 or 16)
+    switch (g_cfg.read_per_lane) {
+        case 4: hipLaunchKernelGGL(k_stream_read<4>, dim3((unsigned)((n16 + kBlock * 4 - 1) / (kBlock * 4))), blk, 0, st, s4, n16, k4); break;
+        case 8: hipLaunchKernelGGL(k_stream_read<8>, dim3((unsigned)((n16 + kBlock * 8 - 1) / (kBlock * 8))), blk, 0, st, s4, n16, k4); break;
+        default: hipLaunchKernelGGL(k_stream_read<16>, dim3((unsigned)blocks), blk, 0, st, s4, n16, k4); break;
+    }
     return check_launch("fa_stream_read");
 }
 

@@ -213,7 +213,8 @@ def stream_read_sink(src):
 
 _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _abi.FA_TUNE_NT,
           "fastdiv": _abi.FA_TUNE_FASTDIV, "lanetab": _abi.FA_TUNE_LANETAB,
-          "grid": _abi.FA_TUNE_GRID}
+          "grid": _abi.FA_TUNE_GRID, "read": _abi.FA_TUNE_READ,
+          "block": _abi.FA_TUNE_BLOCK}
 
 
 def tune(**knobs):

@@ -30,6 +30,9 @@ for s in $STEPS; do
     fedopt)
       timeout -k 10 900 python tools/bench_fedopt.py > "$OUT/fedopt.log" 2>&1; rc=$?
       echo "fedopt rc=$rc"; grep -v amdgpu.ids "$OUT/fedopt.log" | tail -8; [ $rc -eq 0 ] || exit $rc ;;
+    ingest)
+      timeout -k 10 900 python tools/bench_ingest.py > "$OUT/ingest.log" 2>&1; rc=$?
+      echo "ingest rc=$rc"; grep -v amdgpu.ids "$OUT/ingest.log" | tail -4; [ $rc -eq 0 ] || exit $rc ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc_$c" -o run -- \

@@ -42,8 +42,11 @@ def main():
     nb = 8 << 30
     src = torch.empty(nb, dtype=torch.uint8, device=dev).random_()
     sink = ops.stream_read_sink(src)
-    med, best = timed(lambda: ops.stream_read(src, sink))
-    print(json.dumps({"kernel": "stream_read", "bytes": nb, "ms": med, "GBps": nb / med / 1e6, "best_GBps": nb / best / 1e6}), flush=True)
+    for rpl in (4, 8, 16):
+        ops.tune(read=rpl)
+        med, best = timed(lambda: ops.stream_read(src, sink))
+        print(json.dumps({"kernel": f"stream_read x{rpl}/lane", "bytes": nb, "ms": med, "GBps": nb / med / 1e6,
+                          "best_GBps": nb / best / 1e6}), flush=True)
     half = src[: nb // 2]
     dst = torch.empty(nb // 2, dtype=torch.uint8, device=dev)
     med, best = timed(lambda: ops.stream_copy(dst, half))
@@ -66,16 +69,16 @@ def main():
     med, best = timed(lambda: ops.stream_sum(agg, ups))
     print(json.dumps({"kernel": "stream_sum (fold traversal, 1 add)", "ms": med, "GBps": alg / med / 1e6,
                       "best_GBps": alg / best / 1e6}), flush=True)
-    combos = [(S, U, 0, 1, 0, 0) for S, U in ((1, 8), (4, 1))]
-    combos += [(S, 0, 0, 1, 0, G) for S in (2, 4) for G in (0, 2, 4, 6, 8)]
-    for S, U, NT, F, L, G in combos:
-                ops.tune(strips=S, unroll=U, nt=NT, fastdiv=F, lanetab=L, grid=G)
+    combos = [(S, U, 0, 1, 0, 0, 256) for S, U in ((1, 8), (4, 1))]
+    combos += [(S, 0, 0, 1, 0, 0, B) for S, B in ((4, 256), (8, 256), (4, 512), (8, 512), (2, 1024), (4, 1024))]
+    for S, U, NT, F, L, G, B in combos:
+                ops.tune(strips=S, unroll=U, nt=NT, fastdiv=F, lanetab=L, grid=G, block=B)
                 med, best = timed(lambda: ops.fedavg_fold(agg, ups, ns, Ns, init=True))
                 torch.cuda.synchronize()
                 if ref_out is None:
                     ref_out = agg.clone()
                 same = bool(torch.equal(agg.view(torch.int32), ref_out.view(torch.int32)))
-                print(json.dumps({"kernel": "fedavg", "strips": S, "unroll": U, "nt": NT, "fastdiv": F, "lanetab": L, "grid": G, "K": K, "P": P, "ms": med,
+                print(json.dumps({"kernel": "fedavg", "strips": S, "unroll": U, "nt": NT, "fastdiv": F, "lanetab": L, "grid": G, "block": B, "K": K, "P": P, "ms": med,
                                   "GBps": alg / med / 1e6, "best_GBps": alg / best / 1e6, "identical": same}), flush=True)
     # one contiguous [K, P] slab instead of K separate allocations
     slab = torch.stack(ups)
@@ -89,7 +92,7 @@ def main():
                           "GBps": alg / med / 1e6}), flush=True)
     del slab, rows
     # reset defaults
-    ops.tune(strips=4, unroll=0, nt=0, fastdiv=1, lanetab=0, grid=0)
+    ops.tune(strips=4, unroll=0, nt=0, fastdiv=1, lanetab=0, grid=0, block=256)
     # K = 8 (BASELINE config 2) and bf16 inputs
     med, _ = timed(lambda: ops.fedavg_fold(agg, ups[:8], ns[:8], Ns[:8], init=True))
     b8 = 8 * P * 4 + P * 4
