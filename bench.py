@@ -102,10 +102,16 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
-    device = torch.device("cuda", local)
+    # FEDN_AMD_BENCH_ONE_GPU=1: rehearsal of the N>1 code path on a one-GPU box (every rank on
+    # cuda:0, gloo instead of RCCL); never used for reported numbers
+    rehearsal = os.environ.get("FEDN_AMD_BENCH_ONE_GPU") == "1"
+    device = torch.device("cuda", 0 if rehearsal else local)
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     from fedn_amd import _abi, ops
     from fedn_amd.sharded import ShardedFedAvg
@@ -140,7 +146,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(s.elapsed_time(e) for s, e in ev) / a.steps
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cpu" if rehearsal else device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms = float(t[0]), float(t[1])
@@ -152,24 +158,27 @@ def main():
 
     allgather = None
     if world > 1 and not a.no_allgather:
+        gather_src = agg.cpu() if rehearsal else agg
         for _ in range(2):
-            full = sh.allgather(agg)
+            full = sh.allgather(gather_src)
         del full
         torch.cuda.synchronize(device)
         dist.barrier()
         t1 = time.perf_counter()
         reps = 5
         for _ in range(reps):
-            full = sh.allgather(agg)
+            full = sh.allgather(gather_src)
             del full
         torch.cuda.synchronize(device)
-        ag = torch.tensor([(time.perf_counter() - t1) / reps], dtype=torch.float64, device=device)
+        ag = torch.tensor([(time.perf_counter() - t1) / reps], dtype=torch.float64,
+                          device="cpu" if rehearsal else device)
         dist.all_reduce(ag, op=dist.ReduceOp.MAX)
         ag_s = float(ag[0])
         nbytes = sh.shard * world * 4
         allgather = {"ms": ag_s * 1e3, "bytes_in_per_rank": sh.shard * (world - 1) * 4,
                      "algbw_GBps": nbytes / ag_s / 1e9, "busbw_GBps": nbytes * (world - 1) / world / ag_s / 1e9,
-                     "backend": "rccl", "note": "reassembles the world*params model on every GPU; not in value"}
+                     "backend": "gloo (rehearsal)" if rehearsal else "rccl",
+                     "note": "reassembles the world*params model on every GPU; not in value"}
 
     base = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
@@ -181,7 +190,7 @@ def main():
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
             "data": "synthetic: base~N(0,1), client=base+0.01*N(0,1), num_examples~U{1..5000}, device-resident",
-            "config": {"workload": f"FedAvg {K} clients x {P} params {a.dtype} per GPU (BASELINE configs[1]/north "
+            "config": {"workload": f"FedAvg {K} clients x {a.params} params {a.dtype} per GPU (BASELINE configs[1]/north "
                                    "star; device-resident, one fused fold launch per aggregation)",
                        "clients": K, "params_per_gpu": a.params, "global_params": P_total,
                        "parallelism": f"param-slice shards x{world}, no data-path collective"},

@@ -24,6 +24,20 @@ from .aggregatorbase import AggregatorBase
 logger = logging.getLogger("fedn")
 
 
+def env_devices():
+    """FEDN_AMD_DEVICES="cuda:0,cuda:1,..." selects the single-process multi-GPU pipeline."""
+    v = os.environ.get("FEDN_AMD_DEVICES")
+    return [d.strip() for d in v.split(",") if d.strip()] if v else None
+
+
+def make_fedavg_pipeline(first, device=None, devices=None):
+    devices = devices or env_devices()
+    if devices and len(devices) > 1:
+        from ..multidev import ShardedFedAvgPipeline
+        return ShardedFedAvgPipeline(devices, first)
+    return FedAvgPipeline(device or (devices[0] if devices else None) or default_device(), first)
+
+
 def default_device():
     dev = os.environ.get("FEDN_AMD_DEVICE")
     if dev:
@@ -36,10 +50,11 @@ def default_device():
 class Aggregator(AggregatorBase):
     """Federated Averaging on MI355X (weighted incremental mean of client updates)."""
 
-    def __init__(self, update_handler, device=None):
+    def __init__(self, update_handler, device=None, devices=None):
         super().__init__(update_handler)
         self.name = "fedavg"
         self.device = torch.device(device) if device is not None else None
+        self.devices = devices   # several devices: parameter-slice sharding in this process (multidev.py)
 
     def combine_models(self, helper=None, delete_models=True, parameters=None):
         data = {"time_model_load": 0.0, "time_model_aggregation": 0.0}
@@ -60,7 +75,7 @@ class Aggregator(AggregatorBase):
 
                 tic = time.time()
                 if nr_aggregated_models == 0:
-                    pipe = FedAvgPipeline(self.device or default_device(), model_next)
+                    pipe = make_fedavg_pipeline(model_next, self.device, self.devices)
                 else:
                     pipe.add(model_next, metadata["num_examples"], total_examples)
                 data["time_model_aggregation"] += time.time() - tic

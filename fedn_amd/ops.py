@@ -114,10 +114,10 @@ def fedavg_fold(agg, updates, n, N, init, stream=None):
         _check_dev(f"updates[{i}]", u, P, dev)
         if u.dtype != upd_dt:
             raise TypeError("all updates in one fold call must share a dtype")
-    with torch.cuda.device(dev):
+    with torch.cuda.device(dev):        # launch on the tensors' device (multi-GPU processes)
         st = _stream_handle(agg, stream)
-    rc = lib.fa_fedavg_fold(agg.data_ptr(), fa_dtype(agg), _abi.ptr_array([u.data_ptr() for u in updates]),
-                            fa_dtype(upd_dt), _abi.double_array(n), _abi.double_array(N), K, P, int(bool(init)), st)
+        rc = lib.fa_fedavg_fold(agg.data_ptr(), fa_dtype(agg), _abi.ptr_array([u.data_ptr() for u in updates]),
+                                fa_dtype(upd_dt), _abi.double_array(n), _abi.double_array(N), K, P, int(bool(init)), st)
     _abi.check(rc)
     return agg
 
@@ -176,12 +176,12 @@ def fedopt_step(old, updates, n, N, *, first, final, pg=None, m_in=None, m_out=N
     ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
     with torch.cuda.device(dev):
         st = _stream_handle(old, stream)
-    rc = lib.fa_fedopt_step(
-        old.data_ptr(), fa_dtype(old), _abi.ptr_array([u.data_ptr() for u in updates]), fa_dtype(upd_dt),
-        _abi.double_array(n), _abi.double_array(N), K, ptr(pg), flags,
-        ptr(m_in), _abi.FA_NONE if m_in is None else fa_dtype(m_in), ptr(m_out),
-        ptr(v_in), ptr(v_out), ptr(out), _OPTS[serveropt], float(learning_rate), float(beta1), float(beta2),
-        float(tau), P, st)
+        rc = lib.fa_fedopt_step(
+            old.data_ptr(), fa_dtype(old), _abi.ptr_array([u.data_ptr() for u in updates]), fa_dtype(upd_dt),
+            _abi.double_array(n), _abi.double_array(N), K, ptr(pg), flags,
+            ptr(m_in), _abi.FA_NONE if m_in is None else fa_dtype(m_in), ptr(m_out),
+            ptr(v_in), ptr(v_out), ptr(out), _OPTS[serveropt], float(learning_rate), float(beta1), float(beta2),
+            float(tau), P, st)
     _abi.check(rc)
 
 

@@ -85,6 +85,9 @@ class _Pipeline:
         if isinstance(arrays, StagedModel):
             self.layout.check_layout(arrays.layout)      # raises the numpy-like error
             self.compute.wait_event(arrays.ready)
+            if arrays.dev.device != self.device:         # staged on another GPU: one D2D copy
+                arrays = StagedModel(arrays.layout, arrays.dev.to(self.device, non_blocking=True),
+                                     arrays.ready, None)
             self._hold.append(arrays)                    # keep HBM alive until the round ends
             return arrays
         self.layout.check(arrays)
