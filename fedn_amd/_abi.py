@@ -22,6 +22,7 @@ FA_OK, FA_EINVAL, FA_EDTYPE, FA_EHIP = 0, 1, 2, 3
 # server optimizers (enum fa_serveropt)
 FA_ADAM, FA_YOGI, FA_ADAGRAD = 0, 1, 2
 FA_PG_FIRST, FA_PG_FINAL = 1, 2
+FA_EW_AXPBY, FA_EW_MUL, FA_EW_DIV, FA_EW_SQRT, FA_EW_SQUARE, FA_EW_SIGN, FA_EW_FILL = 0, 1, 2, 3, 4, 5, 6
 (FA_TUNE_STRIPS, FA_TUNE_UNROLL, FA_TUNE_NT, FA_TUNE_FASTDIV, FA_TUNE_LANETAB, FA_TUNE_GRID, FA_TUNE_READ,
  FA_TUNE_BLOCK) = 0, 1, 2, 3, 4, 5, 6, 7
 
@@ -47,6 +48,9 @@ EXPORTS = {
     "fa_tune": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "fa_stream_sum": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int64,
                                      ctypes.c_void_p]),
+    "fa_elementwise": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int64,
+                                      ctypes.c_void_p]),
     "fa_stream_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "fa_stream_read_blocks": (ctypes.c_int64, [ctypes.c_int64]),
     "fa_stream_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),

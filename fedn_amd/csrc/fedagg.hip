@@ -646,6 +646,52 @@ k_fedopt(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::
 }
 
 // ----------------------------------------------------------------------------
+// numpyhelper primitives (numpyhelper.py:34-142) as elementwise kernels, numpy rounding:
+// every product/quotient in its operand's dtype (python floats are weak scalars), the
+// final combination in the promoted dtype.
+// ----------------------------------------------------------------------------
+template <typename T> __device__ __forceinline__ T as_t(double v) { return (T)v; }
+
+template <typename TX, typename TY, typename TO>
+__global__ void __launch_bounds__(kBlock)
+k_elementwise(int op, TO* __restrict__ out, const TX* __restrict__ x, const TY* __restrict__ y, double a, double b,
+              int64_t P) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < P; i += (int64_t)gridDim.x * kBlock) {
+        TO r;
+        switch (op) {
+            case FA_EW_AXPBY: {                                   // x*a + y*b   (numpyhelper.add)
+                const TX xa = x[i] * as_t<TX>(a);
+                const TY yb = y[i] * as_t<TY>(b);
+                r = (TO)xa + (TO)yb;
+                break;
+            }
+            case FA_EW_MUL:                                       // numpyhelper.multiply
+                r = y ? (TO)x[i] * (TO)y[i] : (TO)(x[i] * as_t<TX>(a));
+                break;
+            case FA_EW_DIV:                                       // numpyhelper.divide
+                r = y ? (TO)x[i] / (TO)y[i] : (TO)(x[i] / as_t<TX>(a));
+                break;
+            case FA_EW_SQRT:                                      // numpyhelper.sqrt
+                r = (TO)__builtin_sqrt((double)x[i]);
+                if constexpr (std::is_same<TX, float>::value) r = (TO)__builtin_sqrtf(x[i]);
+                break;
+            case FA_EW_SQUARE:                                    // numpyhelper.power(m, 2)
+                r = (TO)(x[i] * x[i]);
+                break;
+            case FA_EW_SIGN: {                                    // numpyhelper.sign
+                const TX v = x[i];
+                r = v > (TX)0 ? (TO)1 : (v < (TX)0 ? (TO)-1 : (v == (TX)0 ? (TO)0 : (TO)v));
+                break;
+            }
+            default:                                              // FA_EW_FILL: np.ones(shape) * a
+                r = (TO)(1.0 * a);
+                break;
+        }
+        out[i] = r;
+    }
+}
+
+// ----------------------------------------------------------------------------
 // measurement kernels
 // ----------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) k_stream_copy(u32x4* __restrict__ dst, const u32x4* __restrict__ src, int64_t n16) {
@@ -1010,6 +1056,36 @@ int fa_stream_sum(float* out, const float* const* bufs, int K, int64_t P, void* 
     fill_table<float>(tab, reinterpret_cast<const void* const*>(bufs), ones.data(), ones.data(), 0, K);
     launch_fedavg_pipe<float, float, CADD, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
     return check_launch("fa_stream_sum");
+}
+
+int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype, const void* y, int y_dtype,
+                   double a, double b, int64_t P, void* stream) {
+    g_err[0] = 0;
+    if (P < 0 || !out || (op != FA_EW_FILL && !x)) return fail(FA_EINVAL, "fa_elementwise: bad arguments");
+    if (op < FA_EW_AXPBY || op > FA_EW_FILL) return fail(FA_EINVAL, "fa_elementwise: unknown op %d", op);
+    if (op == FA_EW_AXPBY && !y) return fail(FA_EINVAL, "fa_elementwise: AXPBY needs y");
+    if (P == 0) return FA_OK;
+    auto isf = [](int d) { return d == FA_F32 || d == FA_F64; };
+    if (op == FA_EW_FILL) x_dtype = out_dtype;
+    if (!y) y_dtype = x_dtype;
+    if (!isf(out_dtype) || !isf(x_dtype) || !isf(y_dtype)) return fail(FA_EDTYPE, "fa_elementwise: f32/f64 only");
+    const int want = (op == FA_EW_FILL) ? out_dtype
+                     : (op == FA_EW_AXPBY || ((op == FA_EW_MUL || op == FA_EW_DIV) && y)) ? fa_promote(x_dtype, y_dtype)
+                     : x_dtype;
+    if (out_dtype != want) return fail(FA_EDTYPE, "fa_elementwise: output dtype must be %d", want);
+    const dim3 grid((unsigned)std::min<int64_t>((P + kBlock - 1) / kBlock, 8192));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+#define FA_EW(TX, TY, TO) \
+    hipLaunchKernelGGL((k_elementwise<TX, TY, TO>), grid, dim3(kBlock), 0, st, op, static_cast<TO*>(out), \
+                       static_cast<const TX*>(x), static_cast<const TY*>(y), a, b, P)
+    const bool x32 = x_dtype == FA_F32, y32 = y_dtype == FA_F32, o32 = out_dtype == FA_F32;
+    if (x32 && y32 && o32) FA_EW(float, float, float);
+    else if (x32 && y32) FA_EW(float, float, double);
+    else if (x32) FA_EW(float, double, double);
+    else if (y32) FA_EW(double, float, double);
+    else FA_EW(double, double, double);
+#undef FA_EW
+    return check_launch("fa_elementwise");
 }
 
 int fa_stream_copy(void* dst, const void* src, int64_t bytes, void* stream) {

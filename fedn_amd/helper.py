@@ -7,10 +7,15 @@ FEDn's ``HelperBase`` requires (helperbase.py:4-40) plus its file-type API:
                                               output readable by np.load
   load(path, file_type="npz")                 numpyhelper.py:171-189: native inflate (parallel
                                               for archives this codec wrote); raw_binary as FEDn
+  add / subtract / multiply / divide / sqrt / power(., 2) / sign / ones
+                                              numpyhelper.py:34-142 on the GPU (fa_elementwise),
+                                              numpy's dtype promotion and rounding, so FEDn's
+                                              stock fedopt.py runs unchanged on this helper
+Inputs may be numpy arrays (results come back as numpy arrays, like numpyhelper) or device
+tensors (results stay on the device, so chains of primitives never leave HBM).
+``norm`` (numpyhelper.py:106-117, unused by the aggregators) is not provided.
 FEDn selects helpers by module name (helpers.py:7-17); install with a shim module
-``fedn/utils/helpers/plugins/fednamdhelper.py``. The server-optimizer
-primitives (add, subtract, ...) are not provided: fedn_amd's fedopt plug-in fuses them on
-the GPU and never calls the helper for arithmetic.
+``fedn/utils/helpers/plugins/fednamdhelper.py`` (INTEGRATION.md).
 """
 import os
 import tempfile
@@ -19,6 +24,26 @@ from io import BytesIO
 import numpy as np
 
 from . import codec
+
+
+def _device():
+    from .aggregators.fedavg import default_device
+    return default_device()
+
+
+def _to_dev(x, dev):
+    """(device tensor, came_from_numpy)"""
+    import torch
+    if isinstance(x, torch.Tensor):
+        return x.contiguous(), False
+    a = np.ascontiguousarray(x)
+    if a.dtype not in (np.float32, np.float64):
+        raise TypeError(f"fednamdhelper primitives support float32/float64 arrays, got {a.dtype}")
+    return torch.from_numpy(a).to(dev), True
+
+
+def _back(t, host, shape):
+    return t.to("cpu").numpy().reshape(shape) if host else t.reshape(shape)
 
 
 class Helper:
@@ -33,6 +58,69 @@ class Helper:
         pipe = FedAvgPipeline(default_device(), list(m1))
         pipe.add(list(m2), n, N)
         return pipe.result()
+
+    # ---- numpyhelper primitives on the GPU (numpyhelper.py:34-142) ----------------------------
+    def _ew(self, op, m1, m2=None, a=0.0, b=0.0):
+        import torch
+
+        from . import ops
+        dev = _device()
+        out = []
+        for i, x in enumerate(m1):
+            shape = tuple(x.shape)
+            xd, host = _to_dev(x, dev)
+            xd = xd.reshape(-1)
+            y = None if m2 is None else m2[i]
+            yd = None
+            if isinstance(y, np.generic):          # numpy scalars (0-d results) are arrays here
+                y = np.asarray(y)
+            if y is not None and not isinstance(y, (int, float)):
+                if tuple(y.shape) != shape:
+                    raise ValueError(f"operands could not be broadcast together with shapes {shape} {tuple(y.shape)}")
+                yd, yhost = _to_dev(y, dev)
+                yd = yd.reshape(-1)
+                host = host or yhost
+            elif y is not None:
+                a = float(y)                     # multiply/divide by a python scalar (weak)
+            if op == "fill":
+                odt = torch.float64
+            elif op == "axpby" or (op in ("mul", "div") and yd is not None):
+                odt = ops.promote(xd.dtype, yd.dtype)
+            else:
+                odt = xd.dtype
+            o = torch.empty(xd.numel(), dtype=odt, device=dev)
+            ops.elementwise(op, o, xd, yd, a, b)
+            out.append(_back(o, host, shape))
+        return out
+
+    def add(self, m1, m2, a=1.0, b=1.0):
+        """m1*a + m2*b (numpyhelper.py:34-44)."""
+        return self._ew("axpby", m1, m2, a, b)
+
+    def subtract(self, m1, m2, a=1.0, b=1.0):
+        """m1*a - m2*b (numpyhelper.py:46-56)."""
+        return self.add(m1, m2, a, -b)
+
+    def divide(self, m1, m2):
+        return self._ew("div", m1, m2)
+
+    def multiply(self, m1, m2):
+        return self._ew("mul", m1, m2)
+
+    def sqrt(self, m1):
+        return self._ew("sqrt", m1)
+
+    def power(self, m1, a):
+        if a != 2:
+            raise NotImplementedError("fednamdhelper.power supports the exponent 2 (numpy's square path)")
+        return self._ew("square", m1)
+
+    def sign(self, m1):
+        return self._ew("sign", m1)
+
+    def ones(self, m1, a):
+        """np.ones(shape) * a: float64 (numpyhelper.py:129-142)."""
+        return self._ew("fill", m1, None, a)
 
     def save(self, weights, path=None, file_type="npz"):
         self.check_supported_file_type(file_type)

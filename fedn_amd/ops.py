@@ -222,3 +222,24 @@ def tune(**knobs):
     lib = _abi.load()
     for k, v in knobs.items():
         _abi.check(lib.fa_tune(_KNOBS[k], int(v)))
+
+
+_EW = {"axpby": _abi.FA_EW_AXPBY, "mul": _abi.FA_EW_MUL, "div": _abi.FA_EW_DIV, "sqrt": _abi.FA_EW_SQRT,
+       "square": _abi.FA_EW_SQUARE, "sign": _abi.FA_EW_SIGN, "fill": _abi.FA_EW_FILL}
+
+
+def elementwise(op, out, x=None, y=None, a=0.0, b=0.0, stream=None):
+    """numpyhelper primitive on device tensors (``fa_elementwise``); see include/fedagg.h."""
+    lib = _abi.load()
+    P = out.numel()
+    _check_dev("out", out, P, None)
+    for name, t in (("x", x), ("y", y)):
+        if t is not None:
+            _check_dev(name, t, P, out.device)
+    with torch.cuda.device(out.device):
+        st = _stream_handle(out, stream)
+        rc = lib.fa_elementwise(_EW[op], out.data_ptr(), fa_dtype(out), 0 if x is None else x.data_ptr(),
+                                fa_dtype(out) if x is None else fa_dtype(x), 0 if y is None else y.data_ptr(),
+                                _abi.FA_NONE if y is None else fa_dtype(y), float(a), float(b), P, st)
+    _abi.check(rc)
+    return out

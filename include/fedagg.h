@@ -119,6 +119,23 @@ int fa_fedopt_step(const void* old, int old_dtype,
                    int serveropt, double lr, double beta1, double beta2, double tau,
                    int64_t P, void* stream);
 
+/*
+ * numpyhelper primitives (numpyhelper.py:34-142) on device buffers, numpy rounding (python
+ * scalars a, b are weak: x*a is computed in x's dtype, then promoted). F32 / F64 only.
+ *   FA_EW_AXPBY   out = x*a + y*b                 numpyhelper.add / subtract (b -> -b)
+ *   FA_EW_MUL     out = x*y, or x*a if y == NULL   numpyhelper.multiply
+ *   FA_EW_DIV     out = x/y, or x/a if y == NULL   numpyhelper.divide
+ *   FA_EW_SQRT    out = sqrt(x)                    numpyhelper.sqrt
+ *   FA_EW_SQUARE  out = x*x                        numpyhelper.power(m, 2)
+ *   FA_EW_SIGN    out = sign(x) (+-1, 0, NaN)      numpyhelper.sign
+ *   FA_EW_FILL    out = 1.0*a (x unused)           numpyhelper.ones
+ * out_dtype must be the numpy result dtype of the op.
+ */
+enum fa_ew_op { FA_EW_AXPBY = 0, FA_EW_MUL = 1, FA_EW_DIV = 2, FA_EW_SQRT = 3, FA_EW_SQUARE = 4, FA_EW_SIGN = 5,
+                FA_EW_FILL = 6 };
+int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype, const void* y, int y_dtype,
+                   double a, double b, int64_t P, void* stream);
+
 /* dtype promotion used by the two entry points above (numpy result_type for the
  * pairs this library supports; bf16 promotes as f32). Returns FA_NONE if unsupported. */
 int fa_promote(int a, int b);

@@ -370,3 +370,61 @@ def test_multidevice_large_flat():
         total += n
         pipe.add([u], n, total)
     assert_lists_identical(pipe.result(), [want], "multidev flat")
+
+
+# ------------------------------------------------------------------------- helper primitives on the GPU
+def test_helper_primitives_golden():
+    """fedn_amd.helper.Helper primitives vs the REAL numpyhelper outputs (helper_ops fixture)."""
+    from fedn_amd.helper import Helper
+    h = Helper()
+    c = load_case("helper_ops")["raw"]
+    x32, y32, x64 = c["x32"], c["y32"], c["x64"]
+    got = {
+        "add_32_32": h.add([x32], [y32], 0.9, 0.1)[0],
+        "add_64_32": h.add([x64], [y32], 0.99, 1.0 - 0.99)[0],
+        "sub_32_64": h.subtract([x32], [x64])[0],
+        "mul_32_s": h.multiply([x32], [1.0 - 0.9])[0],
+        "pow_32": h.power([x32], 2)[0],
+        "sqrt_64": h.sqrt([np.abs(x64)])[0],
+        "div_32_64": h.divide([x32], [np.abs(x64) + 1.0])[0],
+        "sign_64": h.sign([np.concatenate([x64, [0.0, -0.0]])])[0],
+        "ones_32": h.ones([x32], 1e-4 ** 2)[0],
+    }
+    for k, v in got.items():
+        assert_lists_identical([v], [c[k]], k)
+
+
+@pytest.mark.parametrize("name", ["fedopt_adam_3r", "fedopt_yogi_3r", "fedopt_adagrad_3r"])
+def test_stock_fedopt_server_step_on_gpu_helper(name):
+    """FEDn's stock serveropt_* (fedopt.py:151-258), written against the helper API, run with
+    fedn_amd.helper.Helper: the pseudo-gradient from the oracle, the server step on the GPU."""
+    import math
+    from fedn_amd.helper import Helper
+    h = Helper()
+    case = load_case(name)
+    opt = (case["params"] or {}).get("serveropt", "adam")
+    b1, b2, lr, tau = 0.9, 0.99, 1e-3, 1e-4
+    m = v = None
+    for r, rd in enumerate(case["rounds"]):
+        pg, nr, total = None, 0, 0
+        for arrays, n in rd["updates"]:              # fedopt.py:86-94
+            total += n
+            pg = ref.subtract(arrays, rd["old"]) if nr == 0 else ref.increment_average(
+                pg, ref.subtract(arrays, rd["old"]), n, total)
+            nr += 1
+        if v is None:
+            v = h.ones(pg, math.pow(tau, 2))
+        m = h.multiply(pg, [(1.0 - b1)] * len(pg)) if m is None else h.add(m, pg, b1, (1.0 - b1))
+        p = h.power(pg, 2)
+        if opt == "adam":
+            v = h.add(v, p, b2, (1.0 - b2))
+        elif opt == "yogi":
+            s = h.multiply(h.sign(h.add(v, p, 1.0, -1.0)), p)
+            v = h.add(v, s, 1.0, -(1.0 - b2))
+        else:
+            v = h.add(v, p, 1.0, 1.0)
+        sv = h.add(h.sqrt(v), h.ones(v, tau))
+        model = h.add(rd["old"], h.divide(m, sv), 1.0, lr)
+        assert_lists_identical(model, rd["out"], f"{name} r{r}")
+        assert_lists_identical(m, rd["m"], f"{name} r{r} m")
+        assert_lists_identical(v, rd["v"], f"{name} r{r} v")
