@@ -972,10 +972,15 @@ int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, i
     if ((!first || !final_ || K > kMaxK) && !pg) return fail(FA_EINVAL, "fa_fedopt_step: pg workspace required");
     if (final_ && (!m_out || !v_out || !out)) return fail(FA_EINVAL, "fa_fedopt_step: null output buffer");
     if (serveropt < FA_ADAM || serveropt > FA_ADAGRAD) return fail(FA_EINVAL, "fa_fedopt_step: unsupported serveropt %d", serveropt);
-    if (old_dtype != FA_F32 && old_dtype != FA_F64) return fail(FA_EDTYPE, "fa_fedopt_step: old dtype %d", old_dtype);
-    if (upd_dtype != FA_F32 && upd_dtype != FA_F64 && upd_dtype != FA_BF16)
+    auto is_int = [](int d) { return d == FA_I32 || d == FA_I64; };
+    if (old_dtype != FA_F32 && old_dtype != FA_F64 && !is_int(old_dtype))
+        return fail(FA_EDTYPE, "fa_fedopt_step: old dtype %d", old_dtype);
+    if (upd_dtype != FA_F32 && upd_dtype != FA_F64 && upd_dtype != FA_BF16 && !is_int(upd_dtype))
         return fail(FA_EDTYPE, "fa_fedopt_step: update dtype %d", upd_dtype);
-    const int pg_dt = fa_promote(upd_dtype, old_dtype);
+    if (is_int(old_dtype) && !is_int(upd_dtype))
+        return fail(FA_EDTYPE, "fa_fedopt_step: integer global model with float updates is unsupported");
+    // integer tensors: subtract = next*1.0 + old*(-1.0) turns them into float64 (numpy: int * python float)
+    const int pg_dt = is_int(upd_dtype) ? FA_F64 : fa_promote(upd_dtype, old_dtype);
     if (m_in && m_in_dtype != FA_F32 && m_in_dtype != FA_F64) return fail(FA_EDTYPE, "fa_fedopt_step: m dtype %d", m_in_dtype);
     if (!m_in) m_in_dtype = FA_NONE;
     const int m_out_dt = fa_promote(m_in_dtype, pg_dt);
@@ -1003,6 +1008,12 @@ int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, i
     if (upd_dtype == FA_F64 && old_dtype == FA_F64) return launch_fedopt<double, double, CF64>(b, s, updates, n, N, K, P, flags, st);
     if (upd_dtype == FA_BF16 && old_dtype == FA_F64) return launch_fedopt<bf16, double, CF64>(b, s, updates, n, N, K, P, flags, st);
     if (upd_dtype == FA_F64 && old_dtype == FA_F32) return launch_fedopt<double, float, CF64>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_I64 && old_dtype == FA_I64) return launch_fedopt<int64_t, int64_t, CF64>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_I64 && old_dtype == FA_F64) return launch_fedopt<int64_t, double, CF64>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_I64 && old_dtype == FA_F32) return launch_fedopt<int64_t, float, CF64>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_I32 && old_dtype == FA_I32) return launch_fedopt<int32_t, int32_t, CF64>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_I32 && old_dtype == FA_F64) return launch_fedopt<int32_t, double, CF64>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_I32 && old_dtype == FA_F32) return launch_fedopt<int32_t, float, CF64>(b, s, updates, n, N, K, P, flags, st);
     return fail(FA_EDTYPE, "fa_fedopt_step: unsupported dtype pair (update %d, old %d)", upd_dtype, old_dtype);
 }
 

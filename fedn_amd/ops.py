@@ -141,8 +141,9 @@ def promote(a, b):
 
 
 def fedopt_dtypes(upd_dt, old_dt, m_dt):
-    """(pg dtype, m_out dtype) for fedopt.py's expressions; v and out are always f64."""
-    pg = promote(upd_dt, old_dt)
+    """(pg dtype, m_out dtype) for fedopt.py's expressions; v and out are always f64.
+    Integer updates: ``next*1.0 + old*(-1.0)`` is float64 in numpy (int array * python float)."""
+    pg = torch.float64 if upd_dt in (torch.int32, torch.int64) else promote(upd_dt, old_dt)
     return pg, promote(m_dt, pg)
 
 

@@ -252,8 +252,8 @@ class FedOptPipeline(_Pipeline):
         else:
             self.layout.check(arrays)
         for dt in self.layout.groups:
-            if ops.torch_dtype(dt) not in (torch.float32, torch.float64):
-                raise TypeError(f"FedOpt supports float32/float64 updates, got {dt}")
+            if ops.torch_dtype(dt) not in (torch.float32, torch.float64, torch.int32, torch.int64):
+                raise TypeError(f"FedOpt supports float32/float64/int32/int64 updates, got {dt}")
         slot = self.acquire(arrays)
         span = self._kernel_span()
         first = self.nfolds == 0

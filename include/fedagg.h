@@ -95,11 +95,13 @@ int fa_fedavg_fold(void* agg, int agg_dtype,
  * FedOpt (fedopt.py:74-118, 151-258), fused: pseudo-gradient running mean over the
  * K updates followed (FA_PG_FINAL) by one Adam / Yogi / AdaGrad server step.
  *
- * old       device, P elements of old_dtype (F32 | F64): the global model the
+ * old       device, P elements of old_dtype (F32 | F64 | I32 | I64): the global model the
  *           clients trained from (fedopt.py:90)
- * updates   HOST array of K DEVICE pointers (F32 | BF16 | F64)
+ * updates   HOST array of K DEVICE pointers (F32 | BF16 | F64 | I32 | I64); integer tensors
+ *           (e.g. BatchNorm counters) become float64 exactly as numpy's int * 1.0 does
  * n, N      HOST arrays of K doubles (num_examples, running total)
- * pg        device workspace, P elements of pg dtype = promote(upd, old); read when
+ * pg        device workspace, P elements of pg dtype = promote(upd, old) (F64 for integer
+ *           updates); read when
  *           !FA_PG_FIRST, written when !FA_PG_FINAL (and used internally when
  *           K exceeds one launch); may be NULL when FIRST|FINAL and K <= 64
  * m_in      device, P elements of m_in_dtype, or NULL with m_in_dtype = FA_NONE

@@ -107,6 +107,28 @@ ODD_SHAPES = [(7,), (3, 5, 11), (1,), (129, 3), ()]
 MNIST_SHAPES = [(64, 784), (64,), (32, 64), (32,), (10, 32), (10,)]  # examples/mnist-pytorch/client/model.py:18-32
 
 
+def fedavg_mixed_case(ref, name, rng, nks):
+    """A model with float32 weights and int64 counters (BatchNorm-like), folded by FedAvg."""
+    h = Harness(ref, "fedavg")
+    d = {"kind": np.array("fedavg"), "name": np.array(name)}
+    base = _rng_model(rng, [(16, 3), (3,)], np.float64)
+    for k, n in enumerate(nks):
+        u = _perturb(rng, base, np.float32) + [np.array(1000 + 37 * k, dtype=np.int64),
+                                               (np.arange(4) * (k + 3)).astype(np.int64)]
+        h.push_update(u, int(n), "global-0")
+        _store_list(d, f"r0_u{k}", u)
+    d["r0_n"] = np.array(nks, dtype=np.int64)
+    d["r0_K"] = np.array(len(nks))
+    model, data = h.combine()
+    d["r0_nr"] = np.array(data["nr_aggregated_models"])
+    d["r0_data_keys"] = np.array(json.dumps(sorted(data)))
+    d["r0_qsize"] = np.array(h.uh.model_updates.qsize())
+    d["r0_out_none"] = np.array(model is None)
+    _store_list(d, "r0_out", model)
+    d["rounds"] = np.array(1)
+    return d
+
+
 def fedavg_case(ref, name, rng, shapes, dtype, nks, bad_index=None, special=None, int_vals=False):
     h = Harness(ref, "fedavg")
     d = {"kind": np.array("fedavg"), "name": np.array(name)}
@@ -144,17 +166,29 @@ def fedavg_case(ref, name, rng, shapes, dtype, nks, bad_index=None, special=None
     return d
 
 
-def fedopt_case(ref, name, rng, shapes, nks_per_round, params=None, old_dtype=np.float32, upd_dtype=np.float32):
+def _mixed_model(rng, old):
+    """float32 weights + an int64 counter (like BatchNorm's num_batches_tracked)."""
+    return [old[0], np.asarray(old[1])]
+
+
+def fedopt_case(ref, name, rng, shapes, nks_per_round, params=None, old_dtype=np.float32, upd_dtype=np.float32,
+                int_tensor=False):
     h = Harness(ref, "fedopt")
     d = {"kind": np.array("fedopt"), "name": np.array(name)}
     d["params"] = np.array(json.dumps(params if params is not None else None))
     old = _rng_model(rng, shapes, old_dtype)
+    if int_tensor:
+        old = old + [np.array(100, dtype=np.int64), np.arange(5, dtype=np.int64)]
     for r, nks in enumerate(nks_per_round):
         gid = f"global-{r}"
         h.put_model(old, gid)
         _store_list(d, f"r{r}_old", old)
         for k, n in enumerate(nks):
-            u = _perturb(rng, old, upd_dtype)
+            if int_tensor:
+                u = _perturb(rng, old[:-2], upd_dtype) + [np.array(100 + 10 * (r + 1) + k, dtype=np.int64),
+                                                         (np.arange(5) * (k + 2) + r).astype(np.int64)]
+            else:
+                u = _perturb(rng, old, upd_dtype)
             h.push_update(u, int(n), gid)
             _store_list(d, f"r{r}_u{k}", u)
         d[f"r{r}_n"] = np.array(nks, dtype=np.int64)
@@ -273,9 +307,16 @@ def main():
     cases.append(fedopt_case(ref, "fedopt_adam_k1", rng, ODD_SHAPES, [[17], [4000]]))
     cases.append(fedopt_case(ref, "fedopt_adam_f64old", rng, ODD_SHAPES, [list(rng.integers(1, 5001, 4))],
                              None, old_dtype=np.float64))
+    cases.append(fedopt_case(ref, "fedopt_adam_int_tensors", rng, [(7,), (3, 4)], [[5, 9, 2], [4, 4]], None,
+                             int_tensor=True))
+    cases.append(fedopt_case(ref, "fedopt_yogi_int_tensors", rng, [(7,), (3, 4)], [[5, 9], [3]], {"serveropt": "yogi"},
+                             int_tensor=True))
     cases.append(fedopt_case(ref, "fedopt_badparam_int_lr", rng, ODD_SHAPES, [[10, 20]], {"learning_rate": 1}))
     cases.append(fedopt_case(ref, "fedopt_badparam_key", rng, ODD_SHAPES, [[10, 20]], {"momentum": 0.5}))
     cases.append(fedopt_case(ref, "fedopt_badopt", rng, ODD_SHAPES, [[10, 20]], {"serveropt": "sgd"}))
+
+    rng = np.random.default_rng(5)
+    cases.append(fedavg_mixed_case(ref, "fedavg_mixed_int_k5", rng, rng.integers(1, 5001, 5)))
 
     # Control.reduce -------------------------------------------------------------------
     rng = np.random.default_rng(4)
