@@ -148,8 +148,12 @@ def fedopt_dtypes(upd_dt, old_dt, m_dt):
 
 
 def fedopt_step(old, updates, n, N, *, first, final, pg=None, m_in=None, m_out=None, v_in=None, v_out=None,
-                out=None, serveropt="adam", learning_rate=1e-3, beta1=0.9, beta2=0.99, tau=1e-4, stream=None):
-    """Fused FedOpt step on device (``fa_fedopt_step``), fedopt.py:74-118 + 151-258."""
+                out=None, serveropt="adam", learning_rate=1e-3, beta1=0.9, beta2=0.99, tau=1e-4, stream=None,
+                upd_dtype=None):
+    """Fused FedOpt step on device (``fa_fedopt_step``), fedopt.py:74-118 + 151-258.
+
+    ``upd_dtype``: dtype of the round's client updates; required when ``updates`` is empty
+    (a server step on an accumulated ``pg``), because it fixes the pseudo-gradient dtype."""
     lib = _abi.load()
     if serveropt not in _OPTS:
         raise ValueError(f"Unsupported server optimizer: {serveropt}")
@@ -157,11 +161,21 @@ def fedopt_step(old, updates, n, N, *, first, final, pg=None, m_in=None, m_out=N
     P = old.numel()
     dev = old.device
     _check_dev("old", old, P, None)
-    upd_dt = updates[0].dtype if K else old.dtype
+    if K:
+        upd_dt = updates[0].dtype
+    elif upd_dtype is not None:
+        upd_dt = upd_dtype
+    elif pg is not None and pg.dtype == torch.float64 and old.dtype != torch.float64:
+        raise ValueError("fedopt_step without updates needs upd_dtype (pg is float64, old is not)")
+    else:
+        upd_dt = pg.dtype if pg is not None else old.dtype
     for i, u in enumerate(updates):
         _check_dev(f"updates[{i}]", u, P, dev)
         if u.dtype != upd_dt:
             raise TypeError("all updates in one call must share a dtype")
+    if pg is not None and pg.dtype != fedopt_dtypes(upd_dt, old.dtype, None)[0]:
+        raise TypeError(f"pg must be {fedopt_dtypes(upd_dt, old.dtype, None)[0]} for {upd_dt} updates over a "
+                        f"{old.dtype} model")
     for name, t in (("pg", pg), ("m_in", m_in), ("m_out", m_out), ("v_in", v_in), ("v_out", v_out), ("out", out)):
         if t is not None:
             _check_dev(name, t, P, dev)

@@ -283,14 +283,15 @@ class FedOptPipeline(_Pipeline):
             old, pg = self.old[dt], self.pg[dt]
             m_in = state.m[dt] if state.m is not None else None
             v_in = state.v[dt] if state.v is not None else None
-            _, m_dt = ops.fedopt_dtypes(pg.dtype, old.dtype, None if m_in is None else m_in.dtype)
+            _, m_dt = ops.fedopt_dtypes(ops.torch_dtype(dt), old.dtype, None if m_in is None else m_in.dtype)
             m_out = m_in if (m_in is not None and m_in.dtype == m_dt) else torch.empty(pg.numel(), dtype=m_dt,
                                                                                         device=self.device)
             v_out = v_in if v_in is not None else torch.empty(pg.numel(), dtype=torch.float64, device=self.device)
             out = torch.empty(pg.numel(), dtype=torch.float64, device=self.device)
             ops.fedopt_step(old, [], [], [], first=False, final=True, pg=pg, m_in=m_in, m_out=m_out, v_in=v_in,
                             v_out=v_out, out=out, serveropt=opt, learning_rate=params["learning_rate"],
-                            beta1=params["beta1"], beta2=params["beta2"], tau=params["tau"], stream=self.compute)
+                            beta1=params["beta1"], beta2=params["beta2"], tau=params["tau"], stream=self.compute,
+                            upd_dtype=ops.torch_dtype(dt))
             new_m[dt], new_v[dt], outs[dt] = m_out, v_out, out
         self._end_span(span)
         state.m, state.v, state.signature, state.layout = new_m, new_v, sig, self.layout

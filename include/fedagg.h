@@ -98,7 +98,8 @@ int fa_fedavg_fold(void* agg, int agg_dtype,
  * old       device, P elements of old_dtype (F32 | F64 | I32 | I64): the global model the
  *           clients trained from (fedopt.py:90)
  * updates   HOST array of K DEVICE pointers (F32 | BF16 | F64 | I32 | I64); integer tensors
- *           (e.g. BatchNorm counters) become float64 exactly as numpy's int * 1.0 does
+ *           (e.g. BatchNorm counters) become float64 exactly as numpy's int * 1.0 does.
+ *           upd_dtype is required even when K = 0: it fixes the pg dtype.
  * n, N      HOST arrays of K doubles (num_examples, running total)
  * pg        device workspace, P elements of pg dtype = promote(upd, old) (F64 for integer
  *           updates); read when

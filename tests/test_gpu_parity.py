@@ -428,3 +428,24 @@ def test_stock_fedopt_server_step_on_gpu_helper(name):
         assert_lists_identical(model, rd["out"], f"{name} r{r}")
         assert_lists_identical(m, rd["m"], f"{name} r{r} m")
         assert_lists_identical(v, rd["v"], f"{name} r{r} v")
+
+
+def test_fedopt_f64_updates_over_f32_model_streamed():
+    """pg dtype comes from the UPDATES (f64 here), also in the K = 0 server step of the
+    streamed (plug-in) path: fedopt.py with float64 client updates over a float32 seed."""
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rng = np.random.default_rng(41)
+    old = [rng.standard_normal(1001).astype(np.float32)]
+    ups = [([(old[0] + 0.01 * rng.standard_normal(1001)).astype(np.float64)], int(n))
+           for n in rng.integers(1, 5001, 4)]
+    st = ref.FedOptState()
+    want, _ = ref.fedopt_combine(st, ups, old, {"serveropt": "adam"})
+    uh = MemoryUpdateHandler()
+    gid = uh.put_global_model(old, "g")
+    for arrays, n in ups:
+        uh.submit(arrays, n, model_id=gid)
+    agg = get_aggregator("fedopt", uh)
+    model, _ = agg.combine_models(parameters={"serveropt": "adam"})
+    assert_lists_identical(model, want, "f64 over f32")
+    assert_lists_identical(agg.m, st.m, "m")
