@@ -92,3 +92,47 @@ class ShardedFedAvg:
         if self.rank != dst:
             return None
         return torch.cat(parts)[:self.P]
+
+
+class ShardedFedOpt:
+    """One rank's share of FedOpt (fedopt.py:74-258) over a P-element flat model: the
+    pseudo-gradient fold and the server step are elementwise, so rank r keeps ITS slice of
+    ``old``, ``m`` and ``v`` resident and never exchanges state; only the new model slice is
+    gathered (``allgather`` / ``gather_to_host`` as in :class:`ShardedFedAvg`).
+
+    ``step_fn(old, updates, n, N, m_in, v_in, params) -> (out, m_out, v_out)`` defaults to the
+    libfedagg kernel (:func:`fedn_amd.ops.fedopt_step`); tests inject a reference step.
+    """
+
+    def __init__(self, P, group=None, step_fn=None, align=ALIGN_ELEMS):
+        self._avg = ShardedFedAvg(P, group=group, fold_fn=lambda *a: None, align=align)
+        self.rank, self.world, self.lo, self.hi = self._avg.rank, self._avg.world, self._avg.lo, self._avg.hi
+        self.step_fn = step_fn or _kernel_fedopt_step
+        self.m = None
+        self.v = None
+
+    def local(self, flat):
+        return flat[self.lo:self.hi]
+
+    def step(self, old_local, updates_local, n, N, params):
+        out, self.m, self.v = self.step_fn(old_local, updates_local, n, N, self.m, self.v, params)
+        return out
+
+    def allgather(self, out_local):
+        return self._avg.allgather(out_local)
+
+    def gather_to_host(self, out_local, dst=0):
+        return self._avg.gather_to_host(out_local, dst)
+
+
+def _kernel_fedopt_step(old, updates, n, N, m_in, v_in, params):
+    from .ops import fedopt_dtypes, fedopt_step
+    pg_dt, m_dt = fedopt_dtypes(updates[0].dtype, old.dtype, None if m_in is None else m_in.dtype)
+    dev, P = old.device, old.numel()
+    m_out = m_in if (m_in is not None and m_in.dtype == m_dt) else torch.empty(P, dtype=m_dt, device=dev)
+    v_out = v_in if v_in is not None else torch.empty(P, dtype=torch.float64, device=dev)
+    out = torch.empty(P, dtype=torch.float64, device=dev)
+    pg = torch.empty(P, dtype=pg_dt, device=dev) if len(updates) > 64 else None
+    fedopt_step(old, updates, n, N, first=True, final=True, pg=pg, m_in=m_in, m_out=m_out, v_in=v_in, v_out=v_out,
+                out=out, **params)
+    return out, m_out, v_out

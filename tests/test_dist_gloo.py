@@ -85,3 +85,60 @@ def test_shard_bounds_cover_and_align():
             for (lo, hi), (lo2, _) in zip(b, b[1:]):
                 assert hi == lo2 and (lo % ALIGN_ELEMS == 0 or lo == P) and (lo2 % ALIGN_ELEMS == 0 or lo2 == P)
             assert all(lo <= hi for lo, hi in b)
+
+
+def _oracle_fedopt_step(old, updates, n, N, m_in, v_in, params):
+    from oracle import numpy_ref as ref
+    st = ref.FedOptState()
+    st.m = None if m_in is None else [m_in.numpy()]
+    st.v = None if v_in is None else [v_in.numpy()]
+    out, _ = ref.fedopt_combine(st, [([u.numpy()], k) for u, k in zip(updates, n)], [old.numpy()], params)
+    return torch.from_numpy(out[0]), torch.from_numpy(st.m[0]), torch.from_numpy(st.v[0])
+
+
+def _fedopt_worker(rank, world, port, P, K, seed, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from fedn_amd.sharded import ShardedFedOpt
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(seed)
+        old = rng.standard_normal(P).astype(np.float32)
+        sh = ShardedFedOpt(P, step_fn=_oracle_fedopt_step)
+        params = {"serveropt": "yogi"}
+        outs = []
+        for r in range(2):
+            ups = [torch.from_numpy((old + 0.01 * rng.standard_normal(P)).astype(np.float32)) for _ in range(K)]
+            ns = [int(v) for v in rng.integers(1, 5001, K)]
+            out = sh.step(sh.local(torch.from_numpy(old)), [sh.local(u) for u in ups], ns, list(np.cumsum(ns)), params)
+            full = sh.allgather(out).numpy().copy()
+            outs.append(full)
+            old = full
+        if rank == 0:
+            q.put(outs)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_fedopt_gloo_two_rounds():
+    """FedOpt state (m, v) stays sharded across rounds; gathered models == single-process oracle."""
+    from oracle import numpy_ref as ref
+    P, K, seed, world = 6000, 4, 23, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pc = mp.start_processes(_fedopt_worker, args=(world, _free_port(), P, K, seed, q), nprocs=world, join=False,
+                            start_method="spawn")
+    outs = q.get(timeout=120)
+    while not pc.join(timeout=60):
+        pass
+    rng = np.random.default_rng(seed)
+    old = rng.standard_normal(P).astype(np.float32)
+    st = ref.FedOptState()
+    for r in range(2):
+        ups = [(old + 0.01 * rng.standard_normal(P)).astype(np.float32) for _ in range(K)]
+        ns = [int(v) for v in rng.integers(1, 5001, K)]
+        want, _ = ref.fedopt_combine(st, [([u], k) for u, k in zip(ups, ns)], [old], {"serveropt": "yogi"})
+        assert outs[r].dtype == want[0].dtype
+        assert np.array_equal(outs[r].view(np.uint64), want[0].view(np.uint64)), f"round {r}"
+        old = want[0]

@@ -449,3 +449,22 @@ def test_fedopt_f64_updates_over_f32_model_streamed():
     model, _ = agg.combine_models(parameters={"serveropt": "adam"})
     assert_lists_identical(model, want, "f64 over f32")
     assert_lists_identical(agg.m, st.m, "m")
+
+
+def test_sharded_fedopt_kernel_single_rank():
+    """ShardedFedOpt's default step (the fused kernel) over two rounds, world size 1."""
+    from fedn_amd.sharded import ShardedFedOpt
+    rng = np.random.default_rng(43)
+    P, K = 5000, 70                                    # K > 64: the chunked path with a pg workspace
+    old = rng.standard_normal(P).astype(np.float32)
+    sh = ShardedFedOpt(P)
+    st = ref.FedOptState()
+    for r in range(2):
+        ups = [(old + 0.01 * rng.standard_normal(P)).astype(np.float32) for _ in range(K)]
+        ns = [int(v) for v in rng.integers(1, 5001, K)]
+        want, _ = ref.fedopt_combine(st, [([u], k) for u, k in zip(ups, ns)], [old], {"serveropt": "adagrad"})
+        out = sh.step(_to_dev(old), [_to_dev(u) for u in ups], ns, list(np.cumsum(ns)),
+                      {"serveropt": "adagrad"})
+        torch.cuda.synchronize()
+        assert_lists_identical([out.cpu().numpy()], want, f"r{r}")
+        old = want[0]
