@@ -84,10 +84,14 @@ class _Pipeline:
         stream waits for its H2D); host arrays are packed into a ring slot."""
         if isinstance(arrays, StagedModel):
             self.layout.check_layout(arrays.layout)      # raises the numpy-like error
-            self.compute.wait_event(arrays.ready)
             if arrays.dev.device != self.device:         # staged on another GPU: one D2D copy
-                arrays = StagedModel(arrays.layout, arrays.dev.to(self.device, non_blocking=True),
-                                     arrays.ready, None)
+                arrays.ready.synchronize()               # (rare) order the copy after its H2D
+                with torch.cuda.device(self.device):
+                    dev = arrays.dev.to(self.device)
+                    ready = torch.cuda.Event()
+                    ready.record(torch.cuda.current_stream(self.device))
+                arrays = StagedModel(arrays.layout, dev, ready, None)
+            self.compute.wait_event(arrays.ready)
             self._hold.append(arrays)                    # keep HBM alive until the round ends
             return arrays
         self.layout.check(arrays)
