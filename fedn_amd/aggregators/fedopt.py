@@ -21,7 +21,7 @@ from ..exceptions import InvalidParameterError
 from ..parameters import Parameters
 from ..staging import FedOptPipeline, FedOptState
 from .aggregatorbase import AggregatorBase
-from .fedavg import default_device
+from .fedavg import default_device, env_devices
 
 logger = logging.getLogger("fedn")
 
@@ -34,11 +34,25 @@ PARAMETER_SCHEMA = {"serveropt": str, "learning_rate": float, "beta1": float, "b
 class Aggregator(AggregatorBase):
     """Federated Optimization (FedOpt) on MI355X."""
 
-    def __init__(self, update_handler, device=None):
+    def __init__(self, update_handler, device=None, devices=None):
         super().__init__(update_handler)
         self.name = "fedopt"
         self.device = torch.device(device) if device is not None else None
-        self.state = FedOptState()
+        # several devices (argument or FEDN_AMD_DEVICES): old / pg / m / v sharded by parameter
+        # slice over them inside this process (multidev.py); fixed for the instance's lifetime
+        self.devices = devices or env_devices()
+        if self.devices and len(self.devices) > 1:
+            from ..multidev import ShardedFedOptState
+            self.state = ShardedFedOptState()
+        else:
+            self.state = FedOptState()
+
+    def _pipeline(self, model_old, model_next):
+        if self.devices and len(self.devices) > 1:
+            from ..multidev import ShardedFedOptPipeline
+            return ShardedFedOptPipeline(self.devices, model_old, model_next)
+        dev = self.device or (self.devices[0] if self.devices else None) or default_device()
+        return FedOptPipeline(dev, model_old, model_next)
 
     # reference attribute names (fedopt.py:37-38): host copies of the HBM-resident state
     @property
@@ -70,7 +84,7 @@ class Aggregator(AggregatorBase):
                 tic = time.time()
                 if nr_aggregated_models == 0:
                     model_old = self.update_handler.load_model(helper, model_update.model_id)
-                    pipe = FedOptPipeline(self.device or default_device(), model_old, model_next)
+                    pipe = self._pipeline(model_old, model_next)
                 pipe.add(model_next, metadata["num_examples"], total_examples)
                 data["time_model_aggregation"] += time.time() - tic
 

@@ -223,6 +223,33 @@ class FedOptState:
         return self._host(self.v)
 
 
+def old_groups(layout, old_arrays):
+    """The global model (fedopt.py:89-94) as one contiguous host array per update dtype group."""
+    if len(old_arrays) != len(layout.shapes):
+        raise ValueError("global model and update have different tensor counts")
+    out = {}
+    for dt in layout.groups:
+        parts = []
+        for i, _ in layout.members[dt]:
+            o = np.asarray(old_arrays[i])
+            if tuple(o.shape) != layout.shapes[i]:
+                raise ValueError(f"operands could not be combined: tensor {i} has shape {o.shape}, "
+                                 f"global model has {layout.shapes[i]}")
+            parts.append(o)
+        odt = {p.dtype for p in parts}
+        if len(odt) != 1:
+            raise TypeError("global-model tensors of one update dtype group must share a dtype")
+        flat = np.concatenate([p.reshape(-1) for p in parts]) if parts else np.empty(0, list(odt)[0])
+        out[dt] = np.ascontiguousarray(flat)
+    return out
+
+
+def check_fedopt_dtypes(layout):
+    for dt in layout.groups:
+        if ops.torch_dtype(dt) not in (torch.float32, torch.float64, torch.int32, torch.int64):
+            raise TypeError(f"FedOpt supports float32/float64/int32/int64 updates, got {dt}")
+
+
 class FedOptPipeline(_Pipeline):
     """Streaming FedOpt on one device: the pseudo-gradient loop of fedopt.py:74-106 on the
     GPU (pg resident in HBM), then the fused server step (fedopt.py:151-258)."""
@@ -230,23 +257,9 @@ class FedOptPipeline(_Pipeline):
     def __init__(self, device, old_arrays, first_arrays, nslots=2):
         layout = first_arrays.layout if isinstance(first_arrays, StagedModel) else Layout.of(first_arrays)
         super().__init__(device, layout, nslots)
-        if len(old_arrays) != len(layout.shapes):
-            raise ValueError("global model and update have different tensor counts")
-        self.old = {}
+        self.old = {dt: torch.from_numpy(flat).pin_memory().to(self.device, non_blocking=True)
+                    for dt, flat in old_groups(layout, old_arrays).items()}
         self.pg = {}
-        for dt in layout.groups:
-            parts = []
-            for i, _ in layout.members[dt]:
-                o = np.asarray(old_arrays[i])
-                if tuple(o.shape) != layout.shapes[i]:
-                    raise ValueError(f"operands could not be combined: tensor {i} has shape {o.shape}, "
-                                     f"global model has {layout.shapes[i]}")
-                parts.append(o)
-            odt = {p.dtype for p in parts}
-            if len(odt) != 1:
-                raise TypeError("global-model tensors of one update dtype group must share a dtype")
-            flat = np.concatenate([p.reshape(-1) for p in parts]) if parts else np.empty(0, list(odt)[0])
-            self.old[dt] = torch.from_numpy(np.ascontiguousarray(flat)).pin_memory().to(self.device, non_blocking=True)
         self.old_arrays = old_arrays
         self.nfolds = 0
 
@@ -255,9 +268,7 @@ class FedOptPipeline(_Pipeline):
             self.layout.check_layout(arrays.layout)
         else:
             self.layout.check(arrays)
-        for dt in self.layout.groups:
-            if ops.torch_dtype(dt) not in (torch.float32, torch.float64, torch.int32, torch.int64):
-                raise TypeError(f"FedOpt supports float32/float64/int32/int64 updates, got {dt}")
+        check_fedopt_dtypes(self.layout)
         slot = self.acquire(arrays)
         span = self._kernel_span()
         first = self.nfolds == 0

@@ -359,6 +359,52 @@ def test_multidevice_fedavg_golden(name, ndev):
     assert_lists_identical(model, rd["out"], f"{name} x{ndev}")
 
 
+@pytest.mark.parametrize("name", case_names("fedopt"))
+@pytest.mark.parametrize("ndev", [2, 3])
+def test_multidevice_fedopt_golden(name, ndev):
+    """FedOpt with old / pg / m / v sharded over devices in one process, over all rounds of
+    every golden FedOpt case (m and v reassembled from the device slices)."""
+    from fedn_amd.aggregators.fedopt import Aggregator
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    case = load_case(name)
+    uh = MemoryUpdateHandler()
+    agg = Aggregator(uh, devices=[DEV] * ndev)
+    for r, rd in enumerate(case["rounds"]):
+        gid = uh.put_global_model(rd["old"], f"global-{r}")
+        for arrays, n in rd["updates"]:
+            uh.submit(arrays, n, model_id=gid)
+        model, data = agg.combine_models(helper=None, delete_models=True, parameters=case["params"])
+        assert_lists_identical(model, rd["out"], f"{name} x{ndev} r{r} out")
+        assert data.get("nr_aggregated_models", -1) == rd["nr"]
+        if rd["m"] is not None:
+            assert_lists_identical(agg.m, rd["m"], f"{name} x{ndev} r{r} m")
+            assert_lists_identical(agg.v, rd["v"], f"{name} x{ndev} r{r} v")
+        else:
+            assert agg.m is None and agg.v is None
+
+
+def test_multidevice_fedopt_large_flat():
+    """3 M params over 4 slices, two yogi rounds, against the oracle."""
+    from fedn_amd.multidev import ShardedFedOptPipeline, ShardedFedOptState
+    rng = np.random.default_rng(37)
+    st, ost = ShardedFedOptState(), ref.FedOptState()
+    params = {"serveropt": "yogi", "learning_rate": 1e-2, "beta1": 0.9, "beta2": 0.99, "tau": 1e-4}
+    old = [rng.standard_normal(3_000_017).astype(np.float32)]
+    for r in range(2):
+        ups, ns = _updates(rng, 5, 3_000_017)
+        pipe = ShardedFedOptPipeline([DEV] * 4, old, [ups[0]])
+        total = 0
+        for u, n in zip(ups, ns):
+            total += n
+            pipe.add([u], n, total)
+        got = pipe.server_step(st, params)
+        want, nr = ref.fedopt_combine(ost, [([u], n) for u, n in zip(ups, ns)], old, params)
+        assert nr == 5
+        assert_lists_identical(got, want, f"r{r}")
+        assert_lists_identical(st.m_host(), ost.m, f"r{r} m")
+        old = got
+
+
 def test_multidevice_large_flat():
     from fedn_amd.multidev import ShardedFedAvgPipeline
     rng = np.random.default_rng(31)
