@@ -9,7 +9,9 @@ Multi-GPU (torchrun, one process per GPU): every rank aggregates its own paramet
 slice of P params (the global model is n_gpus * P params sharded by contiguous slice);
 no collective is on the data path ("scaling": "weak"). The RCCL all-gather that would
 reassemble the model on every GPU is timed separately and reported beside the line
-(``allgather``), not folded into ``value``.
+(``allgather``), not folded into ``value``; so is the fold with that all-gather chunked
+and overlapped (``fold_allgather``: block-cyclic shards, round i gathered on a
+communication stream while round i+1 folds; sharded.CyclicShardedFedAvg).
 
 Also measured in the same run:
   roofline      algorithmic bytes (K*P*4 + P*4 per launch) / average kernel time (HIP events
@@ -48,6 +50,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=100_000_000,
                     help="params per client in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--ag-rounds", type=int, default=4, help="rounds of the overlapped fold + all-gather")
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args()
 
@@ -114,14 +117,19 @@ def main():
             dist.init_process_group("nccl", device_id=device)
 
     from fedn_amd import _abi, ops
-    from fedn_amd.sharded import ShardedFedAvg
+    from fedn_amd.sharded import CyclicShardedFedAvg, ShardedFedAvg
     _abi.load()
 
     K = a.clients
     sh = ShardedFedAvg(a.params * world)          # global model = world x params, one slice per rank
     P = sh.hi - sh.lo                             # this rank's slice (4 KiB-aligned bounds)
     P_total = a.params * world
-    ups = make_updates(K, P, a.dtype, device, a.seed + 1000 * rank)
+    cyc = None
+    if world > 1 and not a.no_allgather:
+        cyc = CyclicShardedFedAvg(P_total, chunk=-(-P_total // (world * a.ag_rounds)))
+    L = max(P, cyc.local_len) if cyc else P
+    ups_full = make_updates(K, L, a.dtype, device, a.seed + 1000 * rank)
+    ups = [u[:P] for u in ups_full]
     ns = [int(v) for v in np.random.default_rng(a.seed).integers(1, 5001, K)]
     Ns = [int(v) for v in np.cumsum(ns)]
     agg = torch.empty(P, dtype=torch.float32, device=device)
@@ -180,6 +188,30 @@ def main():
                      "backend": "gloo (rehearsal)" if rehearsal else "rccl",
                      "note": "reassembles the world*params model on every GPU; not in value"}
 
+    fold_ag = None
+    if cyc is not None:
+        agg_c = torch.empty(cyc.local_len, dtype=torch.float32, device=device)
+        ups_c = [u[:cyc.local_len] for u in ups_full]
+        out_c = None if rehearsal else torch.empty(cyc.full_len, dtype=torch.float32, device=device)
+        for _ in range(2):
+            cyc.fold_allgather(agg_c, ups_c, ns, Ns, init=True, out=out_c)
+        torch.cuda.synchronize(device)
+        dist.barrier()
+        t1 = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            cyc.fold_allgather(agg_c, ups_c, ns, Ns, init=True, out=out_c)
+        torch.cuda.synchronize(device)
+        fa = torch.tensor([(time.perf_counter() - t1) / reps], dtype=torch.float64,
+                          device="cpu" if rehearsal else device)
+        dist.all_reduce(fa, op=dist.ReduceOp.MAX)
+        fa_s = float(fa[0])
+        fold_ag = {"ms": fa_s * 1e3, "value": K * P_total / fa_s, "unit": "params/s", "rounds": cyc.rounds,
+                   "chunk": cyc.C, "backend": "gloo (rehearsal)" if rehearsal else "rccl",
+                   "note": "fold + all-gather of each folded round overlapped on a second stream "
+                           "(block-cyclic shards); the world*params model on every GPU; not in value"}
+        del agg_c, ups_c, out_c
+
     base = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
         base = cpu_baseline(ups, ns, agg, a.cpu_sample)
@@ -202,6 +234,8 @@ def main():
         }
         if allgather:
             line["allgather"] = allgather
+        if fold_ag:
+            line["fold_allgather"] = fold_ag
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

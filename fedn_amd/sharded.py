@@ -136,3 +136,79 @@ def _kernel_fedopt_step(old, updates, n, N, m_in, v_in, params):
     fedopt_step(old, updates, n, N, first=True, final=True, pg=pg, m_in=m_in, m_out=m_out, v_in=v_in, v_out=v_out,
                 out=out, **params)
     return out, m_out, v_out
+
+
+class CyclicShardedFedAvg:
+    """FedAvg sharded block-cyclically, with the all-gather chunked and overlapped with the
+    fold ("chunk it and overlap it with the reduce of the next chunk").
+
+    The flat model is cut into chunks of C elements; chunk j belongs to rank j mod world, so
+    round i of the reduce covers the W consecutive chunks [i·W·C, (i+1)·W·C) — one per rank.
+    Rank r's local buffers hold its chunks back to back (round i at [i·C, (i+1)·C)). Then
+    ``all_gather_into_tensor(full[i·W·C : (i+1)·W·C], agg_local[i·C : (i+1)·C])`` writes
+    round i straight into natural model order — no reassembly pass — and it runs on a
+    communication stream while round i+1 is folded on the compute stream. Every element is
+    folded by the same kernel and client table: bit-identical to one GPU.
+    """
+
+    def __init__(self, P, chunk=1 << 22, group=None, fold_fn=None, align=ALIGN_ELEMS):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.P = P
+        self.C = max(align, -(-chunk // align) * align)
+        nchunks = max(1, -(-P // self.C))
+        self.rounds = -(-nchunks // self.world)
+        self.local_len = self.rounds * self.C
+        self.full_len = self.rounds * self.world * self.C
+        if fold_fn is None:
+            from .ops import fedavg_fold as fold_fn
+        self.fold_fn = fold_fn
+        self._comm = None
+
+    def owned(self):
+        """This rank's chunks as (global_lo, global_hi, local_lo), clipped to [0, P)."""
+        out = []
+        for i in range(self.rounds):
+            g = (i * self.world + self.rank) * self.C
+            if g < self.P:
+                out.append((g, min(g + self.C, self.P), i * self.C))
+        return out
+
+    def local(self, flat):
+        """This rank's chunks of a full flat buffer, as a new padded local buffer."""
+        loc = torch.zeros(self.local_len, dtype=flat.dtype, device=flat.device)
+        for lo, hi, l0 in self.owned():
+            loc[l0:l0 + hi - lo].copy_(flat[lo:hi])
+        return loc
+
+    def fold_allgather(self, agg_local, updates_local, n, N, init, out=None):
+        """Fold every round and gather it as soon as it is folded; returns the full model
+        (``full[:P]``; on the host for gloo). ``agg_local`` / ``updates_local``: local_len each."""
+        C, W = self.C, self.world
+        gloo = W > 1 and dist.get_backend(self.group) == "gloo"
+        dev = agg_local.device
+        on_gpu = dev.type == "cuda" and not gloo
+        if out is None:
+            out = torch.empty(self.full_len, dtype=agg_local.dtype, device=dev if not gloo else "cpu")
+        if on_gpu and W > 1 and self._comm is None:
+            self._comm = torch.cuda.Stream(dev)
+        cur = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+        for i in range(self.rounds):
+            sl = slice(i * C, (i + 1) * C)
+            self.fold_fn(agg_local[sl], [u[sl] for u in updates_local], n, N, init)
+            dst = out[i * W * C:(i + 1) * W * C]
+            if W == 1:
+                dst.copy_(agg_local[sl], non_blocking=True)
+            elif on_gpu:
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                self._comm.wait_event(ev)
+                with torch.cuda.stream(self._comm):
+                    dist.all_gather_into_tensor(dst, agg_local[sl], group=self.group)
+            else:
+                src = agg_local[sl].to("cpu")
+                dist.all_gather(list(dst.chunk(W)), src, group=self.group)
+        if on_gpu and W > 1:
+            cur.wait_stream(self._comm)
+        return out[:self.P]

@@ -142,3 +142,50 @@ def test_sharded_fedopt_gloo_two_rounds():
         assert outs[r].dtype == want[0].dtype
         assert np.array_equal(outs[r].view(np.uint64), want[0].view(np.uint64)), f"round {r}"
         old = want[0]
+
+
+def _cyclic_worker(rank, world, port, P, K, chunk, seed, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from fedn_amd.sharded import CyclicShardedFedAvg
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(seed)
+        base = rng.standard_normal(P).astype(np.float32)
+        ups = [torch.from_numpy((base + 0.01 * rng.standard_normal(P)).astype(np.float32)) for _ in range(K)]
+        ns = [int(v) for v in rng.integers(1, 5001, K)]
+        cs = CyclicShardedFedAvg(P, chunk=chunk, fold_fn=_oracle_fold)
+        agg = torch.empty(cs.local_len, dtype=torch.float32)
+        full = cs.fold_allgather(agg, [cs.local(u) for u in ups], ns, list(np.cumsum(ns)), init=True)
+        q.put((rank, full.numpy().copy(), cs.owned(), cs.rounds))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,P,chunk", [(2, 10_000, 1024), (3, 5_003, 1024), (2, 3_000, 4096), (3, 9_216, 1024)])
+def test_cyclic_fold_allgather_gloo(world, P, chunk):
+    """Block-cyclic shards, per-round fold + all-gather straight into natural order: every
+    rank ends with the full model, bit-identical to the single-process oracle."""
+    from oracle import numpy_ref as ref
+    K, seed = 4, 29
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pc = mp.start_processes(_cyclic_worker, args=(world, _free_port(), P, K, chunk, seed, q), nprocs=world,
+                            join=False, start_method="spawn")
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    while not pc.join(timeout=60):
+        pass
+    rng = np.random.default_rng(seed)
+    base = rng.standard_normal(P).astype(np.float32)
+    ups = [(base + 0.01 * rng.standard_normal(P)).astype(np.float32) for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    want = ref.fedavg_flat(ups, ns)
+    covered = []
+    for rank, full, owned, rounds in res:
+        assert full.shape == (P,)
+        assert np.array_equal(full.view(np.uint32), want.view(np.uint32)), f"rank {rank}"
+        covered += [(lo, hi) for lo, hi, _ in owned]
+    covered.sort()
+    assert covered[0][0] == 0 and covered[-1][1] == P
+    assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))

@@ -405,6 +405,22 @@ def test_multidevice_fedopt_large_flat():
         old = got
 
 
+def test_cyclic_fold_allgather_single_rank():
+    """CyclicShardedFedAvg at world size 1: per-round fold launches over chunk views of the
+    client buffers + the copy into natural order == one fold (the oracle)."""
+    from fedn_amd.sharded import CyclicShardedFedAvg
+    rng = np.random.default_rng(41)
+    P = 2_500_003
+    ups, ns = _updates(rng, 6, P)
+    want = ref.fedavg_flat(ups, ns)
+    cs = CyclicShardedFedAvg(P, chunk=600_000)
+    assert cs.rounds == 5
+    dev_ups = [cs.local(torch.from_numpy(u).to(DEV)) for u in ups]
+    agg = torch.empty(cs.local_len, device=DEV)
+    full = cs.fold_allgather(agg, dev_ups, ns, list(np.cumsum(ns)), init=True)
+    assert_lists_identical([full.cpu().numpy()], [want], "cyclic")
+
+
 def test_multidevice_large_flat():
     from fedn_amd.multidev import ShardedFedAvgPipeline
     rng = np.random.default_rng(31)
