@@ -38,6 +38,8 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
 
+    if a.sweep == "bf16":
+        return bf16_sweep(a)
     # achievable-peak references
     nb = 8 << 30
     src = torch.empty(nb, dtype=torch.uint8, device=dev).random_()
@@ -103,6 +105,30 @@ def main():
     bb = K * P * 2 + P * 4
     print(json.dumps({"kernel": "fedavg_bf16", "K": K, "P": P, "ms": med, "GBps": bb / med / 1e6,
                       "params_per_s": K * P / med * 1e3}), flush=True)
+
+
+def bf16_sweep(a):
+    """bf16 updates (half the bytes per element, same arithmetic): is the fold ALU-sensitive?"""
+    K, P, dev = a.clients, a.params, torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    base = torch.randn(P, generator=g, device=dev)
+    ups = [(base + 0.01 * torch.randn(P, generator=g, device=dev)).to(torch.bfloat16) for _ in range(K)]
+    del base
+    ns = [int(v) for v in np.random.default_rng(0).integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
+    agg = torch.empty(P, device=dev)
+    bb = K * P * 2 + P * 4
+    ref_out = None
+    for S, F, B in ((4, 1, 256), (4, 0, 256), (2, 1, 256), (8, 1, 256), (2, 0, 256), (4, 1, 512)):
+        ops.tune(strips=S, unroll=0, nt=0, fastdiv=F, lanetab=0, grid=0, block=B)
+        med, best = timed(lambda: ops.fedavg_fold(agg, ups, ns, Ns, init=True))
+        torch.cuda.synchronize()
+        if ref_out is None:
+            ref_out = agg.clone()
+        same = bool(torch.equal(agg.view(torch.int32), ref_out.view(torch.int32)))
+        print(json.dumps({"kernel": "fedavg_bf16", "strips": S, "fastdiv": F, "block": B, "ms": med,
+                          "GBps": bb / med / 1e6, "best_GBps": bb / best / 1e6, "identical": same}), flush=True)
+    ops.tune(strips=4, unroll=0, nt=0, fastdiv=1, lanetab=0, grid=0, block=256)
 
 
 if __name__ == "__main__":
