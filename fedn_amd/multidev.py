@@ -14,7 +14,6 @@ model, the pseudo-gradient and the server state m / v resident across rounds
 (ShardedFedOptState), so a session's optimizer state is spread over the node's HBM and never
 moves between devices.
 """
-import numpy as np
 import torch
 
 from . import ops
@@ -46,9 +45,7 @@ def gather_group(layout, bounds, devices, per_dev, dt):
                 flat[lo:hi].copy_(per_dev[d], non_blocking=True)
     for dv in devices:
         torch.cuda.current_stream(dv).synchronize()
-    owned = np.empty(flat.numel(), dtype=ops.numpy_dtype(rdt))
-    owned[:] = flat.numpy()
-    return owned
+    return flat.numpy()   # a new pinned block owned by the caller (see staging._Pipeline._to_host)
 
 
 class _ShardedStaging:

@@ -421,6 +421,35 @@ def test_cyclic_fold_allgather_single_rank():
     assert_lists_identical([full.cpu().numpy()], [want], "cyclic")
 
 
+@pytest.mark.parametrize("kind", ["fedavg", "fedopt"])
+@pytest.mark.parametrize("ndev", [1, 2])
+def test_returned_model_is_caller_owned(kind, ndev):
+    """The model handed back lives in its own host block: three more rounds (which reuse
+    every staging slot and the pinned-host cache) leave it untouched, and it is writable."""
+    from fedn_amd.aggregators.fedavg import Aggregator as FedAvg
+    from fedn_amd.aggregators.fedopt import Aggregator as FedOpt
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rng = np.random.default_rng(43)
+    uh = MemoryUpdateHandler()
+    agg = (FedAvg if kind == "fedavg" else FedOpt)(uh, devices=[DEV] * ndev)
+    shapes = [(300, 70), (70,), (1000,)]
+    old = [rng.standard_normal(sh).astype(np.float32) for sh in shapes]
+    kept, copies = [], []
+    for r in range(4):
+        gid = uh.put_global_model(old, f"g{r}")
+        for _ in range(3):
+            uh.submit([(o + 0.01 * rng.standard_normal(o.shape)).astype(np.float32) for o in old],
+                      int(rng.integers(1, 5000)), model_id=gid)
+        model, _ = agg.combine_models(helper=None, parameters={"serveropt": "adam"} if kind == "fedopt" else None)
+        kept.append(model)
+        copies.append([np.array(a, copy=True) for a in model])
+        old = [np.asarray(a, dtype=np.float32) for a in model]
+    for r, (m, c) in enumerate(zip(kept, copies)):
+        assert_lists_identical(m, c, f"round {r} model changed after later rounds")
+    kept[0][0][0, 0] = 123.0
+    assert kept[1][0][0, 0] != 123.0
+
+
 def test_multidevice_large_flat():
     from fedn_amd.multidev import ShardedFedAvgPipeline
     rng = np.random.default_rng(31)
