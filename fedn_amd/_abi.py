@@ -45,6 +45,15 @@ EXPORTS = {
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,   # v_in, v_out, out
         ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,  # opt, lr, b1, b2, tau
         ctypes.c_int64, ctypes.c_void_p]),                   # P, stream
+    "fa_weighted_sum": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_int,                       # acc, acc_dtype
+        ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,       # updates, upd_dtype
+        ctypes.POINTER(ctypes.c_double), ctypes.c_int,       # w, K
+        ctypes.c_int64, ctypes.c_void_p]),                   # P, stream
+    "fa_running_mean": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,      # g, dtype, m
+        ctypes.c_double, ctypes.c_double, ctypes.c_double,   # a, b, T
+        ctypes.c_int64, ctypes.c_void_p]),                   # P, stream
     "fa_tune": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "fa_stream_sum": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int64,
                                      ctypes.c_void_p]),
@@ -56,7 +65,7 @@ EXPORTS = {
     "fa_stream_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class FedAggLibraryError(ImportError):

@@ -160,6 +160,50 @@ struct CF16 {            // numpy half loops: op in float, round to half after e
     }
 };
 
+// Server-function aggregation rules, the two the reference ships as
+// examples of user `aggregate` / `incremental_aggregate` code (hooks.py:109-143):
+//
+// CWSUM — examples/server-functions/server_functions.py:58-67
+//     weighted_sum[i] += client_parameters[i] * num_examples
+//   the product is taken in the update dtype Y (python scalar w is weak: cast to Y), the sum
+//   in promote(acc, Y), the result stored back in the accumulator dtype X (in-place +=).
+template <typename Y, typename X>
+struct CWSUM {
+    static constexpr bool kF32 = std::is_same<Y, float>::value && std::is_same<X, float>::value;
+    using V = typename std::conditional<kF32, float, double>::type;
+    using S = double;
+    __device__ static __forceinline__ V fold(V x, V y, S w, S, double) {
+        V s;
+        if constexpr (std::is_same<Y, float>::value) {
+            const float p = (float)y * (float)w;     // y holds an exact f32 value
+            s = x + (V)p;
+        } else {
+            s = x + y * w;                           // f64 product, f64 sum
+        }
+        if constexpr (std::is_same<X, float>::value && std::is_same<V, double>::value)
+            return (double)(float)s;                 // += into an f32 accumulator rounds every step
+        else
+            return s;
+    }
+};
+
+// CRUN — examples/server-functions/sf_incremental_aggregation.py:36-37
+//     g = (g * (T - n) + m * n) / T       (T = running total including this client)
+//   g and m share the dtype T_; every python scalar is cast to it (numpy weak scalars) and each
+//   operation rounds in it: RN(RN(RN(g*a) + RN(m*b)) / T). The client table carries
+//   b = n in n[], T in N[] and a = T - n in r[].
+template <typename T_>
+struct CRUN {
+    using V = T_;
+    using S = double;
+    __device__ static __forceinline__ V fold(V x, V y, S b, S T, double a) {
+        const V u = x * (V)a;
+        const V w = y * (V)b;
+        const V s = u + w;
+        return s / (V)T;
+    }
+};
+
 struct CADD {            // measurement only: x <- x + y (same traversal as the fold, minimal VALU)
     using V = float;
     using S = float;
@@ -807,11 +851,20 @@ void launch_fedavg_geom(X* a, const ClientTable<typename CP::S>& tab, int cnt, i
         hipLaunchKernelGGL((k_fedavg<Y, X, CP, E, S, U, false, false, NT>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
 }
 
+template <class CP> struct is_sf_rule : std::false_type {};
+template <typename Y, typename X> struct is_sf_rule<CWSUM<Y, X>> : std::true_type {};
+template <typename T_> struct is_sf_rule<CRUN<T_>> : std::true_type {};
+
 // The tunable geometries are instantiated for the fp32 hot path only; other dtypes use the default.
 template <typename Y, typename X, class CP, int E>
 void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
                        hipStream_t st) {
-    constexpr bool tunable = (std::is_same<Y, float>::value || std::is_same<Y, bf16>::value) && std::is_same<X, float>::value;
+    constexpr bool tunable = (std::is_same<Y, float>::value || std::is_same<Y, bf16>::value) && std::is_same<X, float>::value &&
+                             std::is_same<CP, CF32>::value;
+    if constexpr (is_sf_rule<CP>::value) {
+        launch_fedavg_pipe<Y, X, CP, E, 4, false, false>(a, tab, cnt, P, first, int_first, st);
+        return;
+    }
     if constexpr (tunable) {
         const int key = (g_cfg.block_log == 9 ? 20000 : g_cfg.block_log == 10 ? 30000 : 0) + g_cfg.lanetab * 10000 +
                         g_cfg.strips * 100 + g_cfg.unroll * 2 + g_cfg.nt;
@@ -953,6 +1006,48 @@ int fa_fedavg_fold(void* agg, int agg_dtype, const void* const* updates, int upd
     if (upd_dtype == FA_I64 && agg_dtype == FA_F64) return launch_fedavg<int64_t, double, CF64>(agg, updates, n, N, K, P, init, int_first, st);
     if (upd_dtype == FA_I32 && agg_dtype == FA_F64) return launch_fedavg<int32_t, double, CF64>(agg, updates, n, N, K, P, init, int_first, st);
     return fail(FA_EDTYPE, "fa_fedavg_fold: unsupported dtype pair (update %d, aggregate %d)", upd_dtype, agg_dtype);
+}
+
+int fa_weighted_sum(void* acc, int acc_dtype, const void* const* updates, int upd_dtype, const double* w, int K,
+                    int64_t P, void* stream) {
+    g_err[0] = 0;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (P < 0 || K < 0) return fail(FA_EINVAL, "fa_weighted_sum: negative size (P=%lld, K=%d)", (long long)P, K);
+    if (K == 0 || P == 0) return FA_OK;
+    if (!acc || !updates || !w) return fail(FA_EINVAL, "fa_weighted_sum: null pointer argument");
+    for (int k = 0; k < K; ++k)
+        if (!updates[k]) return fail(FA_EINVAL, "fa_weighted_sum: updates[%d] is NULL", k);
+    // the client table's N is unused by the rule; pass w so fill_table reads valid memory
+    if (upd_dtype == FA_F32 && acc_dtype == FA_F32) return launch_fedavg<float, float, CWSUM<float, float>>(acc, updates, w, w, K, P, 0, false, st);
+    if (upd_dtype == FA_F32 && acc_dtype == FA_F64) return launch_fedavg<float, double, CWSUM<float, double>>(acc, updates, w, w, K, P, 0, false, st);
+    if (upd_dtype == FA_F64 && acc_dtype == FA_F64) return launch_fedavg<double, double, CWSUM<double, double>>(acc, updates, w, w, K, P, 0, false, st);
+    if (upd_dtype == FA_F64 && acc_dtype == FA_F32) return launch_fedavg<double, float, CWSUM<double, float>>(acc, updates, w, w, K, P, 0, false, st);
+    return fail(FA_EDTYPE, "fa_weighted_sum: unsupported dtype pair (update %d, accumulator %d)", upd_dtype, acc_dtype);
+}
+
+int fa_running_mean(void* g, int dtype, const void* m, double a, double b, double T, int64_t P, void* stream) {
+    g_err[0] = 0;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (P < 0) return fail(FA_EINVAL, "fa_running_mean: negative size");
+    if (P == 0) return FA_OK;
+    if (!g || !m) return fail(FA_EINVAL, "fa_running_mean: null pointer argument");
+    const void* ups[1] = {m};
+    const double bb[1] = {b}, TT[1] = {T};
+    auto run = [&](auto tag) -> int {
+        using T_ = decltype(tag);
+        using CP = CRUN<T_>;
+        constexpr int E = 16 / (int)sizeof(T_);
+        ClientTable<double> tab;
+        fill_table<double>(tab, ups, bb, TT, 0, 1);
+        tab.r[0] = a;                                        // a = T - n rides in r[]
+        T_* x = static_cast<T_*>(g);
+        if (aligned16(g) && aligned16(m)) launch_fedavg_vec<T_, T_, CP, E>(x, tab, 1, P, false, false, st);
+        else launch_fedavg_geom<T_, T_, CP, 1, 1, kUnroll, false>(x, tab, 1, P, false, false, st);
+        return check_launch("fa_running_mean: kernel launch");
+    };
+    if (dtype == FA_F32) return run(float{});
+    if (dtype == FA_F64) return run(double{});
+    return fail(FA_EDTYPE, "fa_running_mean: unsupported dtype %d", dtype);
 }
 
 int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, int upd_dtype, const double* n,

@@ -122,6 +122,45 @@ def fedavg_fold(agg, updates, n, N, init, stream=None):
     return agg
 
 
+def weighted_sum(acc, updates, w, stream=None):
+    """``acc[i] += updates[k][i] * w[k]`` for k in order (``fa_weighted_sum``): the loop of the
+    reference's server-function example aggregate (server_functions.py:58-67), numpy rounding."""
+    lib = _abi.load()
+    K = len(updates)
+    if len(w) != K:
+        raise ValueError("w must have one entry per update")
+    P = acc.numel()
+    dev = acc.device
+    _check_dev("acc", acc, P, None)
+    upd_dt = updates[0].dtype if K else acc.dtype
+    for i, u in enumerate(updates):
+        _check_dev(f"updates[{i}]", u, P, dev)
+        if u.dtype != upd_dt:
+            raise TypeError("all updates in one weighted_sum call must share a dtype")
+    with torch.cuda.device(dev):
+        st = _stream_handle(acc, stream)
+        rc = lib.fa_weighted_sum(acc.data_ptr(), fa_dtype(acc), _abi.ptr_array([u.data_ptr() for u in updates]),
+                                 fa_dtype(upd_dt), _abi.double_array(w), K, P, st)
+    _abi.check(rc)
+    return acc
+
+
+def running_mean(g, m, a, b, T, stream=None):
+    """``g = (g*a + m*b)/T`` in place (``fa_running_mean``): one step of the reference's
+    incremental server-function example (sf_incremental_aggregation.py:36-37)."""
+    lib = _abi.load()
+    P = g.numel()
+    _check_dev("g", g, P, None)
+    _check_dev("m", m, P, g.device)
+    if m.dtype != g.dtype:
+        raise TypeError(f"running_mean: model dtype {m.dtype} differs from the running model's {g.dtype}")
+    with torch.cuda.device(g.device):
+        st = _stream_handle(g, stream)
+        rc = lib.fa_running_mean(g.data_ptr(), fa_dtype(g), m.data_ptr(), float(a), float(b), float(T), P, st)
+    _abi.check(rc)
+    return g
+
+
 _OPTS = {"adam": _abi.FA_ADAM, "yogi": _abi.FA_YOGI, "adagrad": _abi.FA_ADAGRAD}
 
 

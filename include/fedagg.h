@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 1
+#define FA_ABI_VERSION 2
 
 /* element type codes */
 enum fa_dtype {
@@ -121,6 +121,26 @@ int fa_fedopt_step(const void* old, int old_dtype,
                    const double* v_in, double* v_out, double* out,
                    int serveropt, double lr, double beta1, double beta2, double tau,
                    int64_t P, void* stream);
+
+/*
+ * Server-function aggregation rules (hooks.py:109-143): the two formulas the reference ships
+ * as examples of user aggregation code, on device buffers with numpy's rounding.
+ *
+ * fa_weighted_sum replaces the loop of examples/server-functions/server_functions.py:58-67
+ *     for each client k in order:  acc[i] += updates[k][i] * w[k]
+ *   the product in the update dtype (w is a weak python scalar), the sum in
+ *   promote(acc, update), stored in the accumulator dtype. acc is read (start from zeros for
+ *   the example's np.zeros_like). The final `/ total_weight` is fa_elementwise(FA_EW_DIV).
+ *   acc_dtype, upd_dtype in {F32, F64}; w: HOST array of K doubles; any K (chunked by 64).
+ *
+ * fa_running_mean replaces examples/server-functions/sf_incremental_aggregation.py:36-37
+ *     g[i] = (g[i] * a + m[i] * b) / T      with a = T - n, b = n, T = running total
+ *   in place, g and m of the same dtype (F32 or F64); every scalar cast to that dtype.
+ */
+int fa_weighted_sum(void* acc, int acc_dtype, const void* const* updates, int upd_dtype,
+                    const double* w, int K, int64_t P, void* stream);
+int fa_running_mean(void* g, int dtype, const void* m, double a, double b, double T,
+                    int64_t P, void* stream);
 
 /*
  * numpyhelper primitives (numpyhelper.py:34-142) on device buffers, numpy rounding (python

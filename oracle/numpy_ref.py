@@ -227,3 +227,56 @@ def control_reduce(fetched):
                 model = data
             i += 1
     return model
+
+
+# ---------------------------------------------------------------------------------------------
+# Server-function aggregation examples (hooks.py:109-143 calls them)
+# ---------------------------------------------------------------------------------------------
+def sf_weighted_average(previous_global, client_updates):
+    """examples/server-functions/server_functions.py:53-68 (ServerFunctions.aggregate).
+
+    ``client_updates``: {client_id: (arrays, metadata)} in arrival order (hooks.py:88-101 stores
+    ``[model, metadata]`` lists). Running sum in previous_global's dtypes (np.zeros_like),
+    in-place ``+=`` of ``params * num_examples``, then ``/ total_weight``.
+    """
+    if len(client_updates) == 0:
+        return previous_global
+    weighted_sum = [np.zeros_like(param) for param in previous_global]
+    total_weight = 0
+    for _cid, (client_parameters, metadata) in client_updates.items():
+        num_examples = metadata.get("num_examples", 1)
+        total_weight += num_examples
+        for i in range(len(weighted_sum)):
+            weighted_sum[i] += client_parameters[i] * num_examples
+    return [weighted / total_weight for weighted in weighted_sum]
+
+
+class SfIncrementalAverage:
+    """examples/server-functions/sf_incremental_aggregation.py:10-48 (the aggregation part).
+
+    Note the example never resets ``total_examples`` (:12, :30): the running total carries
+    over into later rounds, and so it does here.
+    """
+
+    def __init__(self):
+        self.global_model = None
+        self.total_examples = 0
+        self.previous_global = None
+
+    def incremental_aggregate(self, client_id, model, client_metadata, previous_global):
+        self.previous_global = previous_global
+        num_examples = client_metadata.get("num_examples", 1)
+        self.total_examples += num_examples
+        if self.global_model is None:
+            self.global_model = model
+        else:
+            for i in range(len(self.global_model)):
+                self.global_model[i] = (self.global_model[i] * (self.total_examples - num_examples)
+                                        + model[i] * num_examples) / self.total_examples
+
+    def get_incremental_aggregate_model(self):
+        ret = self.global_model
+        self.global_model = None
+        if ret is None:
+            return self.previous_global
+        return ret

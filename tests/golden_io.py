@@ -36,6 +36,21 @@ def load_case(name):
         case["plan"] = plan
         case["models"] = [_list(z, f"c{c}") for c in range(len(plan))]
         case["out"] = None if bool(z["out_none"]) else _list(z, "out")
+    if case["kind"] == "sf_wavg":
+        K = int(z["K"])
+        case["prev"] = _list(z, "prev")
+        case["updates"] = {f"client-{k}": (_list(z, f"u{k}"), json.loads(str(z[f"meta{k}"]))) for k in range(K)}
+        case["out"] = _list(z, "out")
+    if case["kind"] == "sf_inc":
+        case["rounds"] = []
+        for r in range(int(z["rounds"])):
+            K = int(z[f"r{r}_K"])
+            case["rounds"].append({
+                "prev": _list(z, f"r{r}_prev"),
+                "updates": [(f"client-{k}", _list(z, f"r{r}_u{k}"), json.loads(str(z[f"r{r}_meta{k}"])))
+                            for k in range(K)],
+                "out": _list(z, f"r{r}_out"),
+            })
     if case["kind"] in ("fedavg", "fedopt"):
         case["params"] = json.loads(str(z["params"])) if "params" in z else None
         rounds = []

@@ -559,3 +559,59 @@ def test_sharded_fedopt_kernel_single_rank():
         torch.cuda.synchronize()
         assert_lists_identical([out.cpu().numpy()], want, f"r{r}")
         old = want[0]
+
+
+# ------------------------------------------------------------------------- server functions (§8(f)-4)
+@pytest.mark.parametrize("name", case_names("sf_wavg"))
+def test_sf_weighted_average_golden(name):
+    """GPU aggregate == the reference's example server function (server_functions.py:53-68)."""
+    from fedn_amd.serverfunctions import WeightedAverage
+    c = load_case(name)
+    got = WeightedAverage(device=DEV).aggregate(c["prev"], {k: [u, md] for k, (u, md) in c["updates"].items()})
+    assert_lists_identical(got, c["out"], name)
+
+
+@pytest.mark.parametrize("name", case_names("sf_inc"))
+def test_sf_incremental_golden(name):
+    """GPU incremental aggregate == the reference's example (sf_incremental_aggregation.py), all rounds
+    on one instance (running total carried over, stale previous_global on an empty round)."""
+    from fedn_amd.serverfunctions import IncrementalAverage
+    c = load_case(name)
+    sf = IncrementalAverage(device=DEV)
+    for r, rd in enumerate(c["rounds"]):
+        for cid, u, md in rd["updates"]:
+            sf.incremental_aggregate(cid, u, md, rd["prev"])
+        assert_lists_identical(sf.get_incremental_aggregate_model(), rd["out"], f"{name} r{r}")
+
+
+@pytest.mark.parametrize("acc_dt,upd_dt", [(np.float32, np.float32), (np.float64, np.float32),
+                                           (np.float64, np.float64), (np.float32, np.float64)])
+def test_weighted_sum_ops_k70(acc_dt, upd_dt):
+    """fa_weighted_sum over 70 clients in one call (two launches of <= 64) vs numpy's loop."""
+    from fedn_amd import ops
+    rng = np.random.default_rng(47)
+    P, K = 100_003, 70
+    ups = [rng.standard_normal(P).astype(upd_dt) for _ in range(K)]
+    w = [int(v) for v in rng.integers(1, 5001, K)]
+    w[3] = 2.75                                  # a python float weight
+    want = np.zeros(P, acc_dt)
+    for u, k in zip(ups, w):
+        want += u * k
+    acc = torch.zeros(P, dtype=ops.torch_dtype(np.dtype(acc_dt)), device=DEV)
+    ops.weighted_sum(acc, [torch.from_numpy(u).to(DEV) for u in ups], w)
+    assert_lists_identical([acc.cpu().numpy()], [want], "weighted_sum")
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_running_mean_ops(dt):
+    from fedn_amd import ops
+    rng = np.random.default_rng(53)
+    P = 1_000_003
+    g = rng.standard_normal(P).astype(dt)
+    m = rng.standard_normal(P).astype(dt)
+    g[:4] = [0.0, -0.0, np.inf, np.nan]
+    T, n = 123_457, 4_999
+    want = (g * (T - n) + m * n) / T
+    gd = torch.from_numpy(g).to(DEV)
+    ops.running_mean(gd, torch.from_numpy(m).to(DEV), T - n, n, T)
+    assert_lists_identical([gd.cpu().numpy()], [want], "running_mean")

@@ -273,9 +273,107 @@ def reduce_case(ref, name, rng, shapes, plan):
     return d
 
 
+def _example_server_functions(ref, filename):
+    """The REAL example class, instantiated the way the hooks server does it (hooks.py:187-205:
+    compile the user file, exec it, exec ``ServerFunctions()``). Its first line imports
+    ``fedn.network.combiner.hooks.allowed_import``, whose module body builds an APIClient
+    (network); we register that module with the names it re-exports taken from their real
+    sources (numpy, typing, the real ServerFunctionsBase) and ``api_client = None`` — the
+    aggregation methods do not use it."""
+    import typing
+
+    from fedn.network.combiner.hooks.serverfunctionsbase import ServerFunctionsBase
+    ai = types.ModuleType("fedn.network.combiner.hooks.allowed_import")
+    ai.Dict, ai.List, ai.Tuple = typing.Dict, typing.List, typing.Tuple
+    ai.np, ai.ServerFunctionsBase, ai.api_client = np, ServerFunctionsBase, None
+    ai.logger = logging.getLogger("fedn")
+    ai.print = lambda *a, **k: None
+    sys.modules["fedn.network.combiner.hooks.allowed_import"] = ai
+    path = os.path.join(REF, "examples", "server-functions", filename)
+    with open(path) as f:
+        code = compile(f.read(), path, "exec")
+    ns = {"print": ai.print}
+    exec(code, ns)  # noqa: S102 — reference example code, as hooks.py runs it
+    return ns["ServerFunctions"]
+
+
+def _meta(rng, k, kind):
+    if kind == "int":
+        return {"num_examples": int(rng.integers(1, 5001))}
+    if kind == "float":
+        return {"num_examples": float(rng.integers(1, 50000)) / 8.0}
+    if kind == "missing" and k == 1:
+        return {"training_loss": 0.5}            # no num_examples -> metadata.get(..., 1)
+    return {"num_examples": int(rng.integers(1, 5001))}
+
+
+def sf_wavg_case(ref, name, rng, shapes, K, prev_dtype=np.float32, upd_dtype=np.float32, meta="int"):
+    """examples/server-functions/server_functions.py:53-68 run on client_updates built as
+    hooks.py:88-101 builds them ({client_id: [model, metadata]}, arrival order)."""
+    SF = _example_server_functions(ref, "server_functions.py")
+    d = {"kind": np.array("sf_wavg"), "name": np.array(name), "K": np.array(K)}
+    prev = _rng_model(rng, shapes, prev_dtype)
+    _store_list(d, "prev", prev)
+    updates = {}
+    for k in range(K):
+        u = _perturb(rng, prev, upd_dtype)
+        md = _meta(rng, k, meta)
+        _store_list(d, f"u{k}", u)
+        d[f"meta{k}"] = np.array(json.dumps(md))
+        updates[f"client-{k}"] = [u, md]
+    out = SF().aggregate(prev, updates)
+    _store_list(d, "out", out)
+    return d
+
+
+def sf_inc_case(ref, name, rng, shapes, Ks, dtype=np.float32, meta="int"):
+    """examples/server-functions/sf_incremental_aggregation.py over several rounds on ONE
+    instance (the hooks server keeps it across rounds), fed as hooks.py:107-117 feeds it."""
+    SF = _example_server_functions(ref, "sf_incremental_aggregation.py")
+    sf = SF()
+    d = {"kind": np.array("sf_inc"), "name": np.array(name), "rounds": np.array(len(Ks))}
+    prev = _rng_model(rng, shapes, dtype)
+    for r, K in enumerate(Ks):
+        d[f"r{r}_K"] = np.array(K)
+        _store_list(d, f"r{r}_prev", prev)
+        for k in range(K):
+            u = _perturb(rng, prev, dtype)
+            md = _meta(rng, k, meta)
+            _store_list(d, f"r{r}_u{k}", u)
+            d[f"r{r}_meta{k}"] = np.array(json.dumps(md))
+            sf.incremental_aggregate(f"client-{k}", [np.array(a) for a in u], md, prev)
+        # K == 0: the example returns the previous_global it last saw in incremental_aggregate
+        # (it is only set there, sf_incremental_aggregation.py:26), i.e. an earlier round's
+        out = [np.array(a) for a in sf.get_incremental_aggregate_model()]
+        _store_list(d, f"r{r}_out", out)
+        prev = out
+    return d
+
+
+def sf_cases(ref):
+    rng = np.random.default_rng(6)
+    return [
+        sf_wavg_case(ref, "sf_wavg_mnist_k2", rng, MNIST_SHAPES, 2),
+        sf_wavg_case(ref, "sf_wavg_f64prev_k4", rng, ODD_SHAPES, 4, prev_dtype=np.float64),
+        sf_wavg_case(ref, "sf_wavg_f64upd_f32acc_k3", rng, ODD_SHAPES, 3, upd_dtype=np.float64),
+        sf_wavg_case(ref, "sf_wavg_f64_k3", rng, ODD_SHAPES, 3, prev_dtype=np.float64, upd_dtype=np.float64),
+        sf_wavg_case(ref, "sf_wavg_floatw_k4", rng, ODD_SHAPES, 4, meta="float"),
+        sf_wavg_case(ref, "sf_wavg_missingw_k3", rng, ODD_SHAPES, 3, meta="missing"),
+        sf_wavg_case(ref, "sf_wavg_empty", rng, ODD_SHAPES, 0),
+        sf_wavg_case(ref, "sf_wavg_k70", rng, [(1031,)], 70),
+        sf_inc_case(ref, "sf_inc_3r", rng, ODD_SHAPES + [(2053,)], [4, 3, 2]),
+        sf_inc_case(ref, "sf_inc_f64_2r", rng, ODD_SHAPES, [3, 2], dtype=np.float64),
+        sf_inc_case(ref, "sf_inc_floatw_2r", rng, ODD_SHAPES, [3, 3], meta="float"),
+        sf_inc_case(ref, "sf_inc_empty_round", rng, ODD_SHAPES, [2, 0, 2]),
+    ]
+
+
 def main():
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     ref = _import_reference()
     os.makedirs(OUT, exist_ok=True)
+    if only == "sf":      # regenerate just these fixtures; the others stay byte-identical
+        return _write(sf_cases(ref), merge=True)
     cases = []
     cases.append(helper_kat(ref))
     rng = np.random.default_rng(1)
@@ -325,7 +423,15 @@ def main():
     cases.append(reduce_case(ref, "reduce_bad_replaces", rng, ODD_SHAPES, ["ok", "ok", "bad", "ok"]))
     cases.append(reduce_case(ref, "reduce_single", rng, ODD_SHAPES, ["ok"]))
 
+    cases += sf_cases(ref)
+    _write(cases, merge=False)
+
+
+def _write(cases, merge):
     manifest = []
+    if merge:
+        with open(os.path.join(OUT, "manifest.json")) as f:
+            manifest = [n for n in json.load(f)["cases"] if n not in {str(c["name"]) for c in cases}]
     for c in cases:
         name = str(c["name"])
         np.savez(os.path.join(OUT, name + ".npz"), **c)
