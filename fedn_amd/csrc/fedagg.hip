@@ -580,38 +580,20 @@ k_fedopt(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::
         }
     }
     if (full) {
-        // batches of U clients, double-buffered: batch j+1's strips are in flight while batch j
-        // is folded (the explicit ping-pong of k_fedavg_pipe; no dynamic register indexing)
-        constexpr int U = kUnroll / 2;
-        auto loadU = [&](int kk, Y (&y)[U][E]) {
+        for (; k + kUnroll / 2 <= K; k += kUnroll / 2) {
+            Y y[kUnroll / 2][E];
 #pragma unroll
-            for (int u = 0; u < U; ++u) strip_load<Y, E, NT>(static_cast<const Y*>(tab.ptr[kk + u]) + i0, y[u]);
-        };
-        auto foldU = [&](int kk, const Y (&y)[U][E]) {
+            for (int u = 0; u < kUnroll / 2; ++u)
+                strip_load<Y, E, NT>(static_cast<const Y*>(tab.ptr[k + u]) + i0, y[u]);
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const typename PG::S n = tab.n[kk + u], N = tab.N[kk + u];
-                const double r = tab.r[kk + u];
+            for (int u = 0; u < kUnroll / 2; ++u) {
+                const typename PG::S n = tab.n[k + u], N = tab.N[k + u];
+                const double r = tab.r[k + u];
                 V d[E];
 #pragma unroll
                 for (int e = 0; e < E; ++e) d[e] = widen<Y, V>(y[u][e]) - ov[e];   // subtract(next, old)
                 fold_strip<PG, E>(pg, d, n, N, r);
             }
-        };
-        int nb = (K - k) / U;
-        Y ya[U][E], yb[U][E];
-        if (nb > 0) loadU(k, ya);
-        while (nb >= 2) {
-            loadU(k + U, yb);
-            foldU(k, ya);
-            if (nb >= 3) loadU(k + 2 * U, ya);
-            foldU(k + U, yb);
-            k += 2 * U;
-            nb -= 2;
-        }
-        if (nb == 1) {
-            foldU(k, ya);
-            k += U;
         }
     }
     for (; k < K; ++k) {
