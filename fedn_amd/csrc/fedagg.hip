@@ -209,6 +209,9 @@ struct CADD {            // measurement only: x <- x + y (same traversal as the 
     using S = float;
     __device__ static __forceinline__ V fold(V x, V y, S, S, double) { return x + y; }
 };
+struct CADDNW : CADD {};  // measurement only: CADD whose store is skipped (never-true data test)
+template <class CP> struct is_nostore : std::false_type {};
+template <> struct is_nostore<CADDNW> : std::true_type {};
 
 // element-wise client step for policies without a strip-level shortcut
 template <class CP, int E>
@@ -500,6 +503,9 @@ k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const 
             X xo[E];
 #pragma unroll
             for (int e = 0; e < E; ++e) xo[e] = narrow<X, V>(x[s][e]);
+            if constexpr (is_nostore<CP>::value) {
+                if (__float_as_uint(x[s][0]) != 0xFFFFFFFFu) continue;   // keeps loads + adds live
+            }
             strip_store<X, E>(agg + (strip0 + s * BLK) * E, xo);
         }
     }
@@ -806,9 +812,10 @@ struct FedAvgCfg {
     int strips = 4;   // measured best on MI355X (profiles/r01_microbench.md): 4 strips per lane,
     int unroll = 0;   // software-pipelined one client ahead
     int lanetab = 0;
-    int grid_per_cu = 0;
+    int grid_per_cu = 0;      // 0: one tile per block; n: persistent grid of n blocks per CU
     int read_per_lane = 16;   // fa_stream_read probe only
-    int block_log = 8;        // pipelined kernel workgroup size 2^block_log (8, 9, 10)   // 0: one tile per block; n: persistent grid of n blocks per CU
+    int block_log = 8;        // pipelined kernel workgroup size 2^block_log (8, 9, 10)
+    int sum_nostore = 0;      // fa_stream_sum probe: suppress the store (reads + adds only)
     int nt = 0;   // measured: cached loads beat non-temporal ones by ~3% (profiles/)
 };
 FedAvgCfg g_cfg;
@@ -1128,6 +1135,9 @@ int fa_tune(int knob, int value) {
         case FA_TUNE_NT:
             g_cfg.nt = value ? 1 : 0;
             return FA_OK;
+        case FA_TUNE_SUM_NOSTORE:
+            g_cfg.sum_nostore = value != 0;
+            return FA_OK;
         case FA_TUNE_BLOCK:
             if (value != 256 && value != 512 && value != 1024) return fail(FA_EINVAL, "fa_tune: block 256, 512 or 1024");
             g_cfg.block_log = value == 256 ? 8 : value == 512 ? 9 : 10;
@@ -1160,7 +1170,10 @@ int fa_stream_sum(float* out, const float* const* bufs, int K, int64_t P, void* 
     ClientTable<float> tab;
     std::vector<double> ones(K, 1.0);
     fill_table<float>(tab, reinterpret_cast<const void* const*>(bufs), ones.data(), ones.data(), 0, K);
-    launch_fedavg_pipe<float, float, CADD, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
+    if (g_cfg.sum_nostore)
+        launch_fedavg_pipe<float, float, CADDNW, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
+    else
+        launch_fedavg_pipe<float, float, CADD, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
     return check_launch("fa_stream_sum");
 }
 
