@@ -255,7 +255,7 @@ __device__ __forceinline__ void strip_load(const T* __restrict__ p, T (&r)[E]) {
     }
 }
 
-template <typename T, int E>
+template <typename T, int E, bool NTS = false>
 __device__ __forceinline__ void strip_store(T* __restrict__ p, const T (&r)[E]) {
     constexpr int bytes = E * (int)sizeof(T);
     if constexpr (bytes % 16 == 0) {
@@ -264,7 +264,8 @@ __device__ __forceinline__ void strip_store(T* __restrict__ p, const T (&r)[E]) 
         for (int j = 0; j < bytes / 16; ++j) {
             u32x4 w;
             __builtin_memcpy(&w, reinterpret_cast<const char*>(r) + 16 * j, 16);
-            q[j] = w;
+            if constexpr (NTS) __builtin_nontemporal_store(w, q + j);
+            else q[j] = w;
         }
     } else {
 #pragma unroll
@@ -452,7 +453,8 @@ struct LaneTable {
     }
 };
 
-template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK = kBlock>
+template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK = kBlock,
+          bool NTS = false>
 __global__ void __launch_bounds__(BLK)
 k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P) {
     using V = typename CP::V;
@@ -506,7 +508,7 @@ k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const 
             if constexpr (is_nostore<CP>::value) {
                 if (__float_as_uint(x[s][0]) != 0xFFFFFFFFu) continue;   // keeps loads + adds live
             }
-            strip_store<X, E>(agg + (strip0 + s * BLK) * E, xo);
+            strip_store<X, E, NTS>(agg + (strip0 + s * BLK) * E, xo);
         }
     }
 }
@@ -816,6 +818,7 @@ struct FedAvgCfg {
     int read_per_lane = 16;   // fa_stream_read probe only
     int block_log = 8;        // pipelined kernel workgroup size 2^block_log (8, 9, 10)
     int sum_nostore = 0;      // fa_stream_sum probe: suppress the store (reads + adds only)
+    int nt_store = 0;         // pipelined kernel (S = 4, 256 threads) and fa_stream_sum: streaming stores
     int nt = 0;   // measured: cached loads beat non-temporal ones by ~3% (profiles/)
 };
 FedAvgCfg g_cfg;
@@ -828,7 +831,7 @@ int device_cus() {
     return cus > 0 ? cus : 256;
 }
 
-template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT, int BLK = kBlock>
+template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT, int BLK = kBlock, bool NTS = false>
 void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
                         hipStream_t st) {
     const int64_t strips = (P + E - 1) / E;
@@ -837,11 +840,11 @@ void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, i
     const dim3 grid((unsigned)ntiles);
     if (first && int_first) {
         if constexpr (std::is_integral<Y>::value)
-            hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, true, NT, LT, BLK>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
+            hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, true, NT, LT, BLK, NTS>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
     } else if (first)
-        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, false, NT, LT, BLK>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
+        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, false, NT, LT, BLK, NTS>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
     else
-        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, false, false, NT, LT, BLK>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
+        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, false, false, NT, LT, BLK, NTS>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
 }
 
 template <typename Y, typename X, class CP, int E, int S, int U, bool NT>
@@ -882,7 +885,9 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
             FA_GEOM(4, 1, 0) FA_GEOM(4, 2, 0) FA_GEOM(4, 4, 0) FA_GEOM(8, 1, 0) FA_GEOM(8, 2, 0) FA_GEOM(16, 1, 0)
             FA_GEOM(1, 8, 1) FA_GEOM(4, 2, 1) FA_GEOM(8, 1, 1)
             case 2 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 2, false, false>(a, tab, cnt, P, first, int_first, st);
-            case 4 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 4, false, false>(a, tab, cnt, P, first, int_first, st);
+            case 4 * 100 + 0:
+                if (g_cfg.nt_store) return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, true>(a, tab, cnt, P, first, int_first, st);
+                return launch_fedavg_pipe<Y, X, CP, E, 4, false, false>(a, tab, cnt, P, first, int_first, st);
             case 8 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 8, false, false>(a, tab, cnt, P, first, int_first, st);
             case 4 * 100 + 1: return launch_fedavg_pipe<Y, X, CP, E, 4, true, false>(a, tab, cnt, P, first, int_first, st);
             case 20000 + 4 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, 512>(a, tab, cnt, P, first, int_first, st);
@@ -1138,6 +1143,9 @@ int fa_tune(int knob, int value) {
         case FA_TUNE_SUM_NOSTORE:
             g_cfg.sum_nostore = value != 0;
             return FA_OK;
+        case FA_TUNE_NT_STORE:
+            g_cfg.nt_store = value != 0;
+            return FA_OK;
         case FA_TUNE_BLOCK:
             if (value != 256 && value != 512 && value != 1024) return fail(FA_EINVAL, "fa_tune: block 256, 512 or 1024");
             g_cfg.block_log = value == 256 ? 8 : value == 512 ? 9 : 10;
@@ -1172,6 +1180,8 @@ int fa_stream_sum(float* out, const float* const* bufs, int K, int64_t P, void* 
     fill_table<float>(tab, reinterpret_cast<const void* const*>(bufs), ones.data(), ones.data(), 0, K);
     if (g_cfg.sum_nostore)
         launch_fedavg_pipe<float, float, CADDNW, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
+    else if (g_cfg.nt_store)
+        launch_fedavg_pipe<float, float, CADD, 4, 4, false, false, kBlock, true>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
     else
         launch_fedavg_pipe<float, float, CADD, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
     return check_launch("fa_stream_sum");

@@ -268,7 +268,8 @@ def stream_read_sink(src):
 _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _abi.FA_TUNE_NT,
           "fastdiv": _abi.FA_TUNE_FASTDIV, "lanetab": _abi.FA_TUNE_LANETAB,
           "grid": _abi.FA_TUNE_GRID, "read": _abi.FA_TUNE_READ,
-          "block": _abi.FA_TUNE_BLOCK, "sum_nostore": _abi.FA_TUNE_SUM_NOSTORE}
+          "block": _abi.FA_TUNE_BLOCK, "sum_nostore": _abi.FA_TUNE_SUM_NOSTORE,
+          "nt_store": _abi.FA_TUNE_NT_STORE}
 
 
 def tune(**knobs):

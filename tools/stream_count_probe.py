@@ -1,9 +1,14 @@
-"""Does the fold traversal get faster with fewer concurrently read client buffers?
-stream_sum (the FedAvg traversal with one add) over K buffers holding 25.6 GB in total."""
+"""Where the fold traversal loses against a pure streaming read (profiles/r01_store_probe.log).
+
+For K client buffers holding ~25.6 GB in total: stream_sum (the FedAvg traversal with one add)
+with its normal store, with the store suppressed (reads only), and with streaming
+(non-temporal) stores; then the real fp32 fold with normal vs streaming stores.
+"""
 import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -18,19 +23,33 @@ ops.tune(read=16)
 med, best = timed(lambda: ops.stream_read(src, sink))
 print(json.dumps({"kernel": "stream_read x16/lane", "GBps": (8 << 30) / med / 1e6}), flush=True)
 del src, sink
-TOTAL = 6_400_000_000          # fp32 elements across all buffers (25.6 GB)
-for K in (8, 32, 64):
+TOTAL = 6_400_000_000
+for K in (8, 64):
     P = TOTAL // K // 4096 * 4096
     bufs = [torch.empty(P, device="cuda").uniform_() for _ in range(K)]
     out = torch.empty(P, device="cuda")
-    med, best = timed(lambda: ops.stream_sum(out, bufs))
+    ns = [int(v) for v in np.random.default_rng(0).integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
     by = K * P * 4 + P * 4
-    print(json.dumps({"K": K, "P": P, "ms": med, "GBps": by / med / 1e6, "best_GBps": by / best / 1e6,
-                      "read_GBps": K * P * 4 / med / 1e6}), flush=True)
-    ops.tune(sum_nostore=1)            # same traversal, store suppressed: reads only
-    med, best = timed(lambda: ops.stream_sum(out, bufs))
-    ops.tune(sum_nostore=0)
-    print(json.dumps({"K": K, "P": P, "store": False, "ms": med, "read_GBps": K * P * 4 / med / 1e6,
-                      "best_read_GBps": K * P * 4 / best / 1e6}), flush=True)
+    ref = None
+    for name, knobs, fn in (
+            ("stream_sum", {}, lambda: ops.stream_sum(out, bufs)),
+            ("stream_sum no-store", {"sum_nostore": 1}, lambda: ops.stream_sum(out, bufs)),
+            ("stream_sum nt-store", {"nt_store": 1}, lambda: ops.stream_sum(out, bufs)),
+            ("fold", {}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True)),
+            ("fold nt-store", {"nt_store": 1}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True)),
+            ("fold", {}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True))):
+        ops.tune(**knobs)
+        med, best = timed(fn, reps=20)
+        ops.tune(sum_nostore=0, nt_store=0)
+        same = None
+        if name.startswith("fold"):
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = out.clone()
+            same = bool(torch.equal(out.view(torch.int32), ref.view(torch.int32)))
+        nb = K * P * 4 if "no-store" in name else by
+        print(json.dumps({"K": K, "P": P, "kernel": name, "ms": med, "GBps": nb / med / 1e6, "best_GBps": nb / best / 1e6,
+                          "identical": same}), flush=True)
     del bufs, out
     torch.cuda.empty_cache()
