@@ -255,7 +255,9 @@ __device__ __forceinline__ void strip_load(const T* __restrict__ p, T (&r)[E]) {
     }
 }
 
-template <typename T, int E, bool NTS = false>
+// SM (store mode): 0 plain (write-back in L2), 1 non-temporal, 2 write-through (`sc1`,
+// MI355X_MICROARCH.md "stores of each flavour": the line leaves L2 as the store issues)
+template <typename T, int E, int SM = 0>
 __device__ __forceinline__ void strip_store(T* __restrict__ p, const T (&r)[E]) {
     constexpr int bytes = E * (int)sizeof(T);
     if constexpr (bytes % 16 == 0) {
@@ -264,7 +266,8 @@ __device__ __forceinline__ void strip_store(T* __restrict__ p, const T (&r)[E]) 
         for (int j = 0; j < bytes / 16; ++j) {
             u32x4 w;
             __builtin_memcpy(&w, reinterpret_cast<const char*>(r) + 16 * j, 16);
-            if constexpr (NTS) __builtin_nontemporal_store(w, q + j);
+            if constexpr (SM == 1) __builtin_nontemporal_store(w, q + j);
+            else if constexpr (SM == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(q + j), "v"(w) : "memory");
             else q[j] = w;
         }
     } else {
@@ -454,7 +457,7 @@ struct LaneTable {
 };
 
 template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK = kBlock,
-          bool NTS = false>
+          int NTS = 0>
 __global__ void __launch_bounds__(BLK)
 k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P) {
     using V = typename CP::V;
@@ -818,7 +821,7 @@ struct FedAvgCfg {
     int read_per_lane = 16;   // fa_stream_read probe only
     int block_log = 8;        // pipelined kernel workgroup size 2^block_log (8, 9, 10)
     int sum_nostore = 0;      // fa_stream_sum probe: suppress the store (reads + adds only)
-    int nt_store = 0;         // pipelined kernel (S = 4, 256 threads) and fa_stream_sum: streaming stores
+    int nt_store = 0;         // pipelined kernel (S = 4, 256 threads) and fa_stream_sum: store mode 0 plain, 1 nt, 2 sc1
     int nt = 0;   // measured: cached loads beat non-temporal ones by ~3% (profiles/)
 };
 FedAvgCfg g_cfg;
@@ -831,7 +834,7 @@ int device_cus() {
     return cus > 0 ? cus : 256;
 }
 
-template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT, int BLK = kBlock, bool NTS = false>
+template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT, int BLK = kBlock, int NTS = 0>
 void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
                         hipStream_t st) {
     const int64_t strips = (P + E - 1) / E;
@@ -886,7 +889,8 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
             FA_GEOM(1, 8, 1) FA_GEOM(4, 2, 1) FA_GEOM(8, 1, 1)
             case 2 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 2, false, false>(a, tab, cnt, P, first, int_first, st);
             case 4 * 100 + 0:
-                if (g_cfg.nt_store) return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, true>(a, tab, cnt, P, first, int_first, st);
+                if (g_cfg.nt_store == 1) return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 1>(a, tab, cnt, P, first, int_first, st);
+                if (g_cfg.nt_store == 2) return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 2>(a, tab, cnt, P, first, int_first, st);
                 return launch_fedavg_pipe<Y, X, CP, E, 4, false, false>(a, tab, cnt, P, first, int_first, st);
             case 8 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 8, false, false>(a, tab, cnt, P, first, int_first, st);
             case 4 * 100 + 1: return launch_fedavg_pipe<Y, X, CP, E, 4, true, false>(a, tab, cnt, P, first, int_first, st);
@@ -1144,7 +1148,8 @@ int fa_tune(int knob, int value) {
             g_cfg.sum_nostore = value != 0;
             return FA_OK;
         case FA_TUNE_NT_STORE:
-            g_cfg.nt_store = value != 0;
+            if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: store mode 0 (plain), 1 (nt) or 2 (sc1)");
+            g_cfg.nt_store = value;
             return FA_OK;
         case FA_TUNE_BLOCK:
             if (value != 256 && value != 512 && value != 1024) return fail(FA_EINVAL, "fa_tune: block 256, 512 or 1024");
@@ -1180,8 +1185,10 @@ int fa_stream_sum(float* out, const float* const* bufs, int K, int64_t P, void* 
     fill_table<float>(tab, reinterpret_cast<const void* const*>(bufs), ones.data(), ones.data(), 0, K);
     if (g_cfg.sum_nostore)
         launch_fedavg_pipe<float, float, CADDNW, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
-    else if (g_cfg.nt_store)
-        launch_fedavg_pipe<float, float, CADD, 4, 4, false, false, kBlock, true>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
+    else if (g_cfg.nt_store == 1)
+        launch_fedavg_pipe<float, float, CADD, 4, 4, false, false, kBlock, 1>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
+    else if (g_cfg.nt_store == 2)
+        launch_fedavg_pipe<float, float, CADD, 4, 4, false, false, kBlock, 2>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
     else
         launch_fedavg_pipe<float, float, CADD, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
     return check_launch("fa_stream_sum");

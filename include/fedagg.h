@@ -191,7 +191,7 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                     FA_TUNE_GRID = 5, FA_TUNE_READ = 6 /* fa_stream_read loads per lane: 4 | 8 | 16 */,
                     FA_TUNE_BLOCK = 7 /* pipelined kernel workgroup size 256 | 512 | 1024 */,
                     FA_TUNE_SUM_NOSTORE = 8 /* fa_stream_sum probe: 1 = skip the store (reads + adds only) */,
-                    FA_TUNE_NT_STORE = 9 /* 1 = streaming (non-temporal) stores of the aggregate */ };
+                    FA_TUNE_NT_STORE = 9 /* aggregate stores: 0 plain, 1 non-temporal, 2 write-through (sc1) */ };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);

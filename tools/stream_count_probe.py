@@ -36,8 +36,10 @@ for K in (8, 64):
             ("stream_sum", {}, lambda: ops.stream_sum(out, bufs)),
             ("stream_sum no-store", {"sum_nostore": 1}, lambda: ops.stream_sum(out, bufs)),
             ("stream_sum nt-store", {"nt_store": 1}, lambda: ops.stream_sum(out, bufs)),
+            ("stream_sum sc1-store", {"nt_store": 2}, lambda: ops.stream_sum(out, bufs)),
             ("fold", {}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True)),
             ("fold nt-store", {"nt_store": 1}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True)),
+            ("fold sc1-store", {"nt_store": 2}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True)),
             ("fold", {}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True))):
         ops.tune(**knobs)
         med, best = timed(fn, reps=20)
