@@ -524,7 +524,6 @@ struct OptScalars {
     double lr, b1, b2, tau, tau2, c1, c2, nc2;   // c1 = 1-b1, c2 = 1-b2, nc2 = -(1-b2)
     float b1f, c1f, c2f;                         // the same cast to f32 (numpy weak-scalar rule)
     int opt;
-    int store_mode;                              // 0 plain, 1 non-temporal stores of m / v / out
 };
 
 struct OptBuffers {
@@ -681,20 +680,15 @@ k_fedopt(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::
         }
         // ---- stores
         if (full) {
-            auto stores = [&](auto sm) {
-                constexpr int SM = decltype(sm)::value;
-                strip_store<double, E, SM>(b.v_out + i0, v);
-                strip_store<double, E, SM>(b.out + i0, o);
-                if (b.m_out_f64) strip_store<double, E, SM>(static_cast<double*>(b.m_out) + i0, m);
-                else {
-                    float mf[E];
+            strip_store<double, E>(b.v_out + i0, v);
+            strip_store<double, E>(b.out + i0, o);
+            if (b.m_out_f64) strip_store<double, E>(static_cast<double*>(b.m_out) + i0, m);
+            else {
+                float mf[E];
 #pragma unroll
-                    for (int e = 0; e < E; ++e) mf[e] = (float)m[e];
-                    strip_store<float, E, SM>(static_cast<float*>(b.m_out) + i0, mf);
-                }
-            };
-            if (s.store_mode == 1) stores(std::integral_constant<int, 1>{});
-            else stores(std::integral_constant<int, 0>{});
+                for (int e = 0; e < E; ++e) mf[e] = (float)m[e];
+                strip_store<float, E>(static_cast<float*>(b.m_out) + i0, mf);
+            }
         } else {
             for (int e = 0; e < rem; ++e) {
                 b.v_out[i0 + e] = v[e];
@@ -1118,7 +1112,6 @@ int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, i
     // fedopt adam: p*(1-beta2); p has the pg dtype
     s.c2f = (float)s.c2;
     s.opt = serveropt;
-    s.store_mode = g_cfg.nt_store == 1 ? 1 : 0;
 
     if (upd_dtype == FA_F32 && old_dtype == FA_F32) return launch_fedopt<float, float, CF32>(b, s, updates, n, N, K, P, flags, st);
     if (upd_dtype == FA_BF16 && old_dtype == FA_F32) return launch_fedopt<bf16, float, CF32>(b, s, updates, n, N, K, P, flags, st);

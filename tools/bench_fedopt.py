@@ -36,7 +36,7 @@ def timed(fn, reps=5, warm=2):
     return sorted(s.elapsed_time(e) for s, e in ev)[reps // 2]
 
 
-def config4(P, K, opt, store_modes=(None,)):
+def config4(P, K, opt):
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(4)
     old32 = torch.randn(P, generator=g, device=dev)
@@ -49,26 +49,18 @@ def config4(P, K, opt, store_modes=(None,)):
     # round 1: old fp32, m/v None -> m fp32, v fp64
     r1 = lambda: ops.fedopt_step(old32, ups, ns, Ns, first=True, final=True, m_out=m32, v_out=v, out=out,  # noqa: E731
                                  serveropt=opt)
+    ms1 = timed(r1)
     b1 = K * P * 4 + P * 4 + P * (4 + 8 + 8)
+    old64 = out.clone()
+    m64 = m32.double()
+    r2 = lambda: ops.fedopt_step(old64, ups, ns, Ns, first=True, final=True, m_in=m64, m_out=m64, v_in=v, v_out=v,  # noqa: E731
+                                 out=out, serveropt=opt)
+    ms2 = timed(r2)
     b2 = P * (4 * K + 48)
-    old64 = m64 = None
-    for sm in store_modes:                      # None: library default; 0 / 1: plain / nt stores
-        if sm is not None:
-            ops.tune(nt_store=sm)
-        ms1 = timed(r1)
-        if old64 is None:
-            old64 = out.clone()
-            m64 = m32.double()
-        r2 = lambda: ops.fedopt_step(old64, ups, ns, Ns, first=True, final=True, m_in=m64, m_out=m64, v_in=v,  # noqa: E731
-                                     v_out=v, out=out, serveropt=opt)
-        ms2 = timed(r2)
-        for name, ms, b in (("round1", ms1, b1), ("steady", ms2, b2)):
-            line = {"config": "config4", "opt": opt, "phase": name, "params": P, "clients": K, "ms": ms,
-                    "params_per_s": K * P / ms * 1e3, "GBps": b / ms / 1e6, "frac_hbm": b / ms / 1e6 / PEAK,
-                    "alg_bytes": b}
-            if sm is not None:
-                line["store_mode"] = sm
-            print(json.dumps(line), flush=True)
+    for name, ms, b in (("round1", ms1, b1), ("steady", ms2, b2)):
+        print(json.dumps({"config": "config4", "opt": opt, "phase": name, "params": P, "clients": K, "ms": ms,
+                          "params_per_s": K * P / ms * 1e3, "GBps": b / ms / 1e6, "frac_hbm": b / ms / 1e6 / PEAK,
+                          "alg_bytes": b}), flush=True)
 
 
 def config5(P, K, W, pool, opt):
@@ -125,13 +117,12 @@ def main():
     ap.add_argument("--k5", type=int, default=128)
     ap.add_argument("--wave", type=int, default=8)
     ap.add_argument("--pool", type=int, default=16)
-    ap.add_argument("--store-ab", action="store_true", help="config 4 with plain / nt stores alternated")
     a = ap.parse_args()
     _abi.load()
     torch.cuda.set_device(0)
     if "4" in a.which:
         for opt in ("adam", "yogi", "adagrad"):
-            config4(a.p4, a.k4, opt, (0, 1, 0, 1) if a.store_ab else (None,))
+            config4(a.p4, a.k4, opt)
             torch.cuda.empty_cache()
     if "5" in a.which:
         config5(a.p5, a.k5, a.wave, a.pool, "yogi")
