@@ -821,7 +821,8 @@ struct FedAvgCfg {
     int read_per_lane = 16;   // fa_stream_read probe only
     int block_log = 8;        // pipelined kernel workgroup size 2^block_log (8, 9, 10)
     int sum_nostore = 0;      // fa_stream_sum probe: suppress the store (reads + adds only)
-    int nt_store = 0;         // pipelined kernel (S = 4, 256 threads) and fa_stream_sum: store mode 0 plain, 1 nt, 2 sc1
+    int nt_store = 1;         // pipelined kernel (S = 4, 256 threads) and fa_stream_sum: store mode 0 plain, 1 nt, 2 sc1;
+                              // nt: -3 % time at K = 8, neutral at K = 64 (profiles/r01_store_probe.log)
     int nt = 0;   // measured: cached loads beat non-temporal ones by ~3% (profiles/)
 };
 FedAvgCfg g_cfg;

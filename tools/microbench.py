@@ -94,7 +94,7 @@ def main():
                           "GBps": alg / med / 1e6}), flush=True)
     del slab, rows
     # reset defaults
-    ops.tune(strips=4, unroll=0, nt=0, fastdiv=1, lanetab=0, grid=0, block=256)
+    ops.tune(strips=4, unroll=0, nt=0, fastdiv=1, lanetab=0, grid=0, block=256, nt_store=1)
     # K = 8 (BASELINE config 2) and bf16 inputs
     med, _ = timed(lambda: ops.fedavg_fold(agg, ups[:8], ns[:8], Ns[:8], init=True))
     b8 = 8 * P * 4 + P * 4
@@ -128,7 +128,7 @@ def bf16_sweep(a):
         same = bool(torch.equal(agg.view(torch.int32), ref_out.view(torch.int32)))
         print(json.dumps({"kernel": "fedavg_bf16", "strips": S, "fastdiv": F, "block": B, "ms": med,
                           "GBps": bb / med / 1e6, "best_GBps": bb / best / 1e6, "identical": same}), flush=True)
-    ops.tune(strips=4, unroll=0, nt=0, fastdiv=1, lanetab=0, grid=0, block=256)
+    ops.tune(strips=4, unroll=0, nt=0, fastdiv=1, lanetab=0, grid=0, block=256, nt_store=1)
 
 
 if __name__ == "__main__":

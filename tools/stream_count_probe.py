@@ -2,7 +2,8 @@
 
 For K client buffers holding ~25.6 GB in total: stream_sum (the FedAvg traversal with one add)
 with its normal store, with the store suppressed (reads only), and with streaming
-(non-temporal) stores; then the real fp32 fold with normal vs streaming stores.
+(non-temporal) or write-through (sc1) stores; then the real fp32 fold with each store mode.
+Plain = store mode 0; the library default is 1 (nt).
 """
 import json
 import os
@@ -33,17 +34,17 @@ for K in (8, 64):
     by = K * P * 4 + P * 4
     ref = None
     for name, knobs, fn in (
-            ("stream_sum", {}, lambda: ops.stream_sum(out, bufs)),
+            ("stream_sum", {"nt_store": 0}, lambda: ops.stream_sum(out, bufs)),
             ("stream_sum no-store", {"sum_nostore": 1}, lambda: ops.stream_sum(out, bufs)),
             ("stream_sum nt-store", {"nt_store": 1}, lambda: ops.stream_sum(out, bufs)),
             ("stream_sum sc1-store", {"nt_store": 2}, lambda: ops.stream_sum(out, bufs)),
-            ("fold", {}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True)),
+            ("fold", {"nt_store": 0}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True)),
             ("fold nt-store", {"nt_store": 1}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True)),
             ("fold sc1-store", {"nt_store": 2}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True)),
-            ("fold", {}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True))):
+            ("fold", {"nt_store": 0}, lambda: ops.fedavg_fold(out, bufs, ns, Ns, init=True))):
         ops.tune(**knobs)
         med, best = timed(fn, reps=20)
-        ops.tune(sum_nostore=0, nt_store=0)
+        ops.tune(sum_nostore=0, nt_store=1)      # library defaults
         same = None
         if name.startswith("fold"):
             torch.cuda.synchronize()
