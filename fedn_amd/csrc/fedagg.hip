@@ -141,10 +141,33 @@ struct CF32 {            // float32 ufunc loops
 struct CF64 {            // float64 ufunc loops
     using V = double;
     using S = double;
-    __device__ static __forceinline__ V fold(V x, V y, S n, S N, double) {
+    // RN64(t/N) without a division when the host supplies r = RN64(1/N) (r == 0: IEEE
+    // division). q0 = RN(t*r) is within 1.5 ulp of z = t/N; one Markstein step
+    // q1 = RN(q0 + RN(t - q0*N)*r) makes it faithful (the error left is ~2^-52 of q0's);
+    // for a faithful q the remainder t - q*N is exact (FMA), and q2 = RN(q1 + (t - q1*N)*r)
+    // lands within |z - q1|*|N*r - 1| < 2^-53.x ulp of z, which is closer than z can be to a
+    // rounding midpoint without being one (|z - mid| >= ulp/(2*N') with N' < 2^53 N's odd
+    // significand; z is never exactly a midpoint), so q2 = RN(z). DESIGN.md §3.2b has the
+    // argument. The bounds |t| in [2^-600, 2^600] (host: |N| in [2^-60, 2^60]) keep every
+    // intermediate and remainder normal; other lanes (0, tiny, huge, inf, NaN) divide.
+    __device__ static __forceinline__ V div(V t, S N, double r) {
+        if (r != 0.0) {
+            const double a = __builtin_fabs(t);
+            if (a >= 0x1p-600 && a <= 0x1p600) {
+                double q = t * r;
+                double e = __builtin_fma(-q, N, t);
+                q = __builtin_fma(e, r, q);
+                e = __builtin_fma(-q, N, t);
+                return __builtin_fma(e, r, q);
+            }
+            if (a == 0.0) return t * r;   // signed zero: sign(t) * sign(N), as t / N
+        }
+        return t / N;
+    }
+    __device__ static __forceinline__ V fold(V x, V y, S n, S N, double r) {
         V t = y - x;
         t = n * t;
-        t = t / N;
+        t = div(t, N, r);
         return x + t;
     }
 };
@@ -548,12 +571,98 @@ __device__ __forceinline__ double np_sign(double d) {
     return d > 0.0 ? 1.0 : (d < 0.0 ? -1.0 : (d == 0.0 ? 0.0 : d));
 }
 
+// The server step for one strip of E elements (fedopt.py:151-258), from the folded
+// pseudo-gradient pg and the widened old model ov (OLD -> V is exact or the same conversion
+// numpy's `old * 1.0` makes, so (double)ov == old as numpy sees it). rem < E: ragged strip.
+template <class PG, int E>
+__device__ __forceinline__ void opt_final(const OptBuffers& b, const OptScalars& s, const typename PG::V (&pg)[E],
+                                          const typename PG::V (&ov)[E], int64_t i0, int rem) {
+    using V = typename PG::V;
+    constexpr bool PG32 = std::is_same<PG, CF32>::value;
+    const bool full = rem == E;
+    // ---- m (fedopt.py:173-176 and the two twins)
+    double m[E];
+    if (b.m_in_f64 < 0) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) m[e] = mul_pg<PG>((double)pg[e], s.c1, s.c1f);
+    } else if (b.m_in_f64 == 0) {
+        float mi[E];
+        const float* mp = static_cast<const float*>(b.m_in) + i0;
+        if (full) strip_load<float, E, false>(mp, mi);
+        else
+            for (int e = 0; e < E; ++e) mi[e] = e < rem ? mp[e] : 0.f;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const float a = mi[e] * s.b1f;                               // m*beta1 in f32
+            if constexpr (PG32) m[e] = (double)(a + (float)pg[e] * s.c1f);  // f32 + f32
+            else m[e] = (double)a + (double)pg[e] * s.c1;                   // f32 -> f64 add
+        }
+    } else {
+        double mi[E];
+        const double* mp = static_cast<const double*>(b.m_in) + i0;
+        if (full) strip_load<double, E, false>(mp, mi);
+        else
+            for (int e = 0; e < E; ++e) mi[e] = e < rem ? mp[e] : 0.0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) m[e] = mi[e] * s.b1 + mul_pg<PG>((double)pg[e], s.c1, s.c1f);
+    }
+    // ---- v (fedopt.py:170-171, 178-179 / 214-217 / 251-252)
+    double v[E];
+    if (b.v_in) {
+        const double* vp = b.v_in + i0;
+        if (full) strip_load<double, E, false>(vp, v);
+        else
+            for (int e = 0; e < E; ++e) v[e] = e < rem ? vp[e] : 0.0;
+    } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = s.tau2;
+    }
+    double o[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const V pv = pg[e];
+        const double p = (double)(V)(pv * pv);   // power(pg, 2) in the pg dtype
+        if (s.opt == FA_ADAM) {
+            v[e] = v[e] * s.b2 + mul_pg<PG>(p, s.c2, s.c2f);
+        } else if (s.opt == FA_YOGI) {
+            const double sg = np_sign(v[e] - p);
+            v[e] = v[e] + (sg * p) * s.nc2;
+        } else {
+            v[e] = v[e] + p;
+        }
+        const double sv = __builtin_sqrt(v[e]) + s.tau;
+        const double t = m[e] / sv;
+        o[e] = (double)ov[e] + t * s.lr;
+    }
+    // ---- stores
+    if (full) {
+        strip_store<double, E>(b.v_out + i0, v);
+        strip_store<double, E>(b.out + i0, o);
+        if (b.m_out_f64) strip_store<double, E>(static_cast<double*>(b.m_out) + i0, m);
+        else {
+            float mf[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) mf[e] = (float)m[e];
+            strip_store<float, E>(static_cast<float*>(b.m_out) + i0, mf);
+        }
+    } else {
+        for (int e = 0; e < rem; ++e) {
+            b.v_out[i0 + e] = v[e];
+            b.out[i0 + e] = o[e];
+            if (b.m_out_f64) static_cast<double*>(b.m_out)[i0 + e] = m[e];
+            else static_cast<float*>(b.m_out)[i0 + e] = (float)m[e];
+        }
+    }
+}
+
+// One lane's strip of E elements at i0 < P, clients batched kUnroll/2 at a time. (A
+// k_fedavg_pipe-style traversal — 2 or 4 strips per lane, next client in flight — measured
+// within noise of this one on configs[3]: profiles/r01_fedopt_ab.log)
 template <typename Y, typename OLD, class PG, int E, bool FIRST, bool FINAL, bool NT>
-__global__ void __launch_bounds__(kBlock)
-k_fedopt(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
+__device__ __forceinline__ void fedopt_strip(const OptBuffers& b, const OptScalars& s,
+                                             const ClientTable<typename PG::S>& tab, const int K, const int64_t P,
+                                             const int64_t i0) {
     using V = typename PG::V;   // float or double
-    const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * E;
-    if (i0 >= P) return;
     const int rem = (P - i0) < E ? (int)(P - i0) : E;
     const bool full = rem == E;
 
@@ -623,81 +732,15 @@ k_fedopt(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::
             for (int e = 0; e < rem; ++e) pgp[e] = pg[e];
         return;
     } else {
-        constexpr bool PG32 = std::is_same<PG, CF32>::value;
-        // ---- m (fedopt.py:173-176 and the two twins)
-        double m[E];
-        if (b.m_in_f64 < 0) {
-#pragma unroll
-            for (int e = 0; e < E; ++e) m[e] = mul_pg<PG>((double)pg[e], s.c1, s.c1f);
-        } else if (b.m_in_f64 == 0) {
-            float mi[E];
-            const float* mp = static_cast<const float*>(b.m_in) + i0;
-            if (full) strip_load<float, E, false>(mp, mi);
-            else
-                for (int e = 0; e < E; ++e) mi[e] = e < rem ? mp[e] : 0.f;
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const float a = mi[e] * s.b1f;                               // m*beta1 in f32
-                if constexpr (PG32) m[e] = (double)(a + (float)pg[e] * s.c1f);  // f32 + f32
-                else m[e] = (double)a + (double)pg[e] * s.c1;                   // f32 -> f64 add
-            }
-        } else {
-            double mi[E];
-            const double* mp = static_cast<const double*>(b.m_in) + i0;
-            if (full) strip_load<double, E, false>(mp, mi);
-            else
-                for (int e = 0; e < E; ++e) mi[e] = e < rem ? mp[e] : 0.0;
-#pragma unroll
-            for (int e = 0; e < E; ++e) m[e] = mi[e] * s.b1 + mul_pg<PG>((double)pg[e], s.c1, s.c1f);
-        }
-        // ---- v (fedopt.py:170-171, 178-179 / 214-217 / 251-252)
-        double v[E];
-        if (b.v_in) {
-            const double* vp = b.v_in + i0;
-            if (full) strip_load<double, E, false>(vp, v);
-            else
-                for (int e = 0; e < E; ++e) v[e] = e < rem ? vp[e] : 0.0;
-        } else {
-#pragma unroll
-            for (int e = 0; e < E; ++e) v[e] = s.tau2;
-        }
-        double o[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const V pv = pg[e];
-            const double p = (double)(V)(pv * pv);   // power(pg, 2) in the pg dtype
-            if (s.opt == FA_ADAM) {
-                v[e] = v[e] * s.b2 + mul_pg<PG>(p, s.c2, s.c2f);
-            } else if (s.opt == FA_YOGI) {
-                const double sg = np_sign(v[e] - p);
-                v[e] = v[e] + (sg * p) * s.nc2;
-            } else {
-                v[e] = v[e] + p;
-            }
-            const double sv = __builtin_sqrt(v[e]) + s.tau;
-            const double t = m[e] / sv;
-            o[e] = widen<OLD, double>(old[e]) + t * s.lr;
-        }
-        // ---- stores
-        if (full) {
-            strip_store<double, E>(b.v_out + i0, v);
-            strip_store<double, E>(b.out + i0, o);
-            if (b.m_out_f64) strip_store<double, E>(static_cast<double*>(b.m_out) + i0, m);
-            else {
-                float mf[E];
-#pragma unroll
-                for (int e = 0; e < E; ++e) mf[e] = (float)m[e];
-                strip_store<float, E>(static_cast<float*>(b.m_out) + i0, mf);
-            }
-        } else {
-            for (int e = 0; e < rem; ++e) {
-                b.v_out[i0 + e] = v[e];
-                b.out[i0 + e] = o[e];
-                if (b.m_out_f64) static_cast<double*>(b.m_out)[i0 + e] = m[e];
-                else static_cast<float*>(b.m_out)[i0 + e] = (float)m[e];
-            }
-        }
+        opt_final<PG, E>(b, s, pg, ov, i0, rem);
     }
+}
+
+template <typename Y, typename OLD, class PG, int E, bool FIRST, bool FINAL, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
+    const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * E;
+    if (i0 < P) fedopt_strip<Y, OLD, PG, E, FIRST, FINAL, NT>(b, s, tab, K, P, i0);
 }
 
 // ----------------------------------------------------------------------------
@@ -781,6 +824,7 @@ __global__ void __launch_bounds__(kBlock) k_stream_read(const u32x4* __restrict_
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 int g_fastdiv = 1;
+int g_fastdiv64 = 1;
 
 template <typename S>
 void fill_table(ClientTable<S>& t, const void* const* ptrs, const double* n, const double* N, int k0, int cnt) {
@@ -788,10 +832,17 @@ void fill_table(ClientTable<S>& t, const void* const* ptrs, const double* n, con
         t.ptr[j] = ptrs[k0 + j];
         t.n[j] = (S)n[k0 + j];
         t.N[j] = (S)N[k0 + j];
-        // reciprocal for CF32's division shortcut: only for N that keep every normal-range
-        // quotient normal (|N| < 2^28) and only when enabled
-        const float Nf = (float)N[k0 + j];
-        t.r[j] = (g_fastdiv && Nf != 0.0f && std::fabs(Nf) < 0x1p28f) ? 1.0 / (double)Nf : 0.0;
+        if constexpr (std::is_same<S, double>::value) {
+            // CF64's division shortcut: r = RN64(1/N) for 2^-60 <= |N| <= 2^60 (CWSUM ignores r,
+            // CRUN overwrites it)
+            const double Nd = N[k0 + j], a = std::fabs(Nd);
+            t.r[j] = (g_fastdiv64 && a >= 0x1p-60 && a <= 0x1p60) ? 1.0 / Nd : 0.0;
+        } else {
+            // reciprocal for CF32's division shortcut: only for N that keep every normal-range
+            // quotient normal (|N| < 2^28) and only when enabled
+            const float Nf = (float)N[k0 + j];
+            t.r[j] = (g_fastdiv && Nf != 0.0f && std::fabs(Nf) < 0x1p28f) ? 1.0 / (double)Nf : 0.0;
+        }
     }
     for (int j = cnt; j < kMaxK; ++j) {
         t.ptr[j] = nullptr;
@@ -1169,6 +1220,9 @@ int fa_tune(int knob, int value) {
             return FA_OK;
         case FA_TUNE_FASTDIV:
             g_fastdiv = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_FASTDIV64:
+            g_fastdiv64 = value ? 1 : 0;
             return FA_OK;
         default:
             return fail(FA_EINVAL, "fa_tune: unknown knob %d", knob);

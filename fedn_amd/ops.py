@@ -269,11 +269,11 @@ _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _a
           "fastdiv": _abi.FA_TUNE_FASTDIV, "lanetab": _abi.FA_TUNE_LANETAB,
           "grid": _abi.FA_TUNE_GRID, "read": _abi.FA_TUNE_READ,
           "block": _abi.FA_TUNE_BLOCK, "sum_nostore": _abi.FA_TUNE_SUM_NOSTORE,
-          "nt_store": _abi.FA_TUNE_NT_STORE}
+          "nt_store": _abi.FA_TUNE_NT_STORE, "fastdiv64": _abi.FA_TUNE_FASTDIV64}
 
 
 def tune(**knobs):
-    """Set fp32 FedAvg launch knobs (fa_tune): strips, unroll, nt, fastdiv. Results never change."""
+    """Set launch knobs (fa_tune): FedAvg strips, unroll, nt, fastdiv, ...; and fastdiv64 (CF64's division). Results never change (every setting is bit-identical)."""
     lib = _abi.load()
     for k, v in knobs.items():
         _abi.check(lib.fa_tune(_KNOBS[k], int(v)))

@@ -63,6 +63,51 @@ def config4(P, K, opt):
                           "alg_bytes": b}), flush=True)
 
 
+def config4_ab(P, K, opts, settings):
+    """Kernel A/B on configs[3]: fp64 division knob (fastdiv64 0 = IEEE, 1 = RN64(1/N) + Markstein),
+    round 1 and steady state, outputs checked bit-identical to the first setting's."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(4)
+    old32 = torch.randn(P, generator=g, device=dev)
+    ups = [torch.randn(P, generator=g, device=dev).mul_(0.01).add_(old32) for _ in range(K)]
+    ns = [int(v) for v in np.random.default_rng(4).integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
+    out = torch.empty(P, dtype=torch.float64, device=dev)
+    v = torch.empty(P, dtype=torch.float64, device=dev)
+    m32 = torch.empty(P, dtype=torch.float32, device=dev)
+    m64o = torch.empty(P, dtype=torch.float64, device=dev)
+    v2 = torch.empty(P, dtype=torch.float64, device=dev)
+    out2 = torch.empty(P, dtype=torch.float64, device=dev)
+    for opt in opts:
+        ref = None
+        # fixed steady-state inputs (old/m/v fp64) from one round-1 step with the default knobs
+        ops.tune(fastdiv64=0)
+        ops.fedopt_step(old32, ups, ns, Ns, first=True, final=True, m_out=m32, v_out=v, out=out, serveropt=opt)
+        old64, m64, v64 = out.clone(), m32.double(), v.clone()
+        for fd in settings:
+            ops.tune(fastdiv64=fd)
+            r1 = lambda: ops.fedopt_step(old32, ups, ns, Ns, first=True, final=True, m_out=m32, v_out=v,  # noqa: E731
+                                         out=out, serveropt=opt)
+            ms1 = timed(r1)
+            r2 = lambda: ops.fedopt_step(old64, ups, ns, Ns, first=True, final=True, m_in=m64, m_out=m64o,  # noqa: E731
+                                         v_in=v64, v_out=v2, out=out2, serveropt=opt)
+            ms2 = timed(r2)
+            got = [t.clone() for t in (out, m32, v, out2, m64o, v2)]
+            if ref is None:
+                ref = got
+            same = all(torch.equal(a.view(torch.int32) if a.dtype == torch.float32 else a.view(torch.int64),
+                                   b.view(torch.int32) if b.dtype == torch.float32 else b.view(torch.int64))
+                       for a, b in zip(got, ref))
+            b1 = K * P * 4 + P * 4 + P * (4 + 8 + 8)
+            b2 = P * (4 * K + 48)
+            print(json.dumps({"config": "config4", "opt": opt, "fastdiv64": fd,
+                              "round1_ms": ms1, "round1_GBps": b1 / ms1 / 1e6, "steady_ms": ms2,
+                              "steady_GBps": b2 / ms2 / 1e6, "steady_frac": b2 / ms2 / 1e6 / PEAK,
+                              "bit_identical_to_first": same}), flush=True)
+            del got
+    ops.tune(fastdiv64=1)
+
+
 def config5(P, K, W, pool, opt):
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(5)
@@ -117,9 +162,13 @@ def main():
     ap.add_argument("--k5", type=int, default=128)
     ap.add_argument("--wave", type=int, default=8)
     ap.add_argument("--pool", type=int, default=16)
+    ap.add_argument("--ab", action="store_true", help="A/B the FedOpt traversal and fp64 division knobs")
     a = ap.parse_args()
     _abi.load()
     torch.cuda.set_device(0)
+    if a.ab:
+        config4_ab(a.p4, a.k4, ("adam", "yogi", "adagrad"), [0, 1, 0, 1])
+        return
     if "4" in a.which:
         for opt in ("adam", "yogi", "adagrad"):
             config4(a.p4, a.k4, opt)

@@ -30,6 +30,9 @@ for s in $STEPS; do
     fedopt)
       timeout -k 10 900 python tools/bench_fedopt.py > "$OUT/fedopt.log" 2>&1; rc=$?
       echo "fedopt rc=$rc"; grep -v amdgpu.ids "$OUT/fedopt.log" | tail -8; [ $rc -eq 0 ] || exit $rc ;;
+    fedopt_ab)
+      timeout -k 10 900 python tools/bench_fedopt.py --ab > "$OUT/fedopt_ab.log" 2>&1; rc=$?
+      echo "fedopt_ab rc=$rc"; grep -v amdgpu.ids "$OUT/fedopt_ab.log" | tail -20; [ $rc -eq 0 ] || exit $rc ;;
     ingest)
       timeout -k 10 900 python tools/bench_ingest.py > "$OUT/ingest.log" 2>&1; rc=$?
       echo "ingest rc=$rc"; grep -v amdgpu.ids "$OUT/ingest.log" | tail -4; [ $rc -eq 0 ] || exit $rc ;;
