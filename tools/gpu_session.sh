@@ -33,6 +33,12 @@ for s in $STEPS; do
     fedopt_ab)
       timeout -k 10 900 python tools/bench_fedopt.py --ab > "$OUT/fedopt_ab.log" 2>&1; rc=$?
       echo "fedopt_ab rc=$rc"; grep -v amdgpu.ids "$OUT/fedopt_ab.log" | tail -20; [ $rc -eq 0 ] || exit $rc ;;
+    layout)
+      timeout -k 10 600 python tools/layout_probe.py > "$OUT/layout.log" 2>&1; rc=$?
+      echo "layout rc=$rc"; grep -v amdgpu.ids "$OUT/layout.log" | tail -14; [ $rc -eq 0 ] || exit $rc ;;
+    counters)
+      timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1; rc=$?
+      echo "counters rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     ingest)
       timeout -k 10 900 python tools/bench_ingest.py > "$OUT/ingest.log" 2>&1; rc=$?
       echo "ingest rc=$rc"; grep -v amdgpu.ids "$OUT/ingest.log" | tail -4; [ $rc -eq 0 ] || exit $rc ;;
@@ -42,6 +48,20 @@ for s in $STEPS; do
           python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 > "$GRAFT_REPO_ROOT/$OUT/pmc_$c.log" 2>&1; rc=$?
         cd "$GRAFT_REPO_ROOT"; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done ;;
+    pmcprobe)
+      PA="TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum TCP_UTCL1_THRASHING_STALL_sum TCP_UTCL1_STALL_MULTI_MISS_sum GRBM_GUI_ACTIVE"
+      PB="TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum"
+      PC="TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum"
+      for wl in read sum8 sum64 fold64; do
+        for ps in A B C; do
+          eval "ctrs=\$P$ps"
+          cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv \
+            -d "$GRAFT_REPO_ROOT/$OUT/pmcprobe/${wl}_$ps" -o run -- python3 "$GRAFT_REPO_ROOT/tools/pmc_probe.py" $wl \
+            > "$GRAFT_REPO_ROOT/$OUT/pmcprobe_${wl}_$ps.log" 2>&1; rc=$?
+          cd "$GRAFT_REPO_ROOT"; echo "pmcprobe $wl $ps rc=$rc"; [ $rc -eq 0 ] || exit $rc
+        done
+      done
+      python tools/pmc_probe_report.py "$OUT/pmcprobe" ;;
     prof)
       cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- \
         python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 --cpu-sample 0 > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1; rc=$?
