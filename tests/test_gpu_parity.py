@@ -304,6 +304,92 @@ def test_staging_ingest_fedopt_golden(name):
     st.close()
 
 
+def _mixed_round(rng, uh, st, shapes, K, host_at, model_id="global", base=None):
+    """K updates in FIFO order; those at positions in ``host_at`` bypass the ingest (host
+    arrays at combine time), the rest are staged into HBM on arrival (StagedModel)."""
+    if base is None:
+        base = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    ups = []
+    for k in range(K):
+        arrays = [(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base]
+        arrays.append(np.array([int(rng.integers(0, 1000))], dtype=np.int64))   # BatchNorm-like counter
+        n = int(rng.integers(1, 5001))
+        uh.submit(arrays, n, model_id=model_id, via=None if k in host_at else st)
+        ups.append((arrays, n))
+    return ups
+
+
+@pytest.mark.parametrize("K,host_at", [(150, {70, 71, 72, 100}), (64, set()), (65, set()), (3, {0})])
+def test_staging_batched_fedavg_mixed(K, host_at):
+    """Device-resident updates fold in batched multi-client launches (flush at 64), host
+    updates in between on arrival, the last batch chunk by chunk with overlapped D2H:
+    bit-identical to the oracle's sequential fold, int64 group included."""
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rng = np.random.default_rng(K)
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=None, device=DEV, workers=3)
+    ups = _mixed_round(rng, uh, st, [(300, 7), (1029,), (5,)], K, host_at)
+    model, data = get_aggregator("fedavg", st).combine_models(helper=None)
+    st.close()
+    want, nr = ref.fedavg_combine(ups)
+    assert data["nr_aggregated_models"] == nr == K
+    assert_lists_identical(model, want, f"K={K}")
+
+
+@pytest.mark.parametrize("K,host_at", [(150, {0, 90}), (70, set()), (20, {5})])
+def test_staging_batched_fedopt_mixed(K, host_at):
+    """FedOpt with staged updates: pending batches fold into pg (flush at 64) or straight into
+    the fused server step; two rounds with m / v carried; == the oracle."""
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rng = np.random.default_rng(1000 + K)
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=None, device=DEV, workers=3)
+    agg = get_aggregator("fedopt", st)
+    shapes = [(64, 33), (17,)]
+    old = [rng.standard_normal(s).astype(np.float32) for s in shapes] + [np.array([3], dtype=np.int64)]
+    state = ref.FedOptState()
+    params = {"serveropt": "yogi", "learning_rate": 1e-2}
+    for r in range(2):
+        gid = uh.put_global_model(old, f"g{r}")
+        ups = _mixed_round(rng, uh, st, shapes, K, host_at, model_id=gid,
+                           base=[o.astype(np.float32) for o in old[:2]])
+        model, data = agg.combine_models(helper=None, parameters=params)
+        want, _ = ref.fedopt_combine(state, ups, old, params)
+        assert data["nr_aggregated_models"] == K
+        assert_lists_identical(model, want, f"K={K} r{r}")
+        assert_lists_identical(agg.m, state.m, f"K={K} r{r} m")
+        assert_lists_identical(agg.v, state.v, f"K={K} r{r} v")
+        old = want
+    st.close()
+
+
+def test_staging_batched_large_chunked_d2h():
+    """A 24 M-element fp32 model (three 32 MiB D2H chunks) from 12 staged updates: the chunked
+    fold + overlapped D2H equals one whole-buffer fold on the device."""
+    from fedn_amd import ops
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rng = np.random.default_rng(24)
+    P, K = 24_000_000 + 77, 12
+    base = rng.standard_normal(P).astype(np.float32)
+    ups = [(base + np.float32(0.01) * rng.standard_normal(P).astype(np.float32)) for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=None, device=DEV, workers=4)
+    for u, n in zip(ups, ns):
+        uh.submit([u], n, via=st)
+    model, _ = get_aggregator("fedavg", st).combine_models(helper=None)
+    st.close()
+    want = torch.empty(P, dtype=torch.float32, device=DEV)
+    ops.fedavg_fold(want, [torch.from_numpy(u).to(DEV) for u in ups], ns, list(np.cumsum(ns)), init=True)
+    assert np.array_equal(model[0].view(np.uint32), want.cpu().numpy().view(np.uint32))
+
+
 @pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k8", "fedavg_int32_k3", "fedavg_skipbad_k4"])
 def test_staging_ingest_npz_bytes(name, native):

@@ -36,6 +36,9 @@ for s in $STEPS; do
     layout)
       timeout -k 10 600 python tools/layout_probe.py > "$OUT/layout.log" 2>&1; rc=$?
       echo "layout rc=$rc"; grep -v amdgpu.ids "$OUT/layout.log" | tail -14; [ $rc -eq 0 ] || exit $rc ;;
+    roundend)
+      timeout -k 10 600 python tools/bench_roundend.py > "$OUT/roundend.log" 2>&1; rc=$?
+      echo "roundend rc=$rc"; grep -v amdgpu.ids "$OUT/roundend.log" | tail -6; [ $rc -eq 0 ] || exit $rc ;;
     counters)
       timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1; rc=$?
       echo "counters rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
