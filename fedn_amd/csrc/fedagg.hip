@@ -119,16 +119,17 @@ struct CF32 {            // float32 ufunc loops
         }
         if (r != 0.0) {
             V q[E];
-            bool tiny = false;
+            bool small = false;   // |t| < 2^-98, zeros included: one compare per element
 #pragma unroll
             for (int e = 0; e < E; ++e) {
                 q[e] = (float)((double)t[e] * r);
-                tiny |= __builtin_fabsf(t[e]) < 0x1p-98f && t[e] != 0.0f;
+                small |= __builtin_fabsf(t[e]) < 0x1p-98f;
             }
-            if (__builtin_expect(tiny, 0)) {
+            if (__builtin_expect(small, 0)) {
+                // zero lanes already hold the right signed zero (t*r); only nonzero tiny t divide
 #pragma unroll
                 for (int e = 0; e < E; ++e)
-                    if (__builtin_fabsf(t[e]) < 0x1p-98f) q[e] = t[e] / N;
+                    if (__builtin_fabsf(t[e]) < 0x1p-98f && t[e] != 0.0f) q[e] = t[e] / N;
             }
 #pragma unroll
             for (int e = 0; e < E; ++e) x[e] = x[e] + q[e];
