@@ -58,6 +58,79 @@ class StagedModel:
         return iter(self.host)
 
 
+class ShardedStagedModel:
+    """One decoded client update resident in HBM as parameter slices over several devices
+    (Layout.shard_geometry, the layout of multidev.py): ``bufs[d]`` holds device d's [lo, hi)
+    of every dtype group, ready once ``ready[d]`` has fired. The multi-device pipelines fold it
+    in place; ``host`` reassembles host arrays only when needed (a round's sole update)."""
+
+    __slots__ = ("layout", "devices", "bounds", "dev_off", "bufs", "ready", "_host")
+
+    def __init__(self, layout, devices, bufs, ready, host=None):
+        self.layout, self.devices, self.bufs, self.ready, self._host = layout, list(devices), bufs, ready, host
+        self.bounds, self.dev_off, _ = layout.shard_geometry(len(self.devices))
+
+    def view(self, d, dt):
+        """Device d's slice of group ``dt`` (flat torch view)."""
+        lo, hi = self.bounds[dt][d]
+        off = self.dev_off[d][dt]
+        return self.bufs[d][off:off + (hi - lo) * dt.itemsize].view(_torch_dtype(dt))
+
+    @property
+    def host(self):
+        if self._host is None:
+            out = [None] * len(self.layout.shapes)
+            for dt in self.layout.groups:
+                flat = np.empty(self.layout.group_elems[dt], dtype=dt)
+                for d in range(len(self.devices)):
+                    lo, hi = self.bounds[dt][d]
+                    if hi > lo:
+                        self.ready[d].synchronize()
+                        flat[lo:hi] = self.view(d, dt).cpu().numpy()
+                self.layout.unpack_group(flat, dt, out, copy=False)
+            self._host = out
+        return self._host
+
+    def __len__(self):
+        return len(self.layout.shapes)
+
+    def __getitem__(self, i):
+        return self.host[i]
+
+    def __iter__(self):
+        return iter(self.host)
+
+
+def _torch_dtype(dt):
+    from .ops import torch_dtype
+    return torch_dtype(dt)
+
+
+def stage_sharded(layout, pinned, devices, streams, host=None):
+    """Copy each device's slices of a pinned, layout-packed update (``pinned``: uint8 tensor)
+    to that device on ``streams[d]`` (every device over its own link, concurrently); returns a
+    :class:`ShardedStagedModel` once the copies no longer read ``pinned``."""
+    bounds, dev_off, dev_bytes = layout.shard_geometry(len(devices))
+    bufs, ready = [], []
+    for d, dv in enumerate(devices):
+        with torch.cuda.device(dv):
+            buf = torch.empty(dev_bytes[d], dtype=torch.uint8, device=dv)
+            with torch.cuda.stream(streams[d]):
+                for dt in layout.groups:
+                    lo, hi = bounds[dt][d]
+                    if hi > lo:
+                        g0, o = layout.group_byte_offset[dt], dev_off[d][dt]
+                        buf[o:o + (hi - lo) * dt.itemsize].copy_(
+                            pinned[g0 + lo * dt.itemsize:g0 + hi * dt.itemsize], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(streams[d])
+        bufs.append(buf)
+        ready.append(ev)
+    for ev in ready:
+        ev.synchronize()
+    return ShardedStagedModel(layout, devices, bufs, ready, host)
+
+
 def stage_arrays(arrays, device, stream):
     """Pack host ``arrays`` into pinned memory and copy them to a new device buffer on
     ``stream``; returns a :class:`StagedModel` (the H2D may still be in flight)."""
@@ -101,12 +174,19 @@ class StagingUpdateHandler:
     native_decode  take the raw npz bytes (UpdateHandler.load_model_update_byte,
              updatehandler.py:119-144) and inflate them with fedn_amd.codec straight into
              pinned memory in the pipelines' layout
+    devices  several devices (argument or FEDN_AMD_DEVICES, as the aggregators use): every
+             update is staged as parameter slices over them (ShardedStagedModel), each device
+             receiving only its slice over its own link, for multidev.py's pipelines
     Every attribute not defined here (``model_updates``, ``next_model_update``, ``load_model``,
     ``waitforit``, ...) is the wrapped handler's.
     """
 
-    def __init__(self, inner, helper=None, device=None, workers=4, native_decode=True):
+    def __init__(self, inner, helper=None, device=None, workers=4, native_decode=True, devices=None):
         self.inner = inner
+        if devices is None:
+            from .aggregators.fedavg import env_devices
+            devices = env_devices()
+        self.devices = [torch.device(d) for d in devices] if devices and len(devices) > 1 else None
         self.native_decode = native_decode
         self.helper = helper
         self.device = torch.device(device) if device is not None else None
@@ -124,15 +204,37 @@ class StagingUpdateHandler:
             self.device = default_device()
         return self.device
 
-    def _stream(self):
-        tid = threading.get_ident()
+    def _stream(self, dev=None):
+        dev = dev if dev is not None else self._device()
+        key = (threading.get_ident(), str(dev))
         with self._lock:
-            st = self._streams.get(tid)
+            st = self._streams.get(key)
             if st is None:
-                st = self._streams[tid] = torch.cuda.Stream(self._device())
+                st = self._streams[key] = torch.cuda.Stream(dev)
         return st
 
+    def _stage_sharded(self, model_update):
+        streams = [self._stream(dv) for dv in self.devices]
+        if self.native_decode and hasattr(self.inner, "load_model_update_byte"):
+            try:
+                data, metadata = self.inner.load_model_update_byte(model_update)
+            except Exception:  # noqa: BLE001 — not held as bytes: decode through the helper
+                data = None
+            if data is not None:
+                from . import codec
+                layout, pinned = codec.load_npz_into_layout(
+                    data, lambda nbytes: torch.empty(nbytes, dtype=torch.uint8, pin_memory=True))
+                return stage_sharded(layout, pinned, self.devices, streams), metadata
+        arrays, metadata = self.inner.load_model_update(model_update, self.helper)
+        arrays = [np.asarray(a) for a in arrays]
+        layout = Layout.of(arrays)
+        pinned = torch.empty(layout.nbytes, dtype=torch.uint8, pin_memory=True)
+        layout.pack(arrays, pinned.numpy())
+        return stage_sharded(layout, pinned, self.devices, streams, arrays), metadata
+
     def _stage(self, model_update):
+        if self.devices:
+            return self._stage_sharded(model_update)
         dev = self._device()
         if self.native_decode and hasattr(self.inner, "load_model_update_byte"):
             try:

@@ -69,6 +69,24 @@ class Layout:
         self.nbytes = max(off, ALIGN)
         self.nparams = sum(self.sizes)
 
+    def shard_geometry(self, ndev):
+        """Parameter-slice sharding over ``ndev`` devices (multidev.py, ingest.py):
+        ``bounds[dt][d]`` = device d's [lo, hi) of group dt (4 KiB-aligned,
+        sharded.shard_bounds), ``dev_off[d][dt]`` = byte offset of that slice in device d's
+        buffer (each slice ALIGN-aligned), ``dev_bytes[d]`` = size of device d's buffer."""
+        from .sharded import shard_bounds
+        bounds = {dt: shard_bounds(self.group_elems[dt], ndev) for dt in self.groups}
+        dev_off, dev_bytes = [], []
+        for d in range(ndev):
+            off, offs = 0, {}
+            for dt in self.groups:
+                lo, hi = bounds[dt][d]
+                offs[dt] = off
+                off += _round_up((hi - lo) * dt.itemsize, ALIGN)
+            dev_off.append(offs)
+            dev_bytes.append(max(off, ALIGN))
+        return bounds, dev_off, dev_bytes
+
     @classmethod
     def of(cls, arrays):
         arrays = [np.asarray(a) for a in arrays]

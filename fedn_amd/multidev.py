@@ -1,26 +1,34 @@
 """One combiner process, several GPUs: parameter-slice sharding without a collective.
 
 FEDn runs one combiner process per node (combiner.py). With several MI355X in that node the
-natural layout is the one of sharded.py, inside one process: every update is packed ONCE
-into pinned host memory, device d copies only its 4 KiB-aligned slice of every dtype group
-over its own PCIe link (H2D in parallel across devices), folds that slice with the same
-kernel and client table, and at the end copies its slice of the aggregate straight into
-the host result buffer. The host result is the concatenation of the slices, bit-identical
-to one device. No xGMI traffic: the consumer of the model is the host
+natural layout is the one of sharded.py, inside one process: device d owns a 4 KiB-aligned
+slice of every dtype group (Layout.shard_geometry), folds that slice of every update with the
+same kernel and client table, and copies its slice of the aggregate straight into the host
+result buffer over its own link. The host result is the concatenation of the slices,
+bit-identical to one device. No xGMI traffic: the consumer of the model is the host
 (roundhandler.py:465-468).
+
+Updates reach the devices two ways:
+* host arrays: packed ONCE into pinned host memory, device d copies only its slice (H2D in
+  parallel across devices), folded on arrival;
+* already sliced over these devices by the streaming ingest
+  (ingest.StagingUpdateHandler(devices=...) -> ShardedStagedModel): they queue and fold
+  together in one multi-client launch per device (flushed at staging.BATCH), and the round's
+  last launch is chunked so that each chunk's D2H — every device over its own link —
+  overlaps the next chunk.
 
 FedOpt shards the same way (ShardedFedOptPipeline): device d keeps ITS slice of the global
 model, the pseudo-gradient and the server state m / v resident across rounds
 (ShardedFedOptState), so a session's optimizer state is spread over the node's HBM and never
-moves between devices.
+moves between devices. The global model streams in through a pinned ring (no whole-model
+pinning), chunk by chunk with the server step when every update was device-resident.
 """
 import torch
 
 from . import ops
-from .ingest import StagedModel
-from .layout import ALIGN, Layout
-from .staging import check_fedopt_dtypes, old_groups
-from .sharded import shard_bounds
+from .ingest import ShardedStagedModel, StagedModel
+from .layout import Layout
+from .staging import BATCH, HostStreamer, check_fedopt_dtypes, chunks, old_members
 
 
 class _DevSlot:
@@ -48,39 +56,60 @@ def gather_group(layout, bounds, devices, per_dev, dt):
     return flat.numpy()   # a new pinned block owned by the caller (see staging._Pipeline._to_host)
 
 
+def _same_devices(a, b):
+    return [str(torch.device(d)) for d in a] == [str(torch.device(d)) for d in b]
+
+
+def _host_arrays(arrays):
+    """Host arrays of an update staged for other devices (re-sharded from the host copy)."""
+    return arrays.host if isinstance(arrays, (StagedModel, ShardedStagedModel)) else arrays
+
+
 class _ShardedStaging:
-    """Host slots packed once, each device's slice of every group copied over its own link."""
+    """Host slots packed once, each device's slice of every group copied over its own link; or
+    updates already sliced over these devices (ShardedStagedModel), used in place."""
 
     def __init__(self, devices, layout, nslots):
         self.devices = [torch.device(d) for d in devices]
         self.layout = layout
-        D = len(self.devices)
-        # per device: its [lo, hi) of every group and the byte offset of that slice in its slot
-        self.bounds = {dt: shard_bounds(self.layout.group_elems[dt], D) for dt in self.layout.groups}
-        self.dev_off, self.dev_bytes = [], []
-        for d in range(D):
-            off, offs = 0, {}
-            for dt in self.layout.groups:
-                lo, hi = self.bounds[dt][d]
-                offs[dt] = off
-                off += -(-((hi - lo) * dt.itemsize) // ALIGN) * ALIGN
-            self.dev_off.append(offs)
-            self.dev_bytes.append(max(off, ALIGN))
+        self.bounds, self.dev_off, self.dev_bytes = layout.shard_geometry(len(self.devices))
         self.compute = [torch.cuda.current_stream(dv) for dv in self.devices]
         self.copy = [torch.cuda.Stream(dv) for dv in self.devices]
+        self.d2h = [torch.cuda.Stream(dv) for dv in self.devices]
         self.nslots = nslots
-        self.host = [torch.empty(self.layout.nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(nslots)]
+        self.host = None                               # pinned host slots: on the first host update
         self.host_done = [None] * nslots               # per host slot: the H2D events reading it
-        self.dslots = [[_DevSlot(self.dev_bytes[d], self.devices[d]) for _ in range(nslots)] for d in range(D)]
+        self.dslots = None
         self._next = 0
         self.reserved = set()
+        self.pending = []                              # resident updates not folded yet: (model, n, N)
+
+    def _ensure_slots(self):
+        if self.host is None:
+            self.host = [torch.empty(self.layout.nbytes, dtype=torch.uint8, pin_memory=True)
+                         for _ in range(self.nslots)]
+            self.dslots = [[_DevSlot(self.dev_bytes[d], self.devices[d]) for _ in range(self.nslots)]
+                           for d in range(len(self.devices))]
 
     def _dev_view(self, d, slot, dt):
         lo, hi = self.bounds[dt][d]
         off = self.dev_off[d][dt]
         return self.dslots[d][slot].dev[off:off + (hi - lo) * dt.itemsize].view(ops.torch_dtype(dt))
 
+    def _view(self, d, src, dt):
+        """Device d's slice of group dt of an update: a host-staged slot or a ShardedStagedModel."""
+        return self._dev_view(d, src, dt) if isinstance(src, int) else src.view(d, dt)
+
+    def _resident(self, arrays):
+        return isinstance(arrays, ShardedStagedModel) and _same_devices(arrays.devices, self.devices)
+
+    def _accept(self, model):
+        """Order every device's compute stream after the resident update's H2D."""
+        for d in range(len(self.devices)):
+            self.compute[d].wait_event(model.ready[d])
+
     def _stage(self, arrays):
+        self._ensure_slots()
         for _ in range(self.nslots):
             s = self._next
             self._next = (self._next + 1) % self.nslots
@@ -109,8 +138,28 @@ class _ShardedStaging:
         self.host_done[s] = evs
         return s
 
-    def _gather_group(self, per_dev, dt):
-        return gather_group(self.layout, self.bounds[dt], self.devices, per_dev, dt)
+    def _to_host_chunks(self, dt, per_dev, fold_chunk, rdtype):
+        """New pinned host array of group ``dt``: device d's slice ``per_dev[d]`` is D2H'd into
+        its [lo, hi) chunk by chunk on the device's d2h stream, ``fold_chunk(d, clo, chi)`` (if
+        given) enqueued on its compute stream first, so each chunk's D2H overlaps the next."""
+        flat = torch.empty(self.layout.group_elems[dt], dtype=rdtype, pin_memory=True)
+        for d, dv in enumerate(self.devices):
+            lo, hi = self.bounds[dt][d]
+            src = per_dev[d]
+            with torch.cuda.device(dv):
+                for clo, chi in chunks(hi - lo, src.element_size()):
+                    if fold_chunk is not None:
+                        fold_chunk(d, clo, chi)
+                    ev = torch.cuda.Event()
+                    ev.record(self.compute[d])
+                    self.d2h[d].wait_event(ev)
+                    with torch.cuda.stream(self.d2h[d]):
+                        flat[lo + clo:lo + chi].copy_(src[clo:chi], non_blocking=True)
+        return flat
+
+    def _sync_d2h(self):
+        for st in self.d2h:
+            st.synchronize()
 
     def timings(self):
         return {}
@@ -120,47 +169,102 @@ class ShardedFedAvgPipeline(_ShardedStaging):
     """FedAvgPipeline over ``devices`` (a list; the same device may repeat, e.g. in tests)."""
 
     def __init__(self, devices, first_arrays, nslots=3):
-        if isinstance(first_arrays, StagedModel):
-            first_arrays = first_arrays.host     # staged on one device: re-shard from the host copy
-        super().__init__(devices, Layout.of(first_arrays), nslots)
+        if isinstance(first_arrays, ShardedStagedModel) and _same_devices(first_arrays.devices, devices):
+            super().__init__(devices, first_arrays.layout, nslots)
+            self._accept(first_arrays)
+            self.first = first_arrays
+        else:
+            first_arrays = _host_arrays(first_arrays)
+            super().__init__(devices, Layout.of(first_arrays), nslots)
+            self.first = self._stage(first_arrays)
+            self.reserved = {self.first}
         self.first_arrays = first_arrays
-        self.first = self._stage(first_arrays)
-        self.reserved = {self.first}
         self.nfolds = 0
+        self.agg_started = False
         self.agg = [dict() for _ in self.devices]
 
     def add(self, arrays, n, N):
-        if isinstance(arrays, StagedModel):
-            arrays = arrays.host
-        self.layout.check(arrays)
-        for dt in self.layout.groups:
+        resident = self._resident(arrays)
+        if resident:
+            self.layout.check_layout(arrays.layout)
+        else:
+            arrays = _host_arrays(arrays)
+            self.layout.check(arrays)
+        for dt in self.layout.groups:           # refuse before touching device state
             ops.fa_dtype(ops.torch_dtype(dt))
-        s = self._stage(arrays)
-        for d, dv in enumerate(self.devices):
-            for dt in self.layout.groups:
-                y = self._dev_view(d, s, dt)
-                if self.nfolds == 0:
-                    x0 = self._dev_view(d, self.first, dt)
-                    acc = torch.empty(y.numel(), dtype=ops.fold_result_dtype(y.dtype, y.dtype), device=dv)
-                    if y.numel():
-                        ops.fedavg_fold(acc, [x0, y], [0.0, n], [1.0, N], init=True, stream=self.compute[d])
-                    self.agg[d][dt] = acc
-                elif y.numel():
-                    ops.fedavg_fold(self.agg[d][dt], [y], [n], [N], init=False, stream=self.compute[d])
-            self.dslots[d][s].consumed.record(self.compute[d])
-            if self.nfolds == 0:
-                self.dslots[d][self.first].consumed.record(self.compute[d])
-        if self.nfolds == 0:
-            self.reserved = set()
+        if resident:
+            self._accept(arrays)
+            self.pending.append((arrays, n, N))
+            if len(self.pending) >= BATCH:
+                self._flush()
+        else:
+            self._flush()
+            s = self._stage(arrays)
+            self._fold_all([(s, n, N)])
+            for d in range(len(self.devices)):
+                self.dslots[d][s].consumed.record(self.compute[d])
         self.nfolds += 1
+
+    def _agg(self, d, dt):
+        if dt not in self.agg[d]:
+            t = ops.torch_dtype(dt)
+            lo, hi = self.bounds[dt][d]
+            self.agg[d][dt] = torch.empty(hi - lo, dtype=ops.fold_result_dtype(t, t), device=self.devices[d])
+        return self.agg[d][dt]
+
+    def _fold_dev(self, d, dt, entries, init, clo, chi):
+        """Enqueue device d's fold of ``entries`` over elements [clo, chi) of its slice of ``dt``."""
+        if chi <= clo:
+            return
+        ys = [self._view(d, e[0], dt)[clo:chi] for e in entries]
+        ns = [e[1] for e in entries]
+        Ns = [e[2] for e in entries]
+        acc = self._agg(d, dt)[clo:chi]
+        if init:                                # agg := first update, then fold (fedavg.py:127-133)
+            x0 = self._view(d, self.first, dt)[clo:chi]
+            ops.fedavg_fold(acc, [x0] + ys, [0.0] + ns, [1.0] + Ns, init=True, stream=self.compute[d])
+        else:
+            ops.fedavg_fold(acc, ys, ns, Ns, init=False, stream=self.compute[d])
+
+    def _folded(self):
+        if not self.agg_started and isinstance(self.first, int):
+            for d in range(len(self.devices)):
+                self.dslots[d][self.first].consumed.record(self.compute[d])
+            self.reserved = set()
+        self.agg_started = True
+
+    def _fold_all(self, entries):
+        init = not self.agg_started
+        for d in range(len(self.devices)):
+            for dt in self.layout.groups:
+                lo, hi = self.bounds[dt][d]
+                self._fold_dev(d, dt, entries, init, 0, hi - lo)
+        self._folded()
+
+    def _flush(self):
+        if self.pending:
+            entries, self.pending = self.pending, []
+            self._fold_all(entries)
 
     def result(self):
         if self.nfolds == 0:
-            return self.first_arrays
+            return _host_arrays(self.first_arrays)     # `model = model_next` alias (fedavg.py:127-128)
+        entries, self.pending = self.pending, []
+        init = not self.agg_started
+        flats = {}
+        for dt in self.layout.groups:
+            t = ops.torch_dtype(dt)
+            fold = None
+            if entries:
+                fold = lambda d, clo, chi, dt=dt: self._fold_dev(d, dt, entries, init, clo, chi)  # noqa: E731
+            per_dev = [self._agg(d, dt) for d in range(len(self.devices))]
+            flats[dt] = self._to_host_chunks(dt, per_dev, fold, ops.fold_result_dtype(t, t))
+        if entries:
+            self._folded()
+        self._sync_d2h()
         out = [None] * len(self.layout.shapes)
         for dt in self.layout.groups:
-            owned = self._gather_group([a[dt] for a in self.agg], dt)
-            self.layout.unpack_group(owned, dt, out, copy=False)
+            self.layout.unpack_group(flats[dt].numpy(), dt, out, copy=False)
         return out
 
 
@@ -199,38 +303,84 @@ class ShardedFedOptPipeline(_ShardedStaging):
     every device's slice, each with its slice of old / pg / m / v resident in its HBM."""
 
     def __init__(self, devices, old_arrays, first_arrays, nslots=2):
-        if isinstance(first_arrays, StagedModel):
-            first_arrays = first_arrays.host
-        super().__init__(devices, Layout.of(first_arrays), nslots)
-        self.old = [dict() for _ in self.devices]
-        for dt, flat in old_groups(self.layout, old_arrays).items():
-            for d, dv in enumerate(self.devices):
+        if isinstance(first_arrays, ShardedStagedModel) and _same_devices(first_arrays.devices, devices):
+            layout = first_arrays.layout
+        else:
+            layout = Layout.of(_host_arrays(first_arrays))
+        super().__init__(devices, layout, nslots)
+        # the global model reaches each device lazily through a pinned ring: whole (when a host
+        # update must fold into pg) or chunk by chunk inside the server step (H2D || step || D2H)
+        self.old_host = old_members(layout, old_arrays)
+        self.old = []
+        for d, dv in enumerate(self.devices):
+            per = {}
+            for dt, (odt, _) in self.old_host.items():
                 lo, hi = self.bounds[dt][d]
-                src = torch.from_numpy(flat[lo:hi]).pin_memory()
-                with torch.cuda.device(dv):
-                    self.old[d][dt] = src.to(dv, non_blocking=True)
+                per[dt] = torch.empty(hi - lo, dtype=ops.torch_dtype(odt), device=dv)
+            self.old.append(per)
+        self.old_ready = set()
+        self.streamer = HostStreamer()
         self.pg = [dict() for _ in self.devices]
+        self.pg_started = False
         self.nfolds = 0
 
     def add(self, arrays, n, N):
-        if isinstance(arrays, StagedModel):
-            arrays = arrays.host
-        self.layout.check(arrays)
+        resident = self._resident(arrays)
+        if resident:
+            self.layout.check_layout(arrays.layout)
+        else:
+            arrays = _host_arrays(arrays)
+            self.layout.check(arrays)
         check_fedopt_dtypes(self.layout)
-        s = self._stage(arrays)
-        first = self.nfolds == 0
-        for d, dv in enumerate(self.devices):
-            for dt in self.layout.groups:
-                y = self._dev_view(d, s, dt)
-                old = self.old[d][dt]
-                if first:
-                    pg_dt, _ = ops.fedopt_dtypes(y.dtype, old.dtype, None)
-                    self.pg[d][dt] = torch.empty(y.numel(), dtype=pg_dt, device=dv)
-                if y.numel():
-                    ops.fedopt_step(old, [y], [n], [N], first=first, final=False, pg=self.pg[d][dt],
-                                    stream=self.compute[d])
-            self.dslots[d][s].consumed.record(self.compute[d])
+        if resident:
+            self._accept(arrays)
+            self.pending.append((arrays, n, N))
+            if len(self.pending) >= BATCH:
+                self._flush()
+        else:
+            self._flush()
+            s = self._stage(arrays)
+            self._fold_pg([(s, n, N)])
+            for d in range(len(self.devices)):
+                self.dslots[d][s].consumed.record(self.compute[d])
         self.nfolds += 1
+
+    def _pg(self, d, dt):
+        if dt not in self.pg[d]:
+            lo, hi = self.bounds[dt][d]
+            pg_dt, _ = ops.fedopt_dtypes(ops.torch_dtype(dt), self.old[d][dt].dtype, None)
+            self.pg[d][dt] = torch.empty(hi - lo, dtype=pg_dt, device=self.devices[d])
+        return self.pg[d][dt]
+
+    def _h2d_old(self, d, dt, clo, chi):
+        """Enqueue the H2D of elements [clo, chi) of device d's slice of the global model."""
+        odt, parts = self.old_host[dt]
+        lo = self.bounds[dt][d][0]
+        return self.streamer.h2d(parts, odt, lo + clo, lo + chi, self.old[d][dt][clo:chi], self.copy[d])
+
+    def _old_all(self, dt):
+        if dt not in self.old_ready:
+            for d in range(len(self.devices)):
+                lo, hi = self.bounds[dt][d]
+                self.compute[d].wait_event(self._h2d_old(d, dt, 0, hi - lo))
+            self.old_ready.add(dt)
+
+    def _fold_pg(self, entries):
+        for dt in self.layout.groups:
+            self._old_all(dt)
+            for d in range(len(self.devices)):
+                lo, hi = self.bounds[dt][d]
+                pg = self._pg(d, dt)
+                if hi > lo:
+                    ys = [self._view(d, e[0], dt) for e in entries]
+                    ops.fedopt_step(self.old[d][dt], ys, [e[1] for e in entries], [e[2] for e in entries],
+                                    first=not self.pg_started, final=False, pg=pg, stream=self.compute[d])
+        self.pg_started = True
+
+    def _flush(self):
+        if self.pending:
+            entries, self.pending = self.pending, []
+            self._fold_pg(entries)
 
     def server_step(self, state, params):
         opt = params["serveropt"]
@@ -239,30 +389,51 @@ class ShardedFedOptPipeline(_ShardedStaging):
         sig = (self.layout.signature(), tuple(str(d) for d in self.devices))
         if state.signature is not None and state.signature != sig:
             raise ValueError("model layout or devices changed between rounds; FedOpt state (m, v) does not match")
+        # per device and group, one fused launch: pending (resident) updates folded into the
+        # pseudo-gradient in registers (FIRST when pg holds nothing yet) and the server step,
+        # chunked so that the global model's H2D, the step and the result's D2H overlap
+        entries, self.pending = self.pending, []
+        first = not self.pg_started
+        ns, Ns = [e[1] for e in entries], [e[2] for e in entries]
         new_m = [dict() for _ in self.devices]
         new_v = [dict() for _ in self.devices]
-        outs = [dict() for _ in self.devices]
-        for d, dv in enumerate(self.devices):
-            for dt in self.layout.groups:
-                old, pg = self.old[d][dt], self.pg[d][dt]
+        flats = {}
+        sl = lambda t, lo, hi: None if t is None else t[lo:hi]  # noqa: E731
+        for dt in self.layout.groups:
+            stream_old = dt not in self.old_ready
+            ctx = []
+            for d, dv in enumerate(self.devices):
+                lo, hi = self.bounds[dt][d]
+                P = hi - lo
+                old = self.old[d][dt]
                 m_in = state.m[d][dt] if state.m is not None else None
                 v_in = state.v[d][dt] if state.v is not None else None
                 _, m_dt = ops.fedopt_dtypes(ops.torch_dtype(dt), old.dtype, None if m_in is None else m_in.dtype)
-                P = pg.numel()
                 m_out = m_in if (m_in is not None and m_in.dtype == m_dt) else torch.empty(P, dtype=m_dt, device=dv)
                 v_out = v_in if v_in is not None else torch.empty(P, dtype=torch.float64, device=dv)
                 out = torch.empty(P, dtype=torch.float64, device=dv)
-                if P:
-                    ops.fedopt_step(old, [], [], [], first=False, final=True, pg=pg, m_in=m_in, m_out=m_out,
-                                    v_in=v_in, v_out=v_out, out=out, serveropt=opt,
-                                    learning_rate=params["learning_rate"], beta1=params["beta1"],
-                                    beta2=params["beta2"], tau=params["tau"], stream=self.compute[d],
-                                    upd_dtype=ops.torch_dtype(dt))
-                new_m[d][dt], new_v[d][dt], outs[d][dt] = m_out, v_out, out
+                pg = self._pg(d, dt) if (not first or len(entries) > BATCH) else None
+                new_m[d][dt], new_v[d][dt] = m_out, v_out
+                ctx.append((old, pg, m_in, m_out, v_in, v_out, out))
+
+            def step(d, clo, chi, dt=dt, ctx=ctx, stream_old=stream_old):
+                old, pg, m_in, m_out, v_in, v_out, out = ctx[d]
+                if stream_old:
+                    self.compute[d].wait_event(self._h2d_old(d, dt, clo, chi))
+                ys = [self._view(d, e[0], dt)[clo:chi] for e in entries]
+                ops.fedopt_step(old[clo:chi], ys, ns, Ns, first=first, final=True, pg=sl(pg, clo, chi),
+                                m_in=sl(m_in, clo, chi), m_out=m_out[clo:chi], v_in=sl(v_in, clo, chi),
+                                v_out=v_out[clo:chi], out=out[clo:chi], serveropt=opt,
+                                learning_rate=params["learning_rate"], beta1=params["beta1"],
+                                beta2=params["beta2"], tau=params["tau"], stream=self.compute[d],
+                                upd_dtype=ops.torch_dtype(dt))
+            flats[dt] = self._to_host_chunks(dt, [c[6] for c in ctx], step, torch.float64)
+            self.old_ready.add(dt)
+        self.pg_started = True
+        self._sync_d2h()
         state.m, state.v, state.signature = new_m, new_v, sig
         state.layout, state.bounds, state.devices = self.layout, self.bounds, self.devices
         model = [None] * len(self.layout.shapes)
         for dt in self.layout.groups:
-            owned = self._gather_group([o[dt] for o in outs], dt)
-            self.layout.unpack_group(owned, dt, model, copy=False)
+            self.layout.unpack_group(flats[dt].numpy(), dt, model, copy=False)
         return model

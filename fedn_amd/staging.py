@@ -45,6 +45,46 @@ def chunks(n, itemsize):
     return [(lo, min(n, lo + C)) for lo in range(0, n, C)]
 
 
+class HostStreamer:
+    """Host -> device streaming of host arrays through a small ring of pinned pieces filled by
+    the pack threads: no whole-buffer concatenation or pinning (both cost more than the DMA
+    for a multi-GB global model)."""
+
+    def __init__(self, nbuf=3, nbytes=RING_BYTES):
+        self.nbuf, self.nbytes = nbuf, nbytes
+        self.ring, self.ev, self.i = [], [None] * nbuf, 0
+
+    def h2d(self, parts, odt, lo, hi, dst, stream):
+        """Enqueue on ``stream`` the copy of elements [lo, hi) of the concatenation of ``parts``
+        ((flat host array, element offset) pairs of dtype ``odt``) into the device tensor
+        ``dst`` (hi - lo elements); returns an event recorded after it."""
+        if not self.ring:
+            self.ring = [torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(self.nbuf)]
+        isz = np.dtype(odt).itemsize
+        step = self.nbytes // isz
+        with torch.cuda.device(dst.device):
+            for plo in range(lo, hi, step):
+                phi = min(hi, plo + step)
+                i = self.i
+                self.i = (i + 1) % self.nbuf
+                if self.ev[i] is not None:
+                    self.ev[i].synchronize()            # the piece's previous H2D has read it
+                buf = self.ring[i][:(phi - plo) * isz]
+                view = buf.numpy().view(odt)
+                for a, off in parts:                    # members overlapping [plo, phi)
+                    s0, s1 = max(plo, off), min(phi, off + a.size)
+                    if s0 < s1:
+                        parallel_copy(view[s0 - plo:s1 - plo], a[s0 - off:s1 - off])
+                with torch.cuda.stream(stream):
+                    dst[plo - lo:phi - lo].copy_(buf.view(dst.dtype), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                self.ev[i] = ev
+            done = torch.cuda.Event()
+            done.record(stream)
+        return done
+
+
 class _Slot:
     __slots__ = ("host", "host_np", "dev", "h2d_start", "h2d_done", "consumed", "used", "reserved")
 
@@ -376,9 +416,7 @@ class FedOptPipeline(_Pipeline):
         self.old = {dt: torch.empty(layout.group_elems[dt], dtype=ops.torch_dtype(odt), device=self.device)
                     for dt, (odt, _) in self.old_host.items()}
         self.old_ready = set()
-        self._ring = []
-        self._ring_ev = []
-        self._ring_i = 0
+        self.streamer = HostStreamer()
         self.pg = {}
         self.pg_started = False                  # pg holds a partial pseudo-gradient
         self.old_arrays = old_arrays
@@ -411,35 +449,9 @@ class FedOptPipeline(_Pipeline):
         return self.pg[dt]
 
     def _h2d_old(self, dt, lo, hi):
-        """Enqueue the H2D of elements [lo, hi) of the global model's group ``dt`` on the copy
-        stream, through a ring of pinned pieces filled by the pack threads; returns an event."""
+        """Enqueue the H2D of elements [lo, hi) of the global model's group ``dt`` (copy stream)."""
         odt, parts = self.old_host[dt]
-        dst = self.old[dt]
-        isz = dst.element_size()
-        if not self._ring:
-            self._ring = [torch.empty(RING_BYTES, dtype=torch.uint8, pin_memory=True) for _ in range(3)]
-            self._ring_ev = [None] * 3
-        step = RING_BYTES // isz
-        for plo in range(lo, hi, step):
-            phi = min(hi, plo + step)
-            i = self._ring_i
-            self._ring_i = (i + 1) % len(self._ring)
-            if self._ring_ev[i] is not None:
-                self._ring_ev[i].synchronize()          # the piece's previous H2D has read it
-            buf = self._ring[i][:(phi - plo) * isz]
-            view = buf.numpy().view(odt)
-            for a, off in parts:                        # members overlapping [plo, phi)
-                s0, s1 = max(plo, off), min(phi, off + a.size)
-                if s0 < s1:
-                    parallel_copy(view[s0 - plo:s1 - plo], a[s0 - off:s1 - off])
-            with torch.cuda.stream(self.copy):
-                dst[plo:phi].copy_(buf.view(dst.dtype), non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(self.copy)
-            self._ring_ev[i] = ev
-        done = torch.cuda.Event()
-        done.record(self.copy)
-        return done
+        return self.streamer.h2d(parts, odt, lo, hi, self.old[dt][lo:hi], self.copy)
 
     def _old_dev(self, dt):
         """The whole global-model group on the device (compute stream ordered after its H2D)."""
