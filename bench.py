@@ -11,7 +11,8 @@ no collective is on the data path ("scaling": "weak"). The RCCL all-gather that 
 reassemble the model on every GPU is timed separately and reported beside the line
 (``allgather``), not folded into ``value``; so is the fold with that all-gather chunked
 and overlapped (``fold_allgather``: block-cyclic shards, round i gathered on a
-communication stream while round i+1 folds; sharded.CyclicShardedFedAvg).
+communication stream while round i+1 folds; sharded.CyclicShardedFedAvg), and the copy of
+every rank's slice to host memory, FEDn's actual consumer (``gather_to_host``).
 
 Also measured in the same run:
   roofline      algorithmic bytes (K*P*4 + P*4 per launch) / average kernel time (HIP events
@@ -212,6 +213,29 @@ def main():
                            "(block-cyclic shards); the world*params model on every GPU; not in value"}
         del agg_c, ups_c, out_c
 
+    # the model to the host, FEDn's consumer (roundhandler.py:465-468): every rank D2H's its own
+    # slice over its own PCIe link into pinned memory, concurrently (SURVEY.md §5 alternative to
+    # the all-gather); value excludes it
+    host = torch.empty(P, dtype=torch.float32, pin_memory=True)
+    for _ in range(2):
+        host.copy_(agg, non_blocking=True)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    reps = 5
+    for _ in range(reps):
+        host.copy_(agg, non_blocking=True)
+    torch.cuda.synchronize(device)
+    gh = torch.tensor([(time.perf_counter() - t1) / reps], dtype=torch.float64, device="cpu" if rehearsal else device)
+    if world > 1:
+        dist.all_reduce(gh, op=dist.ReduceOp.MAX)
+    gh_s = float(gh[0])
+    gather_host = {"ms": gh_s * 1e3, "bytes_per_rank": P * 4, "GBps_aggregate": world * P * 4 / gh_s / 1e9,
+                   "note": "each rank D2H's its slice of the aggregate into pinned host memory, all ranks "
+                           "concurrently over their own links; max over ranks; not in value"}
+    del host
+
     base = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
         base = cpu_baseline(ups, ns, agg, a.cpu_sample)
@@ -232,6 +256,7 @@ def main():
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": base,
         }
+        line["gather_to_host"] = gather_host
         if allgather:
             line["allgather"] = allgather
         if fold_ag:
