@@ -165,8 +165,7 @@ def main():
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
     workload = f"fedavg_k{K}_p{P}_{a.dtype}"
 
-    allgather = None
-    if world > 1 and not a.no_allgather:
+    def measure_allgather():
         gather_src = agg.cpu() if rehearsal else agg
         for _ in range(2):
             full = sh.allgather(gather_src)
@@ -184,13 +183,12 @@ def main():
         dist.all_reduce(ag, op=dist.ReduceOp.MAX)
         ag_s = float(ag[0])
         nbytes = sh.shard * world * 4
-        allgather = {"ms": ag_s * 1e3, "bytes_in_per_rank": sh.shard * (world - 1) * 4,
-                     "algbw_GBps": nbytes / ag_s / 1e9, "busbw_GBps": nbytes * (world - 1) / world / ag_s / 1e9,
-                     "backend": "gloo (rehearsal)" if rehearsal else "rccl",
-                     "note": "reassembles the world*params model on every GPU; not in value"}
+        return {"ms": ag_s * 1e3, "bytes_in_per_rank": sh.shard * (world - 1) * 4,
+                "algbw_GBps": nbytes / ag_s / 1e9, "busbw_GBps": nbytes * (world - 1) / world / ag_s / 1e9,
+                "backend": "gloo (rehearsal)" if rehearsal else "rccl",
+                "note": "reassembles the world*params model on every GPU; not in value"}
 
-    fold_ag = None
-    if cyc is not None:
+    def measure_fold_allgather():
         agg_c = torch.empty(cyc.local_len, dtype=torch.float32, device=device)
         ups_c = [u[:cyc.local_len] for u in ups_full]
         out_c = None if rehearsal else torch.empty(cyc.full_len, dtype=torch.float32, device=device)
@@ -207,11 +205,20 @@ def main():
                           device="cpu" if rehearsal else device)
         dist.all_reduce(fa, op=dist.ReduceOp.MAX)
         fa_s = float(fa[0])
-        fold_ag = {"ms": fa_s * 1e3, "value": K * P_total / fa_s, "unit": "params/s", "rounds": cyc.rounds,
-                   "chunk": cyc.C, "backend": "gloo (rehearsal)" if rehearsal else "rccl",
-                   "note": "fold + all-gather of each folded round overlapped on a second stream "
-                           "(block-cyclic shards); the world*params model on every GPU; not in value"}
-        del agg_c, ups_c, out_c
+        return {"ms": fa_s * 1e3, "value": K * P_total / fa_s, "unit": "params/s", "rounds": cyc.rounds,
+                "chunk": cyc.C, "backend": "gloo (rehearsal)" if rehearsal else "rccl",
+                "note": "fold + all-gather of each folded round overlapped on a second stream "
+                        "(block-cyclic shards); the world*params model on every GPU; not in value"}
+
+    def side(fn):
+        """A beside-the-line measurement: an error is reported in its field, never instead of value."""
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001
+            return {"error": f"{type(e).__name__}: {e}"}
+
+    allgather = side(measure_allgather) if world > 1 and not a.no_allgather else None
+    fold_ag = side(measure_fold_allgather) if cyc is not None else None
 
     # the model to the host, FEDn's consumer (roundhandler.py:465-468): every rank D2H's its own
     # slice over its own PCIe link into pinned memory, concurrently (SURVEY.md §5 alternative to
