@@ -7,7 +7,9 @@ Same contract and observable behaviour as fedavg.py:8-83:
   * the first update is the model (fedavg.py:127-128): K = 1 returns it unchanged;
   * returns ``(model, data)`` with ``time_model_load``, ``time_model_aggregation``,
     ``nr_aggregated_models`` (fedavg.py:99-101, 142), ``(None, data)`` if nothing folded.
-The fold ``x + (n*(y-x))/N`` (numpyhelper.py:32) runs in libfedagg on the GPU, bit-exact;
+The fold ``x + (n*(y-x))/N`` (numpyhelper.py:32; binaryhelper inherits it) runs in libfedagg
+on the GPU, bit-exact; a session on androidhelper folds with ITS rule instead,
+``(1 - w)*x + w*y`` on one flat array (androidhelper.py:21-39, staging.AndroidFedAvgPipeline);
 updates are staged through pinned memory and folded on arrival (fedn_amd/staging.py).
 Extra ``data`` keys: ``time_h2d`` / ``time_kernel`` (HIP events), ``time_pack``, ``time_d2h``.
 """
@@ -18,7 +20,7 @@ import traceback
 
 import torch
 
-from ..staging import FedAvgPipeline
+from ..staging import AndroidFedAvgPipeline, FedAvgPipeline, helper_kind
 from .aggregatorbase import AggregatorBase
 
 logger = logging.getLogger("fedn")
@@ -30,8 +32,10 @@ def env_devices():
     return [d.strip() for d in v.split(",") if d.strip()] if v else None
 
 
-def make_fedavg_pipeline(first, device=None, devices=None):
+def make_fedavg_pipeline(first, device=None, devices=None, helper=None):
     devices = devices or env_devices()
+    if helper_kind(helper) == "androidhelper":   # its own fold rule and model format
+        return AndroidFedAvgPipeline(device or (devices[0] if devices else None) or default_device(), first)
     if devices and len(devices) > 1:
         from ..multidev import ShardedFedAvgPipeline
         return ShardedFedAvgPipeline(devices, first)
@@ -75,7 +79,7 @@ class Aggregator(AggregatorBase):
 
                 tic = time.time()
                 if nr_aggregated_models == 0:
-                    pipe = make_fedavg_pipeline(model_next, self.device, self.devices)
+                    pipe = make_fedavg_pipeline(model_next, self.device, self.devices, helper)
                 else:
                     pipe.add(model_next, metadata["num_examples"], total_examples)
                 data["time_model_aggregation"] += time.time() - tic

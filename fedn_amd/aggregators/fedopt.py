@@ -82,6 +82,10 @@ class Aggregator(AggregatorBase):
 
                 total_examples += metadata["num_examples"]
                 tic = time.time()
+                if helper is not None and not hasattr(helper, "subtract"):
+                    # androidhelper has no numpyhelper primitives: fedopt.py:91 raises here for every
+                    # update, each is logged and skipped, and the round returns (None, data)
+                    raise AttributeError(f"'{type(helper).__name__}' object has no attribute 'subtract'")
                 if nr_aggregated_models == 0:
                     model_old = self.update_handler.load_model(helper, model_update.model_id)
                     pipe = self._pipeline(model_old, model_next)

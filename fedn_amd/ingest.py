@@ -215,7 +215,7 @@ class StagingUpdateHandler:
 
     def _stage_sharded(self, model_update):
         streams = [self._stream(dv) for dv in self.devices]
-        if self.native_decode and hasattr(self.inner, "load_model_update_byte"):
+        if self._native():
             try:
                 data, metadata = self.inner.load_model_update_byte(model_update)
             except Exception:  # noqa: BLE001 — not held as bytes: decode through the helper
@@ -232,11 +232,18 @@ class StagingUpdateHandler:
         layout.pack(arrays, pinned.numpy())
         return stage_sharded(layout, pinned, self.devices, streams, arrays), metadata
 
+    def _native(self):
+        """Raw-bytes decode applies to npz (numpyhelper / fednamdhelper); binaryhelper's raw
+        float64 bytes go through the helper's own load."""
+        from .staging import helper_kind
+        return self.native_decode and helper_kind(self.helper) != "binaryhelper" and \
+            hasattr(self.inner, "load_model_update_byte")
+
     def _stage(self, model_update):
         if self.devices:
             return self._stage_sharded(model_update)
         dev = self._device()
-        if self.native_decode and hasattr(self.inner, "load_model_update_byte"):
+        if self._native():
             try:
                 data, metadata = self.inner.load_model_update_byte(model_update)
             except Exception:  # noqa: BLE001 — not held as bytes: decode through the helper
@@ -255,6 +262,9 @@ class StagingUpdateHandler:
             valid = True
         except (KeyError, TypeError, ValueError):
             valid = False
+        from .staging import helper_kind
+        if valid and helper_kind(self.helper) == "androidhelper":
+            valid = False    # one flat array with its own fold rule: the aggregator takes it from the host
         if valid:
             self._device()
             with self._lock:

@@ -320,6 +320,60 @@ class FedAvgPipeline(_Pipeline):
         return out
 
 
+def helper_kind(helper):
+    """Which FEDn helper plug-in a round uses. package.py:24 accepts numpyhelper, binaryhelper
+    and androidhelper; the aggregators fold with the helper's own arithmetic (fedavg.py:68).
+    androidhelper sets ``name`` and HelperBase resets it to the class name, so the plug-in's
+    module decides; None (tests, tools) means numpyhelper."""
+    if helper is None:
+        return "numpyhelper"
+    mod = type(helper).__module__.rsplit(".", 1)[-1]
+    if mod in ("numpyhelper", "binaryhelper", "androidhelper"):
+        return mod
+    return getattr(helper, "name", "numpyhelper")
+
+
+class AndroidFedAvgPipeline(_Pipeline):
+    """FedAvg in a session on FEDn's androidhelper, whose increment_average is
+    ``(1 - w) * model + w * model_next`` with ``w = num_examples / total_examples`` on ONE flat
+    array (androidhelper.py:21-39; its load gives float64, :78-92) — not numpyhelper's
+    ``x + n*(y - x)/N``. Device form: one ``fa_running_mean`` launch per update,
+    ``g = (g*a + m*b) / T`` with a = 1 - w, b = w, T = 1 (the division by 1 is exact), which
+    rounds exactly as numpy: RN(RN(g*a) + RN(m*b)). Mobile models are small; updates are
+    staged and folded on arrival."""
+
+    def __init__(self, device, first_arrays):
+        first = np.asarray(first_arrays)
+        super().__init__(device, Layout.of([first]), 2)
+        self.first_arrays = first_arrays
+        self.nfolds = 0
+        self.g = None
+
+    def add(self, arrays, n, N):
+        arr = np.asarray(arrays)
+        self.layout.check([arr])                # numpy would refuse other lengths too
+        dt = self.layout.groups[0]
+        if ops.torch_dtype(dt) not in (torch.float32, torch.float64):
+            raise TypeError(f"androidhelper models are float arrays, got {dt}")
+        w = n / N
+        if self.g is None:
+            s0 = self.stage([np.asarray(self.first_arrays)])
+            with torch.cuda.stream(self.compute):
+                self.g = self.group(s0, dt).clone()
+            s0.consumed.record(self.compute)
+        s = self.stage([arr])
+        span = self._kernel_span()
+        ops.running_mean(self.g, self.group(s, dt), 1 - w, w, 1.0, stream=self.compute)
+        self._end_span(span)
+        s.consumed.record(self.compute)
+        self.nfolds += 1
+
+    def result(self):
+        if self.nfolds == 0:
+            return self.first_arrays            # `model = model_next` alias (fedavg.py:127-128)
+        return self._to_host(self.g).numpy()
+
+
 class FedOptState:
     """Server-optimizer state of one fedopt Aggregator instance (fedopt.py:36-38), in HBM.
 

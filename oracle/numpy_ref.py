@@ -86,7 +86,14 @@ def ones(m1, a):
 # --------------------------------------------------------------------------------------
 # FedAvg — fedn/network/combiner/aggregators/fedavg.py:22-83
 # --------------------------------------------------------------------------------------
-def fedavg_combine(updates):
+def android_increment_average(model, model_next, num_examples, total_examples):
+    """androidhelper.Helper.increment_average, fedn/utils/helpers/plugins/androidhelper.py:21-39:
+    one flat float64 array (its load, :78-92)."""
+    w = num_examples / total_examples
+    return (1 - w) * model + w * model_next
+
+
+def fedavg_combine(updates, increment=None):
     """Fold ``updates`` = [(arrays, num_examples), ...] in FIFO order.
 
     Returns (model or None, nr_aggregated_models). Mirrors fedavg.py:109-140: the
@@ -94,6 +101,7 @@ def fedavg_combine(updates):
     is aliased (fedavg.py:127-128), and a fold that raises is skipped while its
     examples stay counted (fedavg.py:137-140).
     """
+    increment = increment or increment_average      # the session helper's rule (fedavg.py:68)
     model, nr, total = None, 0, 0
     for arrays, n in updates:
         total += n
@@ -101,7 +109,7 @@ def fedavg_combine(updates):
             if nr == 0:
                 model = arrays
             else:
-                model = increment_average(model, arrays, n, total)
+                model = increment(model, arrays, n, total)
         except Exception:  # noqa: BLE001  (reference logs and continues)
             continue
         nr += 1

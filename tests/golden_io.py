@@ -51,6 +51,23 @@ def load_case(name):
                             for k in range(K)],
                 "out": _list(z, f"r{r}_out"),
             })
+    if case["kind"] in ("helper_fedavg", "helper_fedopt"):
+        # a session on a non-numpy helper: one flat array per model (see tools/gen_golden.py helper_case)
+        case["helper"] = str(z["helper"])
+        case["params"] = json.loads(str(z["params"])) if "params" in z else None
+        case["rounds"] = []
+        for r in range(int(z["rounds"])):
+            K = int(z[f"r{r}_K"])
+            ns = [int(v) for v in z[f"r{r}_n"]]
+            case["rounds"].append({
+                "updates": [(z[f"r{r}_u{k}"], ns[k]) for k in range(K)],
+                "old": z[f"r{r}_old"],
+                "out": None if bool(z[f"r{r}_out_none"]) else z[f"r{r}_out"],
+                "nr": int(z[f"r{r}_nr"]),
+                "qsize": int(z[f"r{r}_qsize"]),
+                "m": z.get(f"r{r}_m"),
+                "v": z.get(f"r{r}_v"),
+            })
     if case["kind"] in ("fedavg", "fedopt"):
         case["params"] = json.loads(str(z["params"])) if "params" in z else None
         rounds = []

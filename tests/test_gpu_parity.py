@@ -774,3 +774,80 @@ def test_multidevice_sharded_ingest_npz(native):
     st.close()
     assert data["nr_aggregated_models"] == rd["nr"]
     assert_lists_identical(model, rd["out"], "sharded npz")
+
+
+# ------------------------------------------------------------------------- non-numpy FEDn helpers
+def _helper_stub(kind):
+    """An object that identifies as FEDn's helper plug-in ``kind`` the way the real one does
+    (module fedn.utils.helpers.plugins.<kind>; androidhelper's ``name`` reads "Helper")."""
+    cls = type("Helper", (), {"__module__": f"fedn.utils.helpers.plugins.{kind}"})
+    h = cls()
+    h.name = "Helper" if kind == "androidhelper" else kind
+    if kind != "androidhelper":
+        h.subtract = lambda *a: None     # numpyhelper's primitives exist (binaryhelper inherits them)
+    return h
+
+
+@pytest.mark.parametrize("name", case_names("helper_fedavg"))
+def test_helper_fedavg_plugin(name):
+    """The plug-in folds with the session helper's rule: androidhelper's (1 - w)*x + w*y on one
+    flat float64 array (returned as that array), binaryhelper's numpyhelper rule on [array]."""
+    case = load_case(name)
+    rd = case["rounds"][0]
+    android = case["helper"] == "androidhelper"
+    uh, agg = _plugin("fedavg")
+    for u, n in rd["updates"]:
+        uh.submit(u if android else [u], n)
+    model, data = agg.combine_models(helper=_helper_stub(case["helper"]))
+    assert data["nr_aggregated_models"] == rd["nr"]
+    got = model if android else model[0]
+    assert isinstance(got, np.ndarray)
+    assert_lists_identical([got], [rd["out"]], name)
+
+
+@pytest.mark.parametrize("name", case_names("helper_fedopt"))
+def test_helper_fedopt_plugin(name):
+    case = load_case(name)
+    android = case["helper"] == "androidhelper"
+    uh, agg = _plugin("fedopt")
+    helper = _helper_stub(case["helper"])
+    for r, rd in enumerate(case["rounds"]):
+        gid = uh.put_global_model(rd["old"] if android else [rd["old"]], f"g{r}")
+        for u, n in rd["updates"]:
+            uh.submit(u if android else [u], n, model_id=gid)
+        model, data = agg.combine_models(helper=helper, parameters=case["params"])
+        assert data["nr_aggregated_models"] == rd["nr"]
+        assert uh.model_updates.qsize() == rd["qsize"]
+        if rd["out"] is None:
+            assert model is None
+        else:
+            assert_lists_identical(model, [rd["out"]], f"{name} r{r}")
+            assert_lists_identical(agg.m, [rd["m"]], f"{name} r{r} m")
+            assert_lists_identical(agg.v, [rd["v"]], f"{name} r{r} v")
+
+
+@pytest.mark.parametrize("name", ["binary_fedavg_k5", "android_fedavg_k9"])
+def test_helper_sessions_through_ingest(name):
+    """The streaming ingest leaves androidhelper updates to the host path and decodes binaryhelper
+    bytes with the helper's load (never as npz); the plug-in result is unchanged."""
+    import io
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    case = load_case(name)
+    rd = case["rounds"][0]
+    android = case["helper"] == "androidhelper"
+    helper = _helper_stub(case["helper"])
+    if not android:      # decode raw float64 bytes like numpyhelper.load(file_type="raw_binary")
+        helper.load = lambda fh: [np.frombuffer(fh.read(), dtype=np.float64)]
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=helper, device=DEV, workers=2)
+    for u, n in rd["updates"]:
+        if android:
+            uh.submit(u, n, via=st)
+        else:
+            uh.submit_bytes(np.asarray(u, dtype=np.float64).tobytes(), n, via=st)
+    model, data = get_aggregator("fedavg", st).combine_models(helper=helper)
+    st.close()
+    assert data["nr_aggregated_models"] == rd["nr"]
+    assert_lists_identical([model if android else model[0]], [rd["out"]], name)

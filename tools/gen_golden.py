@@ -22,9 +22,11 @@ pull in opentelemetry (not installed). We pre-register a bare ``fedn`` package a
 
 Usage:  python tools/gen_golden.py            (writes tests/golden/*.npz + manifest.json)
 """
+import io
 import json
 import logging
 import os
+import struct
 import sys
 import tempfile
 import types
@@ -368,12 +370,77 @@ def sf_cases(ref):
     ]
 
 
+def _payload(helper_name, vals):
+    """Update bytes as the helper's save() writes them (androidhelper.py:62-76: struct of
+    float32; binaryhelper -> numpyhelper.save raw_binary: float64 tofile)."""
+    if helper_name == "androidhelper":
+        return struct.pack("f" * len(vals), *np.asarray(vals, dtype=np.float32).tolist())
+    return np.asarray(vals, dtype=np.float64).tobytes()
+
+
+def helper_case(ref, name, helper_cls, agg_name, rng, P, nks_per_round, params=None):
+    """FedAvg / FedOpt with a non-numpy helper FEDn accepts (package.py:24): the aggregator folds
+    with THAT helper (fedavg.py:68 helper.increment_average; fedopt.py:89-94 helper.subtract ...).
+    Updates are uploaded as the helper's bytes and loaded back by UpdateHandler.load_model_update
+    with the helper (updatehandler.py:90-117, modelservice.py:110-125)."""
+    h = Harness(ref, agg_name)
+    h.helper = helper_cls()
+    hn = type(h.helper).__module__.rsplit(".", 1)[-1]   # androidhelper sets name, HelperBase resets it
+    d = {"kind": np.array("helper_" + agg_name), "name": np.array(name), "helper": np.array(hn)}
+    if params is not None:
+        d["params"] = np.array(json.dumps(params))
+    unwrap = (lambda m: m) if hn == "androidhelper" else (lambda m: m[0])
+    old = rng.standard_normal(P)
+    for r, nks in enumerate(nks_per_round):
+        gid = f"global-{r}"
+        h.ms.set_model(io.BytesIO(_payload(hn, old)), gid)
+        d[f"r{r}_old"] = np.asarray(unwrap(h.helper.load(io.BytesIO(_payload(hn, old)))))
+        for k, n in enumerate(nks):
+            vals = old + 0.01 * rng.standard_normal(P)
+            uid = str(uuid.uuid4())
+            h.ms.set_model(io.BytesIO(_payload(hn, vals)), uid)
+            meta = json.dumps({"training_metadata": {"num_examples": int(n)}, "config": json.dumps({"round_id": "1"})})
+            h.uh.on_model_update(ref["pb2"].ModelUpdate(model_id=gid, model_update_id=uid, meta=meta))
+            d[f"r{r}_u{k}"] = np.asarray(unwrap(h.helper.load(io.BytesIO(_payload(hn, vals)))))
+        d[f"r{r}_n"] = np.array(nks, dtype=np.int64)
+        d[f"r{r}_K"] = np.array(len(nks))
+        model, data = h.combine(ref["Parameters"](params) if params is not None else None)
+        d[f"r{r}_nr"] = np.array(data["nr_aggregated_models"])
+        d[f"r{r}_qsize"] = np.array(h.uh.model_updates.qsize())
+        d[f"r{r}_out_none"] = np.array(model is None)
+        if model is not None:
+            d[f"r{r}_out"] = np.asarray(unwrap(model))
+            old = np.asarray(unwrap(model), dtype=np.float64)
+        if agg_name == "fedopt" and h.agg.m is not None:
+            d[f"r{r}_m"] = np.asarray(unwrap(h.agg.m))
+            d[f"r{r}_v"] = np.asarray(unwrap(h.agg.v))
+    d["rounds"] = np.array(len(nks_per_round))
+    return d
+
+
+def helper_cases(ref):
+    from fedn.utils.helpers.plugins.androidhelper import Helper as Android
+    from fedn.utils.helpers.plugins.binaryhelper import Helper as Binary
+    rng = np.random.default_rng(6)
+    return [
+        helper_case(ref, "android_fedavg_k1", Android, "fedavg", rng, 1000, [[77]]),
+        helper_case(ref, "android_fedavg_k2", Android, "fedavg", rng, 1000, [list(rng.integers(1, 5001, 2))]),
+        helper_case(ref, "android_fedavg_k9", Android, "fedavg", rng, 4099, [list(rng.integers(1, 5001, 9))]),
+        helper_case(ref, "android_fedopt_k3", Android, "fedopt", rng, 1000, [list(rng.integers(1, 5001, 3))]),
+        helper_case(ref, "binary_fedavg_k5", Binary, "fedavg", rng, 2053, [list(rng.integers(1, 5001, 5))]),
+        helper_case(ref, "binary_fedopt_2r", Binary, "fedopt", rng, 2053,
+                    [list(rng.integers(1, 5001, 4)), list(rng.integers(1, 5001, 3))], {"serveropt": "yogi"}),
+    ]
+
+
 def main():
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     ref = _import_reference()
     os.makedirs(OUT, exist_ok=True)
     if only == "sf":      # regenerate just these fixtures; the others stay byte-identical
         return _write(sf_cases(ref), merge=True)
+    if only == "helpers":
+        return _write(helper_cases(ref), merge=True)
     cases = []
     cases.append(helper_kat(ref))
     rng = np.random.default_rng(1)
@@ -424,6 +491,7 @@ def main():
     cases.append(reduce_case(ref, "reduce_single", rng, ODD_SHAPES, ["ok"]))
 
     cases += sf_cases(ref)
+    cases += helper_cases(ref)
     _write(cases, merge=False)
 
 
