@@ -165,6 +165,61 @@ def stage_npz(data, device, stream):
     return StagedModel(layout, dev, ready)
 
 
+def _member_spans(layout, dt, lo, hi):
+    """(tensor index, first element within the tensor, element count, element offset from
+    ``lo``) for every tensor of group ``dt`` that overlaps the group range [lo, hi)."""
+    out = []
+    for i, off in layout.members[dt]:
+        a, b = max(lo, off), min(hi, off + layout.sizes[i])
+        if b > a:
+            out.append((i, a - off, b - a, a - lo))
+    return out
+
+
+def stage_decoded(decoded, device, stream):
+    """Copy an update decoded during its upload (upload.DecodedUpdate: one pinned block per
+    tensor) into a new device buffer in the pipelines' layout on ``stream``, tensor by
+    tensor: no pack, no second host copy."""
+    layout = Layout.of(decoded.arrays)
+    dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
+    ready = torch.cuda.Event()
+    with torch.cuda.stream(stream):
+        for dt in layout.groups:
+            g0 = layout.group_byte_offset[dt]
+            for i, e0, n, o in _member_spans(layout, dt, 0, layout.group_elems[dt]):
+                src = torch.from_numpy(decoded.arrays[i].reshape(-1).view(np.uint8))
+                dev[g0 + o * dt.itemsize:g0 + (o + n) * dt.itemsize].copy_(src, non_blocking=True)
+        ready.record(stream)
+    ready.synchronize()
+    return StagedModel(layout, dev, ready)
+
+
+def stage_decoded_sharded(decoded, devices, streams):
+    """:func:`stage_decoded` for the multi-device layout: device d receives only the parts of
+    each tensor inside its parameter slices (Layout.shard_geometry), over its own link."""
+    layout = Layout.of(decoded.arrays)
+    bounds, dev_off, dev_bytes = layout.shard_geometry(len(devices))
+    flat = {i: torch.from_numpy(a.reshape(-1).view(np.uint8)) for i, a in enumerate(decoded.arrays)}
+    bufs, ready = [], []
+    for d, dv in enumerate(devices):
+        with torch.cuda.device(dv):
+            buf = torch.empty(dev_bytes[d], dtype=torch.uint8, device=dv)
+            with torch.cuda.stream(streams[d]):
+                for dt in layout.groups:
+                    lo, hi = bounds[dt][d]
+                    base, isz = dev_off[d][dt], dt.itemsize
+                    for i, e0, n, o in _member_spans(layout, dt, lo, hi):
+                        buf[base + o * isz:base + (o + n) * isz].copy_(flat[i][e0 * isz:(e0 + n) * isz],
+                                                                       non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(streams[d])
+        bufs.append(buf)
+        ready.append(ev)
+    for ev in ready:
+        ev.synchronize()
+    return ShardedStagedModel(layout, devices, bufs, ready)
+
+
 class StagingUpdateHandler:
     """Drop-in wrapper of a FEDn ``UpdateHandler`` that decodes + stages updates on arrival.
 
@@ -181,8 +236,11 @@ class StagingUpdateHandler:
     ``waitforit``, ...) is the wrapped handler's.
     """
 
-    def __init__(self, inner, helper=None, device=None, workers=4, native_decode=True, devices=None):
+    def __init__(self, inner, helper=None, device=None, workers=4, native_decode=True, devices=None,
+                 max_unclaimed_upload_bytes=16 << 30):
+        from .upload import AdoptedUploads
         self.inner = inner
+        self._uploads = AdoptedUploads(max_unclaimed_upload_bytes)
         if devices is None:
             from .aggregators.fedavg import env_devices
             devices = env_devices()
@@ -213,8 +271,41 @@ class StagingUpdateHandler:
                 st = self._streams[key] = torch.cuda.Stream(dev)
         return st
 
+    # -- updates decoded while they uploaded (upload.StreamingUpload) -------------------------
+    def wants_upload(self):
+        """Whether uploads should be decoded as they stream in: npz helpers only (binaryhelper
+        holds raw float64 bytes; androidhelper updates are folded from the host)."""
+        from .staging import helper_kind
+        return self.native_decode and helper_kind(self.helper) not in ("binaryhelper", "androidhelper")
+
+    def adopt(self, model_id, fut):
+        """Hold the decode of upload ``model_id`` (Future of upload.DecodedUpdate) for the
+        ModelUpdate that names it (model_update_id == the upload's request id)."""
+        self._uploads.put(model_id, fut)
+
+    def _decoded_upload(self, model_update):
+        fut = self._uploads.pop(model_update.model_update_id)
+        if fut is None:
+            return None
+        try:
+            return fut.result()
+        except Exception:  # noqa: BLE001 — not decodable while streaming: take the normal path
+            return None
+
+    def _metadata(self, model_update):
+        """training_metadata as UpdateHandler.load_model_update returns it (updatehandler.py:106-116)."""
+        metadata = json.loads(model_update.meta)
+        config = json.loads(metadata["config"]) if "config" in metadata else json.loads(model_update.config)
+        training_metadata = metadata["training_metadata"]
+        if "round_id" in config:
+            training_metadata["round_id"] = config["round_id"]
+        return training_metadata
+
     def _stage_sharded(self, model_update):
         streams = [self._stream(dv) for dv in self.devices]
+        decoded = self._decoded_upload(model_update)
+        if decoded is not None:
+            return stage_decoded_sharded(decoded, self.devices, streams), self._metadata(model_update)
         if self._native():
             try:
                 data, metadata = self.inner.load_model_update_byte(model_update)
@@ -243,6 +334,10 @@ class StagingUpdateHandler:
         if self.devices:
             return self._stage_sharded(model_update)
         dev = self._device()
+        decoded = self._decoded_upload(model_update)
+        if decoded is not None:
+            with torch.cuda.device(dev):
+                return stage_decoded(decoded, dev, self._stream()), self._metadata(model_update)
         if self._native():
             try:
                 data, metadata = self.inner.load_model_update_byte(model_update)
@@ -281,6 +376,7 @@ class StagingUpdateHandler:
     def delete_model(self, model_update):
         with self._lock:
             self._staged.pop(model_update.model_update_id, None)
+        self._uploads.pop(model_update.model_update_id)
         return self.inner.delete_model(model_update)
 
     def close(self):

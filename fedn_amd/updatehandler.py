@@ -47,6 +47,54 @@ class MemoryModelStore:
         return self.models.pop(model_id, None) is not None
 
 
+MODEL_STATUS_OK = 0            # fedn.proto:147-153 (ModelStatus)
+MODEL_STATUS_IN_PROGRESS = 1
+CHUNK_SIZE = 1 << 20           # modelservice.py:12
+
+
+@dataclass
+class ModelRequest:
+    """The fields of fedn.proto ``ModelRequest`` that ModelService.Upload reads."""
+
+    id: str
+    data: bytes = b""
+    status: int = MODEL_STATUS_IN_PROGRESS
+
+
+@dataclass
+class ModelResponse:
+    id: str
+    status: int
+    message: str = ""
+
+
+def upload_requests(data, model_id, chunk=CHUNK_SIZE):
+    """The request stream a FEDn client sends (upload_request_generator, modelservice.py:15-31):
+    ``chunk``-byte IN_PROGRESS requests, then an empty OK request."""
+    mv = memoryview(data)
+    for o in range(0, len(mv), chunk):
+        yield ModelRequest(id=model_id, data=bytes(mv[o:o + chunk]), status=MODEL_STATUS_IN_PROGRESS)
+    yield ModelRequest(id=model_id, data=b"", status=MODEL_STATUS_OK)
+
+
+class MemoryModelService:
+    """``ModelService.Upload`` (modelservice.py:198-221) over the in-memory store: chunks are
+    appended per id; the OK request commits the bytes under that id and ends the call."""
+
+    def __init__(self, store):
+        self.store = store
+        self._parts = {}
+
+    def Upload(self, request_iterator, context):
+        for request in request_iterator:
+            if request.status == MODEL_STATUS_IN_PROGRESS:
+                self._parts.setdefault(request.id, bytearray()).extend(request.data)
+            if request.status == MODEL_STATUS_OK and not request.data:
+                self.store.put(request.id, _NpzBytes(bytes(self._parts.pop(request.id, b""))))
+                return ModelResponse(id=request.id, status=MODEL_STATUS_OK, message="Got model successfully.")
+        return None
+
+
 class MemoryUpdateHandler:
     def __init__(self, store=None):
         self.model_updates = queue.Queue()
@@ -70,6 +118,15 @@ class MemoryUpdateHandler:
         meta = json.dumps({"training_metadata": {"num_examples": num_examples},
                            "config": json.dumps({"round_id": round_id})})
         mu = ModelUpdate(model_id=model_id, model_update_id=uid, meta=meta)
+        (via or self).on_model_update(mu)
+        return mu
+
+    def submit_uploaded(self, model_update_id, num_examples, model_id="global", round_id="1", via=None):
+        """Enqueue the ModelUpdate of an update already uploaded under ``model_update_id``
+        (the client's Upload, then SendModelUpdate, combiner.py:783-797)."""
+        meta = json.dumps({"training_metadata": {"num_examples": num_examples},
+                           "config": json.dumps({"round_id": round_id})})
+        mu = ModelUpdate(model_id=model_id, model_update_id=model_update_id, meta=meta)
         (via or self).on_model_update(mu)
         return mu
 

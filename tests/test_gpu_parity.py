@@ -414,6 +414,38 @@ def test_staging_ingest_npz_bytes(name, native):
     assert_lists_identical(model, rd["out"], name)
 
 
+@pytest.mark.parametrize("ndev", [1, 2])
+@pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k8", "fedavg_int32_k3", "fedavg_skipbad_k4"])
+def test_streaming_upload_ingest(name, ndev):
+    """Updates uploaded through ModelService.Upload in 64 KiB chunks are decoded WHILE they
+    stream (upload.StreamingUpload, pinned blocks), adopted by the staging handler when their
+    ModelUpdate arrives and copied to HBM tensor by tensor (one device, or as parameter slices
+    over two): folded bit-exactly; the stored upload bytes are untouched."""
+    import io
+    from fedn_amd.aggregators.fedavg import Aggregator
+    from fedn_amd.helper import Helper
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryModelService, MemoryUpdateHandler, upload_requests
+    from fedn_amd.upload import StreamingUpload
+    rd = load_case(name)["rounds"][0]
+    uh = MemoryUpdateHandler()
+    devs = [DEV] * ndev
+    st = StagingUpdateHandler(uh, helper=Helper(), device=DEV, workers=3, devices=devs if ndev > 1 else None)
+    svc = StreamingUpload(MemoryModelService(uh.store), st, workers=2)
+    for k, (arrays, n) in enumerate(rd["updates"]):
+        b = io.BytesIO()
+        np.savez_compressed(b, **{str(i): a for i, a in enumerate(arrays)})
+        svc.Upload(upload_requests(b.getvalue(), f"up{k}", chunk=65536), None)
+        assert uh.store.get(f"up{k}").data == b.getvalue()
+        uh.submit_uploaded(f"up{k}", n, via=st)
+    agg = Aggregator(st, devices=devs) if ndev > 1 else Aggregator(st)
+    model, data = agg.combine_models(helper=Helper())
+    svc.close()
+    st.close()
+    assert data["nr_aggregated_models"] == rd["nr"]
+    assert_lists_identical(model, rd["out"], name)
+
+
 def test_helper_increment_average_gpu():
     """fedn_amd.helper.Helper.increment_average == numpyhelper's (the reference KAT + random)."""
     from fedn_amd.helper import Helper

@@ -45,6 +45,12 @@ for s in $STEPS; do
     ingest)
       timeout -k 10 900 python tools/bench_ingest.py > "$OUT/ingest.log" 2>&1; rc=$?
       echo "ingest rc=$rc"; grep -v amdgpu.ids "$OUT/ingest.log" | tail -4; [ $rc -eq 0 ] || exit $rc ;;
+    upload)
+      timeout -k 10 600 python tools/bench_upload.py > "$OUT/upload.log" 2>&1; rc=$?
+      echo "upload rc=$rc"; grep -v amdgpu.ids "$OUT/upload.log" | tail -5; [ $rc -eq 0 ] || exit $rc ;;
+    upload100m)
+      timeout -k 10 600 python tools/bench_upload.py --params 100000000 --clients 8 --client-MBps 400 > "$OUT/upload100m.log" 2>&1; rc=$?
+      echo "upload100m rc=$rc"; grep -v amdgpu.ids "$OUT/upload100m.log" | tail -5; [ $rc -eq 0 ] || exit $rc ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc_$c" -o run -- \
