@@ -60,6 +60,13 @@ def load_lib():
                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_void_p),
                                        ctypes.POINTER(ctypes.c_int64), ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                        ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+            lib.fnpz_stream_open.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+            lib.fnpz_stream_close.argtypes = [ctypes.c_void_p]
+            lib.fnpz_stream_close.restype = None
+            lib.fnpz_stream_feed.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]
+            lib.fnpz_stream_next.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(Entry),
+                                             ctypes.POINTER(ctypes.c_int64)]
             if lib.fnpz_abi_version() != 1:
                 raise ImportError("libfednpz.so ABI mismatch; rebuild")
             _lib = lib

@@ -380,6 +380,153 @@ void deflate_block(const MemberSrc& m, Block& blk, int level) {
     deflateEnd(&zs);
 }
 
+// ---------------------------------------------------------------------------------------
+// streaming reader: the archive arrives front to back in pieces (an upload's chunks), so
+// members are read from their LOCAL headers as they come; the central directory at the end
+// is only recognised, never needed. Payload bytes are inflated straight into the caller's
+// window (e.g. a pinned slot); the CRC-32 covers the .npy header and payload as in the zip.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t kDescSig = 0x08074b50;
+constexpr size_t kMaxNpyHeader = 1u << 20;
+
+}  // namespace
+
+struct fnpz_stream {
+    std::vector<uint8_t> in;            // buffered input; in[pos:] not consumed yet
+    size_t pos = 0;
+    enum State { HDR, NPY, DATA, DESC, END } st = HDR;
+    std::string name;
+    uint16_t flags = 0;
+    int method = 0;
+    uint32_t crc_want = 0;
+    uint64_t raw_left = 0;              // stored member: bytes still to read
+    bool zip64 = false;
+    z_stream zs{};
+    bool zinit = false;
+    bool zend = false;                  // the member's data ended
+    uLong crc = 0;
+    std::vector<uint8_t> pend;          // inflated bytes not delivered yet (header + first payload)
+    size_t pend_pos = 0;
+    int64_t left = 0;                   // payload bytes still to deliver
+    int err = 0;
+
+    ~fnpz_stream() {
+        if (zinit) inflateEnd(&zs);
+    }
+    size_t avail() const { return in.size() - pos; }
+
+    // Pull up to cap uncompressed bytes of the current member into dst. Returns the count
+    // (crc updated); sets zend at the member's end; -1 on a corrupt stream.
+    int64_t produce(uint8_t* dst, int64_t cap) {
+        if (zend || cap <= 0) return 0;
+        if (method == 0) {
+            const int64_t n = (int64_t)std::min<uint64_t>({(uint64_t)cap, (uint64_t)avail(), raw_left});
+            std::memcpy(dst, in.data() + pos, (size_t)n);
+            pos += (size_t)n;
+            raw_left -= (uint64_t)n;
+            crc = crc32(crc, dst, (uInt)n);
+            if (raw_left == 0) zend = true;
+            return n;
+        }
+        zs.next_in = in.data() + pos;
+        zs.avail_in = (uInt)std::min<size_t>(avail(), kChunk);
+        zs.next_out = dst;
+        zs.avail_out = (uInt)std::min<int64_t>(cap, kChunk);
+        const uInt in0 = zs.avail_in, out0 = zs.avail_out;
+        const int rc = inflate(&zs, Z_NO_FLUSH);
+        pos += in0 - zs.avail_in;
+        const int64_t n = out0 - zs.avail_out;
+        crc = crc32(crc, dst, (uInt)n);
+        if (rc == Z_STREAM_END) zend = true;
+        else if (rc != Z_OK && rc != Z_BUF_ERROR) return -1;
+        return n;
+    }
+};
+
+namespace {
+
+int sfail(fnpz_stream* s, int code, const char* fmt, const char* a) {
+    s->err = code;
+    return fail(code, fmt, a);
+}
+
+// local file header at s->in[s->pos]: 1 = parsed, 0 = need input, < 0 = -status
+int stream_local_header(fnpz_stream* s) {
+    const uint8_t* h = s->in.data() + s->pos;
+    if (s->avail() < 30) return 0;
+    const uint16_t nlen = rd16(h + 26), xlen = rd16(h + 28);
+    if (s->avail() < 30u + nlen + xlen) return 0;
+    s->flags = rd16(h + 6);
+    s->method = rd16(h + 8);
+    s->crc_want = rd32(h + 14);
+    uint64_t csize = rd32(h + 18), usize = rd32(h + 22);
+    s->name.assign(reinterpret_cast<const char*>(h + 30), nlen);
+    s->zip64 = false;
+    const uint8_t* x = h + 30 + nlen;
+    const uint8_t* xe = x + xlen;
+    while (x + 4 <= xe) {
+        const uint16_t id = rd16(x), sz = rd16(x + 2);
+        if (id == 0x0001) {                       // ZIP64 extended information
+            s->zip64 = true;
+            const uint8_t* v = x + 4;
+            if (usize == 0xFFFFFFFFu && v + 8 <= x + 4 + sz) usize = rd64(v), v += 8;
+            if (csize == 0xFFFFFFFFu && v + 8 <= x + 4 + sz) csize = rd64(v);
+        }
+        x += 4 + sz;
+    }
+    if (s->method != 0 && s->method != 8) return -sfail(s, FNPZ_EFORMAT, "%s: compression method unsupported", s->name.c_str());
+    if (s->method == 0 && (s->flags & 8)) return -sfail(s, FNPZ_EFORMAT, "%s: stored member with a data descriptor", s->name.c_str());
+    s->pos += 30u + nlen + xlen;
+    s->raw_left = csize;
+    if (s->method == 8) {
+        const int rc = s->zinit ? inflateReset(&s->zs) : inflateInit2(&s->zs, -MAX_WBITS);
+        if (rc != Z_OK) return -sfail(s, FNPZ_ECORRUPT, "%s: inflate init failed", s->name.c_str());
+        s->zinit = true;
+    }
+    s->zend = false;
+    s->crc = crc32(0L, Z_NULL, 0);
+    s->pend.clear();
+    s->pend_pos = 0;
+    (void)usize;
+    return 1;
+}
+
+// .npy preamble + dict at the front of s->pend: 1 = parsed into *e, 0 = need more, < 0 = -status
+int stream_npy_header(fnpz_stream* s, fnpz_entry* e) {
+    const std::vector<uint8_t>& p = s->pend;
+    if (p.size() < 10) return 0;
+    if (std::memcmp(p.data(), "\x93NUMPY", 6) != 0) return -sfail(s, FNPZ_EFORMAT, "%s: not a .npy member", s->name.c_str());
+    size_t hoff, hlen;
+    if (p[6] == 1) {
+        hoff = 10;
+        hlen = rd16(p.data() + 8);
+    } else if (p[6] == 2 || p[6] == 3) {
+        if (p.size() < 12) return 0;
+        hoff = 12;
+        hlen = rd32(p.data() + 8);
+    } else {
+        return -sfail(s, FNPZ_EFORMAT, "%s: .npy version unsupported", s->name.c_str());
+    }
+    if (hoff + hlen > kMaxNpyHeader) return -sfail(s, FNPZ_EFORMAT, "%s: .npy header too long", s->name.c_str());
+    if (p.size() < hoff + hlen) return 0;
+    std::memset(e, 0, sizeof(*e));
+    std::string nm = s->name;
+    if (nm.size() >= 4 && nm.compare(nm.size() - 4, 4, ".npy") == 0) nm.resize(nm.size() - 4);
+    if (nm.size() >= sizeof(e->name)) return -sfail(s, FNPZ_EFORMAT, "%s: member name too long", s->name.c_str());
+    std::memcpy(e->name, nm.data(), nm.size());
+    const std::string dict(reinterpret_cast<const char*>(p.data() + hoff), hlen);
+    if (!parse_npy_dict(dict, e)) return -sfail(s, FNPZ_EFORMAT, "%s: unsupported .npy header", s->name.c_str());
+    int64_t count = 1;
+    for (int d = 0; d < e->ndim; ++d) count *= e->shape[d];
+    e->nbytes = count * descr_itemsize(e->descr);
+    e->npy_header = (int64_t)(hoff + hlen);
+    e->method = s->method;
+    e->crc32 = s->crc_want;
+    s->pend_pos = hoff + hlen;
+    s->left = e->nbytes;
+    return 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -643,6 +790,123 @@ int fnpz_write(int n, const char* const* names, const uint8_t* const* headers, c
     p += 22;
     *out_len = (int64_t)(p - out);
     return FNPZ_OK;
+}
+
+int fnpz_stream_open(fnpz_stream** s) {
+    if (!s) return fail(FNPZ_EINVAL, "fnpz_stream_open: bad arguments");
+    *s = new fnpz_stream();
+    return FNPZ_OK;
+}
+
+void fnpz_stream_close(fnpz_stream* s) { delete s; }
+
+int fnpz_stream_feed(fnpz_stream* s, const uint8_t* data, int64_t len) {
+    if (!s || len < 0 || (len > 0 && !data)) return fail(FNPZ_EINVAL, "fnpz_stream_feed: bad arguments");
+    if (s->pos > 0 && s->pos >= s->in.size() / 2) {      // drop consumed input
+        s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)s->pos);
+        s->pos = 0;
+    }
+    s->in.insert(s->in.end(), data, data + len);
+    return FNPZ_OK;
+}
+
+int fnpz_stream_next(fnpz_stream* s, uint8_t* out, int64_t out_cap, int* event, fnpz_entry* entry, int64_t* out_len) {
+    if (!s || !event || !out_len || (out_cap > 0 && !out)) return fail(FNPZ_EINVAL, "fnpz_stream_next: bad arguments");
+    *out_len = 0;
+    if (s->err) return fail(s->err, "fnpz_stream_next: the stream already failed");
+    for (;;) {
+        switch (s->st) {
+        case fnpz_stream::HDR: {
+            if (s->avail() < 4) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+            const uint32_t sig = rd32(s->in.data() + s->pos);
+            if (sig == kCentralSig || sig == kEocdSig || sig == kZ64EocdSig || sig == kZ64LocSig) {
+                s->st = fnpz_stream::END;
+                continue;
+            }
+            if (sig != kLocalSig) return sfail(s, FNPZ_EFORMAT, "%s", "not a zip local file header");
+            const int rc = stream_local_header(s);
+            if (rc < 0) return -rc;
+            if (rc == 0) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+            s->st = fnpz_stream::NPY;
+            continue;
+        }
+        case fnpz_stream::NPY: {
+            if (!entry) return fail(FNPZ_EINVAL, "fnpz_stream_next: a member header needs an entry");
+            const int rc = stream_npy_header(s, entry);
+            if (rc < 0) return -rc;
+            if (rc == 1) {
+                s->st = fnpz_stream::DATA;
+                return *event = FNPZ_EV_MEMBER, FNPZ_OK;
+            }
+            if (s->zend) return sfail(s, FNPZ_ECORRUPT, "%s: truncated .npy header", s->name.c_str());
+            const size_t old = s->pend.size();
+            s->pend.resize(old + 4096);
+            const size_t pos0 = s->pos;
+            const int64_t n = s->produce(s->pend.data() + old, 4096);
+            if (n < 0) return sfail(s, FNPZ_ECORRUPT, "%s: corrupt deflate stream", s->name.c_str());
+            s->pend.resize(old + (size_t)n);
+            if (n == 0 && s->pos == pos0 && !s->zend) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+            continue;
+        }
+        case fnpz_stream::DATA: {
+            if (s->pend_pos < s->pend.size()) {                // payload inflated with the header
+                const int64_t have = (int64_t)(s->pend.size() - s->pend_pos);
+                if (have > s->left) return sfail(s, FNPZ_EFORMAT, "%s: more data than its .npy header declares", s->name.c_str());
+                const int64_t n = std::min(have, out_cap);
+                if (n == 0) return fail(FNPZ_EINVAL, "fnpz_stream_next: payload pending and no output window");
+                std::memcpy(out, s->pend.data() + s->pend_pos, (size_t)n);
+                s->pend_pos += (size_t)n;
+                s->left -= n;
+                *out_len = n;
+                return *event = FNPZ_EV_DATA, FNPZ_OK;
+            }
+            const size_t pos0 = s->pos;
+            if (s->left > 0) {
+                if (out_cap <= 0) return fail(FNPZ_EINVAL, "fnpz_stream_next: payload pending and no output window");
+                if (s->zend) return sfail(s, FNPZ_ECORRUPT, "%s: member shorter than its .npy header declares", s->name.c_str());
+                const int64_t n = s->produce(out, std::min(out_cap, s->left));
+                if (n < 0) return sfail(s, FNPZ_ECORRUPT, "%s: corrupt deflate stream", s->name.c_str());
+                if (n > 0) {
+                    s->left -= n;
+                    *out_len = n;
+                    return *event = FNPZ_EV_DATA, FNPZ_OK;
+                }
+                if (s->pos == pos0 && !s->zend) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+                continue;
+            }
+            if (!s->zend) {                                    // payload complete: the stream must end here
+                uint8_t extra;
+                const int64_t n = s->produce(&extra, 1);
+                if (n < 0) return sfail(s, FNPZ_ECORRUPT, "%s: corrupt deflate stream", s->name.c_str());
+                if (n > 0) return sfail(s, FNPZ_EFORMAT, "%s: more data than its .npy header declares", s->name.c_str());
+                if (!s->zend) {
+                    if (s->pos == pos0) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+                    continue;
+                }
+            }
+            if (s->flags & 8) {
+                s->st = fnpz_stream::DESC;
+                continue;
+            }
+            if ((uint32_t)s->crc != s->crc_want) return sfail(s, FNPZ_ECORRUPT, "%s: CRC-32 mismatch", s->name.c_str());
+            s->st = fnpz_stream::HDR;
+            return *event = FNPZ_EV_MEMBER_END, FNPZ_OK;
+        }
+        case fnpz_stream::DESC: {
+            if (s->avail() < 4) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+            const bool has_sig = rd32(s->in.data() + s->pos) == kDescSig;
+            const size_t size = (has_sig ? 4 : 0) + 4 + (s->zip64 ? 16 : 8);
+            if (s->avail() < size) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+            const uint32_t crc = rd32(s->in.data() + s->pos + (has_sig ? 4 : 0));
+            s->pos += size;
+            if ((uint32_t)s->crc != crc) return sfail(s, FNPZ_ECORRUPT, "%s: CRC-32 mismatch", s->name.c_str());
+            s->st = fnpz_stream::HDR;
+            return *event = FNPZ_EV_MEMBER_END, FNPZ_OK;
+        }
+        case fnpz_stream::END:
+            return *event = FNPZ_EV_END, FNPZ_OK;
+        }
+    }
 }
 
 }  // extern "C"

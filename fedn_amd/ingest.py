@@ -177,9 +177,25 @@ def _member_spans(layout, dt, lo, hi):
 
 
 def stage_decoded(decoded, device, stream):
-    """Copy an update decoded during its upload (upload.DecodedUpdate: one pinned block per
-    tensor) into a new device buffer in the pipelines' layout on ``stream``, tensor by
-    tensor: no pack, no second host copy."""
+    """Copy an update decoded during its upload into a new device buffer in the pipelines'
+    layout on ``stream``, tensor by tensor: from HBM (upload.DeviceDecodedUpdate, decoded
+    through DeviceSink: a D2D copy per tensor once its H2D copies have landed) or from one
+    pinned block per tensor (upload.DecodedUpdate): no pack, no second host copy."""
+    from .upload import DeviceDecodedUpdate
+    if isinstance(decoded, DeviceDecodedUpdate):
+        layout = Layout(decoded.shapes, decoded.dtypes)
+        dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
+        ready = torch.cuda.Event()
+        with torch.cuda.stream(stream):
+            stream.wait_event(decoded.ready)
+            for dt in layout.groups:
+                g0 = layout.group_byte_offset[dt]
+                for i, e0, n, o in _member_spans(layout, dt, 0, layout.group_elems[dt]):
+                    dev[g0 + o * dt.itemsize:g0 + (o + n) * dt.itemsize].copy_(
+                        decoded.blocks[i][e0 * dt.itemsize:(e0 + n) * dt.itemsize], non_blocking=True)
+            ready.record(stream)
+        ready.synchronize()               # the per-tensor blocks are released after the copies
+        return StagedModel(layout, dev, ready)
     layout = Layout.of(decoded.arrays)
     dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
     ready = torch.cuda.Event()
@@ -278,6 +294,11 @@ class StagingUpdateHandler:
         from .staging import helper_kind
         return self.native_decode and helper_kind(self.helper) not in ("binaryhelper", "androidhelper")
 
+    def upload_device(self):
+        """The device uploads are decoded into (upload.DeviceSink), or None when updates are
+        staged as parameter slices over several devices (decoded to host, sliced at staging)."""
+        return None if self.devices else self._device()
+
     def adopt(self, model_id, fut):
         """Hold the decode of upload ``model_id`` (Future of upload.DecodedUpdate) for the
         ModelUpdate that names it (model_update_id == the upload's request id)."""
@@ -304,7 +325,7 @@ class StagingUpdateHandler:
     def _stage_sharded(self, model_update):
         streams = [self._stream(dv) for dv in self.devices]
         decoded = self._decoded_upload(model_update)
-        if decoded is not None:
+        if decoded is not None and hasattr(decoded, "arrays"):
             return stage_decoded_sharded(decoded, self.devices, streams), self._metadata(model_update)
         if self._native():
             try:

@@ -4,22 +4,22 @@ In FEDn a client streams its update to the combiner in 1 MiB chunks (ModelServic
 modelservice.py:196-220; upload_request_generator, :15-31), which only appends them to a temp
 file; the npz is inflated later, when the update is loaded (updatehandler.py:90-117,
 modelservice.py:110-125). A numpy-written npz (np.savez_compressed) is one deflate stream per
-tensor, so inflating a 100 M-parameter update takes ~0.3 s on one core, and it starts only
+tensor, so inflating a 100 M-parameter update takes ~1 s on one core, and it starts only
 after the last byte arrived. :class:`StreamingUpload` wraps the combiner's ModelService:
 every chunk still goes to the original Upload unchanged, and a copy is fed to a decoder on a
-worker thread (:class:`NpzStreamDecoder`: ZIP local headers + .npy headers parsed as they
-arrive, deflate inflated incrementally with zlib, CRC-32 checked), so decoding overlaps the
-network transfer. When the upload completes, the decoded update is handed to the
-:class:`~fedn_amd.ingest.StagingUpdateHandler`, which copies it to HBM when the matching
-``ModelUpdate`` arrives (SendModelUpdate) instead of decoding the file again. Anything the
-decoder does not handle (non-npz helpers' bytes, Fortran-ordered or object arrays, a corrupt
-stream) is simply not adopted: the update then takes the normal path.
+worker thread (:class:`NpzStreamDecoder` over libfednpz's native streaming reader: ZIP local
+headers and .npy headers parsed as they arrive, deflate inflated incrementally, CRC-32
+checked), so decoding overlaps the network transfer. The payload is inflated into a small
+ring of pinned slots that are copied to HBM as they fill (:class:`DeviceSink`), so the
+update is already on the device when its upload completes. The decoded update is handed to
+the :class:`~fedn_amd.ingest.StagingUpdateHandler`, which places it in the pipelines' layout
+when the matching ``ModelUpdate`` arrives (SendModelUpdate) instead of decoding the file
+again. Anything the decoder does not handle (non-npz helpers' bytes, Fortran-ordered or
+object arrays, a corrupt stream) is simply not adopted: the update then takes the normal path.
 """
-import io
+import ctypes
 import queue
-import struct
 import threading
-import zlib
 from collections import OrderedDict
 from concurrent.futures import Future, ThreadPoolExecutor
 
@@ -28,212 +28,192 @@ import numpy as np
 MODEL_STATUS_OK = 0            # fedn.proto:147-153 (ModelStatus)
 MODEL_STATUS_IN_PROGRESS = 1
 
-_LOCAL = b"PK\x03\x04"
-_DESC = b"PK\x07\x08"
-_END = (b"PK\x01\x02", b"PK\x05\x06", b"PK\x06\x06", b"PK\x06\x07")
-
-
 class DecodeError(ValueError):
     pass
 
 
-class _Member:
-    __slots__ = ("name", "method", "flags", "crc", "csize", "usize", "zip64", "inflater", "consumed", "hdr",
-                 "array", "view", "filled", "crc_run", "raw_left")
+EV_NEED_INPUT, EV_MEMBER, EV_DATA, EV_MEMBER_END, EV_END = range(5)     # include/fednpz.h (fnpz_event)
+
+
+class HostSink:
+    """Decoded payload into one host buffer per member (``alloc(nbytes)`` → uint8 numpy)."""
+
+    def __init__(self, alloc=None):
+        self.alloc = alloc or (lambda n: np.empty(n, dtype=np.uint8))
+
+    def open(self, nbytes):
+        return self.alloc(nbytes)
+
+    def window(self, view, offset):
+        """(address, bytes) the decoder may inflate the member's bytes from ``offset`` into."""
+        return view.ctypes.data + offset, view.size - offset
+
+    def commit(self, view, offset, n):
+        pass
+
+    def close(self, view):
+        pass
+
+    def finish(self):
+        return None
+
+
+class DeviceSink:
+    """Decoded payload straight to HBM through a small ring of pinned slots: one device block
+    per member; the decoder inflates into the current slot, and every full slot (and each
+    member's end) is copied H2D on ``stream`` while the ring moves on (a slot is refilled
+    only after its copy completed). Pinned memory per upload is ``ring * slot`` instead of
+    the whole update, and the H2D runs while later chunks are still arriving. ``finish()``
+    records the event that the last copy fired."""
+
+    def __init__(self, device, stream, slot=8 << 20, ring=4):
+        import torch
+        self.torch, self.device, self.stream, self.slot = torch, device, stream, slot
+        self.ring = [torch.empty(slot, dtype=torch.uint8, pin_memory=True) for _ in range(ring)]
+        self.addr = [t.data_ptr() for t in self.ring]
+        self.events = [None] * ring
+        self.i = self.fill = 0
+        self.cur, self.cur_off = None, 0
+
+    def open(self, nbytes):
+        return self.torch.empty(max(nbytes, 1), dtype=self.torch.uint8, device=self.device)
+
+    def window(self, blk, offset):
+        if self.fill and (self.cur is not blk or self.cur_off + self.fill != offset):
+            self._flush()
+        if self.fill == 0:
+            ev = self.events[self.i]
+            if ev is not None:
+                ev.synchronize()
+            self.cur, self.cur_off = blk, offset
+        return self.addr[self.i] + self.fill, self.slot - self.fill
+
+    def commit(self, blk, offset, n):
+        self.fill += n
+        if self.fill == self.slot:
+            self._flush()
+
+    def _flush(self):
+        if not self.fill:
+            return
+        torch = self.torch
+        with torch.cuda.device(self.device), torch.cuda.stream(self.stream):
+            self.cur[self.cur_off:self.cur_off + self.fill].copy_(self.ring[self.i][:self.fill], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.events[self.i] = ev
+        self.i = (self.i + 1) % len(self.ring)
+        self.fill, self.cur = 0, None
+
+    def close(self, blk):
+        self._flush()
+
+    def finish(self):
+        self._flush()
+        torch = self.torch
+        with torch.cuda.device(self.device):
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return ev
 
 
 class NpzStreamDecoder:
     """Incremental decoder of an npz archive (a ZIP of ``.npy`` members, stored or deflated)
-    fed in arbitrary chunks. ``alloc(nbytes)`` returns a writable uint8 numpy buffer for one
-    member's array data (e.g. a view of pinned host memory); ``members()`` returns
-    ``[(name, dtype, shape, uint8 buffer)]`` in archive order once ``finish()`` succeeded."""
+    fed in arbitrary chunks: the native streaming reader of libfednpz.so (fnpz_stream_*,
+    include/fednpz.h) parses local headers and inflates each payload straight into the
+    sink's window (no GIL held while it inflates, no intermediate Python bytes). Payload
+    bytes go to a sink (:class:`HostSink` by default: ``alloc(nbytes)`` returns a writable
+    uint8 numpy buffer for one member); ``finish()`` returns ``[(name, dtype, shape,
+    handle)]`` in archive order once the archive ended cleanly."""
 
-    def __init__(self, alloc=None):
-        self.alloc = alloc or (lambda n: np.empty(n, dtype=np.uint8))
-        self.buf = bytearray()
-        self.state = "header"
-        self.cur = None
+    def __init__(self, alloc=None, sink=None):
+        from .codec import Entry, load_lib
+        self.lib = load_lib()
+        self.sink = sink if sink is not None else HostSink(alloc)
+        self.h = ctypes.c_void_p()
+        self._check(self.lib.fnpz_stream_open(ctypes.byref(self.h)))
+        self.ent = Entry()
+        self.ev = ctypes.c_int()
+        self.n = ctypes.c_int64()
+        self.cur = None           # [name, dtype, shape, handle, nbytes, filled]
         self.done = []
         self.finished = False
 
-    # -- feeding ------------------------------------------------------------------------
+    def __del__(self):
+        h, self.h = getattr(self, "h", None), None
+        if h:
+            self.lib.fnpz_stream_close(h)
+
+    def _check(self, rc):
+        if rc:
+            raise DecodeError(f"fednpz status {rc}: {self.lib.fnpz_last_error().decode(errors='replace')}")
+
     def feed(self, data):
         if self.finished:
             return
-        self.buf += data
-        while self._step():
-            pass
+        self._check(self.lib.fnpz_stream_feed(self.h, bytes(data), len(data)))
+        self._drain()
+
+    def _drain(self):
+        lib, ev, n = self.lib, self.ev, self.n
+        while True:
+            c = self.cur
+            if c is not None and c[5] < c[4]:
+                addr, cap = self.sink.window(c[3], c[5])
+                cap = min(cap, c[4] - c[5])
+            else:
+                addr, cap = None, 0
+            self._check(lib.fnpz_stream_next(self.h, addr, cap, ctypes.byref(ev), ctypes.byref(self.ent),
+                                             ctypes.byref(n)))
+            e = ev.value
+            if e == EV_NEED_INPUT:
+                return
+            if e == EV_DATA:
+                self.sink.commit(c[3], c[5], n.value)
+                c[5] += n.value
+            elif e == EV_MEMBER:
+                self.cur = self._open_member()
+            elif e == EV_MEMBER_END:
+                self.sink.close(c[3])
+                self.done.append((c[0], c[1], c[2], c[3]))
+                self.cur = None
+            elif e == EV_END:
+                self.finished = True
+                return
+
+    def _open_member(self):
+        ent = self.ent
+        name = ent.name.decode(errors="replace")
+        try:
+            dtype = np.dtype(ent.descr.decode())
+        except TypeError as exc:
+            raise DecodeError(f"member {name}: dtype {ent.descr!r}: {exc}") from None
+        if dtype.hasobject:
+            raise DecodeError(f"member {name}: object arrays are not decoded (allow_pickle=False)")
+        shape = tuple(ent.shape[d] for d in range(ent.ndim))
+        if ent.fortran_order and len(shape) > 1:
+            raise DecodeError(f"member {name}: Fortran-ordered arrays take the normal path")
+        nbytes = int(ent.nbytes)
+        if nbytes != int(np.prod(shape, dtype=np.int64)) * dtype.itemsize:
+            raise DecodeError(f"member {name}: {nbytes} payload bytes for {dtype} {shape}")
+        return [name, dtype, shape, self.sink.open(nbytes), nbytes, 0]
 
     def finish(self):
         """Check the archive ended cleanly; returns the decoded members."""
-        while self._step():
-            pass
-        if not self.finished and not (self.state == "header" and not self.buf and self.done):
-            raise DecodeError(f"archive truncated (state {self.state})")
+        if not self.finished:
+            self._drain()
+        if not self.finished:
+            raise DecodeError("archive truncated before its central directory")
         return self.done
 
-    def _step(self):
-        if self.state == "header":
-            return self._header()
-        if self.state == "data":
-            return self._data()
-        if self.state == "descriptor":
-            return self._descriptor()
-        return False
 
-    # -- ZIP local file header ----------------------------------------------------------------
-    def _header(self):
-        if len(self.buf) < 4:
-            return False
-        sig = bytes(self.buf[:4])
-        if sig in _END:                               # central directory: every member is in
-            self.finished = True
-            self.state = "end"
-            self.buf = bytearray()
-            return False
-        if sig != _LOCAL:
-            raise DecodeError("not a ZIP local file header")
-        if len(self.buf) < 30:
-            return False
-        (_, _, flags, method, _, _, crc, csize, usize, nlen, xlen) = struct.unpack("<IHHHHHIIIHH", bytes(self.buf[:30]))
-        if len(self.buf) < 30 + nlen + xlen:
-            return False
-        name = bytes(self.buf[30:30 + nlen]).decode("utf-8", "replace")
-        extra = bytes(self.buf[30 + nlen:30 + nlen + xlen])
-        zip64 = False
-        p = 0
-        while p + 4 <= len(extra):                    # zip64 extended information (0x0001)
-            tag, size = struct.unpack("<HH", extra[p:p + 4])
-            if tag == 0x0001:
-                zip64 = True
-                vals = extra[p + 4:p + 4 + size]
-                q = 0
-                if usize == 0xFFFFFFFF and q + 8 <= len(vals):
-                    usize = struct.unpack("<Q", vals[q:q + 8])[0]
-                    q += 8
-                if csize == 0xFFFFFFFF and q + 8 <= len(vals):
-                    csize = struct.unpack("<Q", vals[q:q + 8])[0]
-            p += 4 + size
-        if method not in (0, 8):
-            raise DecodeError(f"member {name}: compression method {method}")
-        if method == 0 and flags & 8:
-            raise DecodeError(f"member {name}: stored with a data descriptor (size unknown)")
-        del self.buf[:30 + nlen + xlen]
-        m = _Member()
-        m.name, m.method, m.flags, m.crc, m.csize, m.usize, m.zip64 = name, method, flags, crc, csize, usize, zip64
-        m.inflater = zlib.decompressobj(-15) if method == 8 else None
-        m.raw_left = csize if method == 0 else None
-        m.hdr = bytearray()
-        m.array = None
-        m.view = None
-        m.filled = 0
-        m.crc_run = 0
-        self.cur = m
-        self.state = "data"
-        return True
-
-    # -- member payload ---------------------------------------------------------------------
-    def _data(self):
-        m = self.cur
-        if not self.buf:
-            return False
-        if m.method == 0:
-            take = min(len(self.buf), m.raw_left)
-            out = bytes(self.buf[:take])
-            del self.buf[:take]
-            m.raw_left -= take
-            ended = m.raw_left == 0
-        else:
-            out = m.inflater.decompress(bytes(self.buf))
-            self.buf = bytearray()
-            ended = m.inflater.eof
-            if ended:
-                self.buf = bytearray(m.inflater.unused_data)
-        if out:
-            m.crc_run = zlib.crc32(out, m.crc_run)
-            self._emit(m, out)
-        if not ended:
-            return False
-        self._end_member(m)
-        return True
-
-    def _emit(self, m, out):
-        if m.array is None:                           # still inside the .npy header
-            m.hdr += out
-            hdr = self._npy_header(m)
-            if hdr is None:
-                return
-            used, dtype, shape = hdr
-            rest = bytes(m.hdr[used:])
-            m.hdr = None
-            nbytes = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
-            m.view = self.alloc(nbytes)
-            m.array = (dtype, tuple(shape))
-            out = rest
-        if out:
-            n = len(out)
-            if m.filled + n > m.view.size:
-                raise DecodeError(f"member {m.name}: more data than its .npy header declares")
-            m.view[m.filled:m.filled + n] = np.frombuffer(out, dtype=np.uint8)
-            m.filled += n
-
-    @staticmethod
-    def _npy_header(m):
-        h = bytes(m.hdr)
-        if len(h) < 10:
-            return None
-        if h[:6] != b"\x93NUMPY":
-            raise DecodeError(f"member {m.name} is not a .npy array")
-        major = h[6]
-        hl_size = 2 if major == 1 else 4
-        if len(h) < 8 + hl_size:
-            return None
-        hlen = struct.unpack("<H" if hl_size == 2 else "<I", h[8:8 + hl_size])[0]
-        used = 8 + hl_size + hlen
-        if len(h) < used:
-            return None
-        f = io.BytesIO(h[:used])
-        version = np.lib.format.read_magic(f)
-        shape, fortran, dtype = np.lib.format._read_array_header(f, version)   # safe literal parse
-        if dtype.hasobject:
-            raise DecodeError(f"member {m.name}: object arrays are not decoded (allow_pickle=False)")
-        if fortran and len(shape) > 1:
-            raise DecodeError(f"member {m.name}: Fortran-ordered arrays take the normal path")
-        return used, dtype, shape
-
-    def _end_member(self, m):
-        if m.array is None:
-            raise DecodeError(f"member {m.name}: truncated .npy header")
-        if m.filled != m.view.size:
-            raise DecodeError(f"member {m.name}: {m.filled} of {m.view.size} bytes")
-        if m.flags & 8:
-            self.state = "descriptor"
-        else:
-            if (m.crc_run & 0xFFFFFFFF) != m.crc:
-                raise DecodeError(f"member {m.name}: CRC-32 mismatch")
-            self._push(m)
-            self.state = "header"
-
-    def _descriptor(self):
-        m = self.cur
-        has_sig = len(self.buf) >= 4 and bytes(self.buf[:4]) == _DESC
-        size = (4 if has_sig else 0) + 4 + (16 if m.zip64 else 8)
-        if len(self.buf) < size:
-            return False
-        o = 4 if has_sig else 0
-        crc = struct.unpack("<I", bytes(self.buf[o:o + 4]))[0]
-        del self.buf[:size]
-        if (m.crc_run & 0xFFFFFFFF) != crc:
-            raise DecodeError(f"member {m.name}: CRC-32 mismatch")
-        self._push(m)
-        self.state = "header"
-        return True
-
-    def _push(self, m):
-        dtype, shape = m.array
-        name = m.name[:-4] if m.name.endswith(".npy") else m.name
-        self.done.append((name, dtype, shape, m.view))
-        self.cur = None
+def _ordered(members):
+    """numpyhelper.load order: a[str(i)] for i in range(len(files)) (numpyhelper.py:180-182)."""
+    by_name = {m[0]: m for m in members}
+    try:
+        return [by_name[str(i)] for i in range(len(members))]
+    except KeyError as e:
+        raise DecodeError(f"npz keys are not 0..{len(members) - 1}: missing {e}") from None
 
 
 class DecodedUpdate:
@@ -242,14 +222,24 @@ class DecodedUpdate:
     __slots__ = ("arrays", "nbytes", "pinned")
 
     def __init__(self, members, pinned):
-        by_name = {m[0]: m for m in members}
-        try:                          # numpyhelper.load order: a[str(i)] (numpyhelper.py:180-182)
-            members = [by_name[str(i)] for i in range(len(members))]
-        except KeyError as e:
-            raise DecodeError(f"npz keys are not 0..{len(members) - 1}: missing {e}") from None
-        self.arrays = [view.view(dtype).reshape(shape) for _, dtype, shape, view in members]
+        self.arrays = [view.view(dtype).reshape(shape) for _, dtype, shape, view in _ordered(members)]
         self.nbytes = sum(a.nbytes for a in self.arrays)
         self.pinned = pinned          # keeps the pinned blocks alive
+
+
+class DeviceDecodedUpdate:
+    """An update decoded during its upload straight into HBM (:class:`DeviceSink`): one
+    device block (uint8) per tensor in FEDn's key order, valid once ``ready`` has fired."""
+
+    __slots__ = ("shapes", "dtypes", "blocks", "ready", "device", "nbytes")
+
+    def __init__(self, members, ready, device):
+        members = _ordered(members)
+        self.shapes = [tuple(shape) for _, _, shape, _ in members]
+        self.dtypes = [dtype for _, dtype, _, _ in members]
+        self.blocks = [blk for _, _, _, blk in members]
+        self.ready, self.device = ready, device
+        self.nbytes = sum(int(np.prod(sh, dtype=np.int64)) * dt.itemsize for sh, dt in zip(self.shapes, self.dtypes))
 
 
 class StreamingUpload:
@@ -261,11 +251,32 @@ class StreamingUpload:
     unclaimed uploads (e.g. the combiner's own global models) are dropped beyond
     ``max_unclaimed_bytes``. Every other attribute is the wrapped service's."""
 
-    def __init__(self, inner, handler, workers=4, pinned=True):
+    def __init__(self, inner, handler, workers=4, pinned=True, device_decode=True, slot=8 << 20, ring=4):
         self.inner = inner
         self.handler = handler
         self.pinned = pinned
+        self.device_decode = device_decode and pinned
+        self.slot, self.ring = slot, ring
         self._pool = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="fedn_amd_upload")
+        self._streams = {}
+        self._lock = threading.Lock()
+
+    def _device(self):
+        """Where the handler wants decoded uploads: a device (decode through DeviceSink) or
+        None (host buffers, e.g. a multi-device handler that slices them itself)."""
+        if not self.device_decode:
+            return None
+        get = getattr(self.handler, "upload_device", None)
+        return get() if get is not None else None
+
+    def _stream(self, device):
+        import torch
+        key = (threading.get_ident(), str(device))
+        with self._lock:
+            st = self._streams.get(key)
+            if st is None:
+                st = self._streams[key] = torch.cuda.Stream(device)
+        return st
 
     def __getattr__(self, name):
         return getattr(self.inner, name)
@@ -282,18 +293,25 @@ class StreamingUpload:
             return a
         return alloc
 
-    def _decode(self, q, fut):
+    def _decode(self, q, fut, device):
         keep = []
-        dec = NpzStreamDecoder(self._alloc(keep))
         ended = False
         try:
+            if device is not None:
+                sink = DeviceSink(device, self._stream(device), self.slot, self.ring)
+            else:
+                sink = HostSink(self._alloc(keep))
+            dec = NpzStreamDecoder(sink=sink)
             while True:
                 chunk = q.get()
                 if chunk is None:
                     ended = True
                     break
                 dec.feed(chunk)
-            fut.set_result(DecodedUpdate(dec.finish(), keep))
+            members = dec.finish()
+            ready = sink.finish()
+            fut.set_result(DeviceDecodedUpdate(members, ready, device) if device is not None
+                           else DecodedUpdate(members, keep))
         except Exception as e:  # noqa: BLE001 — not adopted: the update takes the normal path
             keep.clear()
             fut.set_exception(e)
@@ -311,7 +329,7 @@ class StreamingUpload:
                         st = streams.get(rid)
                         if st is None and self.handler.wants_upload():
                             q, fut = queue.Queue(), Future()
-                            self._pool.submit(self._decode, q, fut)
+                            self._pool.submit(self._decode, q, fut, self._device())
                             st = streams[rid] = (q, fut)
                         if st is not None:
                             st[0].put(bytes(request.data))

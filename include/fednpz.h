@@ -72,6 +72,26 @@ int fnpz_write(int n, const char* const* names, const uint8_t* const* headers, c
                const void* const* datas, const int64_t* nbytes, int level, int threads, int64_t block,
                uint8_t* out, int64_t out_cap, int64_t* out_len);
 
+/* Streaming reader — an archive decoded while it arrives (ModelService.Upload chunks,
+ * fedn/network/combiner/modelservice.py:198-221), members taken from their local headers in
+ * archive order. Feed input with fnpz_stream_feed (copied), then call fnpz_stream_next until
+ * it reports FNPZ_EV_NEED_INPUT:
+ *   FNPZ_EV_MEMBER      *entry = the next member (name without ".npy", descr, fortran_order,
+ *                       shape, nbytes); its payload follows as FNPZ_EV_DATA events
+ *   FNPZ_EV_DATA        *out_len (> 0) payload bytes were inflated into out[0..out_cap); pass a
+ *                       window of at most the member's remaining bytes
+ *   FNPZ_EV_MEMBER_END  the member's payload is complete and its CRC-32 matched
+ *   FNPZ_EV_END         the central directory was reached: every member has been delivered
+ * An error status is sticky: the stream stays failed. */
+typedef struct fnpz_stream fnpz_stream;
+enum fnpz_event { FNPZ_EV_NEED_INPUT = 0, FNPZ_EV_MEMBER = 1, FNPZ_EV_DATA = 2, FNPZ_EV_MEMBER_END = 3, FNPZ_EV_END = 4 };
+
+int fnpz_stream_open(fnpz_stream** stream);
+void fnpz_stream_close(fnpz_stream* stream);
+int fnpz_stream_feed(fnpz_stream* stream, const uint8_t* data, int64_t len);
+int fnpz_stream_next(fnpz_stream* stream, uint8_t* out, int64_t out_cap, int* event, fnpz_entry* entry,
+                     int64_t* out_len);
+
 #ifdef __cplusplus
 }
 #endif

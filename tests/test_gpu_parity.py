@@ -414,13 +414,15 @@ def test_staging_ingest_npz_bytes(name, native):
     assert_lists_identical(model, rd["out"], name)
 
 
-@pytest.mark.parametrize("ndev", [1, 2])
+@pytest.mark.parametrize("ndev,sink", [(1, "device"), (1, "device-tiny"), (1, "host"), (2, "host")])
 @pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k8", "fedavg_int32_k3", "fedavg_skipbad_k4"])
-def test_streaming_upload_ingest(name, ndev):
+def test_streaming_upload_ingest(name, ndev, sink):
     """Updates uploaded through ModelService.Upload in 64 KiB chunks are decoded WHILE they
-    stream (upload.StreamingUpload, pinned blocks), adopted by the staging handler when their
-    ModelUpdate arrives and copied to HBM tensor by tensor (one device, or as parameter slices
-    over two): folded bit-exactly; the stored upload bytes are untouched."""
+    stream (upload.StreamingUpload), adopted by the staging handler when their ModelUpdate
+    arrives and placed in HBM: decoded straight to device blocks through the pinned ring
+    (sink "device"; "device-tiny" = 4 KiB slots x 2, so the ring wraps many times inside and
+    across tensors), or to pinned host blocks copied tensor by tensor (one device, or as
+    parameter slices over two): folded bit-exactly; the stored upload bytes are untouched."""
     import io
     from fedn_amd.aggregators.fedavg import Aggregator
     from fedn_amd.helper import Helper
@@ -431,7 +433,8 @@ def test_streaming_upload_ingest(name, ndev):
     uh = MemoryUpdateHandler()
     devs = [DEV] * ndev
     st = StagingUpdateHandler(uh, helper=Helper(), device=DEV, workers=3, devices=devs if ndev > 1 else None)
-    svc = StreamingUpload(MemoryModelService(uh.store), st, workers=2)
+    kw = {"host": {"device_decode": False}, "device": {}, "device-tiny": {"slot": 4096, "ring": 2}}[sink]
+    svc = StreamingUpload(MemoryModelService(uh.store), st, workers=2, **kw)
     for k, (arrays, n) in enumerate(rd["updates"]):
         b = io.BytesIO()
         np.savez_compressed(b, **{str(i): a for i, a in enumerate(arrays)})
@@ -444,6 +447,39 @@ def test_streaming_upload_ingest(name, ndev):
     st.close()
     assert data["nr_aggregated_models"] == rd["nr"]
     assert_lists_identical(model, rd["out"], name)
+
+
+def test_streaming_upload_ingest_large_ring():
+    """Multi-MiB tensors (fp32 + int64 + fp16) through the device sink with 64 KiB slots x 3,
+    the clients' chunks cut at odd sizes: == the oracle's fold of the same arrays."""
+    import io
+    from fedn_amd.aggregators.fedavg import Aggregator
+    from fedn_amd.helper import Helper
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryModelService, MemoryUpdateHandler, upload_requests
+    from fedn_amd.upload import StreamingUpload
+    rng = np.random.default_rng(77)
+    base = [rng.standard_normal((1031, 997)).astype(np.float32), rng.standard_normal(333_333).astype(np.float16)]
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=Helper(), device=DEV, workers=3)
+    svc = StreamingUpload(MemoryModelService(uh.store), st, workers=3, slot=65536, ring=3)
+    ups = []
+    for k in range(5):
+        arrays = [(base[0] + 0.01 * rng.standard_normal(base[0].shape)).astype(np.float32),
+                  rng.integers(-9, 9, 4099).astype(np.int64),
+                  (base[1] + 0.01 * rng.standard_normal(base[1].shape)).astype(np.float16)]
+        n = int(rng.integers(1, 5001))
+        b = io.BytesIO()
+        np.savez_compressed(b, **{str(i): a for i, a in enumerate(arrays)})
+        svc.Upload(upload_requests(b.getvalue(), f"L{k}", chunk=100_003 + 7 * k), None)
+        uh.submit_uploaded(f"L{k}", n, via=st)
+        ups.append((arrays, n))
+    model, data = Aggregator(st).combine_models(helper=Helper())
+    svc.close()
+    st.close()
+    want, nr = ref.fedavg_combine(ups)
+    assert data["nr_aggregated_models"] == nr == 5
+    assert_lists_identical(model, want, "large ring")
 
 
 def test_helper_increment_average_gpu():

@@ -7,8 +7,10 @@ tensor, as FEDn clients write it) concurrently in 1 MiB chunks, each paced at
 
   after-arrival  StagingUpdateHandler alone: each update is inflated by the native codec
                  when its ModelUpdate arrives (after its last chunk), then H2D
-  streaming      StreamingUpload in front of the ModelService: the update is inflated while
-                 its chunks arrive; the ModelUpdate only triggers the H2D
+  streaming-host StreamingUpload in front of the ModelService: the update is inflated while
+                 its chunks arrive into pinned host blocks; the ModelUpdate triggers the H2D
+  streaming      the same, inflated through DeviceSink's pinned ring straight to HBM while
+                 the chunks arrive; the ModelUpdate only triggers a D2D into the layout
 
 Reported: ``tail_s`` = last ModelUpdate → combine_models returned (what a round waits for
 after its last byte landed), the round wall time, and bit-equality of the two modes with a
@@ -40,9 +42,16 @@ def run(mode, blob, ns, rate, workers):
     uh = MemoryUpdateHandler()
     st = StagingUpdateHandler(uh, helper=Helper(), workers=workers)
     svc = MemoryModelService(uh.store)
-    if mode == "streaming":
-        svc = StreamingUpload(svc, st, workers=K)
+    if mode.startswith("streaming"):
+        svc = StreamingUpload(svc, st, workers=K, device_decode=mode == "streaming")
     order, lock, last = [], threading.Lock(), [0.0]
+    decoded_at = []
+    adopt = st.adopt
+
+    def adopt_timed(rid, fut):                        # when each streamed decode completed
+        fut.add_done_callback(lambda f: decoded_at.append(time.perf_counter()))
+        adopt(rid, fut)
+    st.adopt = adopt_timed
 
     def client(k):
         def paced():
@@ -65,13 +74,26 @@ def run(mode, blob, ns, rate, workers):
         t.start()
     for t in ths:
         t.join()
-    model, data = get_aggregator("fedavg", st).combine_models(helper=Helper())
+    t_agg = time.perf_counter()
+    agg = get_aggregator("fedavg", st)
+    t_init = time.perf_counter() - t_agg
+    t_del = [0.0]
+    delete = st.delete_model
+
+    def delete_timed(mu):
+        t = time.perf_counter()
+        delete(mu)
+        t_del[0] += time.perf_counter() - t
+    st.delete_model = delete_timed
+    model, data = agg.combine_models(helper=Helper())
     t1 = time.perf_counter()
     st.close()
-    if mode == "streaming":
+    if mode.startswith("streaming"):
         svc.close()
+    t_comb = t1 - t_agg
     return model, order, {"round_s": t1 - t0, "tail_s": t1 - last[0], "upload_s": last[0] - t0,
-                          "time_model_load": data["time_model_load"]}
+                          "decode_lag_s": (max(decoded_at) - last[0]) if decoded_at else None,
+                          "combine_s": t_comb, "aggregator_init_s": t_init, "delete_s": t_del[0], **{k: v for k, v in data.items() if isinstance(v, float)}}
 
 
 def main():
@@ -95,7 +117,7 @@ def main():
     ns = [int(v) for v in np.random.default_rng(0).integers(1, 5001, K)]
     res = {}
     for rep in range(a.reps):                         # rep 0 warms pinned / device pools
-        for mode in ("after-arrival", "streaming"):
+        for mode in ("after-arrival", "streaming-host", "streaming"):
             model, order, t = run(mode, blob, ns, a.client_MBps * 1e6, a.workers)
             uh = MemoryUpdateHandler()                # the same fold from host arrays
             for k in order:
@@ -107,10 +129,11 @@ def main():
                                                            for k, v in t.items()}}), flush=True)
     print(json.dumps({"what": "upload", "clients": K, "params": P, "archive_MB": round(len(blob) / 1e6, 1),
                       "client_MBps": a.client_MBps, "tail_after_arrival_s": round(res["after-arrival"]["tail_s"], 4),
+                      "tail_streaming_host_s": round(res["streaming-host"]["tail_s"], 4),
                       "tail_streaming_s": round(res["streaming"]["tail_s"], 4),
                       "round_after_arrival_s": round(res["after-arrival"]["round_s"], 4),
                       "round_streaming_s": round(res["streaming"]["round_s"], 4),
-                      "bit_exact": res["after-arrival"]["bit_exact"] and res["streaming"]["bit_exact"]}), flush=True)
+                      "bit_exact": all(r["bit_exact"] for r in res.values())}), flush=True)
 
 
 if __name__ == "__main__":
