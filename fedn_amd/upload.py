@@ -251,8 +251,10 @@ class StreamingUpload:
     unclaimed uploads (e.g. the combiner's own global models) are dropped beyond
     ``max_unclaimed_bytes``. Every other attribute is the wrapped service's."""
 
-    def __init__(self, inner, handler, workers=4, pinned=True, device_decode=True, slot=8 << 20, ring=4):
+    def __init__(self, inner, handler, workers=4, pinned=True, device_decode=True, slot=8 << 20, ring=4,
+                 upload=None):
         self.inner = inner
+        self._upload = upload if upload is not None else inner.Upload
         self.handler = handler
         self.pinned = pinned
         self.device_decode = device_decode and pinned
@@ -343,10 +345,38 @@ class StreamingUpload:
                     q.put(None)
                 streams.clear()
 
-        return self.inner.Upload(tee(), context)
+        return self._upload(tee(), context)
 
     def close(self):
         self._pool.shutdown(wait=True)
+
+
+class StreamingUploadMixin:
+    """The same, as a mixin of FEDn's ``ModelService`` (the gRPC server registers the model
+    servicer only if it IS a ``ModelServiceServicer``, grpc/server.py:57-58)::
+
+        class StreamingModelService(StreamingUploadMixin, ModelService): pass
+
+    ``attach(handler)`` starts decoding uploads for that handler; until then, and after
+    ``detach()``, ``Upload`` is the base class's unchanged."""
+
+    _streaming = None
+
+    def attach(self, handler, **kw):
+        base = super(StreamingUploadMixin, self).Upload
+        self._streaming = StreamingUpload(self, handler, upload=base, **kw)
+        return self._streaming
+
+    def detach(self):
+        s, self._streaming = self._streaming, None
+        if s is not None:
+            s.close()
+
+    def Upload(self, request_iterator, context):
+        s = self._streaming
+        if s is None:
+            return super().Upload(request_iterator, context)
+        return s.Upload(request_iterator, context)
 
 
 class AdoptedUploads:

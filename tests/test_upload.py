@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from fedn_amd import codec
-from fedn_amd.updatehandler import MemoryModelService, MemoryModelStore, ModelRequest, upload_requests
+from fedn_amd.updatehandler import MemoryModelService, MemoryModelStore, upload_requests
 from fedn_amd.upload import DecodedUpdate, DecodeError, NpzStreamDecoder, StreamingUpload
 
 ARRAYS = [np.arange(12, dtype=np.float32).reshape(3, 4), np.float64(2.5) * np.ones(()), np.zeros((0, 7), np.float32),
@@ -188,6 +188,28 @@ def test_streaming_upload_abandoned_stream_does_not_hang():
     t.start()
     t.join(30)
     assert not t.is_alive()
+
+
+def test_streaming_upload_mixin():
+    """StreamingUploadMixin on a ModelService class: the subclass is still the service (the
+    gRPC server's isinstance check), uploads are teed once a handler is attached."""
+    from fedn_amd.upload import StreamingUploadMixin
+
+    class Service(StreamingUploadMixin, MemoryModelService):
+        pass
+
+    store = MemoryModelStore()
+    svc = Service(store)
+    assert isinstance(svc, MemoryModelService)
+    data = _savez([np.arange(50_000, dtype=np.float32)])
+    svc.Upload(upload_requests(data, "plain", chunk=4096), None)
+    h = _Handler()
+    svc.attach(h, workers=1, pinned=False)
+    svc.Upload(upload_requests(data, "teed", chunk=4096), None)
+    assert store.get("plain").data == data and store.get("teed").data == data
+    assert list(h.adopted) == ["teed"]
+    _same_as_npload(data, h.adopted["teed"].result(timeout=30).arrays)
+    svc.detach()
 
 
 def test_staging_handler_upload_policy():
