@@ -321,6 +321,11 @@ class StreamingUpload:
                 ended = q.get() is None
 
     def Upload(self, request_iterator, context):
+        if context is self.inner or context is self:
+            # the service uploading to itself: ModelService.set_model passes the service as
+            # the context (modelservice.py:184-195), for the combiner's own global models,
+            # which no ModelUpdate will claim
+            return self._upload(request_iterator, context)
         streams = {}
 
         def tee():

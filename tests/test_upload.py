@@ -208,6 +208,8 @@ def test_streaming_upload_mixin():
     svc.Upload(upload_requests(data, "teed", chunk=4096), None)
     assert store.get("plain").data == data and store.get("teed").data == data
     assert list(h.adopted) == ["teed"]
+    svc.Upload(upload_requests(data, "own-global", chunk=4096), svc)   # ModelService.set_model (context=self)
+    assert store.get("own-global").data == data and "own-global" not in h.adopted
     _same_as_npload(data, h.adopted["teed"].result(timeout=30).arrays)
     svc.detach()
 
