@@ -449,6 +449,34 @@ def test_streaming_upload_ingest(name, ndev, sink):
     assert_lists_identical(model, rd["out"], name)
 
 
+@pytest.mark.parametrize("name", ["fedopt_adam_3r", "fedopt_yogi_lr1e-2_k8", "fedopt_adagrad_3r"])
+def test_streaming_upload_fedopt(name):
+    """FedOpt over three rounds with every client update decoded into HBM during its upload
+    (the global model from load_model, m / v carried): == the reference's fixtures."""
+    import io
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.helper import Helper
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryModelService, MemoryUpdateHandler, upload_requests
+    from fedn_amd.upload import StreamingUpload
+    case = load_case(name)
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=Helper(), device=DEV, workers=2)
+    svc = StreamingUpload(MemoryModelService(uh.store), st, workers=2, slot=8192, ring=2)
+    agg = get_aggregator("fedopt", st)
+    for r, rd in enumerate(case["rounds"]):
+        gid = uh.put_global_model(rd["old"], f"global-{r}")
+        for k, (arrays, n) in enumerate(rd["updates"]):
+            b = io.BytesIO()
+            np.savez_compressed(b, **{str(i): a for i, a in enumerate(arrays)})
+            svc.Upload(upload_requests(b.getvalue(), f"r{r}u{k}", chunk=5000), None)
+            uh.submit_uploaded(f"r{r}u{k}", n, model_id=gid, via=st)
+        model, _ = agg.combine_models(helper=Helper(), parameters=case["params"])
+        assert_lists_identical(model, rd["out"], f"{name} r{r}")
+    svc.close()
+    st.close()
+
+
 def test_streaming_upload_ingest_large_ring():
     """Multi-MiB tensors (fp32 + int64 + fp16) through the device sink with 64 KiB slots x 3,
     the clients' chunks cut at odd sizes: == the oracle's fold of the same arrays."""
