@@ -248,8 +248,9 @@ def test_fedavg_full_size_sampled():
 
 
 # ------------------------------------------------------------------------- Control.reduce
+@pytest.mark.parametrize("workers", [1, 3])
 @pytest.mark.parametrize("name", case_names("reduce"))
-def test_control_reduce_golden(name):
+def test_control_reduce_golden(name, workers):
     from fedn_amd.reduce import reduce_models
     case = load_case(name)
     store = {f"m{c}": m for c, (m, kind) in enumerate(zip(case["models"], case["plan"])) if kind != "missing"}
@@ -261,7 +262,7 @@ def test_control_reduce_golden(name):
         return store[mid]
 
     combiners = [{"name": f"c{c}", "model_id": f"m{c}"} for c in range(len(case["plan"]))]
-    model, meta = reduce_models(combiners, fetch=fetch, load=lambda d: d, delete=deleted.append)
+    model, meta = reduce_models(combiners, fetch=fetch, load=lambda d: d, delete=deleted.append, workers=workers)
     assert_lists_identical(model, case["out"], name)
     assert deleted == [c["model_id"] for c in combiners]
     assert set(meta) == {"time_fetch_model", "time_load_model", "time_aggregate_model"}

@@ -89,3 +89,24 @@ def test_update_handler_rejects_missing_metadata():
     uh = MemoryUpdateHandler()
     assert not uh.on_model_update(ModelUpdate("g", "u", '{"training_metadata": {}}'))
     assert uh.model_updates.empty()
+
+
+@pytest.mark.parametrize("workers", [1, 4])
+def test_reduce_load_error_propagates_in_order(workers):
+    """Control.reduce (control.py:674-690): a model whose decode raises is decoded again in the
+    except branch, which raises out of reduce — after the earlier combiners' deletions and
+    before any later one, also when later models were already decoded ahead."""
+    from fedn_amd.reduce import reduce_models
+    calls = []
+
+    def load(data):
+        calls.append(data)
+        raise ValueError(f"cannot decode {data}")
+
+    deleted = []
+    combiners = [{"name": f"c{c}", "model_id": f"m{c}"} for c in range(5)]
+    fetch = {"m1": "b1", "m2": "b2", "m3": "b3", "m4": "b4"}.__getitem__     # m0 missing
+    with pytest.raises(ValueError, match="cannot decode b1"):
+        reduce_models(combiners, fetch=fetch, load=load, delete=deleted.append, workers=workers)
+    assert deleted == ["m0"]
+    assert calls.count("b1") == 2

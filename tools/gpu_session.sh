@@ -45,6 +45,9 @@ for s in $STEPS; do
     ingest)
       timeout -k 10 900 python tools/bench_ingest.py > "$OUT/ingest.log" 2>&1; rc=$?
       echo "ingest rc=$rc"; grep -v amdgpu.ids "$OUT/ingest.log" | tail -4; [ $rc -eq 0 ] || exit $rc ;;
+    reduce)
+      timeout -k 10 600 python tools/bench_reduce.py > "$OUT/reduce.log" 2>&1; rc=$?
+      echo "reduce rc=$rc"; grep -v amdgpu.ids "$OUT/reduce.log" | tail -3; [ $rc -eq 0 ] || exit $rc ;;
     upload)
       timeout -k 10 600 python tools/bench_upload.py > "$OUT/upload.log" 2>&1; rc=$?
       echo "upload rc=$rc"; grep -v amdgpu.ids "$OUT/upload.log" | tail -5; [ $rc -eq 0 ] || exit $rc ;;
