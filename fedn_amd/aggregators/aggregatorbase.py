@@ -8,9 +8,68 @@ module at ``fedn/network/combiner/aggregators/<name>.py`` re-exports our Aggrega
 (see INTEGRATION.md).
 """
 import importlib
+import os
 from abc import ABC, abstractmethod
+from collections import deque
+from concurrent.futures import ThreadPoolExecutor
 
 AGGREGATOR_PLUGIN_PATH = "fedn_amd.aggregators.{}"
+LOAD_AHEAD = int(os.environ.get("FEDN_AMD_LOAD_AHEAD", "8"))
+
+
+def _raiser(e):
+    def load():
+        raise e
+    return load
+
+
+def queued_updates(update_handler, helper, ahead=None):
+    """The aggregators' drain of ``update_handler.model_updates`` (fedavg.py:109-112,
+    fedopt.py:76-80): yields ``(model_update, load)`` in FIFO order until the queue is empty,
+    where ``load()`` returns ``update_handler.load_model_update(model_update, helper)`` or
+    raises its error (``model_update`` is None if dequeuing itself raised). The caller folds
+    in that order, under its per-update error handling, exactly as the sequential loop.
+
+    FEDn decodes each update inside the loop, one after the other; an npz update is one
+    deflate stream per tensor (one core per update). Here up to ``ahead`` queued updates
+    are dequeued and decoded concurrently while earlier ones fold, so the fold waits for at
+    most one decode. A handler that stages updates on arrival (ingest.StagingUpdateHandler)
+    is drained one by one: its loads are already done."""
+    ahead = LOAD_AHEAD if ahead is None else ahead
+    q = update_handler.model_updates
+    if ahead <= 1 or getattr(update_handler, "stages_on_arrival", False):
+        while not q.empty():
+            try:
+                mu = update_handler.next_model_update()
+            except Exception as e:  # noqa: BLE001 — raised inside the caller's try, as FEDn's loop
+                yield None, _raiser(e)
+                continue
+            yield mu, (lambda mu=mu: update_handler.load_model_update(mu, helper))
+        return
+    pool = ThreadPoolExecutor(max_workers=ahead, thread_name_prefix="fedn_amd_load")
+    window = deque()
+
+    def fill():
+        while len(window) < ahead and not q.empty():
+            try:
+                mu = update_handler.next_model_update()
+            except Exception as e:  # noqa: BLE001
+                window.append((None, None, e))
+                continue
+            window.append((mu, pool.submit(update_handler.load_model_update, mu, helper), None))
+
+    try:
+        fill()
+        while window:
+            mu, fut, err = window.popleft()
+            fill()
+            yield mu, (_raiser(err) if err is not None else fut.result)
+            fill()
+    finally:
+        for _, fut, _ in window:
+            if fut is not None:
+                fut.cancel()
+        pool.shutdown(wait=True)
 
 
 class AggregatorBase(ABC):

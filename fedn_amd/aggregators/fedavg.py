@@ -21,7 +21,7 @@ import traceback
 import torch
 
 from ..staging import AndroidFedAvgPipeline, FedAvgPipeline, helper_kind
-from .aggregatorbase import AggregatorBase
+from .aggregatorbase import AggregatorBase, queued_updates
 
 logger = logging.getLogger("fedn")
 
@@ -68,11 +68,10 @@ class Aggregator(AggregatorBase):
         pipe = None
 
         logger.info("AGGREGATOR({}): Aggregating model updates... ".format(self.name))
-        while not self.update_handler.model_updates.empty():
+        for model_update, load in queued_updates(self.update_handler, helper):
             try:
-                model_update = self.update_handler.next_model_update()
                 tic = time.time()
-                model_next, metadata = self.update_handler.load_model_update(model_update, helper)
+                model_next, metadata = load()
                 data["time_model_load"] += time.time() - tic
 
                 total_examples += metadata["num_examples"]

@@ -20,7 +20,7 @@ import traceback
 from ..exceptions import InvalidParameterError
 from ..parameters import Parameters
 from ..staging import FedOptPipeline, FedOptState
-from .aggregatorbase import AggregatorBase
+from .aggregatorbase import AggregatorBase, queued_updates
 from .fedavg import default_device, env_devices
 
 logger = logging.getLogger("fedn")
@@ -73,11 +73,10 @@ class Aggregator(AggregatorBase):
 
         pipe = None
         nr_aggregated_models, total_examples = 0, 0
-        while not self.update_handler.model_updates.empty():
+        for model_update, load in queued_updates(self.update_handler, helper):
             try:
-                model_update = self.update_handler.next_model_update()
                 tic = time.time()
-                model_next, metadata = self.update_handler.load_model_update(model_update, helper)
+                model_next, metadata = load()
                 data["time_model_load"] += time.time() - tic
 
                 total_examples += metadata["num_examples"]

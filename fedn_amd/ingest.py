@@ -252,6 +252,8 @@ class StagingUpdateHandler:
     ``waitforit``, ...) is the wrapped handler's.
     """
 
+    stages_on_arrival = True       # aggregatorbase.queued_updates: loads are already done
+
     def __init__(self, inner, helper=None, device=None, workers=4, native_decode=True, devices=None,
                  max_unclaimed_upload_bytes=16 << 30):
         from .upload import AdoptedUploads

@@ -4,6 +4,8 @@ and the aggregate is encoded again for storage (roundhandler.py:465-470).
 
   reference-like  per update np.load (numpy inflate) serially inside the round, then the
                   GPU fold; np.savez_compressed of the result (what FEDn does on the host)
+  plain plug-in   the aggregator without the ingest wrapper: np.load of up to 8 queued
+                  updates concurrently ahead of the fold (aggregatorbase.queued_updates)
   fedn_amd        StagingUpdateHandler: each update inflated by the native codec straight
                   into pinned memory by a worker pool as it arrives + H2D, the fold in
                   combine_models, codec.save_npz (parallel deflate) of the result
@@ -73,11 +75,23 @@ def main():
         def load(self, f):
             z = np.load(f)
             return [z[str(i)] for i in range(len(z.files))]
+    from fedn_amd.aggregators import aggregatorbase
+    aggregatorbase.LOAD_AHEAD = 1            # FEDn's loop: each update decoded in turn
     model, data = get_aggregator("fedavg", uh).combine_models(helper=NumpyHelper())
+    aggregatorbase.LOAD_AHEAD = 8
     b = io.BytesIO()
     np.savez_compressed(b, **{str(i): w for i, w in enumerate(model)})
     t_ref = time.perf_counter() - t0
     ref_model = model
+
+    # the plain plug-in (no ingest wrapper): updates decoded 8 ahead of the fold (np.load)
+    t0 = time.perf_counter()
+    uh = MemoryUpdateHandler()
+    for k in range(K):
+        uh.submit_bytes(blob, ns[k])
+    model_pf, data_pf = get_aggregator("fedavg", uh).combine_models(helper=NumpyHelper())
+    t_plain = time.perf_counter() - t0
+    exact_pf = all(np.array_equal(p.view(np.uint32), q.view(np.uint32)) for p, q in zip(model_pf, ref_model))
 
     # fedn_amd: staged on arrival, native codec both ways
     for _ in range(2):                       # first pass warms pinned / device pools
@@ -92,7 +106,9 @@ def main():
         st.close()
     exact = all(np.array_equal(p.view(np.uint32), q.view(np.uint32)) for p, q in zip(model, ref_model))
     print(json.dumps({"what": "round", "clients": K, "params": P, "reference_like_s": t_ref,
-                      "reference_time_model_load": data["time_model_load"], "fedn_amd_s": t_ours,
+                      "reference_time_model_load": data["time_model_load"],
+                      "plain_plugin_load_ahead8_s": t_plain, "plain_plugin_bit_exact": exact_pf,
+                      "plain_plugin_time_model_load": data_pf["time_model_load"], "fedn_amd_s": t_ours,
                       "speedup": t_ref / t_ours, "bit_exact": exact, "workers": a.workers,
                       "fedn_amd_data": {k: round(v, 4) for k, v in data2.items() if isinstance(v, float)},
                       "encoded_MB": len(out) / 1e6}), flush=True)
