@@ -110,3 +110,25 @@ def test_reduce_load_error_propagates_in_order(workers):
         reduce_models(combiners, fetch=fetch, load=load, delete=deleted.append, workers=workers)
     assert deleted == ["m0"]
     assert calls.count("b1") == 2
+
+
+@pytest.mark.parametrize("ahead", [1, 3, 8])
+def test_queued_updates_fifo_errors_and_late_arrivals(ahead):
+    """aggregatorbase.queued_updates: FIFO order, a failing load raises from its own load()
+    (the caller skips it), and updates enqueued while the round drains are consumed too."""
+    from fedn_amd.aggregators.aggregatorbase import queued_updates
+    uh = MemoryUpdateHandler()
+    for k in range(5):
+        uh.submit([np.full(3, k, np.float32)], k + 1)
+    uh.store.models[list(uh.store.models)[2]] = None          # update 2 cannot be loaded
+    seen, errors = [], 0
+    for i, (mu, load) in enumerate(queued_updates(uh, None, ahead=ahead)):
+        try:
+            arrays, meta = load()
+            seen.append((int(arrays[0][0]), meta["num_examples"]))
+        except RuntimeError:
+            errors += 1
+        if i == 1:
+            uh.submit([np.full(3, 9, np.float32)], 10)          # arrives mid-round
+    assert seen == [(0, 1), (1, 2), (3, 4), (4, 5), (9, 10)] and errors == 1
+    assert uh.model_updates.empty()
