@@ -24,7 +24,7 @@ FA_ADAM, FA_YOGI, FA_ADAGRAD = 0, 1, 2
 FA_PG_FIRST, FA_PG_FINAL = 1, 2
 FA_EW_AXPBY, FA_EW_MUL, FA_EW_DIV, FA_EW_SQRT, FA_EW_SQUARE, FA_EW_SIGN, FA_EW_FILL = 0, 1, 2, 3, 4, 5, 6
 (FA_TUNE_STRIPS, FA_TUNE_UNROLL, FA_TUNE_NT, FA_TUNE_FASTDIV, FA_TUNE_LANETAB, FA_TUNE_GRID, FA_TUNE_READ,
- FA_TUNE_BLOCK, FA_TUNE_SUM_NOSTORE, FA_TUNE_NT_STORE, FA_TUNE_FASTDIV64) = range(11)
+ FA_TUNE_BLOCK, FA_TUNE_SUM_NOSTORE, FA_TUNE_NT_STORE, FA_TUNE_FASTDIV64, FA_TUNE_TILEMAP) = range(12)
 
 EXPORTS = {
     # name: (restype, argtypes)

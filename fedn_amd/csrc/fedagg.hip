@@ -480,8 +480,26 @@ struct LaneTable {
     }
 };
 
+// Workgroup -> tile order for the one-tile-per-workgroup grid (fa_tune FA_TUNE_TILEMAP).
+// Workgroups are dealt round-robin to the 8 XCDs, so with MAP 0 consecutive tiles run on
+// different XCDs. MAP = R > 0 gives each XCD runs of R consecutive tiles (groups of 8R tiles,
+// XCD x taking tiles [xR, xR + R) of each group): a bijection on the first whole groups and
+// the identity on the rest. (One contiguous eighth of the model per XCD measured 0.5-4 %
+// slower than identity: profiles/r01_tilemap.log.)
+template <int MAP>
+__device__ __forceinline__ int64_t map_tile(int64_t t, int64_t ntiles) {
+    if constexpr (MAP > 0) {
+        const int64_t g = ntiles / (8 * MAP);
+        if (t < 8 * MAP * g) {
+            const int64_t j = t / 8;
+            t = (j / MAP) * (8 * MAP) + (t % 8) * MAP + (j % MAP);
+        }
+    }
+    return t;
+}
+
 template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK = kBlock,
-          int NTS = 0>
+          int NTS = 0, int MAP = 0>
 __global__ void __launch_bounds__(BLK)
 k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P) {
     using V = typename CP::V;
@@ -489,7 +507,8 @@ k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const 
     const int64_t ntiles = ((P + E - 1) / E + (int64_t)BLK * S - 1) / ((int64_t)BLK * S);
     // one tile per block (gridDim == ntiles), or a persistent grid sweeping tiles in grid
     // order so the tiles read concurrently from one client buffer are adjacent
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int64_t tile = map_tile<MAP>(t, ntiles);
         const int64_t strip0 = tile * (BLK * S) + threadIdx.x;
         if ((strip0 + (int64_t)(S - 1) * BLK) * E + E > P) {
             k_fedavg_tail<Y, X, CP, E, S, INIT, INT_FIRST, BLK>(agg, tab, K, P, strip0);
@@ -876,6 +895,7 @@ struct FedAvgCfg {
     int nt_store = 1;         // pipelined kernel (S = 4, 256 threads) and fa_stream_sum: store mode 0 plain, 1 nt, 2 sc1;
                               // nt: -3 % time at K = 8, neutral at K = 64 (profiles/r01_store_probe.log)
     int nt = 0;   // measured: cached loads beat non-temporal ones by ~3% (profiles/)
+    int tilemap = 0;          // pipelined kernel (S = 4, nt stores): workgroup -> tile order (run length), see map_tile
 };
 FedAvgCfg g_cfg;
 
@@ -887,20 +907,23 @@ int device_cus() {
     return cus > 0 ? cus : 256;
 }
 
-template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT, int BLK = kBlock, int NTS = 0>
+template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT, int BLK = kBlock, int NTS = 0, int MAP = 0>
 void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
                         hipStream_t st) {
     const int64_t strips = (P + E - 1) / E;
     int64_t ntiles = (strips + (int64_t)BLK * S - 1) / ((int64_t)BLK * S);
-    if (g_cfg.grid_per_cu > 0) ntiles = std::min<int64_t>(ntiles, (int64_t)g_cfg.grid_per_cu * device_cus());
+    if (g_cfg.grid_per_cu > 0) {
+        if constexpr (MAP != 0) return launch_fedavg_pipe<Y, X, CP, E, S, NT, LT, BLK, NTS, 0>(a, tab, cnt, P, first, int_first, st);
+        ntiles = std::min<int64_t>(ntiles, (int64_t)g_cfg.grid_per_cu * device_cus());
+    }
     const dim3 grid((unsigned)ntiles);
     if (first && int_first) {
         if constexpr (std::is_integral<Y>::value)
-            hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, true, NT, LT, BLK, NTS>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
+            hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, true, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
     } else if (first)
-        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, false, NT, LT, BLK, NTS>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
+        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
     else
-        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, false, false, NT, LT, BLK, NTS>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
+        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, false, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
 }
 
 template <typename Y, typename X, class CP, int E, int S, int U, bool NT>
@@ -942,6 +965,15 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
             FA_GEOM(1, 8, 1) FA_GEOM(4, 2, 1) FA_GEOM(8, 1, 1)
             case 2 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 2, false, false>(a, tab, cnt, P, first, int_first, st);
             case 4 * 100 + 0:
+                if (g_cfg.nt_store == 1 && g_cfg.tilemap > 0) {
+                    switch (g_cfg.tilemap) {
+#define FA_MAP(R_) \
+    case R_: return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 1, R_>(a, tab, cnt, P, first, int_first, st);
+                        FA_MAP(2) FA_MAP(4) FA_MAP(8) FA_MAP(16) FA_MAP(32)
+#undef FA_MAP
+                        default: break;
+                    }
+                }
                 if (g_cfg.nt_store == 1) return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 1>(a, tab, cnt, P, first, int_first, st);
                 if (g_cfg.nt_store == 2) return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 2>(a, tab, cnt, P, first, int_first, st);
                 return launch_fedavg_pipe<Y, X, CP, E, 4, false, false>(a, tab, cnt, P, first, int_first, st);
@@ -1215,6 +1247,11 @@ int fa_tune(int knob, int value) {
         case FA_TUNE_GRID:
             if (value < 0 || value > 64) return fail(FA_EINVAL, "fa_tune: grid blocks per CU must be 0..64");
             g_cfg.grid_per_cu = value;
+            return FA_OK;
+        case FA_TUNE_TILEMAP:
+            if (value != 0 && value != 2 && value != 4 && value != 8 && value != 16 && value != 32)
+                return fail(FA_EINVAL, "fa_tune: tile map 0 (identity) or runs of 2, 4, 8, 16, 32 tiles per XCD");
+            g_cfg.tilemap = value;
             return FA_OK;
         case FA_TUNE_LANETAB:
             g_cfg.lanetab = value ? 1 : 0;

@@ -269,7 +269,8 @@ _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _a
           "fastdiv": _abi.FA_TUNE_FASTDIV, "lanetab": _abi.FA_TUNE_LANETAB,
           "grid": _abi.FA_TUNE_GRID, "read": _abi.FA_TUNE_READ,
           "block": _abi.FA_TUNE_BLOCK, "sum_nostore": _abi.FA_TUNE_SUM_NOSTORE,
-          "nt_store": _abi.FA_TUNE_NT_STORE, "fastdiv64": _abi.FA_TUNE_FASTDIV64}
+          "nt_store": _abi.FA_TUNE_NT_STORE, "fastdiv64": _abi.FA_TUNE_FASTDIV64,
+          "tilemap": _abi.FA_TUNE_TILEMAP}
 
 
 def tune(**knobs):
