@@ -60,12 +60,14 @@ EXPORTS = {
     "fa_elementwise": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int64,
                                       ctypes.c_void_p]),
+    "fa_cast": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                               ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "fa_stream_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "fa_stream_read_blocks": (ctypes.c_int64, [ctypes.c_int64]),
     "fa_stream_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class FedAggLibraryError(ImportError):
@@ -131,6 +133,13 @@ def ptr_array(ptrs):
     arr = (ctypes.c_void_p * max(1, len(ptrs)))()
     for i, p in enumerate(ptrs):
         arr[i] = ctypes.c_void_p(int(p))
+    return arr
+
+
+def int64_array(vals):
+    arr = (ctypes.c_int64 * max(1, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = int(v)
     return arr
 
 

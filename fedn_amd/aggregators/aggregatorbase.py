@@ -13,8 +13,12 @@ from abc import ABC, abstractmethod
 from collections import deque
 from concurrent.futures import ThreadPoolExecutor
 
+import numpy as np
+
 AGGREGATOR_PLUGIN_PATH = "fedn_amd.aggregators.{}"
 LOAD_AHEAD = int(os.environ.get("FEDN_AMD_LOAD_AHEAD", "8"))
+# host bytes of decoded-but-not-yet-folded updates the read-ahead may hold (FEDn holds one)
+LOAD_AHEAD_BYTES = int(os.environ.get("FEDN_AMD_LOAD_AHEAD_BYTES", str(2 << 30)))
 
 
 def _raiser(e):
@@ -23,7 +27,25 @@ def _raiser(e):
     return load
 
 
-def queued_updates(update_handler, helper, ahead=None):
+def model_nbytes(model):
+    """Host bytes of a decoded update (list of arrays); 0 if unknown."""
+    try:
+        return int(sum(np.asarray(a).nbytes for a in model))
+    except Exception:  # noqa: BLE001
+        return 0
+
+
+def requeue_front(q, items):
+    """Put dequeued ``items`` back at the HEAD of queue ``q`` in their FIFO order, as if they
+    had never been taken (``get`` does not count towards ``task_done``, so neither does this)."""
+    if not items:
+        return
+    with q.mutex:
+        q.queue.extendleft(reversed(items))
+        q.not_empty.notify(len(items))
+
+
+def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None):
     """The aggregators' drain of ``update_handler.model_updates`` (fedavg.py:109-112,
     fedopt.py:76-80): yields ``(model_update, load)`` in FIFO order until the queue is empty,
     where ``load()`` returns ``update_handler.load_model_update(model_update, helper)`` or
@@ -31,11 +53,18 @@ def queued_updates(update_handler, helper, ahead=None):
     in that order, under its per-update error handling, exactly as the sequential loop.
 
     FEDn decodes each update inside the loop, one after the other; an npz update is one
-    deflate stream per tensor (one core per update). Here up to ``ahead`` queued updates
-    are dequeued and decoded concurrently while earlier ones fold, so the fold waits for at
-    most one decode. A handler that stages updates on arrival (ingest.StagingUpdateHandler)
-    is drained one by one: its loads are already done."""
+    deflate stream per tensor (one core per update). Here queued updates are dequeued and
+    decoded concurrently while earlier ones fold, so the fold waits for at most one decode:
+    up to ``ahead`` updates, and — once the first decoded update shows the model's size — no
+    more than ``ahead_bytes`` of decoded updates (one at least). A handler that stages updates
+    on arrival (ingest.StagingUpdateHandler) is drained one by one: its loads are already done.
+
+    Lossless: if the caller stops early (an exception that escapes its per-update handling,
+    e.g. a BaseException, or ``close()``), the updates dequeued ahead but not yet handed out go
+    back to the head of the queue in FIFO order — what FEDn's sequential loop leaves queued.
+    Use it under ``contextlib.closing`` so that happens deterministically."""
     ahead = LOAD_AHEAD if ahead is None else ahead
+    ahead_bytes = LOAD_AHEAD_BYTES if ahead_bytes is None else ahead_bytes
     q = update_handler.model_updates
     if ahead <= 1 or getattr(update_handler, "stages_on_arrival", False):
         while not q.empty():
@@ -48,9 +77,15 @@ def queued_updates(update_handler, helper, ahead=None):
         return
     pool = ThreadPoolExecutor(max_workers=ahead, thread_name_prefix="fedn_amd_load")
     window = deque()
+    size = [None]                     # bytes of one decoded update, once known
+
+    def allowed():
+        if size[0] is None:
+            return 1
+        return max(1, min(ahead, ahead_bytes // max(1, size[0])))
 
     def fill():
-        while len(window) < ahead and not q.empty():
+        while len(window) < allowed() and not q.empty():
             try:
                 mu = update_handler.next_model_update()
             except Exception as e:  # noqa: BLE001
@@ -58,18 +93,29 @@ def queued_updates(update_handler, helper, ahead=None):
                 continue
             window.append((mu, pool.submit(update_handler.load_model_update, mu, helper), None))
 
+    def sized(fut):
+        def load():
+            res = fut.result()
+            if size[0] is None:
+                size[0] = model_nbytes(res[0])
+            return res
+        return load
+
     try:
         fill()
         while window:
             mu, fut, err = window.popleft()
             fill()
-            yield mu, (_raiser(err) if err is not None else fut.result)
+            yield mu, (_raiser(err) if err is not None else sized(fut))
             fill()
     finally:
+        back = [mu for mu, _, _ in window if mu is not None]
         for _, fut, _ in window:
             if fut is not None:
                 fut.cancel()
+        window.clear()
         pool.shutdown(wait=True)
+        requeue_front(q, back)
 
 
 class AggregatorBase(ABC):

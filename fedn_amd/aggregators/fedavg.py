@@ -13,6 +13,7 @@ on the GPU, bit-exact; a session on androidhelper folds with ITS rule instead,
 updates are staged through pinned memory and folded on arrival (fedn_amd/staging.py).
 Extra ``data`` keys: ``time_h2d`` / ``time_kernel`` (HIP events), ``time_pack``, ``time_d2h``.
 """
+import contextlib
 import logging
 import os
 import time
@@ -68,27 +69,28 @@ class Aggregator(AggregatorBase):
         pipe = None
 
         logger.info("AGGREGATOR({}): Aggregating model updates... ".format(self.name))
-        for model_update, load in queued_updates(self.update_handler, helper):
-            try:
-                tic = time.time()
-                model_next, metadata = load()
-                data["time_model_load"] += time.time() - tic
+        with contextlib.closing(queued_updates(self.update_handler, helper)) as updates:
+            for model_update, load in updates:
+                try:
+                    tic = time.time()
+                    model_next, metadata = load()
+                    data["time_model_load"] += time.time() - tic
 
-                total_examples += metadata["num_examples"]
+                    total_examples += metadata["num_examples"]
 
-                tic = time.time()
-                if nr_aggregated_models == 0:
-                    pipe = make_fedavg_pipeline(model_next, self.device, self.devices, helper)
-                else:
-                    pipe.add(model_next, metadata["num_examples"], total_examples)
-                data["time_model_aggregation"] += time.time() - tic
+                    tic = time.time()
+                    if nr_aggregated_models == 0:
+                        pipe = make_fedavg_pipeline(model_next, self.device, self.devices, helper)
+                    else:
+                        pipe.add(model_next, metadata["num_examples"], total_examples)
+                    data["time_model_aggregation"] += time.time() - tic
 
-                nr_aggregated_models += 1
-                if delete_models:
-                    self.update_handler.delete_model(model_update)
-            except Exception as e:  # noqa: BLE001 — fedavg.py:137-140: log and continue
-                logger.error(f"AGGREGATOR({self.name}): Error encoutered while processing model update: {e}")
-                logger.error(traceback.format_exc())
+                    nr_aggregated_models += 1
+                    if delete_models:
+                        self.update_handler.delete_model(model_update)
+                except Exception as e:  # noqa: BLE001 — fedavg.py:137-140: log and continue
+                    logger.error(f"AGGREGATOR({self.name}): Error encoutered while processing model update: {e}")
+                    logger.error(traceback.format_exc())
 
         data["nr_aggregated_models"] = nr_aggregated_models
         if pipe is not None:

@@ -13,6 +13,7 @@ Same contract and observable behaviour as fedopt.py:13-258:
   * output dtype float64 (``v`` starts as ``np.ones(...) * tau**2``, numpyhelper.py:141).
 The whole reduction runs in libfedagg (bit-exact to the numpy reference).
 """
+import contextlib
 import logging
 import time
 import traceback
@@ -73,33 +74,34 @@ class Aggregator(AggregatorBase):
 
         pipe = None
         nr_aggregated_models, total_examples = 0, 0
-        for model_update, load in queued_updates(self.update_handler, helper):
-            try:
-                tic = time.time()
-                model_next, metadata = load()
-                data["time_model_load"] += time.time() - tic
+        with contextlib.closing(queued_updates(self.update_handler, helper)) as updates:
+            for model_update, load in updates:
+                try:
+                    tic = time.time()
+                    model_next, metadata = load()
+                    data["time_model_load"] += time.time() - tic
 
-                total_examples += metadata["num_examples"]
-                tic = time.time()
-                if helper is not None and not hasattr(helper, "subtract"):
-                    # androidhelper has no numpyhelper primitives: fedopt.py:91 raises here for every
-                    # update, each is logged and skipped, and the round returns (None, data)
-                    raise AttributeError(f"'{type(helper).__name__}' object has no attribute 'subtract'")
-                if nr_aggregated_models == 0:
-                    model_old = self.update_handler.load_model(helper, model_update.model_id)
-                    pipe = self._pipeline(model_old, model_next)
-                pipe.add(model_next, metadata["num_examples"], total_examples)
-                data["time_model_aggregation"] += time.time() - tic
+                    total_examples += metadata["num_examples"]
+                    tic = time.time()
+                    if helper is not None and not hasattr(helper, "subtract"):
+                        # androidhelper has no numpyhelper primitives: fedopt.py:91 raises here for every
+                        # update, each is logged and skipped, and the round returns (None, data)
+                        raise AttributeError(f"'{type(helper).__name__}' object has no attribute 'subtract'")
+                    if nr_aggregated_models == 0:
+                        model_old = self.update_handler.load_model(helper, model_update.model_id)
+                        pipe = self._pipeline(model_old, model_next)
+                    pipe.add(model_next, metadata["num_examples"], total_examples)
+                    data["time_model_aggregation"] += time.time() - tic
 
-                nr_aggregated_models += 1
-                if delete_models:
-                    self.update_handler.delete_model(model_update)
-            except Exception as e:  # noqa: BLE001 — fedopt.py:103-106
-                logger.error(f"Error processing model update: {e}. Skipping this update.")
-                logger.error(traceback.format_exc())
-                if nr_aggregated_models == 0:
-                    pipe = None
-                continue
+                    nr_aggregated_models += 1
+                    if delete_models:
+                        self.update_handler.delete_model(model_update)
+                except Exception as e:  # noqa: BLE001 — fedopt.py:103-106
+                    logger.error(f"Error processing model update: {e}. Skipping this update.")
+                    logger.error(traceback.format_exc())
+                    if nr_aggregated_models == 0:
+                        pipe = None
+                    continue
 
         data["nr_aggregated_models"] = nr_aggregated_models
         if pipe is None or nr_aggregated_models == 0:

@@ -810,6 +810,38 @@ k_elementwise(int op, TO* __restrict__ out, const TX* __restrict__ x, const TY* 
 }
 
 // ----------------------------------------------------------------------------
+// broadcast + widening conversion (fa_cast): numpy's implicit operand preparation when a
+// client update differs from the running model in dtype or broadcastable shape. Only the
+// per-tensor path (fedn_amd/mixed.py) uses it; the uniform-round kernels above never do.
+// ----------------------------------------------------------------------------
+constexpr int kCastMaxDim = 8;
+struct CastGeom {
+    int64_t shape[kCastMaxDim];    // out shape (C order)
+    int64_t stride[kCastMaxDim];   // element strides of `in` per out dimension (0 = broadcast)
+    int ndim;
+};
+
+template <> __device__ __forceinline__ double widen<f16, double>(f16 v) { return (double)f16_to_f32(v.bits); }
+
+template <typename TI, typename TO, bool BC>
+__global__ void __launch_bounds__(kBlock)
+k_cast(TO* __restrict__ out, const TI* __restrict__ in, const CastGeom g, const int64_t P) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < P; i += (int64_t)gridDim.x * kBlock) {
+        int64_t j = i;
+        if constexpr (BC) {
+            int64_t rem = i;
+            j = 0;
+            for (int d = g.ndim - 1; d >= 0; --d) {
+                const int64_t q = rem / g.shape[d];
+                j += (rem - q * g.shape[d]) * g.stride[d];
+                rem = q;
+            }
+        }
+        out[i] = widen<TI, TO>(in[j]);
+    }
+}
+
+// ----------------------------------------------------------------------------
 // measurement kernels
 // ----------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) k_stream_copy(u32x4* __restrict__ dst, const u32x4* __restrict__ src, int64_t n16) {
@@ -1315,6 +1347,53 @@ int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype,
     else FA_EW(double, double, double);
 #undef FA_EW
     return check_launch("fa_elementwise");
+}
+
+int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, const int64_t* out_shape,
+            const int64_t* in_strides, void* stream) {
+    g_err[0] = 0;
+    if (!out_shape || !in_strides) return fail(FA_EINVAL, "fa_cast: null shape or strides");
+    if (ndim < 1 || ndim > kCastMaxDim) return fail(FA_EINVAL, "fa_cast: ndim must be 1..%d, got %d", kCastMaxDim, ndim);
+    CastGeom g;
+    g.ndim = ndim;
+    int64_t P = 1, cstride = 1;
+    bool bc = false;
+    for (int d = ndim - 1; d >= 0; --d) {
+        if (out_shape[d] < 0) return fail(FA_EINVAL, "fa_cast: negative dimension");
+        g.shape[d] = out_shape[d];
+        g.stride[d] = in_strides[d];
+        if (out_shape[d] != 1 && in_strides[d] != cstride) bc = true;   // not the contiguous identity map
+        cstride *= out_shape[d];
+    }
+    for (int d = 0; d < ndim; ++d) P *= out_shape[d];
+    if (P == 0) return FA_OK;
+    if (!out || !in) return fail(FA_EINVAL, "fa_cast: null buffer");
+    const dim3 grid((unsigned)std::min<int64_t>((P + kBlock - 1) / kBlock, 16384));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+#define FA_CAST(DI, TI, DO, TO)                                                                                     \
+    if (in_dtype == DI && out_dtype == DO) {                                                                        \
+        if (bc) hipLaunchKernelGGL((k_cast<TI, TO, true>), grid, dim3(kBlock), 0, st, static_cast<TO*>(out),        \
+                                   static_cast<const TI*>(in), g, P);                                                \
+        else hipLaunchKernelGGL((k_cast<TI, TO, false>), grid, dim3(kBlock), 0, st, static_cast<TO*>(out),          \
+                                static_cast<const TI*>(in), g, P);                                                   \
+        return check_launch("fa_cast");                                                                             \
+    }
+    FA_CAST(FA_F32, float, FA_F32, float)
+    FA_CAST(FA_F64, double, FA_F64, double)
+    FA_CAST(FA_F16, f16, FA_F16, f16)
+    FA_CAST(FA_BF16, bf16, FA_BF16, bf16)
+    FA_CAST(FA_I32, int32_t, FA_I32, int32_t)
+    FA_CAST(FA_I64, int64_t, FA_I64, int64_t)
+    FA_CAST(FA_F16, f16, FA_F32, float)
+    FA_CAST(FA_F16, f16, FA_F64, double)
+    FA_CAST(FA_BF16, bf16, FA_F32, float)
+    FA_CAST(FA_BF16, bf16, FA_F64, double)
+    FA_CAST(FA_F32, float, FA_F64, double)
+    FA_CAST(FA_I32, int32_t, FA_I64, int64_t)
+    FA_CAST(FA_I32, int32_t, FA_F64, double)
+    FA_CAST(FA_I64, int64_t, FA_F64, double)
+#undef FA_CAST
+    return fail(FA_EDTYPE, "fa_cast: unsupported conversion %d -> %d", in_dtype, out_dtype);
 }
 
 int fa_stream_copy(void* dst, const void* src, int64_t bytes, void* stream) {

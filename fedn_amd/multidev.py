@@ -23,12 +23,13 @@ model, the pseudo-gradient and the server state m / v resident across rounds
 moves between devices. The global model streams in through a pinned ring (no whole-model
 pinning), chunk by chunk with the server step when every update was device-resident.
 """
+import numpy as np
 import torch
 
-from . import ops
+from . import mixed, ops
 from .ingest import ShardedStagedModel, StagedModel
 from .layout import Layout
-from .staging import BATCH, HostStreamer, check_fedopt_dtypes, chunks, old_members
+from .staging import BATCH, HostStreamer, check_fedopt_dtypes, chunks, fused_fedopt_pair, group_tensors, old_members
 
 
 class _DevSlot:
@@ -108,6 +109,33 @@ class _ShardedStaging:
         for d in range(len(self.devices)):
             self.compute[d].wait_event(model.ready[d])
 
+    # ---- per-tensor path (mixed.py) on the first device: updates that differ in layout ------
+    def compatible(self, arrays):
+        if self._resident(arrays):
+            return arrays.layout.signature() == self.layout.signature()
+        arrays = _host_arrays(arrays)
+        if len(arrays) != len(self.layout.shapes):
+            return False
+        return all(tuple(np.shape(a)) == self.layout.shapes[i] and np.asarray(a).dtype == self.layout.dtypes[i]
+                   for i, a in enumerate(arrays))
+
+    def meta_of(self, arrays):
+        if self._resident(arrays):
+            return list(zip(arrays.layout.shapes, arrays.layout.dtypes))
+        return mixed.host_meta(_host_arrays(arrays))
+
+    def gathered(self, layout, bounds, slices):
+        """Per-tensor tensors on the first device from per-device slices ``slices[d][dt]``."""
+        return mixed.tensor_views(layout, mixed.gather_flats(layout, bounds, self.devices, slices, self.devices[0]))
+
+    def tensors_of(self, arrays):
+        """An update as per-tensor tensors on the first device (the per-tensor path runs there)."""
+        if self._resident(arrays):
+            self._accept(arrays)
+            return self.gathered(arrays.layout, arrays.bounds, [{dt: arrays.view(d, dt) for dt in arrays.layout.groups}
+                                                 for d in range(len(self.devices))])
+        return mixed.upload(_host_arrays(arrays), self.devices[0], self.compute[0])
+
     def _stage(self, arrays):
         self._ensure_slots()
         for _ in range(self.nslots):
@@ -182,14 +210,39 @@ class ShardedFedAvgPipeline(_ShardedStaging):
         self.nfolds = 0
         self.agg_started = False
         self.agg = [dict() for _ in self.devices]
+        self.general = None
+
+    def _state_meta(self):
+        lay = self.layout
+        if self.nfolds == 0:
+            return list(zip(lay.shapes, lay.dtypes))
+        return [(sh, mixed.np_dtype(ops.fold_result_dtype(ops.torch_dtype(d), ops.torch_dtype(d))))
+                for sh, d in zip(lay.shapes, lay.dtypes)]
+
+    def _enter_general(self):
+        """Continue the round per tensor on the first device (mixed.TensorFedAvg)."""
+        self._flush()
+        if self.agg_started:
+            slices = [{dt: self._agg(d, dt) for dt in self.layout.groups} for d in range(len(self.devices))]
+        else:
+            slices = [{dt: self._view(d, self.first, dt) for dt in self.layout.groups} for d in range(len(self.devices))]
+        self.general = mixed.TensorFedAvg(self.devices[0], self.compute[0], self.gathered(self.layout, self.bounds, slices),
+                                          owned=True)
 
     def add(self, arrays, n, N):
+        if self.general is None and not self.compatible(arrays):
+            plan = mixed.fold_plan(self._state_meta(), self.meta_of(arrays), n, N)   # raises as numpy
+            self._enter_general()
+            self.general.fold(self.tensors_of(arrays), n, N, plan=plan)
+            self.nfolds += 1
+            return
+        if self.general is not None:
+            self.general.fold(self.tensors_of(arrays), n, N)
+            self.nfolds += 1
+            return
         resident = self._resident(arrays)
-        if resident:
-            self.layout.check_layout(arrays.layout)
-        else:
+        if not resident:
             arrays = _host_arrays(arrays)
-            self.layout.check(arrays)
         for dt in self.layout.groups:           # refuse before touching device state
             ops.fa_dtype(ops.torch_dtype(dt))
         if resident:
@@ -249,6 +302,8 @@ class ShardedFedAvgPipeline(_ShardedStaging):
     def result(self):
         if self.nfolds == 0:
             return _host_arrays(self.first_arrays)     # `model = model_next` alias (fedavg.py:127-128)
+        if self.general is not None:
+            return self.general.result()
         entries, self.pending = self.pending, []
         init = not self.agg_started
         flats = {}
@@ -269,7 +324,9 @@ class ShardedFedAvgPipeline(_ShardedStaging):
 
 
 class ShardedFedOptState:
-    """FedOptState whose m / v are per-device slices: ``m[d][dt]`` is device d's slice."""
+    """FedOptState whose m / v are per-device slices: ``m[d][dt]`` is device d's slice. After a
+    round on the per-tensor path the state is per tensor on the first device (``m_t``/``v_t``)
+    and is re-sliced over the devices when a later round's layout allows it."""
 
     def __init__(self):
         self.m = None
@@ -278,24 +335,56 @@ class ShardedFedOptState:
         self.layout = None
         self.bounds = None
         self.devices = None
+        self.m_t = None
+        self.v_t = None
 
     def reset(self):
         self.__init__()
 
-    def _host(self, per_dev):
-        if per_dev is None:
-            return None
-        out = [None] * len(self.layout.shapes)
-        for dt in self.layout.groups:
-            owned = gather_group(self.layout, self.bounds[dt], self.devices, [x[dt] for x in per_dev], dt)
-            self.layout.unpack_group(owned, dt, out, copy=False)
-        return out
+    def tensors(self, device=None):
+        """(m, v) per tensor (model order) on ``device`` (default: the first device), or (None, None)."""
+        if self.m_t is not None:
+            return self.m_t, self.v_t
+        if self.m is None:
+            return None, None
+        dev = device if device is not None else self.devices[0]
+        out = []
+        for per_dev in (self.m, self.v):
+            flats = mixed.gather_flats(self.layout, self.bounds, self.devices, per_dev, dev)
+            out.append(mixed.tensor_views(self.layout, flats))
+        return out[0], out[1]
+
+    def set_tensors(self, m_t, v_t):
+        self.m = self.v = self.signature = self.layout = self.bounds = self.devices = None
+        self.m_t, self.v_t = m_t, v_t
+
+    def regroup(self, layout, sig, bounds, devices):
+        """Make the sliced form match ``layout`` over ``devices`` (see staging.FedOptState.regroup)."""
+        if self.m is None and self.m_t is None:
+            return True
+        if self.m is not None and self.signature == sig:
+            return True
+        m_t, v_t = self.tensors(devices[0])
+        grouped = group_tensors(layout, m_t, v_t, devices[0])
+        if grouped is None:
+            return False
+        m_flat, v_flat = grouped
+        self.m = [{dt: m_flat[dt][bounds[dt][d][0]:bounds[dt][d][1]].to(dv) for dt in layout.groups}
+                  for d, dv in enumerate(devices)]
+        self.v = [{dt: v_flat[dt][bounds[dt][d][0]:bounds[dt][d][1]].to(dv) for dt in layout.groups}
+                  for d, dv in enumerate(devices)]
+        self.signature, self.layout, self.bounds, self.devices = sig, layout, bounds, list(devices)
+        self.m_t = self.v_t = None
+        return True
+
+    def _host(self, ts):
+        return None if ts is None else [t.to("cpu").numpy() for t in ts]
 
     def m_host(self):
-        return self._host(self.m)
+        return self._host(self.tensors()[0])
 
     def v_host(self):
-        return self._host(self.v)
+        return self._host(self.tensors()[1])
 
 
 class ShardedFedOptPipeline(_ShardedStaging):
@@ -308,9 +397,21 @@ class ShardedFedOptPipeline(_ShardedStaging):
         else:
             layout = Layout.of(_host_arrays(first_arrays))
         super().__init__(devices, layout, nslots)
+        self.old_arrays = old_arrays
+        self.general = None
+        # see staging.FedOptPipeline: otherwise the round runs per tensor (first device)
+        self.fused_ok = True
+        try:
+            self.old_host = old_members(layout, old_arrays)
+            check_fedopt_dtypes(layout)
+            for dt, (odt, _) in self.old_host.items():
+                if not fused_fedopt_pair(ops.torch_dtype(dt), ops.torch_dtype(odt)):
+                    raise TypeError(f"no fused kernel for {dt} updates over a {odt} global model")
+        except (ValueError, TypeError):
+            self.fused_ok = False
+            self.old_host = {}
         # the global model reaches each device lazily through a pinned ring: whole (when a host
         # update must fold into pg) or chunk by chunk inside the server step (H2D || step || D2H)
-        self.old_host = old_members(layout, old_arrays)
         self.old = []
         for d, dv in enumerate(self.devices):
             per = {}
@@ -324,14 +425,33 @@ class ShardedFedOptPipeline(_ShardedStaging):
         self.pg_started = False
         self.nfolds = 0
 
+    def _pg_meta(self):
+        return [(sh, mixed.np_dtype(ops.fedopt_dtypes(ops.torch_dtype(d), self.old[0][d].dtype, None)[0]))
+                for sh, d in zip(self.layout.shapes, self.layout.dtypes)]
+
+    def _enter_general(self):
+        """Continue the round per tensor on the first device (mixed.TensorFedOpt)."""
+        self._flush()
+        pg = None
+        if self.pg_started:
+            pg = self.gathered(self.layout, self.bounds, [{dt: self._pg(d, dt) for dt in self.layout.groups}
+                                             for d in range(len(self.devices))])
+        old = mixed.upload(self.old_arrays, self.devices[0], self.compute[0])
+        self.general = mixed.TensorFedOpt(self.devices[0], self.compute[0], old, pg)
+
     def add(self, arrays, n, N):
+        if self.general is None and not (self.fused_ok and self.compatible(arrays)):
+            splan = mixed.sub_plan(self.meta_of(arrays), mixed.host_meta(self.old_arrays))   # raises as numpy
+            if self.nfolds:
+                mixed.fold_plan(self._pg_meta(), [(sh, d) for d, sh in splan], n, N)
+            self._enter_general()
+        if self.general is not None:
+            self.general.add(self.tensors_of(arrays), n, N)
+            self.nfolds += 1
+            return
         resident = self._resident(arrays)
-        if resident:
-            self.layout.check_layout(arrays.layout)
-        else:
+        if not resident:
             arrays = _host_arrays(arrays)
-            self.layout.check(arrays)
-        check_fedopt_dtypes(self.layout)
         if resident:
             self._accept(arrays)
             self.pending.append((arrays, n, N))
@@ -387,8 +507,13 @@ class ShardedFedOptPipeline(_ShardedStaging):
         if opt not in ("adam", "yogi", "adagrad"):
             raise ValueError(f"Unsupported server optimizer: {opt}")
         sig = (self.layout.signature(), tuple(str(d) for d in self.devices))
-        if state.signature is not None and state.signature != sig:
-            raise ValueError("model layout or devices changed between rounds; FedOpt state (m, v) does not match")
+        if self.general is None and not state.regroup(self.layout, sig, self.bounds, self.devices):
+            self._enter_general()               # the state's layout differs from this round's
+        if self.general is not None:
+            m, v = state.tensors(self.devices[0])
+            model, m, v = self.general.server_step(m, v, params)
+            state.set_tensors(m, v)
+            return model
         # per device and group, one fused launch: pending (resident) updates folded into the
         # pseudo-gradient in registers (FIRST when pg holds nothing yet) and the server step,
         # chunked so that the global model's H2D, the step and the result's D2H overlap

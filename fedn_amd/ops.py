@@ -239,6 +239,51 @@ def fedopt_step(old, updates, n, N, *, first, final, pg=None, m_in=None, m_out=N
     _abi.check(rc)
 
 
+def cast(out, x, stream=None):
+    """``out[...] = x`` broadcast to ``out.shape`` and widened to ``out.dtype`` (``fa_cast``):
+    numpy's implicit operand preparation for a binary ufunc whose operands differ in dtype or
+    broadcastable shape. ``out`` is contiguous; ``x`` any strided device tensor."""
+    lib = _abi.load()
+    if out.device != x.device:
+        raise ValueError(f"cast: {x.device} -> {out.device}")
+    if not out.is_contiguous():
+        raise ValueError("cast: out must be contiguous")
+    oshape = tuple(out.shape)
+    xshape = tuple(x.shape)
+    if len(xshape) > len(oshape):
+        raise ValueError(f"cast: cannot broadcast {xshape} to {oshape}")
+    # right-align x's dims to out's (numpy broadcasting); stride 0 where x has extent 1
+    lead = len(oshape) - len(xshape)
+    strides = [0] * lead
+    for d, (xs, st) in enumerate(zip(xshape, x.stride())):
+        os_ = oshape[lead + d]
+        if xs == os_:
+            strides.append(st if xs != 1 else 0)
+        elif xs == 1:
+            strides.append(0)
+        else:
+            raise ValueError(f"cast: cannot broadcast {xshape} to {oshape}")
+    # drop extent-1 dims, then merge adjacent dims that are contiguous in both (keeps ndim
+    # within the kernel's limit)
+    dims = [(s, t) for s, t in zip(oshape, strides) if s != 1] or [(1, 0)]
+    ms, mt = [dims[0][0]], [dims[0][1]]
+    for s, t in dims[1:]:
+        if mt[-1] == t * s:
+            ms[-1] *= s
+            mt[-1] = t
+        else:
+            ms.append(s)
+            mt.append(t)
+    if len(ms) > 8:
+        raise ValueError(f"cast: {len(ms)} non-mergeable dimensions (kernel limit 8)")
+    with torch.cuda.device(out.device):
+        st = _stream_handle(out, stream)
+        rc = lib.fa_cast(out.data_ptr(), fa_dtype(out), x.data_ptr(), fa_dtype(x), len(ms), _abi.int64_array(ms),
+                         _abi.int64_array(mt), st)
+    _abi.check(rc)
+    return out
+
+
 def stream_copy(dst, src, stream=None):
     lib = _abi.load()
     st = _stream_handle(src, stream)

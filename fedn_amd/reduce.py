@@ -14,6 +14,7 @@ Use it from FEDn by mixing :class:`GpuReduceMixin` into ``Control`` (INTEGRATION
 import time
 from concurrent.futures import ThreadPoolExecutor
 
+from .aggregators.aggregatorbase import LOAD_AHEAD_BYTES, model_nbytes
 from .aggregators.fedavg import default_device
 from .staging import FedAvgPipeline
 
@@ -44,8 +45,9 @@ def reduce_models(combiners, fetch, load, delete=None, device=None, workers=8):
     delete(model_id) optional repository cleanup.
     workers         combiners fetched + decoded ahead of the fold, concurrently (decoding an
                     npz is one deflate stream per tensor, i.e. one core per model; FEDn does
-                    them one after the other). The fold order, the replace-on-error rule and
-                    the deletions stay those of the sequential loop.
+                    them one after the other), within LOAD_AHEAD_BYTES of decoded models. The
+                    fold order, the replace-on-error rule and the deletions stay those of the
+                    sequential loop.
     """
     meta = {"time_fetch_model": 0.0, "time_load_model": 0.0, "time_aggregate_model": 0.0}
     i = 1
@@ -53,19 +55,26 @@ def reduce_models(combiners, fetch, load, delete=None, device=None, workers=8):
     ids = [c["model_id"] for c in combiners]
     pool = ThreadPoolExecutor(max_workers=max(1, workers), thread_name_prefix="fedn_amd_reduce") if workers > 1 else None
     pending = {}
+    nxt = [0]                              # next combiner index to submit
+    size = [None]                          # host bytes of one decoded model, once known
 
-    def submit(j):
-        if pool is not None and j < len(ids) and j not in pending:
-            pending[j] = pool.submit(_fetch_load, fetch, load, ids[j])
+    def top_up():
+        """Keep up to ``workers`` decodes in flight, and no more decoded-but-unfolded bytes than
+        LOAD_AHEAD_BYTES once a model's size is known (one at a time until then)."""
+        cap = 1 if size[0] is None else max(1, min(workers, LOAD_AHEAD_BYTES // max(1, size[0])))
+        while pool is not None and nxt[0] < len(ids) and len(pending) < cap:
+            pending[nxt[0]] = pool.submit(_fetch_load, fetch, load, ids[nxt[0]])
+            nxt[0] += 1
 
     try:
-        for j in range(min(workers, len(ids))):
-            submit(j)
         for j, model_id in enumerate(ids):
+            top_up()
             fut = pending.pop(j, None)
             data, model_next, err, t_fetch, t_load = fut.result() if fut is not None else \
                 _fetch_load(fetch, load, model_id)
-            submit(j + max(1, workers))
+            if size[0] is None and model_next is not None:
+                size[0] = model_nbytes(model_next)
+            top_up()
             meta["time_fetch_model"] += t_fetch
             if data is not None:
                 meta["time_load_model"] += t_load if err is None else 0.0

@@ -25,7 +25,7 @@ import time
 import numpy as np
 import torch
 
-from . import ops
+from . import mixed, ops
 from .ingest import StagedModel
 from .layout import Layout, parallel_copy
 
@@ -150,18 +150,50 @@ class _Pipeline:
         stream waits for its H2D); host arrays are packed into a ring slot."""
         if isinstance(arrays, StagedModel):
             self.layout.check_layout(arrays.layout)      # raises the numpy-like error
-            if arrays.dev.device != self.device:         # staged on another GPU: one D2D copy
-                arrays.ready.synchronize()               # (rare) order the copy after its H2D
-                with torch.cuda.device(self.device):
-                    dev = arrays.dev.to(self.device)
-                    ready = torch.cuda.Event()
-                    ready.record(torch.cuda.current_stream(self.device))
-                arrays = StagedModel(arrays.layout, dev, ready, None)
-            self.compute.wait_event(arrays.ready)
-            self._hold.append(arrays)                    # keep HBM alive until the round ends
-            return arrays
+            return self._resident(arrays)
         self.layout.check(arrays)
         return self.stage(arrays)
+
+    def _resident(self, arrays):
+        """A StagedModel usable on this device: the compute stream waits for its H2D (one D2D
+        copy first if it was staged on another GPU); held until the round ends."""
+        if arrays.dev.device != self.device:         # staged on another GPU: one D2D copy
+            arrays.ready.synchronize()               # (rare) order the copy after its H2D
+            with torch.cuda.device(self.device):
+                dev = arrays.dev.to(self.device)
+                ready = torch.cuda.Event()
+                ready.record(torch.cuda.current_stream(self.device))
+            arrays = StagedModel(arrays.layout, dev, ready, None)
+        self.compute.wait_event(arrays.ready)
+        self._hold.append(arrays)                    # keep HBM alive until the round ends
+        return arrays
+
+    # ---- per-tensor path (mixed.py): updates that differ from the first in dtype or shape ----
+    def compatible(self, arrays):
+        """Whether ``arrays`` has exactly this round's layout (the fused multi-client path)."""
+        if isinstance(arrays, StagedModel):
+            return arrays.layout.signature() == self.layout.signature()
+        if len(arrays) != len(self.layout.shapes):
+            return False
+        for i, a in enumerate(arrays):
+            a = np.asarray(a)
+            if tuple(a.shape) != self.layout.shapes[i] or a.dtype != self.layout.dtypes[i]:
+                return False
+        return True
+
+    def tensors_of(self, arrays):
+        """Per-tensor device tensors of an update for the per-tensor path: views of a staged
+        update (the compute stream ordered after its H2D), or host arrays copied per tensor."""
+        if isinstance(arrays, StagedModel):
+            arrays = self._resident(arrays)
+            return mixed.tensor_views(arrays.layout, mixed.u8_flats(arrays.layout, arrays.dev))
+        return mixed.upload(arrays, self.device, self.compute)
+
+    @staticmethod
+    def meta_of(arrays):
+        if isinstance(arrays, StagedModel):
+            return list(zip(arrays.layout.shapes, arrays.layout.dtypes))
+        return mixed.host_meta(arrays)
 
     def group(self, slot, dt):
         """Device view (flat, torch dtype) of group ``dt`` inside a staged slot."""
@@ -231,11 +263,44 @@ class FedAvgPipeline(_Pipeline):
         self.nfolds = 0
         self.agg_started = False                 # agg holds a fold of the first update
         self.agg = {}
+        self.general = None                      # mixed.TensorFedAvg once an update differs in layout
+
+    def _state_meta(self):
+        """(shape, dtype) per tensor of the running model: the first update's before any fold,
+        numpy's fold result dtype after."""
+        lay = self.layout
+        if self.nfolds == 0:
+            return list(zip(lay.shapes, lay.dtypes))
+        return [(s, mixed.np_dtype(ops.fold_result_dtype(ops.torch_dtype(d), ops.torch_dtype(d))))
+                for s, d in zip(lay.shapes, lay.dtypes)]
+
+    def _enter_general(self):
+        """Hand the running model to the per-tensor path (mixed.TensorFedAvg)."""
+        self._flush()
+        if self.agg_started:
+            views = mixed.tensor_views(self.layout, {dt: self._agg(dt) for dt in self.layout.groups})
+            self.general = mixed.TensorFedAvg(self.device, self.compute, views, owned=True)
+        else:
+            src = self.first.dev
+            views = mixed.tensor_views(self.layout, mixed.u8_flats(self.layout, src))
+            self.general = mixed.TensorFedAvg(self.device, self.compute, views, owned=False)
 
     def add(self, arrays, n, N):
         """Fold one more update (n = its num_examples, N = running total including it).
         A device-resident update (StagedModel) joins the pending batch; host arrays are
-        staged and folded on arrival (after any pending batch, keeping FIFO order)."""
+        staged and folded on arrival (after any pending batch, keeping FIFO order). An update
+        whose dtypes or shapes differ from the first's moves the round to the per-tensor path
+        (numpy promotion / broadcasting, mixed.py) — checked before any state changes."""
+        if self.general is None and not self.compatible(arrays):
+            plan = mixed.fold_plan(self._state_meta(), self.meta_of(arrays), n, N)   # raises as numpy
+            self._enter_general()
+            self.general.fold(self.tensors_of(arrays), n, N, plan=plan)
+            self.nfolds += 1
+            return
+        if self.general is not None:
+            self.general.fold(self.tensors_of(arrays), n, N)
+            self.nfolds += 1
+            return
         if isinstance(arrays, StagedModel):
             self.layout.check_layout(arrays.layout)
         else:
@@ -298,6 +363,8 @@ class FedAvgPipeline(_Pipeline):
         if self.nfolds == 0:
             first = self.first_arrays           # `model = model_next` alias (fedavg.py:127-128)
             return first.host if isinstance(first, StagedModel) else first
+        if self.general is not None:
+            return self.general.result()
         tic = time.perf_counter()
         entries, self.pending = self.pending, []
         init = not self.agg_started
@@ -377,8 +444,10 @@ class AndroidFedAvgPipeline(_Pipeline):
 class FedOptState:
     """Server-optimizer state of one fedopt Aggregator instance (fedopt.py:36-38), in HBM.
 
-    ``m`` / ``v`` map a layout group to a flat device tensor (m: f32 or f64, v: f64);
-    None until the first server step, exactly like the reference's ``self.m``/``self.v``.
+    Fused form: ``m`` / ``v`` map a layout group to a flat device tensor (m: f32 or f64,
+    v: f64) for ``layout``. Per-tensor form (after a round on the per-tensor path, mixed.py):
+    ``m_t`` / ``v_t`` are lists of device tensors in model order. Both None until the first
+    server step, exactly like the reference's ``self.m``/``self.v``.
     """
 
     def __init__(self):
@@ -386,26 +455,73 @@ class FedOptState:
         self.v = None
         self.signature = None
         self.layout = None
+        self.m_t = None
+        self.v_t = None
 
     def reset(self):
         self.__init__()
 
-    def _host(self, d):
-        if d is None:
+    def tensors(self):
+        """(m, v) as per-tensor device tensors in model order, or (None, None)."""
+        if self.m_t is not None:
+            return self.m_t, self.v_t
+        if self.m is None:
+            return None, None
+        return mixed.tensor_views(self.layout, self.m), mixed.tensor_views(self.layout, self.v)
+
+    def set_tensors(self, m_t, v_t):
+        self.m = self.v = self.signature = self.layout = None
+        self.m_t, self.v_t = m_t, v_t
+
+    def regroup(self, layout, sig, device):
+        """Make the fused form match ``layout``: True if it does (or the state is empty), False
+        if the per-tensor state cannot be grouped that way (shapes differ, or one group would
+        need two m dtypes) — then the round's server step runs per tensor."""
+        if self.m is None and self.m_t is None:
+            return True
+        if self.m is not None and self.signature == sig:
+            return True
+        m_t, v_t = self.tensors()
+        grouped = group_tensors(layout, m_t, v_t, device)
+        if grouped is None:
+            return False
+        self.m, self.v = grouped
+        self.signature, self.layout = sig, layout
+        self.m_t = self.v_t = None
+        return True
+
+    def _host(self, ts):
+        if ts is None:
             return None
-        out = [None] * len(self.layout.shapes)
-        for dt in self.layout.groups:
-            h = d[dt].to("cpu").numpy()
-            for i, off in self.layout.members[dt]:
-                out[i] = np.array(h[off:off + self.layout.sizes[i]]).reshape(self.layout.shapes[i])
-        return out
+        return [t.to("cpu").numpy() for t in ts]
 
     def m_host(self):
         """``m`` as host ``list[np.ndarray]`` in tensor order (what fedopt.py keeps in self.m)."""
-        return self._host(self.m)
+        return self._host(self.tensors()[0])
 
     def v_host(self):
-        return self._host(self.v)
+        return self._host(self.tensors()[1])
+
+
+def group_tensors(layout, m_t, v_t, device):
+    """Per-tensor (m, v) -> fused ({group: flat m}, {group: flat v}) on ``device`` for ``layout``,
+    or None when not expressible (tensor count or shapes differ; mixed m dtypes in a group)."""
+    if len(m_t) != len(layout.shapes) or len(v_t) != len(layout.shapes):
+        return None
+    m, v = {}, {}
+    for dt in layout.groups:
+        idx = [i for i, _ in layout.members[dt]]
+        mdts = {m_t[i].dtype for i in idx}
+        if len(mdts) != 1 or any(tuple(m_t[i].shape) != layout.shapes[i] or tuple(v_t[i].shape) != layout.shapes[i]
+                                 for i in idx):
+            return None
+        fm = torch.empty(layout.group_elems[dt], dtype=mdts.pop(), device=device)
+        fv = torch.empty(layout.group_elems[dt], dtype=torch.float64, device=device)
+        for i, off in layout.members[dt]:
+            fm[off:off + layout.sizes[i]].copy_(m_t[i].reshape(-1))
+            fv[off:off + layout.sizes[i]].copy_(v_t[i].reshape(-1))
+        m[dt], v[dt] = fm, fv
+    return m, v
 
 
 def old_groups(layout, old_arrays):
@@ -451,6 +567,17 @@ def old_members(layout, old_arrays):
     return out
 
 
+_FUSED_OPT = {(torch.float32, torch.float32), (torch.bfloat16, torch.float32), (torch.float32, torch.float64),
+              (torch.float64, torch.float64), (torch.bfloat16, torch.float64), (torch.float64, torch.float32),
+              (torch.int64, torch.int64), (torch.int64, torch.float64), (torch.int64, torch.float32),
+              (torch.int32, torch.int32), (torch.int32, torch.float64), (torch.int32, torch.float32)}
+
+
+def fused_fedopt_pair(upd, old):
+    """Whether fa_fedopt_step instantiates (update dtype, global-model dtype)."""
+    return (upd, old) in _FUSED_OPT
+
+
 def check_fedopt_dtypes(layout):
     for dt in layout.groups:
         if ops.torch_dtype(dt) not in (torch.float32, torch.float64, torch.int32, torch.int64):
@@ -464,27 +591,61 @@ class FedOptPipeline(_Pipeline):
     def __init__(self, device, old_arrays, first_arrays, nslots=2):
         layout = first_arrays.layout if isinstance(first_arrays, StagedModel) else Layout.of(first_arrays)
         super().__init__(device, layout, nslots)
-        # the global model reaches HBM lazily: whole (when a host update must fold into pg) or
-        # chunk by chunk inside the server step's pipeline (H2D || step || D2H)
-        self.old_host = old_members(layout, old_arrays)
-        self.old = {dt: torch.empty(layout.group_elems[dt], dtype=ops.torch_dtype(odt), device=self.device)
-                    for dt, (odt, _) in self.old_host.items()}
-        self.old_ready = set()
-        self.streamer = HostStreamer()
-        self.pg = {}
-        self.pg_started = False                  # pg holds a partial pseudo-gradient
         self.old_arrays = old_arrays
         self.nfolds = 0
+        self.pg = {}
+        self.pg_started = False                  # pg holds a partial pseudo-gradient
+        self.general = None                      # mixed.TensorFedOpt once an update differs in layout
+        self.old_ready = set()
+        self.streamer = HostStreamer()
+        # the fused path needs the global model to share the update's shapes with one dtype per
+        # update-dtype group, and a (update, old) dtype pair the kernel instantiates; otherwise
+        # the round runs on the per-tensor path (numpy promotion / broadcasting, mixed.py)
+        self.fused_ok = True
+        try:
+            self.old_host = old_members(layout, old_arrays)
+            check_fedopt_dtypes(layout)
+            for dt, (odt, _) in self.old_host.items():
+                if not fused_fedopt_pair(ops.torch_dtype(dt), ops.torch_dtype(odt)):
+                    raise TypeError(f"no fused kernel for {dt} updates over a {odt} global model")
+        except (ValueError, TypeError):
+            self.fused_ok = False
+            self.old_host = {}
+        # the global model reaches HBM lazily: whole (when a host update must fold into pg) or
+        # chunk by chunk inside the server step's pipeline (H2D || step || D2H)
+        self.old = {dt: torch.empty(layout.group_elems[dt], dtype=ops.torch_dtype(odt), device=self.device)
+                    for dt, (odt, _) in self.old_host.items()}
+
+    def _pg_meta(self):
+        """(shape, dtype) per tensor of the pseudo-gradient folded so far (fused layout)."""
+        return [(s, mixed.np_dtype(ops.fedopt_dtypes(ops.torch_dtype(d), self.old[d].dtype, None)[0]))
+                for s, d in zip(self.layout.shapes, self.layout.dtypes)]
+
+    def _enter_general(self):
+        """Hand the round to the per-tensor path (mixed.TensorFedOpt): pending updates are folded
+        into pg first, which then continues per tensor."""
+        self._flush()
+        pg = None
+        if self.pg_started:
+            pg = mixed.tensor_views(self.layout, {dt: self._pg(dt) for dt in self.layout.groups})
+        old = mixed.upload(self.old_arrays, self.device, self.compute)
+        self.general = mixed.TensorFedOpt(self.device, self.compute, old, pg)
 
     def add(self, arrays, n, N):
         """One more update into the pseudo-gradient (fedopt.py:89-94). Device-resident updates
         join the pending batch, which the server step folds in its fused launch; host arrays
-        are staged and folded into pg on arrival (after any pending batch)."""
-        if isinstance(arrays, StagedModel):
-            self.layout.check_layout(arrays.layout)
-        else:
-            self.layout.check(arrays)
-        check_fedopt_dtypes(self.layout)
+        are staged and folded into pg on arrival (after any pending batch). Updates that differ
+        from the first in dtype or shape, or from the global model in shape, run per tensor."""
+        if self.general is None and not (self.fused_ok and self.compatible(arrays)):
+            ym = self.meta_of(arrays)
+            splan = mixed.sub_plan(ym, mixed.host_meta(self.old_arrays))          # raises as numpy
+            if self.nfolds:
+                mixed.fold_plan(self._pg_meta(), [(sh, d) for d, sh in splan], n, N)
+            self._enter_general()
+        if self.general is not None:
+            self.general.add(self.tensors_of(arrays), n, N)
+            self.nfolds += 1
+            return
         if isinstance(arrays, StagedModel):
             self.pending.append((self.acquire(arrays), n, N))
             if len(self.pending) >= BATCH:
@@ -534,8 +695,13 @@ class FedOptPipeline(_Pipeline):
         if opt not in ("adam", "yogi", "adagrad"):
             raise ValueError(f"Unsupported server optimizer: {opt}")
         sig = self.layout.signature()
-        if state.signature is not None and state.signature != sig:
-            raise ValueError("model layout changed between rounds; FedOpt state (m, v) does not match")
+        if self.general is None and not state.regroup(self.layout, sig, self.device):
+            self._enter_general()               # the state's layout differs from this round's
+        if self.general is not None:
+            m, v = state.tensors()
+            model, m, v = self.general.server_step(m, v, params)
+            state.set_tensors(m, v)
+            return model
         # one fused launch per group: the pending (device-resident) updates, if any, folded into
         # the pseudo-gradient in registers (FIRST when pg holds nothing yet) and the server
         # step; chunked so that each chunk's D2H of the new model overlaps the next chunk

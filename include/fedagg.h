@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 2
+#define FA_ABI_VERSION 3
 
 /* element type codes */
 enum fa_dtype {
@@ -162,6 +162,23 @@ int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype,
 /* dtype promotion used by the two entry points above (numpy result_type for the
  * pairs this library supports; bf16 promotes as f32). Returns FA_NONE if unsupported. */
 int fa_promote(int a, int b);
+
+/*
+ * Broadcast + widening conversion, the implicit step numpy takes before a binary ufunc whose
+ * operands differ in dtype or (broadcastable) shape — e.g. numpyhelper.py:32 folding a float64
+ * client into a float32 model, an int64 model with a float32 client, or a (1,) tensor against
+ * (n,). Used by the per-tensor path of the plug-ins (fedn_amd/mixed.py) when client updates
+ * differ from the running model (fedavg.py:68, fedopt.py:91-94, control.py:682).
+ *
+ *   out[i] = convert(in[j(i)])      i over the ndim-dimensional C-order index space out_shape,
+ *                                   j(i) = sum_d i_d * in_strides[d] (element strides; 0 along
+ *                                   broadcast dimensions)
+ * Conversions (numpy's casting of the value): identity for every dtype; F16/BF16 -> F32/F64 and
+ * F32 -> F64 (exact); I32 -> I64 (exact); I32/I64 -> F64 (round to nearest even). Narrowing
+ * conversions are refused (FA_EDTYPE). 1 <= ndim <= 8; out is contiguous.
+ */
+int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, const int64_t* out_shape,
+            const int64_t* in_strides, void* stream);
 
 /*
  * Measurement helpers (not part of the reference interface): achievable-peak

@@ -13,6 +13,10 @@ from oracle import numpy_ref as ref
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
+# clients that differ from the first in dtype / broadcastable shape (numpy promotion, mixed.py)
+MIXED_FEDAVG = [n for n in case_names("fedavg") if "_mix_" in n or "_bcast_" in n or "fewer_tensors" in n]
+MIXED_FEDOPT = [n for n in case_names("fedopt") if "_mix_" in n or "_bcast_" in n or "layout_change" in n
+                or "f64_clients" in n]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -270,7 +274,7 @@ def test_control_reduce_golden(name, workers):
 
 # ------------------------------------------------------------------------- streaming ingest
 @pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k17", "fedavg_skipbad_k4", "fedavg_int64_k3",
-                                  "fedavg_odd_k1"])
+                                  "fedavg_odd_k1"] + MIXED_FEDAVG)
 def test_staging_ingest_fedavg_golden(name):
     """Updates staged into HBM on arrival (ingest.StagingUpdateHandler) give the same result."""
     from fedn_amd.aggregators import get_aggregator
@@ -287,7 +291,7 @@ def test_staging_ingest_fedavg_golden(name):
     assert_lists_identical(model, rd["out"], name)
 
 
-@pytest.mark.parametrize("name", ["fedopt_adam_3r", "fedopt_yogi_lr1e-2_k8"])
+@pytest.mark.parametrize("name", ["fedopt_adam_3r", "fedopt_yogi_lr1e-2_k8"] + MIXED_FEDOPT)
 def test_staging_ingest_fedopt_golden(name):
     from fedn_amd.aggregators import get_aggregator
     from fedn_amd.ingest import StagingUpdateHandler
@@ -392,7 +396,8 @@ def test_staging_batched_large_chunked_d2h():
 
 
 @pytest.mark.parametrize("native", [True, False])
-@pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k8", "fedavg_int32_k3", "fedavg_skipbad_k4"])
+@pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k8", "fedavg_int32_k3", "fedavg_skipbad_k4",
+                                  "fedavg_mix_f32_f64_k4", "fedavg_bcast_k4", "fedavg_mix_pertensor_k5"])
 def test_staging_ingest_npz_bytes(name, native):
     """Updates arriving as npz bytes (numpy savez_compressed, as FEDn clients upload them):
     inflated by the native codec straight into pinned memory (native=True) or decoded by
@@ -416,7 +421,8 @@ def test_staging_ingest_npz_bytes(name, native):
 
 
 @pytest.mark.parametrize("ndev,sink", [(1, "device"), (1, "device-tiny"), (1, "host"), (2, "host")])
-@pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k8", "fedavg_int32_k3", "fedavg_skipbad_k4"])
+@pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k8", "fedavg_int32_k3", "fedavg_skipbad_k4",
+                                  "fedavg_mix_i64_f32_k3", "fedavg_bcast_k4"])
 def test_streaming_upload_ingest(name, ndev, sink):
     """Updates uploaded through ModelService.Upload in 64 KiB chunks are decoded WHILE they
     stream (upload.StreamingUpload), adopted by the staging handler when their ModelUpdate
@@ -450,7 +456,8 @@ def test_streaming_upload_ingest(name, ndev, sink):
     assert_lists_identical(model, rd["out"], name)
 
 
-@pytest.mark.parametrize("name", ["fedopt_adam_3r", "fedopt_yogi_lr1e-2_k8", "fedopt_adagrad_3r"])
+@pytest.mark.parametrize("name", ["fedopt_adam_3r", "fedopt_yogi_lr1e-2_k8", "fedopt_adagrad_3r",
+                                  "fedopt_mix_yogi_3r"])
 def test_streaming_upload_fedopt(name):
     """FedOpt over three rounds with every client update decoded into HBM during its upload
     (the global model from load_model, m / v carried): == the reference's fixtures."""
@@ -525,7 +532,7 @@ def test_helper_increment_average_gpu():
 
 # ------------------------------------------------------------------------- one process, several devices
 @pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k17", "fedavg_int64_k3", "fedavg_skipbad_k4",
-                                  "fedavg_odd_k1", "fedavg_flat_k8"])
+                                  "fedavg_odd_k1", "fedavg_flat_k8"] + MIXED_FEDAVG)
 @pytest.mark.parametrize("ndev", [2, 3])
 def test_multidevice_fedavg_golden(name, ndev):
     """Parameter-slice sharding across devices inside one process (multidev.py); the box has
@@ -948,3 +955,82 @@ def test_helper_sessions_through_ingest(name):
     st.close()
     assert data["nr_aggregated_models"] == rd["nr"]
     assert_lists_identical([model if android else model[0]], [rd["out"]], name)
+
+
+# ------------------------------------------------------------------------- fa_cast (mixed.py operand prep)
+@pytest.mark.parametrize("src,dst", [(np.float16, np.float32), (np.float16, np.float64), (np.float32, np.float64),
+                                     (np.int32, np.int64), (np.int32, np.float64), (np.int64, np.float64),
+                                     (np.float32, np.float32), (np.int64, np.int64), (np.float16, np.float16)])
+@pytest.mark.parametrize("xshape,oshape", [((1000,), (1000,)), ((1,), (4099,)), ((), (3, 5)), ((3, 1), (3, 7)),
+                                           ((1, 7), (5, 7)), ((2, 1, 3), (4, 2, 5, 3)), ((0,), (0,))])
+def test_cast_broadcast_vs_numpy(src, dst, xshape, oshape):
+    """fa_cast == np.broadcast_to(x, shape).astype(dst): numpy's operand conversion (values that
+    stress int64 -> float64 rounding included)."""
+    from fedn_amd import ops
+    rng = np.random.default_rng(11)
+    if np.dtype(src).kind == "i":
+        x = rng.integers(np.iinfo(src).min, np.iinfo(src).max, size=xshape, dtype=src)
+    else:
+        x = (rng.standard_normal(xshape) * 100).astype(src)
+    out = torch.empty(oshape, dtype=ops.torch_dtype(dst), device=DEV)
+    ops.cast(out, torch.from_numpy(np.ascontiguousarray(x)).to(DEV))
+    want = np.broadcast_to(x, oshape).astype(dst)
+    assert_lists_identical([out.cpu().numpy()], [want], f"{src}->{dst} {xshape}->{oshape}")
+
+
+def test_cast_strided_source():
+    """A non-contiguous source view (a transposed slice) is read through its strides."""
+    from fedn_amd import ops
+    x = torch.arange(60, dtype=torch.float32, device=DEV).view(6, 10)[:, 2:7].t()   # (5, 6), strided
+    out = torch.empty(5, 6, dtype=torch.float64, device=DEV)
+    ops.cast(out, x)
+    assert torch.equal(out.cpu(), x.cpu().double())
+
+
+def test_cast_refuses_narrowing():
+    from fedn_amd import _abi, ops
+    x = torch.ones(8, dtype=torch.float64, device=DEV)
+    with pytest.raises(_abi.FedAggError):
+        ops.cast(torch.empty(8, dtype=torch.float32, device=DEV), x)
+
+
+@pytest.mark.parametrize("ndev", [2, 3])
+@pytest.mark.parametrize("name", ["fedavg_mix_f32_f64_k4", "fedavg_bcast_k4", "fedavg_mix_i64_f32_k3"])
+def test_multidevice_sharded_ingest_mixed(name, ndev):
+    """Updates staged as parameter slices over several devices (ShardedStagedModel) whose layouts
+    differ: the round moves to the per-tensor path on the first device, bit-exact."""
+    from fedn_amd.aggregators.fedavg import Aggregator
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rd = load_case(name)["rounds"][0]
+    uh = MemoryUpdateHandler()
+    devs = [DEV] * ndev
+    st = StagingUpdateHandler(uh, helper=None, device=DEV, workers=2, devices=devs)
+    for arrays, n in rd["updates"]:
+        uh.submit(arrays, n, via=st)
+    model, data = Aggregator(st, devices=devs).combine_models(helper=None)
+    st.close()
+    assert data["nr_aggregated_models"] == rd["nr"]
+    assert_lists_identical(model, rd["out"], f"{name} x{ndev}")
+
+
+@pytest.mark.parametrize("ndev", [2])
+@pytest.mark.parametrize("name", ["fedopt_mix_adam_3r", "fedopt_layout_change_3r"])
+def test_multidevice_sharded_ingest_fedopt_mixed(name, ndev):
+    from fedn_amd.aggregators.fedopt import Aggregator
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    case = load_case(name)
+    uh = MemoryUpdateHandler()
+    devs = [DEV] * ndev
+    st = StagingUpdateHandler(uh, helper=None, device=DEV, workers=2, devices=devs)
+    agg = Aggregator(st, devices=devs)
+    for r, rd in enumerate(case["rounds"]):
+        gid = uh.put_global_model(rd["old"], f"global-{r}")
+        for arrays, n in rd["updates"]:
+            uh.submit(arrays, n, model_id=gid, via=st)
+        model, _ = agg.combine_models(helper=None, parameters=case["params"])
+        assert_lists_identical(model, rd["out"], f"{name} x{ndev} r{r}")
+        assert_lists_identical(agg.m, rd["m"], f"{name} x{ndev} r{r} m")
+        assert_lists_identical(agg.v, rd["v"], f"{name} x{ndev} r{r} v")
+    st.close()

@@ -132,3 +132,118 @@ def test_queued_updates_fifo_errors_and_late_arrivals(ahead):
             uh.submit([np.full(3, 9, np.float32)], 10)          # arrives mid-round
     assert seen == [(0, 1), (1, 2), (3, 4), (4, 5), (9, 10)] and errors == 1
     assert uh.model_updates.empty()
+
+
+class _Abort(BaseException):
+    """Escapes the aggregators' per-update ``except Exception`` (like InvalidParameterError)."""
+
+
+def _ids(q):
+    return [mu.model_update_id for mu in list(q.queue)]
+
+
+@pytest.mark.parametrize("ahead", [1, 3, 8])
+@pytest.mark.parametrize("where", ["body", "load"])
+def test_queued_updates_lossless_on_abort(ahead, where):
+    """An exception that escapes the caller's per-update handling mid-round — raised by the loop
+    body, or by load_model_update itself (a BaseException travels out of the worker's future) —
+    leaves exactly what FEDn's sequential loop leaves queued (fedavg.py:47-78): every update after
+    the one being processed, in FIFO order; the read-ahead puts back what it dequeued early."""
+    import contextlib
+
+    from fedn_amd.aggregators.aggregatorbase import queued_updates
+    uh = MemoryUpdateHandler()
+    for k in range(10):
+        uh.submit([np.full(3, k, np.float32)], k + 1)
+    order = _ids(uh.model_updates)
+    if where == "load":
+        inner = uh.load_model_update
+
+        def load_model_update(mu, helper):
+            if mu.model_update_id == order[3]:
+                raise _Abort()
+            return inner(mu, helper)
+        uh.load_model_update = load_model_update
+    got = []
+    with pytest.raises(_Abort):
+        with contextlib.closing(queued_updates(uh, None, ahead=ahead)) as it:
+            for mu, load in it:
+                arrays, _ = load()
+                got.append(int(arrays[0][0]))
+                if where == "body" and len(got) == 4:
+                    raise _Abort()
+    assert _ids(uh.model_updates) == order[4:]          # update 3 was being processed: consumed
+    assert got == [0, 1, 2, 3] if where == "body" else got == [0, 1, 2]
+
+
+def test_queued_updates_byte_cap():
+    """Once one decoded update's size is known, the read-ahead holds at most ahead_bytes of
+    decoded updates (at least one), whatever ``ahead`` says."""
+    import threading
+
+    from fedn_amd.aggregators.aggregatorbase import queued_updates
+    uh = MemoryUpdateHandler()
+    for k in range(12):
+        uh.submit([np.full(250, k, np.float32)], 1)          # 1000 bytes per update
+    started, lock = [], threading.Lock()
+    inner = uh.load_model_update
+
+    def load_model_update(mu, helper):
+        with lock:
+            started.append(mu.model_update_id)
+        return inner(mu, helper)
+    uh.load_model_update = load_model_update
+    consumed = 0
+    for mu, load in queued_updates(uh, None, ahead=8, ahead_bytes=2500):
+        load()
+        consumed += 1
+        # decodes started so far <= consumed + the 2 the byte budget allows (+1 being handed out)
+        assert len(started) <= consumed + 3
+    assert consumed == 12
+
+
+def test_reduce_byte_cap_keeps_order():
+    """reduce_models with a byte budget smaller than one model still folds in combiner order."""
+    import fedn_amd.reduce as red
+    seen = []
+
+    class Pipe:
+        def __init__(self, dev, m):
+            seen.append(("first", int(m[0][0])))
+
+        def add(self, m, n, N):
+            seen.append((int(m[0][0]), N))
+
+        def result(self):
+            return "ok"
+    saved = red.FedAvgPipeline, red.LOAD_AHEAD_BYTES
+    red.FedAvgPipeline, red.LOAD_AHEAD_BYTES = Pipe, 10
+    try:
+        combiners = [{"name": f"c{c}", "model_id": c} for c in range(6)]
+        model, _ = red.reduce_models(combiners, fetch=lambda c: c, load=lambda c: [np.full(100, c, np.float32)],
+                                     device="cpu", workers=4)
+    finally:
+        red.FedAvgPipeline, red.LOAD_AHEAD_BYTES = saved
+    assert model == "ok"
+    assert seen == [("first", 0), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6)]
+
+
+def test_mixed_fold_plan_is_numpy():
+    """mixed.fold_plan / sub_plan infer numpy's result dtypes and shapes (numpyhelper.py:32, :44)
+    from metadata alone, and raise where numpy raises."""
+    from fedn_amd import mixed
+    f4, f8, i4, i8, f2 = (np.dtype(t) for t in (np.float32, np.float64, np.int32, np.int64, np.float16))
+    cases = [((f4, (7,)), (f8, (7,))), ((i8, (3,)), (f4, (3,))), ((f2, (2, 1)), (f4, (1, 5))),
+             ((i4, ()), (i8, (4,))), ((f8, (1,)), (i4, (6,)))]
+    for (xd, xs), (yd, ys) in cases:
+        (d, r, shape), = mixed.fold_plan([(xs, xd)], [(ys, yd)], 37, 1234)
+        x, y = np.ones(xs, xd), np.ones(ys, yd)
+        want = np.add(x, 37 * (y - x) / 1234)
+        assert (r, shape) == (want.dtype, want.shape) and d == (y - x).dtype
+    with pytest.raises(ValueError):
+        mixed.fold_plan([((5,), f4)], [((4,), f4)], 1, 2)
+    assert len(mixed.fold_plan([((1,), f4)] * 3, [((1,), f4)] * 2, 1, 2)) == 2       # zip truncates
+    with pytest.raises(TypeError):
+        mixed.fold_plan([((3,), i8)], [((3,), i8)], 2.5, 4)                          # int diff, float n
+    (r, shape), = mixed.sub_plan([((3,), i8)], [((1,), f4)])
+    assert r == (np.ones(3, i8) * 1.0 + np.ones(1, f4) * -1.0).dtype and shape == (3,)

@@ -275,6 +275,158 @@ def reduce_case(ref, name, rng, shapes, plan):
     return d
 
 
+def _tensor(rng, shape, dtype):
+    """One client tensor: integers for integer dtypes, ~1 + 0.01 N(0,1) for floats."""
+    dtype = np.dtype(dtype)
+    if dtype.kind in "iu":
+        return rng.integers(-1000, 1000, size=shape).astype(dtype)
+    return (1.0 + 0.01 * rng.standard_normal(shape)).astype(dtype)
+
+
+def fedavg_clients_case(ref, name, rng, clients, nks):
+    """FedAvg over clients whose tensors differ from the first client's in dtype and/or
+    (broadcastable) shape: numpyhelper.py:32 promotes and broadcasts them. ``clients`` holds,
+    per client, a list of (shape, dtype) per tensor."""
+    h = Harness(ref, "fedavg")
+    d = {"kind": np.array("fedavg"), "name": np.array(name)}
+    for k, (spec, n) in enumerate(zip(clients, nks)):
+        u = [_tensor(rng, s, dt) for s, dt in spec]
+        h.push_update(u, int(n), "global-0")
+        _store_list(d, f"r0_u{k}", u)
+    d["r0_n"] = np.array(nks, dtype=np.int64)
+    d["r0_K"] = np.array(len(nks))
+    model, data = h.combine()
+    d["r0_nr"] = np.array(data["nr_aggregated_models"])
+    d["r0_data_keys"] = np.array(json.dumps(sorted(data)))
+    d["r0_qsize"] = np.array(h.uh.model_updates.qsize())
+    d["r0_out_none"] = np.array(model is None)
+    if model is not None:
+        _store_list(d, "r0_out", model)
+    d["rounds"] = np.array(1)
+    return d
+
+
+def fedopt_clients_case(ref, name, rng, old_spec, rounds, params=None):
+    """FedOpt rounds whose clients differ from the global model (and from each other) in dtype
+    and/or broadcastable shape (fedopt.py:89-94: subtract + increment_average promote and
+    broadcast). ``rounds`` holds, per round, per client a list of (shape, dtype); a round's
+    global model is the previous round's output."""
+    h = Harness(ref, "fedopt")
+    d = {"kind": np.array("fedopt"), "name": np.array(name)}
+    d["params"] = np.array(json.dumps(params))
+    old = [_tensor(rng, s, dt) for s, dt in old_spec]
+    for r, clients in enumerate(rounds):
+        gid = f"global-{r}"
+        h.put_model(old, gid)
+        _store_list(d, f"r{r}_old", old)
+        nks = rng.integers(1, 5001, len(clients))
+        for k, (spec, n) in enumerate(zip(clients, nks)):
+            u = [_tensor(rng, s, dt) for s, dt in spec]
+            h.push_update(u, int(n), gid)
+            _store_list(d, f"r{r}_u{k}", u)
+        d[f"r{r}_n"] = np.array(nks, dtype=np.int64)
+        d[f"r{r}_K"] = np.array(len(clients))
+        model, data = h.combine(ref["Parameters"](params) if params is not None else None)
+        d[f"r{r}_nr"] = np.array(data.get("nr_aggregated_models", -1))
+        d[f"r{r}_data_keys"] = np.array(json.dumps(sorted(data)))
+        d[f"r{r}_qsize"] = np.array(h.uh.model_updates.qsize())
+        d[f"r{r}_out_none"] = np.array(model is None)
+        if model is not None:
+            _store_list(d, f"r{r}_out", model)
+        d[f"r{r}_m_none"] = np.array(h.agg.m is None)
+        d[f"r{r}_v_none"] = np.array(h.agg.v is None)
+        if h.agg.m is not None:
+            _store_list(d, f"r{r}_m", h.agg.m)
+        if h.agg.v is not None:
+            _store_list(d, f"r{r}_v", h.agg.v)
+        if model is not None:
+            old = model
+    d["rounds"] = np.array(len(rounds))
+    return d
+
+
+def reduce_dtypes_case(ref, name, rng, shapes, dtypes):
+    """Control.reduce (control.py:648-693, loop restated as in reduce_case) over combiner models
+    saved in different dtypes: every fold is the REAL numpyhelper.increment_average."""
+    h = ref["Helper"]()
+    plan = ["ok"] * len(dtypes)
+    d = {"kind": np.array("reduce"), "name": np.array(name), "plan": np.array(json.dumps(plan))}
+    models = []
+    for c, dt in enumerate(dtypes):
+        m = [_tensor(rng, s, dt) for s in shapes]
+        models.append(m)
+        _store_list(d, f"c{c}", m)
+    i, model = 1, None
+    for m in models:
+        try:
+            model = h.increment_average(model, m, 1.0, i)
+        except Exception:  # noqa: BLE001  (control.py:683-686)
+            model = m
+        i = i + 1
+    _store_list(d, "out", model)
+    d["out_none"] = np.array(False)
+    return d
+
+
+F16, F32, F64, I32, I64 = np.float16, np.float32, np.float64, np.int32, np.int64
+MIX_SHAPES = [(7,), (3, 5), (2053,), ()]
+
+
+def _spec(dtypes, shapes=MIX_SHAPES):
+    """(shape, dtype) per tensor; one dtype for all tensors or one per tensor."""
+    if not isinstance(dtypes, (list, tuple)):
+        dtypes = [dtypes] * len(shapes)
+    return list(zip(shapes, dtypes))
+
+
+def mixed_cases(ref):
+    """Clients whose updates differ in dtype or broadcastable shape."""
+    rng = np.random.default_rng(7)
+    nk = lambda K: rng.integers(1, 5001, K)  # noqa: E731
+    cases = [
+        fedavg_clients_case(ref, "fedavg_mix_f32_f64_k4", rng, [_spec(F32), _spec(F64), _spec(F32), _spec(F64)], nk(4)),
+        fedavg_clients_case(ref, "fedavg_mix_f64_f32_k3", rng, [_spec(F64), _spec(F32), _spec(F32)], nk(3)),
+        fedavg_clients_case(ref, "fedavg_mix_i64_f32_k3", rng, [_spec(I64), _spec(F32), _spec(I64)], nk(3)),
+        fedavg_clients_case(ref, "fedavg_mix_f32_i64_i32_k4", rng,
+                            [_spec(F32), _spec(I64), _spec(I32), _spec(F32)], nk(4)),
+        fedavg_clients_case(ref, "fedavg_mix_i32_i64_k3", rng, [_spec(I32), _spec(I64), _spec(I32)], nk(3)),
+        fedavg_clients_case(ref, "fedavg_mix_f16_f32_k4", rng, [_spec(F16), _spec(F32), _spec(F16), _spec(F32)], nk(4)),
+        fedavg_clients_case(ref, "fedavg_mix_f32_f16_k3", rng, [_spec(F32), _spec(F16), _spec(F16)], nk(3)),
+        fedavg_clients_case(ref, "fedavg_mix_pertensor_k5", rng,
+                            [_spec(F32), _spec([F32, F64, F32, F32]), _spec(F32), _spec([F32, F32, F64, I64]),
+                             _spec(F32)], nk(5)),
+        fedavg_clients_case(ref, "fedavg_bcast_k4", rng,
+                            [_spec(F32, [(1,), (3, 5), (1, 6), ()]), _spec(F32, [(7,), (1, 5), (4, 1), (9,)]),
+                             _spec(F32, [(7,), (3, 5), (4, 6), ()]), _spec(F64, [(1,), (3, 1), (4, 6), (9,)])],
+                            nk(4)),
+        fedavg_clients_case(ref, "fedavg_fewer_tensors_k3", rng,          # zip() truncates the model
+                            [_spec(F32), _spec(F32, MIX_SHAPES[:3]), _spec(F32)], nk(3)),
+        fedavg_clients_case(ref, "fedavg_bcast_then_bad_k4", rng,
+                            [_spec(F32, [(5,), (2, 3)]), _spec(F32, [(1,), (2, 3)]),
+                             _spec(F32, [(4,), (2, 3)]), _spec(F32, [(5,), (3,)])], nk(4)),
+    ]
+    fo = [(7,), (3, 5), (2053,)]
+    for opt in ("adam", "yogi", "adagrad"):
+        params = None if opt == "adam" else {"serveropt": opt}
+        cases.append(fedopt_clients_case(
+            ref, f"fedopt_mix_{opt}_3r", rng, _spec(F32, fo),
+            [[_spec(F32, fo), _spec(F64, fo), _spec(F32, fo)],      # one float64 client mid-round
+             [_spec(F64, fo), _spec(F32, fo)],                      # the first client is float64
+             [_spec(F32, fo), _spec([F32, I64, F32], fo), _spec(F32, fo)]], params))
+    cases.append(fedopt_clients_case(ref, "fedopt_layout_change_3r", rng, _spec(F32, fo),
+                                     [[_spec(F32, fo)] * 3, [_spec(F64, fo)] * 2, [_spec(F32, fo)] * 2]))
+    cases.append(fedopt_clients_case(ref, "fedopt_f64_clients_f32_model_2r", rng, _spec(F32, fo),
+                                     [[_spec(F64, fo)] * 3, [_spec(F64, fo)] * 2], {"serveropt": "yogi"}))
+    cases.append(fedopt_clients_case(ref, "fedopt_bcast_2r", rng, _spec(F32, [(7,), (3, 5)]),
+                                     [[_spec(F32, [(7,), (3, 5)]), _spec(F32, [(1,), (1, 5)]),
+                                       _spec(F32, [(7,), (3, 1)])],
+                                      [_spec(F32, [(1,), (3, 5)]), _spec(F32, [(7,), (3, 5)])]]))
+    rng = np.random.default_rng(8)
+    cases.append(reduce_dtypes_case(ref, "reduce_mix_f32_f64_f32", rng, ODD_SHAPES, [F32, F64, F32]))
+    cases.append(reduce_dtypes_case(ref, "reduce_mix_f64_f32", rng, ODD_SHAPES, [F64, F32, F32]))
+    return cases
+
+
 def _example_server_functions(ref, filename):
     """The REAL example class, instantiated the way the hooks server does it (hooks.py:187-205:
     compile the user file, exec it, exec ``ServerFunctions()``). Its first line imports
@@ -441,6 +593,8 @@ def main():
         return _write(sf_cases(ref), merge=True)
     if only == "helpers":
         return _write(helper_cases(ref), merge=True)
+    if only == "mixed":
+        return _write(mixed_cases(ref), merge=True)
     cases = []
     cases.append(helper_kat(ref))
     rng = np.random.default_rng(1)
@@ -492,6 +646,7 @@ def main():
 
     cases += sf_cases(ref)
     cases += helper_cases(ref)
+    cases += mixed_cases(ref)
     _write(cases, merge=False)
 
 
