@@ -2,28 +2,40 @@
 
 One "step" = one complete FedAvg aggregation of K client updates (default 64 x 100 M
 fp32, all resident in HBM) into a fresh aggregate: fedavg.py's fold loop
-``x <- x + (n_k*(y_k - x))/N_k`` over k = 1..K-1 in queue order, as ONE libfedagg
-launch. value = aggregated client-params/s = n_gpus * K * P / t_step.
+``x <- x + (n_k*(y_k - x))/N_k`` over k = 1..K-1 in queue order.
+value = aggregated client-params/s = K * P / t_step for the WHOLE job.
 
-Multi-GPU (torchrun, one process per GPU): every rank aggregates its own parameter
-slice of P params (the global model is n_gpus * P params sharded by contiguous slice);
-no collective is on the data path ("scaling": "weak"). The RCCL all-gather that would
-reassemble the model on every GPU is timed separately and reported beside the line
-(``allgather``), not folded into ``value``; so is the fold with that all-gather chunked
-and overlapped (``fold_allgather``: block-cyclic shards, round i gathered on a
-communication stream while round i+1 folds; sharded.CyclicShardedFedAvg), and the copy of
-every rank's slice to host memory, FEDn's actual consumer (``gather_to_host``).
+N = 1 (BASELINE configs[1] / the north-star line): one libfedagg launch per step.
+
+N > 1 (BASELINE configs[2]: the same 100 M-param model, param-sharded across N GPUs with an
+RCCL all-gather): one process per GPU; the flat model is dealt block-cyclically over the
+ranks in R rounds (sharded.CyclicShardedFedAvg); each rank folds its chunk of round i and an
+RCCL ``all_gather_into_tensor`` of round i (on a communication stream) runs while round i+1
+folds, so every GPU ends the step holding the whole aggregated model. The all-gather is
+INSIDE the timed step; total work is fixed as N grows ("scaling": "strong").
+Beside the line at N > 1: ``weak_scaling`` (every rank folds its own 100 M slice, no
+collective), ``allgather`` (a plain all-gather of the model), ``gather_to_host`` (each rank
+D2H's its slice, FEDn's real consumer, roundhandler.py:465-468) and ``in_process`` (one
+process driving all N GPUs, as a FEDn combiner with FEDN_AMD_DEVICES does: each device folds
+its slice and copies it into one pinned host model).
 
 Also measured in the same run:
-  roofline      algorithmic bytes (K*P*4 + P*4 per launch) / average kernel time (HIP events
-                on the launch stream) vs the 8.0 TB/s HBM3E peak; ``traffic`` = HBM bytes per
-                launch from rocprofv3 PMC counters (profiles/pmc_*.json, collected by
-                tools/pmc_traffic.py), or null if not collected for this workload
+  roofline      algorithmic bytes of the fold (K*P*4 + P*4 per launch at N = 1; per rank and
+                step at N > 1) / its kernel time (HIP events on the launch stream) vs the
+                8.0 TB/s HBM3E peak; ``traffic`` = HBM bytes per launch from rocprofv3 PMC
+                counters (profiles/pmc_traffic.json, collected by tools/pmc_collect.sh) when
+                that entry was measured on the current kernel source (sha256 of fedagg.hip),
+                else null with the reason
   cpu_baseline  the numpy restatement of numpyhelper.increment_average (oracle/, bit-equal to
                 FEDn) on a bounded sample (K clients x S params) on one host core; its result is
-                also compared bit-for-bit with the GPU aggregate of the same elements.
+                also compared bit-for-bit with the GPU aggregate of the same elements
+  fedopt        (N = 1) BASELINE configs[3]: FedAdam over 32 device-resident 350 M fp32 updates,
+                one fused pseudo-gradient + server-step launch; round 1 and steady state (fp64
+                old / m / v, the dtype flow fedopt.py produces), each with its own roofline and
+                a bit-exact check of a sample against the oracle
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -38,6 +50,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "aggregated params/sec (device-resident) — FedAvg 64-client reduce, 100M fp32"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+KERNEL_SRC = os.path.join(ROOT, "fedn_amd", "csrc", "fedagg.hip")
 
 
 def parse():
@@ -46,12 +59,14 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--clients", type=int, default=64)
-    ap.add_argument("--params", type=int, default=100_000_000, help="params per GPU")
+    ap.add_argument("--params", type=int, default=100_000_000, help="params of the (global) model")
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32")
     ap.add_argument("--cpu-sample", type=int, default=100_000_000,
                     help="params per client in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--no-allgather", action="store_true")
-    ap.add_argument("--ag-rounds", type=int, default=4, help="rounds of the overlapped fold + all-gather")
+    ap.add_argument("--ag-rounds", type=int, default=4, help="N > 1: rounds of the overlapped fold + all-gather")
+    ap.add_argument("--fedopt-params", type=int, default=350_000_000, help="configs[3] side field (0 = skip)")
+    ap.add_argument("--fedopt-clients", type=int, default=32)
+    ap.add_argument("--no-side", action="store_true", help="N > 1: skip the beside-the-line measurements")
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args()
 
@@ -69,15 +84,28 @@ def make_updates(K, P, dtype, device, seed):
     return ups
 
 
+def kernel_sha():
+    with open(KERNEL_SRC, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def pmc_traffic(workload):
-    """HBM bytes per launch measured by rocprofv3 PMC (tools/pmc_traffic.py), or None."""
+    """(HBM bytes per launch, provenance) from rocprofv3 PMC runs (tools/pmc_collect.sh) — only if
+    that entry was collected on the current kernel source; else (None, reason)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             ent = json.load(f).get(workload)
     except (OSError, ValueError):
-        return None
-    return None if ent is None else ent["bytes"]
+        return None, {"note": "profiles/pmc_traffic.json unreadable"}
+    if ent is None:
+        return None, {"note": f"no PMC entry for workload {workload}"}
+    src = {"file": "profiles/pmc_traffic.json", "workload": workload, "kernel_src_sha": ent.get("kernel_src_sha"),
+           "collected": ent.get("collected"), "read_bytes": ent.get("read_bytes"), "write_bytes": ent.get("write_bytes")}
+    if ent.get("kernel_src_sha") != kernel_sha():
+        src["note"] = "stale: collected on another revision of fedagg.hip; re-run tools/pmc_collect.sh"
+        return None, src
+    return ent["bytes"], src
 
 
 def cpu_baseline(ups, ns, agg, S):
@@ -96,6 +124,107 @@ def cpu_baseline(ups, ns, agg, S):
                       f"numpy {np.__version__} oracle/numpy_ref.fedavg_flat, single-threaded, "
                       f"{os.cpu_count()} host cores present", "seconds": dt,
             "gpu_bit_exact_on_sample": exact}
+
+
+def timed_steps(step, steps, stream, world, device, on_cpu):
+    """Barrier + sync, ``steps`` calls of ``step`` bracketed by HIP events on ``stream``, sync +
+    barrier; returns (wall seconds, mean event ms), each the max over ranks."""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        step()
+        e.record(stream)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ev_ms = sum(s.elapsed_time(e) for s, e in ev) / steps
+    t = torch.tensor([elapsed, ev_ms], dtype=torch.float64, device="cpu" if on_cpu else device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0]), float(t[1])
+
+
+def side(fn):
+    """A beside-the-line measurement: an error is reported in its field, never instead of value."""
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
+def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000):
+    """BASELINE configs[3]: FedAdam, K device-resident fp32 updates of P params, state in HBM;
+    one fused fa_fedopt_step launch per round. Round 1 (old fp32, m / v None) and steady state
+    (old / m / v fp64). Algorithmic bytes: K*P*4 + P*4 + P*(4+8+8) and P*(4K+48)."""
+    from fedn_amd import ops
+    from oracle import numpy_ref as ref  # the checker of the sample only
+
+    g = torch.Generator(device=device).manual_seed(4)
+    old32 = torch.randn(P, generator=g, device=device)
+    ups = [torch.randn(P, generator=g, device=device).mul_(0.01).add_(old32) for _ in range(K)]
+    ns = [int(v) for v in np.random.default_rng(4).integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
+    out = torch.empty(P, dtype=torch.float64, device=device)
+    v = torch.empty(P, dtype=torch.float64, device=device)
+    m32 = torch.empty(P, dtype=torch.float32, device=device)
+    stream = torch.cuda.current_stream(device)
+    params = {"serveropt": "adam", "learning_rate": 1e-3, "beta1": 0.9, "beta2": 0.99, "tau": 1e-4}
+    kw = {k: params[k] for k in ("learning_rate", "beta1", "beta2", "tau")}
+
+    def r1():
+        ops.fedopt_step(old32, ups, ns, Ns, first=True, final=True, m_out=m32, v_out=v, out=out, serveropt="adam",
+                        stream=stream, **kw)
+
+    res = {}
+    for _ in range(warm):
+        r1()
+    _, ms1 = timed_steps(r1, steps, stream, 1, device, False)
+    # checker: round 1 on a sample, then the steady-state inputs of the sample
+    S = min(sample, P)
+    old_s = old32[:S].cpu().numpy()
+    ups_s = [([u[:S].cpu().numpy()], n) for u, n in zip(ups, ns)]
+    st = ref.FedOptState()
+    want1, _ = ref.fedopt_combine(st, ups_s, [old_s], params)
+    ok1 = bool(np.array_equal(out[:S].cpu().numpy().view(np.uint64), want1[0].view(np.uint64)) and
+               np.array_equal(m32[:S].cpu().numpy().view(np.uint32), st.m[0].view(np.uint32)) and
+               np.array_equal(v[:S].cpu().numpy().view(np.uint64), st.v[0].view(np.uint64)))
+    old64, m64, v64 = out.clone(), m32.double(), v.clone()
+    m_out = torch.empty(P, dtype=torch.float64, device=device)
+    v_out = torch.empty(P, dtype=torch.float64, device=device)
+    out2 = torch.empty(P, dtype=torch.float64, device=device)
+
+    def r2():
+        ops.fedopt_step(old64, ups, ns, Ns, first=True, final=True, m_in=m64, m_out=m_out, v_in=v64, v_out=v_out,
+                        out=out2, serveropt="adam", stream=stream, **kw)
+
+    for _ in range(warm):
+        r2()
+    _, ms2 = timed_steps(r2, steps, stream, 1, device, False)
+    st.m = [st.m[0].astype(np.float64)]           # the GPU's steady state takes m in float64 (round >= 3)
+    want2, _ = ref.fedopt_combine(st, ups_s, want1, params)
+    ok2 = bool(np.array_equal(out2[:S].cpu().numpy().view(np.uint64), want2[0].view(np.uint64)) and
+               np.array_equal(m_out[:S].cpu().numpy().view(np.uint64), st.m[0].view(np.uint64)) and
+               np.array_equal(v_out[:S].cpu().numpy().view(np.uint64), st.v[0].view(np.uint64)))
+    for phase, ms, b, ok in (("round1", ms1, K * P * 4 + P * 4 + P * 20, ok1), ("steady", ms2, P * (4 * K + 48), ok2)):
+        wl = f"fedopt_adam_{phase}_k{K}_p{P}"
+        traffic, tsrc = pmc_traffic(wl)
+        gbs = b / ms / 1e6
+        res[phase] = {"ms": ms, "params_per_s": K * P / (ms / 1e3),
+                      "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+                                   "kernel": "k_fedopt (pseudo-gradient fold + Adam step fused)",
+                                   "alg_bytes_per_launch": b},
+                      "bit_exact_on_sample": ok, "sample": f"first {S} params of every buffer vs oracle/numpy_ref"}
+    res["config"] = (f"BASELINE configs[3]: FedAdam, {K} device-resident fp32 updates x {P} params, m / v in HBM "
+                     "(fedopt.py:151-185), one fused launch per round")
+    del ups, old32, out, v, m32, old64, m64, v64, m_out, v_out, out2
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():
@@ -122,155 +251,200 @@ def main():
     _abi.load()
 
     K = a.clients
-    sh = ShardedFedAvg(a.params * world)          # global model = world x params, one slice per rank
-    P = sh.hi - sh.lo                             # this rank's slice (4 KiB-aligned bounds)
-    P_total = a.params * world
-    cyc = None
-    if world > 1 and not a.no_allgather:
-        cyc = CyclicShardedFedAvg(P_total, chunk=-(-P_total // (world * a.ag_rounds)))
-    L = max(P, cyc.local_len) if cyc else P
-    ups_full = make_updates(K, L, a.dtype, device, a.seed + 1000 * rank)
-    ups = [u[:P] for u in ups_full]
+    P_total = a.params
+    in_bytes = 2 if a.dtype == "bf16" else 4
     ns = [int(v) for v in np.random.default_rng(a.seed).integers(1, 5001, K)]
     Ns = [int(v) for v in np.cumsum(ns)]
-    agg = torch.empty(P, dtype=torch.float32, device=device)
     stream = torch.cuda.current_stream(device)
+    extra = {}
 
-    def step():
-        ops.fedavg_fold(agg, ups, ns, Ns, init=True, stream=stream)
+    if world == 1:
+        P = P_total
+        ups = make_updates(K, P, a.dtype, device, a.seed)
+        agg = torch.empty(P, dtype=torch.float32, device=device)
 
-    for _ in range(a.warmup):
-        step()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
-        step()
-        e.record(stream)
-    torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(s.elapsed_time(e) for s, e in ev) / a.steps
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cpu" if rehearsal else device)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
+        def step():
+            ops.fedavg_fold(agg, ups, ns, Ns, init=True, stream=stream)
 
-    in_bytes = 2 if a.dtype == "bf16" else 4
-    alg_bytes = K * P * in_bytes + P * 4           # read every update once, write the aggregate once
+        for _ in range(a.warmup):
+            step()
+        elapsed, kern_ms = timed_steps(step, a.steps, stream, world, device, rehearsal)
+        alg_bytes = K * P * in_bytes + P * 4           # read every update once, write the aggregate once
+        workload = f"fedavg_k{K}_p{P}_{a.dtype}"
+        kernel = "k_fedavg_pipe (fp32, 4 x 16-B strips per lane, next client prefetched)"
+        config = {"workload": f"FedAvg {K} clients x {P} params {a.dtype} per GPU (BASELINE configs[1]/north "
+                              "star; device-resident, one fused fold launch per aggregation)",
+                  "clients": K, "params_per_gpu": P, "global_params": P_total,
+                  "parallelism": "param-slice shards x1, no data-path collective"}
+        scaling = "weak"
+    else:
+        cyc = CyclicShardedFedAvg(P_total, chunk=-(-P_total // (world * a.ag_rounds)))
+        L = cyc.local_len
+        P = L
+        ups_local = make_updates(K, L, a.dtype, device, a.seed + 1000 * rank)   # this rank's chunks, every client
+        agg = torch.empty(L, dtype=torch.float32, device=device)
+        full = None if rehearsal else torch.empty(cyc.full_len, dtype=torch.float32, device=device)
+
+        def step():
+            cyc.fold_allgather(agg, ups_local, ns, Ns, init=True, out=full)
+
+        def fold_only():
+            for i in range(cyc.rounds):
+                sl = slice(i * cyc.C, (i + 1) * cyc.C)
+                ops.fedavg_fold(agg[sl], [u[sl] for u in ups_local], ns, Ns, init=True, stream=stream)
+
+        for _ in range(a.warmup):
+            step()
+        elapsed, _ = timed_steps(step, a.steps, stream, world, device, rehearsal)
+        for _ in range(2):
+            fold_only()
+        _, kern_ms = timed_steps(fold_only, a.steps, stream, world, device, rehearsal)
+        alg_bytes = K * L * in_bytes + L * 4              # this rank's fold, per step (all rounds)
+        workload = f"fedavg_k{K}_p{L}_{a.dtype}_rank_of_{world}"
+        kernel = (f"k_fedavg_pipe over this rank's {cyc.rounds} chunks of {cyc.C} params (fold-only timing; "
+                  "max over ranks)")
+        config = {"workload": f"FedAvg {K} clients x {P_total} params {a.dtype}, param-sharded block-cyclically over "
+                              f"{world} GPUs; RCCL all-gather of each folded round overlapped with the next round's "
+                              "fold, inside the timed step (BASELINE configs[2])",
+                  "clients": K, "params_per_gpu": L, "global_params": P_total, "rounds": cyc.rounds,
+                  "chunk": cyc.C, "parallelism": f"param-slice x{world} + RCCL all-gather"}
+        scaling = "strong"
+        extra["fold_allgather_ms"] = elapsed / a.steps * 1e3
+        if not a.no_side:
+            extra.update(multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, ups_local, stream))
+        ups = ups_local
+
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-    workload = f"fedavg_k{K}_p{P}_{a.dtype}"
-
-    def measure_allgather():
-        gather_src = agg.cpu() if rehearsal else agg
-        for _ in range(2):
-            full = sh.allgather(gather_src)
-        del full
-        torch.cuda.synchronize(device)
-        dist.barrier()
-        t1 = time.perf_counter()
-        reps = 5
-        for _ in range(reps):
-            full = sh.allgather(gather_src)
-            del full
-        torch.cuda.synchronize(device)
-        ag = torch.tensor([(time.perf_counter() - t1) / reps], dtype=torch.float64,
-                          device="cpu" if rehearsal else device)
-        dist.all_reduce(ag, op=dist.ReduceOp.MAX)
-        ag_s = float(ag[0])
-        nbytes = sh.shard * world * 4
-        return {"ms": ag_s * 1e3, "bytes_in_per_rank": sh.shard * (world - 1) * 4,
-                "algbw_GBps": nbytes / ag_s / 1e9, "busbw_GBps": nbytes * (world - 1) / world / ag_s / 1e9,
-                "backend": "gloo (rehearsal)" if rehearsal else "rccl",
-                "note": "reassembles the world*params model on every GPU; not in value"}
-
-    def measure_fold_allgather():
-        agg_c = torch.empty(cyc.local_len, dtype=torch.float32, device=device)
-        ups_c = [u[:cyc.local_len] for u in ups_full]
-        out_c = None if rehearsal else torch.empty(cyc.full_len, dtype=torch.float32, device=device)
-        for _ in range(2):
-            cyc.fold_allgather(agg_c, ups_c, ns, Ns, init=True, out=out_c)
-        torch.cuda.synchronize(device)
-        dist.barrier()
-        t1 = time.perf_counter()
-        reps = 5
-        for _ in range(reps):
-            cyc.fold_allgather(agg_c, ups_c, ns, Ns, init=True, out=out_c)
-        torch.cuda.synchronize(device)
-        fa = torch.tensor([(time.perf_counter() - t1) / reps], dtype=torch.float64,
-                          device="cpu" if rehearsal else device)
-        dist.all_reduce(fa, op=dist.ReduceOp.MAX)
-        fa_s = float(fa[0])
-        return {"ms": fa_s * 1e3, "value": K * P_total / fa_s, "unit": "params/s", "rounds": cyc.rounds,
-                "chunk": cyc.C, "backend": "gloo (rehearsal)" if rehearsal else "rccl",
-                "note": "fold + all-gather of each folded round overlapped on a second stream "
-                        "(block-cyclic shards); the world*params model on every GPU; not in value"}
-
-    def side(fn):
-        """A beside-the-line measurement: an error is reported in its field, never instead of value."""
-        try:
-            return fn()
-        except Exception as e:  # noqa: BLE001
-            return {"error": f"{type(e).__name__}: {e}"}
-
-    allgather = side(measure_allgather) if world > 1 and not a.no_allgather else None
-    fold_ag = side(measure_fold_allgather) if cyc is not None else None
-
-    # the model to the host, FEDn's consumer (roundhandler.py:465-468): every rank D2H's its own
-    # slice over its own PCIe link into pinned memory, concurrently (SURVEY.md §5 alternative to
-    # the all-gather); value excludes it
-    host = torch.empty(P, dtype=torch.float32, pin_memory=True)
-    for _ in range(2):
-        host.copy_(agg, non_blocking=True)
-    torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    reps = 5
-    for _ in range(reps):
-        host.copy_(agg, non_blocking=True)
-    torch.cuda.synchronize(device)
-    gh = torch.tensor([(time.perf_counter() - t1) / reps], dtype=torch.float64, device="cpu" if rehearsal else device)
-    if world > 1:
-        dist.all_reduce(gh, op=dist.ReduceOp.MAX)
-    gh_s = float(gh[0])
-    gather_host = {"ms": gh_s * 1e3, "bytes_per_rank": P * 4, "GBps_aggregate": world * P * 4 / gh_s / 1e9,
-                   "note": "each rank D2H's its slice of the aggregate into pinned host memory, all ranks "
-                           "concurrently over their own links; max over ranks; not in value"}
-    del host
-
+    traffic, tsrc = pmc_traffic(workload)
     base = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
         base = cpu_baseline(ups, ns, agg, a.cpu_sample)
+    if world == 1:
+        # the model to the host, FEDn's consumer (roundhandler.py:465-468); value excludes it
+        host = torch.empty(P, dtype=torch.float32, pin_memory=True)
+        for _ in range(2):
+            host.copy_(agg, non_blocking=True)
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        for _ in range(5):
+            host.copy_(agg, non_blocking=True)
+        torch.cuda.synchronize(device)
+        gh = (time.perf_counter() - t1) / 5
+        extra["gather_to_host"] = {"ms": gh * 1e3, "bytes_per_rank": P * 4, "GBps_aggregate": P * 4 / gh / 1e9,
+                                   "note": "D2H of the aggregate into pinned host memory; not in value"}
+        del host
+        del ups, agg
+        torch.cuda.empty_cache()
+        if rank == 0 and a.fedopt_params > 0:
+            extra["fedopt"] = side(lambda: fedopt_side(a.fedopt_params, a.fedopt_clients, device))
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": K * P_total / (elapsed / a.steps), "unit": "params/s",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": a.dtype,
             "data": "synthetic: base~N(0,1), client=base+0.01*N(0,1), num_examples~U{1..5000}, device-resident",
-            "config": {"workload": f"FedAvg {K} clients x {a.params} params {a.dtype} per GPU (BASELINE configs[1]/north "
-                                   "star; device-resident, one fused fold launch per aggregation)",
-                       "clients": K, "params_per_gpu": a.params, "global_params": P_total,
-                       "parallelism": f"param-slice shards x{world}, no data-path collective"},
+            "config": config,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(workload),
-                         "kernel": "k_fedavg_pipe (fp32, 4 x 16-B strips per lane, next client prefetched)", "kernel_ms": kern_ms,
-                         "alg_bytes_per_launch": alg_bytes},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+                         "kernel": kernel, "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": base,
         }
-        line["gather_to_host"] = gather_host
-        if allgather:
-            line["allgather"] = allgather
-        if fold_ag:
-            line["fold_allgather"] = fold_ag
+        line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, ups_local, stream):
+    """The N > 1 measurements beside the line (none of them is in value)."""
+    from fedn_amd import ops
+    from fedn_amd.sharded import ShardedFedAvg
+    out = {}
+    on_cpu = rehearsal
+
+    def plain_allgather():
+        sh = ShardedFedAvg(P_total)
+        src = torch.zeros(sh.hi - sh.lo, dtype=torch.float32, device=device)
+        gsrc = src.cpu() if rehearsal else src
+        for _ in range(2):
+            sh.allgather(gsrc)
+        el, _ = timed_steps(lambda: sh.allgather(gsrc), 5, stream, world, device, on_cpu)
+        nbytes = sh.shard * world * 4
+        ag_s = el / 5
+        return {"ms": ag_s * 1e3, "bytes_in_per_rank": sh.shard * (world - 1) * 4,
+                "algbw_GBps": nbytes / ag_s / 1e9, "busbw_GBps": nbytes * (world - 1) / world / ag_s / 1e9,
+                "backend": "gloo (rehearsal)" if rehearsal else "rccl",
+                "note": f"all-gather of the {P_total}-param fp32 model (one slice per rank), not overlapped; not in value"}
+
+    def gather_to_host():
+        host = torch.empty(agg.numel(), dtype=torch.float32, pin_memory=True)
+        host.copy_(agg, non_blocking=True)
+        el, _ = timed_steps(lambda: host.copy_(agg, non_blocking=True), 5, stream, world, device, on_cpu)
+        gh = el / 5
+        return {"ms": gh * 1e3, "bytes_per_rank": agg.numel() * 4, "GBps_aggregate": world * agg.numel() * 4 / gh / 1e9,
+                "note": "each rank D2H's its slice of the aggregate into pinned host memory, all ranks "
+                        "concurrently over their own links; max over ranks; not in value"}
+
+    def weak():
+        P = P_total
+        ups = make_updates(K, P, a.dtype, device, a.seed + 7 + 1000 * rank)
+        agg_w = torch.empty(P, dtype=torch.float32, device=device)
+        step = lambda: ops.fedavg_fold(agg_w, ups, ns, Ns, init=True, stream=stream)  # noqa: E731
+        for _ in range(2):
+            step()
+        el, kms = timed_steps(step, a.steps, stream, world, device, on_cpu)
+        del ups, agg_w
+        torch.cuda.empty_cache()
+        return {"value": K * P * world / (el / a.steps), "ms_per_step": el / a.steps * 1e3, "kernel_ms": kms,
+                "params_per_gpu": P, "global_params": P * world,
+                "note": f"every rank folds its own {P}-param slice of a world x {P} model; no collective; not in value"}
+
+    def in_process():
+        """One process (rank 0) drives all N GPUs: each folds its slice of the 64 updates and copies it
+        into one pinned host model (the multidev.py layout FEDN_AMD_DEVICES selects)."""
+        from fedn_amd.sharded import shard_bounds
+        res = None
+        if True:
+            devs = [torch.device("cuda", 0 if rehearsal else d) for d in range(world)]
+            bounds = shard_bounds(P_total, world)
+            data = []
+            for d, dv in enumerate(devs):
+                lo, hi = bounds[d]
+                with torch.cuda.device(dv):
+                    u = make_updates(K, hi - lo, a.dtype, dv, a.seed + 31 + d)
+                    data.append((u, torch.empty(hi - lo, dtype=torch.float32, device=dv)))
+            host = torch.empty(P_total, dtype=torch.float32, pin_memory=True)
+
+            def run():
+                for d, dv in enumerate(devs):
+                    lo, hi = bounds[d]
+                    u, ag = data[d]
+                    with torch.cuda.device(dv):
+                        ops.fedavg_fold(ag, u, ns, Ns, init=True, stream=torch.cuda.current_stream(dv))
+                        host[lo:hi].copy_(ag, non_blocking=True)
+                for dv in devs:
+                    torch.cuda.synchronize(dv)
+            run()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                run()
+            t = (time.perf_counter() - t0) / 5
+            res = {"ms": t * 1e3, "value": K * P_total / t, "devices": len(devs),
+                   "note": "one process, all GPUs: each folds its slice of the 64 device-resident updates and "
+                           "D2H's it into one pinned host model (fold + PCIe copy, no collective); not in value"}
+            del data, host
+            torch.cuda.empty_cache()
+        return res
+
+    out["allgather"] = side(plain_allgather)
+    out["gather_to_host"] = side(gather_to_host)
+    out["weak_scaling"] = side(weak)
+    ip = side(in_process) if rank == 0 else None     # the other ranks wait (their GPUs are in use)
+    dist.barrier()
+    if rank == 0:
+        out["in_process"] = ip
+    return out
 
 
 if __name__ == "__main__":

@@ -54,14 +54,17 @@ EXPORTS = {
         ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,      # g, dtype, m
         ctypes.c_double, ctypes.c_double, ctypes.c_double,   # a, b, T
         ctypes.c_int64, ctypes.c_void_p]),                   # P, stream
-    "fa_tune": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
-    "fa_stream_sum": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int64,
-                                     ctypes.c_void_p]),
     "fa_elementwise": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int64,
                                       ctypes.c_void_p]),
     "fa_cast": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
+}
+# measurement / tuning entry points: libfedagg_probe.so only (include/fedagg_probe.h)
+PROBE_EXPORTS = {
+    "fa_tune": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "fa_stream_sum": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int64,
+                                     ctypes.c_void_p]),
     "fa_stream_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "fa_stream_read_blocks": (ctypes.c_int64, [ctypes.c_int64]),
     "fa_stream_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
@@ -84,43 +87,77 @@ class FedAggError(RuntimeError):
 
 _lock = threading.Lock()
 _lib = None
+_probe = None
+_active = None          # the probe library, while a tool or test measures with it (use_probe)
+PROBE_PATH = os.path.join(_HERE, "libfedagg_probe.so")
 
 
 def lib_path():
     return os.environ.get("FEDN_AMD_LIB", LIB_PATH)
 
 
+def _open(path, exports):
+    import torch  # noqa: F401  (binds the library to torch's HIP runtime)
+
+    if not os.path.exists(path):
+        raise FedAggLibraryError(
+            f"{path} not found: build it first (python -c 'import __graft_entry__ as g; g.build()' "
+            "or python -m fedn_amd.build). The HIP library is required; there is no CPU fallback.")
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as e:
+        raise FedAggLibraryError(f"cannot load {path}: {e}") from e
+    for name, (res, args) in exports.items():
+        try:
+            fn = getattr(lib, name)
+        except AttributeError as e:
+            raise FedAggLibraryError(f"{path} does not export {name}") from e
+        fn.restype = res
+        fn.argtypes = args
+    ver = lib.fa_abi_version()
+    if ver != ABI_VERSION:
+        raise FedAggLibraryError(f"{path}: ABI version {ver}, expected {ABI_VERSION}; rebuild it")
+    return lib
+
+
 def load():
-    """Open libfedagg.so once (thread-safe) and attach the C signatures."""
+    """The library entry points run in: libfedagg.so (opened once, thread-safe), or the probe
+    library while ``use_probe`` is in effect."""
     global _lib
+    if _active is not None:
+        return _active
     if _lib is not None:
         return _lib
     with _lock:
-        if _lib is not None:
-            return _lib
-        import torch  # noqa: F401  (binds the library to torch's HIP runtime)
+        if _lib is None:
+            _lib = _open(lib_path(), EXPORTS)
+        return _lib
 
-        path = lib_path()
-        if not os.path.exists(path):
-            raise FedAggLibraryError(
-                f"{path} not found: build it first (python -c 'import __graft_entry__ as g; g.build()' "
-                "or python -m fedn_amd.build). The HIP library is required; there is no CPU fallback.")
-        try:
-            lib = ctypes.CDLL(path)
-        except OSError as e:
-            raise FedAggLibraryError(f"cannot load {path}: {e}") from e
-        for name, (res, args) in EXPORTS.items():
-            try:
-                fn = getattr(lib, name)
-            except AttributeError as e:
-                raise FedAggLibraryError(f"{path} does not export {name}") from e
-            fn.restype = res
-            fn.argtypes = args
-        ver = lib.fa_abi_version()
-        if ver != ABI_VERSION:
-            raise FedAggLibraryError(f"{path}: ABI version {ver}, expected {ABI_VERSION}; rebuild it")
-        _lib = lib
-        return lib
+
+def load_probe():
+    """libfedagg_probe.so: the same kernels plus fa_tune and the probe kernels (measurement only)."""
+    global _probe
+    with _lock:
+        if _probe is None:
+            _probe = _open(PROBE_PATH, {**EXPORTS, **PROBE_EXPORTS})
+        return _probe
+
+
+class use_probe:
+    """Route every ops.* call of this process to the probe library (tools/, A/B tests):
+    ``_abi.use_probe()`` for the rest of the process, or ``with _abi.use_probe(): ...``."""
+
+    def __init__(self):
+        global _active
+        self._prev = _active
+        _active = load_probe()
+
+    def __enter__(self):
+        return _active
+
+    def __exit__(self, *exc):
+        global _active
+        _active = self._prev
 
 
 def check(status):

@@ -9,6 +9,8 @@ ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "fedagg.hip")
 HDR = os.path.join(ROOT, "include", "fedagg.h")
 OUT = os.path.join(HERE, "libfedagg.so")
+PROBE_HDR = os.path.join(ROOT, "include", "fedagg_probe.h")
+PROBE_OUT = os.path.join(HERE, "libfedagg_probe.so")   # + measurement knobs / probe kernels (tools/)
 ARCH = os.environ.get("FEDN_AMD_ARCH", "gfx950")
 
 # -ffp-contract=off: numpy never fuses a*b+c, so neither may we (bit-exact parity).
@@ -48,22 +50,29 @@ def build_codec(force=False, verbose=True):
 
 
 def build(force=False, verbose=True):
-    build_codec(force, verbose)
-    return build_hip(force, verbose)
+    """Product library, probe library and codec; the two hipcc builds run concurrently."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(3) as ex:
+        futs = [ex.submit(build_codec, force, verbose), ex.submit(build_hip, force, verbose),
+                ex.submit(build_hip, force, verbose, True)]
+        for f in futs:
+            f.result()
+    return OUT
 
 
-def build_hip(force=False, verbose=True):
-    if not force and os.path.exists(OUT):
-        t = os.path.getmtime(OUT)
-        if t >= os.path.getmtime(SRC) and t >= os.path.getmtime(HDR):
-            return OUT
-    tmp = OUT + ".tmp"
-    cmd = [hipcc()] + FLAGS + ["-I", os.path.join(ROOT, "include"), "-o", tmp, SRC]
+def build_hip(force=False, verbose=True, probe=False):
+    out = PROBE_OUT if probe else OUT
+    deps = (SRC, HDR, PROBE_HDR)
+    if not force and not _stale(out, *deps):
+        return out
+    tmp = out + ".tmp"
+    cmd = [hipcc()] + FLAGS + (["-DFEDAGG_PROBES"] if probe else []) + ["-I", os.path.join(ROOT, "include"),
+                                                                          "-o", tmp, SRC]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

@@ -27,11 +27,15 @@
 #include <cstdint>
 #include <cstdio>
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <type_traits>
 #include <vector>
 
 #include "../../include/fedagg.h"
+#ifdef FEDAGG_PROBES
+#include "../../include/fedagg_probe.h"
+#endif
 
 namespace {
 
@@ -228,14 +232,16 @@ struct CRUN {
     }
 };
 
+template <class CP> struct is_nostore : std::false_type {};
+#ifdef FEDAGG_PROBES
 struct CADD {            // measurement only: x <- x + y (same traversal as the fold, minimal VALU)
     using V = float;
     using S = float;
     __device__ static __forceinline__ V fold(V x, V y, S, S, double) { return x + y; }
 };
 struct CADDNW : CADD {};  // measurement only: CADD whose store is skipped (never-true data test)
-template <class CP> struct is_nostore : std::false_type {};
 template <> struct is_nostore<CADDNW> : std::true_type {};
+#endif
 
 // element-wise client step for policies without a strip-level shortcut
 template <class CP, int E>
@@ -841,8 +847,9 @@ k_cast(TO* __restrict__ out, const TI* __restrict__ in, const CastGeom g, const 
     }
 }
 
+#ifdef FEDAGG_PROBES
 // ----------------------------------------------------------------------------
-// measurement kernels
+// measurement kernels (libfedagg_probe.so only)
 // ----------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) k_stream_copy(u32x4* __restrict__ dst, const u32x4* __restrict__ src, int64_t n16) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -869,14 +876,31 @@ __global__ void __launch_bounds__(kBlock) k_stream_read(const u32x4* __restrict_
         sink[blockIdx.x] = r;
     }
 }
+#endif  // FEDAGG_PROBES
 
 // ----------------------------------------------------------------------------
 // host side
 // ----------------------------------------------------------------------------
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-int g_fastdiv = 1;
-int g_fastdiv64 = 1;
+// Launch configuration. The product library (libfedagg.so) is built with the measured-best
+// settings as compile-time constants: nothing in it is mutable or process-global. The probe
+// build (-DFEDAGG_PROBES -> libfedagg_probe.so, tools/ and the division tests only) adds the
+// fa_tune knobs that produced those measurements (profiles/r01_microbench.md).
+#ifdef FEDAGG_PROBES
+struct FedAvgCfg {
+    std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1};
+};
+FedAvgCfg g_cfg;
+int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
+int cfg_fastdiv64() { return g_cfg.fastdiv64.load(std::memory_order_relaxed); }
+int cfg_grid_per_cu() { return g_cfg.grid_per_cu.load(std::memory_order_relaxed); }
+#else
+constexpr int cfg_fastdiv() { return 1; }     // fp32 t/N via the exact RN64(1/N) product
+constexpr int cfg_fastdiv64() { return 1; }   // fp64 t/N via RN64(1/N) + two exact corrections (§3.2b)
+constexpr int cfg_grid_per_cu() { return 0; } // one 16-KiB-per-client tile per workgroup
+#endif
 
 template <typename S>
 void fill_table(ClientTable<S>& t, const void* const* ptrs, const double* n, const double* N, int k0, int cnt) {
@@ -888,12 +912,12 @@ void fill_table(ClientTable<S>& t, const void* const* ptrs, const double* n, con
             // CF64's division shortcut: r = RN64(1/N) for 2^-60 <= |N| <= 2^60 (CWSUM ignores r,
             // CRUN overwrites it)
             const double Nd = N[k0 + j], a = std::fabs(Nd);
-            t.r[j] = (g_fastdiv64 && a >= 0x1p-60 && a <= 0x1p60) ? 1.0 / Nd : 0.0;
+            t.r[j] = (cfg_fastdiv64() && a >= 0x1p-60 && a <= 0x1p60) ? 1.0 / Nd : 0.0;
         } else {
             // reciprocal for CF32's division shortcut: only for N that keep every normal-range
             // quotient normal (|N| < 2^28) and only when enabled
             const float Nf = (float)N[k0 + j];
-            t.r[j] = (g_fastdiv && Nf != 0.0f && std::fabs(Nf) < 0x1p28f) ? 1.0 / (double)Nf : 0.0;
+            t.r[j] = (cfg_fastdiv() && Nf != 0.0f && std::fabs(Nf) < 0x1p28f) ? 1.0 / (double)Nf : 0.0;
         }
     }
     for (int j = cnt; j < kMaxK; ++j) {
@@ -915,22 +939,6 @@ int64_t grid_for(int64_t P, int E) {
     return (strips + kBlock - 1) / kBlock;
 }
 
-// FedAvg launch geometry (fa_tune): strips per lane, clients in flight, non-temporal loads.
-struct FedAvgCfg {
-    int strips = 4;   // measured best on MI355X (profiles/r01_microbench.md): 4 strips per lane,
-    int unroll = 0;   // software-pipelined one client ahead
-    int lanetab = 0;
-    int grid_per_cu = 0;      // 0: one tile per block; n: persistent grid of n blocks per CU
-    int read_per_lane = 16;   // fa_stream_read probe only
-    int block_log = 8;        // pipelined kernel workgroup size 2^block_log (8, 9, 10)
-    int sum_nostore = 0;      // fa_stream_sum probe: suppress the store (reads + adds only)
-    int nt_store = 1;         // pipelined kernel (S = 4, 256 threads) and fa_stream_sum: store mode 0 plain, 1 nt, 2 sc1;
-                              // nt: -3 % time at K = 8, neutral at K = 64 (profiles/r01_store_probe.log)
-    int nt = 0;   // measured: cached loads beat non-temporal ones by ~3% (profiles/)
-    int tilemap = 0;          // pipelined kernel (S = 4, nt stores): workgroup -> tile order (run length), see map_tile
-};
-FedAvgCfg g_cfg;
-
 int device_cus() {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -944,9 +952,9 @@ void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, i
                         hipStream_t st) {
     const int64_t strips = (P + E - 1) / E;
     int64_t ntiles = (strips + (int64_t)BLK * S - 1) / ((int64_t)BLK * S);
-    if (g_cfg.grid_per_cu > 0) {
+    if (cfg_grid_per_cu() > 0) {
         if constexpr (MAP != 0) return launch_fedavg_pipe<Y, X, CP, E, S, NT, LT, BLK, NTS, 0>(a, tab, cnt, P, first, int_first, st);
-        ntiles = std::min<int64_t>(ntiles, (int64_t)g_cfg.grid_per_cu * device_cus());
+        ntiles = std::min<int64_t>(ntiles, (int64_t)cfg_grid_per_cu() * device_cus());
     }
     const dim3 grid((unsigned)ntiles);
     if (first && int_first) {
@@ -987,8 +995,11 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
         return;
     }
     if constexpr (tunable) {
-        const int key = (g_cfg.block_log == 9 ? 20000 : g_cfg.block_log == 10 ? 30000 : 0) + g_cfg.lanetab * 10000 +
-                        g_cfg.strips * 100 + g_cfg.unroll * 2 + g_cfg.nt;
+#ifdef FEDAGG_PROBES
+        const int block_log = g_cfg.block_log, strips = g_cfg.strips, unroll = g_cfg.unroll, nt = g_cfg.nt;
+        const int lanetab = g_cfg.lanetab, nt_store = g_cfg.nt_store, tilemap = g_cfg.tilemap;
+        const int key = (block_log == 9 ? 20000 : block_log == 10 ? 30000 : 0) + lanetab * 10000 + strips * 100 +
+                        unroll * 2 + nt;
         switch (key) {
 #define FA_GEOM(S_, U_, NT_) \
     case S_ * 100 + U_ * 2 + NT_: return launch_fedavg_geom<Y, X, CP, E, S_, U_, NT_>(a, tab, cnt, P, first, int_first, st);
@@ -997,8 +1008,8 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
             FA_GEOM(1, 8, 1) FA_GEOM(4, 2, 1) FA_GEOM(8, 1, 1)
             case 2 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 2, false, false>(a, tab, cnt, P, first, int_first, st);
             case 4 * 100 + 0:
-                if (g_cfg.nt_store == 1 && g_cfg.tilemap > 0) {
-                    switch (g_cfg.tilemap) {
+                if (nt_store == 1 && tilemap > 0) {
+                    switch (tilemap) {
 #define FA_MAP(R_) \
     case R_: return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 1, R_>(a, tab, cnt, P, first, int_first, st);
                         FA_MAP(2) FA_MAP(4) FA_MAP(8) FA_MAP(16) FA_MAP(32)
@@ -1006,8 +1017,8 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
                         default: break;
                     }
                 }
-                if (g_cfg.nt_store == 1) return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 1>(a, tab, cnt, P, first, int_first, st);
-                if (g_cfg.nt_store == 2) return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 2>(a, tab, cnt, P, first, int_first, st);
+                if (nt_store == 1) return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 1>(a, tab, cnt, P, first, int_first, st);
+                if (nt_store == 2) return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 2>(a, tab, cnt, P, first, int_first, st);
                 return launch_fedavg_pipe<Y, X, CP, E, 4, false, false>(a, tab, cnt, P, first, int_first, st);
             case 8 * 100 + 0: return launch_fedavg_pipe<Y, X, CP, E, 8, false, false>(a, tab, cnt, P, first, int_first, st);
             case 4 * 100 + 1: return launch_fedavg_pipe<Y, X, CP, E, 4, true, false>(a, tab, cnt, P, first, int_first, st);
@@ -1021,6 +1032,11 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
 #undef FA_GEOM
             default: break;
         }
+#else
+        // measured best on MI355X (profiles/r01_microbench.md): 4 x 16-B strips per lane, the next
+        // client's strips in flight (pipelined), cached loads, non-temporal aggregate stores
+        return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 1>(a, tab, cnt, P, first, int_first, st);
+#endif
     }
     launch_fedavg_geom<Y, X, CP, E, 1, kUnroll, false>(a, tab, cnt, P, first, int_first, st);
 }
@@ -1245,80 +1261,6 @@ int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, i
     return fail(FA_EDTYPE, "fa_fedopt_step: unsupported dtype pair (update %d, old %d)", upd_dtype, old_dtype);
 }
 
-int fa_tune(int knob, int value) {
-    g_err[0] = 0;
-    switch (knob) {
-        case FA_TUNE_STRIPS:
-            if (value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
-                return fail(FA_EINVAL, "fa_tune: strips must be 1, 2, 4, 8 or 16");
-            g_cfg.strips = value;
-            return FA_OK;
-        case FA_TUNE_UNROLL:
-            if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
-                return fail(FA_EINVAL, "fa_tune: unroll must be 0 (pipelined), 1, 2, 4, 8 or 16");
-            g_cfg.unroll = value;
-            return FA_OK;
-        case FA_TUNE_NT:
-            g_cfg.nt = value ? 1 : 0;
-            return FA_OK;
-        case FA_TUNE_SUM_NOSTORE:
-            g_cfg.sum_nostore = value != 0;
-            return FA_OK;
-        case FA_TUNE_NT_STORE:
-            if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: store mode 0 (plain), 1 (nt) or 2 (sc1)");
-            g_cfg.nt_store = value;
-            return FA_OK;
-        case FA_TUNE_BLOCK:
-            if (value != 256 && value != 512 && value != 1024) return fail(FA_EINVAL, "fa_tune: block 256, 512 or 1024");
-            g_cfg.block_log = value == 256 ? 8 : value == 512 ? 9 : 10;
-            return FA_OK;
-        case FA_TUNE_READ:
-            if (value != 4 && value != 8 && value != 16) return fail(FA_EINVAL, "fa_tune: read probe depth 4, 8 or 16");
-            g_cfg.read_per_lane = value;
-            return FA_OK;
-        case FA_TUNE_GRID:
-            if (value < 0 || value > 64) return fail(FA_EINVAL, "fa_tune: grid blocks per CU must be 0..64");
-            g_cfg.grid_per_cu = value;
-            return FA_OK;
-        case FA_TUNE_TILEMAP:
-            if (value != 0 && value != 2 && value != 4 && value != 8 && value != 16 && value != 32)
-                return fail(FA_EINVAL, "fa_tune: tile map 0 (identity) or runs of 2, 4, 8, 16, 32 tiles per XCD");
-            g_cfg.tilemap = value;
-            return FA_OK;
-        case FA_TUNE_LANETAB:
-            g_cfg.lanetab = value ? 1 : 0;
-            return FA_OK;
-        case FA_TUNE_FASTDIV:
-            g_fastdiv = value ? 1 : 0;
-            return FA_OK;
-        case FA_TUNE_FASTDIV64:
-            g_fastdiv64 = value ? 1 : 0;
-            return FA_OK;
-        default:
-            return fail(FA_EINVAL, "fa_tune: unknown knob %d", knob);
-    }
-}
-
-int fa_stream_sum(float* out, const float* const* bufs, int K, int64_t P, void* stream) {
-    g_err[0] = 0;
-    if (K < 1 || K > kMaxK || P < 0 || !out || !bufs) return fail(FA_EINVAL, "fa_stream_sum: bad arguments");
-    bool vec = aligned16(out);
-    for (int k = 0; k < K; ++k) vec = vec && bufs[k] && aligned16(bufs[k]);
-    if (!vec) return fail(FA_EINVAL, "fa_stream_sum: buffers must be 16-B aligned");
-    ClientTable<float> tab;
-    std::vector<double> ones(K, 1.0);
-    fill_table<float>(tab, reinterpret_cast<const void* const*>(bufs), ones.data(), ones.data(), 0, K);
-    if (g_cfg.sum_nostore)
-        launch_fedavg_pipe<float, float, CADDNW, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
-    else if (g_cfg.nt_store == 1)
-        launch_fedavg_pipe<float, float, CADD, 4, 4, false, false, kBlock, 1>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
-    else if (g_cfg.nt_store == 2)
-        launch_fedavg_pipe<float, float, CADD, 4, 4, false, false, kBlock, 2>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
-    else
-        launch_fedavg_pipe<float, float, CADD, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
-    return check_launch("fa_stream_sum");
-}
-
 int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype, const void* y, int y_dtype,
                    double a, double b, int64_t P, void* stream) {
     g_err[0] = 0;
@@ -1396,6 +1338,81 @@ int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, co
     return fail(FA_EDTYPE, "fa_cast: unsupported conversion %d -> %d", in_dtype, out_dtype);
 }
 
+#ifdef FEDAGG_PROBES
+int fa_tune(int knob, int value) {
+    g_err[0] = 0;
+    switch (knob) {
+        case FA_TUNE_STRIPS:
+            if (value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
+                return fail(FA_EINVAL, "fa_tune: strips must be 1, 2, 4, 8 or 16");
+            g_cfg.strips = value;
+            return FA_OK;
+        case FA_TUNE_UNROLL:
+            if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
+                return fail(FA_EINVAL, "fa_tune: unroll must be 0 (pipelined), 1, 2, 4, 8 or 16");
+            g_cfg.unroll = value;
+            return FA_OK;
+        case FA_TUNE_NT:
+            g_cfg.nt = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_SUM_NOSTORE:
+            g_cfg.sum_nostore = value != 0;
+            return FA_OK;
+        case FA_TUNE_NT_STORE:
+            if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: store mode 0 (plain), 1 (nt) or 2 (sc1)");
+            g_cfg.nt_store = value;
+            return FA_OK;
+        case FA_TUNE_BLOCK:
+            if (value != 256 && value != 512 && value != 1024) return fail(FA_EINVAL, "fa_tune: block 256, 512 or 1024");
+            g_cfg.block_log = value == 256 ? 8 : value == 512 ? 9 : 10;
+            return FA_OK;
+        case FA_TUNE_READ:
+            if (value != 4 && value != 8 && value != 16) return fail(FA_EINVAL, "fa_tune: read probe depth 4, 8 or 16");
+            g_cfg.read_per_lane = value;
+            return FA_OK;
+        case FA_TUNE_GRID:
+            if (value < 0 || value > 64) return fail(FA_EINVAL, "fa_tune: grid blocks per CU must be 0..64");
+            g_cfg.grid_per_cu = value;
+            return FA_OK;
+        case FA_TUNE_TILEMAP:
+            if (value != 0 && value != 2 && value != 4 && value != 8 && value != 16 && value != 32)
+                return fail(FA_EINVAL, "fa_tune: tile map 0 (identity) or runs of 2, 4, 8, 16, 32 tiles per XCD");
+            g_cfg.tilemap = value;
+            return FA_OK;
+        case FA_TUNE_LANETAB:
+            g_cfg.lanetab = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_FASTDIV:
+            g_cfg.fastdiv = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_FASTDIV64:
+            g_cfg.fastdiv64 = value ? 1 : 0;
+            return FA_OK;
+        default:
+            return fail(FA_EINVAL, "fa_tune: unknown knob %d", knob);
+    }
+}
+
+int fa_stream_sum(float* out, const float* const* bufs, int K, int64_t P, void* stream) {
+    g_err[0] = 0;
+    if (K < 1 || K > kMaxK || P < 0 || !out || !bufs) return fail(FA_EINVAL, "fa_stream_sum: bad arguments");
+    bool vec = aligned16(out);
+    for (int k = 0; k < K; ++k) vec = vec && bufs[k] && aligned16(bufs[k]);
+    if (!vec) return fail(FA_EINVAL, "fa_stream_sum: buffers must be 16-B aligned");
+    ClientTable<float> tab;
+    std::vector<double> ones(K, 1.0);
+    fill_table<float>(tab, reinterpret_cast<const void* const*>(bufs), ones.data(), ones.data(), 0, K);
+    if (g_cfg.sum_nostore)
+        launch_fedavg_pipe<float, float, CADDNW, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
+    else if (g_cfg.nt_store == 1)
+        launch_fedavg_pipe<float, float, CADD, 4, 4, false, false, kBlock, 1>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
+    else if (g_cfg.nt_store == 2)
+        launch_fedavg_pipe<float, float, CADD, 4, 4, false, false, kBlock, 2>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
+    else
+        launch_fedavg_pipe<float, float, CADD, 4, 4, false, false>(out, tab, K, P, true, false, static_cast<hipStream_t>(stream));
+    return check_launch("fa_stream_sum");
+}
+
 int fa_stream_copy(void* dst, const void* src, int64_t bytes, void* stream) {
     g_err[0] = 0;
     if (bytes < 0 || (bytes & 15) || !aligned16(dst) || !aligned16(src))
@@ -1432,5 +1449,7 @@ int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream) {
     }
     return check_launch("fa_stream_read");
 }
+
+#endif  // FEDAGG_PROBES
 
 }  // extern "C"

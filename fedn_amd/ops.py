@@ -284,28 +284,37 @@ def cast(out, x, stream=None):
     return out
 
 
-def stream_copy(dst, src, stream=None):
+def _probe_lib():
+    """The measurement entry points exist only in libfedagg_probe.so (include/fedagg_probe.h)."""
     lib = _abi.load()
+    if lib is not _abi._probe:
+        raise RuntimeError("measurement / tuning entry point: call fedn_amd._abi.use_probe() first "
+                           "(libfedagg_probe.so; the product libfedagg.so has no knobs)")
+    return lib
+
+
+def stream_copy(dst, src, stream=None):
+    lib = _probe_lib()
     st = _stream_handle(src, stream)
     _abi.check(lib.fa_stream_copy(dst.data_ptr(), src.data_ptr(), src.numel() * src.element_size(), st))
 
 
 def stream_sum(out, bufs, stream=None):
     """Measurement: out = sum of bufs (fp32) with the FedAvg kernel's traversal."""
-    lib = _abi.load()
+    lib = _probe_lib()
     st = _stream_handle(out, stream)
     _abi.check(lib.fa_stream_sum(out.data_ptr(), _abi.ptr_array([b.data_ptr() for b in bufs]), len(bufs),
                                  out.numel(), st))
 
 
 def stream_read(src, sink, stream=None):
-    lib = _abi.load()
+    lib = _probe_lib()
     st = _stream_handle(src, stream)
     _abi.check(lib.fa_stream_read(src.data_ptr(), src.numel() * src.element_size(), sink.data_ptr(), st))
 
 
 def stream_read_sink(src):
-    lib = _abi.load()
+    lib = _probe_lib()
     blocks = lib.fa_stream_read_blocks(src.numel() * src.element_size())
     return torch.empty(max(1, blocks) * 16, dtype=torch.uint8, device=src.device)
 
@@ -320,7 +329,7 @@ _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _a
 
 def tune(**knobs):
     """Set launch knobs (fa_tune): FedAvg strips, unroll, nt, fastdiv, ...; and fastdiv64 (CF64's division). Results never change (every setting is bit-identical)."""
-    lib = _abi.load()
+    lib = _probe_lib()
     for k, v in knobs.items():
         _abi.check(lib.fa_tune(_KNOBS[k], int(v)))
 

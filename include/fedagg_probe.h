@@ -1,0 +1,61 @@
+/*
+ * fedagg_probe.h — measurement and tuning entry points of `libfedagg_probe.so`.
+ *
+ * NOT part of the drop-in boundary: the product library `libfedagg.so` exports only
+ * include/fedagg.h, built with the measured-best launch settings as compile-time constants
+ * (no mutable or process-global state). `libfedagg_probe.so` is the same source compiled with
+ * -DFEDAGG_PROBES: it exports everything fedagg.h declares PLUS the knobs and probe kernels
+ * below, which tools/ (microbench, PMC probes, A/B runs) and the division tests use to measure
+ * alternatives. Knob settings are process-global (atomics) within the probe library only.
+ */
+#ifndef FEDAGG_PROBE_H
+#define FEDAGG_PROBE_H
+
+#include "fedagg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/*
+ * Measurement helpers (not part of the reference interface): achievable-peak
+ * reference kernels for the roofline section of bench.py.
+ *   fa_stream_copy  dst[i] = src[i], 16 B per lane
+ *   fa_stream_read  reads `bytes` and writes one 16-B word per workgroup to `sink`
+ *                   (sink must hold >= 16 * fa_stream_read_blocks(bytes) bytes)
+ */
+int fa_stream_copy(void* dst, const void* src, int64_t bytes, void* stream);
+/* out[i] = sum_k bufs[k][i] (fp32, K <= 64) with exactly the traversal of the FedAvg fold
+ * kernel but one add per element: the access-pattern ceiling of fa_fedavg_fold.        */
+int fa_stream_sum(float* out, const float* const* bufs, int K, int64_t P, void* stream);
+
+/* Launch-geometry knobs of the fp32 FedAvg kernel (process-global; measurement and
+ * tuning only, results are identical for every setting):
+ *   FA_TUNE_STRIPS  16-B strips per lane (1 | 2 | 4 | 8 | 16)
+ *   FA_TUNE_UNROLL  clients loaded before folding (1 | 2 | 4 | 8 | 16)
+ *   (instantiated pairs: see launch_fedavg_vec; other pairs fall back to 1 x 8)
+ *   FA_TUNE_NT      non-temporal loads of the client buffers (0 | 1)
+ *   FA_TUNE_FASTDIV fp32 t/N via the exact RN64(1/N) product (1, default) or IEEE
+ *                   division (0); both are correctly rounded
+ *   FA_TUNE_LANETAB pipelined kernel (unroll 0) reads the client table from registers
+ *                   via v_readlane (1) or by scalar loads (0)
+ *   FA_TUNE_GRID    pipelined kernel: 0 = one 16-KiB-per-client tile per workgroup,
+ *                   n = persistent grid of n workgroups per CU sweeping tiles        */
+enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_TUNE_FASTDIV = 3, FA_TUNE_LANETAB = 4,
+                    FA_TUNE_GRID = 5, FA_TUNE_READ = 6 /* fa_stream_read loads per lane: 4 | 8 | 16 */,
+                    FA_TUNE_BLOCK = 7 /* pipelined kernel workgroup size 256 | 512 | 1024 */,
+                    FA_TUNE_SUM_NOSTORE = 8 /* fa_stream_sum probe: 1 = skip the store (reads + adds only) */,
+                    FA_TUNE_NT_STORE = 9 /* aggregate stores: 0 plain, 1 non-temporal, 2 write-through (sc1) */,
+                    FA_TUNE_FASTDIV64 = 10 /* fp64 t/N via RN64(1/N) + two exact Markstein corrections (1,
+                                              default) or IEEE division (0); both correctly rounded */,
+                    FA_TUNE_TILEMAP = 11 /* pipelined kernel: workgroup -> tile order, 0 identity or runs of
+                                            R = 2 | 4 | 8 | 16 | 32 consecutive tiles per XCD */ };
+int fa_tune(int knob, int value);
+int64_t fa_stream_read_blocks(int64_t bytes);
+int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FEDAGG_PROBE_H */

@@ -10,10 +10,11 @@ from fedn_amd import _abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "fedagg.h")
+PROBE_HEADER = os.path.join(ROOT, "include", "fedagg_probe.h")
 
 
-def header_functions():
-    src = open(HEADER).read()
+def header_functions(path=HEADER):
+    src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(fa_[a-z0-9_]+)\s*\(", src)))
 
@@ -31,6 +32,18 @@ def test_exports_every_declared_symbol():
     for n in names:
         assert hasattr(raw, n), f"libfedagg.so does not export {n}"
     assert set(names) == set(_abi.EXPORTS), "ctypes signature table out of sync with the header"
+    for n in header_functions(PROBE_HEADER):
+        assert not hasattr(raw, n), f"the product library exports the measurement entry point {n}"
+
+
+def test_probe_library_exports_both_headers():
+    """libfedagg_probe.so (tools/, A/B tests) = the product entry points + fedagg_probe.h."""
+    raw = ctypes.CDLL(_abi.PROBE_PATH)
+    probe = header_functions(PROBE_HEADER)
+    assert "fa_tune" in probe and set(probe) == set(_abi.PROBE_EXPORTS)
+    for n in header_functions() + probe:
+        assert hasattr(raw, n), f"libfedagg_probe.so does not export {n}"
+    assert _abi.load_probe().fa_abi_version() == _abi.ABI_VERSION
 
 
 def test_promote_table():

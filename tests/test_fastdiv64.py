@@ -11,7 +11,7 @@ representable values, and random operands over the whole guarded exponent range.
   product rounded once by Python's correctly rounded int/Fraction -> float conversion),
   against Python's correctly rounded t / N.
 * GPU: the fused FedAvg kernel computing 0 + (1*(t - 0))/N with the shortcut vs numpy's
-  t / N, and vs the kernel's own IEEE division on random operands (fa_tune fastdiv64=0).
+  t / N, and vs the kernel's own IEEE division on random operands (fa_tune fastdiv64=0 in libfedagg_probe.so).
 """
 import math
 from fractions import Fraction
@@ -114,8 +114,7 @@ def test_gpu_fastdiv64_vs_numpy():
     from fedn_amd import ops
     rng = np.random.default_rng(6464)
     dev = "cuda:0"
-    ops.tune(fastdiv64=1)
-    nbad = ntot = 0
+    nbad = ntot = 0          # the product library: its fp64 division is the corrected reciprocal
     # one launch per divisor (N is per client step), 400 + 100 divisors x 256 quotients
     for N, tl in {**hard_cases(rng, 400, 256), **near_exact_cases(rng, 100, 256)}.items():
         tt = torch.tensor(tl, dtype=torch.float64, device=dev)
@@ -132,7 +131,7 @@ def test_gpu_fastdiv64_vs_numpy():
 def test_gpu_fastdiv64_random_vs_ieee():
     import torch
 
-    from fedn_amd import ops
+    from fedn_amd import _abi, ops
     dev = "cuda:0"
     n = 1 << 24
     g = torch.Generator(device=dev).manual_seed(99)
@@ -153,14 +152,15 @@ def test_gpu_fastdiv64_random_vs_ieee():
     try:
         for t in (t_all, t_rng):
             for N in divisors:
-                ops.tune(fastdiv64=1)
-                ops.fedavg_fold(a, [z, t], [0, 1], [1, N], init=True)
-                ops.tune(fastdiv64=0)
-                ops.fedavg_fold(b, [z, t], [0, 1], [1, N], init=True)
+                ops.fedavg_fold(a, [z, t], [0, 1], [1, N], init=True)        # product libfedagg.so
+                with _abi.use_probe():                                      # IEEE division, probe build
+                    ops.tune(fastdiv64=0)
+                    ops.fedavg_fold(b, [z, t], [0, 1], [1, N], init=True)
                 diff = (a.view(torch.int64) != b.view(torch.int64)) & ~(torch.isnan(a) & torch.isnan(b))
                 nd = int(diff.sum())
                 if nd:
                     bad[N] = bad.get(N, 0) + nd
     finally:
-        ops.tune(fastdiv64=1)
+        with _abi.use_probe():
+            ops.tune(fastdiv64=1)
     assert not bad, f"fp64 fast division differs from IEEE division: {bad}"

@@ -3,7 +3,7 @@
 For every binary32 bit pattern t (all 2^32, NaNs and infinities included) and a set of
 divisors N, the fused FedAvg kernel computes x + (1*(t - x))/N with x = 0, i.e. RN(t/N)
 (then 0 + q). We run it once with the RN64(1/N)-product shortcut and once with IEEE
-division (fa_tune fastdiv=0, itself pinned to numpy by the golden tests) and require
+division (fa_tune fastdiv=0 in libfedagg_probe.so, itself pinned to numpy by the golden tests) and require
 bit-identical outputs.
 """
 import numpy as np
@@ -19,7 +19,7 @@ DIVISORS += [int(v) for v in np.random.default_rng(1234).integers(1, 1 << 24, 8)
 
 
 def test_fastdiv_exhaustive():
-    from fedn_amd import ops
+    from fedn_amd import _abi, ops
     dev = "cuda:0"
     chunk = 1 << 28
     zeros = torch.zeros(chunk, dtype=torch.float32, device=dev)
@@ -32,15 +32,16 @@ def test_fastdiv_exhaustive():
             t = (bits - (1 << 31)).to(torch.int32).view(torch.float32)   # every pattern once over all chunks
             del bits
             for N in DIVISORS:
-                ops.tune(fastdiv=1)
-                ops.fedavg_fold(a, [zeros, t], [0, 1], [1, N], init=True)
-                ops.tune(fastdiv=0)
-                ops.fedavg_fold(b, [zeros, t], [0, 1], [1, N], init=True)
+                ops.fedavg_fold(a, [zeros, t], [0, 1], [1, N], init=True)    # product libfedagg.so
+                with _abi.use_probe():                                      # IEEE division, probe build
+                    ops.tune(fastdiv=0)
+                    ops.fedavg_fold(b, [zeros, t], [0, 1], [1, N], init=True)
                 ai, bi = a.view(torch.int32), b.view(torch.int32)
                 diff = (ai != bi) & ~(torch.isnan(a) & torch.isnan(b))
                 nd = int(diff.sum())
                 if nd:
                     bad[N] = bad.get(N, 0) + nd
     finally:
-        ops.tune(fastdiv=1)
+        with _abi.use_probe():
+            ops.tune(fastdiv=1)
     assert not bad, f"fast division differs from IEEE division: {bad}"

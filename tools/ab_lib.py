@@ -15,7 +15,7 @@ from tools.microbench import timed  # noqa: E402
 
 
 def main():
-    _abi.load()
+    _abi.use_probe()
     torch.cuda.set_device(0)
     P = 100_000_000
     lib = os.path.basename(os.environ.get("FEDN_AMD_LIB", "libfedagg.so"))

@@ -167,6 +167,7 @@ def main():
     _abi.load()
     torch.cuda.set_device(0)
     if a.ab:
+        _abi.use_probe()          # fa_tune (fastdiv64 A/B) lives in libfedagg_probe.so
         config4_ab(a.p4, a.k4, ("adam", "yogi", "adagrad"), [0, 1, 0, 1])
         return
     if "4" in a.which:

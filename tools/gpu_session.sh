@@ -21,6 +21,12 @@ for s in $STEPS; do
     bench)
       timeout -k 10 600 python bench.py > "$OUT/bench.log" 2>&1; rc=$?
       echo "bench rc=$rc"; tail -3 "$OUT/bench.log"; [ $rc -eq 0 ] || exit $rc ;;
+    rehearsal)
+      # the N>1 code path (strong-scaling line + side fields) with 2 ranks on this box's one GPU (gloo)
+      FEDN_AMD_BENCH_ONE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --params 20000000 \
+        --clients 16 > "$OUT/rehearsal.log" 2>&1; rc=$?
+      echo "rehearsal rc=$rc"; grep -v amdgpu.ids "$OUT/rehearsal.log" | tail -3; [ $rc -eq 0 ] || exit $rc ;;
     micro)
       timeout -k 10 600 python tools/microbench.py > "$OUT/micro.log" 2>&1; rc=$?
       echo "micro rc=$rc"; cat "$OUT/micro.log" | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc ;;
@@ -55,11 +61,23 @@ for s in $STEPS; do
       timeout -k 10 600 python tools/bench_upload.py --params 100000000 --clients 8 --client-MBps 400 > "$OUT/upload100m.log" 2>&1; rc=$?
       echo "upload100m rc=$rc"; grep -v amdgpu.ids "$OUT/upload100m.log" | tail -5; [ $rc -eq 0 ] || exit $rc ;;
     pmc)
-      for c in FETCH_SIZE WRITE_SIZE; do
-        cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc_$c" -o run -- \
-          python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 > "$GRAFT_REPO_ROOT/$OUT/pmc_$c.log" 2>&1; rc=$?
-        cd "$GRAFT_REPO_ROOT"; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
-      done ;;
+      # HBM traffic per launch for every workload bench.py reports: one rocprofv3 pass per counter
+      # (FETCH_SIZE and WRITE_SIZE cannot share a pass), then profiles/pmc_traffic.json
+      i=0
+      for args in "--clients 64" "--clients 8 --fedopt-params 0" "--clients 64 --dtype bf16 --fedopt-params 0"; do
+        i=$((i+1))
+        for c in FETCH_SIZE WRITE_SIZE; do
+          cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc$i/pmc_$c" -o run -- \
+            python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 $args > "$GRAFT_REPO_ROOT/$OUT/pmc${i}_$c.log" 2>&1; rc=$?
+          cd "$GRAFT_REPO_ROOT"; echo "pmc$i $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+        done
+      done
+      P=100000000; Q=350000000
+      python tools/pmc_traffic.py $OUT/pmc1 fedavg_k64_p${P}_f32 "k_fedavg_pipe<float, float" $((64*P*4+P*4)) &&
+      python tools/pmc_traffic.py $OUT/pmc1 fedopt_adam_round1_k32_p$Q "k_fedopt<float, float" $((32*Q*4+Q*24)) &&
+      python tools/pmc_traffic.py $OUT/pmc1 fedopt_adam_steady_k32_p$Q "k_fedopt<float, double" $((Q*(4*32+48))) &&
+      python tools/pmc_traffic.py $OUT/pmc2 fedavg_k8_p${P}_f32 "k_fedavg_pipe<float, float" $((8*P*4+P*4)) &&
+      python tools/pmc_traffic.py $OUT/pmc3 fedavg_k64_p${P}_bf16 "bf16, float" $((64*P*2+P*4)) || exit 3 ;;
     pmcprobe)
       PA="TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum TCP_UTCL1_THRASHING_STALL_sum TCP_UTCL1_STALL_MULTI_MISS_sum GRBM_GUI_ACTIVE"
       PB="TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum"

@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--params", type=int, default=100_000_000)
     ap.add_argument("--pads", default="0,256,1024,4096,4352,65536,65792,1048576,2097152,2101248,3145728")
     a = ap.parse_args()
-    _abi.load()
+    _abi.use_probe()
     torch.cuda.set_device(0)
     K, P = a.clients, a.params
     g = torch.Generator(device="cuda").manual_seed(0)

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--clients", type=int, default=64)
     ap.add_argument("--sweep", default="all")
     a = ap.parse_args()
+    _abi.use_probe()
     lib = _abi.load()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)

@@ -19,7 +19,7 @@ TOTAL = 6_400_000_000
 
 
 def main(which):
-    _abi.load()
+    _abi.use_probe()
     torch.cuda.set_device(0)
     if which == "read":
         src = torch.empty(TOTAL, dtype=torch.uint8, device="cuda").random_()

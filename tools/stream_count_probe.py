@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fedn_amd import _abi, ops  # noqa: E402
 from tools.microbench import timed  # noqa: E402
 
-_abi.load()
+_abi.use_probe()
 torch.cuda.set_device(0)
 src = torch.empty(8 << 30, dtype=torch.uint8, device="cuda").random_()
 sink = ops.stream_read_sink(src)

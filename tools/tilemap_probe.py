@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--params", type=int, default=100_000_000)
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
-    _abi.load()
+    _abi.use_probe()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     P = a.params
