@@ -15,9 +15,11 @@ folds, so every GPU ends the step holding the whole aggregated model. The all-ga
 INSIDE the timed step; total work is fixed as N grows ("scaling": "strong").
 Beside the line at N > 1: ``weak_scaling`` (every rank folds its own 100 M slice, no
 collective), ``allgather`` (a plain all-gather of the model), ``gather_to_host`` (each rank
-D2H's its slice, FEDn's real consumer, roundhandler.py:465-468) and ``in_process`` (one
+D2H's its slice, FEDn's real consumer, roundhandler.py:465-468), ``in_process`` (one
 process driving all N GPUs, as a FEDn combiner with FEDN_AMD_DEVICES does: each device folds
-its slice and copies it into one pinned host model).
+its slice and copies it into one pinned host model) and ``fedopt_waves`` (BASELINE configs[4]:
+1 B bf16 params x 128 FedYogi updates streamed from pinned host memory in waves, sliced over the
+N GPUs of one process, each over its own PCIe link; fedn_amd/waves.py).
 
 Also measured in the same run:
   roofline      algorithmic bytes of the fold (K*P*4 + P*4 per launch at N = 1; per rank and
@@ -67,6 +69,9 @@ def parse():
     ap.add_argument("--fedopt-params", type=int, default=350_000_000, help="configs[3] side field (0 = skip)")
     ap.add_argument("--fedopt-clients", type=int, default=32)
     ap.add_argument("--no-side", action="store_true", help="N > 1: skip the beside-the-line measurements")
+    ap.add_argument("--waves-params", type=int, default=1_000_000_000, help="N > 1: configs[4] side field (0 = skip)")
+    ap.add_argument("--waves-clients", type=int, default=128)
+    ap.add_argument("--waves-pool", type=int, default=8, help="distinct pinned host updates (reused cyclically)")
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args()
 
@@ -440,10 +445,48 @@ def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, u
     out["allgather"] = side(plain_allgather)
     out["gather_to_host"] = side(gather_to_host)
     out["weak_scaling"] = side(weak)
+    def fedopt_waves():
+        """BASELINE configs[4] on this node: K bf16 updates of P params streamed from pinned host
+        memory in waves of 8, FedYogi, parameter-sliced over all N GPUs in one process (each GPU
+        copies only its slice of every update over its own PCIe link; fedn_amd.waves)."""
+        import hashlib
+
+        from fedn_amd.waves import WaveFedOpt
+        P, K, pool = a.waves_params, a.waves_clients, a.waves_pool
+        devs = [torch.device("cuda", 0 if rehearsal else d) for d in range(world)]
+        g = torch.Generator(device=devs[0]).manual_seed(5)
+        base = torch.randn(P, generator=g, device=devs[0])
+        host = []
+        for _ in range(pool):
+            h = torch.empty(P, dtype=torch.bfloat16, pin_memory=True)
+            h.copy_((base + 0.01 * torch.randn(P, generator=g, device=devs[0])).to(torch.bfloat16))
+            host.append(h)
+        base = base.cpu()
+        ups = [host[k % pool] for k in range(K)]
+        ns = [int(v) for v in np.random.default_rng(5).integers(1, 5001, K)]
+        wf = WaveFedOpt(devs, P, wave=8)
+        old = wf.slices(base.double())
+        wf.round(ups[:8], ns[:8], old, {"serveropt": "yogi"})         # warm-up (allocations, kernels)
+        wf = WaveFedOpt(devs, P, wave=8)
+        t0 = time.perf_counter()
+        outs = wf.round(ups, ns, old, {"serveropt": "yogi"})
+        t = time.perf_counter() - t0
+        res = wf.gather(outs)
+        del host, ups, old, outs, wf
+        torch.cuda.empty_cache()
+        return {"s": t, "value": K * P / t, "unit": "params/s", "params": P, "clients": K, "wave": 8, "devices": len(devs),
+                "h2d_GBps_total": K * P * 2 / t / 1e9, "h2d_GBps_per_link": K * P * 2 / t / 1e9 / len(devs),
+                "checksum_sha256_16": hashlib.sha256(res.numpy().tobytes()).hexdigest()[:16],
+                "note": f"BASELINE configs[4]: {pool} distinct pinned bf16 updates reused cyclically (every one "
+                        "crosses PCIe); PCIe-bound by design; not in value"}
+
     ip = side(in_process) if rank == 0 else None     # the other ranks wait (their GPUs are in use)
+    fw = side(fedopt_waves) if rank == 0 and a.waves_params > 0 else None
     dist.barrier()
     if rank == 0:
         out["in_process"] = ip
+        if fw is not None:
+            out["fedopt_waves"] = fw
     return out
 
 

@@ -22,9 +22,10 @@ FA_OK, FA_EINVAL, FA_EDTYPE, FA_EHIP = 0, 1, 2, 3
 # server optimizers (enum fa_serveropt)
 FA_ADAM, FA_YOGI, FA_ADAGRAD = 0, 1, 2
 FA_PG_FIRST, FA_PG_FINAL = 1, 2
-FA_EW_AXPBY, FA_EW_MUL, FA_EW_DIV, FA_EW_SQRT, FA_EW_SQUARE, FA_EW_SIGN, FA_EW_FILL = 0, 1, 2, 3, 4, 5, 6
+FA_EW_AXPBY, FA_EW_MUL, FA_EW_DIV, FA_EW_SQRT, FA_EW_SQUARE, FA_EW_SIGN, FA_EW_FILL, FA_EW_POW, FA_EW_IPOW = range(9)
 (FA_TUNE_STRIPS, FA_TUNE_UNROLL, FA_TUNE_NT, FA_TUNE_FASTDIV, FA_TUNE_LANETAB, FA_TUNE_GRID, FA_TUNE_READ,
- FA_TUNE_BLOCK, FA_TUNE_SUM_NOSTORE, FA_TUNE_NT_STORE, FA_TUNE_FASTDIV64, FA_TUNE_TILEMAP) = range(12)
+ FA_TUNE_BLOCK, FA_TUNE_SUM_NOSTORE, FA_TUNE_NT_STORE, FA_TUNE_FASTDIV64, FA_TUNE_TILEMAP, FA_TUNE_OPT_NT,
+ FA_TUNE_OPT_NOSTORE, FA_TUNE_OPT_STORE) = range(15)
 
 EXPORTS = {
     # name: (restype, argtypes)
@@ -57,6 +58,9 @@ EXPORTS = {
     "fa_elementwise": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int64,
                                       ctypes.c_void_p]),
+    "fa_norm1_work": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int]),
+    "fa_norm1": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "fa_cast": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
 }

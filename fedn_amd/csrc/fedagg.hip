@@ -600,7 +600,7 @@ __device__ __forceinline__ double np_sign(double d) {
 // The server step for one strip of E elements (fedopt.py:151-258), from the folded
 // pseudo-gradient pg and the widened old model ov (OLD -> V is exact or the same conversion
 // numpy's `old * 1.0` makes, so (double)ov == old as numpy sees it). rem < E: ragged strip.
-template <class PG, int E>
+template <class PG, int E, bool NOST = false, int OSM = 0>
 __device__ __forceinline__ void opt_final(const OptBuffers& b, const OptScalars& s, const typename PG::V (&pg)[E],
                                           const typename PG::V (&ov)[E], int64_t i0, int rem) {
     using V = typename PG::V;
@@ -661,15 +661,18 @@ __device__ __forceinline__ void opt_final(const OptBuffers& b, const OptScalars&
         o[e] = (double)ov[e] + t * s.lr;
     }
     // ---- stores
+    if constexpr (NOST) {   // probe build: stores skipped behind a never-true data test (reads + math live)
+        if (__double_as_longlong(o[0]) != 0x7FF4DEADBEEF0001LL) return;
+    }
     if (full) {
-        strip_store<double, E>(b.v_out + i0, v);
-        strip_store<double, E>(b.out + i0, o);
-        if (b.m_out_f64) strip_store<double, E>(static_cast<double*>(b.m_out) + i0, m);
+        strip_store<double, E, OSM>(b.v_out + i0, v);
+        strip_store<double, E, OSM>(b.out + i0, o);
+        if (b.m_out_f64) strip_store<double, E, OSM>(static_cast<double*>(b.m_out) + i0, m);
         else {
             float mf[E];
 #pragma unroll
             for (int e = 0; e < E; ++e) mf[e] = (float)m[e];
-            strip_store<float, E>(static_cast<float*>(b.m_out) + i0, mf);
+            strip_store<float, E, OSM>(static_cast<float*>(b.m_out) + i0, mf);
         }
     } else {
         for (int e = 0; e < rem; ++e) {
@@ -684,7 +687,7 @@ __device__ __forceinline__ void opt_final(const OptBuffers& b, const OptScalars&
 // One lane's strip of E elements at i0 < P, clients batched kUnroll/2 at a time. (A
 // k_fedavg_pipe-style traversal — 2 or 4 strips per lane, next client in flight — measured
 // within noise of this one on configs[3]: profiles/r01_fedopt_ab.log)
-template <typename Y, typename OLD, class PG, int E, bool FIRST, bool FINAL, bool NT>
+template <typename Y, typename OLD, class PG, int E, bool FIRST, bool FINAL, bool NT, bool NOST = false, int OSM = 0>
 __device__ __forceinline__ void fedopt_strip(const OptBuffers& b, const OptScalars& s,
                                              const ClientTable<typename PG::S>& tab, const int K, const int64_t P,
                                              const int64_t i0) {
@@ -758,15 +761,15 @@ __device__ __forceinline__ void fedopt_strip(const OptBuffers& b, const OptScala
             for (int e = 0; e < rem; ++e) pgp[e] = pg[e];
         return;
     } else {
-        opt_final<PG, E>(b, s, pg, ov, i0, rem);
+        opt_final<PG, E, NOST, OSM>(b, s, pg, ov, i0, rem);
     }
 }
 
-template <typename Y, typename OLD, class PG, int E, bool FIRST, bool FINAL, bool NT>
+template <typename Y, typename OLD, class PG, int E, bool FIRST, bool FINAL, bool NT, bool NOST = false, int OSM = 0>
 __global__ void __launch_bounds__(kBlock)
 k_fedopt(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
     const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * E;
-    if (i0 < P) fedopt_strip<Y, OLD, PG, E, FIRST, FINAL, NT>(b, s, tab, K, P, i0);
+    if (i0 < P) fedopt_strip<Y, OLD, PG, E, FIRST, FINAL, NT, NOST, OSM>(b, s, tab, K, P, i0);
 }
 
 // ----------------------------------------------------------------------------
@@ -807,12 +810,79 @@ k_elementwise(int op, TO* __restrict__ out, const TX* __restrict__ x, const TY* 
                 r = v > (TX)0 ? (TO)1 : (v < (TX)0 ? (TO)-1 : (v == (TX)0 ? (TO)0 : (TO)v));
                 break;
             }
+            case FA_EW_POW:                                       // numpyhelper.power(m, a), float a
+                if constexpr (std::is_same<TX, float>::value) r = (TO)(float)::pow((double)x[i], a);
+                else r = (TO)::pow((double)x[i], a);
+                break;
             default:                                              // FA_EW_FILL: np.ones(shape) * a
                 r = (TO)(1.0 * a);
                 break;
         }
         out[i] = r;
     }
+}
+
+// numpyhelper.power on an integer array with a non-negative python int exponent: numpy's
+// exponentiation by squaring in the array's integer type (wrapping products).
+template <typename T>
+__global__ void __launch_bounds__(kBlock) k_ipow(T* __restrict__ out, const T* __restrict__ x, uint64_t e, int64_t P) {
+    using U = typename std::make_unsigned<T>::type;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < P; i += (int64_t)gridDim.x * kBlock) {
+        U base = (U)x[i], r = 1;
+        for (uint64_t k = e; k; k >>= 1) {
+            if (k & 1) r *= base;
+            base *= base;
+        }
+        out[i] = (T)r;
+    }
+}
+
+// numpyhelper.norm (numpyhelper.py:106-117): np.linalg.norm(x, 1) of one tensor, accumulated in f64
+// with a fixed (deterministic) order. Vector: sum |x|, grid-stride partials per block then one
+// block sums the partials. Matrix (rows x cols, C order): column sums of |x| (one lane per
+// column, rows in order), then the max over columns (NaN propagates, as numpy's max).
+constexpr int kNormBlocks = 1024;
+template <typename T>
+__global__ void __launch_bounds__(kBlock) k_abssum_partial(const T* __restrict__ x, int64_t P, double* __restrict__ work) {
+    __shared__ double red[kBlock];
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < P; i += (int64_t)gridDim.x * kBlock)
+        acc += __builtin_fabs((double)x[i]);
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) work[blockIdx.x] = red[0];
+}
+template <typename T>
+__global__ void __launch_bounds__(kBlock) k_colabssum(const T* __restrict__ x, int64_t rows, int64_t cols,
+                                                      double* __restrict__ work) {
+    for (int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x; c < cols; c += (int64_t)gridDim.x * kBlock) {
+        double acc = 0.0;
+        for (int64_t r = 0; r < rows; ++r) acc += __builtin_fabs((double)x[r * cols + c]);
+        work[c] = acc;
+    }
+}
+__global__ void __launch_bounds__(kBlock) k_final_reduce(const double* __restrict__ work, int64_t n, int is_max,
+                                                         double* __restrict__ out) {
+    __shared__ double red[kBlock];
+    double acc = is_max ? -__builtin_inf() : 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += kBlock) {
+        const double v = work[i];
+        acc = is_max ? (acc != acc ? acc : (v != v || v > acc ? v : acc)) : acc + v;   // NaN wins, as numpy max
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            const double a = red[threadIdx.x], b = red[threadIdx.x + w];
+            red[threadIdx.x] = is_max ? (a != a ? a : (b != b || b > a ? b : a)) : a + b;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = (n == 0 && is_max) ? 0.0 : red[0];
 }
 
 // ----------------------------------------------------------------------------
@@ -890,7 +960,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -1075,6 +1145,20 @@ template <typename Y, typename OLD, class PG, int E, bool NT>
 int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTable<typename PG::S>& tab, int cnt,
                       int64_t P, bool first, bool final_, hipStream_t st) {
     const dim3 grid((unsigned)grid_for(P, E));
+#ifdef FEDAGG_PROBES
+    if (first && final_ && g_cfg.opt_nostore) {
+        hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, true>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        return check_launch("fa_fedopt_step: kernel launch");
+    }
+    if (first && final_ && g_cfg.opt_store == 1) {
+        hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, false, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        return check_launch("fa_fedopt_step: kernel launch");
+    }
+    if (first && final_ && g_cfg.opt_store == 2) {
+        hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, false, 2>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        return check_launch("fa_fedopt_step: kernel launch");
+    }
+#endif
     if (first && final_) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
     else if (first) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, false, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
     else if (final_) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, false, true, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
@@ -1098,6 +1182,15 @@ int launch_fedopt(const OptBuffers& b, const OptScalars& s, const void* const* u
         fill_table<S>(tab, ups, n, N, k0, cnt);
         const bool last = k0 + cnt >= K;
         const bool fin = last && final_all;
+#ifdef FEDAGG_PROBES
+        if (vec && !g_cfg.opt_nt) {
+            int rc = launch_fedopt_one<Y, OLD, PG, 4, false>(b, s, tab, cnt, P, first, fin, st);
+            if (rc) return rc;
+            first = false;
+            k0 += cnt;
+            continue;
+        }
+#endif
         int rc = vec ? launch_fedopt_one<Y, OLD, PG, 4, true>(b, s, tab, cnt, P, first, fin, st)
                      : launch_fedopt_one<Y, OLD, PG, 1, false>(b, s, tab, cnt, P, first, fin, st);
         if (rc) return rc;
@@ -1265,9 +1358,24 @@ int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype,
                    double a, double b, int64_t P, void* stream) {
     g_err[0] = 0;
     if (P < 0 || !out || (op != FA_EW_FILL && !x)) return fail(FA_EINVAL, "fa_elementwise: bad arguments");
-    if (op < FA_EW_AXPBY || op > FA_EW_FILL) return fail(FA_EINVAL, "fa_elementwise: unknown op %d", op);
+    if (op < FA_EW_AXPBY || op > FA_EW_IPOW) return fail(FA_EINVAL, "fa_elementwise: unknown op %d", op);
     if (op == FA_EW_AXPBY && !y) return fail(FA_EINVAL, "fa_elementwise: AXPBY needs y");
     if (P == 0) return FA_OK;
+    if (op == FA_EW_IPOW) {
+        if (out_dtype != x_dtype || (x_dtype != FA_I32 && x_dtype != FA_I64))
+            return fail(FA_EDTYPE, "fa_elementwise: IPOW takes an int32/int64 array and returns its dtype");
+        if (!(a >= 0.0) || a != std::floor(a) || a > 0x1p63)
+            return fail(FA_EINVAL, "fa_elementwise: IPOW exponent must be a non-negative integer");
+        const dim3 g((unsigned)std::min<int64_t>((P + kBlock - 1) / kBlock, 8192));
+        hipStream_t sti = static_cast<hipStream_t>(stream);
+        if (x_dtype == FA_I32)
+            hipLaunchKernelGGL(k_ipow<int32_t>, g, dim3(kBlock), 0, sti, static_cast<int32_t*>(out),
+                               static_cast<const int32_t*>(x), (uint64_t)a, P);
+        else
+            hipLaunchKernelGGL(k_ipow<int64_t>, g, dim3(kBlock), 0, sti, static_cast<int64_t*>(out),
+                               static_cast<const int64_t*>(x), (uint64_t)a, P);
+        return check_launch("fa_elementwise");
+    }
     auto isf = [](int d) { return d == FA_F32 || d == FA_F64; };
     if (op == FA_EW_FILL) x_dtype = out_dtype;
     if (!y) y_dtype = x_dtype;
@@ -1289,6 +1397,39 @@ int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype,
     else FA_EW(double, double, double);
 #undef FA_EW
     return check_launch("fa_elementwise");
+}
+
+int64_t fa_norm1_work(int64_t rows, int64_t cols, int matrix) {
+    return matrix ? std::max<int64_t>(cols, 1) : kNormBlocks;
+}
+
+int fa_norm1(double* out, const void* x, int dtype, int64_t rows, int64_t cols, int matrix, double* work,
+             void* stream) {
+    g_err[0] = 0;
+    if (!out || !work || rows < 0 || cols < 0 || (rows * cols > 0 && !x)) return fail(FA_EINVAL, "fa_norm1: bad arguments");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int64_t P = rows * cols;
+    auto run = [&](auto tag) -> int {
+        using T = decltype(tag);
+        const T* xp = static_cast<const T*>(x);
+        if (matrix) {
+            if (cols > 0)
+                hipLaunchKernelGGL(k_colabssum<T>, dim3((unsigned)std::min<int64_t>((cols + kBlock - 1) / kBlock, 4096)),
+                                   dim3(kBlock), 0, st, xp, rows, cols, work);
+            hipLaunchKernelGGL(k_final_reduce, dim3(1), dim3(kBlock), 0, st, work, cols, 1, out);
+        } else {
+            hipLaunchKernelGGL(k_abssum_partial<T>, dim3(kNormBlocks), dim3(kBlock), 0, st, xp, P, work);
+            hipLaunchKernelGGL(k_final_reduce, dim3(1), dim3(kBlock), 0, st, work, (int64_t)kNormBlocks, 0, out);
+        }
+        return check_launch("fa_norm1");
+    };
+    switch (dtype) {
+        case FA_F32: return run(float{});
+        case FA_F64: return run(double{});
+        case FA_I32: return run(int32_t{});
+        case FA_I64: return run(int64_t{});
+        default: return fail(FA_EDTYPE, "fa_norm1: dtype %d", dtype);
+    }
 }
 
 int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, const int64_t* out_shape,
@@ -1387,6 +1528,16 @@ int fa_tune(int knob, int value) {
             return FA_OK;
         case FA_TUNE_FASTDIV64:
             g_cfg.fastdiv64 = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_OPT_NT:
+            g_cfg.opt_nt = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_OPT_NOSTORE:
+            g_cfg.opt_nostore = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_OPT_STORE:
+            if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: FedOpt store mode 0 (plain), 1 (nt) or 2 (sc1)");
+            g_cfg.opt_store = value;
             return FA_OK;
         default:
             return fail(FA_EINVAL, "fa_tune: unknown knob %d", knob);

@@ -7,13 +7,14 @@ FEDn's ``HelperBase`` requires (helperbase.py:4-40) plus its file-type API:
                                               output readable by np.load
   load(path, file_type="npz")                 numpyhelper.py:171-189: native inflate (parallel
                                               for archives this codec wrote); raw_binary as FEDn
-  add / subtract / multiply / divide / sqrt / power(., 2) / sign / ones
+  add / subtract / multiply / divide / sqrt / sign / ones
                                               numpyhelper.py:34-142 on the GPU (fa_elementwise),
                                               numpy's dtype promotion and rounding, so FEDn's
                                               stock fedopt.py runs unchanged on this helper
 Inputs may be numpy arrays (results come back as numpy arrays, like numpyhelper) or device
 tensors (results stay on the device, so chains of primitives never leave HBM).
-``norm`` (numpyhelper.py:106-117, unused by the aggregators) is not provided.
+  power(m, a) / norm(m)                       numpyhelper.py:94-117 on the GPU (general exponents,
+                                              integer powers; the matrix 1-norm for 2-D tensors)
 FEDn selects helpers by module name (helpers.py:7-17); install with a shim module
 ``fedn/utils/helpers/plugins/fednamdhelper.py`` (INTEGRATION.md).
 """
@@ -46,18 +47,34 @@ def _back(t, host, shape):
     return t.to("cpu").numpy().reshape(shape) if host else t.reshape(shape)
 
 
+CACHED_LAYOUTS = 2     # model layouts whose staging slots increment_average keeps
+
+
 class Helper:
     def __init__(self):
         self.name = "fednamdhelper"
+        self._cache = {}
 
     def increment_average(self, m1, m2, n, N):
-        """One FedAvg fold of two models on the GPU (same rounding as numpyhelper.py:32)."""
+        """One FedAvg fold of two models on the GPU (same rounding and promotion as
+        numpyhelper.py:32). Stock FEDn calls this once per client (fedavg.py:68), so the pinned /
+        device staging slots and streams are kept per (device, model layout) and reused: a call
+        allocates only its result block."""
         from .aggregators.fedavg import default_device
+        from .layout import Layout
         from .staging import FedAvgPipeline
 
-        pipe = FedAvgPipeline(default_device(), list(m1))
-        pipe.add(list(m2), n, N)
-        return pipe.result()
+        m1, m2 = list(m1), list(m2)
+        dev = default_device()
+        key = (str(dev), Layout.of(m1).signature())
+        slots, streams = self._cache.pop(key, (None, None))
+        pipe = FedAvgPipeline(dev, m1, nslots=2, slots=slots, streams=streams)
+        pipe.add(m2, n, N)
+        out = pipe.result()
+        self._cache[key] = (pipe.slots, (pipe.copy, pipe.d2h))
+        while len(self._cache) > CACHED_LAYOUTS:              # oldest layout out
+            self._cache.pop(next(iter(self._cache)))
+        return out
 
     # ---- numpyhelper primitives on the GPU (numpyhelper.py:34-142) ----------------------------
     def _ew(self, op, m1, m2=None, a=0.0, b=0.0):
@@ -111,9 +128,61 @@ class Helper:
         return self._ew("sqrt", m1)
 
     def power(self, m1, a):
-        if a != 2:
-            raise NotImplementedError("fednamdhelper.power supports the exponent 2 (numpy's square path)")
-        return self._ew("square", m1)
+        """np.power(x, a) per tensor (numpyhelper.py:94-104), numpy's dtype rules: a float array
+        keeps its dtype for a python scalar a; an integer array with a non-negative python int
+        stays integer (exponentiation by squaring, wrapping), with a float a becomes float64.
+        a == 2 is x*x, numpy's exact result; other float exponents run the device pow (numpy's
+        own float power comes from its host SIMD library and differs between hosts: parity is
+        1e-6 relative for float32, 1e-15 for float64)."""
+        import torch
+
+        from . import ops
+        dev = _device()
+        out = []
+        for x in m1:
+            host = not isinstance(x, torch.Tensor)
+            xa = np.asarray(x) if host else None
+            xdt = xa.dtype if host else ops.numpy_dtype(x.dtype)
+            shape = tuple(x.shape)
+            if xdt.kind in "iu" and isinstance(a, (int, np.integer)) and a < 0:
+                raise ValueError("Integers to negative integer powers are not allowed.")
+            rdt = np.power(np.empty(0, xdt), a).dtype               # numpy's result dtype (no data)
+            xd = torch.from_numpy(np.ascontiguousarray(xa).reshape(-1)).to(dev) if host else x.contiguous().reshape(-1)
+            o = torch.empty(xd.numel(), dtype=ops.torch_dtype(rdt), device=dev)
+            if rdt.kind in "iu":
+                ops.elementwise("ipow", o, xd, None, float(a))
+            else:
+                if xd.dtype != o.dtype:
+                    xd = ops.cast(torch.empty(xd.numel(), dtype=o.dtype, device=dev), xd)
+                ops.elementwise("square" if a == 2 else "pow", o, xd, None, float(a))
+            out.append(_back(o, host, shape))
+        return out
+
+    def norm(self, m):
+        """numpyhelper.norm (numpyhelper.py:106-117): the sum over tensors of np.linalg.norm(x, 1) —
+        sum |x| of a vector, the max column sum of |x| of a matrix (the MATRIX 1-norm), a
+        ValueError for 0-d or >2-d tensors — accumulated from a python 0.0 as the reference does
+        (so float32 models give a numpy float32). Each tensor's norm is one device reduction in
+        float64 (numpy sums float32 pairwise in float32: parity 1e-6 relative)."""
+        import torch
+
+        from . import ops
+        dev = _device()
+        n = 0.0
+        for x in m:
+            host = not isinstance(x, torch.Tensor)
+            xa = np.asarray(x) if host else None
+            xdt = xa.dtype if host else ops.numpy_dtype(x.dtype)
+            nd = len(x.shape)
+            if nd not in (1, 2):
+                raise ValueError("Improper number of dimensions to norm.")
+            if nd == 2 and x.shape[1] == 0:
+                raise ValueError("zero-size array to reduction operation maximum which has no identity")
+            xd = torch.from_numpy(np.ascontiguousarray(xa)).to(dev) if host else x.contiguous()
+            val = float(ops.norm1(xd, nd == 2).item())
+            rdt = xdt if xdt.kind == "f" else np.dtype(np.float64)   # numpy: non-inexact -> astype(float)
+            n += rdt.type(val)
+        return n
 
     def sign(self, m1):
         return self._ew("sign", m1)

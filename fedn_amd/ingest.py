@@ -336,9 +336,12 @@ class StagingUpdateHandler:
                 data = None
             if data is not None:
                 from . import codec
-                layout, pinned = codec.load_npz_into_layout(
-                    data, lambda nbytes: torch.empty(nbytes, dtype=torch.uint8, pin_memory=True))
-                return stage_sharded(layout, pinned, self.devices, streams), metadata
+                try:
+                    layout, pinned = codec.load_npz_into_layout(
+                        data, lambda nbytes: torch.empty(nbytes, dtype=torch.uint8, pin_memory=True))
+                    return stage_sharded(layout, pinned, self.devices, streams), metadata
+                except codec.CodecError:
+                    pass     # e.g. Fortran-ordered members: decode through the helper (np.load) below
         arrays, metadata = self.inner.load_model_update(model_update, self.helper)
         arrays = [np.asarray(a) for a in arrays]
         layout = Layout.of(arrays)
@@ -367,8 +370,12 @@ class StagingUpdateHandler:
             except Exception:  # noqa: BLE001 — not held as bytes: decode through the helper
                 data = None
             if data is not None:
-                with torch.cuda.device(dev):
-                    return stage_npz(data, dev, self._stream()), metadata
+                from . import codec
+                try:
+                    with torch.cuda.device(dev):
+                        return stage_npz(data, dev, self._stream()), metadata
+                except codec.CodecError:
+                    pass     # e.g. Fortran-ordered members: decode through the helper (np.load) below
         arrays, metadata = self.inner.load_model_update(model_update, self.helper)
         with torch.cuda.device(dev):
             return stage_arrays(arrays, dev, self._stream()), metadata
@@ -387,6 +394,8 @@ class StagingUpdateHandler:
             self._device()
             with self._lock:
                 self._staged[model_update.model_update_id] = self._pool.submit(self._stage, model_update)
+        else:
+            self._uploads.pop(model_update.model_update_id)   # FEDn drops the update: free its decode
         return self.inner.on_model_update(model_update)
 
     def load_model_update(self, model_update, helper):

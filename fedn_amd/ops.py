@@ -324,7 +324,8 @@ _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _a
           "grid": _abi.FA_TUNE_GRID, "read": _abi.FA_TUNE_READ,
           "block": _abi.FA_TUNE_BLOCK, "sum_nostore": _abi.FA_TUNE_SUM_NOSTORE,
           "nt_store": _abi.FA_TUNE_NT_STORE, "fastdiv64": _abi.FA_TUNE_FASTDIV64,
-          "tilemap": _abi.FA_TUNE_TILEMAP}
+          "tilemap": _abi.FA_TUNE_TILEMAP, "opt_nt": _abi.FA_TUNE_OPT_NT, "opt_nostore": _abi.FA_TUNE_OPT_NOSTORE,
+          "opt_store": _abi.FA_TUNE_OPT_STORE}
 
 
 def tune(**knobs):
@@ -335,7 +336,8 @@ def tune(**knobs):
 
 
 _EW = {"axpby": _abi.FA_EW_AXPBY, "mul": _abi.FA_EW_MUL, "div": _abi.FA_EW_DIV, "sqrt": _abi.FA_EW_SQRT,
-       "square": _abi.FA_EW_SQUARE, "sign": _abi.FA_EW_SIGN, "fill": _abi.FA_EW_FILL}
+       "square": _abi.FA_EW_SQUARE, "sign": _abi.FA_EW_SIGN, "fill": _abi.FA_EW_FILL, "pow": _abi.FA_EW_POW,
+       "ipow": _abi.FA_EW_IPOW}
 
 
 def elementwise(op, out, x=None, y=None, a=0.0, b=0.0, stream=None):
@@ -351,5 +353,21 @@ def elementwise(op, out, x=None, y=None, a=0.0, b=0.0, stream=None):
         rc = lib.fa_elementwise(_EW[op], out.data_ptr(), fa_dtype(out), 0 if x is None else x.data_ptr(),
                                 fa_dtype(out) if x is None else fa_dtype(x), 0 if y is None else y.data_ptr(),
                                 _abi.FA_NONE if y is None else fa_dtype(y), float(a), float(b), P, st)
+    _abi.check(rc)
+    return out
+
+
+def norm1(x, matrix, stream=None):
+    """np.linalg.norm(x, 1) of one device tensor (``fa_norm1``): a 0-dim f64 device tensor.
+    ``matrix``: x is 2-D (max column sum of |x|), else the sum of |x| over all elements."""
+    lib = _abi.load()
+    if not x.is_contiguous():
+        raise ValueError("norm1: x must be contiguous")
+    rows, cols = (x.shape[0], x.shape[1]) if matrix else (1, x.numel())
+    work = torch.empty(max(1, int(lib.fa_norm1_work(rows, cols, int(matrix)))), dtype=torch.float64, device=x.device)
+    out = torch.empty((), dtype=torch.float64, device=x.device)
+    with torch.cuda.device(x.device):
+        st = _stream_handle(x, stream)
+        rc = lib.fa_norm1(out.data_ptr(), x.data_ptr(), fa_dtype(x), rows, cols, int(matrix), work.data_ptr(), st)
     _abi.check(rc)
     return out

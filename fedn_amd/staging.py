@@ -100,14 +100,19 @@ class _Slot:
 
 
 class _Pipeline:
-    def __init__(self, device, layout, nslots):
+    def __init__(self, device, layout, nslots, slots=None, streams=None):
         self.device = torch.device(device)
         self.layout = layout
         self.compute = torch.cuda.current_stream(self.device)
-        self.copy = torch.cuda.Stream(self.device)      # H2D (update slots, FedOpt's global model)
-        self.d2h = torch.cuda.Stream(self.device)       # D2H of the result (full duplex with H2D)
+        # H2D (update slots, FedOpt's global model) and D2H of the result (full duplex with H2D)
+        self.copy, self.d2h = streams if streams is not None else (torch.cuda.Stream(self.device),
+                                                                   torch.cuda.Stream(self.device))
         self.nslots = nslots
-        self.slots = []                          # created on first use (staged inputs need none)
+        # created on first use (staged inputs need none); a caller that folds many models of one
+        # layout (helper.Helper.increment_average) hands the same slots to every pipeline
+        self.slots = slots if slots is not None else []
+        for sl in self.slots:
+            sl.reserved = False
         self._next = 0
         self._h2d = []
         self._kern = []
@@ -253,9 +258,9 @@ class _Pipeline:
 class FedAvgPipeline(_Pipeline):
     """Streaming FedAvg on one device: fedavg.py:109-133 with the fold on the GPU."""
 
-    def __init__(self, device, first_arrays, nslots=3):
+    def __init__(self, device, first_arrays, nslots=3, slots=None, streams=None):
         staged = isinstance(first_arrays, StagedModel)
-        super().__init__(device, first_arrays.layout if staged else Layout.of(first_arrays), nslots)
+        super().__init__(device, first_arrays.layout if staged else Layout.of(first_arrays), nslots, slots, streams)
         self.first_arrays = first_arrays         # a StagedModel materialises host arrays only if needed
         self.first = self.acquire(first_arrays) if staged else self.stage(first_arrays)
         if not staged:

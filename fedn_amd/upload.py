@@ -20,6 +20,7 @@ object arrays, a corrupt stream) is simply not adopted: the update then takes th
 import ctypes
 import queue
 import threading
+import time
 from collections import OrderedDict
 from concurrent.futures import Future, ThreadPoolExecutor
 
@@ -252,8 +253,13 @@ class StreamingUpload:
     ``max_unclaimed_bytes``. Every other attribute is the wrapped service's."""
 
     def __init__(self, inner, handler, workers=4, pinned=True, device_decode=True, slot=8 << 20, ring=4,
-                 upload=None):
+                 upload=None, max_queued_chunks=64):
         self.inner = inner
+        # bounded tee: at most 4 x workers uploads are decoded at once (a decoder waits for a worker
+        # with at most max_queued_chunks chunks buffered; one that falls further behind is
+        # abandoned), later ones take the normal path — the host memory the tee holds is bounded
+        self._free = threading.Semaphore(4 * workers)
+        self.max_queued_chunks = max_queued_chunks
         self._upload = upload if upload is not None else inner.Upload
         self.handler = handler
         self.pinned = pinned
@@ -295,7 +301,7 @@ class StreamingUpload:
             return a
         return alloc
 
-    def _decode(self, q, fut, device):
+    def _decode(self, q, fut, device, stop):
         keep = []
         ended = False
         try:
@@ -309,7 +315,11 @@ class StreamingUpload:
                 if chunk is None:
                     ended = True
                     break
+                if stop.is_set():
+                    raise RuntimeError("decode abandoned: the upload outpaced the decoder")
                 dec.feed(chunk)
+            if stop.is_set():
+                raise RuntimeError("decode abandoned: the upload outpaced the decoder")
             members = dec.finish()
             ready = sink.finish()
             fut.set_result(DeviceDecodedUpdate(members, ready, device) if device is not None
@@ -319,6 +329,16 @@ class StreamingUpload:
             fut.set_exception(e)
             while not ended:                           # drain to the end of the upload
                 ended = q.get() is None
+        finally:
+            self._free.release()
+
+    def _start(self):
+        """A decoder for a new upload, or None when too many are in flight (normal path)."""
+        if not self.handler.wants_upload() or not self._free.acquire(blocking=False):
+            return None
+        q, fut, stop = queue.Queue(maxsize=self.max_queued_chunks), Future(), threading.Event()
+        self._pool.submit(self._decode, q, fut, self._device(), stop)
+        return q, fut, stop
 
     def Upload(self, request_iterator, context):
         if context is self.inner or context is self:
@@ -333,21 +353,30 @@ class StreamingUpload:
                 for request in request_iterator:
                     rid = request.id
                     if request.status == MODEL_STATUS_IN_PROGRESS and request.data:
-                        st = streams.get(rid)
-                        if st is None and self.handler.wants_upload():
-                            q, fut = queue.Queue(), Future()
-                            self._pool.submit(self._decode, q, fut, self._device())
-                            st = streams[rid] = (q, fut)
+                        if rid not in streams:
+                            streams[rid] = self._start()
+                        st = streams[rid]
                         if st is not None:
-                            st[0].put(bytes(request.data))
-                    if request.status == MODEL_STATUS_OK and not request.data and rid in streams:
-                        q, fut = streams.pop(rid)
+                            try:
+                                st[0].put_nowait(bytes(request.data))
+                            except queue.Full:          # decoder too slow: give this upload up
+                                st[2].set()
+                                try:                        # drop the backlog (never block the upload)
+                                    while True:
+                                        st[0].get_nowait()
+                                except queue.Empty:
+                                    pass
+                                st[0].put_nowait(None)
+                                streams[rid] = None
+                    if request.status == MODEL_STATUS_OK and not request.data and streams.get(rid) is not None:
+                        q, fut, _ = streams.pop(rid)
                         q.put(None)
                         self.handler.adopt(rid, fut)
                     yield request
             finally:                                   # stream ended (or Upload gave up) without OK
-                for q, _ in streams.values():
-                    q.put(None)
+                for st in streams.values():
+                    if st is not None:
+                        st[0].put(None)
                 streams.clear()
 
         return self._upload(tee(), context)
@@ -385,16 +414,25 @@ class StreamingUploadMixin:
 
 
 class AdoptedUploads:
-    """Decoded uploads waiting for their ModelUpdate, bounded by bytes (oldest dropped first)."""
+    """Decoded uploads waiting for their ModelUpdate, bounded by bytes (oldest dropped first) and
+    by age: an upload whose ModelUpdate never arrives (the client died after uploading, or the
+    update was rejected) is dropped after ``ttl`` seconds, so its host / HBM blocks are freed."""
 
-    def __init__(self, max_bytes=16 << 30):
+    def __init__(self, max_bytes=16 << 30, ttl=3600.0):
         self.max_bytes = max_bytes
+        self.ttl = ttl
         self._lock = threading.Lock()
         self._items = OrderedDict()       # id -> Future[DecodedUpdate]
+        self._born = {}
 
     def put(self, rid, fut):
+        now = time.monotonic()
         with self._lock:
             self._items[rid] = fut
+            self._born[rid] = now
+            for k in [k for k, t in self._born.items() if now - t > self.ttl]:
+                self._items.pop(k, None)
+                self._born.pop(k, None)
             total, drop = 0, []
             for k, f in reversed(self._items.items()):
                 if f.done() and f.exception() is None:
@@ -403,7 +441,9 @@ class AdoptedUploads:
                         drop.append(k)
             for k in drop:
                 self._items.pop(k, None)
+                self._born.pop(k, None)
 
     def pop(self, rid):
         with self._lock:
+            self._born.pop(rid, None)
             return self._items.pop(rid, None)

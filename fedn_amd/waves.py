@@ -1,0 +1,108 @@
+"""FedOpt over client updates that do not fit in HBM at once (BASELINE.json configs[4]: 1 B-param
+bf16 x 128 clients = 256 GB), streamed from host memory in waves, parameter-sliced over the
+node's GPUs.
+
+FEDn folds the pseudo-gradient client by client in queue order (fedopt.py:89-94) and applies the
+server step once (fedopt.py:110-118). Here the K host-resident updates (pinned CPU tensors, one
+flat buffer each, e.g. decoded by the streaming ingest) go to the devices W at a time: device d
+copies ONLY its parameter slice [lo_d, hi_d) of every update over its own PCIe link (one copy
+stream per device, two wave buffers: the H2D of wave i+1 overlaps the fold of wave i), folds the
+wave into its slice of the running pseudo-gradient (``fa_fedopt_step`` without FINAL keeps pg in
+HBM; FIRST on the first wave), and after the last wave runs the server step on its slice
+(K = 0, FINAL) with its slices of old / m / v resident. Every element sees the same client order
+and the same kernel, so the result is bit-identical for any device count and any wave size.
+"""
+import numpy as np
+import torch
+
+from . import ops
+from .sharded import shard_bounds
+
+
+class WaveFedOpt:
+    """One session's FedOpt state sliced over ``devices`` (a list; a device may repeat, e.g. on a
+    one-GPU box), for P-element flat models whose updates stream from host memory."""
+
+    def __init__(self, devices, P, wave=8):
+        self.devices = [torch.device(d) for d in devices]
+        self.P = P
+        self.wave = wave
+        self.bounds = shard_bounds(P, len(self.devices))
+        self.m = [None] * len(self.devices)
+        self.v = [None] * len(self.devices)
+        self.copy = [torch.cuda.Stream(d) for d in self.devices]
+        self.compute = [torch.cuda.current_stream(d) for d in self.devices]
+
+    def round(self, host_updates, ns, old, params):
+        """One aggregation round: ``host_updates`` = K flat CPU tensors (pinned for full-rate
+        H2D) in FIFO order, ``ns`` their num_examples, ``old`` the global model as one flat
+        tensor per device slice (``old[d]`` on device d, any dtype fa_fedopt_step takes).
+        Returns the new model as per-device f64 slices; m / v stay on the devices."""
+        K = len(host_updates)
+        if K == 0:
+            raise ValueError("no updates")
+        Ns = [int(v) for v in np.cumsum(ns)]
+        W = self.wave
+        upd_dt = host_updates[0].dtype
+        outs = []
+        ctx = []
+        for d, dv in enumerate(self.devices):
+            lo, hi = self.bounds[d]
+            with torch.cuda.device(dv):
+                n = hi - lo
+                pg_dt, m_dt = ops.fedopt_dtypes(upd_dt, old[d].dtype, None if self.m[d] is None else self.m[d].dtype)
+                slots = [[torch.empty(n, dtype=upd_dt, device=dv) for _ in range(W)] for _ in range(2)]
+                ctx.append({"n": n, "slots": slots, "pg": torch.empty(n, dtype=pg_dt, device=dv), "m_dt": m_dt,
+                            "loaded": [torch.cuda.Event() for _ in range(2)],
+                            "used": [torch.cuda.Event() for _ in range(2)]})
+        waves = (K + W - 1) // W
+        for w in range(waves):                       # every device's wave w, then wave w + 1, ...
+            b = w % 2
+            ks = list(range(w * W, min(K, (w + 1) * W)))
+            for d, dv in enumerate(self.devices):
+                lo, hi = self.bounds[d]
+                c = ctx[d]
+                if c["n"] == 0:
+                    continue
+                with torch.cuda.device(dv):
+                    if w >= 2:
+                        self.copy[d].wait_event(c["used"][b])     # the fold of wave w-2 read these buffers
+                    with torch.cuda.stream(self.copy[d]):
+                        for j, k in enumerate(ks):
+                            c["slots"][b][j].copy_(host_updates[k][lo:hi], non_blocking=True)
+                        c["loaded"][b].record(self.copy[d])
+                    self.compute[d].wait_event(c["loaded"][b])
+                    ops.fedopt_step(old[d], c["slots"][b][:len(ks)], [ns[k] for k in ks], [Ns[k] for k in ks],
+                                    first=(w == 0), final=False, pg=c["pg"], stream=self.compute[d])
+                    c["used"][b].record(self.compute[d])
+        for d, dv in enumerate(self.devices):
+            c = ctx[d]
+            with torch.cuda.device(dv):
+                m_out = torch.empty(c["n"], dtype=c["m_dt"], device=dv)
+                v_out = self.v[d] if self.v[d] is not None else torch.empty(c["n"], dtype=torch.float64, device=dv)
+                out = torch.empty(c["n"], dtype=torch.float64, device=dv)
+                if c["n"]:
+                    ops.fedopt_step(old[d], [], [], [], first=False, final=True, pg=c["pg"], m_in=self.m[d], m_out=m_out,
+                                    v_in=self.v[d], v_out=v_out, out=out, serveropt=params.get("serveropt", "adam"),
+                                    learning_rate=params.get("learning_rate", 1e-3), beta1=params.get("beta1", 0.9),
+                                    beta2=params.get("beta2", 0.99), tau=params.get("tau", 1e-4),
+                                    stream=self.compute[d], upd_dtype=upd_dt)
+                self.m[d], self.v[d] = m_out, v_out
+                outs.append(out)
+        for d, dv in enumerate(self.devices):
+            torch.cuda.synchronize(dv)
+        return outs
+
+    def slices(self, flat):
+        """``flat`` (a host or device tensor of P elements) cut into per-device slices on their devices."""
+        return [flat[lo:hi].to(dv) for (lo, hi), dv in zip(self.bounds, self.devices)]
+
+    def gather(self, per_dev):
+        """Per-device slices -> one host tensor (each device copies its slice over its own link)."""
+        host = torch.empty(self.P, dtype=per_dev[0].dtype, pin_memory=True)
+        for (lo, hi), t, dv in zip(self.bounds, per_dev, self.devices):
+            with torch.cuda.device(dv):
+                host[lo:hi].copy_(t, non_blocking=True)
+        for dv in self.devices:
+            torch.cuda.synchronize(dv)
+        return host

@@ -152,12 +152,29 @@ int fa_running_mean(void* g, int dtype, const void* m, double a, double b, doubl
  *   FA_EW_SQUARE  out = x*x                        numpyhelper.power(m, 2)
  *   FA_EW_SIGN    out = sign(x) (+-1, 0, NaN)      numpyhelper.sign
  *   FA_EW_FILL    out = 1.0*a (x unused)           numpyhelper.ones
+ *   FA_EW_POW     out = x**a (float a)             numpyhelper.power(m, a); f32 computed as the f64
+ *                                                  power rounded once (numpy's own float power is its
+ *                                                  host libm's / SIMD library's: not bit-reproducible
+ *                                                  across hosts; parity: 1e-6 relative, f64 1e-15)
+ *   FA_EW_IPOW    out = x**a, x I32 | I64, a a non-negative integer: exponentiation by squaring
+ *                 with wrapping products, out_dtype = x_dtype (numpy's integer power)
  * out_dtype must be the numpy result dtype of the op.
  */
 enum fa_ew_op { FA_EW_AXPBY = 0, FA_EW_MUL = 1, FA_EW_DIV = 2, FA_EW_SQRT = 3, FA_EW_SQUARE = 4, FA_EW_SIGN = 5,
-                FA_EW_FILL = 6 };
+                FA_EW_FILL = 6, FA_EW_POW = 7, FA_EW_IPOW = 8 };
 int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype, const void* y, int y_dtype,
                    double a, double b, int64_t P, void* stream);
+
+/*
+ * numpyhelper.norm (numpyhelper.py:106-117) for one tensor: np.linalg.norm(x, 1), i.e. sum |x| of a
+ * vector (matrix = 0; rows*cols elements) or the max column sum of |x| of a C-order rows x cols
+ * matrix (matrix = 1). x: F32 | F64 | I32 | I64. Accumulated in f64 in a fixed order (numpy sums f32
+ * pairwise in f32: parity 1e-6 relative). out: DEVICE double (written on `stream`); work: DEVICE
+ * scratch of fa_norm1_work(rows, cols, matrix) doubles.
+ */
+int64_t fa_norm1_work(int64_t rows, int64_t cols, int matrix);
+int fa_norm1(double* out, const void* x, int dtype, int64_t rows, int64_t cols, int matrix, double* work,
+             void* stream);
 
 /* dtype promotion used by the two entry points above (numpy result_type for the
  * pairs this library supports; bf16 promotes as f32). Returns FA_NONE if unsupported. */

@@ -49,7 +49,10 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                     FA_TUNE_FASTDIV64 = 10 /* fp64 t/N via RN64(1/N) + two exact Markstein corrections (1,
                                               default) or IEEE division (0); both correctly rounded */,
                     FA_TUNE_TILEMAP = 11 /* pipelined kernel: workgroup -> tile order, 0 identity or runs of
-                                            R = 2 | 4 | 8 | 16 | 32 consecutive tiles per XCD */ };
+                                            R = 2 | 4 | 8 | 16 | 32 consecutive tiles per XCD */,
+                    FA_TUNE_OPT_NT = 12 /* FedOpt client loads non-temporal (1, product) or cached (0) */,
+                    FA_TUNE_OPT_NOSTORE = 13 /* FedOpt FIRST|FINAL launch: 1 = skip the stores (reads + math) */,
+                    FA_TUNE_OPT_STORE = 14 /* FedOpt FIRST|FINAL stores: 0 plain, 1 non-temporal, 2 write-through */ };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);

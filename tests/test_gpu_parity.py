@@ -1034,3 +1034,126 @@ def test_multidevice_sharded_ingest_fedopt_mixed(name, ndev):
         assert_lists_identical(agg.m, rd["m"], f"{name} x{ndev} r{r} m")
         assert_lists_identical(agg.v, rd["v"], f"{name} x{ndev} r{r} v")
     st.close()
+
+
+# ------------------------------------------------------------------------- GPU helper: power / norm
+def test_helper_power_golden():
+    """fednamdhelper.power vs the REAL numpyhelper (fixture): dtypes exact; integer powers and x**2
+    bit-exact; other float exponents within 1e-6 relative (float32, the north-star bar) / 1e-15
+    (float64) — numpy's float power is its host SIMD library's and is not reproducible across hosts."""
+    from fedn_amd.helper import Helper
+    c = load_case("helper_power_norm")["raw"]
+    h = Helper()
+    for a, tag in ((0.5, "half"), (3, "i3"), (-1.5, "neg1p5"), (2, "sq"), (0.7, "p07")):
+        for src, key, rtol in (("x32", "pow32", 1e-6), ("x64", "pow64", 1e-15)):
+            got, want = h.power([c[src]], a)[0], c[f"{key}_{tag}"]
+            assert got.dtype == want.dtype and got.shape == want.shape
+            if a == 2:
+                assert_lists_identical([got], [want], f"{key}_{tag}")
+            else:
+                np.testing.assert_allclose(got, want, rtol=rtol, atol=0, err_msg=f"{key}_{tag}")
+    assert_lists_identical(h.power([c["i64"]], 3), [c["powi64_3"]], "i64^3")
+    assert_lists_identical(h.power([c["i64"]], 0), [c["powi64_0"]], "i64^0")
+    got = h.power([np.abs(c["i64"])], 0.5)[0]
+    assert got.dtype == c["powi64_f"].dtype
+    np.testing.assert_allclose(got, c["powi64_f"], rtol=1e-15, atol=0)
+    with pytest.raises(ValueError):
+        h.power([c["i64"]], -1)
+
+
+def test_helper_norm_golden():
+    """fednamdhelper.norm vs the REAL numpyhelper: the matrix 1-norm for 2-D tensors, the float32
+    accumulation dtype of a float32 model, 1e-6 relative."""
+    from fedn_amd.helper import Helper
+    c = load_case("helper_power_norm")["raw"]
+    h = Helper()
+    for args, key in (([c["x32"]], "norm_vec32"), ([c["m32"]], "norm_mat32"),
+                      ([c["m32"], c["x64"], c["i64"], c["m64"]], "norm_mixed")):
+        got = h.norm(args)
+        assert np.asarray(got).dtype == c[key].dtype, key
+        np.testing.assert_allclose(float(got), float(c[key]), rtol=1e-6, atol=0, err_msg=key)
+    with pytest.raises(ValueError):
+        h.norm([np.float32(3.0)])
+
+
+def test_helper_increment_average_reuses_slots():
+    """Stock fedavg.py on the helper calls increment_average once per client: the staging slots of
+    a layout are allocated once and reused; results stay bit-exact (mixed layouts included)."""
+    from fedn_amd.helper import Helper
+    rng = np.random.default_rng(21)
+    h = Helper()
+    base = [rng.standard_normal((300, 7)).astype(np.float32), rng.standard_normal(11).astype(np.float32)]
+    model, want, total = base, base, 0
+    ids = set()
+    for k in range(6):
+        nxt = [(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base]
+        n = int(rng.integers(1, 5001))
+        total += n
+        model = h.increment_average(model, nxt, n, total)
+        want = ref.increment_average(want, nxt, n, total)
+        ids |= {id(s) for sl, _ in h._cache.values() for s in sl}
+    assert_lists_identical(model, want, "cached slots")
+    assert len(ids) <= 2            # one layout, two slots, reused by all six calls
+    mixed = h.increment_average(model, [b.astype(np.float64) for b in base], 7, total + 7)
+    assert_lists_identical(mixed, ref.increment_average(model, [b.astype(np.float64) for b in base], 7, total + 7),
+                           "f32 model + f64 client")
+
+
+@pytest.mark.parametrize("ndev", [1, 2])
+def test_staging_ingest_fortran_member_falls_back(ndev):
+    """An npz whose member is Fortran-ordered cannot be inflated into the flat layout by the native
+    codec; the ingest decodes it through the helper (np.load) instead, as FEDn does, and the round
+    is bit-exact (no update may be skipped for the codec's sake)."""
+    import io
+    from fedn_amd.aggregators.fedavg import Aggregator
+    from fedn_amd.helper import Helper
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rng = np.random.default_rng(5)
+    uh = MemoryUpdateHandler()
+    devs = [DEV] * ndev
+    st = StagingUpdateHandler(uh, helper=Helper(), device=DEV, workers=2, devices=devs if ndev > 1 else None)
+    ups = []
+    for k in range(4):
+        w = rng.standard_normal((33, 17)).astype(np.float32)
+        arrays = [np.asfortranarray(w) if k % 2 else w, rng.standard_normal(9).astype(np.float32)]
+        b = io.BytesIO()
+        np.savez_compressed(b, **{str(i): a for i, a in enumerate(arrays)})
+        n = int(rng.integers(1, 5001))
+        uh.submit_bytes(b.getvalue(), n, via=st)
+        ups.append(([np.ascontiguousarray(a) for a in arrays], n))
+    agg = Aggregator(st, devices=devs) if ndev > 1 else Aggregator(st)
+    model, data = agg.combine_models(helper=Helper())
+    st.close()
+    want, nr = ref.fedavg_combine(ups)
+    assert data["nr_aggregated_models"] == nr == 4
+    assert_lists_identical(model, want, f"fortran x{ndev}")
+
+
+# ------------------------------------------------------------------------- configs[4]: waves from host
+@pytest.mark.parametrize("ndev", [1, 2, 3])
+def test_fedopt_bf16_waves_two_rounds(ndev):
+    """BASELINE configs[4] shape at 1 M params: bf16 updates streamed from pinned host memory in
+    waves of 8 (FA_PG_FIRST wave, non-final waves, then a K = 0 FA_PG_FINAL server step), FedYogi,
+    K = 130 (two 64-client kernel tables per wave boundary crossing included), two rounds with m / v
+    carried, sliced over 1-3 devices: bit-exact to the oracle run on the exact f32 upcasts."""
+    from fedn_amd.waves import WaveFedOpt
+    P, K, W = 1_000_003, 130, 8
+    g = torch.Generator().manual_seed(55)
+    old = torch.randn(P, generator=g).numpy()                  # round-1 global model, float32
+    params = {"serveropt": "yogi", "learning_rate": 1e-2}
+    wf = WaveFedOpt([DEV] * ndev, P, wave=W)
+    state = ref.FedOptState()
+    old_np = old
+    for r in range(2):
+        base = torch.from_numpy(np.asarray(old_np, dtype=np.float32))
+        host = [(base + 0.01 * torch.randn(P, generator=g)).to(torch.bfloat16).pin_memory() for _ in range(K)]
+        ns = [int(v) for v in np.random.default_rng(r).integers(1, 5001, K)]
+        outs = wf.round(host, ns, wf.slices(torch.from_numpy(np.asarray(old_np))), params)
+        got = wf.gather(outs).numpy()
+        want, nr = ref.fedopt_combine(state, [([h.float().numpy()], n) for h, n in zip(host, ns)], [old_np], params)
+        assert nr == K
+        assert_lists_identical([got], want, f"round {r} x{ndev}")
+        assert_lists_identical([wf.gather(wf.m).numpy()], state.m, f"round {r} m")
+        assert_lists_identical([wf.gather(wf.v).numpy()], state.v, f"round {r} v")
+        old_np = want[0]

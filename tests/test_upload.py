@@ -227,3 +227,28 @@ def test_staging_handler_upload_policy():
     st.helper = binaryhelper()
     assert not st.wants_upload()
     st.close()
+
+
+def test_streaming_upload_tee_is_bounded():
+    """More concurrent uploads than the tee allows take the normal path, and an upload that
+    outpaces its decoder by more than max_queued_chunks is abandoned (not adopted): the chunks
+    held in host memory stay bounded; every upload is still stored untouched."""
+    store = MemoryModelStore()
+    h = _Handler()
+    svc = StreamingUpload(MemoryModelService(store), h, workers=1, pinned=False, max_queued_chunks=4)
+    blocker = threading.Event()
+    svc._pool.submit(blocker.wait)                       # the only worker is busy: decoders must queue
+    data = _savez([np.arange(40_000, dtype=np.float32)])
+    svc.Upload(upload_requests(data, "late", chunk=1000), None)       # 160 chunks >> 4 queued
+    blocker.set()
+    assert store.get("late").data == data
+    assert "late" not in h.adopted or h.adopted["late"].exception(timeout=30) is not None
+    gens = [iter(upload_requests(data, f"c{i}", chunk=20_000)) for i in range(6)]
+    outs = [threading.Thread(target=svc.Upload, args=(g, None)) for g in gens]
+    for t in outs:
+        t.start()
+    for t in outs:
+        t.join(60)
+    assert all(store.get(f"c{i}").data == data for i in range(6))
+    svc.close()
+    assert svc._free._value == 4                        # every decoder slot released

@@ -108,49 +108,51 @@ def config4_ab(P, K, opts, settings):
     ops.tune(fastdiv64=1)
 
 
-def config5(P, K, W, pool, opt):
-    dev = torch.device("cuda", 0)
-    g = torch.Generator(device=dev).manual_seed(5)
-    old = torch.randn(P, generator=g, device=dev, dtype=torch.float64)
+def config5(P, K, W, pool, opt, ndev=1, check=True):
+    """BASELINE configs[4]: K bf16 updates of P params streamed from pinned host memory in waves of
+    W (fedn_amd.waves.WaveFedOpt), FedYogi, parameter-sliced over ``ndev`` devices (each copies only
+    its slice of every update over its own PCIe link). Reports per-link H2D GB/s and a checksum of
+    the result; with ``check`` the result is compared bit-for-bit with a one-device run."""
+    import hashlib
+
+    from fedn_amd.waves import WaveFedOpt
+    ngpu = torch.cuda.device_count()
+    devs = [torch.device("cuda", d % ngpu) for d in range(ndev)]
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    old = torch.randn(P, generator=g, device="cuda:0", dtype=torch.float64)
     host = []
     for _ in range(pool):
         h = torch.empty(P, dtype=torch.bfloat16, pin_memory=True)
-        h.copy_((old + 0.01 * torch.randn(P, generator=g, device=dev, dtype=torch.float64)).to(torch.bfloat16))
+        h.copy_((old + 0.01 * torch.randn(P, generator=g, device="cuda:0", dtype=torch.float64)).to(torch.bfloat16))
         host.append(h)
+    ups = [host[k % pool] for k in range(K)]
     ns = [int(v) for v in np.random.default_rng(5).integers(1, 5001, K)]
-    Ns = [int(v) for v in np.cumsum(ns)]
-    slots = [[torch.empty(P, dtype=torch.bfloat16, device=dev) for _ in range(W)] for _ in range(2)]
-    pg = torch.empty(P, dtype=torch.float64, device=dev)
-    m = torch.empty(P, dtype=torch.float64, device=dev)
-    v = torch.empty(P, dtype=torch.float64, device=dev)
-    out = torch.empty(P, dtype=torch.float64, device=dev)
-    comp = torch.cuda.current_stream(dev)
-    copy = torch.cuda.Stream(dev)
-    loaded = [torch.cuda.Event() for _ in range(2)]
-    used = [torch.cuda.Event() for _ in range(2)]
-    waves = (K + W - 1) // W
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for w in range(waves):
-        b = w % 2
-        ks = list(range(w * W, min(K, (w + 1) * W)))
-        if w >= 2:
-            copy.wait_event(used[b])
-        with torch.cuda.stream(copy):
-            for j, k in enumerate(ks):
-                slots[b][j].copy_(host[k % pool], non_blocking=True)
-            loaded[b].record(copy)
-        comp.wait_event(loaded[b])
-        ops.fedopt_step(old, slots[b][:len(ks)], [ns[k] for k in ks], [Ns[k] for k in ks], first=(w == 0),
-                        final=False, pg=pg, stream=comp)
-        used[b].record(comp)
-    ops.fedopt_step(old, [], [], [], first=False, final=True, pg=pg, m_out=m, v_out=v, out=out, serveropt=opt,
-                    stream=comp)
-    torch.cuda.synchronize()
-    t = time.perf_counter() - t0
-    print(json.dumps({"config": "config5", "opt": opt, "params": P, "clients": K, "wave": W, "s": t,
-                      "params_per_s": K * P / t, "h2d_GBps": K * P * 2 / t / 1e9,
-                      "note": f"{pool} distinct pinned bf16 updates reused cyclically"}), flush=True)
+    params = {"serveropt": opt}
+    old_h = old.cpu()
+
+    def run(devices):
+        wf = WaveFedOpt(devices, P, wave=W)
+        old_d = wf.slices(old_h)
+        for dv in devices:
+            torch.cuda.synchronize(dv)
+        t0 = time.perf_counter()
+        outs = wf.round(ups, ns, old_d, params)
+        t = time.perf_counter() - t0
+        return wf.gather(outs), t, wf
+
+    out, t, wf = run(devs)
+    digest = hashlib.sha256(out.numpy().tobytes()).hexdigest()[:16]
+    line = {"config": "config5", "opt": opt, "params": P, "clients": K, "wave": W, "devices": len(devs),
+            "distinct_gpus": len({str(d) for d in devs}), "s": t, "params_per_s": K * P / t,
+            "h2d_GBps_total": K * P * 2 / t / 1e9,
+            "h2d_GBps_per_link": [K * (hi - lo) * 2 / t / 1e9 for lo, hi in wf.bounds],
+            "checksum_sha256_16": digest,
+            "note": f"{pool} distinct pinned bf16 updates reused cyclically; every update still crosses PCIe"}
+    if check and len(devs) > 1:
+        ref_out, t1, _ = run([devs[0]])
+        line["bit_identical_to_1_device"] = bool(torch.equal(out.view(torch.int64), ref_out.view(torch.int64)))
+        line["s_1_device"] = t1
+    print(json.dumps(line), flush=True)
 
 
 def main():
@@ -162,6 +164,7 @@ def main():
     ap.add_argument("--k5", type=int, default=128)
     ap.add_argument("--wave", type=int, default=8)
     ap.add_argument("--pool", type=int, default=16)
+    ap.add_argument("--devices", type=int, default=1, help="config5: parameter slices over this many devices")
     ap.add_argument("--ab", action="store_true", help="A/B the FedOpt traversal and fp64 division knobs")
     a = ap.parse_args()
     _abi.load()
@@ -175,7 +178,7 @@ def main():
             config4(a.p4, a.k4, opt)
             torch.cuda.empty_cache()
     if "5" in a.which:
-        config5(a.p5, a.k5, a.wave, a.pool, "yogi")
+        config5(a.p5, a.k5, a.wave, a.pool, "yogi", a.devices)
 
 
 if __name__ == "__main__":

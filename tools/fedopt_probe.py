@@ -1,0 +1,71 @@
+"""A/B probe of the fused FedOpt kernel on BASELINE configs[3] (350 M x 32 FedAdam, device-resident):
+client loads non-temporal vs cached (opt_nt), and the same traversal with its stores skipped
+(opt_nostore: loads + arithmetic stay live) — the read-side ceiling of the kernel. Settings are
+interleaved over several repeats; median ms per setting. libfedagg_probe.so only."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fedn_amd import _abi, ops  # noqa: E402
+
+PEAK = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--params", type=int, default=350_000_000)
+    ap.add_argument("--clients", type=int, default=32)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    _abi.use_probe()
+    dev = torch.device("cuda", 0)
+    P, K = a.params, a.clients
+    g = torch.Generator(device=dev).manual_seed(4)
+    old32 = torch.randn(P, generator=g, device=dev)
+    ups = [torch.randn(P, generator=g, device=dev).mul_(0.01).add_(old32) for _ in range(K)]
+    ns = [int(v) for v in np.random.default_rng(4).integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
+    out = torch.empty(P, dtype=torch.float64, device=dev)
+    v = torch.empty(P, dtype=torch.float64, device=dev)
+    m32 = torch.empty(P, dtype=torch.float32, device=dev)
+    ops.fedopt_step(old32, ups, ns, Ns, first=True, final=True, m_out=m32, v_out=v, out=out)
+    old64, m64, v64 = out.clone(), m32.double(), v.clone()
+    m_o = torch.empty(P, dtype=torch.float64, device=dev)
+    v_o = torch.empty(P, dtype=torch.float64, device=dev)
+    o2 = torch.empty(P, dtype=torch.float64, device=dev)
+    phases = {
+        "round1": (lambda: ops.fedopt_step(old32, ups, ns, Ns, first=True, final=True, m_out=m32, v_out=v, out=out),
+                   K * P * 4 + P * 24),
+        "steady": (lambda: ops.fedopt_step(old64, ups, ns, Ns, first=True, final=True, m_in=m64, m_out=m_o, v_in=v64,
+                                           v_out=v_o, out=o2), P * (4 * K + 48)),
+    }
+    settings = [(1, 0, 0), (1, 0, 1), (1, 0, 2), (1, 1, 0)]
+    res = {}
+    for rep in range(a.reps):
+        for name, (fn, b) in phases.items():
+            for nt, nost, sm in settings:
+                ops.tune(opt_nt=nt, opt_nostore=nost, opt_store=sm)
+                fn()
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+                for s_, e_ in ev:
+                    s_.record()
+                    fn()
+                    e_.record()
+                torch.cuda.synchronize()
+                ms = sorted(s_.elapsed_time(e_) for s_, e_ in ev)[2]
+                res.setdefault((name, nt, nost, sm), []).append(ms)
+    ops.tune(opt_nt=1, opt_nostore=0, opt_store=0)
+    for (name, nt, nost, sm), mss in res.items():
+        ms = float(np.median(mss))
+        b = phases[name][1]
+        print(json.dumps({"phase": name, "opt_nt": nt, "nostore": nost, "store_mode": sm, "ms": ms, "GBps_alg": b / ms / 1e6,
+                          "frac": b / ms / 1e6 / PEAK, "reps": mss}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -243,6 +243,29 @@ def helper_ops(ref, rng):
     return d
 
 
+def helper_power_norm(ref, rng):
+    """numpyhelper.power with general exponents and numpyhelper.norm (numpyhelper.py:94-117), the
+    real helper on float32 / float64 / int64 tensors, vectors and matrices."""
+    h = ref["Helper"]()
+    x32 = np.abs(rng.standard_normal(513)).astype(np.float32) + np.float32(0.01)
+    x64 = np.abs(rng.standard_normal(257)) + 0.01
+    i64 = rng.integers(-50, 50, 129).astype(np.int64)
+    m32 = rng.standard_normal((37, 11)).astype(np.float32)
+    m64 = rng.standard_normal((5, 300))
+    d = {"kind": np.array("helper_ops2"), "name": np.array("helper_power_norm"), "x32": x32, "x64": x64, "i64": i64,
+         "m32": m32, "m64": m64}
+    for a, tag in ((0.5, "half"), (3, "i3"), (-1.5, "neg1p5"), (2, "sq"), (0.7, "p07")):
+        d[f"pow32_{tag}"] = h.power([x32], a)[0]
+        d[f"pow64_{tag}"] = h.power([x64], a)[0]
+    d["powi64_3"] = h.power([i64], 3)[0]
+    d["powi64_0"] = h.power([i64], 0)[0]
+    d["powi64_f"] = h.power([np.abs(i64)], 0.5)[0]
+    d["norm_vec32"] = np.array(h.norm([x32]))
+    d["norm_mat32"] = np.array(h.norm([m32]))
+    d["norm_mixed"] = np.array(h.norm([m32, x64, i64, m64]))
+    return d
+
+
 def reduce_case(ref, name, rng, shapes, plan):
     """Control.reduce (fedn/network/controller/control.py:648-693). control.py cannot be imported
     here (it needs `tenacity`, absent from the image, and we do not stub libraries), so its
@@ -595,6 +618,8 @@ def main():
         return _write(helper_cases(ref), merge=True)
     if only == "mixed":
         return _write(mixed_cases(ref), merge=True)
+    if only == "power_norm":
+        return _write([helper_power_norm(ref, np.random.default_rng(9))], merge=True)
     cases = []
     cases.append(helper_kat(ref))
     rng = np.random.default_rng(1)
@@ -647,6 +672,7 @@ def main():
     cases += sf_cases(ref)
     cases += helper_cases(ref)
     cases += mixed_cases(ref)
+    cases.append(helper_power_norm(ref, np.random.default_rng(9)))
     _write(cases, merge=False)
 
 

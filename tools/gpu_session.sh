@@ -25,7 +25,7 @@ for s in $STEPS; do
       # the N>1 code path (strong-scaling line + side fields) with 2 ranks on this box's one GPU (gloo)
       FEDN_AMD_BENCH_ONE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --params 20000000 \
-        --clients 16 > "$OUT/rehearsal.log" 2>&1; rc=$?
+        --clients 16 --waves-params 50000000 --waves-clients 32 > "$OUT/rehearsal.log" 2>&1; rc=$?
       echo "rehearsal rc=$rc"; grep -v amdgpu.ids "$OUT/rehearsal.log" | tail -3; [ $rc -eq 0 ] || exit $rc ;;
     micro)
       timeout -k 10 600 python tools/microbench.py > "$OUT/micro.log" 2>&1; rc=$?
@@ -72,12 +72,7 @@ for s in $STEPS; do
           cd "$GRAFT_REPO_ROOT"; echo "pmc$i $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
         done
       done
-      P=100000000; Q=350000000
-      python tools/pmc_traffic.py $OUT/pmc1 fedavg_k64_p${P}_f32 "k_fedavg_pipe<float, float" $((64*P*4+P*4)) &&
-      python tools/pmc_traffic.py $OUT/pmc1 fedopt_adam_round1_k32_p$Q "k_fedopt<float, float" $((32*Q*4+Q*24)) &&
-      python tools/pmc_traffic.py $OUT/pmc1 fedopt_adam_steady_k32_p$Q "k_fedopt<float, double" $((Q*(4*32+48))) &&
-      python tools/pmc_traffic.py $OUT/pmc2 fedavg_k8_p${P}_f32 "k_fedavg_pipe<float, float" $((8*P*4+P*4)) &&
-      python tools/pmc_traffic.py $OUT/pmc3 fedavg_k64_p${P}_bf16 "bf16, float" $((64*P*2+P*4)) || exit 3 ;;
+      echo "pmc: now run  python tools/pmc_traffic.py --session $OUT  in the build container" ;;
     pmcprobe)
       PA="TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum TCP_UTCL1_THRASHING_STALL_sum TCP_UTCL1_STALL_MULTI_MISS_sum GRBM_GUI_ACTIVE"
       PB="TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum"

@@ -2,6 +2,7 @@
 
 Usage: python tools/pmc_traffic.py <dir with pmc_FETCH_SIZE/ and pmc_WRITE_SIZE/> <workload key> [kernel substring]
        [algorithmic bytes per launch]
+       python tools/pmc_traffic.py --session gpurun_out/<tag>      (every workload of gpu_session.sh "pmc")
 
 gfx950 corrections (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7): FETCH_SIZE and
 WRITE_SIZE are in KiB; FETCH_SIZE reports exactly 1/2 of the bytes of a wide (16 B/lane)
@@ -33,15 +34,12 @@ def per_launch(path, kernel):
     return sum(vals) / len(vals), len(vals)
 
 
-def main():
-    d, key = sys.argv[1], sys.argv[2]
-    kernel = sys.argv[3] if len(sys.argv) > 3 else "k_fedavg"
-    alg = float(sys.argv[4]) if len(sys.argv) > 4 else None
+def record(d, key, kernel, alg=None):
     fetch, nf = per_launch(os.path.join(d, "pmc_FETCH_SIZE", "run_counter_collection.csv"), kernel)
     write, nw = per_launch(os.path.join(d, "pmc_WRITE_SIZE", "run_counter_collection.csv"), kernel)
     read_b = 2 * fetch * 1024
     write_b = write * 1024
-    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+    out = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     db = json.load(open(out)) if os.path.exists(out) else {}
     db[key] = {"bytes": read_b + write_b, "read_bytes": read_b, "write_bytes": write_b,
                "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write, "launches": [nf, nw], "kernel": kernel,
@@ -50,7 +48,29 @@ def main():
                "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count on 16-B streaming loads); "
                              "write = WRITE_SIZE x 1024"}
     json.dump(db, open(out, "w"), indent=1)
-    print(json.dumps(db[key]))
+    print(json.dumps({key: db[key]}))
+
+
+# the workloads bench.py reports (tools/gpu_session.sh step "pmc" runs the passes into pmc1..3)
+P, Q = 100_000_000, 350_000_000
+SESSION = [
+    ("pmc1", f"fedavg_k64_p{P}_f32", "k_fedavg_pipe<float, float", 64 * P * 4 + P * 4),
+    ("pmc1", f"fedopt_adam_round1_k32_p{Q}", "k_fedopt<float, float", 32 * Q * 4 + Q * 24),
+    ("pmc1", f"fedopt_adam_steady_k32_p{Q}", "k_fedopt<float, double", Q * (4 * 32 + 48)),
+    ("pmc2", f"fedavg_k8_p{P}_f32", "k_fedavg_pipe<float, float", 8 * P * 4 + P * 4),
+    ("pmc3", f"fedavg_k64_p{P}_bf16", "bf16, float", 64 * P * 2 + P * 4),
+]
+
+
+def main():
+    if sys.argv[1] == "--session":
+        for sub, key, kernel, alg in SESSION:
+            record(os.path.join(sys.argv[2], sub), key, kernel, alg)
+        return
+    d, key = sys.argv[1], sys.argv[2]
+    kernel = sys.argv[3] if len(sys.argv) > 3 else "k_fedavg"
+    alg = float(sys.argv[4]) if len(sys.argv) > 4 else None
+    record(d, key, kernel, alg)
 
 
 if __name__ == "__main__":
