@@ -436,7 +436,7 @@ def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, u
                 run()
             t = (time.perf_counter() - t0) / 5
             res = {"ms": t * 1e3, "value": K * P_total / t, "devices": len(devs),
-                   "note": "one process, all GPUs: each folds its slice of the 64 device-resident updates and "
+                   "note": f"one process, all GPUs: each folds its slice of the {K} device-resident updates and "
                            "D2H's it into one pinned host model (fold + PCIe copy, no collective); not in value"}
             del data, host
             torch.cuda.empty_cache()

@@ -268,6 +268,7 @@ template <> __device__ __forceinline__ f16 narrow<f16, float>(float v) { return 
 // 16-byte strip loads/stores (E elements of T). NT = non-temporal (read-once data)
 // ----------------------------------------------------------------------------
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 template <typename T, int E, bool NT>
 __device__ __forceinline__ void strip_load(const T* __restrict__ p, T (&r)[E]) {
@@ -279,6 +280,14 @@ __device__ __forceinline__ void strip_load(const T* __restrict__ p, T (&r)[E]) {
             u32x4 w = NT ? __builtin_nontemporal_load(q + j) : q[j];
             __builtin_memcpy(reinterpret_cast<char*>(r) + 16 * j, &w, 16);
         }
+    } else if constexpr (bytes == 8) {          // one dwordx2 (8-B aligned: the caller's contract)
+        const u32x2* q = reinterpret_cast<const u32x2*>(p);
+        u32x2 w = NT ? __builtin_nontemporal_load(q) : *q;
+        __builtin_memcpy(reinterpret_cast<char*>(r), &w, 8);
+    } else if constexpr (bytes == 4) {          // one dword (4-B aligned)
+        const unsigned int* q = reinterpret_cast<const unsigned int*>(p);
+        unsigned int w = NT ? __builtin_nontemporal_load(q) : *q;
+        __builtin_memcpy(reinterpret_cast<char*>(r), &w, 4);
     } else {
 #pragma unroll
         for (int e = 0; e < E; ++e) r[e] = p[e];
@@ -290,7 +299,15 @@ __device__ __forceinline__ void strip_load(const T* __restrict__ p, T (&r)[E]) {
 template <typename T, int E, int SM = 0>
 __device__ __forceinline__ void strip_store(T* __restrict__ p, const T (&r)[E]) {
     constexpr int bytes = E * (int)sizeof(T);
-    if constexpr (bytes % 16 == 0) {
+    if constexpr (bytes == 8 && SM == 0) {
+        u32x2 w;
+        __builtin_memcpy(&w, reinterpret_cast<const char*>(r), 8);
+        *reinterpret_cast<u32x2*>(p) = w;
+    } else if constexpr (bytes == 8 && SM == 1) {
+        u32x2 w;
+        __builtin_memcpy(&w, reinterpret_cast<const char*>(r), 8);
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x2*>(p));
+    } else if constexpr (bytes % 16 == 0) {
         u32x4* q = reinterpret_cast<u32x4*>(p);
 #pragma unroll
         for (int j = 0; j < bytes / 16; ++j) {
@@ -597,12 +614,45 @@ __device__ __forceinline__ double np_sign(double d) {
     return d > 0.0 ? 1.0 : (d < 0.0 ? -1.0 : (d == 0.0 ? 0.0 : d));
 }
 
+// The server state of one strip: m_in (as exact f64 values; f32 state is widened exactly) and
+// v_in (or tau**2 when v is None, fedopt.py:170-171). rem < E: ragged strip.
+template <int E, bool SNT = false>
+__device__ __forceinline__ void opt_load_state(const OptBuffers& b, const OptScalars& s, int64_t i0, int rem,
+                                               double (&mi)[E], double (&v)[E]) {
+    const bool full = rem == E;
+    if (b.m_in_f64 == 0) {
+        float mf[E];
+        const float* mp = static_cast<const float*>(b.m_in) + i0;
+        if (full) strip_load<float, E, SNT>(mp, mf);
+        else
+            for (int e = 0; e < E; ++e) mf[e] = e < rem ? mp[e] : 0.f;
+#pragma unroll
+        for (int e = 0; e < E; ++e) mi[e] = (double)mf[e];
+    } else if (b.m_in_f64 > 0) {
+        const double* mp = static_cast<const double*>(b.m_in) + i0;
+        if (full) strip_load<double, E, SNT>(mp, mi);
+        else
+            for (int e = 0; e < E; ++e) mi[e] = e < rem ? mp[e] : 0.0;
+    }
+    if (b.v_in) {
+        const double* vp = b.v_in + i0;
+        if (full) strip_load<double, E, SNT>(vp, v);
+        else
+            for (int e = 0; e < E; ++e) v[e] = e < rem ? vp[e] : 0.0;
+    } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = s.tau2;
+    }
+}
+
 // The server step for one strip of E elements (fedopt.py:151-258), from the folded
-// pseudo-gradient pg and the widened old model ov (OLD -> V is exact or the same conversion
-// numpy's `old * 1.0` makes, so (double)ov == old as numpy sees it). rem < E: ragged strip.
+// pseudo-gradient pg, the widened old model ov (OLD -> V is exact or the same conversion
+// numpy's `old * 1.0` makes, so (double)ov == old as numpy sees it) and the state loaded by
+// opt_load_state (mi, v; v is updated in place). rem < E: ragged strip.
 template <class PG, int E, bool NOST = false, int OSM = 0>
-__device__ __forceinline__ void opt_final(const OptBuffers& b, const OptScalars& s, const typename PG::V (&pg)[E],
-                                          const typename PG::V (&ov)[E], int64_t i0, int rem) {
+__device__ __forceinline__ void opt_apply(const OptBuffers& b, const OptScalars& s, const typename PG::V (&pg)[E],
+                                          const typename PG::V (&ov)[E], const double (&mi)[E], double (&v)[E],
+                                          int64_t i0, int rem) {
     using V = typename PG::V;
     constexpr bool PG32 = std::is_same<PG, CF32>::value;
     const bool full = rem == E;
@@ -612,37 +662,17 @@ __device__ __forceinline__ void opt_final(const OptBuffers& b, const OptScalars&
 #pragma unroll
         for (int e = 0; e < E; ++e) m[e] = mul_pg<PG>((double)pg[e], s.c1, s.c1f);
     } else if (b.m_in_f64 == 0) {
-        float mi[E];
-        const float* mp = static_cast<const float*>(b.m_in) + i0;
-        if (full) strip_load<float, E, false>(mp, mi);
-        else
-            for (int e = 0; e < E; ++e) mi[e] = e < rem ? mp[e] : 0.f;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            const float a = mi[e] * s.b1f;                               // m*beta1 in f32
+            const float a = (float)mi[e] * s.b1f;                        // m*beta1 in f32 (mi is an exact f32)
             if constexpr (PG32) m[e] = (double)(a + (float)pg[e] * s.c1f);  // f32 + f32
             else m[e] = (double)a + (double)pg[e] * s.c1;                   // f32 -> f64 add
         }
     } else {
-        double mi[E];
-        const double* mp = static_cast<const double*>(b.m_in) + i0;
-        if (full) strip_load<double, E, false>(mp, mi);
-        else
-            for (int e = 0; e < E; ++e) mi[e] = e < rem ? mp[e] : 0.0;
 #pragma unroll
         for (int e = 0; e < E; ++e) m[e] = mi[e] * s.b1 + mul_pg<PG>((double)pg[e], s.c1, s.c1f);
     }
-    // ---- v (fedopt.py:170-171, 178-179 / 214-217 / 251-252)
-    double v[E];
-    if (b.v_in) {
-        const double* vp = b.v_in + i0;
-        if (full) strip_load<double, E, false>(vp, v);
-        else
-            for (int e = 0; e < E; ++e) v[e] = e < rem ? vp[e] : 0.0;
-    } else {
-#pragma unroll
-        for (int e = 0; e < E; ++e) v[e] = s.tau2;
-    }
+    // ---- v (fedopt.py:178-179 / 214-217 / 251-252)
     double o[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -682,6 +712,14 @@ __device__ __forceinline__ void opt_final(const OptBuffers& b, const OptScalars&
             else static_cast<float*>(b.m_out)[i0 + e] = (float)m[e];
         }
     }
+}
+
+template <class PG, int E, bool NOST = false, int OSM = 0>
+__device__ __forceinline__ void opt_final(const OptBuffers& b, const OptScalars& s, const typename PG::V (&pg)[E],
+                                          const typename PG::V (&ov)[E], int64_t i0, int rem) {
+    double mi[E], v[E];
+    opt_load_state<E>(b, s, i0, rem, mi, v);
+    opt_apply<PG, E, NOST, OSM>(b, s, pg, ov, mi, v, i0, rem);
 }
 
 // One lane's strip of E elements at i0 < P, clients batched kUnroll/2 at a time. (A
@@ -762,6 +800,92 @@ __device__ __forceinline__ void fedopt_strip(const OptBuffers& b, const OptScala
         return;
     } else {
         opt_final<PG, E, NOST, OSM>(b, s, pg, ov, i0, rem);
+    }
+}
+
+// The same lane work with a wave-coalesced element map: lane L owns elements {i0, i0+1} and
+// {i0b, i0b+1} = wave tile base + 2L and + 128 + 2L, so every 8-byte stream (old, m, v, pg, out)
+// moves one contiguous 1 KiB per wave instruction (full 128-B lines, no half-line stores) and the
+// client loads are contiguous 512-B dwordx2 wave instructions. Whole wave tiles only.
+template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM = 0>
+__device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const OptScalars& s,
+                                                   const ClientTable<typename PG::S>& tab, const int K,
+                                                   const int64_t i0, const int64_t i0b) {
+    using V = typename PG::V;
+    constexpr int E = 4, H = 2;
+    auto half = [](auto& a, int h) -> auto& {
+        using T = std::remove_reference_t<decltype(a[0])>;
+        return *reinterpret_cast<T(*)[H]>(&a[h * H]);
+    };
+    constexpr int U = kUnroll / 2;           // clients in flight (8: no faster, profiles/r02_fedopt_coal_probe.log)
+    OLD old[E];
+    strip_load<OLD, H, false>(static_cast<const OLD*>(b.old) + i0, half(old, 0));
+    strip_load<OLD, H, false>(static_cast<const OLD*>(b.old) + i0b, half(old, 1));
+    V ov[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) ov[e] = widen<OLD, V>(old[e]);
+    V pg[E];
+    int k = 0;
+    if constexpr (FIRST) {
+        Y y[E];
+        const Y* yp = static_cast<const Y*>(tab.ptr[0]);
+        strip_load<Y, H, NT>(yp + i0, half(y, 0));
+        strip_load<Y, H, NT>(yp + i0b, half(y, 1));
+#pragma unroll
+        for (int e = 0; e < E; ++e) pg[e] = widen<Y, V>(y[e]) - ov[e];
+        k = 1;
+    } else {
+        strip_load<V, H, false>(static_cast<const V*>(b.pg) + i0, half(pg, 0));
+        strip_load<V, H, false>(static_cast<const V*>(b.pg) + i0b, half(pg, 1));
+    }
+    for (; k + U <= K; k += U) {
+        Y y[U][E];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const Y* yp = static_cast<const Y*>(tab.ptr[k + u]);
+            strip_load<Y, H, NT>(yp + i0, half(y[u], 0));
+            strip_load<Y, H, NT>(yp + i0b, half(y[u], 1));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            V d[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) d[e] = widen<Y, V>(y[u][e]) - ov[e];
+            fold_strip<PG, E>(pg, d, tab.n[k + u], tab.N[k + u], tab.r[k + u]);
+        }
+    }
+    for (; k < K; ++k) {
+        const Y* yp = static_cast<const Y*>(tab.ptr[k]);
+        Y y[E];
+        strip_load<Y, H, NT>(yp + i0, half(y, 0));
+        strip_load<Y, H, NT>(yp + i0b, half(y, 1));
+        V d[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) d[e] = widen<Y, V>(y[e]) - ov[e];
+        fold_strip<PG, E>(pg, d, tab.n[k], tab.N[k], tab.r[k]);
+    }
+    if constexpr (!FINAL) {
+        strip_store<V, H>(static_cast<V*>(b.pg) + i0, half(pg, 0));
+        strip_store<V, H>(static_cast<V*>(b.pg) + i0b, half(pg, 1));
+    } else {
+        double mi[E], vv[E];
+        opt_load_state<H>(b, s, i0, H, half(mi, 0), half(vv, 0));
+        opt_load_state<H>(b, s, i0b, H, half(mi, 1), half(vv, 1));
+        opt_apply<PG, H, false, OSM>(b, s, half(pg, 0), half(ov, 0), half(mi, 0), half(vv, 0), i0, H);
+        opt_apply<PG, H, false, OSM>(b, s, half(pg, 1), half(ov, 1), half(mi, 1), half(vv, 1), i0b, H);
+    }
+}
+
+template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM = 0>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_c(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
+    const int64_t base = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 256;   // this wave's tile
+    const int lane = threadIdx.x & 63;
+    if (base + 256 <= P) {
+        fedopt_strip_split<Y, OLD, PG, FIRST, FINAL, NT, OSM>(b, s, tab, K, base + 2 * lane, base + 128 + 2 * lane);
+    } else {
+        const int64_t i0 = base + 4 * lane;          // the ragged last tile: the per-lane strip map
+        if (i0 < P) fedopt_strip<Y, OLD, PG, 4, FIRST, FINAL, NT, false, OSM>(b, s, tab, K, P, i0);
     }
 }
 
@@ -960,7 +1084,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{1};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -1150,19 +1274,29 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
         hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, true>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
         return check_launch("fa_fedopt_step: kernel launch");
     }
-    if (first && final_ && g_cfg.opt_store == 1) {
-        hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, false, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
-        return check_launch("fa_fedopt_step: kernel launch");
-    }
-    if (first && final_ && g_cfg.opt_store == 2) {
-        hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, false, 2>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+    if (first && final_ && !g_cfg.opt_coal) {    // the per-lane 4-element strip map (r01), for A/B
+        if (g_cfg.opt_store == 1)
+            hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, false, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        else if (g_cfg.opt_store == 2)
+            hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, false, 2>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        else
+            hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
         return check_launch("fa_fedopt_step: kernel launch");
     }
 #endif
-    if (first && final_) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
-    else if (first) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, false, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
-    else if (final_) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, false, true, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
-    else hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, false, false, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+    if constexpr (E == 4) {
+        // wave-coalesced element map + non-temporal state / model stores: +3-4 % over the per-lane
+        // strip map on configs[3], bit-identical (profiles/r02_fedopt_coal_probe.log)
+        if (first && final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        else if (first) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, false, NT, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        else if (final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, false, true, NT, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        else hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, false, false, NT, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+    } else {
+        if (first && final_) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        else if (first) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, false, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        else if (final_) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, false, true, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        else hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, false, false, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+    }
     return check_launch("fa_fedopt_step: kernel launch");
 }
 
@@ -1534,6 +1668,9 @@ int fa_tune(int knob, int value) {
             return FA_OK;
         case FA_TUNE_OPT_NOSTORE:
             g_cfg.opt_nostore = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_OPT_COAL:
+            g_cfg.opt_coal = value ? 1 : 0;
             return FA_OK;
         case FA_TUNE_OPT_STORE:
             if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: FedOpt store mode 0 (plain), 1 (nt) or 2 (sc1)");

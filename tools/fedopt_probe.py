@@ -44,12 +44,13 @@ def main():
         "steady": (lambda: ops.fedopt_step(old64, ups, ns, Ns, first=True, final=True, m_in=m64, m_out=m_o, v_in=v64,
                                            v_out=v_o, out=o2), P * (4 * K + 48)),
     }
-    settings = [(1, 0, 0), (1, 0, 1), (1, 0, 2), (1, 1, 0)]
+    # (client loads nt, nostore, store mode of the strip map, coalesced map (product), unused)
+    settings = [(1, 0, 0, 0, 0), (1, 0, 1, 0, 0), (1, 0, 0, 1, 0), (0, 0, 0, 1, 0), (1, 1, 0, 0, 0)]
     res = {}
     for rep in range(a.reps):
         for name, (fn, b) in phases.items():
-            for nt, nost, sm in settings:
-                ops.tune(opt_nt=nt, opt_nostore=nost, opt_store=sm)
+            for nt, nost, sm, coal, snt in settings:
+                ops.tune(opt_nt=nt, opt_nostore=nost, opt_store=sm, opt_coal=coal)
                 fn()
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
                 for s_, e_ in ev:
@@ -58,12 +59,23 @@ def main():
                     e_.record()
                 torch.cuda.synchronize()
                 ms = sorted(s_.elapsed_time(e_) for s_, e_ in ev)[2]
-                res.setdefault((name, nt, nost, sm), []).append(ms)
-    ops.tune(opt_nt=1, opt_nostore=0, opt_store=0)
-    for (name, nt, nost, sm), mss in res.items():
+                if coal:                     # the coalesced map must give the same bits
+                    ref_fn = {"round1": out, "steady": o2}[name]
+                    keep = ref_fn.clone()
+                    ops.tune(opt_coal=0)
+                    fn()
+                    same = bool(torch.equal(keep.view(torch.int64), ref_fn.view(torch.int64)))
+                    res.setdefault(("same", name, coal, snt), []).append(same)
+                res.setdefault((name, nt, nost, sm, coal, snt), []).append(ms)
+    ops.tune(opt_nt=1, opt_nostore=0, opt_store=0, opt_coal=1)
+    for key, mss in res.items():
+        if key[0] == "same":
+            print(json.dumps({"bit_identical": key[1:], "all": all(mss)}))
+            continue
+        name, nt, nost, sm, coal, snt = key
         ms = float(np.median(mss))
         b = phases[name][1]
-        print(json.dumps({"phase": name, "opt_nt": nt, "nostore": nost, "store_mode": sm, "ms": ms, "GBps_alg": b / ms / 1e6,
+        print(json.dumps({"phase": name, "opt_nt": nt, "nostore": nost, "store_mode": sm, "coal": coal, "state_nt": snt, "ms": ms, "GBps_alg": b / ms / 1e6,
                           "frac": b / ms / 1e6 / PEAK, "reps": mss}), flush=True)
 
 
