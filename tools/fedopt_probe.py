@@ -38,11 +38,19 @@ def main():
     m_o = torch.empty(P, dtype=torch.float64, device=dev)
     v_o = torch.empty(P, dtype=torch.float64, device=dev)
     o2 = torch.empty(P, dtype=torch.float64, device=dev)
+    m64b, v64b, old64b = m64.clone(), v64.clone(), old64.clone()
     phases = {
         "round1": (lambda: ops.fedopt_step(old32, ups, ns, Ns, first=True, final=True, m_out=m32, v_out=v, out=out),
                    K * P * 4 + P * 24),
         "steady": (lambda: ops.fedopt_step(old64, ups, ns, Ns, first=True, final=True, m_in=m64, m_out=m_o, v_in=v64,
                                            v_out=v_o, out=o2), P * (4 * K + 48)),
+        # the production pipeline updates m / v in place (staging.FedOptPipeline.server_step); the
+        # values drift from step to step, which does not change the work
+        "steady_mv_inplace": (lambda: ops.fedopt_step(old64b, ups, ns, Ns, first=True, final=True, m_in=m64b,
+                                                      m_out=m64b, v_in=v64b, v_out=v64b, out=o2), P * (4 * K + 48)),
+        "steady_all_inplace": (lambda: ops.fedopt_step(old64b, ups, ns, Ns, first=True, final=True, m_in=m64b,
+                                                       m_out=m64b, v_in=v64b, v_out=v64b, out=old64b),
+                               P * (4 * K + 48)),
     }
     # (client loads nt, nostore, store mode of the strip map, coalesced map (product), unused)
     settings = [(1, 0, 0, 0, 0), (1, 0, 1, 0, 0), (1, 0, 0, 1, 0), (0, 0, 0, 1, 0), (1, 1, 0, 0, 0)]
@@ -59,7 +67,7 @@ def main():
                     e_.record()
                 torch.cuda.synchronize()
                 ms = sorted(s_.elapsed_time(e_) for s_, e_ in ev)[2]
-                if coal:                     # the coalesced map must give the same bits
+                if coal and name in ("round1", "steady"):   # the coalesced map must give the same bits
                     ref_fn = {"round1": out, "steady": o2}[name]
                     keep = ref_fn.clone()
                     ops.tune(opt_coal=0)
