@@ -803,24 +803,25 @@ __device__ __forceinline__ void fedopt_strip(const OptBuffers& b, const OptScala
     }
 }
 
-// The same lane work with a wave-coalesced element map: lane L owns elements {i0, i0+1} and
-// {i0b, i0b+1} = wave tile base + 2L and + 128 + 2L, so every 8-byte stream (old, m, v, pg, out)
-// moves one contiguous 1 KiB per wave instruction (full 128-B lines, no half-line stores) and the
-// client loads are contiguous 512-B dwordx2 wave instructions. Whole wave tiles only.
-template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM = 0>
+// The same lane work with a wave-coalesced element map: lane L of a wave tile of 128*NH elements
+// owns the pairs {2L, 2L+1} + 128 j, j < NH, so every 8-byte stream (old, m, v, pg, out) moves one
+// contiguous 1 KiB per wave instruction (full 128-B lines, no half-line stores) and the client loads
+// are contiguous 512-B dwordx2 wave instructions. Whole wave tiles only.
+template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM = 0, int NH = 2,
+          int U = kUnroll / 2>
 __device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const OptScalars& s,
                                                    const ClientTable<typename PG::S>& tab, const int K,
-                                                   const int64_t i0, const int64_t i0b) {
+                                                   const int64_t i0) {
     using V = typename PG::V;
-    constexpr int E = 4, H = 2;
+    constexpr int H = 2, E = H * NH;
     auto half = [](auto& a, int h) -> auto& {
         using T = std::remove_reference_t<decltype(a[0])>;
         return *reinterpret_cast<T(*)[H]>(&a[h * H]);
     };
-    constexpr int U = kUnroll / 2;           // clients in flight (8: no faster, profiles/r02_fedopt_coal_probe.log)
+    auto at = [i0](int h) { return i0 + (int64_t)h * 128; };
     OLD old[E];
-    strip_load<OLD, H, false>(static_cast<const OLD*>(b.old) + i0, half(old, 0));
-    strip_load<OLD, H, false>(static_cast<const OLD*>(b.old) + i0b, half(old, 1));
+#pragma unroll
+    for (int h = 0; h < NH; ++h) strip_load<OLD, H, false>(static_cast<const OLD*>(b.old) + at(h), half(old, h));
     V ov[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) ov[e] = widen<OLD, V>(old[e]);
@@ -829,22 +830,22 @@ __device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const Op
     if constexpr (FIRST) {
         Y y[E];
         const Y* yp = static_cast<const Y*>(tab.ptr[0]);
-        strip_load<Y, H, NT>(yp + i0, half(y, 0));
-        strip_load<Y, H, NT>(yp + i0b, half(y, 1));
+#pragma unroll
+        for (int h = 0; h < NH; ++h) strip_load<Y, H, NT>(yp + at(h), half(y, h));
 #pragma unroll
         for (int e = 0; e < E; ++e) pg[e] = widen<Y, V>(y[e]) - ov[e];
         k = 1;
     } else {
-        strip_load<V, H, false>(static_cast<const V*>(b.pg) + i0, half(pg, 0));
-        strip_load<V, H, false>(static_cast<const V*>(b.pg) + i0b, half(pg, 1));
+#pragma unroll
+        for (int h = 0; h < NH; ++h) strip_load<V, H, false>(static_cast<const V*>(b.pg) + at(h), half(pg, h));
     }
     for (; k + U <= K; k += U) {
         Y y[U][E];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const Y* yp = static_cast<const Y*>(tab.ptr[k + u]);
-            strip_load<Y, H, NT>(yp + i0, half(y[u], 0));
-            strip_load<Y, H, NT>(yp + i0b, half(y[u], 1));
+#pragma unroll
+            for (int h = 0; h < NH; ++h) strip_load<Y, H, NT>(yp + at(h), half(y[u], h));
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -857,35 +858,41 @@ __device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const Op
     for (; k < K; ++k) {
         const Y* yp = static_cast<const Y*>(tab.ptr[k]);
         Y y[E];
-        strip_load<Y, H, NT>(yp + i0, half(y, 0));
-        strip_load<Y, H, NT>(yp + i0b, half(y, 1));
+#pragma unroll
+        for (int h = 0; h < NH; ++h) strip_load<Y, H, NT>(yp + at(h), half(y, h));
         V d[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) d[e] = widen<Y, V>(y[e]) - ov[e];
         fold_strip<PG, E>(pg, d, tab.n[k], tab.N[k], tab.r[k]);
     }
     if constexpr (!FINAL) {
-        strip_store<V, H>(static_cast<V*>(b.pg) + i0, half(pg, 0));
-        strip_store<V, H>(static_cast<V*>(b.pg) + i0b, half(pg, 1));
+#pragma unroll
+        for (int h = 0; h < NH; ++h) strip_store<V, H>(static_cast<V*>(b.pg) + at(h), half(pg, h));
     } else {
         double mi[E], vv[E];
-        opt_load_state<H>(b, s, i0, H, half(mi, 0), half(vv, 0));
-        opt_load_state<H>(b, s, i0b, H, half(mi, 1), half(vv, 1));
-        opt_apply<PG, H, false, OSM>(b, s, half(pg, 0), half(ov, 0), half(mi, 0), half(vv, 0), i0, H);
-        opt_apply<PG, H, false, OSM>(b, s, half(pg, 1), half(ov, 1), half(mi, 1), half(vv, 1), i0b, H);
+#pragma unroll
+        for (int h = 0; h < NH; ++h) opt_load_state<H>(b, s, at(h), H, half(mi, h), half(vv, h));
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+            opt_apply<PG, H, false, OSM>(b, s, half(pg, h), half(ov, h), half(mi, h), half(vv, h), at(h), H);
     }
 }
 
-template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM = 0>
+template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM = 0, int NH = 2,
+          int U = kUnroll / 2>
 __global__ void __launch_bounds__(kBlock)
 k_fedopt_c(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
-    const int64_t base = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 256;   // this wave's tile
+    constexpr int64_t T = 128 * NH;                                     // elements per wave tile
+    const int64_t base = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * T;
     const int lane = threadIdx.x & 63;
-    if (base + 256 <= P) {
-        fedopt_strip_split<Y, OLD, PG, FIRST, FINAL, NT, OSM>(b, s, tab, K, base + 2 * lane, base + 128 + 2 * lane);
-    } else {
-        const int64_t i0 = base + 4 * lane;          // the ragged last tile: the per-lane strip map
-        if (i0 < P) fedopt_strip<Y, OLD, PG, 4, FIRST, FINAL, NT, false, OSM>(b, s, tab, K, P, i0);
+    if (base + T <= P) {
+        fedopt_strip_split<Y, OLD, PG, FIRST, FINAL, NT, OSM, NH, U>(b, s, tab, K, base + 2 * lane);
+    } else {                                      // the ragged last tile: the per-lane strip map
+#pragma unroll
+        for (int j = 0; j < NH / 2; ++j) {
+            const int64_t i0 = base + j * 256 + 4 * lane;
+            if (i0 < P) fedopt_strip<Y, OLD, PG, 4, FIRST, FINAL, NT, false, OSM>(b, s, tab, K, P, i0);
+        }
     }
 }
 
@@ -1084,7 +1091,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{1};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -1274,6 +1281,12 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
         hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, true>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
         return check_launch("fa_fedopt_step: kernel launch");
     }
+    if constexpr (E == 4) {
+        if (first && final_ && g_cfg.opt_coal == 1) {   // 2 pairs per lane (a 256-element wave tile)
+            hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1, 2>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+            return check_launch("fa_fedopt_step: kernel launch");
+        }
+    }
     if (first && final_ && !g_cfg.opt_coal) {    // the per-lane 4-element strip map (r01), for A/B
         if (g_cfg.opt_store == 1)
             hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, false, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
@@ -1285,12 +1298,14 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
     }
 #endif
     if constexpr (E == 4) {
-        // wave-coalesced element map + non-temporal state / model stores: +3-4 % over the per-lane
-        // strip map on configs[3], bit-identical (profiles/r02_fedopt_coal_probe.log)
-        if (first && final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
-        else if (first) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, false, NT, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
-        else if (final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, false, true, NT, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
-        else hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, false, false, NT, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        // wave-coalesced element map, 4 pairs per lane (512-element wave tiles), non-temporal state /
+        // model stores: +3-6 % over the per-lane strip map on configs[3], bit-identical
+        // (profiles/r02_fedopt_coal_*.log)
+        const dim3 g4((unsigned)((P + 4 * 512 - 1) / (4 * 512)));
+        if (first && final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        else if (first) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, false, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        else if (final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, false, true, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+        else hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, false, false, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
     } else {
         if (first && final_) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
         else if (first) hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, false, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
@@ -1670,7 +1685,9 @@ int fa_tune(int knob, int value) {
             g_cfg.opt_nostore = value ? 1 : 0;
             return FA_OK;
         case FA_TUNE_OPT_COAL:
-            g_cfg.opt_coal = value ? 1 : 0;
+            if (value < 0 || value > 2)
+                return fail(FA_EINVAL, "fa_tune: FedOpt map 0 (strip), 1 (coalesced, 2 pairs/lane), 2 (4 pairs/lane: product)");
+            g_cfg.opt_coal = value;
             return FA_OK;
         case FA_TUNE_OPT_STORE:
             if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: FedOpt store mode 0 (plain), 1 (nt) or 2 (sc1)");

@@ -53,8 +53,9 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                     FA_TUNE_OPT_NT = 12 /* FedOpt client loads non-temporal (1, product) or cached (0) */,
                     FA_TUNE_OPT_NOSTORE = 13 /* FedOpt FIRST|FINAL launch: 1 = skip the stores (reads + math) */,
                     FA_TUNE_OPT_STORE = 14 /* FedOpt FIRST|FINAL, strip map (OPT_COAL 0): stores 0 plain, 1 nt, 2 sc1 */,
-                    FA_TUNE_OPT_COAL = 15 /* FedOpt FIRST|FINAL: 1 = the product's wave-coalesced map (k_fedopt_c,
-                                             nt stores), 0 = the r01 per-lane 4-element strip map */ };
+                    FA_TUNE_OPT_COAL = 15 /* FedOpt FIRST|FINAL element map: 2 = the product's (k_fedopt_c, 4
+                                             coalesced pairs per lane, nt stores), 1 = 2 pairs per lane,
+                                             0 = the r01 per-lane 4-element strip map */ };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);
