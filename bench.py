@@ -25,7 +25,7 @@ Also measured in the same run:
   roofline      algorithmic bytes of the fold (K*P*4 + P*4 per launch at N = 1; per rank and
                 step at N > 1) / its kernel time (HIP events on the launch stream) vs the
                 8.0 TB/s HBM3E peak; ``traffic`` = HBM bytes per launch from rocprofv3 PMC
-                counters (profiles/pmc_traffic.json, collected by tools/pmc_collect.sh) when
+                counters (profiles/pmc_traffic.json, collected by tools/gpu_session.sh pmc + tools/pmc_traffic.py --session) when
                 that entry was measured on the current kernel source (sha256 of fedagg.hip),
                 else null with the reason
   cpu_baseline  the numpy restatement of numpyhelper.increment_average (oracle/, bit-equal to
@@ -95,7 +95,7 @@ def kernel_sha():
 
 
 def pmc_traffic(workload):
-    """(HBM bytes per launch, provenance) from rocprofv3 PMC runs (tools/pmc_collect.sh) — only if
+    """(HBM bytes per launch, provenance) from rocprofv3 PMC runs (tools/gpu_session.sh pmc) — only if
     that entry was collected on the current kernel source; else (None, reason)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -108,7 +108,7 @@ def pmc_traffic(workload):
     src = {"file": "profiles/pmc_traffic.json", "workload": workload, "kernel_src_sha": ent.get("kernel_src_sha"),
            "collected": ent.get("collected"), "read_bytes": ent.get("read_bytes"), "write_bytes": ent.get("write_bytes")}
     if ent.get("kernel_src_sha") != kernel_sha():
-        src["note"] = "stale: collected on another revision of fedagg.hip; re-run tools/pmc_collect.sh"
+        src["note"] = "stale: collected on another revision of fedagg.hip; re-run tools/gpu_session.sh pmc + tools/pmc_traffic.py --session"
         return None, src
     return ent["bytes"], src
 
@@ -222,7 +222,7 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000):
         res[phase] = {"ms": ms, "params_per_s": K * P / (ms / 1e3),
                       "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-                                   "kernel": "k_fedopt (pseudo-gradient fold + Adam step fused)",
+                                   "kernel": "k_fedopt_c (pseudo-gradient fold + Adam step fused; 4 coalesced element pairs per lane)",
                                    "alg_bytes_per_launch": b},
                       "bit_exact_on_sample": ok, "sample": f"first {S} params of every buffer vs oracle/numpy_ref"}
     res["config"] = (f"BASELINE configs[3]: FedAdam, {K} device-resident fp32 updates x {P} params, m / v in HBM "
@@ -276,7 +276,8 @@ def main():
         elapsed, kern_ms = timed_steps(step, a.steps, stream, world, device, rehearsal)
         alg_bytes = K * P * in_bytes + P * 4           # read every update once, write the aggregate once
         workload = f"fedavg_k{K}_p{P}_{a.dtype}"
-        kernel = "k_fedavg_pipe (fp32, 4 x 16-B strips per lane, next client prefetched)"
+        kernel = ("k_fedavg_pipe (fp32, 4 x 16-B strips per lane, next client prefetched)" if a.dtype == "f32" else
+                  "k_fedavg_pipe (bf16 -> f32, 8 strips of 4 elements per lane, next client prefetched)")
         config = {"workload": f"FedAvg {K} clients x {P} params {a.dtype} per GPU (BASELINE configs[1]/north "
                               "star; device-resident, one fused fold launch per aggregation)",
                   "clients": K, "params_per_gpu": P, "global_params": P_total,

@@ -1091,7 +1091,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -1201,6 +1201,10 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
         const int lanetab = g_cfg.lanetab, nt_store = g_cfg.nt_store, tilemap = g_cfg.tilemap;
         const int key = (block_log == 9 ? 20000 : block_log == 10 ? 30000 : 0) + lanetab * 10000 + strips * 100 +
                         unroll * 2 + nt;
+        if constexpr (sizeof(Y) < sizeof(X) && E % 2 == 0) {
+            if (g_cfg.narrow && key == 4 * 100 + 0 && nt_store == 1 && tilemap == 0)
+                return launch_fedavg_pipe<Y, X, CP, E / 2, 8, false, false, kBlock, 1>(a, tab, cnt, P, first, int_first, st);
+        }
         switch (key) {
 #define FA_GEOM(S_, U_, NT_) \
     case S_ * 100 + U_ * 2 + NT_: return launch_fedavg_geom<Y, X, CP, E, S_, U_, NT_>(a, tab, cnt, P, first, int_first, st);
@@ -1235,8 +1239,13 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
         }
 #else
         // measured best on MI355X (profiles/r01_microbench.md): 4 x 16-B strips per lane, the next
-        // client's strips in flight (pipelined), cached loads, non-temporal aggregate stores
-        return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 1>(a, tab, cnt, P, first, int_first, st);
+        // client's strips in flight (pipelined), cached loads, non-temporal aggregate stores.
+        // bf16 clients: strips of 4 elements (8-B loads, 16-B f32 stores), 8 per lane, so every wave
+        // store is one contiguous 1 KiB — +3.5 % at K = 64, +7 % at K = 8 (profiles/r02_narrow_probe.log)
+        if constexpr (sizeof(Y) < sizeof(X) && E % 2 == 0)
+            return launch_fedavg_pipe<Y, X, CP, E / 2, 8, false, false, kBlock, 1>(a, tab, cnt, P, first, int_first, st);
+        else
+            return launch_fedavg_pipe<Y, X, CP, E, 4, false, false, kBlock, 1>(a, tab, cnt, P, first, int_first, st);
 #endif
     }
     launch_fedavg_geom<Y, X, CP, E, 1, kUnroll, false>(a, tab, cnt, P, first, int_first, st);
@@ -1692,6 +1701,9 @@ int fa_tune(int knob, int value) {
         case FA_TUNE_OPT_STORE:
             if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: FedOpt store mode 0 (plain), 1 (nt) or 2 (sc1)");
             g_cfg.opt_store = value;
+            return FA_OK;
+        case FA_TUNE_NARROW:
+            g_cfg.narrow = value ? 1 : 0;
             return FA_OK;
         default:
             return fail(FA_EINVAL, "fa_tune: unknown knob %d", knob);

@@ -55,7 +55,11 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                     FA_TUNE_OPT_STORE = 14 /* FedOpt FIRST|FINAL, strip map (OPT_COAL 0): stores 0 plain, 1 nt, 2 sc1 */,
                     FA_TUNE_OPT_COAL = 15 /* FedOpt FIRST|FINAL element map: 2 = the product's (k_fedopt_c, 4
                                              coalesced pairs per lane, nt stores), 1 = 2 pairs per lane,
-                                             0 = the r01 per-lane 4-element strip map */ };
+                                             0 = the r01 per-lane 4-element strip map */,
+                    FA_TUNE_NARROW = 16 /* bf16 -> f32 FedAvg: 1 = the product's 8-B client strips / 16-B
+                                           aggregate strips (4 elements, 8 strips per lane: every wave store
+                                           one contiguous 1 KiB), 0 = r01's 16-B client strips (8 elements,
+                                           4 per lane) */ };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);

@@ -1157,3 +1157,66 @@ def test_fedopt_bf16_waves_two_rounds(ndev):
         assert_lists_identical([wf.gather(wf.m).numpy()], state.m, f"round {r} m")
         assert_lists_identical([wf.gather(wf.v).numpy()], state.v, f"round {r} v")
         old_np = want[0]
+
+
+# ------------------------------------------------------------------------- N > 1 with the HIP kernel
+def _hip_gloo_worker(rank, world, port, P, K, q):
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+
+    from fedn_amd.sharded import CyclicShardedFedAvg, ShardedFedAvg
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        g = torch.Generator(device="cuda:0").manual_seed(3)
+        base = torch.randn(P, generator=g, device="cuda:0")
+        ups = [torch.randn(P, generator=g, device="cuda:0").mul_(0.01).add_(base) for _ in range(K)]
+        ns = [int(v) for v in np.random.default_rng(3).integers(1, 5001, K)]
+        Ns = [int(v) for v in np.cumsum(ns)]
+        sh = ShardedFedAvg(P)                                     # default fold: the libfedagg kernel
+        agg = torch.empty(sh.hi - sh.lo, device="cuda:0")
+        sh.fold(agg, [sh.local(u) for u in ups], ns, Ns, init=True)
+        host = sh.gather_to_host(agg)
+        cs = CyclicShardedFedAvg(P, chunk=8192)
+        aggc = torch.empty(cs.local_len, device="cuda:0")
+        full = cs.fold_allgather(aggc, [cs.local(u) for u in ups], ns, Ns, init=True)
+        torch.cuda.synchronize()
+        q.put((rank, None if host is None else host.numpy().copy(), full.cpu().numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_gloo_world2_hip_kernel():
+    """The N > 1 exchange logic (parameter slices + gather to host, and the block-cyclic fold with the
+    all-gather of each round) with the HIP kernel doing every fold: 2 gloo ranks on this box's GPU,
+    bit-identical to one single-device fold (RCCL refuses two ranks on one GPU)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from fedn_amd import ops
+    P, K, world = 200_003, 7, 2
+    s_ = socket.socket()
+    s_.bind(("127.0.0.1", 0))
+    port = s_.getsockname()[1]
+    s_.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pc = mp.start_processes(_hip_gloo_worker, args=(world, port, P, K, q), nprocs=world, join=False,
+                            start_method="spawn")
+    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    while not pc.join(timeout=60):
+        pass
+    g = torch.Generator(device=DEV).manual_seed(3)
+    base = torch.randn(P, generator=g, device=DEV)
+    ups = [torch.randn(P, generator=g, device=DEV).mul_(0.01).add_(base) for _ in range(K)]
+    ns = [int(v) for v in np.random.default_rng(3).integers(1, 5001, K)]
+    want = torch.empty(P, device=DEV)
+    ops.fedavg_fold(want, ups, ns, [int(v) for v in np.cumsum(ns)], init=True)
+    want = want.cpu().numpy()
+    assert np.array_equal(res[0][1].view(np.uint32), want.view(np.uint32))
+    for rank, _, full in res:
+        assert np.array_equal(full.view(np.uint32), want.view(np.uint32)), f"rank {rank}"
