@@ -521,10 +521,10 @@ __device__ __forceinline__ int64_t map_tile(int64_t t, int64_t ntiles) {
     return t;
 }
 
-template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK = kBlock,
-          int NTS = 0, int MAP = 0>
-__global__ void __launch_bounds__(BLK)
-k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P) {
+template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK, int NTS,
+          int MAP>
+__device__ __forceinline__ void fedavg_pipe_body(X* __restrict__ agg, const ClientTable<typename CP::S>& tab, const int K,
+                                                 const int64_t P) {
     using V = typename CP::V;
     const LaneTable<CP> lt(tab);
     const int64_t ntiles = ((P + E - 1) / E + (int64_t)BLK * S - 1) / ((int64_t)BLK * S);
@@ -581,6 +581,23 @@ k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const 
         }
     }
 }
+
+template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK = kBlock,
+          int NTS = 0, int MAP = 0>
+__global__ void __launch_bounds__(BLK)
+k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P) {
+    fedavg_pipe_body<Y, X, CP, E, S, INIT, INT_FIRST, NT, LT, BLK, NTS, MAP>(agg, tab, K, P);
+}
+
+#ifdef FEDAGG_PROBES
+// occupancy probe (FA_TUNE_WPE): the same body compiled for at least W waves per SIMD
+template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK, int NTS,
+          int MAP, int W>
+__global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(W)))
+k_fedavg_pipe_w(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P) {
+    fedavg_pipe_body<Y, X, CP, E, S, INIT, INT_FIRST, NT, LT, BLK, NTS, MAP>(agg, tab, K, P);
+}
+#endif
 
 // ----------------------------------------------------------------------------
 // FedOpt kernel: pseudo-gradient fold + server step, fused
@@ -878,10 +895,9 @@ __device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const Op
     }
 }
 
-template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM = 0, int NH = 2,
-          int U = kUnroll / 2>
-__global__ void __launch_bounds__(kBlock)
-k_fedopt_c(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
+template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM, int NH, int U>
+__device__ __forceinline__ void fedopt_c_body(const OptBuffers& b, const OptScalars& s, const ClientTable<typename PG::S>& tab,
+                                              const int K, const int64_t P) {
     constexpr int64_t T = 128 * NH;                                     // elements per wave tile
     const int64_t base = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * T;
     const int lane = threadIdx.x & 63;
@@ -895,6 +911,21 @@ k_fedopt_c(const OptBuffers b, const OptScalars s, const ClientTable<typename PG
         }
     }
 }
+
+template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM = 0, int NH = 2,
+          int U = kUnroll / 2>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_c(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
+    fedopt_c_body<Y, OLD, PG, FIRST, FINAL, NT, OSM, NH, U>(b, s, tab, K, P);
+}
+
+#ifdef FEDAGG_PROBES
+template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM, int NH, int U, int W>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W)))
+k_fedopt_c_w(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
+    fedopt_c_body<Y, OLD, PG, FIRST, FINAL, NT, OSM, NH, U>(b, s, tab, K, P);
+}
+#endif
 
 template <typename Y, typename OLD, class PG, int E, bool FIRST, bool FINAL, bool NT, bool NOST = false, int OSM = 0>
 __global__ void __launch_bounds__(kBlock)
@@ -1091,7 +1122,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -1158,13 +1189,30 @@ void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, i
         ntiles = std::min<int64_t>(ntiles, (int64_t)cfg_grid_per_cu() * device_cus());
     }
     const dim3 grid((unsigned)ntiles);
+    unsigned shm = 0;
+#ifdef FEDAGG_PROBES
+    shm = (unsigned)g_cfg.lds_kib * 1024u;     // occupancy probe: LDS the kernel never touches
+    if constexpr (std::is_same<X, float>::value && S * E * (int)sizeof(Y) == 64 && BLK == kBlock && MAP == 0 && !LT && !NT) {
+        const int w = g_cfg.wpe;
+        if (w > 0 && !int_first) {
+#define FA_WPE(W_)                                                                                                      \
+    if (w == W_) {                                                                                                      \
+        if (first) hipLaunchKernelGGL((k_fedavg_pipe_w<Y, X, CP, E, S, true, false, NT, LT, BLK, NTS, MAP, W_>), grid, dim3(BLK), shm, st, a, tab, cnt, P); \
+        else hipLaunchKernelGGL((k_fedavg_pipe_w<Y, X, CP, E, S, false, false, NT, LT, BLK, NTS, MAP, W_>), grid, dim3(BLK), shm, st, a, tab, cnt, P); \
+        return;                                                                                                         \
+    }
+            FA_WPE(5) FA_WPE(6) FA_WPE(8)
+#undef FA_WPE
+        }
+    }
+#endif
     if (first && int_first) {
         if constexpr (std::is_integral<Y>::value)
-            hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, true, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
+            hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, true, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), shm, st, a, tab, cnt, P);
     } else if (first)
-        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
+        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, true, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), shm, st, a, tab, cnt, P);
     else
-        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, false, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), 0, st, a, tab, cnt, P);
+        hipLaunchKernelGGL((k_fedavg_pipe<Y, X, CP, E, S, false, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), shm, st, a, tab, cnt, P);
 }
 
 template <typename Y, typename X, class CP, int E, int S, int U, bool NT>
@@ -1311,6 +1359,21 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
         // model stores: +3-6 % over the per-lane strip map on configs[3], bit-identical
         // (profiles/r02_fedopt_coal_*.log)
         const dim3 g4((unsigned)((P + 4 * 512 - 1) / (4 * 512)));
+#ifdef FEDAGG_PROBES
+        const unsigned shm = (unsigned)g_cfg.lds_kib * 1024u;
+        if (first && final_) {
+            switch (g_cfg.wpe) {
+#define FA_WPE(W_) \
+    case W_: hipLaunchKernelGGL((k_fedopt_c_w<Y, OLD, PG, true, true, NT, 1, 4, kUnroll / 2, W_>), g4, dim3(kBlock), shm, st, b, s, tab, cnt, P); \
+        return check_launch("fa_fedopt_step: kernel launch");
+                FA_WPE(6) FA_WPE(8)
+#undef FA_WPE
+                default:
+                    hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1, 4>), g4, dim3(kBlock), shm, st, b, s, tab, cnt, P);
+                    return check_launch("fa_fedopt_step: kernel launch");
+            }
+        }
+#endif
         if (first && final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
         else if (first) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, false, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
         else if (final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, false, true, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
@@ -1704,6 +1767,15 @@ int fa_tune(int knob, int value) {
             return FA_OK;
         case FA_TUNE_NARROW:
             g_cfg.narrow = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_LDS:
+            if (value < 0 || value > 64) return fail(FA_EINVAL, "fa_tune: occupancy-probe LDS 0..64 KiB per workgroup");
+            g_cfg.lds_kib = value;
+            return FA_OK;
+        case FA_TUNE_WPE:
+            if (value != 0 && value != 5 && value != 6 && value != 8)
+                return fail(FA_EINVAL, "fa_tune: waves per SIMD 0 (compiler's choice), 5, 6 or 8");
+            g_cfg.wpe = value;
             return FA_OK;
         default:
             return fail(FA_EINVAL, "fa_tune: unknown knob %d", knob);

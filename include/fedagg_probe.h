@@ -59,7 +59,11 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                     FA_TUNE_NARROW = 16 /* bf16 -> f32 FedAvg: 1 = the product's 8-B client strips / 16-B
                                            aggregate strips (4 elements, 8 strips per lane: every wave store
                                            one contiguous 1 KiB), 0 = r01's 16-B client strips (8 elements,
-                                           4 per lane) */ };
+                                           4 per lane) */,
+                    FA_TUNE_LDS = 17 /* occupancy probe: KiB of (unused) dynamic LDS per workgroup of the fold
+                                        and FedOpt kernels, 0..64 */,
+                    FA_TUNE_WPE = 18 /* occupancy probe: fp32 fold / FedOpt FIRST|FINAL kernels compiled for at
+                                        least W waves per SIMD (0 = compiler's choice, 5, 6, 8) */ };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);
