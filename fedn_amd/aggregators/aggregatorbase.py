@@ -56,7 +56,7 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None):
     deflate stream per tensor (one core per update). Here queued updates are dequeued and
     decoded concurrently while earlier ones fold, so the fold waits for at most one decode:
     up to ``ahead`` updates, and — once the first decoded update shows the model's size — no
-    more than ``ahead_bytes`` of decoded updates (one at least). A handler that stages updates
+    more than ``ahead_bytes`` of decoded updates (one at least), counting the one being folded. A handler that stages updates
     on arrival (ingest.StagingUpdateHandler) is drained one by one: its loads are already done.
 
     Lossless: if the caller stops early (an exception that escapes its per-update handling,
@@ -84,8 +84,9 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None):
             return 1
         return max(1, min(ahead, ahead_bytes // max(1, size[0])))
 
-    def fill():
-        while len(window) < allowed() and not q.empty():
+    def fill(held=0):
+        # ``held``: an update handed out and still being folded keeps its decoded arrays
+        while len(window) + held < allowed() and not q.empty():
             try:
                 mu = update_handler.next_model_update()
             except Exception as e:  # noqa: BLE001
@@ -105,7 +106,7 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None):
         fill()
         while window:
             mu, fut, err = window.popleft()
-            fill()
+            fill(held=1)
             yield mu, (_raiser(err) if err is not None else sized(fut))
             fill()
     finally:
