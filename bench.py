@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32")
     ap.add_argument("--cpu-sample", type=int, default=100_000_000,
                     help="params per client in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--ag-rounds", type=int, default=4, help="N > 1: rounds of the overlapped fold + all-gather")
+    ap.add_argument("--ag-rounds", type=int, default=8, help="N > 1: rounds of the overlapped fold + all-gather")
     ap.add_argument("--fedopt-params", type=int, default=350_000_000, help="configs[3] side field (0 = skip)")
     ap.add_argument("--fedopt-clients", type=int, default=32)
     ap.add_argument("--no-side", action="store_true", help="N > 1: skip the beside-the-line measurements")
