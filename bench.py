@@ -481,6 +481,50 @@ def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, u
                 "note": f"BASELINE configs[4]: {pool} distinct pinned bf16 updates reused cyclically (every one "
                         "crosses PCIe); PCIe-bound by design; not in value"}
 
+    def fedopt_sharded():
+        """BASELINE configs[3] on N GPUs: the same FedAdam model (P params, K fp32 updates) sliced over
+        the ranks (sharded.ShardedFedOpt's bounds); each rank keeps its slices of the updates, old, m
+        and v resident and runs the fused steady-state step on them — no collective (FedOpt state
+        never moves); then each rank D2H's its fp64 slice of the new model (FEDn's consumer)."""
+        from fedn_amd.sharded import shard_bounds
+        P, Kf = a.fedopt_params, a.fedopt_clients
+        lo, hi = shard_bounds(P, world)[rank]
+        n = hi - lo
+        g = torch.Generator(device=device).manual_seed(4 + rank)
+        old32 = torch.randn(n, generator=g, device=device)
+        fups = [torch.randn(n, generator=g, device=device).mul_(0.01).add_(old32) for _ in range(Kf)]
+        fns = [int(v) for v in np.random.default_rng(4).integers(1, 5001, Kf)]
+        fNs = [int(v) for v in np.cumsum(fns)]
+        out1 = torch.empty(n, dtype=torch.float64, device=device)
+        v1 = torch.empty(n, dtype=torch.float64, device=device)
+        m1 = torch.empty(n, dtype=torch.float32, device=device)
+        ops.fedopt_step(old32, fups, fns, fNs, first=True, final=True, m_out=m1, v_out=v1, out=out1, stream=stream)
+        old64, m64 = out1, m1.double()
+        del old32, m1
+        m_o = torch.empty(n, dtype=torch.float64, device=device)
+        v_o = torch.empty(n, dtype=torch.float64, device=device)
+        o2 = torch.empty(n, dtype=torch.float64, device=device)
+        step = lambda: ops.fedopt_step(old64, fups, fns, fNs, first=True, final=True, m_in=m64, m_out=m_o,  # noqa: E731
+                                       v_in=v1, v_out=v_o, out=o2, stream=stream)
+        for _ in range(2):
+            step()
+        el, kms = timed_steps(step, 10, stream, world, device, on_cpu)
+        host = torch.empty(n, dtype=torch.float64, pin_memory=True)
+        host.copy_(o2, non_blocking=True)
+        elh, _ = timed_steps(lambda: host.copy_(o2, non_blocking=True), 5, stream, world, device, on_cpu)
+        t = el / 10
+        b = n * (4 * Kf + 48)
+        del fups, old64, m64, v1, m_o, v_o, o2, out1, host
+        torch.cuda.empty_cache()
+        return {"ms": t * 1e3, "value": Kf * P / t, "unit": "params/s", "params": P, "clients": Kf,
+                "params_per_gpu": n, "kernel_ms": kms, "frac_per_rank": b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                "gather_to_host_ms": elh / 5 * 1e3,
+                "note": "BASELINE configs[3] at N GPUs (strong: the same model sliced): FedAdam steady state, "
+                        "fp64 old / m / v resident per slice, one fused launch per rank, max over ranks; the "
+                        "fp64 model slice's D2H is timed apart; not in value"}
+
+    if a.fedopt_params > 0:
+        out["fedopt_sharded"] = side(fedopt_sharded)
     ip = side(in_process) if rank == 0 else None     # the other ranks wait (their GPUs are in use)
     fw = side(fedopt_waves) if rank == 0 and a.waves_params > 0 else None
     dist.barrier()

@@ -25,7 +25,7 @@ for s in $STEPS; do
       # the N>1 code path (strong-scaling line + side fields) with 2 ranks on this box's one GPU (gloo)
       FEDN_AMD_BENCH_ONE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --params 20000000 \
-        --clients 16 --waves-params 50000000 --waves-clients 32 > "$OUT/rehearsal.log" 2>&1; rc=$?
+        --clients 16 --fedopt-params 20000000 --waves-params 50000000 --waves-clients 32 > "$OUT/rehearsal.log" 2>&1; rc=$?
       echo "rehearsal rc=$rc"; grep -v amdgpu.ids "$OUT/rehearsal.log" | tail -3; [ $rc -eq 0 ] || exit $rc ;;
     micro)
       timeout -k 10 600 python tools/microbench.py > "$OUT/micro.log" 2>&1; rc=$?
