@@ -895,12 +895,24 @@ __device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const Op
     }
 }
 
-template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM, int NH, int U>
+template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM, int NH, int U, bool MV = false>
 __device__ __forceinline__ void fedopt_c_body(const OptBuffers& b, const OptScalars& s, const ClientTable<typename PG::S>& tab,
                                               const int K, const int64_t P) {
     constexpr int64_t T = 128 * NH;                                     // elements per wave tile
     const int64_t base = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * T;
     const int lane = threadIdx.x & 63;
+    if constexpr (MV) {
+        // layout probe (FA_TUNE_OPT_MV): fp64 m and v interleaved per wave tile in one buffer
+        // ([m of tile w | v of tile w] at 2wT), read from m_in and written to m_out; whole tiles only
+        if (base + T > P) return;
+        OptBuffers bb = b;
+        bb.m_in = static_cast<const double*>(b.m_in) + base;
+        bb.v_in = static_cast<const double*>(b.m_in) + base + T;
+        bb.m_out = static_cast<double*>(b.m_out) + base;
+        bb.v_out = static_cast<double*>(b.m_out) + base + T;
+        fedopt_strip_split<Y, OLD, PG, FIRST, FINAL, NT, OSM, NH, U>(bb, s, tab, K, base + 2 * lane);
+        return;
+    }
     if (base + T <= P) {
         fedopt_strip_split<Y, OLD, PG, FIRST, FINAL, NT, OSM, NH, U>(b, s, tab, K, base + 2 * lane);
     } else {                                      // the ragged last tile: the per-lane strip map
@@ -924,6 +936,12 @@ template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, i
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W)))
 k_fedopt_c_w(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
     fedopt_c_body<Y, OLD, PG, FIRST, FINAL, NT, OSM, NH, U>(b, s, tab, K, P);
+}
+
+template <typename Y, typename OLD, class PG, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_c_mv(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
+    fedopt_c_body<Y, OLD, PG, true, true, NT, 1, 4, kUnroll / 2, true>(b, s, tab, K, P);
 }
 #endif
 
@@ -1122,7 +1140,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -1361,6 +1379,12 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
         const dim3 g4((unsigned)((P + 4 * 512 - 1) / (4 * 512)));
 #ifdef FEDAGG_PROBES
         const unsigned shm = (unsigned)g_cfg.lds_kib * 1024u;
+        if (first && final_ && g_cfg.opt_mv) {
+            if (P % (4 * 512) || b.m_in_f64 != 1 || b.m_out_f64 != 1 || !b.v_in)
+                return fail(FA_EINVAL, "fa_tune OPT_MV probe: P %% 2048 == 0, fp64 m in and out, v given");
+            hipLaunchKernelGGL((k_fedopt_c_mv<Y, OLD, PG, NT>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+            return check_launch("fa_fedopt_step: kernel launch");
+        }
         if (first && final_) {
             switch (g_cfg.wpe) {
 #define FA_WPE(W_) \
@@ -1771,6 +1795,9 @@ int fa_tune(int knob, int value) {
         case FA_TUNE_LDS:
             if (value < 0 || value > 64) return fail(FA_EINVAL, "fa_tune: occupancy-probe LDS 0..64 KiB per workgroup");
             g_cfg.lds_kib = value;
+            return FA_OK;
+        case FA_TUNE_OPT_MV:
+            g_cfg.opt_mv = value ? 1 : 0;
             return FA_OK;
         case FA_TUNE_WPE:
             if (value != 0 && value != 5 && value != 6 && value != 8)

@@ -326,7 +326,8 @@ _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _a
           "nt_store": _abi.FA_TUNE_NT_STORE, "fastdiv64": _abi.FA_TUNE_FASTDIV64,
           "tilemap": _abi.FA_TUNE_TILEMAP, "opt_nt": _abi.FA_TUNE_OPT_NT, "opt_nostore": _abi.FA_TUNE_OPT_NOSTORE,
           "opt_store": _abi.FA_TUNE_OPT_STORE, "opt_coal": _abi.FA_TUNE_OPT_COAL, "narrow": _abi.FA_TUNE_NARROW,
-          "lds": _abi.FA_TUNE_LDS, "wpe": _abi.FA_TUNE_WPE}
+          "lds": _abi.FA_TUNE_LDS, "wpe": _abi.FA_TUNE_WPE,
+          "opt_mv": _abi.FA_TUNE_OPT_MV}
 
 
 def tune(**knobs):

@@ -63,7 +63,10 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                     FA_TUNE_LDS = 17 /* occupancy probe: KiB of (unused) dynamic LDS per workgroup of the fold
                                         and FedOpt kernels, 0..64 */,
                     FA_TUNE_WPE = 18 /* occupancy probe: fp32 fold / FedOpt FIRST|FINAL kernels compiled for at
-                                        least W waves per SIMD (0 = compiler's choice, 5, 6, 8) */ };
+                                        least W waves per SIMD (0 = compiler's choice, 5, 6, 8) */,
+                    FA_TUNE_OPT_MV = 19 /* layout probe, FedOpt FIRST|FINAL steady state: 1 = fp64 m and v
+                                           interleaved per 512-element wave tile in ONE buffer passed as
+                                           m_in / m_out (2P doubles each; P % 2048 == 0) */ };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);
