@@ -26,8 +26,8 @@ Also measured in the same run:
                 step at N > 1) / its kernel time (HIP events on the launch stream) vs the
                 8.0 TB/s HBM3E peak; ``traffic`` = HBM bytes per launch from rocprofv3 PMC
                 counters (profiles/pmc_traffic.json, collected by tools/gpu_session.sh pmc + tools/pmc_traffic.py --session) when
-                that entry was measured on the current kernel source (sha256 of fedagg.hip),
-                else null with the reason
+                that entry was measured on the libfedagg.so this run loads (its sha256), else
+                null with the reason
   cpu_baseline  the numpy restatement of numpyhelper.increment_average (oracle/, bit-equal to
                 FEDn) on a bounded sample (K clients x S params) on one host core; its result is
                 also compared bit-for-bit with the GPU aggregate of the same elements
@@ -52,7 +52,6 @@ sys.path.insert(0, ROOT)
 
 METRIC = "aggregated params/sec (device-resident) — FedAvg 64-client reduce, 100M fp32"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-KERNEL_SRC = os.path.join(ROOT, "fedn_amd", "csrc", "fedagg.hip")
 
 
 def parse():
@@ -89,14 +88,16 @@ def make_updates(K, P, dtype, device, seed):
     return ups
 
 
-def kernel_sha():
-    with open(KERNEL_SRC, "rb") as f:
+def file_sha(path):
+    with open(path, "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def pmc_traffic(workload):
     """(HBM bytes per launch, provenance) from rocprofv3 PMC runs (tools/gpu_session.sh pmc) — only if
-    that entry was collected on the current kernel source; else (None, reason)."""
+    that entry was collected on the very libfedagg.so this run loaded (sha256 of the file; the build
+    is deterministic, so probe-only source edits do not invalidate it); else (None, reason)."""
+    from fedn_amd import _abi
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
@@ -105,10 +106,12 @@ def pmc_traffic(workload):
         return None, {"note": "profiles/pmc_traffic.json unreadable"}
     if ent is None:
         return None, {"note": f"no PMC entry for workload {workload}"}
-    src = {"file": "profiles/pmc_traffic.json", "workload": workload, "kernel_src_sha": ent.get("kernel_src_sha"),
-           "collected": ent.get("collected"), "read_bytes": ent.get("read_bytes"), "write_bytes": ent.get("write_bytes")}
-    if ent.get("kernel_src_sha") != kernel_sha():
-        src["note"] = "stale: collected on another revision of fedagg.hip; re-run tools/gpu_session.sh pmc + tools/pmc_traffic.py --session"
+    src = {"file": "profiles/pmc_traffic.json", "workload": workload, "lib_sha": ent.get("lib_sha"),
+           "kernel_src_sha": ent.get("kernel_src_sha"), "collected": ent.get("collected"),
+           "read_bytes": ent.get("read_bytes"), "write_bytes": ent.get("write_bytes")}
+    if ent.get("lib_sha") != file_sha(_abi.lib_path()):
+        src["note"] = ("stale: collected on another build of libfedagg.so; re-run tools/gpu_session.sh pmc + "
+                       "tools/pmc_traffic.py --session")
         return None, src
     return ent["bytes"], src
 

@@ -63,6 +63,7 @@ for s in $STEPS; do
     pmc)
       # HBM traffic per launch for every workload bench.py reports: one rocprofv3 pass per counter
       # (FETCH_SIZE and WRITE_SIZE cannot share a pass), then profiles/pmc_traffic.json
+      sha256sum fedn_amd/libfedagg.so | cut -c1-16 > "$OUT/lib_sha.txt"
       i=0
       for args in "--clients 64" "--clients 8 --fedopt-params 0" "--clients 64 --dtype bf16 --fedopt-params 0"; do
         i=$((i+1))

@@ -19,11 +19,23 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def kernel_sha():
-    """sha256 (16 hex) of fedn_amd/csrc/fedagg.hip: bench.py reports an entry's traffic only while
-    the kernel source is the one it was measured on."""
-    with open(os.path.join(ROOT, "fedn_amd", "csrc", "fedagg.hip"), "rb") as f:
+def file_sha(path):
+    with open(path, "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def kernel_sha():
+    """sha256 (16 hex) of fedn_amd/csrc/fedagg.hip (informational)."""
+    return file_sha(os.path.join(ROOT, "fedn_amd", "csrc", "fedagg.hip"))
+
+
+def lib_sha(session=None):
+    """sha256 (16 hex) of the libfedagg.so the PMC runs loaded (written by gpu_session.sh into the
+    session directory; else the in-tree file): bench.py reports an entry's traffic only while it
+    loads that same library."""
+    if session and os.path.exists(os.path.join(session, "lib_sha.txt")):
+        return open(os.path.join(session, "lib_sha.txt")).read().split()[0][:16]
+    return file_sha(os.path.join(ROOT, "fedn_amd", "libfedagg.so"))
 
 
 def per_launch(path, kernel):
@@ -34,7 +46,7 @@ def per_launch(path, kernel):
     return sum(vals) / len(vals), len(vals)
 
 
-def record(d, key, kernel, alg=None):
+def record(d, key, kernel, alg=None, session=None):
     fetch, nf = per_launch(os.path.join(d, "pmc_FETCH_SIZE", "run_counter_collection.csv"), kernel)
     write, nw = per_launch(os.path.join(d, "pmc_WRITE_SIZE", "run_counter_collection.csv"), kernel)
     read_b = 2 * fetch * 1024
@@ -43,7 +55,7 @@ def record(d, key, kernel, alg=None):
     db = json.load(open(out)) if os.path.exists(out) else {}
     db[key] = {"bytes": read_b + write_b, "read_bytes": read_b, "write_bytes": write_b,
                "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write, "launches": [nf, nw], "kernel": kernel,
-               "kernel_src_sha": kernel_sha(), "collected": datetime.date.today().isoformat(),
+               "lib_sha": lib_sha(session), "kernel_src_sha": kernel_sha(), "collected": datetime.date.today().isoformat(),
                "alg_bytes": alg, "traffic_over_alg": None if not alg else (read_b + write_b) / alg,
                "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count on 16-B streaming loads); "
                              "write = WRITE_SIZE x 1024"}
@@ -65,7 +77,7 @@ SESSION = [
 def main():
     if sys.argv[1] == "--session":
         for sub, key, kernel, alg in SESSION:
-            record(os.path.join(sys.argv[2], sub), key, kernel, alg)
+            record(os.path.join(sys.argv[2], sub), key, kernel, alg, session=sys.argv[2])
         return
     d, key = sys.argv[1], sys.argv[2]
     kernel = sys.argv[3] if len(sys.argv) > 3 else "k_fedavg"
