@@ -25,6 +25,8 @@ class WaveFedOpt:
 
     def __init__(self, devices, P, wave=8):
         self.devices = [torch.device(d) for d in devices]
+        self.devices = [torch.device(d.type, torch.cuda.current_device()) if d.index is None else d
+                        for d in self.devices]
         self.P = P
         self.wave = wave
         self.bounds = shard_bounds(P, len(self.devices))
@@ -41,9 +43,18 @@ class WaveFedOpt:
         K = len(host_updates)
         if K == 0:
             raise ValueError("no updates")
+        if len(ns) != K:
+            raise ValueError(f"{K} updates but {len(ns)} num_examples")
+        upd_dt = host_updates[0].dtype
+        for k, u in enumerate(host_updates):      # a copy_ into the wave slots would cast silently
+            if u.dtype != upd_dt or u.numel() != self.P or u.device.type != "cpu":
+                raise ValueError(f"update {k}: {u.dtype} x {u.numel()} on {u.device}; every update must be a "
+                                 f"host tensor of {self.P} {upd_dt} elements")
+        for d, (lo, hi) in enumerate(self.bounds):
+            if old[d].numel() != hi - lo or old[d].device != self.devices[d]:
+                raise ValueError(f"old[{d}] must hold the {hi - lo} elements of slice {d} on {self.devices[d]}")
         Ns = [int(v) for v in np.cumsum(ns)]
         W = self.wave
-        upd_dt = host_updates[0].dtype
         outs = []
         ctx = []
         for d, dv in enumerate(self.devices):

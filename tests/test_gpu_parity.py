@@ -1220,3 +1220,22 @@ def test_sharded_gloo_world2_hip_kernel():
     assert np.array_equal(res[0][1].view(np.uint32), want.view(np.uint32))
     for rank, _, full in res:
         assert np.array_equal(full.view(np.uint32), want.view(np.uint32)), f"rank {rank}"
+
+
+def test_waves_reject_mismatched_updates():
+    """WaveFedOpt refuses updates whose dtype / size differ from the first (a copy into the bf16
+    wave slots would otherwise round an fp32 update silently) and misplaced old slices."""
+    from fedn_amd.waves import WaveFedOpt
+    P = 10_000
+    wf = WaveFedOpt([DEV, DEV], P, wave=4)
+    old = wf.slices(torch.zeros(P, dtype=torch.float64))
+    ups = [torch.zeros(P, dtype=torch.bfloat16) for _ in range(3)]
+    with pytest.raises(ValueError, match="update 2"):
+        wf.round(ups[:2] + [torch.zeros(P)], [1, 2, 3], old, {})
+    with pytest.raises(ValueError, match="update 1"):
+        wf.round([ups[0], torch.zeros(P - 1, dtype=torch.bfloat16)], [1, 2], old, {})
+    with pytest.raises(ValueError, match="num_examples"):
+        wf.round(ups, [1, 2], old, {})
+    with pytest.raises(ValueError, match="old"):
+        wf.round(ups, [1, 2, 3], [o.cpu() for o in old], {})
+    assert len(wf.round(ups, [1, 2, 3], old, {"serveropt": "yogi"})) == 2
