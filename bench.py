@@ -197,7 +197,9 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000):
     old_s = old32[:S].cpu().numpy()
     ups_s = [([u[:S].cpu().numpy()], n) for u, n in zip(ups, ns)]
     st = ref.FedOptState()
+    t0 = time.perf_counter()
     want1, _ = ref.fedopt_combine(st, ups_s, [old_s], params)
+    cpu1 = time.perf_counter() - t0
     ok1 = bool(np.array_equal(out[:S].cpu().numpy().view(np.uint64), want1[0].view(np.uint64)) and
                np.array_equal(m32[:S].cpu().numpy().view(np.uint32), st.m[0].view(np.uint32)) and
                np.array_equal(v[:S].cpu().numpy().view(np.uint64), st.v[0].view(np.uint64)))
@@ -214,11 +216,14 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000):
         r2()
     _, ms2 = timed_steps(r2, steps, stream, 1, device, False)
     st.m = [st.m[0].astype(np.float64)]           # the GPU's steady state takes m in float64 (round >= 3)
+    t0 = time.perf_counter()
     want2, _ = ref.fedopt_combine(st, ups_s, want1, params)
+    cpu2 = time.perf_counter() - t0
     ok2 = bool(np.array_equal(out2[:S].cpu().numpy().view(np.uint64), want2[0].view(np.uint64)) and
                np.array_equal(m_out[:S].cpu().numpy().view(np.uint64), st.m[0].view(np.uint64)) and
                np.array_equal(v_out[:S].cpu().numpy().view(np.uint64), st.v[0].view(np.uint64)))
-    for phase, ms, b, ok in (("round1", ms1, K * P * 4 + P * 4 + P * 20, ok1), ("steady", ms2, P * (4 * K + 48), ok2)):
+    for phase, ms, b, ok, cpu_s in (("round1", ms1, K * P * 4 + P * 4 + P * 20, ok1, cpu1),
+                                    ("steady", ms2, P * (4 * K + 48), ok2, cpu2)):
         wl = f"fedopt_adam_{phase}_k{K}_p{P}"
         traffic, tsrc = pmc_traffic(wl)
         gbs = b / ms / 1e6
@@ -227,7 +232,10 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000):
                                    "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
                                    "kernel": "k_fedopt_c (pseudo-gradient fold + Adam step fused; 4 coalesced element pairs per lane)",
                                    "alg_bytes_per_launch": b},
-                      "bit_exact_on_sample": ok, "sample": f"first {S} params of every buffer vs oracle/numpy_ref"}
+                      "bit_exact_on_sample": ok, "sample": f"first {S} params of every buffer vs oracle/numpy_ref",
+                      "cpu_baseline": {"value": K * S / cpu_s, "unit": "params/s", "cores": 1, "kind": "port",
+                                       "sample": f"{K} clients x {S} params: oracle/numpy_ref.fedopt_combine (the "
+                                                 "fedopt.py restatement, numpy, single-threaded)", "seconds": cpu_s}}
     res["config"] = (f"BASELINE configs[3]: FedAdam, {K} device-resident fp32 updates x {P} params, m / v in HBM "
                      "(fedopt.py:151-185), one fused launch per round")
     del ups, old32, out, v, m32, old64, m64, v64, m_out, v_out, out2
