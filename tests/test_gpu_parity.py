@@ -157,15 +157,33 @@ def test_fedavg_f32_updates_into_f64_aggregate():
     assert_lists_identical([agg.cpu().numpy()], [want], "f32->f64")
 
 
-def test_fedavg_bf16_defined_as_fp32_on_upcast():
-    """bf16 has no numpy reference: parity = fp32 oracle on the exactly upcast values."""
-    rng = np.random.default_rng(13)
-    ups, ns = _updates(rng, 9, 10001)
+@pytest.mark.parametrize("K,P", [(9, 10001), (2, 1), (3, 5), (70, 8192 * 3 + 7), (64, 1 << 16), (130, 4099)])
+def test_fedavg_bf16_defined_as_fp32_on_upcast(K, P):
+    """bf16 has no numpy reference: parity = fp32 oracle on the exactly upcast values. Covers the
+    8-strips-of-4 map's whole tiles, its ragged tile, and K > 64 (continuing a stored aggregate)."""
+    rng = np.random.default_rng(13 + K + P)
+    ups, ns = _updates(rng, K, P)
     bf = [torch.from_numpy(u).to(torch.bfloat16) for u in ups]
     up32 = [b.to(torch.float32).numpy() for b in bf]
     want = ref.fedavg_flat(up32, ns)
     got = _fold_dev([b.to(DEV) for b in bf], ns, torch.float32)
-    assert_lists_identical([got], [want], "bf16")
+    assert_lists_identical([got], [want], f"bf16 K={K} P={P}")
+    if K > 8:
+        got_c = _fold_dev([b.to(DEV) for b in bf], ns, torch.float32, chunks=[2, 4, K - 6])
+        assert_lists_identical([got_c], [want], "bf16 chunked")
+
+
+def test_fedavg_bf16_special_values():
+    """bf16 zeros, signed zeros, subnormals, extremes, inf and NaN through the f32 fold."""
+    vals = np.array([0.0, -0.0, 1e-40, -9.2e-41, 3.3e38, -3.3e38, np.inf, -np.inf, np.nan, 1.0, -2.5, 7.0],
+                    dtype=np.float32)
+    rng = np.random.default_rng(6)
+    bf = [torch.from_numpy(rng.permutation(np.tile(vals, 700)).astype(np.float32)).to(torch.bfloat16) for _ in range(7)]
+    ns = [3, 1, 4000, 1, 5, 9, 2]
+    with np.errstate(all="ignore"):
+        want = ref.fedavg_flat([b.to(torch.float32).numpy() for b in bf], ns)
+    got = _fold_dev([b.to(DEV) for b in bf], ns, torch.float32)
+    assert_lists_identical([got], [want], "bf16 special")
 
 
 def test_fedavg_special_values():
