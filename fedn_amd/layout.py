@@ -16,7 +16,8 @@ ALIGN = 256
 # host pack: large tensors are copied into the pinned staging buffer by several threads
 # (np.copyto releases the GIL), so the host memcpy keeps up with PCIe Gen5 H2D
 PACK_THREADS = int(os.environ.get("FEDN_AMD_PACK_THREADS", "8"))
-PACK_CHUNK = 16 << 20   # bytes per copy task
+PACK_CHUNK = 16 << 20   # bytes per copy task (at most)
+PACK_MIN_PARALLEL = 1 << 20   # updates smaller than this are packed inline (a task costs ~10 us)
 _pool = None
 
 
@@ -128,13 +129,30 @@ class Layout:
         return buf_np_u8[off:off + n * dt.itemsize].view(dt)
 
     def pack(self, arrays, buf_np_u8):
-        """Copy the tensors of ``arrays`` into their group regions of a host uint8 buffer."""
+        """Copy the tensors of ``arrays`` into their group regions of a host uint8 buffer: inline
+        for a small update; otherwise every tensor is cut into pieces (>= 1 MiB, at most
+        PACK_CHUNK, ~1 per pack thread over the whole update) copied by the pack threads, so a
+        model of many mid-size tensors is packed in parallel, not one tensor at a time."""
+        jobs = []
         for dt in self.groups:
             g = self.group_view(buf_np_u8, dt)
             for i, off in self.members[dt]:
                 sz = self.sizes[i]
                 if sz:
-                    parallel_copy(g[off:off + sz], np.ascontiguousarray(arrays[i]).reshape(-1))
+                    jobs.append((g[off:off + sz], np.ascontiguousarray(arrays[i]).reshape(-1)))
+        total = sum(d.nbytes for d, _ in jobs)
+        if PACK_THREADS <= 1 or total < PACK_MIN_PARALLEL:
+            for d, src in jobs:
+                np.copyto(d, src, casting="no")
+            return
+        piece = max(1 << 20, min(PACK_CHUNK, -(-total // PACK_THREADS)))
+        futs = []
+        for d, src in jobs:
+            step = max(1, piece // src.itemsize)
+            for i in range(0, src.size, step):
+                futs.append(_executor().submit(np.copyto, d[i:i + step], src[i:i + step], casting="no"))
+        for f in futs:
+            f.result()
 
     def unpack_group(self, flat, dt, out, copy=True):
         """Scatter a group's flat host array back into per-tensor arrays. With copy=False

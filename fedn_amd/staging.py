@@ -34,6 +34,12 @@ BATCH = 64                    # device-resident updates folded per launch (the k
 MAX_CHUNKS = 8                # the round's last launch is split into at most this many chunks, each
 MIN_CHUNK_BYTES = 8 << 20     # chunk's D2H (and FedOpt's old-model H2D) overlapping the next chunk
 RING_BYTES = 64 << 20         # pinned ring piece for host -> device streaming of the global model
+# host updates of at most SMALL_UPDATE_BYTES (a packed model) are batched: packed on arrival into a
+# pinned arena of up to BATCH updates / ARENA_BYTES, which reaches HBM in ONE copy right before ONE
+# multi-client launch folds them all — for small models the per-update H2D, events and launch
+# (~0.1 ms of host work each) cost far more than the bytes; larger updates fold on arrival
+SMALL_UPDATE_BYTES = 4 << 20
+ARENA_BYTES = 64 << 20
 
 
 def chunks(n, itemsize):
@@ -99,6 +105,26 @@ class _Slot:
         self.reserved = False
 
 
+class _Arena:
+    """Pinned host + device bytes for up to ``cap`` packed small updates (see SMALL_UPDATE_BYTES)."""
+    __slots__ = ("host", "host_np", "dev", "cap", "count", "done", "used")
+
+    def __init__(self, cap, nbytes, device):
+        self.host = torch.empty(cap * nbytes, dtype=torch.uint8, pin_memory=True)
+        self.host_np = self.host.numpy()
+        self.dev = torch.empty(cap * nbytes, dtype=torch.uint8, device=device)
+        self.cap, self.count, self.used = cap, 0, False
+        self.done = None
+
+
+class _ArenaRef:
+    """One update's bytes inside an arena: ``dev`` is the view the batch's fold reads."""
+    __slots__ = ("dev",)
+
+    def __init__(self, dev):
+        self.dev = dev
+
+
 class _Pipeline:
     def __init__(self, device, layout, nslots, slots=None, streams=None):
         self.device = torch.device(device)
@@ -120,6 +146,10 @@ class _Pipeline:
         self.time_d2h = 0.0
         self._hold = []
         self.pending = []                        # device-resident updates not folded yet: (staged, n, N)
+        # small host updates are batched through arenas (not on the helper path, whose callers fold
+        # one pair per pipeline with cached slots)
+        self.batch_host = slots is None and layout.nbytes <= SMALL_UPDATE_BYTES
+        self._arenas, self._arena, self._arena_i = [], None, 0
 
     # ---- staging ---------------------------------------------------------------------
     def _take_slot(self):
@@ -149,6 +179,47 @@ class _Pipeline:
         self.compute.wait_event(s.h2d_done)
         s.used = True
         return s
+
+    def put_small(self, arrays):
+        """Pack a small host update into the arena being filled (no H2D yet); returns the
+        reference the batch's fold reads once ``upload_arena`` has run."""
+        a = self._arena
+        if a is None:
+            if not self._arenas:
+                cap = max(1, min(BATCH, ARENA_BYTES // self.layout.nbytes))
+                self._arenas = [_Arena(cap, self.layout.nbytes, self.device) for _ in range(2)]
+            a = self._arenas[self._arena_i]
+            self._arena_i = (self._arena_i + 1) % len(self._arenas)
+            if a.used:
+                a.done.synchronize()            # its previous H2D has read the pinned bytes
+            a.count = 0
+            self._arena = a
+        nb, j = self.layout.nbytes, a.count
+        tic = time.perf_counter()
+        self.layout.pack(arrays, a.host_np[j * nb:(j + 1) * nb])
+        self.time_pack += time.perf_counter() - tic
+        a.count += 1
+        return _ArenaRef(a.dev[j * nb:(j + 1) * nb])
+
+    def arena_full(self):
+        return self._arena is not None and self._arena.count >= self._arena.cap
+
+    def upload_arena(self):
+        """ONE H2D of every update packed since the last upload, enqueued on the compute stream:
+        after the folds that last read these device bytes, before the batch's fold."""
+        a = self._arena
+        if a is None or a.count == 0:
+            return
+        n = a.count * self.layout.nbytes
+        start = torch.cuda.Event(enable_timing=True)
+        a.done = torch.cuda.Event(enable_timing=True)
+        with torch.cuda.device(self.device), torch.cuda.stream(self.compute):
+            start.record(self.compute)
+            a.dev[:n].copy_(a.host[:n], non_blocking=True)
+            a.done.record(self.compute)
+        self._h2d.append((start, a.done))
+        a.used = True
+        self._arena = None
 
     def acquire(self, arrays):
         """Device-resident source for ``arrays``: a StagedModel is used in place (the compute
@@ -316,6 +387,10 @@ class FedAvgPipeline(_Pipeline):
             self.pending.append((self.acquire(arrays), n, N))
             if len(self.pending) >= BATCH:
                 self._flush()
+        elif self.batch_host:
+            self.pending.append((self.put_small(arrays), n, N))
+            if len(self.pending) >= BATCH or self.arena_full():
+                self._flush()
         else:
             self._flush()
             slot = self.acquire(arrays)
@@ -359,6 +434,7 @@ class FedAvgPipeline(_Pipeline):
 
     def _flush(self):
         if self.pending:
+            self.upload_arena()
             entries, self.pending = self.pending, []
             self._fold_all(entries)
 
@@ -371,6 +447,7 @@ class FedAvgPipeline(_Pipeline):
         if self.general is not None:
             return self.general.result()
         tic = time.perf_counter()
+        self.upload_arena()
         entries, self.pending = self.pending, []
         init = not self.agg_started
         span = self._kernel_span()
@@ -655,6 +732,11 @@ class FedOptPipeline(_Pipeline):
             self.pending.append((self.acquire(arrays), n, N))
             if len(self.pending) >= BATCH:
                 self._flush()
+        elif self.batch_host:
+            self.layout.check(arrays)
+            self.pending.append((self.put_small(arrays), n, N))
+            if len(self.pending) >= BATCH or self.arena_full():
+                self._flush()
         else:
             self._flush()
             slot = self.acquire(arrays)
@@ -691,6 +773,7 @@ class FedOptPipeline(_Pipeline):
 
     def _flush(self):
         if self.pending:
+            self.upload_arena()
             entries, self.pending = self.pending, []
             self._fold_pg(entries)
 
@@ -711,6 +794,7 @@ class FedOptPipeline(_Pipeline):
         # the pseudo-gradient in registers (FIRST when pg holds nothing yet) and the server
         # step; chunked so that each chunk's D2H of the new model overlaps the next chunk
         tic = time.perf_counter()
+        self.upload_arena()
         entries, self.pending = self.pending, []
         first = not self.pg_started
         new_m, new_v, hosts = {}, {}, {}
