@@ -1257,3 +1257,41 @@ def test_waves_reject_mismatched_updates():
     with pytest.raises(ValueError, match="old"):
         wf.round(ups, [1, 2, 3], [o.cpu() for o in old], {})
     assert len(wf.round(ups, [1, 2, 3], old, {"serveropt": "yogi"})) == 2
+
+
+@pytest.mark.parametrize("kind", ["fedavg", "fedopt"])
+def test_small_host_updates_arena_batches(kind):
+    """Host updates of <= SMALL_UPDATE_BYTES fold in arena batches: K = 70 updates of a ~1.6 MB
+    two-group model (arena capacity 40 -> flushes at 40 and at the end, both arenas reused)
+    through the plug-in, two rounds, bit-exact to the oracle."""
+    from fedn_amd import staging
+    rng = np.random.default_rng(21)
+    shapes = [(300, 1000), (1000,), (7, 3)]
+    base = [rng.standard_normal(shapes[0]).astype(np.float32), rng.standard_normal(shapes[1]).astype(np.float32),
+            rng.integers(-100, 100, shapes[2]).astype(np.int64)]
+    nbytes = sum(a.nbytes for a in base)
+    assert nbytes <= staging.SMALL_UPDATE_BYTES and staging.ARENA_BYTES // nbytes < 64
+    K = 70
+    ups = [[(base[0] + 0.01 * rng.standard_normal(shapes[0])).astype(np.float32),
+            (base[1] + 0.01 * rng.standard_normal(shapes[1])).astype(np.float32),
+            rng.integers(-100, 100, shapes[2]).astype(np.int64)] for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    uh, agg = _plugin(kind)
+    params = {"serveropt": "yogi", "learning_rate": 1e-2, "beta1": 0.9, "beta2": 0.99, "tau": 1e-4}
+    st = ref.FedOptState()
+    old = [b.astype(np.float32) for b in base[:2]]
+    if kind == "fedopt":
+        ups = [u[:2] for u in ups]
+    for r in range(2):
+        gid = uh.put_global_model(old, f"g{r}") if kind == "fedopt" else "global"
+        for a, n in zip(ups, ns):
+            uh.submit(a, n, model_id=gid)
+        model, data = agg.combine_models(helper=None, delete_models=True,
+                                         parameters=params if kind == "fedopt" else None)
+        if kind == "fedavg":
+            want, nr = ref.fedavg_combine(list(zip(ups, ns)))
+        else:
+            want, nr = ref.fedopt_combine(st, list(zip(ups, ns)), old, params)
+            old = want
+        assert data["nr_aggregated_models"] == nr == K
+        assert_lists_identical(model, want, f"{kind} round {r}")
