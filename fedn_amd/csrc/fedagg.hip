@@ -1140,7 +1140,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -1247,6 +1247,22 @@ void launch_fedavg_geom(X* a, const ClientTable<typename CP::S>& tab, int cnt, i
         hipLaunchKernelGGL((k_fedavg<Y, X, CP, E, S, U, false, false, NT>), grid, dim3(kBlock), 0, st, a, tab, cnt, P);
 }
 
+// Launch geometry by model size (profiles/r02_tile_probe.log). Every workgroup folds all K
+// clients over one tile, so the grid must be many times the ~1,024 resident workgroups or its
+// last partial wave decides the time. The pipelined 4-strip kernel (16 KiB of each client per
+// tile) is the fastest once each client buffer is >= kPipeMinClientBytes (>= 10 K tiles: 0.74-0.75
+// of peak at 64 x 100 M fp32 and bf16); below that, one 16-B strip per lane with 4 (fp32) or 8
+// (narrower types, or K <= 8) clients loaded ahead — 4 KiB tiles — holds 0.65-0.80 where the
+// 4-strip tiles drop to 0.25-0.55 (bf16 10 M: 0.27 -> 0.65; fp32 3 M x 64: 0.45 -> 0.67).
+constexpr int64_t kPipeMinClientBytes = 160ll << 20;
+
+template <typename Y>
+inline bool pipe_pays(int64_t P) { return P * (int64_t)sizeof(Y) >= kPipeMinClientBytes; }
+
+template <typename Y, typename X, class CP, int E>
+void launch_fedavg_small(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
+                         hipStream_t st);
+
 template <class CP> struct is_sf_rule : std::false_type {};
 template <typename Y, typename X> struct is_sf_rule<CWSUM<Y, X>> : std::true_type {};
 template <typename T_> struct is_sf_rule<CRUN<T_>> : std::true_type {};
@@ -1258,6 +1274,7 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
     constexpr bool tunable = (std::is_same<Y, float>::value || std::is_same<Y, bf16>::value) && std::is_same<X, float>::value &&
                              std::is_same<CP, CF32>::value;
     if constexpr (is_sf_rule<CP>::value) {
+        if (!pipe_pays<Y>(P)) return launch_fedavg_small<Y, X, CP, E>(a, tab, cnt, P, first, int_first, st);
         launch_fedavg_pipe<Y, X, CP, E, 4, false, false>(a, tab, cnt, P, first, int_first, st);
         return;
     }
@@ -1267,6 +1284,9 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
         const int lanetab = g_cfg.lanetab, nt_store = g_cfg.nt_store, tilemap = g_cfg.tilemap;
         const int key = (block_log == 9 ? 20000 : block_log == 10 ? 30000 : 0) + lanetab * 10000 + strips * 100 +
                         unroll * 2 + nt;
+        // the default settings select the product's size-dependent geometry (FA_TUNE_AUTO_GEOM 0 forces them)
+        if (g_cfg.auto_geom && key == 4 * 100 + 0 && nt_store == 1 && tilemap == 0 && !pipe_pays<Y>(P))
+            return launch_fedavg_small<Y, X, CP, E>(a, tab, cnt, P, first, int_first, st);
         if constexpr (sizeof(Y) < sizeof(X) && E % 2 == 0) {
             if (g_cfg.narrow && key == 4 * 100 + 0 && nt_store == 1 && tilemap == 0)
                 return launch_fedavg_pipe<Y, X, CP, E / 2, 8, false, false, kBlock, 1>(a, tab, cnt, P, first, int_first, st);
@@ -1304,6 +1324,7 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
             default: break;
         }
 #else
+        if (!pipe_pays<Y>(P)) return launch_fedavg_small<Y, X, CP, E>(a, tab, cnt, P, first, int_first, st);
         // measured best on MI355X (profiles/r01_microbench.md): 4 x 16-B strips per lane, the next
         // client's strips in flight (pipelined), cached loads, non-temporal aggregate stores.
         // bf16 clients: strips of 4 elements (8-B loads, 16-B f32 stores), 8 per lane, so every wave
@@ -1315,6 +1336,13 @@ void launch_fedavg_vec(X* a, const ClientTable<typename CP::S>& tab, int cnt, in
 #endif
     }
     launch_fedavg_geom<Y, X, CP, E, 1, kUnroll, false>(a, tab, cnt, P, first, int_first, st);
+}
+
+template <typename Y, typename X, class CP, int E>
+void launch_fedavg_small(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
+                         hipStream_t st) {
+    if (sizeof(Y) < 4 || cnt <= 8) launch_fedavg_geom<Y, X, CP, E, 1, 8, false>(a, tab, cnt, P, first, int_first, st);
+    else launch_fedavg_geom<Y, X, CP, E, 1, 4, false>(a, tab, cnt, P, first, int_first, st);
 }
 
 template <typename Y, typename X, class CP>
@@ -1795,6 +1823,9 @@ int fa_tune(int knob, int value) {
         case FA_TUNE_LDS:
             if (value < 0 || value > 64) return fail(FA_EINVAL, "fa_tune: occupancy-probe LDS 0..64 KiB per workgroup");
             g_cfg.lds_kib = value;
+            return FA_OK;
+        case FA_TUNE_AUTO_GEOM:
+            g_cfg.auto_geom = value ? 1 : 0;
             return FA_OK;
         case FA_TUNE_OPT_MV:
             g_cfg.opt_mv = value ? 1 : 0;

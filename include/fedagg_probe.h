@@ -66,7 +66,11 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                                         least W waves per SIMD (0 = compiler's choice, 5, 6, 8) */,
                     FA_TUNE_OPT_MV = 19 /* layout probe, FedOpt FIRST|FINAL steady state: 1 = fp64 m and v
                                            interleaved per 512-element wave tile in ONE buffer passed as
-                                           m_in / m_out (2P doubles each; P % 2048 == 0) */ };
+                                           m_in / m_out (2P doubles each; P % 2048 == 0) */,
+                    FA_TUNE_AUTO_GEOM = 20 /* 1 (default) = with the default geometry knobs, the product's
+                                              size-dependent choice (4-strip pipelined kernel only for client
+                                              buffers >= 160 MiB, else 1 strip x 4/8 clients ahead); 0 = the
+                                              knobs as set, at every size */ };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);

@@ -1295,3 +1295,30 @@ def test_small_host_updates_arena_batches(kind):
             old = want
         assert data["nr_aggregated_models"] == nr == K
         assert_lists_identical(model, want, f"{kind} round {r}")
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("K,P", [(3, 1), (64, 4099), (130, 8192 * 3 + 7), (9, 100_003)])
+def test_fedavg_pipelined_geometry_forced_small(dt, K, P):
+    """The product folds client buffers under 160 MiB with the 1-strip kernel and larger ones with
+    the pipelined 4-strip kernel (bf16: 8 strips of 4). The probe library forces the pipelined
+    geometry at small sizes so its whole tiles, ragged tile and K > 64 continuation stay covered
+    against the oracle; both geometries must give the same bits."""
+    from fedn_amd import _abi, ops
+    rng = np.random.default_rng(K + P)
+    ups, ns = _updates(rng, K, P)
+    if dt == "bf16":
+        dev = [torch.from_numpy(u).to(torch.bfloat16).to(DEV) for u in ups]
+        ups = [d.to(torch.float32).cpu().numpy() for d in dev]
+    else:
+        dev = [_to_dev(u) for u in ups]
+    want = ref.fedavg_flat(ups, ns)
+    auto = _fold_dev(dev, ns, torch.float32)
+    with _abi.use_probe():
+        ops.tune(auto_geom=0)
+        try:
+            forced = _fold_dev(dev, ns, torch.float32)
+        finally:
+            ops.tune(auto_geom=1)
+    assert_lists_identical([auto], [want], f"{dt} auto")
+    assert_lists_identical([forced], [want], f"{dt} pipelined")
