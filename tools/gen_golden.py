@@ -608,6 +608,21 @@ def helper_cases(ref):
     ]
 
 
+def edge_cases(ref):
+    """Zero-size tensors (alone and among others) and rounds of more than 64 clients (the
+    kernarg client table's size: several launches / arena batches per round)."""
+    rng = np.random.default_rng(11)
+    zshapes = [(4,), (0,), (2, 0, 3), (5,)]
+    return [
+        fedavg_case(ref, "fedavg_zero_size_k3", rng, zshapes, np.float32, rng.integers(1, 5001, 3)),
+        fedavg_case(ref, "fedavg_all_empty_k2", rng, [(0,), (0, 4)], np.float32, rng.integers(1, 5001, 2)),
+        fedavg_case(ref, "fedavg_odd_k70", rng, ODD_SHAPES, np.float32, rng.integers(1, 5001, 70)),
+        fedopt_case(ref, "fedopt_zero_size_2r", rng, zshapes, [list(rng.integers(1, 5001, 3)) for _ in range(2)]),
+        fedopt_case(ref, "fedopt_yogi_k70", rng, ODD_SHAPES, [list(rng.integers(1, 5001, 70)), [3, 9]],
+                    {"serveropt": "yogi"}),
+    ]
+
+
 def main():
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     ref = _import_reference()
@@ -620,6 +635,8 @@ def main():
         return _write(mixed_cases(ref), merge=True)
     if only == "power_norm":
         return _write([helper_power_norm(ref, np.random.default_rng(9))], merge=True)
+    if only == "edge":
+        return _write(edge_cases(ref), merge=True)
     cases = []
     cases.append(helper_kat(ref))
     rng = np.random.default_rng(1)
@@ -673,6 +690,7 @@ def main():
     cases += helper_cases(ref)
     cases += mixed_cases(ref)
     cases.append(helper_power_norm(ref, np.random.default_rng(9)))
+    cases += edge_cases(ref)
     _write(cases, merge=False)
 
 
