@@ -5,7 +5,9 @@ fp32, all resident in HBM) into a fresh aggregate: fedavg.py's fold loop
 ``x <- x + (n_k*(y_k - x))/N_k`` over k = 1..K-1 in queue order.
 value = aggregated client-params/s = K * P / t_step for the WHOLE job.
 
-N = 1 (BASELINE configs[1] / the north-star line): one libfedagg launch per step.
+N = 1 (the BASELINE metric's workload — 64 x 100 M fp32, the north star's one-GPU target — on
+one GPU): one libfedagg launch per step. Beside it: ``configs1`` (BASELINE configs[1]: the same
+model with 8 clients) and ``fedopt`` (configs[3]).
 
 N > 1 (BASELINE configs[2]: the same 100 M-param model, param-sharded across N GPUs with an
 RCCL all-gather): one process per GPU; the flat model is dealt block-cyclically over the
@@ -165,6 +167,32 @@ def side(fn):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+def fold_kernel_label(P, in_bytes, K):
+    if P * in_bytes >= 160 << 20:          # fedagg.hip kPipeMinClientBytes
+        return ("k_fedavg_pipe (fp32, 4 x 16-B strips per lane, next client prefetched)" if in_bytes == 4 else
+                "k_fedavg_pipe (bf16 -> f32, 8 strips of 4 elements per lane, next client prefetched)")
+    return f"k_fedavg (1 x 16-B strip per lane, {8 if in_bytes < 4 or K <= 8 else 4} clients loaded ahead)"
+
+
+def configs1_side(ups, ns, agg, stream, device, in_bytes, a):
+    """BASELINE configs[1]: FedAvg of 8 device-resident updates of the same model (the first 8
+    buffers of the main line's), one launch per step, its own roofline."""
+    from fedn_amd import ops
+    K, P = len(ups), agg.numel()
+    Ns = [int(v) for v in np.cumsum(ns)]
+    step = lambda: ops.fedavg_fold(agg, ups, ns, Ns, init=True, stream=stream)  # noqa: E731
+    for _ in range(3):
+        step()
+    el, kms = timed_steps(step, a.steps, stream, 1, device, False)
+    b = K * P * in_bytes + P * 4
+    traffic, tsrc = pmc_traffic(f"fedavg_k{K}_p{P}_{a.dtype}")
+    return {"value": K * P / (el / a.steps), "unit": "params/s", "ms_per_step": el / a.steps * 1e3,
+            "roofline": {"bound": "hbm", "achieved": b / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+                         "kernel": fold_kernel_label(P, in_bytes, K), "kernel_ms": kms, "alg_bytes_per_launch": b},
+            "config": f"BASELINE configs[1]: FedAvg, {K} device-resident {a.dtype} updates x {P} params"}
+
+
 def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000):
     """BASELINE configs[3]: FedAdam, K device-resident fp32 updates of P params, state in HBM;
     one fused fa_fedopt_step launch per round. Round 1 (old fp32, m / v None) and steady state
@@ -287,10 +315,9 @@ def main():
         elapsed, kern_ms = timed_steps(step, a.steps, stream, world, device, rehearsal)
         alg_bytes = K * P * in_bytes + P * 4           # read every update once, write the aggregate once
         workload = f"fedavg_k{K}_p{P}_{a.dtype}"
-        kernel = ("k_fedavg_pipe (fp32, 4 x 16-B strips per lane, next client prefetched)" if a.dtype == "f32" else
-                  "k_fedavg_pipe (bf16 -> f32, 8 strips of 4 elements per lane, next client prefetched)")
-        config = {"workload": f"FedAvg {K} clients x {P} params {a.dtype} per GPU (BASELINE configs[1]/north "
-                              "star; device-resident, one fused fold launch per aggregation)",
+        kernel = fold_kernel_label(P, in_bytes, K)
+        config = {"workload": f"FedAvg {K} clients x {P} params {a.dtype} per GPU (the BASELINE metric's workload, "
+                              "north star at 1 GPU; device-resident, one fused fold launch per aggregation)",
                   "clients": K, "params_per_gpu": P, "global_params": P_total,
                   "parallelism": "param-slice shards x1, no data-path collective"}
         scaling = "weak"
@@ -318,8 +345,8 @@ def main():
         _, kern_ms = timed_steps(fold_only, a.steps, stream, world, device, rehearsal)
         alg_bytes = K * L * in_bytes + L * 4              # this rank's fold, per step (all rounds)
         workload = f"fedavg_k{K}_p{L}_{a.dtype}_rank_of_{world}"
-        kernel = (f"k_fedavg_pipe over this rank's {cyc.rounds} chunks of {cyc.C} params (fold-only timing; "
-                  "max over ranks)")
+        kernel = (f"{fold_kernel_label(cyc.C, in_bytes, K)} over this rank's {cyc.rounds} chunks of {cyc.C} params "
+                  "(fold-only timing; max over ranks)")
         config = {"workload": f"FedAvg {K} clients x {P_total} params {a.dtype}, param-sharded block-cyclically over "
                               f"{world} GPUs; RCCL all-gather of each folded round overlapped with the next round's "
                               "fold, inside the timed step (BASELINE configs[2])",
@@ -350,6 +377,8 @@ def main():
         extra["gather_to_host"] = {"ms": gh * 1e3, "bytes_per_rank": P * 4, "GBps_aggregate": P * 4 / gh / 1e9,
                                    "note": "D2H of the aggregate into pinned host memory; not in value"}
         del host
+        if K >= 8 and not a.no_side:
+            extra["configs1"] = side(lambda: configs1_side(ups[:8], ns[:8], agg, stream, device, in_bytes, a))
         del ups, agg
         torch.cuda.empty_cache()
         if rank == 0 and a.fedopt_params > 0:
