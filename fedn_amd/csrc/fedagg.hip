@@ -1210,7 +1210,8 @@ void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, i
     unsigned shm = 0;
 #ifdef FEDAGG_PROBES
     shm = (unsigned)g_cfg.lds_kib * 1024u;     // occupancy probe: LDS the kernel never touches
-    if constexpr (std::is_same<X, float>::value && S * E * (int)sizeof(Y) == 64 && BLK == kBlock && MAP == 0 && !LT && !NT) {
+    if constexpr (std::is_same<CP, CF32>::value && std::is_same<X, float>::value && S * E * (int)sizeof(Y) == 64 &&
+                  BLK == kBlock && MAP == 0 && !LT && !NT && NTS == 1) {
         const int w = g_cfg.wpe;
         if (w > 0 && !int_first) {
 #define FA_WPE(W_)                                                                                                      \
@@ -1380,24 +1381,28 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
                       int64_t P, bool first, bool final_, hipStream_t st) {
     const dim3 grid((unsigned)grid_for(P, E));
 #ifdef FEDAGG_PROBES
-    if (first && final_ && g_cfg.opt_nostore) {
-        hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, true>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
-        return check_launch("fa_fedopt_step: kernel launch");
-    }
-    if constexpr (E == 4) {
+    // the probe variants exist for the configs[3] shapes only (fp32 updates over an fp32 or fp64
+    // model, vector path); every other combination runs the product kernels in the probe build too
+    constexpr bool probe_combo = E == 4 && std::is_same<Y, float>::value &&
+                                 (std::is_same<OLD, float>::value || std::is_same<OLD, double>::value);
+    if constexpr (probe_combo) {
+        if (first && final_ && g_cfg.opt_nostore) {
+            hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, true>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+            return check_launch("fa_fedopt_step: kernel launch");
+        }
         if (first && final_ && g_cfg.opt_coal == 1) {   // 2 pairs per lane (a 256-element wave tile)
             hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1, 2>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
             return check_launch("fa_fedopt_step: kernel launch");
         }
-    }
-    if (first && final_ && !g_cfg.opt_coal) {    // the per-lane 4-element strip map (r01), for A/B
-        if (g_cfg.opt_store == 1)
-            hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, false, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
-        else if (g_cfg.opt_store == 2)
-            hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, false, 2>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
-        else
-            hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
-        return check_launch("fa_fedopt_step: kernel launch");
+        if (first && final_ && !g_cfg.opt_coal) {    // the per-lane 4-element strip map (r01), for A/B
+            if (g_cfg.opt_store == 1)
+                hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, false, 1>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+            else if (g_cfg.opt_store == 2)
+                hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, false, 2>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+            else
+                hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+            return check_launch("fa_fedopt_step: kernel launch");
+        }
     }
 #endif
     if constexpr (E == 4) {
@@ -1407,6 +1412,7 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
         const dim3 g4((unsigned)((P + 4 * 512 - 1) / (4 * 512)));
 #ifdef FEDAGG_PROBES
         const unsigned shm = (unsigned)g_cfg.lds_kib * 1024u;
+        if constexpr (probe_combo) {
         if (first && final_ && g_cfg.opt_mv) {
             if (P % (4 * 512) || b.m_in_f64 != 1 || b.m_out_f64 != 1 || !b.v_in)
                 return fail(FA_EINVAL, "fa_tune OPT_MV probe: P %% 2048 == 0, fp64 m in and out, v given");
@@ -1424,6 +1430,7 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
                     hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1, 4>), g4, dim3(kBlock), shm, st, b, s, tab, cnt, P);
                     return check_launch("fa_fedopt_step: kernel launch");
             }
+        }
         }
 #endif
         if (first && final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
@@ -1456,6 +1463,7 @@ int launch_fedopt(const OptBuffers& b, const OptScalars& s, const void* const* u
         const bool last = k0 + cnt >= K;
         const bool fin = last && final_all;
 #ifdef FEDAGG_PROBES
+        if constexpr (std::is_same<Y, float>::value && (std::is_same<OLD, float>::value || std::is_same<OLD, double>::value))
         if (vec && !g_cfg.opt_nt) {
             int rc = launch_fedopt_one<Y, OLD, PG, 4, false>(b, s, tab, cnt, P, first, fin, st);
             if (rc) return rc;
