@@ -74,6 +74,17 @@ for s in $STEPS; do
         done
       done
       echo "pmc: now run  python tools/pmc_traffic.py --session $OUT  in the build container" ;;
+    pmcrank)
+      # HBM traffic of one rank's fold at N = 2, 4, 8 (bench.py's N > 1 roofline), replayed on this GPU
+      sha256sum fedn_amd/libfedagg.so | cut -c1-16 > "$OUT/lib_sha.txt"
+      for n in 2 4 8; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+          cd /tmp && timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmcrank$n/pmc_$c" -o run -- \
+            python3 "$GRAFT_REPO_ROOT/tools/pmc_rank_fold.py" --world $n > "$GRAFT_REPO_ROOT/$OUT/pmcrank${n}_$c.log" 2>&1; rc=$?
+          cd "$GRAFT_REPO_ROOT"; echo "pmcrank$n $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+        done
+      done
+      echo "pmcrank: now run  python tools/pmc_traffic.py --rank-session $OUT  in the build container" ;;
     pmcprobe)
       PA="TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum TCP_UTCL1_THRASHING_STALL_sum TCP_UTCL1_STALL_MULTI_MISS_sum GRBM_GUI_ACTIVE"
       PB="TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum"

@@ -17,6 +17,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def file_sha(path):
@@ -74,7 +75,36 @@ SESSION = [
 ]
 
 
+def record_rank(session, world):
+    """bench.py's N > 1 roofline entry: one rank's fold per step = ``rounds`` launches of the replayed
+    chunk fold (tools/pmc_rank_fold.py); bytes per step = per-launch bytes x rounds."""
+    from tools.pmc_rank_fold import rank_geometry
+    C, rounds, L = rank_geometry(100_000_000, world, 8)
+    d = os.path.join(session, f"pmcrank{world}")
+    kernel = "k_fedavg<float, float"
+    fetch, nf = per_launch(os.path.join(d, "pmc_FETCH_SIZE", "run_counter_collection.csv"), kernel)
+    write, nw = per_launch(os.path.join(d, "pmc_WRITE_SIZE", "run_counter_collection.csv"), kernel)
+    read_b, write_b = 2 * fetch * 1024 * rounds, write * 1024 * rounds
+    alg = rounds * (64 * C * 4 + C * 4)
+    key = f"fedavg_k64_p{L}_f32_rank_of_{world}"
+    out = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    db = json.load(open(out)) if os.path.exists(out) else {}
+    db[key] = {"bytes": read_b + write_b, "read_bytes": read_b, "write_bytes": write_b,
+               "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write, "launches": [nf, nw], "kernel": kernel,
+               "per": f"one rank's step: {rounds} launches of 64 x {C} fp32 (replayed on one GPU)",
+               "lib_sha": lib_sha(session), "kernel_src_sha": kernel_sha(), "collected": datetime.date.today().isoformat(),
+               "alg_bytes": alg, "traffic_over_alg": (read_b + write_b) / alg,
+               "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count on 16-B streaming loads); "
+                             "write = WRITE_SIZE x 1024"}
+    json.dump(db, open(out, "w"), indent=1)
+    print(json.dumps({key: db[key]}))
+
+
 def main():
+    if sys.argv[1] == "--rank-session":
+        for world in (2, 4, 8):
+            record_rank(sys.argv[2], world)
+        return
     if sys.argv[1] == "--session":
         for sub, key, kernel, alg in SESSION:
             record(os.path.join(sys.argv[2], sub), key, kernel, alg, session=sys.argv[2])
