@@ -6,8 +6,8 @@ fp32, all resident in HBM) into a fresh aggregate: fedavg.py's fold loop
 value = aggregated client-params/s = K * P / t_step for the WHOLE job.
 
 N = 1 (the BASELINE metric's workload — 64 x 100 M fp32, the north star's one-GPU target — on
-one GPU): one libfedagg launch per step. Beside it: ``configs1`` (BASELINE configs[1]: the same
-model with 8 clients) and ``fedopt`` (configs[3]).
+one GPU): one libfedagg launch per step. Beside it: ``fedopt`` (configs[3]) and, with --configs1,
+``configs1`` (BASELINE configs[1]: the same model with 8 clients).
 
 N > 1 (BASELINE configs[2]: the same 100 M-param model, param-sharded across N GPUs with an
 RCCL all-gather): one process per GPU; the flat model is dealt block-cyclically over the
@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--fedopt-params", type=int, default=350_000_000, help="configs[3] side field (0 = skip)")
     ap.add_argument("--fedopt-clients", type=int, default=32)
     ap.add_argument("--no-side", action="store_true", help="N > 1: skip the beside-the-line measurements")
+    ap.add_argument("--configs1", action="store_true",
+                    help="N = 1: add the configs[1] field (K = 8, same kernel: off by default so that a rocprofv3 "
+                         "--stats run of the default command averages the headline launches only)")
     ap.add_argument("--waves-params", type=int, default=1_000_000_000, help="N > 1: configs[4] side field (0 = skip)")
     ap.add_argument("--waves-clients", type=int, default=128)
     ap.add_argument("--waves-pool", type=int, default=8, help="distinct pinned host updates (reused cyclically)")
@@ -377,7 +380,7 @@ def main():
         extra["gather_to_host"] = {"ms": gh * 1e3, "bytes_per_rank": P * 4, "GBps_aggregate": P * 4 / gh / 1e9,
                                    "note": "D2H of the aggregate into pinned host memory; not in value"}
         del host
-        if K >= 8 and not a.no_side:
+        if K >= 8 and a.configs1:
             extra["configs1"] = side(lambda: configs1_side(ups[:8], ns[:8], agg, stream, device, in_bytes, a))
         del ups, agg
         torch.cuda.empty_cache()

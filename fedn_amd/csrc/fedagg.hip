@@ -1405,10 +1405,11 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
         }
     }
 #endif
-    if constexpr (E == 4 || (E == 8 && sizeof(Y) == 2)) {
+    if constexpr (E == 4) {
         // wave-coalesced element map, 4 pairs per lane (512-element wave tiles), non-temporal state /
         // model stores: +3-6 % over the per-lane strip map on configs[3], bit-identical
-        // (profiles/r02_fedopt_coal_*.log); bf16 updates: one dword per pair
+        // (profiles/r02_fedopt_coal_*.log); every vector-path update dtype (bf16 /
+        // fp16 updates: one dword per pair)
         const dim3 g4((unsigned)((P + 4 * 512 - 1) / (4 * 512)));
 #ifdef FEDAGG_PROBES
         const unsigned shm = (unsigned)g_cfg.lds_kib * 1024u;

@@ -69,7 +69,7 @@ for s in $STEPS; do
         i=$((i+1))
         for c in FETCH_SIZE WRITE_SIZE; do
           cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc$i/pmc_$c" -o run -- \
-            python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 $args > "$GRAFT_REPO_ROOT/$OUT/pmc${i}_$c.log" 2>&1; rc=$?
+            python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 $args --no-side > "$GRAFT_REPO_ROOT/$OUT/pmc${i}_$c.log" 2>&1; rc=$?
           cd "$GRAFT_REPO_ROOT"; echo "pmc$i $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
         done
       done
