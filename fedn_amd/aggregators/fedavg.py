@@ -21,6 +21,8 @@ import traceback
 
 import torch
 
+from ..ingest import ShardedStagedModel
+from ..layout import Layout, spread
 from ..staging import AndroidFedAvgPipeline, FedAvgPipeline, helper_kind
 from .aggregatorbase import AggregatorBase, queued_updates
 
@@ -33,11 +35,19 @@ def env_devices():
     return [d.strip() for d in v.split(",") if d.strip()] if v else None
 
 
+def _packed_bytes(model):
+    """Packed size of an update (host arrays or a staged model): what layout.spread decides on."""
+    lay = getattr(model, "layout", None)
+    return (lay if lay is not None else Layout.of(model)).nbytes
+
+
 def make_fedavg_pipeline(first, device=None, devices=None, helper=None):
     devices = devices or env_devices()
     if helper_kind(helper) == "androidhelper":   # its own fold rule and model format
         return AndroidFedAvgPipeline(device or (devices[0] if devices else None) or default_device(), first)
-    if devices and len(devices) > 1:
+    # several devices: slice the model over them when it is large (or already staged that way)
+    if devices and len(devices) > 1 and (isinstance(first, ShardedStagedModel) or
+                                         len(spread(devices, _packed_bytes(first))) > 1):
         from ..multidev import ShardedFedAvgPipeline
         return ShardedFedAvgPipeline(devices, first)
     return FedAvgPipeline(device or (devices[0] if devices else None) or default_device(), first)

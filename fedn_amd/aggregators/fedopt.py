@@ -20,9 +20,11 @@ import traceback
 
 from ..exceptions import InvalidParameterError
 from ..parameters import Parameters
+from ..ingest import ShardedStagedModel
+from ..layout import spread
 from ..staging import FedOptPipeline, FedOptState
 from .aggregatorbase import AggregatorBase, queued_updates
-from .fedavg import default_device, env_devices
+from .fedavg import _packed_bytes, default_device, env_devices
 
 logger = logging.getLogger("fedn")
 
@@ -42,14 +44,22 @@ class Aggregator(AggregatorBase):
         # several devices (argument or FEDN_AMD_DEVICES): old / pg / m / v sharded by parameter
         # slice over them inside this process (multidev.py); fixed for the instance's lifetime
         self.devices = devices or env_devices()
-        if self.devices and len(self.devices) > 1:
-            from ..multidev import ShardedFedOptState
-            self.state = ShardedFedOptState()
-        else:
-            self.state = FedOptState()
+        # with several devices the model is sliced over them only when it is large enough
+        # (layout.spread, decided by the session's first round; the state follows that choice)
+        self.state = None
+        self.sharded = None
 
     def _pipeline(self, model_old, model_next):
-        if self.devices and len(self.devices) > 1:
+        if self.sharded is None:
+            self.sharded = bool(self.devices and len(self.devices) > 1 and
+                                (isinstance(model_next, ShardedStagedModel) or
+                                 len(spread(self.devices, _packed_bytes(model_next))) > 1))
+            if self.sharded:
+                from ..multidev import ShardedFedOptState
+                self.state = ShardedFedOptState()
+            else:
+                self.state = FedOptState()
+        if self.sharded:
             from ..multidev import ShardedFedOptPipeline
             return ShardedFedOptPipeline(self.devices, model_old, model_next)
         dev = self.device or (self.devices[0] if self.devices else None) or default_device()
@@ -58,11 +68,11 @@ class Aggregator(AggregatorBase):
     # reference attribute names (fedopt.py:37-38): host copies of the HBM-resident state
     @property
     def m(self):
-        return self.state.m_host()
+        return None if self.state is None else self.state.m_host()
 
     @property
     def v(self):
-        return self.state.v_host()
+        return None if self.state is None else self.state.v_host()
 
     def combine_models(self, helper=None, delete_models=True, parameters=None):
         data = {"time_model_load": 0.0, "time_model_aggregation": 0.0}

@@ -22,7 +22,7 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 import torch
 
-from .layout import Layout
+from .layout import Layout, spread
 
 
 class StagedModel:
@@ -156,13 +156,18 @@ def stage_npz(data, device, stream):
 
     layout, pinned = codec.load_npz_into_layout(
         data, lambda nbytes: torch.empty(nbytes, dtype=torch.uint8, pin_memory=True))
+    return stage_pinned(layout, pinned, device, stream)
+
+
+def stage_pinned(layout, pinned, device, stream, host=None):
+    """Copy a pinned, layout-packed update (uint8 tensor) to a new device buffer on ``stream``."""
     dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
     ready = torch.cuda.Event()
     with torch.cuda.stream(stream):
         dev.copy_(pinned, non_blocking=True)
         ready.record(stream)
     ready.synchronize()
-    return StagedModel(layout, dev, ready)
+    return StagedModel(layout, dev, ready, host)
 
 
 def _member_spans(layout, dt, lo, hi):
@@ -325,10 +330,16 @@ class StagingUpdateHandler:
         return training_metadata
 
     def _stage_sharded(self, model_update):
-        streams = [self._stream(dv) for dv in self.devices]
+        """Stage as parameter slices over the devices — or on the first one alone when the model
+        is small (layout.spread: the rule the aggregators apply to pick their pipeline)."""
         decoded = self._decoded_upload(model_update)
         if decoded is not None and hasattr(decoded, "arrays"):
-            return stage_decoded_sharded(decoded, self.devices, streams), self._metadata(model_update)
+            devs = spread(self.devices, Layout.of(decoded.arrays).nbytes)
+            if len(devs) == 1:
+                with torch.cuda.device(devs[0]):
+                    return stage_decoded(decoded, devs[0], self._stream(devs[0])), self._metadata(model_update)
+            return stage_decoded_sharded(decoded, devs, [self._stream(dv) for dv in devs]), \
+                self._metadata(model_update)
         if self._native():
             try:
                 data, metadata = self.inner.load_model_update_byte(model_update)
@@ -339,7 +350,7 @@ class StagingUpdateHandler:
                 try:
                     layout, pinned = codec.load_npz_into_layout(
                         data, lambda nbytes: torch.empty(nbytes, dtype=torch.uint8, pin_memory=True))
-                    return stage_sharded(layout, pinned, self.devices, streams), metadata
+                    return self._stage_packed(layout, pinned), metadata
                 except codec.CodecError:
                     pass     # e.g. Fortran-ordered members: decode through the helper (np.load) below
         arrays, metadata = self.inner.load_model_update(model_update, self.helper)
@@ -347,7 +358,14 @@ class StagingUpdateHandler:
         layout = Layout.of(arrays)
         pinned = torch.empty(layout.nbytes, dtype=torch.uint8, pin_memory=True)
         layout.pack(arrays, pinned.numpy())
-        return stage_sharded(layout, pinned, self.devices, streams, arrays), metadata
+        return self._stage_packed(layout, pinned, arrays), metadata
+
+    def _stage_packed(self, layout, pinned, host=None):
+        devs = spread(self.devices, layout.nbytes)
+        if len(devs) == 1:
+            with torch.cuda.device(devs[0]):
+                return stage_pinned(layout, pinned, devs[0], self._stream(devs[0]), host)
+        return stage_sharded(layout, pinned, devs, [self._stream(dv) for dv in devs], host)
 
     def _native(self):
         """Raw-bytes decode applies to npz (numpyhelper / fednamdhelper); binaryhelper's raw

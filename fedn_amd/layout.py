@@ -40,6 +40,20 @@ def parallel_copy(dst, src):
         f.result()
 
 
+# FEDN_AMD_DEVICES: a model is sliced over several GPUs of the process only when its packed size
+# is at least this; a smaller one (every per-GPU slice a few MB at most) runs on the first GPU,
+# where one copy and one launch per update beat one per GPU
+MULTIDEV_MIN_BYTES = int(os.environ.get("FEDN_AMD_MULTIDEV_MIN_BYTES", str(64 << 20)))
+
+
+def spread(devices, nbytes):
+    """The devices a model of ``nbytes`` (packed) is sliced over: all of ``devices`` for a large
+    model, only the first below MULTIDEV_MIN_BYTES (read at call time)."""
+    if devices and len(devices) > 1 and nbytes < MULTIDEV_MIN_BYTES:
+        return list(devices[:1])
+    return list(devices) if devices else devices
+
+
 def _round_up(x, a):
     return (x + a - 1) // a * a
 

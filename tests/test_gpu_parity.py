@@ -27,6 +27,14 @@ def _gpu():
     _abi.load()
 
 
+@pytest.fixture(autouse=True)
+def _slice_every_model(monkeypatch):
+    """The multi-device tests use small models: slice them over the devices anyway (the size rule
+    that keeps small models on one GPU, layout.spread, has its own test)."""
+    from fedn_amd import layout
+    monkeypatch.setattr(layout, "MULTIDEV_MIN_BYTES", 0)
+
+
 def _plugin(name):
     from fedn_amd.aggregators import get_aggregator
     from fedn_amd.updatehandler import MemoryUpdateHandler
@@ -1322,3 +1330,42 @@ def test_fedavg_pipelined_geometry_forced_small(dt, K, P):
             ops.tune(auto_geom=1)
     assert_lists_identical([auto], [want], f"{dt} auto")
     assert_lists_identical([forced], [want], f"{dt} pipelined")
+
+
+@pytest.mark.parametrize("threshold,sliced", [(64 << 20, False), (1000, True)])
+def test_multidevice_size_rule(monkeypatch, threshold, sliced):
+    """FEDN_AMD_DEVICES slices a model over the GPUs only when it is at least MULTIDEV_MIN_BYTES
+    packed; smaller models stay on the first GPU — in the ingest and in both aggregators alike.
+    FedAvg and FedOpt (two rounds) through the ingest, bit-exact either way."""
+    from fedn_amd import layout, staging
+    from fedn_amd.aggregators.fedavg import Aggregator as FedAvg, make_fedavg_pipeline
+    from fedn_amd.aggregators.fedopt import Aggregator as FedOpt
+    from fedn_amd.ingest import ShardedStagedModel, StagedModel, StagingUpdateHandler
+    from fedn_amd.multidev import ShardedFedAvgPipeline
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    monkeypatch.setattr(layout, "MULTIDEV_MIN_BYTES", threshold)
+    devs = [DEV, DEV, DEV]
+    case = load_case("fedavg_odd_k8")
+    rd = case["rounds"][0]
+    assert isinstance(make_fedavg_pipeline(rd["updates"][0][0], devices=devs),
+                      ShardedFedAvgPipeline if sliced else staging.FedAvgPipeline)
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=None, devices=devs, workers=2)
+    for arrays, n in rd["updates"]:
+        uh.submit(arrays, n, via=st)
+    staged = [st._staged[k].result()[0] for k in list(st._staged)]
+    assert all(isinstance(x, ShardedStagedModel if sliced else StagedModel) for x in staged)
+    model, data = FedAvg(st, devices=devs).combine_models(helper=None)
+    assert_lists_identical(model, rd["out"], "fedavg size rule")
+    case = load_case("fedopt_adam_3r")
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=None, devices=devs, workers=2)
+    agg = FedOpt(st, devices=devs)
+    for r, rd in enumerate(case["rounds"][:2]):
+        gid = uh.put_global_model(rd["old"], f"g{r}")
+        for arrays, n in rd["updates"]:
+            uh.submit(arrays, n, model_id=gid, via=st)
+        model, data = agg.combine_models(helper=None, parameters=case["params"])
+        assert_lists_identical(model, rd["out"], f"fedopt size rule round {r}")
+    assert agg.sharded is sliced
+    st.close()
