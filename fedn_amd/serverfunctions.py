@@ -11,7 +11,8 @@ rounding, so they return bit-identical models:
 * :class:`WeightedAverage` — ``aggregate`` of server_functions.py:53-68: running
   ``weighted_sum += params * num_examples`` in previous_global's dtypes, then
   ``/ total_weight``; each client is packed into pinned memory, copied to HBM and folded on
-  arrival (``fa_weighted_sum``), the division is one elementwise pass.
+  arrival (``fa_weighted_sum``) — small models in arena batches of up to 64 clients, one copy
+  and one launch each (staging.SMALL_UPDATE_BYTES) — and the division is one elementwise pass.
 * :class:`IncrementalAverage` — sf_incremental_aggregation.py:24-48: the running model stays
   in HBM between calls; each arriving model is one ``fa_running_mean`` launch
   ``g = (g*(T-n) + m*n)/T``. Like the example, ``total_examples`` is not reset between
@@ -25,7 +26,7 @@ import torch
 
 from . import ops
 from .layout import Layout
-from .staging import _Pipeline
+from .staging import BATCH, _Pipeline
 
 
 def _device(device):
@@ -76,14 +77,30 @@ class WeightedAverage:
         with torch.cuda.device(dev):
             acc = {dt: torch.zeros(layout.group_elems[dt], dtype=acc_dt[dt], device=dev) for dt in layout.groups}
         total_weight = 0
+        pending = []                      # small models: arena-batched clients, one launch per batch
+
+        def flush():
+            pipe.upload_arena()
+            for dt in layout.groups:
+                ops.weighted_sum(acc[dt], [pipe.group(e, dt) for e, _ in pending], [w for _, w in pending],
+                                 stream=pipe.compute)
+            pending.clear()
+
         for _cid, (client_parameters, metadata) in client_updates.items():   # :60-64, arrival order
             num_examples = metadata.get("num_examples", 1)
             total_weight += num_examples
             layout.check(client_parameters)
+            if pipe.batch_host:
+                pending.append((pipe.put_small(client_parameters), num_examples))
+                if len(pending) >= BATCH or pipe.arena_full():
+                    flush()
+                continue
             slot = pipe.stage(client_parameters)
             for dt in layout.groups:
                 ops.weighted_sum(acc[dt], [pipe.group(slot, dt)], [num_examples], stream=pipe.compute)
             slot.consumed.record(pipe.compute)
+        if pending:
+            flush()
         out = [None] * len(layout.shapes)
         for dt in layout.groups:                                     # :67 weighted / total_weight
             ops.elementwise("div", acc[dt], x=acc[dt], a=total_weight, stream=pipe.compute)
