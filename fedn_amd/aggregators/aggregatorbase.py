@@ -18,7 +18,7 @@ import numpy as np
 AGGREGATOR_PLUGIN_PATH = "fedn_amd.aggregators.{}"
 LOAD_AHEAD = int(os.environ.get("FEDN_AMD_LOAD_AHEAD", "8"))
 # host bytes of decoded-but-not-yet-folded updates the read-ahead may hold (FEDn holds one)
-LOAD_AHEAD_BYTES = int(os.environ.get("FEDN_AMD_LOAD_AHEAD_BYTES", str(2 << 30)))
+LOAD_AHEAD_BYTES = int(os.environ.get("FEDN_AMD_LOAD_AHEAD_BYTES", str(4 << 30)))
 
 
 def _raiser(e):
@@ -45,7 +45,7 @@ def requeue_front(q, items):
         q.not_empty.notify(len(items))
 
 
-def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None):
+def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_box=None):
     """The aggregators' drain of ``update_handler.model_updates`` (fedavg.py:109-112,
     fedopt.py:76-80): yields ``(model_update, load)`` in FIFO order until the queue is empty,
     where ``load()`` returns ``update_handler.load_model_update(model_update, helper)`` or
@@ -58,6 +58,10 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None):
     up to ``ahead`` updates, and — once the first decoded update shows the model's size — no
     more than ``ahead_bytes`` of decoded updates (one at least), counting the one being folded. A handler that stages updates
     on arrival (ingest.StagingUpdateHandler) is drained one by one: its loads are already done.
+
+    ``size_box``: a one-element list the caller keeps across rounds (the aggregator instance
+    does): it holds the decoded size of the last update seen, so a later round admits its read-
+    ahead at once instead of decoding its first update alone.
 
     Lossless: if the caller stops early (an exception that escapes its per-update handling,
     e.g. a BaseException, or ``close()``), the updates dequeued ahead but not yet handed out go
@@ -77,7 +81,7 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None):
         return
     pool = ThreadPoolExecutor(max_workers=ahead, thread_name_prefix="fedn_amd_load")
     window = deque()
-    size = [None]                     # bytes of one decoded update, once known
+    size = size_box if size_box is not None else [None]   # bytes of one decoded update, once known
 
     def allowed():
         if size[0] is None:
@@ -94,11 +98,14 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None):
                 continue
             window.append((mu, pool.submit(update_handler.load_model_update, mu, helper), None))
 
+    first = [True]
+
     def sized(fut):
         def load():
             res = fut.result()
-            if size[0] is None:
-                size[0] = model_nbytes(res[0])
+            if first[0]:                  # this round's size (a hint from an earlier round is replaced)
+                first[0] = False
+                size[0] = model_nbytes(res[0]) or size[0]
             return res
         return load
 
@@ -126,6 +133,7 @@ class AggregatorBase(ABC):
     def __init__(self, update_handler):
         self.name = self.__class__.__name__
         self.update_handler = update_handler
+        self._ahead_size = [None]        # decoded update size seen last round (queued_updates)
 
     @abstractmethod
     def combine_models(self, helper=None, delete_models=True, parameters=None):

@@ -79,7 +79,7 @@ class Aggregator(AggregatorBase):
         pipe = None
 
         logger.info("AGGREGATOR({}): Aggregating model updates... ".format(self.name))
-        with contextlib.closing(queued_updates(self.update_handler, helper)) as updates:
+        with contextlib.closing(queued_updates(self.update_handler, helper, size_box=self._ahead_size)) as updates:
             for model_update, load in updates:
                 try:
                     tic = time.time()

@@ -84,7 +84,7 @@ class Aggregator(AggregatorBase):
 
         pipe = None
         nr_aggregated_models, total_examples = 0, 0
-        with contextlib.closing(queued_updates(self.update_handler, helper)) as updates:
+        with contextlib.closing(queued_updates(self.update_handler, helper, size_box=self._ahead_size)) as updates:
             for model_update, load in updates:
                 try:
                     tic = time.time()

@@ -11,7 +11,10 @@ deleted from the repository whether or not it could be fetched (control.py:690).
 
 Use it from FEDn by mixing :class:`GpuReduceMixin` into ``Control``.
 """
+import io
+import threading
 import time
+import zipfile
 from concurrent.futures import ThreadPoolExecutor
 
 from .aggregators.aggregatorbase import LOAD_AHEAD_BYTES, model_nbytes
@@ -19,8 +22,18 @@ from .aggregators.fedavg import default_device
 from .staging import FedAvgPipeline
 
 
-def _fetch_load(fetch, load, model_id):
-    """(data, model or None, load exception or None, t_fetch, t_load) for one combiner."""
+def npz_decoded_bytes(data):
+    """Decoded size of an npz payload from its zip central directory (no inflate), else None."""
+    try:
+        with zipfile.ZipFile(io.BytesIO(data)) as z:
+            return sum(i.file_size for i in z.infolist())
+    except Exception:  # noqa: BLE001 — not an npz: the size is learned from the first decoded model
+        return None
+
+
+def _fetch_load(fetch, load, model_id, on_size=None):
+    """(data, model or None, load exception or None, t_fetch, t_load) for one combiner;
+    ``on_size(bytes)`` hears the decoded size as soon as the fetched payload shows it."""
     tic = time.time()
     try:
         data = fetch(model_id)
@@ -29,6 +42,10 @@ def _fetch_load(fetch, load, model_id):
     t_fetch = time.time() - tic
     if data is None:
         return None, None, None, t_fetch, 0.0
+    if on_size is not None and isinstance(data, (bytes, bytearray, memoryview)):
+        est = npz_decoded_bytes(data)
+        if est:
+            on_size(est)
     tic = time.time()
     try:
         model = load(data)
@@ -58,23 +75,36 @@ def reduce_models(combiners, fetch, load, delete=None, device=None, workers=8):
     nxt = [0]                              # next combiner index to submit
     size = [None]                          # host bytes of one decoded model, once known
 
-    def top_up():
+    known = threading.Event()
+
+    def on_size(nbytes):
+        if size[0] is None:
+            size[0] = nbytes
+        known.set()
+
+    def top_up(held=0):
         """Keep up to ``workers`` decodes in flight, and no more decoded-but-unfolded bytes than
-        LOAD_AHEAD_BYTES once a model's size is known (one at a time until then)."""
+        LOAD_AHEAD_BYTES (``held``: a model being waited for or folded counts too) once a model's
+        size is known — from the first payload's zip directory, or the first decoded model —
+        and one at a time until then."""
         cap = 1 if size[0] is None else max(1, min(workers, LOAD_AHEAD_BYTES // max(1, size[0])))
-        while pool is not None and nxt[0] < len(ids) and len(pending) < cap:
-            pending[nxt[0]] = pool.submit(_fetch_load, fetch, load, ids[nxt[0]])
+        while pool is not None and nxt[0] < len(ids) and len(pending) + held < cap:
+            pending[nxt[0]] = pool.submit(_fetch_load, fetch, load, ids[nxt[0]], on_size)
             nxt[0] += 1
 
     try:
         for j, model_id in enumerate(ids):
             top_up()
             fut = pending.pop(j, None)
+            if fut is not None:
+                while size[0] is None and not fut.done() and not known.wait(0.002):
+                    pass                         # the first payload's size admits the others early
+                top_up(held=1)
             data, model_next, err, t_fetch, t_load = fut.result() if fut is not None else \
                 _fetch_load(fetch, load, model_id)
             if size[0] is None and model_next is not None:
                 size[0] = model_nbytes(model_next)
-            top_up()
+            top_up(held=1)
             meta["time_fetch_model"] += t_fetch
             if data is not None:
                 meta["time_load_model"] += t_load if err is None else 0.0

@@ -247,3 +247,92 @@ def test_mixed_fold_plan_is_numpy():
         mixed.fold_plan([((3,), i8)], [((3,), i8)], 2.5, 4)                          # int diff, float n
     (r, shape), = mixed.sub_plan([((3,), i8)], [((1,), f4)])
     assert r == (np.ones(3, i8) * 1.0 + np.ones(1, f4) * -1.0).dtype and shape == (3,)
+
+
+def test_reduce_admits_by_npz_directory_size():
+    """reduce_models learns a model's decoded size from the first payload's zip directory, so
+    the other decodes start at once (not after the first decode), and never more are in flight
+    than the byte budget allows (the model being waited for included)."""
+    import io
+    import threading
+    import time
+
+    import fedn_amd.reduce as red
+
+    class Pipe:
+        def __init__(self, dev, m):
+            pass
+
+        def add(self, m, n, N):
+            pass
+
+        def result(self):
+            return "ok"
+
+    repo = {}
+    for c in range(6):
+        b = io.BytesIO()
+        np.savez_compressed(b, **{"0": np.zeros(250_000, np.float32)})      # 1 MB decoded
+        repo[c] = b.getvalue()
+    assert red.npz_decoded_bytes(repo[0]) >= 1_000_000
+    assert red.npz_decoded_bytes(b"not a zip") is None
+    live, peak, lock = [0], [0], threading.Lock()
+
+    def load(data):
+        with lock:
+            live[0] += 1
+            peak[0] = max(peak[0], live[0])
+        time.sleep(0.2)
+        with lock:
+            live[0] -= 1
+        return [np.zeros(250_000, np.float32)]
+
+    saved = red.FedAvgPipeline, red.LOAD_AHEAD_BYTES
+    red.FedAvgPipeline = Pipe
+    try:
+        combiners = [{"name": f"c{c}", "model_id": c} for c in range(6)]
+        red.LOAD_AHEAD_BYTES = 1 << 30
+        red.reduce_models(combiners, fetch=repo.__getitem__, load=load, device="cpu", workers=8)
+        assert peak[0] == 6                       # all decodes overlapped, the first one included
+        peak[0] = 0
+        red.LOAD_AHEAD_BYTES = 3_100_000          # three decoded models
+        red.reduce_models(combiners, fetch=repo.__getitem__, load=load, device="cpu", workers=8)
+        assert peak[0] == 3
+    finally:
+        red.FedAvgPipeline, red.LOAD_AHEAD_BYTES = saved
+
+
+def test_queued_updates_size_hint_across_rounds():
+    """With the size of the previous round's updates (size_box), a round's read-ahead starts its
+    decodes together instead of decoding the first update alone; without it, one at a time until
+    the first decode shows the size."""
+    import threading
+    import time
+
+    from fedn_amd.aggregators.aggregatorbase import queued_updates
+    box = [None]
+    for rnd in range(2):
+        uh = MemoryUpdateHandler()
+        for k in range(6):
+            uh.submit([np.full(250, k, np.float32)], 1)          # 1000 bytes per update
+        live, peak, lock = [0], [0], threading.Lock()
+        inner = uh.load_model_update
+
+        def load_model_update(mu, helper, inner=inner, live=live, peak=peak):
+            with lock:
+                live[0] += 1
+                peak[0] = max(peak[0], live[0])
+            time.sleep(0.05)
+            with lock:
+                live[0] -= 1
+            return inner(mu, helper)
+        uh.load_model_update = load_model_update
+        it = queued_updates(uh, None, ahead=8, ahead_bytes=1 << 20, size_box=box)
+        mu, load = next(it)
+        time.sleep(0.03)                         # round 2: the others are already decoding
+        first_peak = peak[0]
+        load()
+        for mu, load in it:
+            load()
+        assert box[0] == 1000
+        assert first_peak == (1 if rnd == 0 else 6)
