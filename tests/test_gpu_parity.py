@@ -277,6 +277,69 @@ def test_fedavg_full_size_sampled():
         assert_lists_identical([agg[sl].cpu().numpy()], [want], f"slice {lo}")
 
 
+def test_fedavg_north_star_size_sampled():
+    """The metric's workload at full size, 64 x 100 M fp32 (and bf16), folded in one launch; the
+    oracle checks 3 slices of 200 K elements plus the last tile."""
+    from fedn_amd import ops
+    P, K = 100_000_000, 64
+    g = torch.Generator(device=DEV).manual_seed(2)
+    base = torch.randn(P, generator=g, device=DEV)
+    ups = [torch.randn(P, generator=g, device=DEV).mul_(0.01).add_(base) for _ in range(K)]
+    del base
+    ns = [int(v) for v in np.random.default_rng(2).integers(1, 5001, K)]
+    Ns = list(np.cumsum(ns))
+    for dt in ("f32", "bf16"):
+        if dt == "bf16":
+            ups = [u.to(torch.bfloat16) for u in ups]
+        agg = torch.empty(P, device=DEV)
+        ops.fedavg_fold(agg, ups, ns, Ns, init=True)
+        torch.cuda.synchronize()
+        for lo in (0, 37_000_001, P - 200_000):
+            sl = slice(lo, lo + 200_000)
+            want = ref.fedavg_flat([u[sl].float().cpu().numpy() for u in ups], ns)
+            assert_lists_identical([agg[sl].cpu().numpy()], [want], f"{dt} slice {lo}")
+    del ups, agg
+    torch.cuda.empty_cache()
+
+
+def test_fedopt_configs3_size_sampled():
+    """BASELINE configs[3] at full size: 32 x 350 M fp32 FedAdam, round 1 and the fp64 steady
+    state, one fused launch each; the oracle checks 3 slices of 100 K elements of out, m and v."""
+    from fedn_amd import ops
+    P, K = 350_000_000, 32
+    g = torch.Generator(device=DEV).manual_seed(3)
+    old = torch.randn(P, generator=g, device=DEV)
+    ups = [torch.randn(P, generator=g, device=DEV).mul_(0.01).add_(old) for _ in range(K)]
+    ns = [int(v) for v in np.random.default_rng(3).integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
+    params = {"serveropt": "adam", "learning_rate": 1e-3, "beta1": 0.9, "beta2": 0.99, "tau": 1e-4}
+    kw = {k: params[k] for k in ("learning_rate", "beta1", "beta2", "tau")}
+    out = torch.empty(P, dtype=torch.float64, device=DEV)
+    v = torch.empty(P, dtype=torch.float64, device=DEV)
+    m = torch.empty(P, dtype=torch.float32, device=DEV)
+    ops.fedopt_step(old, ups, ns, Ns, first=True, final=True, m_out=m, v_out=v, out=out, serveropt="adam", **kw)
+    old64, m64 = out.clone(), m.double()
+    del m
+    m2 = torch.empty(P, dtype=torch.float64, device=DEV)
+    v2 = torch.empty(P, dtype=torch.float64, device=DEV)
+    out2 = torch.empty(P, dtype=torch.float64, device=DEV)
+    ops.fedopt_step(old64, ups, ns, Ns, first=True, final=True, m_in=m64, m_out=m2, v_in=v, v_out=v2, out=out2,
+                    serveropt="adam", **kw)
+    torch.cuda.synchronize()
+    for lo in (0, 123_456_789, P - 100_000):
+        sl = slice(lo, lo + 100_000)
+        st = ref.FedOptState()
+        upd = [([u[sl].cpu().numpy()], n) for u, n in zip(ups, ns)]
+        want1, _ = ref.fedopt_combine(st, upd, [old[sl].cpu().numpy()], params)
+        assert_lists_identical([out[sl].cpu().numpy(), v[sl].cpu().numpy()], [want1[0], st.v[0]], f"round 1 {lo}")
+        st.m = [st.m[0].astype(np.float64)]       # the steady state takes m in float64 (round >= 3)
+        want2, _ = ref.fedopt_combine(st, upd, want1, params)
+        assert_lists_identical([out2[sl].cpu().numpy(), m2[sl].cpu().numpy(), v2[sl].cpu().numpy()],
+                               [want2[0], st.m[0], st.v[0]], f"steady {lo}")
+    del ups, old, old64, m64, m2, v, v2, out, out2
+    torch.cuda.empty_cache()
+
+
 # ------------------------------------------------------------------------- Control.reduce
 @pytest.mark.parametrize("workers", [1, 3])
 @pytest.mark.parametrize("name", case_names("reduce"))
