@@ -340,6 +340,42 @@ def test_fedopt_configs3_size_sampled():
     torch.cuda.empty_cache()
 
 
+def test_fedopt_waves_1b_sampled():
+    """BASELINE configs[4]'s model size: 1 B-param bf16 updates streamed from pinned host memory in
+    waves of 8 over 2 parameter slices, FedYogi. 16 updates (8 distinct pinned buffers, each sent
+    twice, as bench.py's fedopt_waves does); the oracle checks 3 slices of 100 K elements."""
+    from fedn_amd.waves import WaveFedOpt
+    P, K, pool = 1_000_000_000, 16, 8
+    g = torch.Generator(device=DEV).manual_seed(6)
+    base = torch.randn(P, generator=g, device=DEV)
+    host = []
+    for _ in range(pool):
+        h = torch.empty(P, dtype=torch.bfloat16, pin_memory=True)
+        h.copy_((base + 0.01 * torch.randn(P, generator=g, device=DEV)).to(torch.bfloat16))
+        host.append(h)
+    base = base.cpu()
+    ups = [host[k % pool] for k in range(K)]
+    ns = [int(v) for v in np.random.default_rng(6).integers(1, 5001, K)]
+    params = {"serveropt": "yogi", "learning_rate": 1e-3, "beta1": 0.9, "beta2": 0.99, "tau": 1e-4}
+    wf = WaveFedOpt([DEV, DEV], P, wave=8)
+    old = wf.slices(base)
+    outs = wf.round(ups, ns, old, params)
+    lo_hi = wf.bounds
+    for lo in (0, 499_999_950, P - 100_000):
+        sl = slice(lo, lo + 100_000)
+        st = ref.FedOptState()
+        upd = [([u[sl].float().numpy()], n) for u, n in zip(ups, ns)]
+        want, _ = ref.fedopt_combine(st, upd, [base[sl].numpy()], params)
+        got = np.empty(100_000)
+        for d, (a, b) in enumerate(lo_hi):      # the slice may straddle the two devices' parts
+            s0, s1 = max(lo, a), min(lo + 100_000, b)
+            if s1 > s0:
+                got[s0 - lo:s1 - lo] = outs[d][s0 - a:s1 - a].cpu().numpy()
+        assert_lists_identical([got], [want[0]], f"slice {lo}")
+    del host, ups, outs, old, wf
+    torch.cuda.empty_cache()
+
+
 # ------------------------------------------------------------------------- Control.reduce
 @pytest.mark.parametrize("workers", [1, 3])
 @pytest.mark.parametrize("name", case_names("reduce"))
