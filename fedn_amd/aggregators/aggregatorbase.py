@@ -8,7 +8,10 @@ module at ``fedn/network/combiner/aggregators/<name>.py`` re-exports our Aggrega
 (see INTEGRATION.md).
 """
 import importlib
+import io
 import os
+import threading
+import zipfile
 from abc import ABC, abstractmethod
 from collections import deque
 from concurrent.futures import ThreadPoolExecutor
@@ -33,6 +36,15 @@ def model_nbytes(model):
         return int(sum(np.asarray(a).nbytes for a in model))
     except Exception:  # noqa: BLE001
         return 0
+
+
+def npz_decoded_bytes(data):
+    """Decoded size of an npz payload from its zip central directory (no inflate), else None."""
+    try:
+        with zipfile.ZipFile(io.BytesIO(data)) as z:
+            return sum(i.file_size for i in z.infolist())
+    except Exception:  # noqa: BLE001 — not an npz: the size is learned from the first decoded update
+        return None
 
 
 def requeue_front(q, items):
@@ -82,6 +94,20 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
     pool = ThreadPoolExecutor(max_workers=ahead, thread_name_prefix="fedn_amd_load")
     window = deque()
     size = size_box if size_box is not None else [None]   # bytes of one decoded update, once known
+    # with no size yet, the first update's raw bytes (UpdateHandler.load_model_update_byte,
+    # updatehandler.py:119-144) show it from the npz directory before its decode ends
+    known = threading.Event()
+    peek = [size[0] is None and hasattr(update_handler, "load_model_update_byte")]
+
+    def peek_then_load(mu):
+        try:
+            est = npz_decoded_bytes(update_handler.load_model_update_byte(mu)[0])
+            if est and size[0] is None:
+                size[0] = est
+        except Exception:  # noqa: BLE001 — no raw bytes: the first decode shows the size
+            pass
+        known.set()
+        return update_handler.load_model_update(mu, helper)
 
     def allowed():
         if size[0] is None:
@@ -96,7 +122,11 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
             except Exception as e:  # noqa: BLE001
                 window.append((None, None, e))
                 continue
-            window.append((mu, pool.submit(update_handler.load_model_update, mu, helper), None))
+            if peek[0]:
+                peek[0] = False
+                window.append((mu, pool.submit(peek_then_load, mu), None))
+            else:
+                window.append((mu, pool.submit(update_handler.load_model_update, mu, helper), None))
 
     first = [True]
 
@@ -113,6 +143,9 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
         fill()
         while window:
             mu, fut, err = window.popleft()
+            if fut is not None and size[0] is None:
+                while not fut.done() and not known.wait(0.002):
+                    pass                  # the first update's npz directory admits the others early
             fill(held=1)
             yield mu, (_raiser(err) if err is not None else sized(fut))
             fill()

@@ -11,24 +11,13 @@ deleted from the repository whether or not it could be fetched (control.py:690).
 
 Use it from FEDn by mixing :class:`GpuReduceMixin` into ``Control``.
 """
-import io
 import threading
 import time
-import zipfile
 from concurrent.futures import ThreadPoolExecutor
 
-from .aggregators.aggregatorbase import LOAD_AHEAD_BYTES, model_nbytes
+from .aggregators.aggregatorbase import LOAD_AHEAD_BYTES, model_nbytes, npz_decoded_bytes
 from .aggregators.fedavg import default_device
 from .staging import FedAvgPipeline
-
-
-def npz_decoded_bytes(data):
-    """Decoded size of an npz payload from its zip central directory (no inflate), else None."""
-    try:
-        with zipfile.ZipFile(io.BytesIO(data)) as z:
-            return sum(i.file_size for i in z.infolist())
-    except Exception:  # noqa: BLE001 — not an npz: the size is learned from the first decoded model
-        return None
 
 
 def _fetch_load(fetch, load, model_id, on_size=None):

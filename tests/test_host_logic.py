@@ -336,3 +336,46 @@ def test_queued_updates_size_hint_across_rounds():
             load()
         assert box[0] == 1000
         assert first_peak == (1 if rnd == 0 else 6)
+
+
+def test_queued_updates_first_round_peeks_npz_size():
+    """With no size yet, the first update's raw npz bytes (load_model_update_byte) show the decoded
+    size from the zip directory, so the first round's decodes start together too."""
+    import io
+    import threading
+    import time
+
+    from fedn_amd.aggregators.aggregatorbase import queued_updates
+
+    class Helper:
+        def load(self, f):
+            z = np.load(f)
+            return [z[k] for k in sorted(z.files, key=int)]
+
+    uh = MemoryUpdateHandler()
+    for k in range(5):
+        b = io.BytesIO()
+        np.savez_compressed(b, **{"0": np.full(250, k, np.float32)})
+        uh.submit_bytes(b.getvalue(), 1)
+    live, peak, lock = [0], [0], threading.Lock()
+    inner = uh.load_model_update
+
+    def load_model_update(mu, helper):
+        with lock:
+            live[0] += 1
+            peak[0] = max(peak[0], live[0])
+        time.sleep(0.05)
+        with lock:
+            live[0] -= 1
+        return inner(mu, helper)
+    uh.load_model_update = load_model_update
+    box = [None]
+    got = []
+    it = queued_updates(uh, Helper(), ahead=8, ahead_bytes=1 << 20, size_box=box)
+    mu, load = next(it)
+    time.sleep(0.03)
+    assert peak[0] == 5                          # every decode running before the first one ended
+    got.append(int(load()[0][0][0]))
+    for mu, load in it:
+        got.append(int(load()[0][0][0]))
+    assert got == [0, 1, 2, 3, 4] and box[0] == 1000
