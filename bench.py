@@ -143,7 +143,8 @@ def timed_steps(step, steps, stream, world, device, on_cpu):
     """Barrier + sync, ``steps`` calls of ``step`` bracketed by HIP events on ``stream``, sync +
     barrier; returns (wall seconds, mean event ms), each the max over ranks."""
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    if world > 1:
+    ranks = dist.is_initialized()
+    if ranks:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
@@ -152,12 +153,12 @@ def timed_steps(step, steps, stream, world, device, on_cpu):
         step()
         e.record(stream)
     torch.cuda.synchronize(device)
-    if world > 1:
+    if ranks:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ev_ms = sum(s.elapsed_time(e) for s, e in ev) / steps
     t = torch.tensor([elapsed, ev_ms], dtype=torch.float64, device="cpu" if on_cpu else device)
-    if world > 1:
+    if ranks:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t[0]), float(t[1])
 
@@ -285,9 +286,13 @@ def main():
     # FEDN_AMD_BENCH_ONE_GPU=1: rehearsal of the N>1 code path on a one-GPU box (every rank on
     # cuda:0, gloo instead of RCCL); never used for reported numbers
     rehearsal = os.environ.get("FEDN_AMD_BENCH_ONE_GPU") == "1"
+    # FEDN_AMD_BENCH_RCCL_WORLD1=1: the N>1 code path at world size 1 over a real RCCL communicator
+    # (every all-gather issued as a collective), so the RCCL calls run on a one-GPU box; never used
+    # for reported numbers
+    rccl1 = world == 1 and os.environ.get("FEDN_AMD_BENCH_RCCL_WORLD1") == "1"
     device = torch.device("cuda", 0 if rehearsal else local)
     torch.cuda.set_device(device)
-    if world > 1:
+    if world > 1 or rccl1:
         if rehearsal:
             dist.init_process_group("gloo")
         else:
@@ -305,7 +310,7 @@ def main():
     stream = torch.cuda.current_stream(device)
     extra = {}
 
-    if world == 1:
+    if world == 1 and not rccl1:
         P = P_total
         ups = make_updates(K, P, a.dtype, device, a.seed)
         agg = torch.empty(P, dtype=torch.float32, device=device)
@@ -325,7 +330,7 @@ def main():
                   "parallelism": "param-slice shards x1, no data-path collective"}
         scaling = "weak"
     else:
-        cyc = CyclicShardedFedAvg(P_total, chunk=-(-P_total // (world * a.ag_rounds)))
+        cyc = CyclicShardedFedAvg(P_total, chunk=-(-P_total // (world * a.ag_rounds)), collective_at_world1=rccl1)
         L = cyc.local_len
         P = L
         ups_local = make_updates(K, L, a.dtype, device, a.seed + 1000 * rank)   # this rank's chunks, every client
@@ -358,7 +363,11 @@ def main():
         scaling = "strong"
         extra["fold_allgather_ms"] = elapsed / a.steps * 1e3
         if not a.no_side:
-            extra.update(multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, ups_local, stream))
+            extra.update(multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, ups_local, stream,
+                                        rccl1))
+        if rccl1:
+            extra["rccl_world1"] = ("rehearsal: the N>1 path at world size 1 over RCCL (all-gathers issued as "
+                                    "collectives); not a reported number")
         ups = ups_local
 
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
@@ -366,7 +375,7 @@ def main():
     base = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
         base = cpu_baseline(ups, ns, agg, a.cpu_sample)
-    if world == 1:
+    if world == 1 and not rccl1:
         # the model to the host, FEDn's consumer (roundhandler.py:465-468); value excludes it
         host = torch.empty(P, dtype=torch.float32, pin_memory=True)
         for _ in range(2):
@@ -401,11 +410,11 @@ def main():
         }
         line.update(extra)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
-def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, ups_local, stream):
+def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, ups_local, stream, rccl1=False):
     """The N > 1 measurements beside the line (none of them is in value)."""
     from fedn_amd import ops
     from fedn_amd.sharded import ShardedFedAvg
@@ -413,7 +422,7 @@ def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, u
     on_cpu = rehearsal
 
     def plain_allgather():
-        sh = ShardedFedAvg(P_total)
+        sh = ShardedFedAvg(P_total, collective_at_world1=rccl1)
         src = torch.zeros(sh.hi - sh.lo, dtype=torch.float32, device=device)
         gsrc = src.cpu() if rehearsal else src
         for _ in range(2):

@@ -39,11 +39,13 @@ class ShardedFedAvg:
     logic can be exercised on CPU-only ranks (gloo) by tests with a reference fold.
     """
 
-    def __init__(self, P, group=None, fold_fn=None, align=ALIGN_ELEMS):
+    def __init__(self, P, group=None, fold_fn=None, align=ALIGN_ELEMS, collective_at_world1=False):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.P = P
+        # issue the collectives even at world size 1 (a one-GPU rehearsal of the RCCL calls)
+        self.collective = self.world > 1 or (collective_at_world1 and dist.is_initialized())
         self.bounds = shard_bounds(P, self.world, align)
         self.lo, self.hi = self.bounds[self.rank]
         self.shard = self.bounds[0][1] - self.bounds[0][0]   # padded per-rank length
@@ -60,7 +62,7 @@ class ShardedFedAvg:
 
     def allgather(self, agg_local):
         """Reassemble the full P-element model on every rank (RCCL all-gather over xGMI)."""
-        if self.world == 1:
+        if not self.collective:
             return agg_local
         buf = agg_local
         if agg_local.numel() != self.shard:
@@ -151,11 +153,13 @@ class CyclicShardedFedAvg:
     folded by the same kernel and client table: bit-identical to one GPU.
     """
 
-    def __init__(self, P, chunk=1 << 22, group=None, fold_fn=None, align=ALIGN_ELEMS):
+    def __init__(self, P, chunk=1 << 22, group=None, fold_fn=None, align=ALIGN_ELEMS, collective_at_world1=False):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.P = P
+        # issue the all-gathers even at world size 1 (a one-GPU rehearsal of the RCCL calls)
+        self.collective = self.world > 1 or (collective_at_world1 and dist.is_initialized())
         self.C = max(align, -(-chunk // align) * align)
         nchunks = max(1, -(-P // self.C))
         self.rounds = -(-nchunks // self.world)
@@ -186,19 +190,20 @@ class CyclicShardedFedAvg:
         """Fold every round and gather it as soon as it is folded; returns the full model
         (``full[:P]``; on the host for gloo). ``agg_local`` / ``updates_local``: local_len each."""
         C, W = self.C, self.world
-        gloo = W > 1 and dist.get_backend(self.group) == "gloo"
+        coll = self.collective
+        gloo = coll and dist.get_backend(self.group) == "gloo"
         dev = agg_local.device
         on_gpu = dev.type == "cuda" and not gloo
         if out is None:
             out = torch.empty(self.full_len, dtype=agg_local.dtype, device=dev if not gloo else "cpu")
-        if on_gpu and W > 1 and self._comm is None:
+        if on_gpu and coll and self._comm is None:
             self._comm = torch.cuda.Stream(dev)
         cur = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
         for i in range(self.rounds):
             sl = slice(i * C, (i + 1) * C)
             self.fold_fn(agg_local[sl], [u[sl] for u in updates_local], n, N, init)
             dst = out[i * W * C:(i + 1) * W * C]
-            if W == 1:
+            if not coll:
                 dst.copy_(agg_local[sl], non_blocking=True)
             elif on_gpu:
                 ev = torch.cuda.Event()
@@ -209,6 +214,6 @@ class CyclicShardedFedAvg:
             else:
                 src = agg_local[sl].to("cpu")
                 dist.all_gather(list(dst.chunk(W)), src, group=self.group)
-        if on_gpu and W > 1:
+        if on_gpu and coll:
             cur.wait_stream(self._comm)
         return out[:self.P]

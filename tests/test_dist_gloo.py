@@ -189,3 +189,44 @@ def test_cyclic_fold_allgather_gloo(world, P, chunk):
     covered.sort()
     assert covered[0][0] == 0 and covered[-1][1] == P
     assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
+
+
+def _world1_worker(rank, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from fedn_amd.sharded import CyclicShardedFedAvg
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        rng = np.random.default_rng(23)
+        P, K = 9_001, 4
+        base = rng.standard_normal(P).astype(np.float32)
+        ups = [torch.from_numpy((base + 0.01 * rng.standard_normal(P)).astype(np.float32)) for _ in range(K)]
+        ns = [int(v) for v in rng.integers(1, 5001, K)]
+        off = CyclicShardedFedAvg(P, chunk=2048, fold_fn=_oracle_fold)
+        on = CyclicShardedFedAvg(P, chunk=2048, fold_fn=_oracle_fold, collective_at_world1=True)
+        sh = ShardedFedAvg(P, collective_at_world1=True)
+        res = []
+        for cs in (off, on):
+            agg = torch.empty(cs.local_len, dtype=torch.float32)
+            res.append(cs.fold_allgather(agg, [cs.local(u) for u in ups], ns, list(np.cumsum(ns)), init=True).numpy())
+        q.put((off.collective, on.collective, sh.collective, res[0].copy(), res[1].copy(),
+               sh.allgather(torch.from_numpy(res[0])).numpy().copy(), [u.numpy() for u in ups], ns))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collective_at_world1_gloo():
+    """collective_at_world1 (the one-GPU rehearsal of the RCCL calls, tests/test_gpu_rccl.py): at
+    world size 1 the all-gathers are issued as collectives and give what the local copy gives."""
+    from oracle import numpy_ref as ref
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pc = mp.start_processes(_world1_worker, args=(_free_port(), q), nprocs=1, join=False, start_method="spawn")
+    off_c, on_c, sh_c, r_off, r_on, r_sh, ups, ns = q.get(timeout=120)
+    while not pc.join(timeout=60):
+        pass
+    assert (off_c, on_c, sh_c) == (False, True, True)
+    want = ref.fedavg_flat(ups, ns)
+    for got in (r_off, r_on, r_sh):
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))

@@ -18,7 +18,9 @@ Updates are pushed exactly as the combiner receives them: npz bytes uploaded thr
 
 Import workaround: ``fedn/__init__.py`` and ``fedn/common/log_config.py``
 pull in opentelemetry (not installed). We pre-register a bare ``fedn`` package and a stub
-``fedn.common.log_config`` exposing ``logger``; nothing else is stubbed.
+``fedn.common.log_config`` exposing ``logger``; nothing else is stubbed. ``Control.reduce`` is
+run from control.py's own source without importing its module (which needs the absent
+``tenacity``): see ``_control_reduce``.
 
 Usage:  python tools/gen_golden.py            (writes tests/golden/*.npz + manifest.json)
 """
@@ -266,13 +268,59 @@ def helper_power_norm(ref, rng):
     return d
 
 
+class _Repository:
+    """The controller's model repository as Control.reduce uses it (control.py:668,690):
+    get_model(model_id) -> the stored bytes (raises for a model that cannot be fetched),
+    delete_model(model_id)."""
+
+    def __init__(self, blobs):
+        self.blobs, self.deleted = blobs, []
+
+    def get_model(self, model_id):
+        if self.blobs[model_id] is None:
+            raise RuntimeError(f"model {model_id} not in the repository")
+        return self.blobs[model_id]
+
+    def delete_model(self, model_id):
+        self.deleted.append(model_id)
+
+
+def _control_reduce(ref, models, plan):
+    """Run the REAL ``Control.reduce`` (fedn/network/controller/control.py:648-693).
+
+    control.py's module imports ``tenacity`` (absent from the image; it decorates other methods),
+    so the module itself is not imported. The method is taken from control.py's own source with
+    ``ast`` and compiled from that file (line numbers kept), in a namespace holding the real
+    objects its body names: ``time``, the fedn logger and modelservice.load_model_from_bytes.
+    ``self`` supplies ``repository`` (get_model / delete_model) and ``get_helper()`` -> the real
+    numpyhelper. Each combiner model is stored as the bytes the real
+    modelservice.serialize_model_to_BytesIO writes; "missing" makes get_model raise."""
+    import ast
+    import time
+
+    from fedn.common.log_config import logger
+    from fedn.network.combiner.modelservice import load_model_from_bytes, serialize_model_to_BytesIO
+    path = os.path.join(REF, "fedn", "network", "controller", "control.py")
+    with open(path) as f:
+        tree = ast.parse(f.read(), path)
+    cls = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "Control")
+    fn = next(n for n in cls.body if isinstance(n, ast.FunctionDef) and n.name == "reduce")
+    ns = {"time": time, "logger": logger, "load_model_from_bytes": load_model_from_bytes}
+    exec(compile(ast.Module(body=[fn], type_ignores=[]), path, "exec"), ns)  # noqa: S102
+    helper = ref["Helper"]()
+    blobs = {f"model-{c}": None if kind == "missing" else serialize_model_to_BytesIO(m, helper).getvalue()
+             for c, (m, kind) in enumerate(zip(models, plan))}
+    ctl = types.SimpleNamespace(repository=_Repository(blobs), get_helper=lambda: helper)
+    combiners = [{"name": f"combiner-{c}", "model_id": f"model-{c}"} for c in range(len(models))]
+    model, meta = ns["reduce"](ctl, combiners)
+    assert ctl.repository.deleted == [c["model_id"] for c in combiners]
+    assert sorted(meta) == ["time_aggregate_model", "time_fetch_model", "time_load_model"]
+    return model
+
+
 def reduce_case(ref, name, rng, shapes, plan):
-    """Control.reduce (fedn/network/controller/control.py:648-693). control.py cannot be imported
-    here (it needs `tenacity`, absent from the image, and we do not stub libraries), so its
-    loop is restated line by line below; every arithmetic step is the REAL
-    numpyhelper.Helper.increment_average(model, model_next, 1.0, i) (control.py:682).
+    """Control.reduce (control.py:648-693), the real method (_control_reduce).
     plan: per combiner "ok" | "missing" (fetch fails -> data None) | "bad" (shape mismatch)."""
-    h = ref["Helper"]()
     d = {"kind": np.array("reduce"), "name": np.array(name), "plan": np.array(json.dumps(plan))}
     base = _rng_model(rng, shapes, np.float32)
     models = []
@@ -283,15 +331,7 @@ def reduce_case(ref, name, rng, shapes, plan):
             m = _perturb(rng, base, np.float32, 0.05)
         models.append(m)
         _store_list(d, f"c{c}", m)
-    i, model = 1, None
-    for m, kind in zip(models, plan):                      # control.py:662-690
-        data = None if kind == "missing" else m
-        if data is not None:
-            try:
-                model = h.increment_average(model, data, 1.0, i)
-            except Exception:  # noqa: BLE001  (control.py:683-686: reload and replace)
-                model = data
-            i = i + 1
+    model = _control_reduce(ref, models, plan)
     d["out_none"] = np.array(model is None)
     if model is not None:
         _store_list(d, "out", model)
@@ -369,9 +409,8 @@ def fedopt_clients_case(ref, name, rng, old_spec, rounds, params=None):
 
 
 def reduce_dtypes_case(ref, name, rng, shapes, dtypes):
-    """Control.reduce (control.py:648-693, loop restated as in reduce_case) over combiner models
-    saved in different dtypes: every fold is the REAL numpyhelper.increment_average."""
-    h = ref["Helper"]()
+    """Control.reduce (control.py:648-693, the real method: _control_reduce) over combiner models
+    saved in different dtypes."""
     plan = ["ok"] * len(dtypes)
     d = {"kind": np.array("reduce"), "name": np.array(name), "plan": np.array(json.dumps(plan))}
     models = []
@@ -379,13 +418,7 @@ def reduce_dtypes_case(ref, name, rng, shapes, dtypes):
         m = [_tensor(rng, s, dt) for s in shapes]
         models.append(m)
         _store_list(d, f"c{c}", m)
-    i, model = 1, None
-    for m in models:
-        try:
-            model = h.increment_average(model, m, 1.0, i)
-        except Exception:  # noqa: BLE001  (control.py:683-686)
-            model = m
-        i = i + 1
+    model = _control_reduce(ref, models, plan)
     _store_list(d, "out", model)
     d["out_none"] = np.array(False)
     return d
@@ -623,6 +656,15 @@ def edge_cases(ref):
     ]
 
 
+def reduce_cases(ref):
+    """Control.reduce (control.py:648-693) over combiner models."""
+    rng = np.random.default_rng(4)
+    return [reduce_case(ref, "reduce_3", rng, ODD_SHAPES, ["ok", "ok", "ok"]),
+            reduce_case(ref, "reduce_missing", rng, ODD_SHAPES, ["missing", "ok", "missing", "ok", "ok"]),
+            reduce_case(ref, "reduce_bad_replaces", rng, ODD_SHAPES, ["ok", "ok", "bad", "ok"]),
+            reduce_case(ref, "reduce_single", rng, ODD_SHAPES, ["ok"])]
+
+
 def main():
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     ref = _import_reference()
@@ -637,6 +679,8 @@ def main():
         return _write([helper_power_norm(ref, np.random.default_rng(9))], merge=True)
     if only == "edge":
         return _write(edge_cases(ref), merge=True)
+    if only == "reduce":
+        return _write(reduce_cases(ref) + mixed_cases(ref)[-2:], merge=True)
     cases = []
     cases.append(helper_kat(ref))
     rng = np.random.default_rng(1)
@@ -679,12 +723,7 @@ def main():
     rng = np.random.default_rng(5)
     cases.append(fedavg_mixed_case(ref, "fedavg_mixed_int_k5", rng, rng.integers(1, 5001, 5)))
 
-    # Control.reduce -------------------------------------------------------------------
-    rng = np.random.default_rng(4)
-    cases.append(reduce_case(ref, "reduce_3", rng, ODD_SHAPES, ["ok", "ok", "ok"]))
-    cases.append(reduce_case(ref, "reduce_missing", rng, ODD_SHAPES, ["missing", "ok", "missing", "ok", "ok"]))
-    cases.append(reduce_case(ref, "reduce_bad_replaces", rng, ODD_SHAPES, ["ok", "ok", "bad", "ok"]))
-    cases.append(reduce_case(ref, "reduce_single", rng, ODD_SHAPES, ["ok"]))
+    cases += reduce_cases(ref)
 
     cases += sf_cases(ref)
     cases += helper_cases(ref)
