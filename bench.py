@@ -54,6 +54,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "aggregated params/sec (device-resident) — FedAvg 64-client reduce, 100M fp32"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+AG_ROUNDS = (1, 2, 4, 8, 16)   # N > 1 candidates for the fold + all-gather rounds (--ag-rounds 0)
 
 
 def parse():
@@ -66,7 +67,9 @@ def parse():
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32")
     ap.add_argument("--cpu-sample", type=int, default=100_000_000,
                     help="params per client in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--ag-rounds", type=int, default=8, help="N > 1: rounds of the overlapped fold + all-gather")
+    ap.add_argument("--ag-rounds", type=int, default=0,
+                    help="N > 1: rounds of the overlapped fold + all-gather (0 = the fastest of AG_ROUNDS, chosen in "
+                         "the untimed warm-up)")
     ap.add_argument("--fedopt-params", type=int, default=350_000_000, help="configs[3] side field (0 = skip)")
     ap.add_argument("--fedopt-clients", type=int, default=32)
     ap.add_argument("--no-side", action="store_true", help="N > 1: skip the beside-the-line measurements")
@@ -330,15 +333,39 @@ def main():
                   "parallelism": "param-slice shards x1, no data-path collective"}
         scaling = "weak"
     else:
-        cyc = CyclicShardedFedAvg(P_total, chunk=-(-P_total // (world * a.ag_rounds)), collective_at_world1=rccl1)
+        # rounds of the overlapped fold + all-gather: fixed (--ag-rounds R) or chosen in the untimed warm-up
+        # among AG_ROUNDS (--ag-rounds 0, the default): the all-gather over xGMI, not the fold, sets the
+        # step at every N > 1, and its efficiency depends on the message size (round i gathers W x C
+        # params) in a way only the node itself can tell
+        cands = [a.ag_rounds] if a.ag_rounds > 0 else list(AG_ROUNDS)
+        geoms = {R: CyclicShardedFedAvg(P_total, chunk=-(-P_total // (world * R)), collective_at_world1=rccl1)
+                 for R in cands}
+        Lmax = max(c.local_len for c in geoms.values())
+        ups_all = make_updates(K, Lmax, a.dtype, device, a.seed + 1000 * rank)   # this rank's chunks, every client
+        agg_all = torch.empty(Lmax, dtype=torch.float32, device=device)
+        full_all = None if rehearsal else torch.empty(max(c.full_len for c in geoms.values()), dtype=torch.float32,
+                                                      device=device)
+
+        def make_step(c):
+            loc = [u[:c.local_len] for u in ups_all]
+            ag, out = agg_all[:c.local_len], None if rehearsal else full_all[:c.full_len]
+            return lambda: c.fold_allgather(ag, loc, ns, Ns, init=True, out=out)
+
+        tuned = {}
+        if len(cands) > 1:
+            for R, c in geoms.items():
+                st = make_step(c)
+                for _ in range(2):
+                    st()
+                el, _ = timed_steps(st, 5, stream, world, device, rehearsal)
+                tuned[R] = el / 5 * 1e3
+        R = min(tuned, key=tuned.get) if tuned else cands[0]
+        cyc = geoms[R]
         L = cyc.local_len
         P = L
-        ups_local = make_updates(K, L, a.dtype, device, a.seed + 1000 * rank)   # this rank's chunks, every client
-        agg = torch.empty(L, dtype=torch.float32, device=device)
-        full = None if rehearsal else torch.empty(cyc.full_len, dtype=torch.float32, device=device)
-
-        def step():
-            cyc.fold_allgather(agg, ups_local, ns, Ns, init=True, out=full)
+        ups_local = [u[:L] for u in ups_all]
+        agg = agg_all[:L]
+        step = make_step(cyc)
 
         def fold_only():
             for i in range(cyc.rounds):
@@ -352,14 +379,15 @@ def main():
             fold_only()
         _, kern_ms = timed_steps(fold_only, a.steps, stream, world, device, rehearsal)
         alg_bytes = K * L * in_bytes + L * 4              # this rank's fold, per step (all rounds)
-        workload = f"fedavg_k{K}_p{L}_{a.dtype}_rank_of_{world}"
+        workload = f"fedavg_k{K}_p{L}_r{cyc.rounds}_{a.dtype}_rank_of_{world}"
         kernel = (f"{fold_kernel_label(cyc.C, in_bytes, K)} over this rank's {cyc.rounds} chunks of {cyc.C} params "
                   "(fold-only timing; max over ranks)")
         config = {"workload": f"FedAvg {K} clients x {P_total} params {a.dtype}, param-sharded block-cyclically over "
                               f"{world} GPUs; RCCL all-gather of each folded round overlapped with the next round's "
                               "fold, inside the timed step (BASELINE configs[2])",
                   "clients": K, "params_per_gpu": L, "global_params": P_total, "rounds": cyc.rounds,
-                  "chunk": cyc.C, "parallelism": f"param-slice x{world} + RCCL all-gather"}
+                  "chunk": cyc.C, "parallelism": f"param-slice x{world} + RCCL all-gather",
+                  "rounds_tuned_ms": {str(k): v for k, v in tuned.items()} or None}
         scaling = "strong"
         extra["fold_allgather_ms"] = elapsed / a.steps * 1e3
         if not a.no_side:

@@ -381,15 +381,19 @@ def test_queued_updates_first_round_peeks_npz_size():
     assert got == [0, 1, 2, 3, 4] and box[0] == 1000
 
 
+@pytest.mark.parametrize("R", [1, 2, 4, 8, 16])
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_pmc_rank_geometry_matches_bench(world, monkeypatch):
+def test_pmc_rank_geometry_matches_bench(world, R, monkeypatch):
     """tools/pmc_rank_fold.py replays one rank's fold of bench.py --gpus N; its chunk / rounds /
-    local length must be CyclicShardedFedAvg's for bench.py's chunk choice (P / (N * 8))."""
+    local length must be CyclicShardedFedAvg's for bench.py's chunk choice (P / (N * R)) for every
+    candidate R of bench.AG_ROUNDS."""
+    import bench
     import fedn_amd.sharded as sh
     from tools.pmc_rank_fold import rank_geometry
     monkeypatch.setattr(sh.dist, "is_initialized", lambda: True)
     monkeypatch.setattr(sh.dist, "get_world_size", lambda group=None: world)
     monkeypatch.setattr(sh.dist, "get_rank", lambda group=None: 0)
     P = 100_000_000
-    cyc = sh.CyclicShardedFedAvg(P, chunk=-(-P // (world * 8)))
-    assert rank_geometry(P, world, 8) == (cyc.C, cyc.rounds, cyc.local_len)
+    assert R in bench.AG_ROUNDS
+    cyc = sh.CyclicShardedFedAvg(P, chunk=-(-P // (world * R)))
+    assert rank_geometry(P, world, R) == (cyc.C, cyc.rounds, cyc.local_len)

@@ -75,13 +75,16 @@ for s in $STEPS; do
       done
       echo "pmc: now run  python tools/pmc_traffic.py --session $OUT  in the build container" ;;
     pmcrank)
-      # HBM traffic of one rank's fold at N = 2, 4, 8 (bench.py's N > 1 roofline), replayed on this GPU
+      # HBM traffic of one rank's fold at N = 2, 4, 8 for every fold + all-gather round count bench.py may
+      # choose (AG_ROUNDS; bench.py's N > 1 roofline), replayed on this GPU
       sha256sum fedn_amd/libfedagg.so | cut -c1-16 > "$OUT/lib_sha.txt"
       for n in 2 4 8; do
-        for c in FETCH_SIZE WRITE_SIZE; do
-          cd /tmp && timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmcrank$n/pmc_$c" -o run -- \
-            python3 "$GRAFT_REPO_ROOT/tools/pmc_rank_fold.py" --world $n > "$GRAFT_REPO_ROOT/$OUT/pmcrank${n}_$c.log" 2>&1; rc=$?
-          cd "$GRAFT_REPO_ROOT"; echo "pmcrank$n $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+        for R in 1 2 4 8 16; do
+          for c in FETCH_SIZE WRITE_SIZE; do
+            cd /tmp && timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmcrank${n}_r$R/pmc_$c" -o run -- \
+              python3 "$GRAFT_REPO_ROOT/tools/pmc_rank_fold.py" --world $n --ag-rounds $R --steps 2 > "$GRAFT_REPO_ROOT/$OUT/pmcrank${n}_r${R}_$c.log" 2>&1; rc=$?
+            cd "$GRAFT_REPO_ROOT"; echo "pmcrank$n r$R $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+          done
         done
       done
       echo "pmcrank: now run  python tools/pmc_traffic.py --rank-session $OUT  in the build container" ;;

@@ -47,7 +47,7 @@ def main():
         ops.fedavg_fold(agg, ups, ns, Ns, init=True)
     torch.cuda.synchronize()
     print(json.dumps({"world": a.world, "chunk": C, "rounds": rounds, "local_len": L,
-                      "workload": f"fedavg_k{a.clients}_p{L}_f32_rank_of_{a.world}"}), flush=True)
+                      "workload": f"fedavg_k{a.clients}_p{L}_r{rounds}_f32_rank_of_{a.world}"}), flush=True)
 
 
 if __name__ == "__main__":

@@ -75,18 +75,18 @@ SESSION = [
 ]
 
 
-def record_rank(session, world):
+def record_rank(session, world, R=8, sub=None):
     """bench.py's N > 1 roofline entry: one rank's fold per step = ``rounds`` launches of the replayed
-    chunk fold (tools/pmc_rank_fold.py); bytes per step = per-launch bytes x rounds."""
+    chunk fold (tools/pmc_rank_fold.py, --ag-rounds R); bytes per step = per-launch bytes x rounds."""
     from tools.pmc_rank_fold import rank_geometry
-    C, rounds, L = rank_geometry(100_000_000, world, 8)
-    d = os.path.join(session, f"pmcrank{world}")
+    C, rounds, L = rank_geometry(100_000_000, world, R)
+    d = os.path.join(session, sub or f"pmcrank{world}")
     kernel = "k_fedavg<float, float"
     fetch, nf = per_launch(os.path.join(d, "pmc_FETCH_SIZE", "run_counter_collection.csv"), kernel)
     write, nw = per_launch(os.path.join(d, "pmc_WRITE_SIZE", "run_counter_collection.csv"), kernel)
     read_b, write_b = 2 * fetch * 1024 * rounds, write * 1024 * rounds
     alg = rounds * (64 * C * 4 + C * 4)
-    key = f"fedavg_k64_p{L}_f32_rank_of_{world}"
+    key = f"fedavg_k64_p{L}_r{rounds}_f32_rank_of_{world}"
     out = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     db = json.load(open(out)) if os.path.exists(out) else {}
     db[key] = {"bytes": read_b + write_b, "read_bytes": read_b, "write_bytes": write_b,
@@ -103,7 +103,12 @@ def record_rank(session, world):
 def main():
     if sys.argv[1] == "--rank-session":
         for world in (2, 4, 8):
-            record_rank(sys.argv[2], world)
+            for R in (1, 2, 4, 8, 16):   # bench.py AG_ROUNDS
+                sub = f"pmcrank{world}_r{R}"
+                if os.path.isdir(os.path.join(sys.argv[2], sub)):
+                    record_rank(sys.argv[2], world, R, sub)
+            if os.path.isdir(os.path.join(sys.argv[2], f"pmcrank{world}")):   # round-2 sessions: R = 8 only
+                record_rank(sys.argv[2], world)
         return
     if sys.argv[1] == "--session":
         for sub, key, kernel, alg in SESSION:
