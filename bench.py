@@ -33,6 +33,9 @@ Also measured in the same run:
   cpu_baseline  the numpy restatement of numpyhelper.increment_average (oracle/, bit-equal to
                 FEDn) on a bounded sample (K clients x S params) on one host core; its result is
                 also compared bit-for-bit with the GPU aggregate of the same elements
+  achievable    (N = 1) the achievable-peak reference on the same box: a STREAM-style
+                copy and a streaming read of one 4 GiB buffer (probe kernels of libfedagg_probe.so)
+                and the headline kernel's fraction of the copy rate
   fedopt        (N = 1) BASELINE configs[3]: FedAdam over 32 device-resident 350 M fp32 updates,
                 one fused pseudo-gradient + server-step launch; round 1 and steady state (fp64
                 old / m / v, the dtype flow fedopt.py produces), each with its own roofline and
@@ -80,6 +83,8 @@ def parse():
     ap.add_argument("--waves-clients", type=int, default=128)
     ap.add_argument("--waves-pool", type=int, default=8, help="distinct pinned host updates (reused cyclically)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-achievable", dest="achievable", action="store_false",
+                    help="N = 1: skip the achievable-peak copy / read reference")
     return ap.parse_args()
 
 
@@ -164,6 +169,35 @@ def timed_steps(step, steps, stream, world, device, on_cpu):
     if ranks:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t[0]), float(t[1])
+
+
+def achieved_of(alg_bytes, kern_ms):
+    return alg_bytes / (kern_ms / 1e3) / 1e9
+
+
+def achievable_side(device, headline_gbs, nbytes=4 << 30):
+    """SURVEY.md §8(d)'s achievable-peak reference on this box: a STREAM-style copy (16 B per lane,
+    read once + written once) and a streaming read of one ``nbytes`` buffer, by the probe kernels
+    of libfedagg_probe.so (measurement only; the headline ran on libfedagg.so)."""
+    from fedn_amd import _abi, ops
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=device).fill_(1.0)
+    dst = torch.empty_like(src)
+    stream = torch.cuda.current_stream(device)
+    res = {}
+    with _abi.use_probe():
+        sink = ops.stream_read_sink(src)
+        for name, fn, moved in (("copy", lambda: ops.stream_copy(dst, src, stream=stream), 2 * nbytes),
+                                ("read", lambda: ops.stream_read(src, sink, stream=stream), nbytes)):
+            for _ in range(3):
+                fn()
+            _, ms = timed_steps(fn, 10, stream, 1, device, False)
+            res[f"{name}_GBps"] = moved / (ms / 1e3) / 1e9
+    res["headline_frac_of_copy"] = headline_gbs / res["copy_GBps"]
+    res["kernels"] = "k_stream_copy / k_stream_read<16> (libfedagg_probe.so)"
+    res["note"] = f"achievable-peak reference on this box over one {nbytes >> 30} GiB buffer; not in value"
+    del src, dst, sink
+    torch.cuda.empty_cache()
+    return res
 
 
 def side(fn):
@@ -421,6 +455,8 @@ def main():
             extra["configs1"] = side(lambda: configs1_side(ups[:8], ns[:8], agg, stream, device, in_bytes, a))
         del ups, agg
         torch.cuda.empty_cache()
+        if a.achievable and not a.no_side:
+            extra["achievable"] = side(lambda: achievable_side(device, achieved_of(alg_bytes, kern_ms)))
         if rank == 0 and a.fedopt_params > 0:
             extra["fedopt"] = side(lambda: fedopt_side(a.fedopt_params, a.fedopt_clients, device))
 

@@ -81,7 +81,8 @@ def record_rank(session, world, R=8, sub=None):
     from tools.pmc_rank_fold import rank_geometry
     C, rounds, L = rank_geometry(100_000_000, world, R)
     d = os.path.join(session, sub or f"pmcrank{world}")
-    kernel = "k_fedavg<float, float"
+    # the product's geometry rule (fedagg.hip kPipeMinClientBytes, bench.fold_kernel_label)
+    kernel = "k_fedavg_pipe<float, float" if C * 4 >= 160 << 20 else "k_fedavg<float, float"
     fetch, nf = per_launch(os.path.join(d, "pmc_FETCH_SIZE", "run_counter_collection.csv"), kernel)
     write, nw = per_launch(os.path.join(d, "pmc_WRITE_SIZE", "run_counter_collection.csv"), kernel)
     read_b, write_b = 2 * fetch * 1024 * rounds, write * 1024 * rounds
