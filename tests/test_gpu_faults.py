@@ -1,0 +1,111 @@
+"""the kernel path never kills the round. A libfedagg call that fails (nonzero
+status -> FedAggError) is handled by the plug-ins exactly as FEDn handles an update whose fold
+raises: the update is logged and skipped with its examples still counted (fedavg.py:137-140,
+fedopt.py:103-106), and a server step that raises gives ``(None, data)`` (fedopt.py:111-116).
+Failures are injected at the C-ABI wrapper (fedn_amd.ops) before anything is enqueued, which
+is where a real status code surfaces; every result is checked against the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import assert_lists_identical
+from oracle import numpy_ref as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _failing(monkeypatch, name, fail_on):
+    """Make fedn_amd.ops.<name> raise FedAggError on the calls ``fail_on`` selects."""
+    from fedn_amd import _abi, ops
+    real = getattr(ops, name)
+    calls = []
+
+    def wrapper(*a, **kw):
+        calls.append(kw)
+        if fail_on(len(calls), kw):
+            raise _abi.FedAggError(_abi.FA_EHIP, f"{name}: injected failure (call {len(calls)})")
+        return real(*a, **kw)
+
+    monkeypatch.setattr(ops, name, wrapper)
+    return calls
+
+
+def _models(rng, K, shapes):
+    base = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    ups = [[(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base] for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    return base, ups, ns
+
+
+@pytest.mark.parametrize("shapes,fail_call", [([(1000, 1100), (999,)], 2), ([(30, 7), (5,)], 1)],
+                         ids=["large", "small_batched"])
+def test_fedavg_fold_failure_skips_the_update(monkeypatch, shapes, fail_call):
+    """Large host updates fold on arrival (one launch per update): the failing update is skipped and
+    counted. Small ones are batched (one launch per <= 64): a failing batch launch is raised at the
+    round end by ``result()`` and escapes ``combine_models``, as any exception that escapes FEDn's
+    loop aborts the round (roundhandler.py:203-205) — never a silently wrong model."""
+    from fedn_amd.aggregators.fedavg import Aggregator
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rng = np.random.default_rng(51)
+    _, ups, ns = _models(rng, 5, shapes)
+    uh = MemoryUpdateHandler()
+    agg = Aggregator(uh, device=DEV)
+    for u, n in zip(ups, ns):
+        uh.submit(u, n)
+    _failing(monkeypatch, "fedavg_fold", lambda i, kw: i == fail_call)
+    if shapes[0] == (30, 7):
+        from fedn_amd import _abi
+        with pytest.raises(_abi.FedAggError):
+            agg.combine_models(helper=None)
+        return
+    model, data = agg.combine_models(helper=None)
+
+    def increment(m1, m2, n, N):                      # the reference fold raising on update 2
+        if m2 is ups[2]:
+            raise RuntimeError("fold failed")
+        return ref.increment_average(m1, m2, n, N)
+
+    want, nr = ref.fedavg_combine(list(zip(ups, ns)), increment)
+    assert nr == data["nr_aggregated_models"] == 4
+    assert_lists_identical(model, want, "fedavg with a failed fold")
+    assert uh.model_updates.qsize() == 0
+
+
+def test_fedopt_server_step_failure_returns_none_and_keeps_state(monkeypatch):
+    """The fused server step fails (at its first launch) in round 2: ``(None, data)``, m / v stay
+    round 1's, and round 3 continues from them exactly as if round 2 had not run. (A device failure
+    part-way through a chunked step can leave v, which is updated in place, partly advanced — as
+    an exception inside fedopt.py's server step can leave self.v assigned and self.m not.)"""
+    from fedn_amd.aggregators.fedopt import Aggregator
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rng = np.random.default_rng(52)
+    shapes = [(700, 900), (333,)]
+    uh = MemoryUpdateHandler()
+    agg = Aggregator(uh, device=DEV)
+    st = ref.FedOptState()
+    old = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    fail = [False]
+    calls = _failing(monkeypatch, "fedopt_step", lambda i, kw: kw.get("final") and fail[0])
+    for r in range(3):
+        fail[0] = r == 1
+        ups = [[(o + 0.01 * rng.standard_normal(o.shape)).astype(o.dtype) for o in old] for _ in range(3)]
+        ns = [int(v) for v in rng.integers(1, 5001, 3)]
+        gid = uh.put_global_model(old, f"global-{r}")
+        for u, n in zip(ups, ns):
+            uh.submit(u, n, model_id=gid)
+        model, data = agg.combine_models(helper=None)
+        assert data["nr_aggregated_models"] == 3
+        if r == 1:
+            assert model is None
+            assert_lists_identical(agg.m, st.m, "m kept")
+            assert_lists_identical(agg.v, st.v, "v kept")
+            continue
+        want, _ = ref.fedopt_combine(st, list(zip(ups, ns)), old)
+        assert_lists_identical(model, want, f"round {r}")
+        assert_lists_identical(agg.m, st.m, f"m r{r}")
+        assert_lists_identical(agg.v, st.v, f"v r{r}")
+        old = want
+    assert any(kw.get("final") for kw in calls)
+    torch.cuda.synchronize()
