@@ -15,6 +15,7 @@ import zipfile
 from abc import ABC, abstractmethod
 from collections import deque
 from concurrent.futures import ThreadPoolExecutor
+from concurrent.futures import wait as wait_futures
 
 import numpy as np
 
@@ -22,6 +23,20 @@ AGGREGATOR_PLUGIN_PATH = "fedn_amd.aggregators.{}"
 LOAD_AHEAD = int(os.environ.get("FEDN_AMD_LOAD_AHEAD", "8"))
 # host bytes of decoded-but-not-yet-folded updates the read-ahead may hold (FEDn holds one)
 LOAD_AHEAD_BYTES = int(os.environ.get("FEDN_AMD_LOAD_AHEAD_BYTES", str(4 << 30)))
+
+
+_pools = {}
+_pools_lock = threading.Lock()
+
+
+def _load_pool(workers):
+    """The read-ahead workers: one process-wide pool per size, created once (a pool per round cost
+    ~0.2 ms of thread start-up, as much as a whole small-model round's GPU work)."""
+    with _pools_lock:
+        pool = _pools.get(workers)
+        if pool is None:
+            pool = _pools[workers] = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="fedn_amd_load")
+        return pool
 
 
 def _raiser(e):
@@ -91,8 +106,9 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
                 continue
             yield mu, (lambda mu=mu: update_handler.load_model_update(mu, helper))
         return
-    pool = ThreadPoolExecutor(max_workers=ahead, thread_name_prefix="fedn_amd_load")
+    pool = _load_pool(ahead)
     window = deque()
+    issued = []                           # loads submitted this round and not finished
     size = size_box if size_box is not None else [None]   # bytes of one decoded update, once known
     # with no size yet, the first update's raw bytes (UpdateHandler.load_model_update_byte,
     # updatehandler.py:119-144) show it from the npz directory before its decode ends
@@ -124,9 +140,12 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
                 continue
             if peek[0]:
                 peek[0] = False
-                window.append((mu, pool.submit(peek_then_load, mu), None))
+                fut = pool.submit(peek_then_load, mu)
             else:
-                window.append((mu, pool.submit(update_handler.load_model_update, mu, helper), None))
+                fut = pool.submit(update_handler.load_model_update, mu, helper)
+            issued[:] = [f for f in issued if not f.done()]   # done loads: their arrays are the caller's
+            issued.append(fut)
+            window.append((mu, fut, None))
 
     first = [True]
 
@@ -155,7 +174,7 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
             if fut is not None:
                 fut.cancel()
         window.clear()
-        pool.shutdown(wait=True)
+        wait_futures([f for f in issued if not f.cancelled()])   # no load of this round outlives it
         requeue_front(q, back)
 
 

@@ -23,7 +23,7 @@ import torch
 
 from ..ingest import ShardedStagedModel
 from ..layout import Layout, spread
-from ..staging import AndroidFedAvgPipeline, FedAvgPipeline, helper_kind
+from ..staging import AndroidFedAvgPipeline, FedAvgPipeline, StagingCache, helper_kind
 from .aggregatorbase import AggregatorBase, queued_updates
 
 logger = logging.getLogger("fedn")
@@ -41,7 +41,7 @@ def _packed_bytes(model):
     return (lay if lay is not None else Layout.of(model)).nbytes
 
 
-def make_fedavg_pipeline(first, device=None, devices=None, helper=None):
+def make_fedavg_pipeline(first, device=None, devices=None, helper=None, cache=None):
     devices = devices or env_devices()
     if helper_kind(helper) == "androidhelper":   # its own fold rule and model format
         return AndroidFedAvgPipeline(device or (devices[0] if devices else None) or default_device(), first)
@@ -50,7 +50,7 @@ def make_fedavg_pipeline(first, device=None, devices=None, helper=None):
                                          len(spread(devices, _packed_bytes(first))) > 1):
         from ..multidev import ShardedFedAvgPipeline
         return ShardedFedAvgPipeline(devices, first)
-    return FedAvgPipeline(device or (devices[0] if devices else None) or default_device(), first)
+    return FedAvgPipeline(device or (devices[0] if devices else None) or default_device(), first, cache=cache)
 
 
 def default_device():
@@ -70,6 +70,7 @@ class Aggregator(AggregatorBase):
         self.name = "fedavg"
         self.device = torch.device(device) if device is not None else None
         self.devices = devices   # several devices: parameter-slice sharding in this process (multidev.py)
+        self._staging = StagingCache()   # pinned slots, arenas and streams reused by the next round
 
     def combine_models(self, helper=None, delete_models=True, parameters=None):
         data = {"time_model_load": 0.0, "time_model_aggregation": 0.0}
@@ -90,7 +91,7 @@ class Aggregator(AggregatorBase):
 
                     tic = time.time()
                     if nr_aggregated_models == 0:
-                        pipe = make_fedavg_pipeline(model_next, self.device, self.devices, helper)
+                        pipe = make_fedavg_pipeline(model_next, self.device, self.devices, helper, self._staging)
                     else:
                         pipe.add(model_next, metadata["num_examples"], total_examples)
                     data["time_model_aggregation"] += time.time() - tic
@@ -108,5 +109,7 @@ class Aggregator(AggregatorBase):
             model = pipe.result()
             data["time_model_aggregation"] += time.time() - tic
             data.update(pipe.timings())
+            if hasattr(pipe, "release"):
+                pipe.release()
         logger.info("AGGREGATOR({}): Aggregation completed, aggregated {} models.".format(self.name, nr_aggregated_models))
         return model, data

@@ -22,7 +22,7 @@ from ..exceptions import InvalidParameterError
 from ..parameters import Parameters
 from ..ingest import ShardedStagedModel
 from ..layout import spread
-from ..staging import FedOptPipeline, FedOptState
+from ..staging import FedOptPipeline, FedOptState, StagingCache
 from .aggregatorbase import AggregatorBase, queued_updates
 from .fedavg import _packed_bytes, default_device, env_devices
 
@@ -48,6 +48,7 @@ class Aggregator(AggregatorBase):
         # (layout.spread, decided by the session's first round; the state follows that choice)
         self.state = None
         self.sharded = None
+        self._staging = StagingCache()   # pinned slots, arenas, streams and ring reused by the next round
 
     def _pipeline(self, model_old, model_next):
         if self.sharded is None:
@@ -63,7 +64,7 @@ class Aggregator(AggregatorBase):
             from ..multidev import ShardedFedOptPipeline
             return ShardedFedOptPipeline(self.devices, model_old, model_next)
         dev = self.device or (self.devices[0] if self.devices else None) or default_device()
-        return FedOptPipeline(dev, model_old, model_next)
+        return FedOptPipeline(dev, model_old, model_next, cache=self._staging)
 
     # reference attribute names (fedopt.py:37-38): host copies of the HBM-resident state
     @property
@@ -121,6 +122,8 @@ class Aggregator(AggregatorBase):
             model = pipe.server_step(self.state, parameters)
             data["time_model_aggregation"] += time.time() - tic
             data.update(pipe.timings())
+            if hasattr(pipe, "release"):
+                pipe.release()
         except Exception as e:  # noqa: BLE001 — fedopt.py:111-116
             logger.error(f"Error during model aggregation: {e}")
             logger.error(traceback.format_exc())

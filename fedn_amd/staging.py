@@ -91,6 +91,27 @@ class HostStreamer:
         return done
 
 
+class StagingCache:
+    """Staging resources an aggregator keeps from one round of a session to the next: the pinned
+    host / device update slots, the small-update arenas, the copy and D2H streams and FedOpt's
+    pinned ring, per (device, packed update size). A round's pipeline takes them when it is built
+    and gives them back when the round's result is on the host (``_Pipeline.release``), so a
+    session's later rounds allocate, pin and create nothing (at most ``keep`` layouts are kept)."""
+
+    def __init__(self, keep=2):
+        self.keep = keep
+        self._res = {}
+
+    def take(self, device, nbytes):
+        return self._res.pop((str(device), nbytes), None)
+
+    def give(self, device, nbytes, res):
+        self._res.pop((str(device), nbytes), None)
+        self._res[(str(device), nbytes)] = res
+        while len(self._res) > self.keep:
+            self._res.pop(next(iter(self._res)))
+
+
 class _Slot:
     __slots__ = ("host", "host_np", "dev", "h2d_start", "h2d_done", "consumed", "used", "reserved")
 
@@ -126,10 +147,15 @@ class _ArenaRef:
 
 
 class _Pipeline:
-    def __init__(self, device, layout, nslots, slots=None, streams=None):
+    def __init__(self, device, layout, nslots, slots=None, streams=None, cache=None):
         self.device = torch.device(device)
         self.layout = layout
         self.compute = torch.cuda.current_stream(self.device)
+        # a session's earlier round left its staging resources in the aggregator's cache
+        self.cache = cache
+        kept = cache.take(self.device, layout.nbytes) if cache is not None else None
+        if kept is not None:
+            slots, streams = kept["slots"], kept["streams"]
         # H2D (update slots, FedOpt's global model) and D2H of the result (full duplex with H2D)
         self.copy, self.d2h = streams if streams is not None else (torch.cuda.Stream(self.device),
                                                                    torch.cuda.Stream(self.device))
@@ -148,8 +174,18 @@ class _Pipeline:
         self.pending = []                        # device-resident updates not folded yet: (staged, n, N)
         # small host updates are batched through arenas (not on the helper path, whose callers fold
         # one pair per pipeline with cached slots)
-        self.batch_host = slots is None and layout.nbytes <= SMALL_UPDATE_BYTES
-        self._arenas, self._arena, self._arena_i = [], None, 0
+        self.batch_host = (slots is None or kept is not None) and layout.nbytes <= SMALL_UPDATE_BYTES
+        self._arenas, self._arena, self._arena_i = (kept["arenas"] if kept else []), None, 0
+        self.streamer = kept["streamer"] if kept else HostStreamer()
+
+    def release(self):
+        """Give the staging resources to the cache for the session's next round (call once the
+        round's result is on the host; the pipeline stages nothing afterwards)."""
+        if self.cache is not None:
+            self.cache.give(self.device, self.layout.nbytes,
+                            {"slots": self.slots, "arenas": self._arenas, "streams": (self.copy, self.d2h),
+                             "streamer": self.streamer})
+            self.cache = None
 
     # ---- staging ---------------------------------------------------------------------
     def _take_slot(self):
@@ -329,9 +365,10 @@ class _Pipeline:
 class FedAvgPipeline(_Pipeline):
     """Streaming FedAvg on one device: fedavg.py:109-133 with the fold on the GPU."""
 
-    def __init__(self, device, first_arrays, nslots=3, slots=None, streams=None):
+    def __init__(self, device, first_arrays, nslots=3, slots=None, streams=None, cache=None):
         staged = isinstance(first_arrays, StagedModel)
-        super().__init__(device, first_arrays.layout if staged else Layout.of(first_arrays), nslots, slots, streams)
+        super().__init__(device, first_arrays.layout if staged else Layout.of(first_arrays), nslots, slots, streams,
+                         cache)
         self.first_arrays = first_arrays         # a StagedModel materialises host arrays only if needed
         self.first = self.acquire(first_arrays) if staged else self.stage(first_arrays)
         if not staged:
@@ -670,16 +707,15 @@ class FedOptPipeline(_Pipeline):
     """Streaming FedOpt on one device: the pseudo-gradient loop of fedopt.py:74-106 on the
     GPU (pg resident in HBM), then the fused server step (fedopt.py:151-258)."""
 
-    def __init__(self, device, old_arrays, first_arrays, nslots=2):
+    def __init__(self, device, old_arrays, first_arrays, nslots=2, cache=None):
         layout = first_arrays.layout if isinstance(first_arrays, StagedModel) else Layout.of(first_arrays)
-        super().__init__(device, layout, nslots)
+        super().__init__(device, layout, nslots, cache=cache)
         self.old_arrays = old_arrays
         self.nfolds = 0
         self.pg = {}
         self.pg_started = False                  # pg holds a partial pseudo-gradient
         self.general = None                      # mixed.TensorFedOpt once an update differs in layout
         self.old_ready = set()
-        self.streamer = HostStreamer()
         # the fused path needs the global model to share the update's shapes with one dtype per
         # update-dtype group, and a (update, old) dtype pair the kernel instantiates; otherwise
         # the round runs on the per-tensor path (numpy promotion / broadcasting, mixed.py)

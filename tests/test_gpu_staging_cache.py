@@ -1,0 +1,82 @@
+"""The plug-ins keep their staging resources (pinned slots, small-update arenas, streams, FedOpt's
+pinned ring) from one round of a session to the next (staging.StagingCache): later rounds reuse
+the very same buffers, and every round stays bit-identical to the oracle — including rounds whose
+model size changes (a new entry) and a returned model that must not alias a reused buffer."""
+import numpy as np
+import pytest
+
+from golden_io import assert_lists_identical
+from oracle import numpy_ref as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _round(rng, shapes, K, dtype=np.float32, old=None):
+    base = old if old is not None else [rng.standard_normal(s).astype(dtype) for s in shapes]
+    ups = [[(b + 0.01 * rng.standard_normal(b.shape)).astype(dtype) for b in base] for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    return base, ups, ns
+
+
+@pytest.mark.parametrize("shapes", [[(30, 7), (5,)], [(1000, 1100), (999,)]], ids=["small", "large"])
+def test_fedavg_rounds_reuse_staging(shapes):
+    from fedn_amd.aggregators.fedavg import Aggregator
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rng = np.random.default_rng(61)
+    uh = MemoryUpdateHandler()
+    agg = Aggregator(uh, device=DEV)
+    kept, outs = None, []
+    for r in range(4):
+        sh = shapes if r != 2 else [(13,), (4, 4)]        # round 2: another layout (its own entry)
+        _, ups, ns = _round(rng, sh, 5)
+        for u, n in zip(ups, ns):
+            uh.submit(u, n)
+        model, data = agg.combine_models(helper=None)
+        want, nr = ref.fedavg_combine(list(zip(ups, ns)))
+        assert nr == data["nr_aggregated_models"] == 5
+        assert_lists_identical(model, want, f"round {r}")
+        outs.append(([np.array(a, copy=True) for a in model], model))
+        res = agg._staging._res
+        if r != 2:
+            entry = res[(DEV, _nbytes(shapes))]
+            ids = [id(s) for s in entry["slots"]] + [id(a) for a in entry["arenas"]]
+            if kept is not None:
+                assert ids == kept                        # the same pinned / device buffers
+            kept = ids
+    for r, (copy, model) in enumerate(outs):              # later rounds left earlier results alone
+        assert_lists_identical(model, copy, f"round {r} result kept")
+
+
+def _nbytes(shapes):
+    from fedn_amd.layout import Layout
+    return Layout.of([np.zeros(s, np.float32) for s in shapes]).nbytes
+
+
+@pytest.mark.parametrize("shapes", [[(30, 7), (5,)], [(1000, 1100), (999,)]], ids=["small", "large"])
+def test_fedopt_rounds_reuse_staging(shapes):
+    from fedn_amd.aggregators.fedopt import Aggregator
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rng = np.random.default_rng(62)
+    uh = MemoryUpdateHandler()
+    agg = Aggregator(uh, device=DEV)
+    st = ref.FedOptState()
+    old = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    kept = None
+    for r in range(3):
+        _, ups, ns = _round(rng, shapes, 4, old=old)     # fp32 clients over an fp32, then fp64, model
+        gid = uh.put_global_model(old, f"g{r}")
+        for u, n in zip(ups, ns):
+            uh.submit(u, n, model_id=gid)
+        model, data = agg.combine_models(helper=None, parameters={"serveropt": "yogi"})
+        want, _ = ref.fedopt_combine(st, list(zip(ups, ns)), old, {"serveropt": "yogi"})
+        assert_lists_identical(model, want, f"round {r}")
+        assert_lists_identical(agg.m, st.m, f"m r{r}")
+        assert_lists_identical(agg.v, st.v, f"v r{r}")
+        (entry,) = agg._staging._res.values()
+        ids = [id(entry["streamer"])] + [id(s) for s in entry["slots"]] + [id(a) for a in entry["arenas"]]
+        if kept is not None:
+            assert ids == kept
+        kept = ids
+        old = want
