@@ -15,10 +15,13 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -910,3 +913,106 @@ int fnpz_stream_next(fnpz_stream* s, uint8_t* out, int64_t out_cap, int* event, 
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// host staging: gather copy on a persistent worker pool
+// ---------------------------------------------------------------------------------------
+namespace {
+
+// Workers created once and parked on a condition variable; run() hands them one job at a time
+// (callers are serialised) and the calling thread works on it too. A worker joins a job only
+// while it is posted (under the lock), so run() returns once every joined worker has left it.
+class CopyPool {
+   public:
+    static CopyPool& get() {
+        static CopyPool pool;
+        return pool;
+    }
+    void run(int threads, int n, const std::function<void(int)>& f) {
+        std::lock_guard<std::mutex> call(call_mu_);
+        std::atomic<int> next{0};
+        Job job{&f, n, &next};
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            while ((int)workers_.size() < threads - 1) workers_.emplace_back([this] { work(); });
+            job_ = &job;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (int i; (i = next.fetch_add(1)) < n;) f(i);
+        std::unique_lock<std::mutex> lk(mu_);
+        job_ = nullptr;                          // late wakers see no job
+        idle_.wait(lk, [this] { return active_ == 0; });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+
+   private:
+    struct Job {
+        const std::function<void(int)>* f;
+        int n;
+        std::atomic<int>* next;
+    };
+    void work() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            Job* j = job_;
+            if (!j) continue;
+            ++active_;
+            lk.unlock();
+            for (int i; (i = j->next->fetch_add(1)) < j->n;) (*j->f)(i);
+            lk.lock();
+            if (--active_ == 0) idle_.notify_all();
+        }
+    }
+    std::mutex call_mu_, mu_;
+    std::condition_variable cv_, idle_;
+    std::vector<std::thread> workers_;
+    Job* job_ = nullptr;
+    uint64_t gen_ = 0;
+    int active_ = 0;
+    bool stop_ = false;
+};
+
+}  // namespace
+
+extern "C" int fnpz_gather(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes, int threads) {
+    if (n < 0 || (n > 0 && (!dsts || !srcs || !nbytes)) || threads < 1)
+        return fail(FNPZ_EINVAL, "fnpz_gather: bad arguments");
+    int64_t total = 0;
+    for (int i = 0; i < n; ++i) {
+        if (nbytes[i] < 0 || (nbytes[i] > 0 && (!dsts[i] || !srcs[i]))) return fail(FNPZ_EINVAL, "fnpz_gather: segment %d", i);
+        total += nbytes[i];
+    }
+    if (total == 0) return FNPZ_OK;
+    struct Piece {
+        uint8_t* d;
+        const uint8_t* s;
+        int64_t len;
+    };
+    const int64_t piece = std::max<int64_t>(1 << 20, (total + 2 * threads - 1) / (2 * threads));
+    std::vector<Piece> pieces;
+    for (int i = 0; i < n; ++i)
+        for (int64_t o = 0; o < nbytes[i]; o += piece)
+            pieces.push_back({static_cast<uint8_t*>(dsts[i]) + o, static_cast<const uint8_t*>(srcs[i]) + o,
+                              std::min(piece, nbytes[i] - o)});
+    const int np = (int)pieces.size();
+    auto copy = [&](int k) { std::memcpy(pieces[k].d, pieces[k].s, (size_t)pieces[k].len); };
+    const int t = std::min(threads, np);
+    if (t <= 1) {
+        for (int k = 0; k < np; ++k) copy(k);
+        return FNPZ_OK;
+    }
+    CopyPool::get().run(t, np, copy);
+    return FNPZ_OK;
+}

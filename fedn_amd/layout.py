@@ -21,6 +21,21 @@ PACK_MIN_PARALLEL = 1 << 20   # updates smaller than this are packed inline (a t
 _pool = None
 
 
+def _native_gather(jobs):
+    """The pack's copies in one call to libfednpz's gather (persistent native threads: no Python
+    future per piece, ~3x the Python pool's rate on mid-size updates); False if the codec library
+    is not built, in which case the Python pool copies (same bytes)."""
+    for d, src in jobs:
+        if d.dtype != src.dtype:
+            raise TypeError(f"pack: {src.dtype} into a {d.dtype} region")   # np.copyto(casting="no")
+    try:
+        from . import codec
+        codec.gather(jobs, PACK_THREADS)
+    except ImportError:
+        return False
+    return True
+
+
 def _executor():
     global _pool
     if _pool is None:
@@ -158,6 +173,8 @@ class Layout:
         if PACK_THREADS <= 1 or total < PACK_MIN_PARALLEL:
             for d, src in jobs:
                 np.copyto(d, src, casting="no")
+            return
+        if _native_gather(jobs):
             return
         piece = max(1 << 20, min(PACK_CHUNK, -(-total // PACK_THREADS)))
         futs = []

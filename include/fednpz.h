@@ -92,6 +92,12 @@ int fnpz_stream_feed(fnpz_stream* stream, const uint8_t* data, int64_t len);
 int fnpz_stream_next(fnpz_stream* stream, uint8_t* out, int64_t out_cap, int* event, fnpz_entry* entry,
                      int64_t* out_len);
 
+/* Host staging (beside the wire format; the aggregators' pack of a decoded update into its pinned
+ * staging buffer, fedn_amd/layout.py): dsts[i][0, nbytes[i]) = srcs[i][0, nbytes[i]) for i < n,
+ * cut into pieces of at least 1 MiB that up to `threads` threads copy (the calling thread and a
+ * pool created once per process: no thread start-up per call). Regions must not overlap. */
+int fnpz_gather(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,6 +22,14 @@ int main(void) {
     if (fa_fedavg_fold(0, FA_F32, 0, FA_F32, 0, 0, 2, 10, 1, 0) != FA_EINVAL) return 4;
     if (fa_last_error()[0] == 0) return 5;
     if (fnpz_open(junk, sizeof junk, &e, 1, &n) != FNPZ_EFORMAT) return 6;
+    {
+        unsigned char dst[32] = {0};
+        void* d = dst;
+        const void* s = junk;
+        int64_t nb = sizeof junk;
+        if (fnpz_gather(1, &d, &s, &nb, 4) != FNPZ_OK || dst[0] != junk[0]) return 7;
+        if (fnpz_gather(1, &d, &s, &nb, 0) != FNPZ_EINVAL) return 8;
+    }
     printf("ok %s\n", fnpz_last_error());
     return 0;
 }

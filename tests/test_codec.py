@@ -119,3 +119,61 @@ def test_numpyhelper_key_order():
     out = codec.load_npz(b.getvalue())
     _same(out[0], np.zeros(3))
     _same(out[1], np.ones(2))
+
+
+def test_gather_pieces_threads_and_concurrent_callers():
+    """fnpz_gather (the pack's native copy): every byte lands, for segments below, at and above
+    the 1 MiB piece size, empty segments, 1..16 threads, and several Python threads calling at
+    once (the native pool serialises its jobs)."""
+    import threading
+
+    from fedn_amd import codec
+    rng = np.random.default_rng(9)
+    sizes = [0, 1, 4095, 1 << 20, (1 << 20) + 7, 5_000_003]
+    srcs = [rng.integers(0, 256, n, dtype=np.uint8) for n in sizes]
+    for threads in (1, 2, 8, 16):
+        dsts = [np.zeros(n, np.uint8) for n in sizes]
+        codec.gather(list(zip(dsts, srcs)), threads)
+        assert all(np.array_equal(d, s) for d, s in zip(dsts, srcs))
+    outs, errs = [], []
+
+    def worker(seed):
+        try:
+            r = np.random.default_rng(seed)
+            src = [r.integers(0, 256, 3_000_017, dtype=np.uint8), r.standard_normal(700_001)]
+            dst = [np.zeros_like(a) for a in src]
+            for _ in range(5):
+                codec.gather(list(zip(dst, src)), 8)
+            outs.append(all(np.array_equal(d, s) for d, s in zip(dst, src)))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker, args=(s,)) for s in range(6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs and outs == [True] * 6
+    with pytest.raises(ValueError):
+        codec.gather([(np.zeros(3, np.uint8), np.zeros(4, np.uint8))], 4)
+    with pytest.raises(codec.CodecError):
+        codec.gather([(np.zeros(3, np.uint8), np.zeros(3, np.uint8))], 0)
+
+
+def test_pack_native_equals_python_pool():
+    """layout.pack through fnpz_gather gives the bytes the Python thread pool gives."""
+    from fedn_amd import layout as L
+    rng = np.random.default_rng(10)
+    arrs = [rng.standard_normal(s).astype(np.float32) for s in [(700, 900), (333,), (2, 1 << 19)]]
+    arrs.append(rng.integers(-5, 5, (1 << 18,)).astype(np.int64))
+    lay = L.Layout.of(arrs)
+    a = np.zeros(lay.nbytes, np.uint8)
+    b = np.zeros(lay.nbytes, np.uint8)             # (alignment padding is never written)
+    lay.pack(arrs, a)
+    orig = L._native_gather
+    try:
+        L._native_gather = lambda jobs: False
+        lay.pack(arrs, b)
+    finally:
+        L._native_gather = orig
+    assert np.array_equal(a, b)
