@@ -89,6 +89,8 @@ def gather(pairs, threads):
     for i, (d, src) in enumerate(pairs):
         if d.nbytes != src.nbytes:
             raise ValueError(f"gather: {d.nbytes} != {src.nbytes} bytes")
+        if not (d.flags.c_contiguous and src.flags.c_contiguous):
+            raise ValueError("gather: non-contiguous array")
         dsts[i], srcs[i], nb[i] = d.ctypes.data, src.ctypes.data, d.nbytes
     _check(load_lib().fnpz_gather(n, dsts, srcs, nb, int(threads)))
 

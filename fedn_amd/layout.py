@@ -28,6 +28,8 @@ def _native_gather(jobs):
     for d, src in jobs:
         if d.dtype != src.dtype:
             raise TypeError(f"pack: {src.dtype} into a {d.dtype} region")   # np.copyto(casting="no")
+        if not (d.flags.c_contiguous and src.flags.c_contiguous):
+            return False
     try:
         from . import codec
         codec.gather(jobs, PACK_THREADS)
@@ -49,6 +51,8 @@ def parallel_copy(dst, src):
     step = max(1, PACK_CHUNK // max(1, src.itemsize))
     if PACK_THREADS <= 1 or n <= 2 * step:
         np.copyto(dst, src, casting="no")
+        return
+    if _native_gather([(dst, src)]):
         return
     futs = [_executor().submit(np.copyto, dst[i:i + step], src[i:i + step], casting="no") for i in range(0, n, step)]
     for f in futs:

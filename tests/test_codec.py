@@ -177,3 +177,14 @@ def test_pack_native_equals_python_pool():
     finally:
         L._native_gather = orig
     assert np.array_equal(a, b)
+
+
+def test_parallel_copy_strided_falls_back():
+    """A strided source never reaches the native byte copy (layout.parallel_copy falls back)."""
+    from fedn_amd import layout as L
+    src = np.arange(3 * (40 << 20) // 4, dtype=np.float32)[::3]
+    dst = np.zeros(src.size, np.float32)
+    L.parallel_copy(dst, src)
+    assert np.array_equal(dst, src)
+    with pytest.raises(ValueError):
+        codec.gather([(np.zeros(src.size, np.float32), src)], 4)
