@@ -38,8 +38,10 @@ Also measured in the same run:
                 and the headline kernel's fraction of the copy rate
   fedopt        (N = 1) BASELINE configs[3]: FedAdam over 32 device-resident 350 M fp32 updates,
                 one fused pseudo-gradient + server-step launch; round 1 and steady state (fp64
-                old / m / v, the dtype flow fedopt.py produces), each with its own roofline and
-                a bit-exact check of a sample against the oracle
+                old / m / v, the dtype flow fedopt.py produces), each with its own roofline, a
+                bit-exact check of a sample against the oracle and ``access_pattern``: the same
+                loads and stores with the arithmetic cut to adds (probe kernel k_fedopt_mix), the
+                HBM ceiling of the kernel's own traffic pattern
 """
 import argparse
 import hashlib
@@ -234,7 +236,7 @@ def configs1_side(ups, ns, agg, stream, device, in_bytes, a):
             "config": f"BASELINE configs[1]: FedAvg, {K} device-resident {a.dtype} updates x {P} params"}
 
 
-def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000):
+def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000, pattern_probe=True):
     """BASELINE configs[3]: FedAdam, K device-resident fp32 updates of P params, state in HBM;
     one fused fa_fedopt_step launch per round. Round 1 (old fp32, m / v None) and steady state
     (old / m / v fp64). Algorithmic bytes: K*P*4 + P*4 + P*(4+8+8) and P*(4K+48)."""
@@ -291,6 +293,21 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000):
     ok2 = bool(np.array_equal(out2[:S].cpu().numpy().view(np.uint64), want2[0].view(np.uint64)) and
                np.array_equal(m_out[:S].cpu().numpy().view(np.uint64), st.m[0].view(np.uint64)) and
                np.array_equal(v_out[:S].cpu().numpy().view(np.uint64), st.v[0].view(np.uint64)))
+    # the ceiling of the kernel's own access pattern: the same loads and stores with one add per value
+    # (k_fedopt_mix, libfedagg_probe.so; its outputs are not used), timed after the product launches
+    pattern = {}
+    if pattern_probe:
+        from fedn_amd import _abi
+        try:
+            with _abi.use_probe():
+                ops.tune(opt_mix=1)
+                for phase, fn in (("round1", r1), ("steady", r2)):
+                    for _ in range(warm):
+                        fn()
+                    pattern[phase] = timed_steps(fn, steps, stream, 1, device, False)[1]
+        finally:
+            with _abi.use_probe():
+                ops.tune(opt_mix=0)
     for phase, ms, b, ok, cpu_s in (("round1", ms1, K * P * 4 + P * 4 + P * 20, ok1, cpu1),
                                     ("steady", ms2, P * (4 * K + 48), ok2, cpu2)):
         wl = f"fedopt_adam_{phase}_k{K}_p{P}"
@@ -305,6 +322,12 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000):
                       "cpu_baseline": {"value": K * S / cpu_s, "unit": "params/s", "cores": 1, "kind": "port",
                                        "sample": f"{K} clients x {S} params: oracle/numpy_ref.fedopt_combine (the "
                                                  "fedopt.py restatement, numpy, single-threaded)", "seconds": cpu_s}}
+        if phase in pattern:
+            res[phase]["access_pattern"] = {
+                "ms": pattern[phase], "frac": b / pattern[phase] / 1e6 / HBM_PEAK_GBS,
+                "kernel_over_pattern": pattern[phase] / ms,
+                "note": "k_fedopt_mix (libfedagg_probe.so): k_fedopt_c's exact loads and stores with one add per value "
+                        "instead of the arithmetic; the HBM ceiling of this traffic pattern on this box"}
     res["config"] = (f"BASELINE configs[3]: FedAdam, {K} device-resident fp32 updates x {P} params, m / v in HBM "
                      "(fedopt.py:151-185), one fused launch per round")
     del ups, old32, out, v, m32, old64, m64, v64, m_out, v_out, out2
@@ -458,7 +481,8 @@ def main():
         if a.achievable and not a.no_side:
             extra["achievable"] = side(lambda: achievable_side(device, achieved_of(alg_bytes, kern_ms)))
         if rank == 0 and a.fedopt_params > 0:
-            extra["fedopt"] = side(lambda: fedopt_side(a.fedopt_params, a.fedopt_clients, device))
+            extra["fedopt"] = side(lambda: fedopt_side(a.fedopt_params, a.fedopt_clients, device,
+                                                       pattern_probe=not a.no_side))
 
     if rank == 0:
         line = {

@@ -943,6 +943,78 @@ __global__ void __launch_bounds__(kBlock)
 k_fedopt_c_mv(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
     fedopt_c_body<Y, OLD, PG, true, true, NT, 1, 4, kUnroll / 2, true>(b, s, tab, K, P);
 }
+
+// access-pattern probe (FA_TUNE_OPT_MIX): exactly k_fedopt_c's loads and stores for a FIRST|FINAL
+// launch — the element map (4 pairs per lane), clients loaded 4 at a time then the K % 4 remainder,
+// the state after the fold, non-temporal stores of v / out / m — with the arithmetic cut to one
+// add per value: the ceiling of the kernel's HBM traffic pattern alone. Whole wave tiles only.
+template <typename Y, typename OLD, typename S, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_mix(const OptBuffers b, const ClientTable<S> tab, const int K, const int64_t P) {
+    constexpr int NH = 4, H = 2, E = 2 * NH, U = kUnroll / 2;
+    constexpr int64_t T = 128 * NH;
+    const int64_t base = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * T;
+    if (base + T > P) return;
+    const int64_t i0 = base + 2 * (threadIdx.x & 63);
+    auto at = [i0](int h) { return i0 + (int64_t)h * 128; };
+    double acc[E];
+    {
+        OLD old[E];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) strip_load<OLD, H, false>(static_cast<const OLD*>(b.old) + at(h), *reinterpret_cast<OLD(*)[H]>(&old[h * H]));
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = (double)widen<OLD, double>(old[e]);
+    }
+    auto add_client = [&](int k, Y (&y)[E]) {
+        const Y* yp = static_cast<const Y*>(tab.ptr[k]);
+#pragma unroll
+        for (int h = 0; h < NH; ++h) strip_load<Y, H, NT>(yp + at(h), *reinterpret_cast<Y(*)[H]>(&y[h * H]));
+    };
+    int k = 0;
+    {
+        Y y[E];
+        add_client(0, y);
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] += (double)widen<Y, double>(y[e]);
+        k = 1;
+    }
+    for (; k + U <= K; k += U) {
+        Y y[U][E];
+#pragma unroll
+        for (int u = 0; u < U; ++u) add_client(k + u, y[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int e = 0; e < E; ++e) acc[e] += (double)widen<Y, double>(y[u][e]);
+    }
+    for (; k < K; ++k) {
+        Y y[E];
+        add_client(k, y);
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] += (double)widen<Y, double>(y[e]);
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        double mi[H] = {}, vv[H] = {};
+        opt_load_state<H>(b, OptScalars{}, at(h), H, mi, vv);
+        double m[H], v[H], o[H];
+#pragma unroll
+        for (int e = 0; e < H; ++e) {
+            m[e] = mi[e] + acc[h * H + e];
+            v[e] = vv[e] + acc[h * H + e];
+            o[e] = acc[h * H + e];
+        }
+        strip_store<double, H, 1>(b.v_out + at(h), v);
+        strip_store<double, H, 1>(b.out + at(h), o);
+        if (b.m_out_f64) strip_store<double, H, 1>(static_cast<double*>(b.m_out) + at(h), m);
+        else {
+            float mf[H];
+#pragma unroll
+            for (int e = 0; e < H; ++e) mf[e] = (float)m[e];
+            strip_store<float, H, 1>(static_cast<float*>(b.m_out) + at(h), mf);
+        }
+    }
+}
 #endif
 
 template <typename Y, typename OLD, class PG, int E, bool FIRST, bool FINAL, bool NT, bool NOST = false, int OSM = 0>
@@ -1140,7 +1212,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -1386,6 +1458,11 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
     constexpr bool probe_combo = E == 4 && std::is_same<Y, float>::value &&
                                  (std::is_same<OLD, float>::value || std::is_same<OLD, double>::value);
     if constexpr (probe_combo) {
+        if (first && final_ && g_cfg.opt_mix) {
+            const dim3 gm((unsigned)((P + 4 * 512 - 1) / (4 * 512)));   // a ragged last tile is skipped
+            hipLaunchKernelGGL((k_fedopt_mix<Y, OLD, typename PG::S, NT>), gm, dim3(kBlock), 0, st, b, tab, cnt, P);
+            return check_launch("fa_fedopt_step: kernel launch");
+        }
         if (first && final_ && g_cfg.opt_nostore) {
             hipLaunchKernelGGL((k_fedopt<Y, OLD, PG, E, true, true, NT, true>), grid, dim3(kBlock), 0, st, b, s, tab, cnt, P);
             return check_launch("fa_fedopt_step: kernel launch");
@@ -1838,6 +1915,9 @@ int fa_tune(int knob, int value) {
             return FA_OK;
         case FA_TUNE_OPT_MV:
             g_cfg.opt_mv = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_OPT_MIX:
+            g_cfg.opt_mix = value ? 1 : 0;
             return FA_OK;
         case FA_TUNE_WPE:
             if (value != 0 && value != 5 && value != 6 && value != 8)

@@ -327,7 +327,8 @@ _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _a
           "tilemap": _abi.FA_TUNE_TILEMAP, "opt_nt": _abi.FA_TUNE_OPT_NT, "opt_nostore": _abi.FA_TUNE_OPT_NOSTORE,
           "opt_store": _abi.FA_TUNE_OPT_STORE, "opt_coal": _abi.FA_TUNE_OPT_COAL, "narrow": _abi.FA_TUNE_NARROW,
           "lds": _abi.FA_TUNE_LDS, "wpe": _abi.FA_TUNE_WPE,
-          "opt_mv": _abi.FA_TUNE_OPT_MV, "auto_geom": _abi.FA_TUNE_AUTO_GEOM}
+          "opt_mv": _abi.FA_TUNE_OPT_MV, "auto_geom": _abi.FA_TUNE_AUTO_GEOM,
+          "opt_mix": _abi.FA_TUNE_OPT_MIX}
 
 
 def tune(**knobs):

@@ -70,7 +70,11 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                     FA_TUNE_AUTO_GEOM = 20 /* 1 (default) = with the default geometry knobs, the product's
                                               size-dependent choice (4-strip pipelined kernel only for client
                                               buffers >= 160 MiB, else 1 strip x 4/8 clients ahead); 0 = the
-                                              knobs as set, at every size */ };
+                                              knobs as set, at every size */,
+                    FA_TUNE_OPT_MIX = 21 /* FedOpt FIRST|FINAL, access-pattern probe: 1 = k_fedopt_c's exact loads
+                                            and stores with one add per value instead of the arithmetic
+                                            (results are NOT the reference's; a ragged last 2048-element
+                                            tile is skipped) */ };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);
