@@ -173,6 +173,21 @@ def timed_steps(step, steps, stream, world, device, on_cpu):
     return float(t[0]), float(t[1])
 
 
+def fedavg_pattern(ups, agg, stream, device, alg_bytes, kern_ms, a):
+    """The headline fold's traversal with one add per element instead of the fold (fa_stream_sum,
+    libfedagg_probe.so: the same pipelined 4-strip kernel, client table and non-temporal stores):
+    the HBM ceiling of the fold's own access pattern on this box."""
+    from fedn_amd import _abi, ops
+    with _abi.use_probe():
+        fn = lambda: ops.stream_sum(agg, ups, stream=stream)  # noqa: E731
+        for _ in range(3):
+            fn()
+        _, ms = timed_steps(fn, a.steps, stream, 1, device, False)
+    return {"ms": ms, "frac": alg_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, "kernel_over_pattern": ms / kern_ms,
+            "kernel": "k_fedavg_pipe<CADD> (fa_stream_sum, libfedagg_probe.so)",
+            "note": "the fold's exact traversal with x + y instead of x + n(y - x)/N; not in value"}
+
+
 def achieved_of(alg_bytes, kern_ms):
     return alg_bytes / (kern_ms / 1e3) / 1e9
 
@@ -474,6 +489,8 @@ def main():
         extra["gather_to_host"] = {"ms": gh * 1e3, "bytes_per_rank": P * 4, "GBps_aggregate": P * 4 / gh / 1e9,
                                    "note": "D2H of the aggregate into pinned host memory; not in value"}
         del host
+        if a.achievable and not a.no_side and a.dtype == "f32" and K <= 64:
+            extra["access_pattern"] = side(lambda: fedavg_pattern(ups, agg, stream, device, alg_bytes, kern_ms, a))
         if K >= 8 and a.configs1:
             extra["configs1"] = side(lambda: configs1_side(ups[:8], ns[:8], agg, stream, device, in_bytes, a))
         del ups, agg
