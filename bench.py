@@ -81,7 +81,7 @@ def parse():
     ap.add_argument("--configs1", action="store_true",
                     help="N = 1: add the configs[1] field (K = 8, same kernel: off by default so that a rocprofv3 "
                          "--stats run of the default command averages the headline launches only)")
-    ap.add_argument("--waves-params", type=int, default=1_000_000_000, help="N > 1: configs[4] side field (0 = skip)")
+    ap.add_argument("--waves-params", type=int, default=1_000_000_000, help="configs[4] side field (0 = skip)")
     ap.add_argument("--waves-clients", type=int, default=128)
     ap.add_argument("--waves-pool", type=int, default=8, help="distinct pinned host updates (reused cyclically)")
     ap.add_argument("--seed", type=int, default=0)
@@ -171,6 +171,50 @@ def timed_steps(step, steps, stream, world, device, on_cpu):
     if ranks:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t[0]), float(t[1])
+
+
+def fedopt_waves_side(a, devs, sample=1_000_000):
+    """BASELINE configs[4]: K bf16 updates of P params streamed from pinned host memory in waves of 8,
+    FedYogi, parameter-sliced over ``devs`` in one process (each GPU copies only its slice of every
+    update over its own PCIe link; fedn_amd.waves). The first ``sample`` params of the result are
+    checked bit-for-bit against the oracle on the exact f32 upcasts of the same bf16 updates."""
+    import hashlib
+
+    from fedn_amd.waves import WaveFedOpt
+    from oracle import numpy_ref as ref  # the checker of the sample only
+    P, K, pool = a.waves_params, a.waves_clients, a.waves_pool
+    g = torch.Generator(device=devs[0]).manual_seed(5)
+    base = torch.randn(P, generator=g, device=devs[0])
+    host = []
+    for _ in range(pool):
+        h = torch.empty(P, dtype=torch.bfloat16, pin_memory=True)
+        h.copy_((base + 0.01 * torch.randn(P, generator=g, device=devs[0])).to(torch.bfloat16))
+        host.append(h)
+    base = base.cpu()
+    ups = [host[k % pool] for k in range(K)]
+    ns = [int(v) for v in np.random.default_rng(5).integers(1, 5001, K)]
+    params = {"serveropt": "yogi"}
+    wf = WaveFedOpt(devs, P, wave=8)
+    old = wf.slices(base.double())
+    wf.round(ups[:8], ns[:8], old, params)                         # warm-up (allocations, kernels)
+    wf = WaveFedOpt(devs, P, wave=8)
+    t0 = time.perf_counter()
+    outs = wf.round(ups, ns, old, params)
+    t = time.perf_counter() - t0
+    res = wf.gather(outs)
+    S = min(sample, P)
+    want, _ = ref.fedopt_combine(ref.FedOptState(), [([ups[k][:S].float().numpy()], n) for k, n in enumerate(ns)],
+                                 [base[:S].double().numpy()], {**ref.DEFAULT_FEDOPT, **params})
+    exact = bool(np.array_equal(res[:S].numpy().view(np.uint64), want[0].view(np.uint64)))
+    checksum = hashlib.sha256(res.numpy().tobytes()).hexdigest()[:16]
+    del host, ups, old, outs, wf, res
+    torch.cuda.empty_cache()
+    return {"s": t, "value": K * P / t, "unit": "params/s", "params": P, "clients": K, "wave": 8, "devices": len(devs),
+            "h2d_GBps_total": K * P * 2 / t / 1e9, "h2d_GBps_per_link": K * P * 2 / t / 1e9 / len(devs),
+            "checksum_sha256_16": checksum, "bit_exact_on_sample": exact,
+            "sample": f"first {S} params vs oracle/numpy_ref.fedopt_combine on the f32 upcasts",
+            "note": f"BASELINE configs[4]: {pool} distinct pinned bf16 updates reused cyclically (every one "
+                    "crosses PCIe); PCIe-bound by design; not in value"}
 
 
 def fedavg_pattern(ups, agg, stream, device, alg_bytes, kern_ms, a):
@@ -497,6 +541,8 @@ def main():
         torch.cuda.empty_cache()
         if a.achievable and not a.no_side:
             extra["achievable"] = side(lambda: achievable_side(device, achieved_of(alg_bytes, kern_ms)))
+        if rank == 0 and a.waves_params > 0 and not a.no_side:
+            extra["fedopt_waves"] = side(lambda: fedopt_waves_side(a, [device]))
         if rank == 0 and a.fedopt_params > 0:
             extra["fedopt"] = side(lambda: fedopt_side(a.fedopt_params, a.fedopt_clients, device,
                                                        pattern_probe=not a.no_side))
@@ -604,39 +650,7 @@ def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, u
     out["gather_to_host"] = side(gather_to_host)
     out["weak_scaling"] = side(weak)
     def fedopt_waves():
-        """BASELINE configs[4] on this node: K bf16 updates of P params streamed from pinned host
-        memory in waves of 8, FedYogi, parameter-sliced over all N GPUs in one process (each GPU
-        copies only its slice of every update over its own PCIe link; fedn_amd.waves)."""
-        import hashlib
-
-        from fedn_amd.waves import WaveFedOpt
-        P, K, pool = a.waves_params, a.waves_clients, a.waves_pool
-        devs = [torch.device("cuda", 0 if rehearsal else d) for d in range(world)]
-        g = torch.Generator(device=devs[0]).manual_seed(5)
-        base = torch.randn(P, generator=g, device=devs[0])
-        host = []
-        for _ in range(pool):
-            h = torch.empty(P, dtype=torch.bfloat16, pin_memory=True)
-            h.copy_((base + 0.01 * torch.randn(P, generator=g, device=devs[0])).to(torch.bfloat16))
-            host.append(h)
-        base = base.cpu()
-        ups = [host[k % pool] for k in range(K)]
-        ns = [int(v) for v in np.random.default_rng(5).integers(1, 5001, K)]
-        wf = WaveFedOpt(devs, P, wave=8)
-        old = wf.slices(base.double())
-        wf.round(ups[:8], ns[:8], old, {"serveropt": "yogi"})         # warm-up (allocations, kernels)
-        wf = WaveFedOpt(devs, P, wave=8)
-        t0 = time.perf_counter()
-        outs = wf.round(ups, ns, old, {"serveropt": "yogi"})
-        t = time.perf_counter() - t0
-        res = wf.gather(outs)
-        del host, ups, old, outs, wf
-        torch.cuda.empty_cache()
-        return {"s": t, "value": K * P / t, "unit": "params/s", "params": P, "clients": K, "wave": 8, "devices": len(devs),
-                "h2d_GBps_total": K * P * 2 / t / 1e9, "h2d_GBps_per_link": K * P * 2 / t / 1e9 / len(devs),
-                "checksum_sha256_16": hashlib.sha256(res.numpy().tobytes()).hexdigest()[:16],
-                "note": f"BASELINE configs[4]: {pool} distinct pinned bf16 updates reused cyclically (every one "
-                        "crosses PCIe); PCIe-bound by design; not in value"}
+        return fedopt_waves_side(a, [torch.device("cuda", 0 if rehearsal else d) for d in range(world)])
 
     def fedopt_sharded():
         """BASELINE configs[3] on N GPUs: the same FedAdam model (P params, K fp32 updates) sliced over
