@@ -1089,6 +1089,21 @@ __global__ void __launch_bounds__(kBlock) k_ipow(T* __restrict__ out, const T* _
     }
 }
 
+// numpyhelper.increment_average (numpyhelper.py:32) on integer arrays folded with a python-float
+// num_examples: numpy subtracts in the integer dtype (wrapping), multiplies the difference by the
+// float n in float64, divides by N in float64 and adds x in float64 — each op rounded once.
+template <typename T>
+__global__ void __launch_bounds__(kBlock) k_ifold(double* __restrict__ out, const T* __restrict__ x,
+                                                  const T* __restrict__ y, double n, double N, int64_t P) {
+    using U = typename std::make_unsigned<T>::type;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < P; i += (int64_t)gridDim.x * kBlock) {
+        const T d = (T)((U)y[i] - (U)x[i]);
+        double t = (double)d * n;
+        t = t / N;
+        out[i] = (double)x[i] + t;
+    }
+}
+
 // numpyhelper.norm (numpyhelper.py:106-117): np.linalg.norm(x, 1) of one tensor, accumulated in f64
 // with a fixed (deterministic) order. Vector: sum |x|, grid-stride partials per block then one
 // block sums the partials. Matrix (rows x cols, C order): column sums of |x| (one lane per
@@ -1717,7 +1732,7 @@ int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype,
                    double a, double b, int64_t P, void* stream) {
     g_err[0] = 0;
     if (P < 0 || !out || (op != FA_EW_FILL && !x)) return fail(FA_EINVAL, "fa_elementwise: bad arguments");
-    if (op < FA_EW_AXPBY || op > FA_EW_IPOW) return fail(FA_EINVAL, "fa_elementwise: unknown op %d", op);
+    if (op < FA_EW_AXPBY || op > FA_EW_IFOLD) return fail(FA_EINVAL, "fa_elementwise: unknown op %d", op);
     if (op == FA_EW_AXPBY && !y) return fail(FA_EINVAL, "fa_elementwise: AXPBY needs y");
     if (P == 0) return FA_OK;
     if (op == FA_EW_IPOW) {
@@ -1733,6 +1748,19 @@ int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype,
         else
             hipLaunchKernelGGL(k_ipow<int64_t>, g, dim3(kBlock), 0, sti, static_cast<int64_t*>(out),
                                static_cast<const int64_t*>(x), (uint64_t)a, P);
+        return check_launch("fa_elementwise");
+    }
+    if (op == FA_EW_IFOLD) {
+        if (!y || out_dtype != FA_F64 || x_dtype != y_dtype || (x_dtype != FA_I32 && x_dtype != FA_I64))
+            return fail(FA_EDTYPE, "fa_elementwise: IFOLD takes two int32 or two int64 arrays and returns float64");
+        const dim3 g((unsigned)std::min<int64_t>((P + kBlock - 1) / kBlock, 8192));
+        hipStream_t sti = static_cast<hipStream_t>(stream);
+        if (x_dtype == FA_I32)
+            hipLaunchKernelGGL(k_ifold<int32_t>, g, dim3(kBlock), 0, sti, static_cast<double*>(out),
+                               static_cast<const int32_t*>(x), static_cast<const int32_t*>(y), a, b, P);
+        else
+            hipLaunchKernelGGL(k_ifold<int64_t>, g, dim3(kBlock), 0, sti, static_cast<double*>(out),
+                               static_cast<const int64_t*>(x), static_cast<const int64_t*>(y), a, b, P);
         return check_launch("fa_elementwise");
     }
     auto isf = [](int d) { return d == FA_F32 || d == FA_F64; };

@@ -68,10 +68,22 @@ def fold_plan(xs, ys, n, N):
         r = np.add(x0, t)
         if d.dtype not in _SUPPORTED or xdt not in _SUPPORTED or ydt not in _SUPPORTED:
             raise TypeError(f"unsupported dtypes for the fold: model {xdt}, update {ydt}")
-        if d.dtype.kind == "i" and not isinstance(n, (int, np.integer)):
-            raise TypeError("integer tensors folded with a non-integer num_examples are not supported")
         plan.append((d.dtype, r.dtype, shape))
     return plan
+
+
+def float_n(n):
+    """True when numpy multiplies an integer difference by ``n`` in float64 (a python float or numpy
+    float num_examples) rather than in the integer dtype (a python / numpy int). n == 1.0 gives the
+    same bits either way (the integer product by 1 is the difference itself)."""
+    return not isinstance(n, (int, np.integer)) and n != 1.0
+
+
+def int_float_n(dtypes, nfolds, n):
+    """Whether folding an update with num_examples ``n`` into a running model that is still the
+    first update (``nfolds == 0``) multiplies an INTEGER difference by a float n — the fused
+    kernels fold integer tensors with an integer n only, so such a fold runs per tensor."""
+    return nfolds == 0 and float_n(n) and any(np.dtype(d).kind == "i" for d in dtypes)
 
 
 def sub_plan(ys, olds):
@@ -179,12 +191,16 @@ class TensorFedAvg:
                     yc = _as(y, td, shape, self.stream)
                     ops.fedavg_fold(xc.view(-1), [yc.view(-1)], [n], [N], init=False, stream=self.stream)
                     new.append(xc)
-                else:                            # integer difference: numpy's int subtract/multiply,
-                    xc = _as(x, td, shape, self.stream)   # then true_divide to float64
+                else:                            # integer difference (numpy's wrapping int subtract)
+                    xc = _as(x, td, shape, self.stream)
                     yc = _as(y, td, shape, self.stream)
                     out = torch.empty(shape, dtype=torch.float64, device=self.device)
-                    ops.fedavg_fold(out.view(-1), [xc.view(-1), yc.view(-1)], [0, n], [1, N], init=True,
-                                    stream=self.stream)
+                    if float_n(n):                   # n * d in float64, / N, + x (fa_elementwise IFOLD)
+                        ops.elementwise("ifold", out.view(-1), xc.view(-1), yc.view(-1), float(n), float(N),
+                                        stream=self.stream)
+                    else:                            # int multiply by n, then true_divide to float64
+                        ops.fedavg_fold(out.view(-1), [xc.view(-1), yc.view(-1)], [0, n], [1, N], init=True,
+                                        stream=self.stream)
                     new.append(out)
         self.x = new
         self.owned = [True] * len(new)

@@ -230,7 +230,8 @@ class ShardedFedAvgPipeline(_ShardedStaging):
                                           owned=True)
 
     def add(self, arrays, n, N):
-        if self.general is None and not self.compatible(arrays):
+        if self.general is None and (not self.compatible(arrays) or
+                                     mixed.int_float_n(self.layout.dtypes, self.nfolds, n)):
             plan = mixed.fold_plan(self._state_meta(), self.meta_of(arrays), n, N)   # raises as numpy
             self._enter_general()
             self.general.fold(self.tensors_of(arrays), n, N, plan=plan)

@@ -340,7 +340,7 @@ def tune(**knobs):
 
 _EW = {"axpby": _abi.FA_EW_AXPBY, "mul": _abi.FA_EW_MUL, "div": _abi.FA_EW_DIV, "sqrt": _abi.FA_EW_SQRT,
        "square": _abi.FA_EW_SQUARE, "sign": _abi.FA_EW_SIGN, "fill": _abi.FA_EW_FILL, "pow": _abi.FA_EW_POW,
-       "ipow": _abi.FA_EW_IPOW}
+       "ipow": _abi.FA_EW_IPOW, "ifold": _abi.FA_EW_IFOLD}
 
 
 def elementwise(op, out, x=None, y=None, a=0.0, b=0.0, stream=None):

@@ -158,10 +158,14 @@ int fa_running_mean(void* g, int dtype, const void* m, double a, double b, doubl
  *                                                  across hosts; parity: 1e-6 relative, f64 1e-15)
  *   FA_EW_IPOW    out = x**a, x I32 | I64, a a non-negative integer: exponentiation by squaring
  *                 with wrapping products, out_dtype = x_dtype (numpy's integer power)
+ *   FA_EW_IFOLD   out = x + ((y - x)*a)/b, x and y both I32 or both I64, out F64: numpyhelper
+ *                 .increment_average (numpyhelper.py:32) on integer arrays with a python-float
+ *                 num_examples a and total b — the difference wraps in the integer dtype, then
+ *                 float64 multiply, divide and add, each rounded once
  * out_dtype must be the numpy result dtype of the op.
  */
 enum fa_ew_op { FA_EW_AXPBY = 0, FA_EW_MUL = 1, FA_EW_DIV = 2, FA_EW_SQRT = 3, FA_EW_SQUARE = 4, FA_EW_SIGN = 5,
-                FA_EW_FILL = 6, FA_EW_POW = 7, FA_EW_IPOW = 8 };
+                FA_EW_FILL = 6, FA_EW_POW = 7, FA_EW_IPOW = 8, FA_EW_IFOLD = 9 };
 int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype, const void* y, int y_dtype,
                    double a, double b, int64_t P, void* stream);
 

@@ -27,6 +27,15 @@ def _list(z, prefix):
     return [z[f"{prefix}_t{t}"] for t in range(int(z[key]))]
 
 
+def _ns(z, key):
+    """num_examples as the python numbers the reference saw: int, or float where the case says so."""
+    isf = z.get(key + "_isfloat")
+    vals = z[key]
+    if isf is None:
+        return [int(v) for v in vals]
+    return [float(v) if f else int(v) for v, f in zip(vals, isf)]
+
+
 def load_case(name):
     with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
         z = {k: z[k] for k in z.files}
@@ -73,7 +82,7 @@ def load_case(name):
         rounds = []
         for r in range(int(z["rounds"])):
             K = int(z[f"r{r}_K"])
-            ns = [int(v) for v in z[f"r{r}_n"]]
+            ns = _ns(z, f"r{r}_n")
             rd = {
                 "updates": [(_list(z, f"r{r}_u{k}"), ns[k]) for k in range(K)],
                 "old": _list(z, f"r{r}_old"),

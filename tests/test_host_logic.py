@@ -243,8 +243,11 @@ def test_mixed_fold_plan_is_numpy():
     with pytest.raises(ValueError):
         mixed.fold_plan([((5,), f4)], [((4,), f4)], 1, 2)
     assert len(mixed.fold_plan([((1,), f4)] * 3, [((1,), f4)] * 2, 1, 2)) == 2       # zip truncates
-    with pytest.raises(TypeError):
-        mixed.fold_plan([((3,), i8)], [((3,), i8)], 2.5, 4)                          # int diff, float n
+    (d, r, shape), = mixed.fold_plan([((3,), i8)], [((3,), i8)], 2.5, 4)             # int diff, float n
+    assert (d, r) == (i8, np.add(np.ones(3, i8), 2.5 * (np.ones(3, i8) - np.ones(3, i8)) / 4).dtype)
+    assert mixed.float_n(2.5) and not mixed.float_n(3) and not mixed.float_n(1.0) and not mixed.float_n(np.int64(2))
+    assert mixed.int_float_n([i8, f4], 0, 2.5) and not mixed.int_float_n([i8], 1, 2.5)
+    assert not mixed.int_float_n([f4, f8], 0, 2.5) and not mixed.int_float_n([i8], 0, 4)
     (r, shape), = mixed.sub_plan([((3,), i8)], [((1,), f4)])
     assert r == (np.ones(3, i8) * 1.0 + np.ones(1, f4) * -1.0).dtype and shape == (3,)
 
