@@ -1614,6 +1614,11 @@ int fa_fedavg_fold(void* agg, int agg_dtype, const void* const* updates, int upd
         return FA_OK;
     }
     const bool int_first = init && (upd_dtype == FA_I64 || upd_dtype == FA_I32);
+    // the first fold of integer updates multiplies in the integer dtype: numpy does that for an int
+    // num_examples only (a float one multiplies in float64: fa_elementwise FA_EW_IFOLD)
+    if (int_first && !(n[1] == std::floor(n[1]) && std::fabs(n[1]) < 0x1p63))
+        return fail(FA_EINVAL, "fa_fedavg_fold: integer updates need an integral n[1] (got %g); a float "
+                               "num_examples folds through fa_elementwise(FA_EW_IFOLD)", n[1]);
     if (upd_dtype == FA_F32 && agg_dtype == FA_F32) return launch_fedavg<float, float, CF32>(agg, updates, n, N, K, P, init, false, st);
     if (upd_dtype == FA_BF16 && agg_dtype == FA_F32) return launch_fedavg<bf16, float, CF32>(agg, updates, n, N, K, P, init, false, st);
     if (upd_dtype == FA_F16 && agg_dtype == FA_F16) return launch_fedavg<f16, f16, CF16>(agg, updates, n, N, K, P, init, false, st);

@@ -85,6 +85,8 @@ const char* fa_last_error(void);
  *   (F32,F32)->f32  (BF16,F32)->f32  (F16,F16)->f16  (F64,F64)->f64
  *   (F32,F64)->f64  (I64,F64)/(I32,F64)->int then f64 (numpy true_divide)
  * With init=1 and K=1 the result is a plain copy and agg_dtype must equal upd_dtype.
+ * Integer updates with init=1: n[1] must be integral (numpy multiplies the first integer difference
+ * in the integer dtype only for an int num_examples; see FA_EW_IFOLD for a float one).
  */
 int fa_fedavg_fold(void* agg, int agg_dtype,
                    const void* const* updates, int upd_dtype,

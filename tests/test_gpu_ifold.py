@@ -37,3 +37,16 @@ def test_ifold_rejects_float_inputs():
     x = torch.zeros(8, dtype=torch.float32, device=DEV)
     with pytest.raises(_abi.FedAggError):
         ops.elementwise("ifold", torch.empty(8, dtype=torch.float64, device=DEV), x, x, 2.5, 3.0)
+
+
+def test_int_first_fold_rejects_float_n():
+    """fa_fedavg_fold folds the first integer difference in the integer dtype, which is numpy's rule
+    for an int num_examples only: a non-integral n is refused (the plug-ins route it to IFOLD)."""
+    from fedn_amd import _abi, ops
+    x = torch.arange(16, dtype=torch.int64, device=DEV)
+    out = torch.empty(16, dtype=torch.float64, device=DEV)
+    with pytest.raises(_abi.FedAggError):
+        ops.fedavg_fold(out, [x, x + 3], [0, 2.5], [1, 3.5], init=True)
+    ops.fedavg_fold(out, [x, x + 3], [0, 2.0], [1, 3.0], init=True)      # integral: the int path
+    want = np.add(np.arange(16), 2 * (np.arange(16) + 3 - np.arange(16)) / 3.0)
+    assert np.array_equal(out.cpu().numpy(), want)
