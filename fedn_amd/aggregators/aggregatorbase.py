@@ -32,10 +32,11 @@ _pools_lock = threading.Lock()
 def _load_pool(workers):
     """The read-ahead workers: one process-wide pool per size, created once (a pool per round cost
     ~0.2 ms of thread start-up, as much as a whole small-model round's GPU work)."""
+    key = (os.getpid(), workers)          # a forked child starts its own (its parent's threads are gone)
     with _pools_lock:
-        pool = _pools.get(workers)
+        pool = _pools.get(key)
         if pool is None:
-            pool = _pools[workers] = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="fedn_amd_load")
+            pool = _pools[key] = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="fedn_amd_load")
         return pool
 
 

@@ -11,6 +11,7 @@
 // inflate the blocks in parallel too. Container layout follows numpy's savez_compressed
 // (ZIP64 extras on every member, names "<key>.npy").
 
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -924,9 +925,19 @@ namespace {
 // while it is posted (under the lock), so run() returns once every joined worker has left it.
 class CopyPool {
    public:
+    // One pool per process: a child forked while the parent's workers existed gets a fresh pool
+    // (the parent's threads do not exist in it, and its mutexes may have been copied locked). Pools
+    // are never destroyed: their parked workers end with the process.
     static CopyPool& get() {
-        static CopyPool pool;
-        return pool;
+        static std::mutex m;
+        static CopyPool* pool = nullptr;
+        static pid_t owner = 0;
+        std::lock_guard<std::mutex> lk(m);
+        if (!pool || owner != getpid()) {
+            pool = new CopyPool();
+            owner = getpid();
+        }
+        return *pool;
     }
     void run(int threads, int n, const std::function<void(int)>& f) {
         std::lock_guard<std::mutex> call(call_mu_);
@@ -943,14 +954,6 @@ class CopyPool {
         std::unique_lock<std::mutex> lk(mu_);
         job_ = nullptr;                          // late wakers see no job
         idle_.wait(lk, [this] { return active_ == 0; });
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : workers_) t.join();
     }
 
    private:
@@ -981,7 +984,7 @@ class CopyPool {
     Job* job_ = nullptr;
     uint64_t gen_ = 0;
     int active_ = 0;
-    bool stop_ = false;
+    bool stop_ = false;   // never set: the pool lives as long as the process
 };
 
 }  // namespace

@@ -40,9 +40,9 @@ def _native_gather(jobs):
 
 def _executor():
     global _pool
-    if _pool is None:
-        _pool = ThreadPoolExecutor(max_workers=PACK_THREADS, thread_name_prefix="fedn_amd_pack")
-    return _pool
+    if _pool is None or _pool[0] != os.getpid():     # a forked child starts its own pool
+        _pool = (os.getpid(), ThreadPoolExecutor(max_workers=PACK_THREADS, thread_name_prefix="fedn_amd_pack"))
+    return _pool[1]
 
 
 def parallel_copy(dst, src):

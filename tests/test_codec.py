@@ -188,3 +188,40 @@ def test_parallel_copy_strided_falls_back():
     assert np.array_equal(dst, src)
     with pytest.raises(ValueError):
         codec.gather([(np.zeros(src.size, np.float32), src)], 4)
+
+
+def _child_after_fork(q):
+    from fedn_amd.aggregators.aggregatorbase import queued_updates
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    src = np.arange(3 << 20, dtype=np.uint8)
+    dst = np.zeros_like(src)
+    codec.gather([(dst, src)], 8)
+    uh = MemoryUpdateHandler()
+    for k in range(5):
+        uh.submit([np.full(3, k, np.float32)], k + 1)
+    got = [int(load()[0][0][0]) for _, load in queued_updates(uh, None, ahead=4)]
+    q.put((bool(np.array_equal(dst, src)), got))
+
+
+def test_thread_pools_survive_fork():
+    """The persistent pools (native gather, read-ahead loads, Python pack) are per process: a child
+    forked after the parent used them starts its own instead of waiting on threads it does not have."""
+    import multiprocessing as mp
+
+    from fedn_amd import layout as L
+    from fedn_amd.aggregators.aggregatorbase import queued_updates
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    src = np.arange(3 << 20, dtype=np.uint8)
+    codec.gather([(np.zeros_like(src), src)], 8)                  # parent: native pool started
+    L.parallel_copy(np.zeros(40 << 20, np.uint8)[::1], np.ones(40 << 20, np.uint8))
+    uh = MemoryUpdateHandler()
+    for k in range(3):
+        uh.submit([np.full(3, k, np.float32)], k + 1)
+    assert [int(load()[0][0][0]) for _, load in queued_updates(uh, None, ahead=4)] == [0, 1, 2]
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    p = ctx.Process(target=_child_after_fork, args=(q,))
+    p.start()
+    ok, got = q.get(timeout=60)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and ok and got == [0, 1, 2, 3, 4]
