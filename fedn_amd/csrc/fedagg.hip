@@ -99,6 +99,7 @@ __device__ __forceinline__ uint16_t f32_to_f16(float f) {
 struct CF32 {            // float32 ufunc loops
     using V = float;     // register type
     using S = float;     // scalar (n, N) type
+    using T = float;     // storage type (FedOpt's pseudo-gradient workspace)
     __device__ static __forceinline__ V fold(V x, V y, S n, S N, double r) {
         V t[1] = {x}, yy[1] = {y};
         fold_strip<1>(t, yy, n, N, r);
@@ -146,6 +147,7 @@ struct CF32 {            // float32 ufunc loops
 struct CF64 {            // float64 ufunc loops
     using V = double;
     using S = double;
+    using T = double;
     // RN64(t/N) without a division when the host supplies r = RN64(1/N) (r == 0: IEEE
     // division). q0 = RN(t*r) is within 1.5 ulp of z = t/N; one Markstein step
     // q1 = RN(q0 + RN(t - q0*N)*r) makes it faithful (the error left is ~2^-52 of q0's);
@@ -179,6 +181,7 @@ struct CF64 {            // float64 ufunc loops
 struct CF16 {            // numpy half loops: op in float, round to half after every op
     using V = float;     // holds a value exactly representable in f16
     using S = float;     // n, N pre-rounded to f16 on the host
+    using T = f16;
     __device__ static __forceinline__ V rh(float a) { return f16_to_f32(f32_to_f16(a)); }
     __device__ static __forceinline__ V fold(V x, V y, S n, S N, double) {
         V t = rh(y - x);
@@ -606,6 +609,7 @@ struct OptScalars {
     // python-float constants exactly as fedopt.py computes them
     double lr, b1, b2, tau, tau2, c1, c2, nc2;   // c1 = 1-b1, c2 = 1-b2, nc2 = -(1-b2)
     float b1f, c1f, c2f;                         // the same cast to f32 (numpy weak-scalar rule)
+    float b1h, c1h, c2h;                         // ... and to f16 (held in f32): float16 state / pg
     int opt;
 };
 
@@ -622,9 +626,19 @@ struct OptBuffers {
 };
 
 // multiply an array element held as PG by a python float constant (numpy weak scalar)
-template <class PG> __device__ __forceinline__ double mul_pg(double a, double c, float cf);
-template <> __device__ __forceinline__ double mul_pg<CF32>(double a, double, float cf) { return (double)((float)a * cf); }
-template <> __device__ __forceinline__ double mul_pg<CF64>(double a, double c, float) { return a * c; }
+template <class PG> __device__ __forceinline__ double mul_pg(double a, double c, float cf, float ch);
+template <> __device__ __forceinline__ double mul_pg<CF32>(double a, double, float cf, float) { return (double)((float)a * cf); }
+template <> __device__ __forceinline__ double mul_pg<CF64>(double a, double c, float, float) { return a * c; }
+template <> __device__ __forceinline__ double mul_pg<CF16>(double a, double, float, float ch) {
+    return (double)CF16::rh((float)a * ch);
+}
+
+// numpyhelper.subtract(next, old) = next*1.0 + old*(-1.0) (numpyhelper.py:44-56) and power(pg, 2)
+// (:94-104) in the pseudo-gradient's dtype: float16 rounds every op to half, as numpy's half loops
+template <class PG> __device__ __forceinline__ typename PG::V pg_sub(typename PG::V y, typename PG::V o) { return y - o; }
+template <> __device__ __forceinline__ float pg_sub<CF16>(float y, float o) { return CF16::rh(y - o); }
+template <class PG> __device__ __forceinline__ typename PG::V pg_sq(typename PG::V v) { return (typename PG::V)(v * v); }
+template <> __device__ __forceinline__ float pg_sq<CF16>(float v) { return CF16::rh(v * v); }
 
 __device__ __forceinline__ double np_sign(double d) {
     // numpy sign: 1 / -1 / 0 (for +-0), NaN propagates
@@ -645,11 +659,19 @@ __device__ __forceinline__ void opt_load_state(const OptBuffers& b, const OptSca
             for (int e = 0; e < E; ++e) mf[e] = e < rem ? mp[e] : 0.f;
 #pragma unroll
         for (int e = 0; e < E; ++e) mi[e] = (double)mf[e];
-    } else if (b.m_in_f64 > 0) {
+    } else if (b.m_in_f64 == 1) {
         const double* mp = static_cast<const double*>(b.m_in) + i0;
         if (full) strip_load<double, E, SNT>(mp, mi);
         else
             for (int e = 0; e < E; ++e) mi[e] = e < rem ? mp[e] : 0.0;
+    } else if (b.m_in_f64 == 2) {                // float16 m (a float16 session's first rounds)
+        f16 mh[E];
+        const f16* mp = static_cast<const f16*>(b.m_in) + i0;
+        if (full) strip_load<f16, E, SNT>(mp, mh);
+        else
+            for (int e = 0; e < E; ++e) mh[e] = e < rem ? mp[e] : f16{0};
+#pragma unroll
+        for (int e = 0; e < E; ++e) mi[e] = (double)f16_to_f32(mh[e].bits);
     }
     if (b.v_in) {
         const double* vp = b.v_in + i0;
@@ -674,29 +696,44 @@ __device__ __forceinline__ void opt_apply(const OptBuffers& b, const OptScalars&
     constexpr bool PG32 = std::is_same<PG, CF32>::value;
     const bool full = rem == E;
     // ---- m (fedopt.py:173-176 and the two twins)
+    constexpr bool PG64 = std::is_same<PG, CF64>::value;
     double m[E];
     if (b.m_in_f64 < 0) {
 #pragma unroll
-        for (int e = 0; e < E; ++e) m[e] = mul_pg<PG>((double)pg[e], s.c1, s.c1f);
-    } else if (b.m_in_f64 == 0) {
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const float a = (float)mi[e] * s.b1f;                        // m*beta1 in f32 (mi is an exact f32)
-            if constexpr (PG32) m[e] = (double)(a + (float)pg[e] * s.c1f);  // f32 + f32
-            else m[e] = (double)a + (double)pg[e] * s.c1;                   // f32 -> f64 add
-        }
+        for (int e = 0; e < E; ++e) m[e] = mul_pg<PG>((double)pg[e], s.c1, s.c1f, s.c1h);
     } else {
+        // m*beta1 in m's dtype, pg*(1-beta1) in pg's dtype, their sum in the promoted dtype
+        // (f16 < f32 < f64); each operand is exact in its dtype, so the float sum rounds once
+        if (b.m_in_f64 == 1) {                     // f64 m: an f64 sum
 #pragma unroll
-        for (int e = 0; e < E; ++e) m[e] = mi[e] * s.b1 + mul_pg<PG>((double)pg[e], s.c1, s.c1f);
+            for (int e = 0; e < E; ++e) m[e] = mi[e] * s.b1 + mul_pg<PG>((double)pg[e], s.c1, s.c1f, s.c1h);
+        } else if (b.m_in_f64 == 0) {              // f32 m (mi is an exact f32)
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float a = (float)mi[e] * s.b1f;
+                const double pm = mul_pg<PG>((double)pg[e], s.c1, s.c1f, s.c1h);
+                if constexpr (PG64) m[e] = (double)a + pm;          // f32 + f64
+                else m[e] = (double)(a + (float)pm);                // f32 + f32 (or f16) in f32
+            }
+        } else {                                   // f16 m (a float16 session's first rounds)
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float a = CF16::rh((float)mi[e] * s.b1h);
+                const double pm = mul_pg<PG>((double)pg[e], s.c1, s.c1f, s.c1h);
+                if constexpr (PG64) m[e] = (double)a + pm;
+                else if constexpr (PG32) m[e] = (double)(a + (float)pm);
+                else m[e] = (double)CF16::rh(a + (float)pm);
+            }
+        }
     }
     // ---- v (fedopt.py:178-179 / 214-217 / 251-252)
     double o[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const V pv = pg[e];
-        const double p = (double)(V)(pv * pv);   // power(pg, 2) in the pg dtype
+        const double p = (double)pg_sq<PG>(pv);   // power(pg, 2) in the pg dtype
         if (s.opt == FA_ADAM) {
-            v[e] = v[e] * s.b2 + mul_pg<PG>(p, s.c2, s.c2f);
+            v[e] = v[e] * s.b2 + mul_pg<PG>(p, s.c2, s.c2f, s.c2h);
         } else if (s.opt == FA_YOGI) {
             const double sg = np_sign(v[e] - p);
             v[e] = v[e] + (sg * p) * s.nc2;
@@ -714,19 +751,25 @@ __device__ __forceinline__ void opt_apply(const OptBuffers& b, const OptScalars&
     if (full) {
         strip_store<double, E, OSM>(b.v_out + i0, v);
         strip_store<double, E, OSM>(b.out + i0, o);
-        if (b.m_out_f64) strip_store<double, E, OSM>(static_cast<double*>(b.m_out) + i0, m);
-        else {
+        if (b.m_out_f64 == 1) strip_store<double, E, OSM>(static_cast<double*>(b.m_out) + i0, m);
+        else if (b.m_out_f64 == 0) {
             float mf[E];
 #pragma unroll
             for (int e = 0; e < E; ++e) mf[e] = (float)m[e];
             strip_store<float, E, OSM>(static_cast<float*>(b.m_out) + i0, mf);
+        } else {                                  // f16 m: every value is already a half
+            f16 mh[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) mh[e] = f16{f32_to_f16((float)m[e])};
+            strip_store<f16, E, 0>(static_cast<f16*>(b.m_out) + i0, mh);
         }
     } else {
         for (int e = 0; e < rem; ++e) {
             b.v_out[i0 + e] = v[e];
             b.out[i0 + e] = o[e];
-            if (b.m_out_f64) static_cast<double*>(b.m_out)[i0 + e] = m[e];
-            else static_cast<float*>(b.m_out)[i0 + e] = (float)m[e];
+            if (b.m_out_f64 == 1) static_cast<double*>(b.m_out)[i0 + e] = m[e];
+            else if (b.m_out_f64 == 0) static_cast<float*>(b.m_out)[i0 + e] = (float)m[e];
+            else static_cast<f16*>(b.m_out)[i0 + e] = f16{f32_to_f16((float)m[e])};
         }
     }
 }
@@ -773,14 +816,19 @@ __device__ __forceinline__ void fedopt_strip(const OptBuffers& b, const OptScala
             for (int e = 0; e < E; ++e) y[e] = e < rem ? yp[e] : Y{};
         }
 #pragma unroll
-        for (int e = 0; e < E; ++e) pg[e] = widen<Y, V>(y[e]) - ov[e];
+        for (int e = 0; e < E; ++e) pg[e] = pg_sub<PG>(widen<Y, V>(y[e]), ov[e]);
         k = 1;
     } else {
-        V* pgp = static_cast<V*>(b.pg) + i0;
-        if (full) strip_load<V, E, false>(pgp, pg);
-        else {
+        using T = typename PG::T;                 // the workspace holds pg in its own dtype
+        const T* pgp = static_cast<const T*>(b.pg) + i0;
+        if (full) {
+            T t[E];
+            strip_load<T, E, false>(pgp, t);
 #pragma unroll
-            for (int e = 0; e < E; ++e) pg[e] = e < rem ? pgp[e] : V{};
+            for (int e = 0; e < E; ++e) pg[e] = widen<T, V>(t[e]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) pg[e] = e < rem ? widen<T, V>(pgp[e]) : V{};
         }
     }
     if (full) {
@@ -795,7 +843,7 @@ __device__ __forceinline__ void fedopt_strip(const OptBuffers& b, const OptScala
                 const double r = tab.r[k + u];
                 V d[E];
 #pragma unroll
-                for (int e = 0; e < E; ++e) d[e] = widen<Y, V>(y[u][e]) - ov[e];   // subtract(next, old)
+                for (int e = 0; e < E; ++e) d[e] = pg_sub<PG>(widen<Y, V>(y[u][e]), ov[e]);   // subtract(next, old)
                 fold_strip<PG, E>(pg, d, n, N, r);
             }
         }
@@ -806,14 +854,18 @@ __device__ __forceinline__ void fedopt_strip(const OptBuffers& b, const OptScala
         const double r = tab.r[k];
 #pragma unroll
         for (int e = 0; e < E; ++e)
-            if (e < rem) pg[e] = PG::fold(pg[e], widen<Y, V>(yp[e]) - ov[e], n, N, r);
+            if (e < rem) pg[e] = PG::fold(pg[e], pg_sub<PG>(widen<Y, V>(yp[e]), ov[e]), n, N, r);
     }
 
     if constexpr (!FINAL) {
-        V* pgp = static_cast<V*>(b.pg) + i0;
-        if (full) strip_store<V, E>(pgp, pg);
+        using T = typename PG::T;
+        T* pgp = static_cast<T*>(b.pg) + i0;
+        T t[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) t[e] = narrow<T, V>(pg[e]);
+        if (full) strip_store<T, E>(pgp, t);
         else
-            for (int e = 0; e < rem; ++e) pgp[e] = pg[e];
+            for (int e = 0; e < rem; ++e) pgp[e] = t[e];
         return;
     } else {
         opt_final<PG, E, NOST, OSM>(b, s, pg, ov, i0, rem);
@@ -850,11 +902,15 @@ __device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const Op
 #pragma unroll
         for (int h = 0; h < NH; ++h) strip_load<Y, H, NT>(yp + at(h), half(y, h));
 #pragma unroll
-        for (int e = 0; e < E; ++e) pg[e] = widen<Y, V>(y[e]) - ov[e];
+        for (int e = 0; e < E; ++e) pg[e] = pg_sub<PG>(widen<Y, V>(y[e]), ov[e]);
         k = 1;
     } else {
+        using T = typename PG::T;                 // the workspace holds pg in its own dtype
+        T t[E];
 #pragma unroll
-        for (int h = 0; h < NH; ++h) strip_load<V, H, false>(static_cast<const V*>(b.pg) + at(h), half(pg, h));
+        for (int h = 0; h < NH; ++h) strip_load<T, H, false>(static_cast<const T*>(b.pg) + at(h), half(t, h));
+#pragma unroll
+        for (int e = 0; e < E; ++e) pg[e] = widen<T, V>(t[e]);
     }
     for (; k + U <= K; k += U) {
         Y y[U][E];
@@ -868,7 +924,7 @@ __device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const Op
         for (int u = 0; u < U; ++u) {
             V d[E];
 #pragma unroll
-            for (int e = 0; e < E; ++e) d[e] = widen<Y, V>(y[u][e]) - ov[e];
+            for (int e = 0; e < E; ++e) d[e] = pg_sub<PG>(widen<Y, V>(y[u][e]), ov[e]);
             fold_strip<PG, E>(pg, d, tab.n[k + u], tab.N[k + u], tab.r[k + u]);
         }
     }
@@ -879,12 +935,16 @@ __device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const Op
         for (int h = 0; h < NH; ++h) strip_load<Y, H, NT>(yp + at(h), half(y, h));
         V d[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) d[e] = widen<Y, V>(y[e]) - ov[e];
+        for (int e = 0; e < E; ++e) d[e] = pg_sub<PG>(widen<Y, V>(y[e]), ov[e]);
         fold_strip<PG, E>(pg, d, tab.n[k], tab.N[k], tab.r[k]);
     }
     if constexpr (!FINAL) {
+        using T = typename PG::T;
+        T t[E];
 #pragma unroll
-        for (int h = 0; h < NH; ++h) strip_store<V, H>(static_cast<V*>(b.pg) + at(h), half(pg, h));
+        for (int e = 0; e < E; ++e) t[e] = narrow<T, V>(pg[e]);
+#pragma unroll
+        for (int h = 0; h < NH; ++h) strip_store<T, H>(static_cast<T*>(b.pg) + at(h), half(t, h));
     } else {
         double mi[E], vv[E];
 #pragma unroll
@@ -1266,10 +1326,9 @@ void fill_table(ClientTable<S>& t, const void* const* ptrs, const double* n, con
 }
 
 // numpy's conversion of a python int to float16 (round-to-nearest-even), kept in f32
-float to_half_value(double v) {
-    __half h = __float2half_rn((float)v);
-    return __half2float(h);
-}
+// a python float / int as numpy's float16 weak scalar: ONE round-to-nearest-even from double (held in
+// an f32; every half is exact in f32)
+float to_half_value(double v) { return (float)(_Float16)v; }
 
 int64_t grid_for(int64_t P, int E) {
     const int64_t strips = (P + E - 1) / E;
@@ -1553,6 +1612,12 @@ int launch_fedopt(const OptBuffers& b, const OptScalars& s, const void* const* u
     do {
         const int cnt = (K - k0) < kMaxK ? (K - k0) : kMaxK;
         fill_table<S>(tab, ups, n, N, k0, cnt);
+        if constexpr (std::is_same<PG, CF16>::value) {
+            for (int j = 0; j < cnt; ++j) {       // numpy casts the python n, N to the half dtype
+                tab.n[j] = (S)to_half_value(n[k0 + j]);
+                tab.N[j] = (S)to_half_value(N[k0 + j]);
+            }
+        }
         const bool last = k0 + cnt >= K;
         const bool fin = last && final_all;
 #ifdef FEDAGG_PROBES
@@ -1689,20 +1754,21 @@ int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, i
     if (final_ && (!m_out || !v_out || !out)) return fail(FA_EINVAL, "fa_fedopt_step: null output buffer");
     if (serveropt < FA_ADAM || serveropt > FA_ADAGRAD) return fail(FA_EINVAL, "fa_fedopt_step: unsupported serveropt %d", serveropt);
     auto is_int = [](int d) { return d == FA_I32 || d == FA_I64; };
-    if (old_dtype != FA_F32 && old_dtype != FA_F64 && !is_int(old_dtype))
+    if (old_dtype != FA_F32 && old_dtype != FA_F64 && old_dtype != FA_F16 && !is_int(old_dtype))
         return fail(FA_EDTYPE, "fa_fedopt_step: old dtype %d", old_dtype);
-    if (upd_dtype != FA_F32 && upd_dtype != FA_F64 && upd_dtype != FA_BF16 && !is_int(upd_dtype))
+    if (upd_dtype != FA_F32 && upd_dtype != FA_F64 && upd_dtype != FA_BF16 && upd_dtype != FA_F16 && !is_int(upd_dtype))
         return fail(FA_EDTYPE, "fa_fedopt_step: update dtype %d", upd_dtype);
     if (is_int(old_dtype) && !is_int(upd_dtype))
         return fail(FA_EDTYPE, "fa_fedopt_step: integer global model with float updates is unsupported");
     // integer tensors: subtract = next*1.0 + old*(-1.0) turns them into float64 (numpy: int * python float)
     const int pg_dt = is_int(upd_dtype) ? FA_F64 : fa_promote(upd_dtype, old_dtype);
-    if (m_in && m_in_dtype != FA_F32 && m_in_dtype != FA_F64) return fail(FA_EDTYPE, "fa_fedopt_step: m dtype %d", m_in_dtype);
+    if (m_in && m_in_dtype != FA_F32 && m_in_dtype != FA_F64 && m_in_dtype != FA_F16)
+        return fail(FA_EDTYPE, "fa_fedopt_step: m dtype %d", m_in_dtype);
     if (!m_in) m_in_dtype = FA_NONE;
     const int m_out_dt = fa_promote(m_in_dtype, pg_dt);
+    auto mcode = [](int d) { return d == FA_NONE ? -1 : d == FA_F64 ? 1 : d == FA_F16 ? 2 : 0; };
 
-    OptBuffers b{old, pg, m_in, m_out, v_in, v_out, out, m_in_dtype == FA_NONE ? -1 : (m_in_dtype == FA_F64 ? 1 : 0),
-                 m_out_dt == FA_F64 ? 1 : 0};
+    OptBuffers b{old, pg, m_in, m_out, v_in, v_out, out, mcode(m_in_dtype), mcode(m_out_dt)};
     OptScalars s;
     s.lr = lr;
     s.b1 = beta1;
@@ -1716,6 +1782,9 @@ int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, i
     s.c1f = (float)s.c1;
     // fedopt adam: p*(1-beta2); p has the pg dtype
     s.c2f = (float)s.c2;
+    s.b1h = to_half_value(beta1);
+    s.c1h = to_half_value(s.c1);
+    s.c2h = to_half_value(s.c2);
     s.opt = serveropt;
 
     if (upd_dtype == FA_F32 && old_dtype == FA_F32) return launch_fedopt<float, float, CF32>(b, s, updates, n, N, K, P, flags, st);
@@ -1724,6 +1793,12 @@ int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, i
     if (upd_dtype == FA_F64 && old_dtype == FA_F64) return launch_fedopt<double, double, CF64>(b, s, updates, n, N, K, P, flags, st);
     if (upd_dtype == FA_BF16 && old_dtype == FA_F64) return launch_fedopt<bf16, double, CF64>(b, s, updates, n, N, K, P, flags, st);
     if (upd_dtype == FA_F64 && old_dtype == FA_F32) return launch_fedopt<double, float, CF64>(b, s, updates, n, N, K, P, flags, st);
+    // float16 sessions (numpy's half loops for the pseudo-gradient while it is float16)
+    if (upd_dtype == FA_F16 && old_dtype == FA_F16) return launch_fedopt<f16, f16, CF16>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_F16 && old_dtype == FA_F32) return launch_fedopt<f16, float, CF32>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_F16 && old_dtype == FA_F64) return launch_fedopt<f16, double, CF64>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_F32 && old_dtype == FA_F16) return launch_fedopt<float, f16, CF32>(b, s, updates, n, N, K, P, flags, st);
+    if (upd_dtype == FA_F64 && old_dtype == FA_F16) return launch_fedopt<double, f16, CF64>(b, s, updates, n, N, K, P, flags, st);
     if (upd_dtype == FA_I64 && old_dtype == FA_I64) return launch_fedopt<int64_t, int64_t, CF64>(b, s, updates, n, N, K, P, flags, st);
     if (upd_dtype == FA_I64 && old_dtype == FA_F64) return launch_fedopt<int64_t, double, CF64>(b, s, updates, n, N, K, P, flags, st);
     if (upd_dtype == FA_I64 && old_dtype == FA_F32) return launch_fedopt<int64_t, float, CF64>(b, s, updates, n, N, K, P, flags, st);

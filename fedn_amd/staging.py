@@ -564,7 +564,7 @@ class AndroidFedAvgPipeline(_Pipeline):
 class FedOptState:
     """Server-optimizer state of one fedopt Aggregator instance (fedopt.py:36-38), in HBM.
 
-    Fused form: ``m`` / ``v`` map a layout group to a flat device tensor (m: f32 or f64,
+    Fused form: ``m`` / ``v`` map a layout group to a flat device tensor (m: f16, f32 or f64,
     v: f64) for ``layout``. Per-tensor form (after a round on the per-tensor path, mixed.py):
     ``m_t`` / ``v_t`` are lists of device tensors in model order. Both None until the first
     server step, exactly like the reference's ``self.m``/``self.v``.
@@ -690,7 +690,10 @@ def old_members(layout, old_arrays):
 _FUSED_OPT = {(torch.float32, torch.float32), (torch.bfloat16, torch.float32), (torch.float32, torch.float64),
               (torch.float64, torch.float64), (torch.bfloat16, torch.float64), (torch.float64, torch.float32),
               (torch.int64, torch.int64), (torch.int64, torch.float64), (torch.int64, torch.float32),
-              (torch.int32, torch.int32), (torch.int32, torch.float64), (torch.int32, torch.float32)}
+              (torch.int32, torch.int32), (torch.int32, torch.float64), (torch.int32, torch.float32),
+              # float16 sessions: a half global model's pseudo-gradient is half (numpy's half loops)
+              (torch.float16, torch.float16), (torch.float16, torch.float32), (torch.float16, torch.float64),
+              (torch.float32, torch.float16), (torch.float64, torch.float16)}
 
 
 def fused_fedopt_pair(upd, old):
@@ -700,8 +703,8 @@ def fused_fedopt_pair(upd, old):
 
 def check_fedopt_dtypes(layout):
     for dt in layout.groups:
-        if ops.torch_dtype(dt) not in (torch.float32, torch.float64, torch.int32, torch.int64):
-            raise TypeError(f"FedOpt supports float32/float64/int32/int64 updates, got {dt}")
+        if ops.torch_dtype(dt) not in (torch.float16, torch.float32, torch.float64, torch.int32, torch.int64):
+            raise TypeError(f"FedOpt supports float16/float32/float64/int32/int64 updates, got {dt}")
 
 
 class FedOptPipeline(_Pipeline):

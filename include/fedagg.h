@@ -97,9 +97,11 @@ int fa_fedavg_fold(void* agg, int agg_dtype,
  * FedOpt (fedopt.py:74-118, 151-258), fused: pseudo-gradient running mean over the
  * K updates followed (FA_PG_FINAL) by one Adam / Yogi / AdaGrad server step.
  *
- * old       device, P elements of old_dtype (F32 | F64 | I32 | I64): the global model the
+ * old       device, P elements of old_dtype (F32 | F64 | F16 | I32 | I64): the global model the
  *           clients trained from (fedopt.py:90)
- * updates   HOST array of K DEVICE pointers (F32 | BF16 | F64 | I32 | I64); integer tensors
+ * updates   HOST array of K DEVICE pointers (F32 | BF16 | F16 | F64 | I32 | I64); a float16
+ *           pseudo-gradient (F16 updates over an F16 model) is computed with numpy's half loops
+ *           (every op rounded to half, python scalars cast to half); integer tensors
  *           (e.g. BatchNorm counters) become float64 exactly as numpy's int * 1.0 does.
  *           upd_dtype is required even when K = 0: it fixes the pg dtype.
  * n, N      HOST arrays of K doubles (num_examples, running total)
@@ -107,7 +109,7 @@ int fa_fedavg_fold(void* agg, int agg_dtype,
  *           updates); read when
  *           !FA_PG_FIRST, written when !FA_PG_FINAL (and used internally when
  *           K exceeds one launch); may be NULL when FIRST|FINAL and K <= 64
- * m_in      device, P elements of m_in_dtype, or NULL with m_in_dtype = FA_NONE
+ * m_in      device, P elements of m_in_dtype (F16 | F32 | F64), or NULL with m_in_dtype = FA_NONE
  * m_out     device, dtype promote(m_in, pg) (pg dtype when m is None); may alias m_in
  *           when the dtypes are equal
  * v_in      device f64, or NULL (v is None -> ones * tau**2, fedopt.py:170-171)

@@ -678,6 +678,26 @@ def numex_cases(ref):
     ]
 
 
+def f16_fedopt_cases(ref):
+    """FedOpt sessions on a float16 global model (VERDICT r2 follow-up): numpy computes the pseudo-
+    gradient in half while it is half (round 1), then float64; m stays half until it meets a float64
+    pseudo-gradient."""
+    rng = np.random.default_rng(13)
+    fo = [(7,), (3, 5), (2053,)]
+    return [
+        fedopt_clients_case(ref, "fedopt_f16_adam_3r", rng, _spec(F16, fo),
+                            [[_spec(F16, fo)] * 3, [_spec(F16, fo)] * 2, [_spec(F16, fo)] * 3]),
+        fedopt_clients_case(ref, "fedopt_f16_yogi_k70_2r", rng, _spec(F16, fo),
+                            [[_spec(F16, fo)] * 70, [_spec(F16, fo)] * 2], {"serveropt": "yogi"}),
+        fedopt_clients_case(ref, "fedopt_f16_adagrad_2r", rng, _spec(F16, fo),
+                            [[_spec(F16, fo)] * 4, [_spec(F16, fo)] * 3], {"serveropt": "adagrad"}),
+        fedopt_clients_case(ref, "fedopt_f16_upd_f32_old_2r", rng, _spec(F32, fo),
+                            [[_spec(F16, fo)] * 3, [_spec(F16, fo)] * 2]),
+        fedopt_clients_case(ref, "fedopt_f32_upd_f16_old_2r", rng, _spec(F16, fo),
+                            [[_spec(F32, fo)] * 3, [_spec(F32, fo)] * 2], {"serveropt": "yogi"}),
+    ]
+
+
 def edge_cases(ref):
     """Zero-size tensors (alone and among others) and rounds of more than 64 clients (the
     kernarg client table's size: several launches / arena batches per round)."""
@@ -716,6 +736,8 @@ def main():
         return _write([helper_power_norm(ref, np.random.default_rng(9))], merge=True)
     if only == "edge":
         return _write(edge_cases(ref), merge=True)
+    if only == "f16opt":
+        return _write(f16_fedopt_cases(ref), merge=True)
     if only == "numex":
         return _write(numex_cases(ref), merge=True)
     if only == "reduce":
@@ -770,6 +792,7 @@ def main():
     cases.append(helper_power_norm(ref, np.random.default_rng(9)))
     cases += edge_cases(ref)
     cases += numex_cases(ref)
+    cases += f16_fedopt_cases(ref)
     _write(cases, merge=False)
 
 
