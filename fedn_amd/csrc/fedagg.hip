@@ -1091,6 +1091,17 @@ k_fedopt(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::
 // ----------------------------------------------------------------------------
 template <typename T> __device__ __forceinline__ T as_t(double v) { return (T)v; }
 
+// numpyhelper.add / subtract on float16 arrays: x*a + y*b with the python scalars cast to half and
+// every op computed in float and rounded to half (numpy's half loops)
+__global__ void __launch_bounds__(kBlock) k_axpby_half(f16* __restrict__ out, const f16* __restrict__ x,
+                                                       const f16* __restrict__ y, float ah, float bh, int64_t P) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < P; i += (int64_t)gridDim.x * kBlock) {
+        const float xa = CF16::rh(f16_to_f32(x[i].bits) * ah);
+        const float yb = CF16::rh(f16_to_f32(y[i].bits) * bh);
+        out[i] = f16{f32_to_f16(xa + yb)};
+    }
+}
+
 template <typename TX, typename TY, typename TO>
 __global__ void __launch_bounds__(kBlock)
 k_elementwise(int op, TO* __restrict__ out, const TX* __restrict__ x, const TY* __restrict__ y, double a, double b,
@@ -1841,6 +1852,12 @@ int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype,
         else
             hipLaunchKernelGGL(k_ifold<int64_t>, g, dim3(kBlock), 0, sti, static_cast<double*>(out),
                                static_cast<const int64_t*>(x), static_cast<const int64_t*>(y), a, b, P);
+        return check_launch("fa_elementwise");
+    }
+    if (op == FA_EW_AXPBY && x_dtype == FA_F16 && y_dtype == FA_F16 && out_dtype == FA_F16) {
+        const dim3 g((unsigned)std::min<int64_t>((P + kBlock - 1) / kBlock, 8192));
+        hipLaunchKernelGGL(k_axpby_half, g, dim3(kBlock), 0, static_cast<hipStream_t>(stream), static_cast<f16*>(out),
+                           static_cast<const f16*>(x), static_cast<const f16*>(y), to_half_value(a), to_half_value(b), P);
         return check_launch("fa_elementwise");
     }
     auto isf = [](int d) { return d == FA_F32 || d == FA_F64; };

@@ -88,12 +88,12 @@ def int_float_n(dtypes, nfolds, n):
 
 def sub_plan(ys, olds):
     """numpyhelper.subtract(next, old) = next*1.0 + old*(-1.0) per tensor (numpyhelper.py:44-56):
-    [(result dtype, shape)], zip-truncated; float32 / float64 results only (fa_elementwise)."""
+    [(result dtype, shape)], zip-truncated; float16 / float32 / float64 results (fa_elementwise)."""
     plan = []
     for (yshape, ydt), (oshape, odt) in zip(ys, olds):
         shape = tuple(np.broadcast_shapes(yshape, oshape))
         r = np.add(np.multiply(_e(ydt), 1.0), np.multiply(_e(odt), -1.0))
-        if ydt not in _SUPPORTED or odt not in _SUPPORTED or r.dtype not in (np.float32, np.float64):
+        if ydt not in _SUPPORTED or odt not in _SUPPORTED or r.dtype not in (np.float16, np.float32, np.float64):
             raise TypeError(f"unsupported dtypes for the pseudo-gradient: update {ydt}, global model {odt}")
         plan.append((r.dtype, shape))
     return plan
@@ -263,17 +263,19 @@ class TensorFedOpt:
             if v is not None:
                 shapes.append(tuple(v[i].shape))
             B = tuple(np.broadcast_shapes(*shapes))
-            if p.dtype not in (torch.float32, torch.float64):
+            if p.dtype not in (torch.float16, torch.float32, torch.float64):
                 raise TypeError(f"pseudo-gradient dtype {p.dtype} is not supported by the server step")
-            odt = torch.float32 if o.dtype == torch.float16 else o.dtype   # f16 -> f32 is exact
-            if odt not in (torch.float32, torch.float64, torch.int32, torch.int64):
+            # a half pg comes from half updates over a half model (numpy's half loops, the kernel's
+            # CF16 step); otherwise a half model enters the step widened to f32, which is exact
+            odt = o.dtype if p.dtype == torch.float16 or o.dtype != torch.float16 else torch.float32
+            if odt not in (torch.float16, torch.float32, torch.float64, torch.int32, torch.int64):
                 raise TypeError(f"global-model dtype {o.dtype} is not supported by the server step")
             # the update dtype handed to fa_fedopt_step only fixes the pg dtype (K = 0)
             upd = odt if odt in (torch.int32, torch.int64) else p.dtype
             if ops.fedopt_dtypes(upd, odt, None)[0] != p.dtype:
                 raise TypeError(f"pseudo-gradient {p.dtype} over a {o.dtype} global model is not supported")
             mdt = None if m is None else m[i].dtype
-            if mdt is not None and mdt not in (torch.float32, torch.float64):
+            if mdt is not None and mdt not in (torch.float16, torch.float32, torch.float64):
                 raise TypeError(f"m dtype {mdt} is not supported")
             plan.append((B, odt, upd, ops.fedopt_dtypes(upd, odt, mdt)[1]))
         model, new_m, new_v = [], [], []

@@ -148,7 +148,8 @@ int fa_running_mean(void* g, int dtype, const void* m, double a, double b, doubl
 
 /*
  * numpyhelper primitives (numpyhelper.py:34-142) on device buffers, numpy rounding (python
- * scalars a, b are weak: x*a is computed in x's dtype, then promoted). F32 / F64 only.
+ * scalars a, b are weak: x*a is computed in x's dtype, then promoted). F32 / F64, and AXPBY on
+ * three F16 arrays (numpy's half loops: a, b cast to half, every op rounded to half).
  *   FA_EW_AXPBY   out = x*a + y*b                 numpyhelper.add / subtract (b -> -b)
  *   FA_EW_MUL     out = x*y, or x*a if y == NULL   numpyhelper.multiply
  *   FA_EW_DIV     out = x/y, or x/a if y == NULL   numpyhelper.divide

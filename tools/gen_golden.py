@@ -695,6 +695,13 @@ def f16_fedopt_cases(ref):
                             [[_spec(F16, fo)] * 3, [_spec(F16, fo)] * 2]),
         fedopt_clients_case(ref, "fedopt_f32_upd_f16_old_2r", rng, _spec(F16, fo),
                             [[_spec(F32, fo)] * 3, [_spec(F32, fo)] * 2], {"serveropt": "yogi"}),
+        # per-tensor path: a broadcast client keeps the pg half; a float32 client promotes it
+        fedopt_clients_case(ref, "fedopt_f16_bcast_2r", rng, _spec(F16, fo),
+                            [[_spec(F16, fo), _spec(F16, [(1,), (3, 5), (2053,)]), _spec(F16, fo)],
+                             [_spec(F16, fo)] * 2]),
+        fedopt_clients_case(ref, "fedopt_f16_mixed_2r", rng, _spec(F16, fo),
+                            [[_spec(F16, fo), _spec(F32, fo), _spec(F16, [(7,), (1, 5), (2053,)])],
+                             [_spec(F16, fo)] * 2], {"serveropt": "adagrad"}),
     ]
 
 
