@@ -400,3 +400,19 @@ def test_pmc_rank_geometry_matches_bench(world, R, monkeypatch):
     assert R in bench.AG_ROUNDS
     cyc = sh.CyclicShardedFedAvg(P, chunk=-(-P // (world * R)))
     assert rank_geometry(P, world, R) == (cyc.C, cyc.rounds, cyc.local_len)
+
+
+def test_staging_cache_keeps_two_sizes_and_hands_out_once():
+    """staging.StagingCache: a round's resources come back for the next round of the same size on
+    the same device, are taken at most once, and at most ``keep`` sizes are kept (oldest dropped)."""
+    from fedn_amd.staging import StagingCache
+    c = StagingCache(keep=2)
+    a, b, d = {"slots": ["a"]}, {"slots": ["b"]}, {"slots": ["d"]}
+    c.give("cuda:0", 100, a)
+    c.give("cuda:0", 200, b)
+    assert c.take("cuda:1", 100) is None                  # another device: nothing
+    assert c.take("cuda:0", 100) is a and c.take("cuda:0", 100) is None
+    c.give("cuda:0", 100, a)
+    c.give("cuda:0", 300, d)                              # third size: the oldest (200) goes
+    assert c.take("cuda:0", 200) is None
+    assert c.take("cuda:0", 100) is a and c.take("cuda:0", 300) is d
