@@ -535,8 +535,9 @@ class ShardedFedOptPipeline(_ShardedStaging):
                 m_in = state.m[d][dt] if state.m is not None else None
                 v_in = state.v[d][dt] if state.v is not None else None
                 _, m_dt = ops.fedopt_dtypes(ops.torch_dtype(dt), old.dtype, None if m_in is None else m_in.dtype)
-                m_out = m_in if (m_in is not None and m_in.dtype == m_dt) else torch.empty(P, dtype=m_dt, device=dv)
-                v_out = v_in if v_in is not None else torch.empty(P, dtype=torch.float64, device=dv)
+                # new m / v buffers: a failed step leaves the session's state untouched (staging.py)
+                m_out = torch.empty(P, dtype=m_dt, device=dv)
+                v_out = torch.empty(P, dtype=torch.float64, device=dv)
                 out = torch.empty(P, dtype=torch.float64, device=dv)
                 pg = self._pg(d, dt) if (not first or len(entries) > BATCH) else None
                 new_m[d][dt], new_v[d][dt] = m_out, v_out

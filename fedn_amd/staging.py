@@ -849,9 +849,10 @@ class FedOptPipeline(_Pipeline):
             m_in = state.m[dt] if state.m is not None else None
             v_in = state.v[dt] if state.v is not None else None
             _, m_dt = ops.fedopt_dtypes(ops.torch_dtype(dt), old.dtype, None if m_in is None else m_in.dtype)
-            m_out = m_in if (m_in is not None and m_in.dtype == m_dt) else torch.empty(P, dtype=m_dt,
-                                                                                        device=self.device)
-            v_out = v_in if v_in is not None else torch.empty(P, dtype=torch.float64, device=self.device)
+            # new m / v buffers (same HBM traffic as in place): a step that fails part-way through
+            # its chunks leaves the session's state exactly as the last completed round left it
+            m_out = torch.empty(P, dtype=m_dt, device=self.device)
+            v_out = torch.empty(P, dtype=torch.float64, device=self.device)
             out = torch.empty(P, dtype=torch.float64, device=self.device)
             # pg workspace: needed unless this launch starts AND ends the pseudo-gradient in registers
             pg = self._pg(dt) if (not first or len(entries) > BATCH) else None

@@ -73,23 +73,32 @@ def test_fedavg_fold_failure_skips_the_update(monkeypatch, shapes, fail_call):
     assert uh.model_updates.qsize() == 0
 
 
-def test_fedopt_server_step_failure_returns_none_and_keeps_state(monkeypatch):
-    """The fused server step fails (at its first launch) in round 2: ``(None, data)``, m / v stay
-    round 1's, and round 3 continues from them exactly as if round 2 had not run. (A device failure
-    part-way through a chunked step can leave v, which is updated in place, partly advanced — as
-    an exception inside fedopt.py's server step can leave self.v assigned and self.m not.)"""
+@pytest.mark.parametrize("shapes,at_chunk", [([(700, 900), (333,)], 1), ([(1500, 1500), (333,)], 2)],
+                         ids=["first_launch", "second_chunk"])
+def test_fedopt_server_step_failure_returns_none_and_keeps_state(monkeypatch, shapes, at_chunk):
+    """The fused server step fails in round 2 — at its first launch, or at the second of the chunked
+    launches after the first chunk's m / v were written: ``(None, data)``, m / v stay round 1's (the
+    step writes new buffers), and round 3 continues from them exactly as if round 2 had not run."""
     from fedn_amd.aggregators.fedopt import Aggregator
     from fedn_amd.updatehandler import MemoryUpdateHandler
     rng = np.random.default_rng(52)
-    shapes = [(700, 900), (333,)]
     uh = MemoryUpdateHandler()
     agg = Aggregator(uh, device=DEV)
     st = ref.FedOptState()
     old = [rng.standard_normal(s).astype(np.float32) for s in shapes]
     fail = [False]
-    calls = _failing(monkeypatch, "fedopt_step", lambda i, kw: kw.get("final") and fail[0])
+    finals = [0]
+
+    def fail_on(i, kw):
+        if not kw.get("final") or not fail[0]:
+            return False
+        finals[0] += 1
+        return finals[0] == at_chunk
+
+    calls = _failing(monkeypatch, "fedopt_step", fail_on)
     for r in range(3):
         fail[0] = r == 1
+        finals[0] = 0
         ups = [[(o + 0.01 * rng.standard_normal(o.shape)).astype(o.dtype) for o in old] for _ in range(3)]
         ns = [int(v) for v in rng.integers(1, 5001, 3)]
         gid = uh.put_global_model(old, f"global-{r}")
