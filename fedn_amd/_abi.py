@@ -17,12 +17,14 @@ LIB_PATH = os.path.join(_HERE, LIB_NAME)
 
 # element type codes (enum fa_dtype)
 FA_NONE, FA_F32, FA_F64, FA_BF16, FA_F16, FA_I32, FA_I64 = -1, 0, 1, 2, 3, 4, 5
+FA_I8, FA_I16, FA_U8, FA_U16, FA_U32, FA_U64 = 6, 7, 8, 9, 10, 11
 # status codes (enum fa_status)
 FA_OK, FA_EINVAL, FA_EDTYPE, FA_EHIP = 0, 1, 2, 3
 # server optimizers (enum fa_serveropt)
 FA_ADAM, FA_YOGI, FA_ADAGRAD = 0, 1, 2
 FA_PG_FIRST, FA_PG_FINAL = 1, 2
-FA_EW_AXPBY, FA_EW_MUL, FA_EW_DIV, FA_EW_SQRT, FA_EW_SQUARE, FA_EW_SIGN, FA_EW_FILL, FA_EW_POW, FA_EW_IPOW, FA_EW_IFOLD = range(10)
+(FA_EW_AXPBY, FA_EW_MUL, FA_EW_DIV, FA_EW_SQRT, FA_EW_SQUARE, FA_EW_SIGN, FA_EW_FILL, FA_EW_POW, FA_EW_IPOW, FA_EW_IFOLD,
+ FA_EW_NFOLD) = range(11)
 (FA_TUNE_STRIPS, FA_TUNE_UNROLL, FA_TUNE_NT, FA_TUNE_FASTDIV, FA_TUNE_LANETAB, FA_TUNE_GRID, FA_TUNE_READ,
  FA_TUNE_BLOCK, FA_TUNE_SUM_NOSTORE, FA_TUNE_NT_STORE, FA_TUNE_FASTDIV64, FA_TUNE_TILEMAP, FA_TUNE_OPT_NT,
  FA_TUNE_OPT_NOSTORE, FA_TUNE_OPT_STORE, FA_TUNE_OPT_COAL, FA_TUNE_NARROW, FA_TUNE_LDS, FA_TUNE_WPE, FA_TUNE_OPT_MV, FA_TUNE_AUTO_GEOM,

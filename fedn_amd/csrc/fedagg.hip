@@ -1163,15 +1163,32 @@ __global__ void __launch_bounds__(kBlock) k_ipow(T* __restrict__ out, const T* _
 // numpyhelper.increment_average (numpyhelper.py:32) on integer arrays folded with a python-float
 // num_examples: numpy subtracts in the integer dtype (wrapping), multiplies the difference by the
 // float n in float64, divides by N in float64 and adds x in float64 — each op rounded once.
+// Any integer width: the difference is taken in the same-width unsigned type (no signed overflow)
+// and wrapped back to T.
 template <typename T>
 __global__ void __launch_bounds__(kBlock) k_ifold(double* __restrict__ out, const T* __restrict__ x,
                                                   const T* __restrict__ y, double n, double N, int64_t P) {
     using U = typename std::make_unsigned<T>::type;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < P; i += (int64_t)gridDim.x * kBlock) {
-        const T d = (T)((U)y[i] - (U)x[i]);
+        const T d = (T)(U)((U)y[i] - (U)x[i]);
         double t = (double)d * n;
         t = t / N;
         out[i] = (double)x[i] + t;
+    }
+}
+
+// The same fold with a python-INT num_examples (numpy's weak int scalar takes the array's dtype):
+// difference AND product wrap in T (computed in a >= 32-bit unsigned type, so no signed overflow
+// and no int promotion surprises for 8/16-bit T), then true_divide by N in float64 and add x.
+template <typename T>
+__global__ void __launch_bounds__(kBlock) k_nfold(double* __restrict__ out, const T* __restrict__ x,
+                                                  const T* __restrict__ y, T n, double N, int64_t P) {
+    using U = typename std::make_unsigned<T>::type;
+    using W = typename std::conditional<(sizeof(T) < 8), uint32_t, uint64_t>::type;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < P; i += (int64_t)gridDim.x * kBlock) {
+        const W d = (W)(U)((W)(U)y[i] - (W)(U)x[i]);
+        const T p = (T)(U)(d * (W)(U)n);
+        out[i] = (double)x[i] + (double)p / N;
     }
 }
 
@@ -1251,7 +1268,10 @@ k_cast(TO* __restrict__ out, const TI* __restrict__ in, const CastGeom g, const 
                 rem = q;
             }
         }
-        out[i] = widen<TI, TO>(in[j]);
+        if constexpr (std::is_same<TO, f16>::value && std::is_integral<TI>::value)
+            out[i] = f16{f32_to_f16((float)in[j])};          // int8 / uint8 only: exact in half
+        else
+            out[i] = widen<TI, TO>(in[j]);
     }
 }
 
@@ -1823,7 +1843,7 @@ int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype,
                    double a, double b, int64_t P, void* stream) {
     g_err[0] = 0;
     if (P < 0 || !out || (op != FA_EW_FILL && !x)) return fail(FA_EINVAL, "fa_elementwise: bad arguments");
-    if (op < FA_EW_AXPBY || op > FA_EW_IFOLD) return fail(FA_EINVAL, "fa_elementwise: unknown op %d", op);
+    if (op < FA_EW_AXPBY || op > FA_EW_NFOLD) return fail(FA_EINVAL, "fa_elementwise: unknown op %d", op);
     if (op == FA_EW_AXPBY && !y) return fail(FA_EINVAL, "fa_elementwise: AXPBY needs y");
     if (P == 0) return FA_OK;
     if (op == FA_EW_IPOW) {
@@ -1841,18 +1861,35 @@ int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype,
                                static_cast<const int64_t*>(x), (uint64_t)a, P);
         return check_launch("fa_elementwise");
     }
-    if (op == FA_EW_IFOLD) {
-        if (!y || out_dtype != FA_F64 || x_dtype != y_dtype || (x_dtype != FA_I32 && x_dtype != FA_I64))
-            return fail(FA_EDTYPE, "fa_elementwise: IFOLD takes two int32 or two int64 arrays and returns float64");
+    if (op == FA_EW_IFOLD || op == FA_EW_NFOLD) {
+        if (!y || out_dtype != FA_F64 || x_dtype != y_dtype)
+            return fail(FA_EDTYPE, "fa_elementwise: IFOLD / NFOLD take two arrays of one integer dtype and return float64");
+        if (op == FA_EW_NFOLD && !(std::fabs(a) < 0x1p53 && a == std::floor(a)))
+            return fail(FA_EINVAL, "fa_elementwise: NFOLD num_examples must be an integer below 2^53 in magnitude");
         const dim3 g((unsigned)std::min<int64_t>((P + kBlock - 1) / kBlock, 8192));
         hipStream_t sti = static_cast<hipStream_t>(stream);
-        if (x_dtype == FA_I32)
-            hipLaunchKernelGGL(k_ifold<int32_t>, g, dim3(kBlock), 0, sti, static_cast<double*>(out),
-                               static_cast<const int32_t*>(x), static_cast<const int32_t*>(y), a, b, P);
-        else
-            hipLaunchKernelGGL(k_ifold<int64_t>, g, dim3(kBlock), 0, sti, static_cast<double*>(out),
-                               static_cast<const int64_t*>(x), static_cast<const int64_t*>(y), a, b, P);
-        return check_launch("fa_elementwise");
+        auto run = [&](auto tag) -> int {
+            using T = decltype(tag);
+            using U = typename std::make_unsigned<T>::type;
+            if (op == FA_EW_IFOLD)
+                hipLaunchKernelGGL(k_ifold<T>, g, dim3(kBlock), 0, sti, static_cast<double*>(out),
+                                   static_cast<const T*>(x), static_cast<const T*>(y), a, b, P);
+            else
+                hipLaunchKernelGGL(k_nfold<T>, g, dim3(kBlock), 0, sti, static_cast<double*>(out),
+                                   static_cast<const T*>(x), static_cast<const T*>(y), (T)(U)(int64_t)a, b, P);
+            return check_launch("fa_elementwise");
+        };
+        switch (x_dtype) {
+            case FA_I8: return run(int8_t{});
+            case FA_I16: return run(int16_t{});
+            case FA_I32: return run(int32_t{});
+            case FA_I64: return run(int64_t{});
+            case FA_U8: return run(uint8_t{});
+            case FA_U16: return run(uint16_t{});
+            case FA_U32: return run(uint32_t{});
+            case FA_U64: return run(uint64_t{});
+            default: return fail(FA_EDTYPE, "fa_elementwise: IFOLD / NFOLD need an integer dtype, got %d", x_dtype);
+        }
     }
     if (op == FA_EW_AXPBY && x_dtype == FA_F16 && y_dtype == FA_F16 && out_dtype == FA_F16) {
         const dim3 g((unsigned)std::min<int64_t>((P + kBlock - 1) / kBlock, 8192));
@@ -1959,6 +1996,42 @@ int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, co
     FA_CAST(FA_I32, int32_t, FA_I64, int64_t)
     FA_CAST(FA_I32, int32_t, FA_F64, double)
     FA_CAST(FA_I64, int64_t, FA_F64, double)
+    // narrow / unsigned integers: identity (broadcast) and numpy's safe widenings
+    FA_CAST(FA_I8, int8_t, FA_I8, int8_t)
+    FA_CAST(FA_I8, int8_t, FA_I16, int16_t)
+    FA_CAST(FA_I8, int8_t, FA_I32, int32_t)
+    FA_CAST(FA_I8, int8_t, FA_I64, int64_t)
+    FA_CAST(FA_I8, int8_t, FA_F16, f16)
+    FA_CAST(FA_I8, int8_t, FA_F32, float)
+    FA_CAST(FA_I8, int8_t, FA_F64, double)
+    FA_CAST(FA_U8, uint8_t, FA_U8, uint8_t)
+    FA_CAST(FA_U8, uint8_t, FA_I16, int16_t)
+    FA_CAST(FA_U8, uint8_t, FA_U16, uint16_t)
+    FA_CAST(FA_U8, uint8_t, FA_I32, int32_t)
+    FA_CAST(FA_U8, uint8_t, FA_U32, uint32_t)
+    FA_CAST(FA_U8, uint8_t, FA_I64, int64_t)
+    FA_CAST(FA_U8, uint8_t, FA_U64, uint64_t)
+    FA_CAST(FA_U8, uint8_t, FA_F16, f16)
+    FA_CAST(FA_U8, uint8_t, FA_F32, float)
+    FA_CAST(FA_U8, uint8_t, FA_F64, double)
+    FA_CAST(FA_I16, int16_t, FA_I16, int16_t)
+    FA_CAST(FA_I16, int16_t, FA_I32, int32_t)
+    FA_CAST(FA_I16, int16_t, FA_I64, int64_t)
+    FA_CAST(FA_I16, int16_t, FA_F32, float)
+    FA_CAST(FA_I16, int16_t, FA_F64, double)
+    FA_CAST(FA_U16, uint16_t, FA_U16, uint16_t)
+    FA_CAST(FA_U16, uint16_t, FA_I32, int32_t)
+    FA_CAST(FA_U16, uint16_t, FA_U32, uint32_t)
+    FA_CAST(FA_U16, uint16_t, FA_I64, int64_t)
+    FA_CAST(FA_U16, uint16_t, FA_U64, uint64_t)
+    FA_CAST(FA_U16, uint16_t, FA_F32, float)
+    FA_CAST(FA_U16, uint16_t, FA_F64, double)
+    FA_CAST(FA_U32, uint32_t, FA_U32, uint32_t)
+    FA_CAST(FA_U32, uint32_t, FA_I64, int64_t)
+    FA_CAST(FA_U32, uint32_t, FA_U64, uint64_t)
+    FA_CAST(FA_U32, uint32_t, FA_F64, double)
+    FA_CAST(FA_U64, uint64_t, FA_U64, uint64_t)
+    FA_CAST(FA_U64, uint64_t, FA_F64, double)
 #undef FA_CAST
     return fail(FA_EDTYPE, "fa_cast: unsupported conversion %d -> %d", in_dtype, out_dtype);
 }

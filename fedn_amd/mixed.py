@@ -28,7 +28,34 @@ import torch
 
 from . import ops
 
-_SUPPORTED = {np.dtype(t) for t in (np.float16, np.float32, np.float64, np.int32, np.int64)}
+_NARROW = {np.dtype(t) for t in (np.int8, np.int16, np.uint8, np.uint16, np.uint32, np.uint64)}
+_SUPPORTED = {np.dtype(t) for t in (np.float16, np.float32, np.float64, np.int32, np.int64)} | _NARROW
+
+
+def per_tensor_dtypes(dtypes):
+    """Whether a layout holds tensors only the per-tensor path folds (8 / 16-bit and unsigned
+    integers: fa_cast + fa_elementwise IFOLD / NFOLD; the fused kernels take f16..f64 / i32 / i64),
+    or bool tensors, whose fold numpy refuses (boolean subtract) before anything changes."""
+    return any(np.dtype(d) in _NARROW or np.dtype(d) == np.bool_ for d in dtypes)
+
+
+def _int_fold_kind(d, n):
+    """How an integer difference of dtype ``d`` is multiplied by num_examples ``n``
+    (numpyhelper.py:32, ``n * (y - x)``): "ifold" in float64 (a float n, or numpy promoting the
+    product to float64), "int" in int32 / int64 (the fused kernel's integer first fold), or
+    "nfold" wrapping in a narrow / unsigned dtype (a python int n, weak, takes d's dtype)."""
+    if float_n(n):
+        return "ifold"
+    if d in (np.dtype(np.int32), np.dtype(np.int64)):
+        return "int"
+    p = np.multiply(n, _e(d)).dtype                # raises OverflowError as numpy does
+    if p == np.float64:
+        return "ifold"
+    if p != d:
+        raise TypeError(f"a {type(n).__name__} num_examples times a {d} difference ({p}) is not supported")
+    if abs(int(n)) >= 1 << 53:
+        raise TypeError(f"num_examples {n} is too large for the {d} fold")
+    return "nfold"
 
 
 def np_dtype(t):
@@ -68,6 +95,8 @@ def fold_plan(xs, ys, n, N):
         r = np.add(x0, t)
         if d.dtype not in _SUPPORTED or xdt not in _SUPPORTED or ydt not in _SUPPORTED:
             raise TypeError(f"unsupported dtypes for the fold: model {xdt}, update {ydt}")
+        if d.dtype.kind in "iu":
+            _int_fold_kind(d.dtype, n)
         plan.append((d.dtype, r.dtype, shape))
     return plan
 
@@ -195,8 +224,12 @@ class TensorFedAvg:
                     xc = _as(x, td, shape, self.stream)
                     yc = _as(y, td, shape, self.stream)
                     out = torch.empty(shape, dtype=torch.float64, device=self.device)
-                    if float_n(n):                   # n * d in float64, / N, + x (fa_elementwise IFOLD)
+                    kind = _int_fold_kind(d1, n)
+                    if kind == "ifold":              # n * d in float64, / N, + x (fa_elementwise IFOLD)
                         ops.elementwise("ifold", out.view(-1), xc.view(-1), yc.view(-1), float(n), float(N),
+                                        stream=self.stream)
+                    elif kind == "nfold":            # n * d wrapping in the narrow dtype (NFOLD)
+                        ops.elementwise("nfold", out.view(-1), xc.view(-1), yc.view(-1), float(int(n)), float(N),
                                         stream=self.stream)
                     else:                            # int multiply by n, then true_divide to float64
                         ops.fedavg_fold(out.view(-1), [xc.view(-1), yc.view(-1)], [0, n], [1, N], init=True,
@@ -268,6 +301,8 @@ class TensorFedOpt:
             # a half pg comes from half updates over a half model (numpy's half loops, the kernel's
             # CF16 step); otherwise a half model enters the step widened to f32, which is exact
             odt = o.dtype if p.dtype == torch.float16 or o.dtype != torch.float16 else torch.float32
+            if np_dtype(odt) in _NARROW:         # old + f64 step: numpy widens the narrow model exactly
+                odt = torch.float64
             if odt not in (torch.float16, torch.float32, torch.float64, torch.int32, torch.int64):
                 raise TypeError(f"global-model dtype {o.dtype} is not supported by the server step")
             # the update dtype handed to fa_fedopt_step only fixes the pg dtype (K = 0)

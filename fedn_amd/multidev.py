@@ -231,7 +231,8 @@ class ShardedFedAvgPipeline(_ShardedStaging):
 
     def add(self, arrays, n, N):
         if self.general is None and (not self.compatible(arrays) or
-                                     mixed.int_float_n(self.layout.dtypes, self.nfolds, n)):
+                                     mixed.int_float_n(self.layout.dtypes, self.nfolds, n) or
+                                     mixed.per_tensor_dtypes(self.layout.dtypes)):
             plan = mixed.fold_plan(self._state_meta(), self.meta_of(arrays), n, N)   # raises as numpy
             self._enter_general()
             self.general.fold(self.tensors_of(arrays), n, N, plan=plan)

@@ -18,6 +18,13 @@ _TORCH_TO_FA = {
     torch.float16: _abi.FA_F16,
     torch.int32: _abi.FA_I32,
     torch.int64: _abi.FA_I64,
+    # narrow / unsigned integers: fa_cast and the IFOLD / NFOLD folds only (the per-tensor path)
+    torch.int8: _abi.FA_I8,
+    torch.int16: _abi.FA_I16,
+    torch.uint8: _abi.FA_U8,
+    torch.uint16: _abi.FA_U16,
+    torch.uint32: _abi.FA_U32,
+    torch.uint64: _abi.FA_U64,
 }
 _FA_TO_TORCH = {v: k for k, v in _TORCH_TO_FA.items()}
 _NP_TO_TORCH = {
@@ -26,6 +33,13 @@ _NP_TO_TORCH = {
     np.dtype(np.float16): torch.float16,
     np.dtype(np.int32): torch.int32,
     np.dtype(np.int64): torch.int64,
+    np.dtype(np.int8): torch.int8,
+    np.dtype(np.int16): torch.int16,
+    np.dtype(np.uint8): torch.uint8,
+    np.dtype(np.uint16): torch.uint16,
+    np.dtype(np.uint32): torch.uint32,
+    np.dtype(np.uint64): torch.uint64,
+    np.dtype(np.bool_): torch.bool,        # staged / returned as is; no kernel takes it (numpy never folds bool)
 }
 _TORCH_TO_NP = {v: k for k, v in _NP_TO_TORCH.items()}
 
@@ -340,7 +354,7 @@ def tune(**knobs):
 
 _EW = {"axpby": _abi.FA_EW_AXPBY, "mul": _abi.FA_EW_MUL, "div": _abi.FA_EW_DIV, "sqrt": _abi.FA_EW_SQRT,
        "square": _abi.FA_EW_SQUARE, "sign": _abi.FA_EW_SIGN, "fill": _abi.FA_EW_FILL, "pow": _abi.FA_EW_POW,
-       "ipow": _abi.FA_EW_IPOW, "ifold": _abi.FA_EW_IFOLD}
+       "ipow": _abi.FA_EW_IPOW, "ifold": _abi.FA_EW_IFOLD, "nfold": _abi.FA_EW_NFOLD}
 
 
 def elementwise(op, out, x=None, y=None, a=0.0, b=0.0, stream=None):

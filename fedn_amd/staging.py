@@ -405,7 +405,8 @@ class FedAvgPipeline(_Pipeline):
         whose dtypes or shapes differ from the first's moves the round to the per-tensor path
         (numpy promotion / broadcasting, mixed.py) — checked before any state changes."""
         if self.general is None and (not self.compatible(arrays) or
-                                     mixed.int_float_n(self.layout.dtypes, self.nfolds, n)):
+                                     mixed.int_float_n(self.layout.dtypes, self.nfolds, n) or
+                                     mixed.per_tensor_dtypes(self.layout.dtypes)):
             plan = mixed.fold_plan(self._state_meta(), self.meta_of(arrays), n, N)   # raises as numpy
             self._enter_general()
             self.general.fold(self.tensors_of(arrays), n, N, plan=plan)

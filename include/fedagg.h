@@ -48,7 +48,15 @@ enum fa_dtype {
     FA_BF16 = 2,
     FA_F16 = 3,
     FA_I32 = 4,
-    FA_I64 = 5
+    FA_I64 = 5,
+    /* narrow / unsigned integers: accepted by fa_cast and the FA_EW_IFOLD / FA_EW_NFOLD folds only
+       (models with such tensors are aggregated by the per-tensor path, fedn_amd/mixed.py) */
+    FA_I8 = 6,
+    FA_I16 = 7,
+    FA_U8 = 8,
+    FA_U16 = 9,
+    FA_U32 = 10,
+    FA_U64 = 11
 };
 
 /* status codes */
@@ -163,14 +171,19 @@ int fa_running_mean(void* g, int dtype, const void* m, double a, double b, doubl
  *                                                  across hosts; parity: 1e-6 relative, f64 1e-15)
  *   FA_EW_IPOW    out = x**a, x I32 | I64, a a non-negative integer: exponentiation by squaring
  *                 with wrapping products, out_dtype = x_dtype (numpy's integer power)
- *   FA_EW_IFOLD   out = x + ((y - x)*a)/b, x and y both I32 or both I64, out F64: numpyhelper
- *                 .increment_average (numpyhelper.py:32) on integer arrays with a python-float
- *                 num_examples a and total b — the difference wraps in the integer dtype, then
- *                 float64 multiply, divide and add, each rounded once
+ *   FA_EW_IFOLD   out = x + ((y - x)*a)/b, x and y of one integer dtype (I8..I64, U8..U64), out
+ *                 F64: numpyhelper.increment_average (numpyhelper.py:32) on integer arrays with a
+ *                 python-float num_examples a and total b — the difference wraps in the integer
+ *                 dtype, then float64 multiply, divide and add, each rounded once
+ *   FA_EW_NFOLD   out = x + T((y - x)*a)/b, x and y of one integer dtype T (I8, I16, U8, U16, U32,
+ *                 U64, I32, I64), out F64: the same fold with a python-INT num_examples a (integral,
+ *                 |a| < 2^53; numpy refuses an a outside T's range, and so must the caller) —
+ *                 difference and product wrap in T, then the float64 divide by b and add
  * out_dtype must be the numpy result dtype of the op.
  */
 enum fa_ew_op { FA_EW_AXPBY = 0, FA_EW_MUL = 1, FA_EW_DIV = 2, FA_EW_SQRT = 3, FA_EW_SQUARE = 4, FA_EW_SIGN = 5,
-                FA_EW_FILL = 6, FA_EW_POW = 7, FA_EW_IPOW = 8, FA_EW_IFOLD = 9 };
+                FA_EW_FILL = 6, FA_EW_POW = 7, FA_EW_IPOW = 8, FA_EW_IFOLD = 9,
+                FA_EW_NFOLD = 10 };
 int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype, const void* y, int y_dtype,
                    double a, double b, int64_t P, void* stream);
 
@@ -200,8 +213,9 @@ int fa_promote(int a, int b);
  *                                   j(i) = sum_d i_d * in_strides[d] (element strides; 0 along
  *                                   broadcast dimensions)
  * Conversions (numpy's casting of the value): identity for every dtype; F16/BF16 -> F32/F64 and
- * F32 -> F64 (exact); I32 -> I64 (exact); I32/I64 -> F64 (round to nearest even). Narrowing
- * conversions are refused (FA_EDTYPE). 1 <= ndim <= 8; out is contiguous.
+ * F32 -> F64 (exact); I32 -> I64 (exact); I32/I64 -> F64 (round to nearest even); I8 / I16 / U8 /
+ * U16 / U32 / U64 to every integer or float dtype numpy casts them to safely (U64 -> F64 rounds to
+ * nearest even, the rest are exact). Narrowing conversions are refused (FA_EDTYPE). 1 <= ndim <= 8; out is contiguous.
  */
 int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, const int64_t* out_shape,
             const int64_t* in_strides, void* stream);

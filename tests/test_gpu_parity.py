@@ -17,6 +17,9 @@ DEV = "cuda:0"
 MIXED_FEDAVG = [n for n in case_names("fedavg") if "_mix_" in n or "_bcast_" in n or "fewer_tensors" in n]
 MIXED_FEDOPT = [n for n in case_names("fedopt") if "_mix_" in n or "_bcast_" in n or "layout_change" in n
                 or "f64_clients" in n]
+_NARROW_KEYS = ("int8", "u8_", "unsigned", "narrow", "bool")
+NARROW_FEDAVG = [n for n in case_names("fedavg") if any(k in n for k in _NARROW_KEYS)]
+NARROW_FEDOPT = [n for n in case_names("fedopt") if any(k in n for k in _NARROW_KEYS)]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -399,7 +402,7 @@ def test_control_reduce_golden(name, workers):
 
 # ------------------------------------------------------------------------- streaming ingest
 @pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k17", "fedavg_skipbad_k4", "fedavg_int64_k3",
-                                  "fedavg_odd_k1"] + MIXED_FEDAVG)
+                                  "fedavg_odd_k1"] + MIXED_FEDAVG + NARROW_FEDAVG)
 def test_staging_ingest_fedavg_golden(name):
     """Updates staged into HBM on arrival (ingest.StagingUpdateHandler) give the same result."""
     from fedn_amd.aggregators import get_aggregator
@@ -416,7 +419,7 @@ def test_staging_ingest_fedavg_golden(name):
     assert_lists_identical(model, rd["out"], name)
 
 
-@pytest.mark.parametrize("name", ["fedopt_adam_3r", "fedopt_yogi_lr1e-2_k8"] + MIXED_FEDOPT)
+@pytest.mark.parametrize("name", ["fedopt_adam_3r", "fedopt_yogi_lr1e-2_k8"] + MIXED_FEDOPT + NARROW_FEDOPT)
 def test_staging_ingest_fedopt_golden(name):
     from fedn_amd.aggregators import get_aggregator
     from fedn_amd.ingest import StagingUpdateHandler
@@ -522,7 +525,8 @@ def test_staging_batched_large_chunked_d2h():
 
 @pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k8", "fedavg_int32_k3", "fedavg_skipbad_k4",
-                                  "fedavg_mix_f32_f64_k4", "fedavg_bcast_k4", "fedavg_mix_pertensor_k5"])
+                                  "fedavg_mix_f32_f64_k4", "fedavg_bcast_k4", "fedavg_mix_pertensor_k5",
+                                  "fedavg_unsigned_k3", "fedavg_narrow_mixed_k3", "fedavg_bool_k3"])
 def test_staging_ingest_npz_bytes(name, native):
     """Updates arriving as npz bytes (numpy savez_compressed, as FEDn clients upload them):
     inflated by the native codec straight into pinned memory (native=True) or decoded by
@@ -657,7 +661,7 @@ def test_helper_increment_average_gpu():
 
 # ------------------------------------------------------------------------- one process, several devices
 @pytest.mark.parametrize("name", ["fedavg_mnist_k2", "fedavg_odd_k17", "fedavg_int64_k3", "fedavg_skipbad_k4",
-                                  "fedavg_odd_k1", "fedavg_flat_k8"] + MIXED_FEDAVG)
+                                  "fedavg_odd_k1", "fedavg_flat_k8"] + MIXED_FEDAVG + NARROW_FEDAVG)
 @pytest.mark.parametrize("ndev", [2, 3])
 def test_multidevice_fedavg_golden(name, ndev):
     """Parameter-slice sharding across devices inside one process (multidev.py); the box has

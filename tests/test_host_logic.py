@@ -416,3 +416,30 @@ def test_staging_cache_keeps_two_sizes_and_hands_out_once():
     c.give("cuda:0", 300, d)                              # third size: the oldest (200) goes
     assert c.take("cuda:0", 200) is None
     assert c.take("cuda:0", 100) is a and c.take("cuda:0", 300) is d
+
+
+def test_narrow_int_fold_kinds():
+    """numpy's rule for n * (y - x) on integer differences (numpyhelper.py:32): a python int n takes a
+    narrow / unsigned dtype (wrapping: NFOLD), a float n or a numpy int that promotes to float64
+    multiplies in float64 (IFOLD), an n outside the dtype raises OverflowError as numpy does."""
+    import numpy as np
+    import pytest
+    from fedn_amd import mixed
+    assert mixed._int_fold_kind(np.dtype(np.int8), 3) == "nfold"
+    assert mixed._int_fold_kind(np.dtype(np.uint64), 7) == "nfold"
+    assert mixed._int_fold_kind(np.dtype(np.int16), 2.5) == "ifold"
+    assert mixed._int_fold_kind(np.dtype(np.uint8), 1.0) == "ifold"
+    assert mixed._int_fold_kind(np.dtype(np.uint64), np.int64(3)) == "ifold"
+    assert mixed._int_fold_kind(np.dtype(np.int32), 3) == "int"
+    with pytest.raises(OverflowError):
+        mixed._int_fold_kind(np.dtype(np.int8), 300)
+    with pytest.raises(TypeError):
+        mixed._int_fold_kind(np.dtype(np.int8), np.int64(3))    # int64 product: not instantiated
+    with pytest.raises(TypeError):
+        mixed._int_fold_kind(np.dtype(np.uint64), 1 << 60)
+    with pytest.raises(TypeError):                              # numpy's boolean-subtract refusal
+        mixed.fold_plan([((3,), np.dtype(bool))], [((3,), np.dtype(bool))], 2, 3)
+    assert mixed.per_tensor_dtypes([np.float32, np.uint16]) and mixed.per_tensor_dtypes([np.bool_])
+    assert not mixed.per_tensor_dtypes([np.float32, np.int64, np.float16])
+    plan = mixed.fold_plan([((5,), np.dtype(np.int8))], [((1,), np.dtype(np.int16))], 9, 13)
+    assert plan == [(np.dtype(np.int16), np.dtype(np.float64), (5,))]

@@ -678,6 +678,28 @@ def numex_cases(ref):
     ]
 
 
+def narrow_cases(ref):
+    """Models with 8 / 16-bit and unsigned integer tensors: the first fold's difference and (python
+    int n) product wrap in the narrow dtype, a float n multiplies in float64, an n outside the dtype's
+    range makes numpy raise (FEDn skips that update), bool tensors never fold (boolean subtract)."""
+    rng = np.random.default_rng(14)
+    I8, I16, U8, U16, U32, U64 = np.int8, np.int16, np.uint8, np.uint16, np.uint32, np.uint64
+    return [
+        fedavg_numex_case(ref, "fedavg_int8_k4", rng, [((5,), I8), ((2, 3), F32), ((7,), I8)], [7, 12, 3, 100]),
+        fedavg_numex_case(ref, "fedavg_u8_i16_n_overflow_k4", rng, [((9,), U8), ((4,), I16)], [5, 300, 7, 2]),
+        fedavg_numex_case(ref, "fedavg_unsigned_k3", rng, [((6,), U16), ((5,), U32), ((4,), U64)], [40000, 7, 3]),
+        fedavg_numex_case(ref, "fedavg_narrow_float_n_k3", rng, [((6,), I8), ((5,), U16), ((3,), U64)], [3, 2.5, 4]),
+        fedavg_clients_case(ref, "fedavg_narrow_mixed_k3", rng,
+                            [_spec([I8, U8, I16], [(5,), (4,), (3,)]), _spec([I16, I8, U16], [(1,), (4,), (3,)]),
+                             _spec([F16, U8, I16], [(5,), (4,), (1,)])], [9, 4, 6]),
+        fedavg_numex_case(ref, "fedavg_bool_k3", rng, [((4,), np.bool_), ((3,), F32)], [2, 3, 4]),
+        fedopt_clients_case(ref, "fedopt_int8_2r", rng, _spec(I8, [(7,), (3, 5)]),
+                            [[_spec(I8, [(7,), (3, 5)])] * 3, [_spec(I8, [(7,), (3, 5)])] * 2]),
+        fedopt_clients_case(ref, "fedopt_u8_old_i16_upd_2r", rng, _spec(U8, [(6,), (2, 2)]),
+                            [[_spec(I16, [(6,), (2, 2)])] * 2, [_spec(U32, [(6,), (2, 2)])] * 2], {"serveropt": "yogi"}),
+    ]
+
+
 def f16_fedopt_cases(ref):
     """FedOpt sessions on a float16 global model (VERDICT r2 follow-up): numpy computes the pseudo-
     gradient in half while it is half (round 1), then float64; m stays half until it meets a float64
@@ -745,6 +767,8 @@ def main():
         return _write(edge_cases(ref), merge=True)
     if only == "f16opt":
         return _write(f16_fedopt_cases(ref), merge=True)
+    if only == "narrow":
+        return _write(narrow_cases(ref), merge=True)
     if only == "numex":
         return _write(numex_cases(ref), merge=True)
     if only == "reduce":
