@@ -125,3 +125,19 @@ def test_nfold_rejects_huge_n():
     x = torch.zeros(8, dtype=torch.uint64, device=DEV)
     with pytest.raises(_abi.FedAggError):
         ops.elementwise("nfold", torch.empty(8, dtype=torch.float64, device=DEV), x, x, float(1 << 60), 3.0)
+
+
+@pytest.mark.parametrize("dtypes,n,N", [((np.int8, np.uint16), 37, 1234), ((np.uint32, np.int16), 2.5, 9.0),
+                                       ((np.uint64, np.int8), 5, 11)])
+def test_helper_increment_average_narrow(dtypes, n, N):
+    """fednamdhelper.increment_average (the stock fedavg.py loop's fold) on narrow / unsigned tensors,
+    against the oracle's numpyhelper.increment_average."""
+    from golden_io import assert_lists_identical
+    from oracle import numpy_ref as ref
+    from fedn_amd.helper import Helper
+    rng = np.random.default_rng(77)
+    m1 = [_rand_ints(rng, dt, 1000 + 7 * i).reshape(-1) for i, dt in enumerate(dtypes)]
+    m2 = [_rand_ints(rng, dt, 1000 + 7 * i).reshape(-1) for i, dt in enumerate(dtypes)]
+    with np.errstate(over="ignore"):
+        want = ref.increment_average(m1, m2, n, N)
+    assert_lists_identical(Helper().increment_average(m1, m2, n, N), want, str(dtypes))
