@@ -697,6 +697,8 @@ def narrow_cases(ref):
                             [[_spec(I8, [(7,), (3, 5)])] * 3, [_spec(I8, [(7,), (3, 5)])] * 2]),
         fedopt_clients_case(ref, "fedopt_u8_old_i16_upd_2r", rng, _spec(U8, [(6,), (2, 2)]),
                             [[_spec(I16, [(6,), (2, 2)])] * 2, [_spec(U32, [(6,), (2, 2)])] * 2], {"serveropt": "yogi"}),
+        reduce_dtypes_case(ref, "reduce_int8_3", rng, ODD_SHAPES, [I8, I8, I8]),
+        reduce_dtypes_case(ref, "reduce_mix_u16_i8_f32", rng, ODD_SHAPES, [U16, I8, F32]),
     ]
 
 
