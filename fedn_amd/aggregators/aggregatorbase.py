@@ -47,7 +47,11 @@ def _raiser(e):
 
 
 def model_nbytes(model):
-    """Host bytes of a decoded update (list of arrays); 0 if unknown."""
+    """Host bytes of a decoded update (list of arrays; a staged update counts its packed layout);
+    0 if unknown."""
+    lay = getattr(model, "layout", None)
+    if lay is not None and hasattr(lay, "nbytes"):
+        return int(lay.nbytes)
     try:
         return int(sum(np.asarray(a).nbytes for a in model))
     except Exception:  # noqa: BLE001
@@ -115,6 +119,7 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
     # updatehandler.py:119-144) show it from the npz directory before its decode ends
     known = threading.Event()
     peek = [size[0] is None and hasattr(update_handler, "load_model_update_byte")]
+    peeking = [False]                     # a peek was issued: ``known`` will be set
 
     def peek_then_load(mu):
         try:
@@ -141,6 +146,7 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
                 continue
             if peek[0]:
                 peek[0] = False
+                peeking[0] = True
                 fut = pool.submit(peek_then_load, mu)
             else:
                 fut = pool.submit(update_handler.load_model_update, mu, helper)
@@ -163,7 +169,7 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
         fill()
         while window:
             mu, fut, err = window.popleft()
-            if fut is not None and size[0] is None:
+            if fut is not None and size[0] is None and peeking[0]:
                 while not fut.done() and not known.wait(0.002):
                     pass                  # the first update's npz directory admits the others early
             fill(held=1)
