@@ -19,6 +19,7 @@ from .layout import Layout
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfednpz.so")
 MAX_DIMS = 16
+FNPZ_ABI_VERSION = 2    # include/fednpz.h
 THREADS = int(os.environ.get("FEDN_AMD_CODEC_THREADS", str(min(16, os.cpu_count() or 1))))
 
 
@@ -47,30 +48,35 @@ def load_lib():
             if not os.path.exists(LIB_PATH):
                 raise ImportError(f"{LIB_PATH} not found: run python -m fedn_amd.build")
             lib = ctypes.CDLL(LIB_PATH)
-            lib.fnpz_abi_version.restype = ctypes.c_int
-            lib.fnpz_last_error.restype = ctypes.c_char_p
-            lib.fnpz_open.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(Entry), ctypes.c_int,
-                                      ctypes.POINTER(ctypes.c_int)]
-            lib.fnpz_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(Entry), ctypes.c_int,
-                                      ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]
-            lib.fnpz_write_bound.restype = ctypes.c_int64
-            lib.fnpz_write_bound.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
-                                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]
-            lib.fnpz_write.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_void_p),
-                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_void_p),
-                                       ctypes.POINTER(ctypes.c_int64), ctypes.c_int, ctypes.c_int, ctypes.c_int64,
-                                       ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
-            lib.fnpz_stream_open.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
-            lib.fnpz_stream_close.argtypes = [ctypes.c_void_p]
-            lib.fnpz_stream_close.restype = None
-            lib.fnpz_stream_feed.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]
-            lib.fnpz_stream_next.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
-                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(Entry),
-                                             ctypes.POINTER(ctypes.c_int64)]
-            lib.fnpz_gather.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
-                                        ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
-            if lib.fnpz_abi_version() != 1:
-                raise ImportError("libfednpz.so ABI mismatch; rebuild")
+            try:
+                # the version first: a library from an older build may lack later symbols
+                lib.fnpz_abi_version.restype = ctypes.c_int
+                if lib.fnpz_abi_version() != FNPZ_ABI_VERSION:
+                    raise ImportError(f"{LIB_PATH}: ABI version {lib.fnpz_abi_version()}, expected "
+                                      f"{FNPZ_ABI_VERSION}; rebuild it (python -m fedn_amd.build)")
+                lib.fnpz_last_error.restype = ctypes.c_char_p
+                lib.fnpz_open.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(Entry), ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_int)]
+                lib.fnpz_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(Entry), ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]
+                lib.fnpz_write_bound.restype = ctypes.c_int64
+                lib.fnpz_write_bound.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+                                                 ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]
+                lib.fnpz_write.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_void_p),
+                                           ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_void_p),
+                                           ctypes.POINTER(ctypes.c_int64), ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                           ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+                lib.fnpz_stream_open.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+                lib.fnpz_stream_close.argtypes = [ctypes.c_void_p]
+                lib.fnpz_stream_close.restype = None
+                lib.fnpz_stream_feed.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]
+                lib.fnpz_stream_next.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                                 ctypes.POINTER(ctypes.c_int), ctypes.POINTER(Entry),
+                                                 ctypes.POINTER(ctypes.c_int64)]
+                lib.fnpz_gather.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+            except AttributeError as e:      # a symbol include/fednpz.h declares is missing
+                raise ImportError(f"{LIB_PATH}: {e}; rebuild it (python -m fedn_amd.build)") from e
             _lib = lib
     return _lib
 

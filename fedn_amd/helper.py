@@ -68,7 +68,7 @@ class Helper:
         dev = default_device()
         key = (str(dev), Layout.of(m1).signature())
         slots, streams = self._cache.pop(key, (None, None))
-        pipe = FedAvgPipeline(dev, m1, nslots=2, slots=slots, streams=streams)
+        pipe = FedAvgPipeline(dev, m1, nslots=2, slots=slots, streams=streams, batch=False)
         pipe.add(m2, n, N)
         out = pipe.result()
         self._cache[key] = (pipe.slots, (pipe.copy, pipe.d2h))

@@ -147,7 +147,7 @@ class _ArenaRef:
 
 
 class _Pipeline:
-    def __init__(self, device, layout, nslots, slots=None, streams=None, cache=None):
+    def __init__(self, device, layout, nslots, slots=None, streams=None, cache=None, batch=True):
         self.device = torch.device(device)
         self.layout = layout
         self.compute = torch.cuda.current_stream(self.device)
@@ -172,9 +172,10 @@ class _Pipeline:
         self.time_d2h = 0.0
         self._hold = []
         self.pending = []                        # device-resident updates not folded yet: (staged, n, N)
-        # small host updates are batched through arenas (not on the helper path, whose callers fold
-        # one pair per pipeline with cached slots)
-        self.batch_host = (slots is None or kept is not None) and layout.nbytes <= SMALL_UPDATE_BYTES
+        # small host updates are batched through arenas; ``batch=False`` on the helper path
+        # (helper.Helper.increment_average folds ONE pair per pipeline: an arena there would be
+        # allocated for a single update and never reused)
+        self.batch_host = batch and layout.nbytes <= SMALL_UPDATE_BYTES
         self._arenas, self._arena, self._arena_i = (kept["arenas"] if kept else []), None, 0
         self.streamer = kept["streamer"] if kept else HostStreamer()
 
@@ -365,10 +366,10 @@ class _Pipeline:
 class FedAvgPipeline(_Pipeline):
     """Streaming FedAvg on one device: fedavg.py:109-133 with the fold on the GPU."""
 
-    def __init__(self, device, first_arrays, nslots=3, slots=None, streams=None, cache=None):
+    def __init__(self, device, first_arrays, nslots=3, slots=None, streams=None, cache=None, batch=True):
         staged = isinstance(first_arrays, StagedModel)
         super().__init__(device, first_arrays.layout if staged else Layout.of(first_arrays), nslots, slots, streams,
-                         cache)
+                         cache, batch)
         self.first_arrays = first_arrays         # a StagedModel materialises host arrays only if needed
         self.first = self.acquire(first_arrays) if staged else self.stage(first_arrays)
         if not staged:

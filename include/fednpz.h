@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define FNPZ_ABI_VERSION 1
+#define FNPZ_ABI_VERSION 2
 #define FNPZ_MAX_DIMS 16
 
 enum fnpz_status { FNPZ_OK = 0, FNPZ_EFORMAT = 1, FNPZ_ECORRUPT = 2, FNPZ_EINVAL = 3, FNPZ_ENOSPC = 4 };

@@ -225,3 +225,26 @@ def test_thread_pools_survive_fork():
     ok, got = q.get(timeout=60)
     p.join(timeout=60)
     assert p.exitcode == 0 and ok and got == [0, 1, 2, 3, 4]
+
+
+@pytest.mark.parametrize("version,symbols", [(1, ""), (2, "")])
+def test_stale_library_is_an_import_error(tmp_path, monkeypatch, version, symbols):
+    """A libfednpz.so from an older build (ABI 1, or missing fnpz_gather) must read as 'codec not
+    built' (ImportError), so the pack falls back to the Python pool instead of raising for every
+    update (advisor finding, round 2)."""
+    import subprocess
+
+    from fedn_amd import layout
+    src = tmp_path / "stale.c"
+    src.write_text(f"int fnpz_abi_version(void) {{ return {version}; }}\n"
+                   "const char* fnpz_last_error(void) { return \"\"; }\n")
+    so = tmp_path / "libfednpz_stale.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    monkeypatch.setattr(codec, "LIB_PATH", str(so))
+    monkeypatch.setattr(codec, "_lib", None)
+    with pytest.raises(ImportError):
+        codec.load_lib()
+    dst, srcarr = np.zeros(1 << 20, np.float32), np.arange(1 << 20, dtype=np.float32)
+    assert layout._native_gather([(dst, srcarr)]) is False
+    layout.parallel_copy(dst, srcarr)
+    assert np.array_equal(dst, srcarr)

@@ -202,14 +202,24 @@ def test_queued_updates_byte_cap():
     assert consumed == 12
 
 
-def test_queued_updates_staged_models_read_ahead():
+def test_queued_updates_staged_models_read_ahead(monkeypatch):
     """Updates that are staged objects (a ``layout`` with ``nbytes``, like ingest.StagedModel) size
-    the read-ahead by their packed layout, so it opens past one update; no 2 ms polling happens when
-    no npz size peek is pending (a handler without load_model_update_byte)."""
-    import time
+    the read-ahead by their packed layout, so it opens past one update; no polling wait happens when
+    no npz size peek is pending (a handler without load_model_update_byte): the drain's Event is
+    never waited on."""
+    import threading
     import types
 
+    from fedn_amd.aggregators import aggregatorbase
     from fedn_amd.aggregators.aggregatorbase import model_nbytes, queued_updates
+    waits = []
+
+    class CountingEvent(threading.Event):
+        def wait(self, timeout=None):
+            waits.append(timeout)
+            return super().wait(timeout)
+
+    monkeypatch.setattr(aggregatorbase, "threading", types.SimpleNamespace(Event=CountingEvent))
     staged = lambda k: types.SimpleNamespace(layout=types.SimpleNamespace(nbytes=1000), k=k)  # noqa: E731
     assert model_nbytes(staged(0)) == 1000
     assert model_nbytes([np.zeros(10, np.float32)]) == 40
@@ -219,13 +229,12 @@ def test_queued_updates_staged_models_read_ahead():
     inner = uh.load_model_update
     uh.load_model_update = lambda mu, helper: (staged(mu.model_update_id), inner(mu, helper)[1])
     ahead_seen = []
-    t0 = time.perf_counter()
     for mu, load in queued_updates(uh, None, ahead=8, ahead_bytes=1 << 30):
         load()
         ahead_seen.append(40 - 1 - len(ahead_seen) - uh.model_updates.qsize())
     assert len(ahead_seen) == 40
     assert max(ahead_seen) > 1                      # read-ahead opened past one update
-    assert time.perf_counter() - t0 < 2.0
+    assert waits == []                              # no size peek pending: never polled
 
 
 def test_reduce_byte_cap_keeps_order():

@@ -38,7 +38,11 @@ class _MU:
 
 class DeviceResidentHandler:
     """The UpdateHandler surface the plug-ins use (updatehandler.py:31-163), serving updates
-    that are already StagedModels in HBM, as ingest.StagingUpdateHandler leaves them."""
+    that are already StagedModels in HBM, as ingest.StagingUpdateHandler leaves them. Like that
+    handler it declares ``stages_on_arrival``: the plug-in drains it one update at a time, with no
+    read-ahead thread (aggregatorbase.queued_updates), the path the product handler takes."""
+
+    stages_on_arrival = True
 
     def __init__(self):
         self.model_updates = queue.Queue()
@@ -88,11 +92,11 @@ def run_fedavg(K, P, reps):
     for mode, batch in (("batched", 64), ("per-update", 1), ("batched", 64)):
         staging.BATCH = batch
         ts = []
+        uh = DeviceResidentHandler()
+        agg = get_aggregator("fedavg", uh)          # one aggregator across reps: a session's rounds
         for _ in range(reps):
-            uh = DeviceResidentHandler()
             for i, (s, n) in enumerate(zip(ups, ns)):
                 uh.submit(s, n, i)
-            agg = get_aggregator("fedavg", uh)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             model, data = agg.combine_models(helper=None)

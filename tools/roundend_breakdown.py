@@ -43,11 +43,11 @@ def main():
     for name in ("add", "result", "timings", "release", "_flush", "_to_host"):
         if hasattr(staging.FedAvgPipeline, name):
             timed(staging.FedAvgPipeline, name, name)
+    uh = DeviceResidentHandler()
+    agg = get_aggregator("fedavg", uh)              # one aggregator: a session's rounds
     for rep in range(6):
-        uh = DeviceResidentHandler()
         for i, (s, n) in enumerate(zip(ups, ns)):
             uh.submit(s, n, i)
-        agg = get_aggregator("fedavg", uh)
         torch.cuda.synchronize()
         T.clear()
         t0 = time.perf_counter()
