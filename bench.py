@@ -87,6 +87,11 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-achievable", dest="achievable", action="store_false",
                     help="N = 1: skip the achievable-peak copy / read reference")
+    ap.add_argument("--transport", choices=["auto", "collective", "p2p"], default="auto",
+                    help="N > 1: how each folded round reaches every GPU (auto = the faster in the untimed warm-up)")
+    ap.add_argument("--host-clients", type=int, default=16,
+                    help="host_resident side field: host numpy updates through the plug-in (0 = skip)")
+    ap.add_argument("--launch-check", action="store_true", help="rank set-up only (gloo, no GPU): the launcher's test")
     return ap.parse_args()
 
 
@@ -394,14 +399,142 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000, pattern_probe=
     return res
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n):
+    """``bench.py --gpus N`` outside torch.distributed.run: start one child process per rank with the
+    contract's environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), wait
+    for all of them, and return the first failure's exit status (the other ranks are then stopped by
+    their exact PIDs). This process only starts children: it never touches the GPU and never execs."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc, live = 0, list(procs)
+    while live:
+        for pr in list(live):
+            r = pr.poll()
+            if r is None:
+                continue
+            live.remove(pr)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                for other in live:
+                    other.kill()
+        time.sleep(0.1)
+    return rc
+
+
+def launch_check(world, rank):
+    """--launch-check: the rank set-up alone (gloo rendezvous, one all-reduce, no GPU) — what the CPU
+    test of the self-launch runs."""
+    dist.init_process_group("gloo")
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    dist.all_reduce(t)
+    pids = [None] * world
+    dist.all_gather_object(pids, (os.getpid(), os.getppid(), int(os.environ["LOCAL_RANK"])))
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "world": dist.get_world_size(), "rank_sum": int(t[0]),
+                          "ranks": pids}), flush=True)
+    dist.destroy_process_group()
+
+
+def global_chunks(geom, K, P_total, dtype, device, seed, sample):
+    """THIS rank's chunks (``geom.local``) of the ONE synthetic model every rank and the N = 1 line
+    derive from the same seed — base ~ N(0,1), client k = base + 0.01 N(0,1), the exact sequence of
+    make_updates(K, P_total, ...) — plus, when ``sample`` > 0, the first ``sample`` params of every
+    client on the host (fp32; for bf16 the exact upcasts of the rounded values) for the checker."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    base = torch.randn(P_total, generator=g, device=device)
+    loc, host = [], []
+    for _ in range(K):
+        u = torch.randn(P_total, generator=g, device=device).mul_(0.01).add_(base)
+        if dtype == "bf16":
+            u = u.to(torch.bfloat16)
+        loc.append(geom.local(u))
+        if sample > 0:
+            host.append(u[:sample].float().cpu().numpy())
+        del u
+    del base
+    torch.cuda.synchronize(device)
+    return loc, host
+
+
+def sample_check(got, host_sample, ns):
+    """Bit-for-bit check of the first params of an aggregate against the oracle (numpy, one core) on
+    the same clients' values; returns (equal, oracle seconds)."""
+    from oracle import numpy_ref as ref  # test infrastructure: the checker only
+    S = host_sample[0].size
+    t0 = time.perf_counter()
+    want = ref.fedavg_flat(host_sample, ns)
+    dt = time.perf_counter() - t0
+    g = got[:S].cpu().numpy() if isinstance(got, torch.Tensor) else np.asarray(got[:S])
+    return bool(np.array_equal(g.view(np.uint32), want.view(np.uint32))), dt
+
+
+def host_resident_side(a, devs, ns_all, clients=16, sample=1_000_000, rounds=3):
+    """The north star's end-to-end rate: the FedAvg PLUG-IN (fedn_amd.aggregators.fedavg.Aggregator,
+    the combiner's call shape) over ``clients`` host-resident numpy updates of the model, with its
+    devices = the N GPUs of the node (FEDN_AMD_DEVICES' multi-device pipeline: each update packed
+    once into pinned memory, each GPU H2D's its parameter slice over its own PCIe link, folds it,
+    D2H's its slice of the result into the host model). A session's rounds after the first; the
+    first ``sample`` params checked bit-for-bit against the oracle."""
+    from fedn_amd.aggregators import get_aggregator  # noqa: F401
+    from fedn_amd.aggregators.fedavg import Aggregator
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    P = a.params
+    ns = ns_all[:clients]
+    g = torch.Generator(device=devs[0]).manual_seed(a.seed + 11)
+    base = torch.randn(P, generator=g, device=devs[0])
+    host = []
+    for _ in range(clients):
+        host.append(torch.randn(P, generator=g, device=devs[0]).mul_(0.01).add_(base).cpu().numpy())
+    del base
+    uh = MemoryUpdateHandler()
+    agg = Aggregator(uh, devices=list(devs))
+    times = []
+    for r in range(rounds + 1):
+        for k in range(clients):
+            uh.submit([host[k]], ns[k])
+        t0 = time.perf_counter()
+        model, data = agg.combine_models(helper=None)
+        if r:
+            times.append(time.perf_counter() - t0)
+    t = sorted(times)[len(times) // 2]
+    S = min(sample, P)
+    exact, _ = sample_check(model[0], [h[:S] for h in host], ns)
+    nbytes = clients * P * 4
+    del host, model, agg, uh
+    torch.cuda.empty_cache()
+    return {"s": t, "value": clients * P / t, "unit": "params/s", "clients": clients, "params": P,
+            "devices": len(devs), "GBps_in": nbytes / t / 1e9, "GBps_per_link": nbytes / t / 1e9 / len(devs),
+            "rounds_s": times, "bit_exact_on_sample": exact, "sample": f"first {S} params vs oracle/numpy_ref.fedavg_flat",
+            "nr_aggregated_models": data.get("nr_aggregated_models"),
+            "note": "FedAvg plug-in over host numpy updates (pack -> pinned -> per-device H2D slice -> fold -> D2H into "
+                    "the host model), median of a session's rounds 2..; PCIe-bound; not in value"}
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        # no launcher: this process starts the ranks itself (never touching the GPU first)
+        raise SystemExit(self_launch(a.gpus))
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    if a.launch_check:
+        return launch_check(world, rank)
     # FEDN_AMD_BENCH_ONE_GPU=1: rehearsal of the N>1 code path on a one-GPU box (every rank on
     # cuda:0, gloo instead of RCCL); never used for reported numbers
     rehearsal = os.environ.get("FEDN_AMD_BENCH_ONE_GPU") == "1"
@@ -418,7 +551,7 @@ def main():
             dist.init_process_group("nccl", device_id=device)
 
     from fedn_amd import _abi, ops
-    from fedn_amd.sharded import CyclicShardedFedAvg, ShardedFedAvg
+    from fedn_amd.sharded import CyclicShardedFedAvg, P2PAllGather
     _abi.load()
 
     K = a.clients
@@ -428,6 +561,8 @@ def main():
     Ns = [int(v) for v in np.cumsum(ns)]
     stream = torch.cuda.current_stream(device)
     extra = {}
+    S = min(a.cpu_sample, P_total) if a.cpu_sample > 0 else 0
+    base = None
 
     if world == 1 and not rccl1:
         P = P_total
@@ -448,40 +583,69 @@ def main():
                   "clients": K, "params_per_gpu": P, "global_params": P_total,
                   "parallelism": "param-slice shards x1, no data-path collective"}
         scaling = "weak"
+        if rank == 0 and S:
+            base = cpu_baseline(ups, ns, agg, S)
     else:
-        # rounds of the overlapped fold + all-gather: fixed (--ag-rounds R) or chosen in the untimed warm-up
-        # among AG_ROUNDS (--ag-rounds 0, the default): the all-gather over xGMI, not the fold, sets the
-        # step at every N > 1, and its efficiency depends on the message size (round i gathers W x C
-        # params) in a way only the node itself can tell
+        # the fold + gather step: rounds R (--ag-rounds, or the fastest of AG_ROUNDS) and transport
+        # (RCCL all-gather, or direct peer copies: P2PAllGather) chosen in the untimed warm-up by
+        # max-over-ranks step time — the all-gather over xGMI, not the fold, sets the step at every
+        # N > 1, and only the node itself can tell which transport and message size move it fastest
         cands = [a.ag_rounds] if a.ag_rounds > 0 else list(AG_ROUNDS)
         geoms = {R: CyclicShardedFedAvg(P_total, chunk=-(-P_total // (world * R)), collective_at_world1=rccl1)
                  for R in cands}
         Lmax = max(c.local_len for c in geoms.values())
-        ups_all = make_updates(K, Lmax, a.dtype, device, a.seed + 1000 * rank)   # this rank's chunks, every client
+        full_all = torch.empty(max(c.full_len for c in geoms.values()), dtype=torch.float32, device=device)
+        transports = {"collective": None}
+        if a.transport in ("auto", "p2p") and (world > 1 or rccl1):
+            try:
+                transports["p2p"] = P2PAllGather(full_all)
+            except Exception as e:  # noqa: BLE001 — reported; the collective stays
+                extra["p2p_error"] = f"{type(e).__name__}: {e}"
+        if a.transport == "p2p" and "p2p" in transports:
+            del transports["collective"]
+        elif a.transport == "collective":
+            transports.pop("p2p", None)
         agg_all = torch.empty(Lmax, dtype=torch.float32, device=device)
-        full_all = None if rehearsal else torch.empty(max(c.full_len for c in geoms.values()), dtype=torch.float32,
-                                                      device=device)
 
-        def make_step(c):
-            loc = [u[:c.local_len] for u in ups_all]
-            ag, out = agg_all[:c.local_len], None if rehearsal else full_all[:c.full_len]
-            return lambda: c.fold_allgather(ag, loc, ns, Ns, init=True, out=out)
+        def make_step(c, tp, loc, res=None):
+            ag = agg_all[:c.local_len]
+            out = None if (rehearsal and tp is None) else full_all[:c.full_len]
+
+            def st():
+                r = c.fold_allgather(ag, loc, ns, Ns, init=True, out=out, p2p=tp)
+                if res is not None:
+                    res[0] = r
+            return st
 
         tuned = {}
-        if len(cands) > 1:
-            for R, c in geoms.items():
-                st = make_step(c)
-                for _ in range(2):
-                    st()
-                el, _ = timed_steps(st, 5, stream, world, device, rehearsal)
-                tuned[R] = el / 5 * 1e3
-        R = min(tuned, key=tuned.get) if tuned else cands[0]
+        if len(cands) * len(transports) > 1:
+            scratch = make_updates(K, Lmax, a.dtype, device, a.seed + 1000 * rank + 1)   # timing only
+            for name, tp in transports.items():
+                for R, c in geoms.items():
+                    st = make_step(c, tp, [u[:c.local_len] for u in scratch])
+                    for _ in range(2):
+                        st()
+                    el, _ = timed_steps(st, 5, stream, world, device, rehearsal)
+                    tuned[f"{name}/R{R}"] = el / 5 * 1e3
+            del scratch
+            torch.cuda.empty_cache()
+            best = min(tuned, key=tuned.get)
+            tname, R = best.split("/R")[0], int(best.split("/R")[1])
+        else:
+            tname, R = next(iter(transports)), cands[0]
+        for name in list(transports):
+            if name != tname and transports[name] is not None:
+                transports.pop(name).close()
+        tp = transports[tname]
         cyc = geoms[R]
         L = cyc.local_len
         P = L
-        ups_local = [u[:L] for u in ups_all]
+        # the timed data: this rank's chunks of ONE seeded global model (the N = 1 line's), so that
+        # rank 0 checks the gathered model bit-for-bit against the oracle
+        ups_local, host_sample = global_chunks(cyc, K, P_total, a.dtype, device, a.seed, S if rank == 0 else 0)
         agg = agg_all[:L]
-        step = make_step(cyc)
+        res = [None]
+        step = make_step(cyc, tp, ups_local, res)
 
         def fold_only():
             for i in range(cyc.rounds):
@@ -491,6 +655,12 @@ def main():
         for _ in range(a.warmup):
             step()
         elapsed, _ = timed_steps(step, a.steps, stream, world, device, rehearsal)
+        full = res[0]
+        # every rank ends the step holding the same model: int64 sum of its bits, compared over ranks
+        bits = full.contiguous().view(torch.int32).to(device).sum(dtype=torch.int64).reshape(1)
+        lohi = torch.cat([bits, -bits]).cpu() if rehearsal else torch.cat([bits, -bits])
+        dist.all_reduce(lohi, op=dist.ReduceOp.MAX)
+        consistent = bool(int(lohi[0]) == -int(lohi[1]))
         for _ in range(2):
             fold_only()
         _, kern_ms = timed_steps(fold_only, a.steps, stream, world, device, rehearsal)
@@ -498,17 +668,32 @@ def main():
         workload = f"fedavg_k{K}_p{L}_r{cyc.rounds}_{a.dtype}_rank_of_{world}"
         kernel = (f"{fold_kernel_label(cyc.C, in_bytes, K)} over this rank's {cyc.rounds} chunks of {cyc.C} params "
                   "(fold-only timing; max over ranks)")
+        backend = dist.get_backend() if dist.is_initialized() else None
+        transport = (f"direct peer copies (P2PAllGather: IPC-mapped peer buffers, one copy stream per peer, "
+                     f"{backend} fences)" if tname == "p2p" else f"{backend} all_gather_into_tensor on a "
+                     "communication stream")
         config = {"workload": f"FedAvg {K} clients x {P_total} params {a.dtype}, param-sharded block-cyclically over "
-                              f"{world} GPUs; RCCL all-gather of each folded round overlapped with the next round's "
-                              "fold, inside the timed step (BASELINE configs[2])",
+                              f"{world} GPUs; each folded round gathered to every GPU while the next round folds, "
+                              "inside the timed step (BASELINE configs[2])",
                   "clients": K, "params_per_gpu": L, "global_params": P_total, "rounds": cyc.rounds,
-                  "chunk": cyc.C, "parallelism": f"param-slice x{world} + RCCL all-gather",
-                  "rounds_tuned_ms": {str(k): v for k, v in tuned.items()} or None}
+                  "chunk": cyc.C, "parallelism": f"param-slice x{world} + all-gather ({tname})",
+                  "transport": transport, "tuned_ms": tuned or None}
         scaling = "strong"
         extra["fold_allgather_ms"] = elapsed / a.steps * 1e3
+        extra["allgather_consistent_over_ranks"] = consistent
+        if rank == 0 and S:
+            exact, dt = sample_check(full, host_sample, ns)
+            base = {"value": K * S / dt, "unit": "params/s", "cores": 1, "kind": "port",
+                    "sample": f"{K} clients x {S} fp32 params (the first {S} of the global model's clients); numpy "
+                              f"{np.__version__} oracle/numpy_ref.fedavg_flat, single-threaded, {os.cpu_count()} host "
+                              "cores present", "seconds": dt,
+                    "gpu_bit_exact_on_sample": exact,
+                    "gpu_sample_source": "rank 0's copy of the all-gathered model"}
         if not a.no_side:
             extra.update(multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, ups_local, stream,
-                                        rccl1))
+                                        rccl1, cyc, host_sample))
+        if tp is not None:
+            tp.close()
         if rccl1:
             extra["rccl_world1"] = ("rehearsal: the N>1 path at world size 1 over RCCL (all-gathers issued as "
                                     "collectives); not a reported number")
@@ -516,9 +701,6 @@ def main():
 
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
     traffic, tsrc = pmc_traffic(workload)
-    base = None
-    if rank == 0 and world == 1 and a.cpu_sample > 0:
-        base = cpu_baseline(ups, ns, agg, a.cpu_sample)
     if world == 1 and not rccl1:
         # the model to the host, FEDn's consumer (roundhandler.py:465-468); value excludes it
         host = torch.empty(P, dtype=torch.float32, pin_memory=True)
@@ -541,6 +723,8 @@ def main():
         torch.cuda.empty_cache()
         if a.achievable and not a.no_side:
             extra["achievable"] = side(lambda: achievable_side(device, achieved_of(alg_bytes, kern_ms)))
+        if rank == 0 and a.host_clients > 0 and not a.no_side:
+            extra["host_resident"] = side(lambda: host_resident_side(a, [device], ns, clients=a.host_clients))
         if rank == 0 and a.waves_params > 0 and not a.no_side:
             extra["fedopt_waves"] = side(lambda: fedopt_waves_side(a, [device]))
         if rank == 0 and a.fedopt_params > 0:
@@ -565,7 +749,8 @@ def main():
         dist.destroy_process_group()
 
 
-def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, ups_local, stream, rccl1=False):
+def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, ups_local, stream, rccl1=False,
+                   cyc=None, host_sample=None):
     """The N > 1 measurements beside the line (none of them is in value)."""
     from fedn_amd import ops
     from fedn_amd.sharded import ShardedFedAvg
@@ -587,13 +772,25 @@ def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, u
                 "note": f"all-gather of the {P_total}-param fp32 model (one slice per rank), not overlapped; not in value"}
 
     def gather_to_host():
-        host = torch.empty(agg.numel(), dtype=torch.float32, pin_memory=True)
-        host.copy_(agg, non_blocking=True)
-        el, _ = timed_steps(lambda: host.copy_(agg, non_blocking=True), 5, stream, world, device, on_cpu)
+        """FEDn's consumer (roundhandler.py:465-468) without a device collective: every rank D2H's its
+        folded chunks over its own PCIe link straight into the node's ONE shared, page-locked host
+        model (CyclicShardedFedAvg.gather_to_host -> sharded.HostGather); rank 0 checks it."""
+        fold = lambda: [ops.fedavg_fold(agg[i * cyc.C:(i + 1) * cyc.C],  # noqa: E731
+                                        [u[i * cyc.C:(i + 1) * cyc.C] for u in ups_local], ns, Ns, init=True,
+                                        stream=stream) for i in range(cyc.rounds)]
+        fold()
+        got = cyc.gather_to_host(agg)                      # maps + pins the shared host model once
+        el, _ = timed_steps(lambda: cyc.gather_to_host(agg), 5, stream, world, device, on_cpu)
         gh = el / 5
-        return {"ms": gh * 1e3, "bytes_per_rank": agg.numel() * 4, "GBps_aggregate": world * agg.numel() * 4 / gh / 1e9,
-                "note": "each rank D2H's its slice of the aggregate into pinned host memory, all ranks "
-                        "concurrently over their own links; max over ranks; not in value"}
+        res = {"ms": gh * 1e3, "bytes_per_rank": cyc.local_len * 4, "GBps_aggregate": P_total * 4 / gh / 1e9,
+               "path": "sharded.CyclicShardedFedAvg.gather_to_host -> HostGather (shared /dev/shm model, "
+                       "fa_host_register, one fa_copy_async per chunk per rank, barrier)",
+               "note": "every rank D2H's its chunks into one pinned host model shared by the ranks, all links at "
+                       "once; max over ranks; not in value"}
+        if rank == 0 and host_sample:
+            res["bit_exact_on_sample"] = sample_check(got, host_sample, ns)[0]
+        cyc._host_gather.close()
+        return res
 
     def weak():
         P = P_total
@@ -696,11 +893,16 @@ def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, u
 
     if a.fedopt_params > 0:
         out["fedopt_sharded"] = side(fedopt_sharded)
+    devs = [torch.device("cuda", 0 if rehearsal else d) for d in range(world)]
     ip = side(in_process) if rank == 0 else None     # the other ranks wait (their GPUs are in use)
+    hr = (side(lambda: host_resident_side(a, devs, ns, clients=a.host_clients))
+          if rank == 0 and a.host_clients > 0 else None)
     fw = side(fedopt_waves) if rank == 0 and a.waves_params > 0 else None
     dist.barrier()
     if rank == 0:
         out["in_process"] = ip
+        if hr is not None:
+            out["host_resident"] = hr
         if fw is not None:
             out["fedopt_waves"] = fw
     return out

@@ -49,6 +49,15 @@ EXPORTS = {
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,   # v_in, v_out, out
         ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,  # opt, lr, b1, b2, tau
         ctypes.c_int64, ctypes.c_void_p]),                   # P, stream
+    "fa_fedopt_step_ex": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_int,                       # old, old_dtype
+        ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,       # updates, upd_dtype
+        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int,  # n, N, K
+        ctypes.c_void_p, ctypes.c_int,                       # pg, flags
+        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,  # m_in, m_in_dtype, m_out, m_out_dtype
+        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,  # v_in, v_in_dt, v_out, out, state_dt
+        ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,  # opt, lr, b1, b2, tau
+        ctypes.c_int64, ctypes.c_void_p]),                   # P, stream
     "fa_weighted_sum": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int,                       # acc, acc_dtype
         ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,       # updates, upd_dtype
@@ -66,6 +75,14 @@ EXPORTS = {
                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "fa_cast": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
+    "fa_ipc_get_handle": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "fa_ipc_open": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p),
+                                   ctypes.POINTER(ctypes.c_void_p)]),
+    "fa_ipc_close": (ctypes.c_int, [ctypes.c_void_p]),
+    "fa_copy_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "fa_peer_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "fa_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "fa_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
 }
 # measurement / tuning entry points: libfedagg_probe.so only (include/fedagg_probe.h)
 PROBE_EXPORTS = {
@@ -77,7 +94,8 @@ PROBE_EXPORTS = {
     "fa_stream_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
+IPC_HANDLE_BYTES = 64    # FA_IPC_HANDLE_BYTES
 
 
 class FedAggLibraryError(ImportError):

@@ -618,11 +618,16 @@ struct OptBuffers {
     void* pg;
     const void* m_in;
     void* m_out;
-    const double* v_in;
-    double* v_out;
-    double* out;
+    const void* v_in;
+    void* v_out;
+    void* out;
     int m_in_f64;    // 0: f32, 1: f64, -1: None
     int m_out_f64;
+    // storage dtype of v and the new model (fa_fedopt_step_ex): 0 = f64 (the reference's), 1 = f32
+    // (the fp32-state mode: same f64 arithmetic, rounded once to f32 on store, widened exactly on load)
+    int v_in_f32;
+    int v_out_f32;
+    int out_f32;
 };
 
 // multiply an array element held as PG by a python float constant (numpy weak scalar)
@@ -673,8 +678,16 @@ __device__ __forceinline__ void opt_load_state(const OptBuffers& b, const OptSca
 #pragma unroll
         for (int e = 0; e < E; ++e) mi[e] = (double)f16_to_f32(mh[e].bits);
     }
-    if (b.v_in) {
-        const double* vp = b.v_in + i0;
+    if (b.v_in && b.v_in_f32) {
+        float vf[E];
+        const float* vp = static_cast<const float*>(b.v_in) + i0;
+        if (full) strip_load<float, E, SNT>(vp, vf);
+        else
+            for (int e = 0; e < E; ++e) vf[e] = e < rem ? vp[e] : 0.f;
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = (double)vf[e];
+    } else if (b.v_in) {
+        const double* vp = static_cast<const double*>(b.v_in) + i0;
         if (full) strip_load<double, E, SNT>(vp, v);
         else
             for (int e = 0; e < E; ++e) v[e] = e < rem ? vp[e] : 0.0;
@@ -749,8 +762,22 @@ __device__ __forceinline__ void opt_apply(const OptBuffers& b, const OptScalars&
         if (__double_as_longlong(o[0]) != 0x7FF4DEADBEEF0001LL) return;
     }
     if (full) {
-        strip_store<double, E, OSM>(b.v_out + i0, v);
-        strip_store<double, E, OSM>(b.out + i0, o);
+        if (b.v_out_f32) {
+            float vf[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) vf[e] = (float)v[e];
+            strip_store<float, E, OSM>(static_cast<float*>(b.v_out) + i0, vf);
+        } else {
+            strip_store<double, E, OSM>(static_cast<double*>(b.v_out) + i0, v);
+        }
+        if (b.out_f32) {
+            float of[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) of[e] = (float)o[e];
+            strip_store<float, E, OSM>(static_cast<float*>(b.out) + i0, of);
+        } else {
+            strip_store<double, E, OSM>(static_cast<double*>(b.out) + i0, o);
+        }
         if (b.m_out_f64 == 1) strip_store<double, E, OSM>(static_cast<double*>(b.m_out) + i0, m);
         else if (b.m_out_f64 == 0) {
             float mf[E];
@@ -765,8 +792,10 @@ __device__ __forceinline__ void opt_apply(const OptBuffers& b, const OptScalars&
         }
     } else {
         for (int e = 0; e < rem; ++e) {
-            b.v_out[i0 + e] = v[e];
-            b.out[i0 + e] = o[e];
+            if (b.v_out_f32) static_cast<float*>(b.v_out)[i0 + e] = (float)v[e];
+            else static_cast<double*>(b.v_out)[i0 + e] = v[e];
+            if (b.out_f32) static_cast<float*>(b.out)[i0 + e] = (float)o[e];
+            else static_cast<double*>(b.out)[i0 + e] = o[e];
             if (b.m_out_f64 == 1) static_cast<double*>(b.m_out)[i0 + e] = m[e];
             else if (b.m_out_f64 == 0) static_cast<float*>(b.m_out)[i0 + e] = (float)m[e];
             else static_cast<f16*>(b.m_out)[i0 + e] = f16{f32_to_f16((float)m[e])};
@@ -1064,8 +1093,8 @@ k_fedopt_mix(const OptBuffers b, const ClientTable<S> tab, const int K, const in
             v[e] = vv[e] + acc[h * H + e];
             o[e] = acc[h * H + e];
         }
-        strip_store<double, H, 1>(b.v_out + at(h), v);
-        strip_store<double, H, 1>(b.out + at(h), o);
+        strip_store<double, H, 1>(static_cast<double*>(b.v_out) + at(h), v);
+        strip_store<double, H, 1>(static_cast<double*>(b.out) + at(h), o);
         if (b.m_out_f64) strip_store<double, H, 1>(static_cast<double*>(b.m_out) + at(h), m);
         else {
             float mf[H];
@@ -1771,6 +1800,17 @@ int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, i
                    const double* N, int K, void* pg, int flags, const void* m_in, int m_in_dtype, void* m_out,
                    const double* v_in, double* v_out, double* out, int serveropt, double lr, double beta1,
                    double beta2, double tau, int64_t P, void* stream) {
+    // the reference's dtype flow: m as numpy promotes it, v and the model float64
+    int pg_dt = (upd_dtype == FA_I32 || upd_dtype == FA_I64) ? FA_F64 : fa_promote(upd_dtype, old_dtype);
+    const int m_out_dt = fa_promote(m_in ? m_in_dtype : FA_NONE, pg_dt);
+    return fa_fedopt_step_ex(old, old_dtype, updates, upd_dtype, n, N, K, pg, flags, m_in, m_in_dtype, m_out,
+                             m_out_dt, v_in, FA_F64, v_out, out, FA_F64, serveropt, lr, beta1, beta2, tau, P, stream);
+}
+
+int fa_fedopt_step_ex(const void* old, int old_dtype, const void* const* updates, int upd_dtype, const double* n,
+                      const double* N, int K, void* pg, int flags, const void* m_in, int m_in_dtype, void* m_out,
+                      int m_out_dtype, const void* v_in, int v_in_dtype, void* v_out, void* out, int state_dtype,
+                      int serveropt, double lr, double beta1, double beta2, double tau, int64_t P, void* stream) {
     g_err[0] = 0;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (P < 0 || K < 0) return fail(FA_EINVAL, "fa_fedopt_step: negative size");
@@ -1796,10 +1836,20 @@ int fa_fedopt_step(const void* old, int old_dtype, const void* const* updates, i
     if (m_in && m_in_dtype != FA_F32 && m_in_dtype != FA_F64 && m_in_dtype != FA_F16)
         return fail(FA_EDTYPE, "fa_fedopt_step: m dtype %d", m_in_dtype);
     if (!m_in) m_in_dtype = FA_NONE;
-    const int m_out_dt = fa_promote(m_in_dtype, pg_dt);
+    if (state_dtype != FA_F64 && state_dtype != FA_F32)
+        return fail(FA_EDTYPE, "fa_fedopt_step_ex: state dtype %d (F64: the reference's, F32: fp32 state)", state_dtype);
+    if (v_in && v_in_dtype != FA_F64 && v_in_dtype != FA_F32)
+        return fail(FA_EDTYPE, "fa_fedopt_step_ex: v dtype %d", v_in_dtype);
+    // m as numpy promotes it; in the fp32-state mode m may instead be stored as f32 (rounded once)
+    const int m_np = fa_promote(m_in_dtype, pg_dt);
+    const int m_out_dt = m_out_dtype;
+    if (final_ && m_out_dt != m_np && !(state_dtype == FA_F32 && m_out_dt == FA_F32))
+        return fail(FA_EDTYPE, "fa_fedopt_step_ex: m_out dtype %d (numpy gives %d%s)", m_out_dt, m_np,
+                    state_dtype == FA_F32 ? "; F32 in the fp32-state mode" : "");
     auto mcode = [](int d) { return d == FA_NONE ? -1 : d == FA_F64 ? 1 : d == FA_F16 ? 2 : 0; };
 
-    OptBuffers b{old, pg, m_in, m_out, v_in, v_out, out, mcode(m_in_dtype), mcode(m_out_dt)};
+    OptBuffers b{old, pg, m_in, m_out, v_in, v_out, out, mcode(m_in_dtype), mcode(final_ ? m_out_dt : m_np),
+                 v_in && v_in_dtype == FA_F32, state_dtype == FA_F32, state_dtype == FA_F32};
     OptScalars s;
     s.lr = lr;
     s.b1 = beta1;
@@ -2034,6 +2084,96 @@ int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, co
     FA_CAST(FA_U64, uint64_t, FA_F64, double)
 #undef FA_CAST
     return fail(FA_EDTYPE, "fa_cast: unsupported conversion %d -> %d", in_dtype, out_dtype);
+}
+
+// ----------------------------------------------------------------------------
+// peer transport of the parameter-sliced all-gather (sharded.P2PAllGather,
+// multidev.allgather_devices): IPC mappings of the peers' model buffers and DMA copies into them
+// ----------------------------------------------------------------------------
+static_assert(sizeof(hipIpcMemHandle_t) <= FA_IPC_HANDLE_BYTES, "IPC handle size");
+
+int fa_ipc_get_handle(const void* dptr, void* handle, uint64_t* offset) {
+    g_err[0] = 0;
+    if (!dptr || !handle || !offset) return fail(FA_EINVAL, "fa_ipc_get_handle: null argument");
+    // a handle names a whole allocation (a caching allocator hands out pieces of one): export the
+    // allocation's base and the piece's offset in it
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    hipError_t e = hipMemGetAddressRange(&base, &size, const_cast<void*>(dptr));
+    if (e != hipSuccess) return fail(FA_EHIP, "fa_ipc_get_handle: hipMemGetAddressRange: %s", hipGetErrorString(e));
+    hipIpcMemHandle_t h;
+    e = hipIpcGetMemHandle(&h, base);
+    if (e != hipSuccess) return fail(FA_EHIP, "fa_ipc_get_handle: hipIpcGetMemHandle: %s", hipGetErrorString(e));
+    std::memset(handle, 0, FA_IPC_HANDLE_BYTES);
+    std::memcpy(handle, &h, sizeof(h));
+    *offset = (uint64_t)(static_cast<const char*>(dptr) - static_cast<const char*>(base));
+    return FA_OK;
+}
+
+int fa_ipc_open(const void* handle, uint64_t offset, void** base, void** dptr) {
+    g_err[0] = 0;
+    if (!handle || !base || !dptr) return fail(FA_EINVAL, "fa_ipc_open: null argument");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle, sizeof(h));
+    void* b = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&b, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return fail(FA_EHIP, "fa_ipc_open: hipIpcOpenMemHandle: %s", hipGetErrorString(e));
+    *base = b;
+    *dptr = static_cast<char*>(b) + offset;
+    return FA_OK;
+}
+
+int fa_ipc_close(void* base) {
+    g_err[0] = 0;
+    if (!base) return FA_OK;
+    hipError_t e = hipIpcCloseMemHandle(base);
+    if (e != hipSuccess) return fail(FA_EHIP, "fa_ipc_close: %s", hipGetErrorString(e));
+    return FA_OK;
+}
+
+int fa_copy_async(void* dst, const void* src, int64_t bytes, void* stream) {
+    g_err[0] = 0;
+    if (bytes < 0 || (bytes > 0 && (!dst || !src))) return fail(FA_EINVAL, "fa_copy_async: bad arguments");
+    if (bytes == 0) return FA_OK;
+    hipError_t e = hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(FA_EHIP, "fa_copy_async: %s", hipGetErrorString(e));
+    return FA_OK;
+}
+
+int fa_host_register(void* p, int64_t bytes) {
+    g_err[0] = 0;
+    if (!p || bytes <= 0) return fail(FA_EINVAL, "fa_host_register: bad arguments");
+    hipError_t e = hipHostRegister(p, (size_t)bytes, hipHostRegisterPortable);
+    if (e != hipSuccess) return fail(FA_EHIP, "fa_host_register: %s", hipGetErrorString(e));
+    return FA_OK;
+}
+
+int fa_host_unregister(void* p) {
+    g_err[0] = 0;
+    if (!p) return FA_OK;
+    hipError_t e = hipHostUnregister(p);
+    if (e != hipSuccess) return fail(FA_EHIP, "fa_host_unregister: %s", hipGetErrorString(e));
+    return FA_OK;
+}
+
+int fa_peer_enable(int dev, int peer) {
+    g_err[0] = 0;
+    if (dev == peer) return FA_OK;
+    int can = 0;
+    hipError_t e = hipDeviceCanAccessPeer(&can, dev, peer);
+    if (e != hipSuccess) return fail(FA_EHIP, "fa_peer_enable: hipDeviceCanAccessPeer: %s", hipGetErrorString(e));
+    if (!can) return fail(FA_EHIP, "fa_peer_enable: device %d cannot access device %d", dev, peer);
+    int cur = 0;
+    hipGetDevice(&cur);
+    e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipDeviceEnablePeerAccess(peer, 0);
+    hipSetDevice(cur);
+    if (e == hipErrorPeerAccessAlreadyEnabled) {
+        (void)hipGetLastError();
+        return FA_OK;
+    }
+    if (e != hipSuccess) return fail(FA_EHIP, "fa_peer_enable(%d -> %d): %s", dev, peer, hipGetErrorString(e));
+    return FA_OK;
 }
 
 #ifdef FEDAGG_PROBES

@@ -232,24 +232,33 @@ def fedopt_step(old, updates, n, N, *, first, final, pg=None, m_in=None, m_out=N
     for name, t in (("pg", pg), ("m_in", m_in), ("m_out", m_out), ("v_in", v_in), ("v_out", v_out), ("out", out)):
         if t is not None:
             _check_dev(name, t, P, dev)
-    if v_in is not None and v_in.dtype != torch.float64:
-        raise TypeError("v must be float64 (fedopt.py:171: np.ones(...) * tau**2)")
+    if v_in is not None and v_in.dtype not in (torch.float64, torch.float32):
+        raise TypeError("v must be float64 (fedopt.py:171: np.ones(...) * tau**2), or float32 (fp32-state mode)")
+    # the storage dtype of the server state: out's (float64: the reference's flow; float32: the
+    # fp32-state mode, fa_fedopt_step_ex — v and the model stored as f32, m as f32 or numpy's dtype)
+    state_dt = out.dtype if out is not None else torch.float64
+    if state_dt not in (torch.float64, torch.float32):
+        raise TypeError("out must be float64 (the reference's model dtype) or float32 (fp32-state mode)")
+    pg_dt, m_np = fedopt_dtypes(upd_dt, old.dtype, None if m_in is None else m_in.dtype)
     if final:
         if m_out is None or v_out is None or out is None:
             raise ValueError("final step needs m_out, v_out and out")
-        pg_dt, m_dt = fedopt_dtypes(upd_dt, old.dtype, None if m_in is None else m_in.dtype)
-        if m_out.dtype != m_dt or v_out.dtype != torch.float64 or out.dtype != torch.float64:
-            raise TypeError(f"output dtypes: m_out {m_dt}, v_out/out float64 required")
+        if v_out.dtype != state_dt:
+            raise TypeError(f"v_out must be {state_dt}, like out")
+        if m_out.dtype != m_np and not (state_dt == torch.float32 and m_out.dtype == torch.float32):
+            raise TypeError(f"output dtypes: m_out {m_np}" + (" or float32" if state_dt == torch.float32 else "") +
+                            f", v_out/out {state_dt}")
     flags = (_abi.FA_PG_FIRST if first else 0) | (_abi.FA_PG_FINAL if final else 0)
     ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
     with torch.cuda.device(dev):
         st = _stream_handle(old, stream)
-        rc = lib.fa_fedopt_step(
+        rc = lib.fa_fedopt_step_ex(
             old.data_ptr(), fa_dtype(old), _abi.ptr_array([u.data_ptr() for u in updates]), fa_dtype(upd_dt),
             _abi.double_array(n), _abi.double_array(N), K, ptr(pg), flags,
             ptr(m_in), _abi.FA_NONE if m_in is None else fa_dtype(m_in), ptr(m_out),
-            ptr(v_in), ptr(v_out), ptr(out), _OPTS[serveropt], float(learning_rate), float(beta1), float(beta2),
-            float(tau), P, st)
+            fa_dtype(m_out) if m_out is not None else fa_dtype(m_np),
+            ptr(v_in), _abi.FA_F64 if v_in is None else fa_dtype(v_in), ptr(v_out), ptr(out),
+            fa_dtype(state_dt), _OPTS[serveropt], float(learning_rate), float(beta1), float(beta2), float(tau), P, st)
     _abi.check(rc)
 
 
@@ -388,3 +397,59 @@ def norm1(x, matrix, stream=None):
         rc = lib.fa_norm1(out.data_ptr(), x.data_ptr(), fa_dtype(x), rows, cols, int(matrix), work.data_ptr(), st)
     _abi.check(rc)
     return out
+
+
+# ---- peer transport of the sliced all-gather (include/fedagg.h fa_ipc_* / fa_copy_async) ----------
+
+def ipc_handle(t):
+    """(handle bytes, byte offset) exporting device tensor ``t``'s memory to another process."""
+    import ctypes
+    lib = _abi.load()
+    h = ctypes.create_string_buffer(_abi.IPC_HANDLE_BYTES)
+    off = ctypes.c_uint64(0)
+    with torch.cuda.device(t.device):
+        _abi.check(lib.fa_ipc_get_handle(t.data_ptr(), h, ctypes.byref(off)))
+    return h.raw, int(off.value)
+
+
+def ipc_open(handle, offset, device):
+    """Map a peer process's buffer on ``device``: (base, device pointer); unmap with ipc_close(base)."""
+    import ctypes
+    lib = _abi.load()
+    if len(handle) != _abi.IPC_HANDLE_BYTES:
+        raise ValueError(f"IPC handle must be {_abi.IPC_HANDLE_BYTES} bytes")
+    base, ptr = ctypes.c_void_p(), ctypes.c_void_p()
+    with torch.cuda.device(device):
+        _abi.check(lib.fa_ipc_open(ctypes.create_string_buffer(handle, len(handle)), int(offset), ctypes.byref(base),
+                                   ctypes.byref(ptr)))
+    return int(base.value or 0), int(ptr.value or 0)
+
+
+def ipc_close(base, device):
+    lib = _abi.load()
+    with torch.cuda.device(device):
+        _abi.check(lib.fa_ipc_close(base))
+
+
+def copy_async(dst_ptr, src, nbytes, stream):
+    """``nbytes`` of device tensor ``src`` (from its start) to device address ``dst_ptr`` on ``stream``
+    (an IPC mapping of a peer's buffer, or another device's tensor): the DMA engines drive the link."""
+    lib = _abi.load()
+    if nbytes > src.numel() * src.element_size():
+        raise ValueError("copy_async: more bytes than the source holds")
+    with torch.cuda.device(src.device):
+        _abi.check(lib.fa_copy_async(int(dst_ptr), src.data_ptr(), int(nbytes), ctypes_stream(stream)))
+
+
+def peer_enable(dev, peer):
+    """Direct access of device ``dev`` to device ``peer``'s memory (in-process multi-GPU)."""
+    _abi.check(_abi.load().fa_peer_enable(int(dev), int(peer)))
+
+
+def host_register(t):
+    """Page-lock the memory of host tensor ``t`` (mapped by the caller, e.g. shared memory)."""
+    _abi.check(_abi.load().fa_host_register(t.data_ptr(), t.numel() * t.element_size()))
+
+
+def host_unregister(t):
+    _abi.check(_abi.load().fa_host_unregister(t.data_ptr()))

@@ -75,25 +75,18 @@ class ShardedFedAvg:
             dist.all_gather_into_tensor(full, buf, group=self.group)
         return full[:self.P]
 
-    def gather_to_host(self, agg_local, dst=0):
-        """Collect every slice into one host tensor on rank ``dst`` (None elsewhere)."""
-        host = agg_local.to("cpu")
+    def gather_to_host(self, agg_local, dst=0, gather=None):
+        """The whole model as ONE host tensor on rank ``dst`` (None elsewhere): every rank D2H's its
+        slice over its own PCIe link straight into the node's shared host model (:class:`HostGather`,
+        made on first use and kept for later rounds; pass ``gather`` to share one). FEDn serialises
+        the model on the host (roundhandler.py:465-468), so no device collective is needed."""
         if self.world == 1:
-            return host
-        buf = torch.zeros(self.shard, dtype=host.dtype)
-        buf[:host.numel()] = host
-        parts = [torch.empty_like(buf) for _ in range(self.world)] if self.rank == dst else None
-        if dist.get_backend(self.group) == "gloo":
-            dist.gather(buf, parts, dst=dst, group=self.group)
-        else:
-            # RCCL gathers device tensors; stage through the device and bring the result back
-            dbuf = buf.to(agg_local.device)
-            dparts = [torch.empty_like(dbuf) for _ in range(self.world)] if self.rank == dst else None
-            dist.gather(dbuf, dparts, dst=dst, group=self.group)
-            parts = [p.cpu() for p in dparts] if self.rank == dst else None
-        if self.rank != dst:
-            return None
-        return torch.cat(parts)[:self.P]
+            return agg_local.to("cpu")
+        if gather is None:
+            if getattr(self, "_host_gather", None) is None or self._host_gather.dst != dst:
+                self._host_gather = HostGather(self.P, agg_local.dtype, self.bounds, group=self.group, dst=dst)
+            gather = self._host_gather
+        return gather.gather(agg_local)
 
 
 class ShardedFedOpt:
@@ -123,8 +116,8 @@ class ShardedFedOpt:
     def allgather(self, out_local):
         return self._avg.allgather(out_local)
 
-    def gather_to_host(self, out_local, dst=0):
-        return self._avg.gather_to_host(out_local, dst)
+    def gather_to_host(self, out_local, dst=0, gather=None):
+        return self._avg.gather_to_host(out_local, dst, gather)
 
 
 def _kernel_fedopt_step(old, updates, n, N, m_in, v_in, params):
@@ -186,10 +179,42 @@ class CyclicShardedFedAvg:
             loc[l0:l0 + hi - lo].copy_(flat[lo:hi])
         return loc
 
-    def fold_allgather(self, agg_local, updates_local, n, N, init, out=None):
+    def gather_to_host(self, agg_local, dst=0, gather=None):
+        """The folded model as ONE host tensor on rank ``dst`` (None elsewhere), without a device
+        collective: every rank D2H's its chunks straight into the node's shared host model
+        (:class:`HostGather`, kept for later rounds) — FEDn's consumer (roundhandler.py:465-468)."""
+        if gather is None:
+            if getattr(self, "_host_gather", None) is None or self._host_gather.dst != dst:
+                self._host_gather = HostGather(self.P, agg_local.dtype, None, group=self.group, dst=dst)
+            gather = self._host_gather
+        return gather.gather(agg_local, self.owned())
+
+    def fold_allgather(self, agg_local, updates_local, n, N, init, out=None, p2p=None):
         """Fold every round and gather it as soon as it is folded; returns the full model
-        (``full[:P]``; on the host for gloo). ``agg_local`` / ``updates_local``: local_len each."""
+        (``full[:P]``; on the host for gloo). ``agg_local`` / ``updates_local``: local_len each.
+
+        ``p2p``: a :class:`P2PAllGather` over this geometry's ``full_len`` buffer — round i is then
+        pushed by direct copies into every peer's buffer (one copy stream per peer) instead of an RCCL
+        all-gather, and the result is ``p2p.full[:P]``, which the NEXT call overwrites: it fences on
+        entry (every rank done with the previous result) and on exit (every rank's pushes landed)."""
         C, W = self.C, self.world
+        if p2p is not None:
+            if p2p.full.numel() < self.full_len:
+                raise ValueError(f"p2p buffer has {p2p.full.numel()} elements, this geometry needs {self.full_len}")
+            dev = agg_local.device
+            cur = torch.cuda.current_stream(dev)
+            out = p2p.full
+            p2p.fence()
+            for i in range(self.rounds):
+                sl = slice(i * C, (i + 1) * C)
+                self.fold_fn(agg_local[sl], [u[sl] for u in updates_local], n, N, init)
+                at = (i * W + self.rank) * C
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                p2p.push(at, agg_local[sl], ev)
+                out[at:at + C].copy_(agg_local[sl], non_blocking=True)
+            p2p.fence()
+            return out[:self.P]
         coll = self.collective
         gloo = coll and dist.get_backend(self.group) == "gloo"
         dev = agg_local.device
@@ -217,3 +242,177 @@ class CyclicShardedFedAvg:
         if on_gpu and coll:
             cur.wait_stream(self._comm)
         return out[:self.P]
+
+
+class P2PAllGather:
+    """Direct peer-to-peer all-gather over xGMI ("prefer ... direct (all 7
+    links)"), the alternative to RCCL's ring / multi-channel all-gather for
+    :meth:`CyclicShardedFedAvg.fold_allgather`.
+
+    Every rank owns a model buffer ``full`` of the same length for the session. The ranks exchange
+    IPC handles of those buffers ONCE (``fa_ipc_get_handle`` / ``fa_ipc_open``, handles passed with
+    ``all_gather_object``), so each rank holds a device pointer into every peer's buffer. A rank then
+    pushes each piece it folds into all peers with one DMA copy per peer (``fa_copy_async``), each
+    peer on its own stream, i.e. over its own link, all links busy at once and no rank forwarding
+    another's data (a ring moves every byte W - 1 hops over one link per rank).
+
+    ``fence()`` orders the ranks: every rank's earlier pushes have completed before any rank's
+    stream runs past it. Under RCCL it is a one-element all-reduce issued after the copy streams
+    (device-side, the host does not block); under gloo (CPU tests, one-GPU rehearsals) a device
+    synchronize and a barrier.
+    """
+
+    def __init__(self, full, group=None):
+        from . import ops
+        self.full = full
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.device = full.device
+        self.esize = full.element_size()
+        handle, off = ops.ipc_handle(full)
+        mine = (handle, off, full.numel(), str(full.dtype))
+        objs = [None] * self.world
+        if self.world > 1:
+            dist.all_gather_object(objs, mine, group=group)
+        else:
+            objs = [mine]
+        for r, (_, _, n, dt) in enumerate(objs):
+            if n != full.numel() or dt != str(full.dtype):
+                raise ValueError(f"P2PAllGather: rank {r} buffer is {n} x {dt}, this rank's {full.numel()} x {full.dtype}")
+        self.peers = {}
+        try:
+            for r, (h, o, _, _) in enumerate(objs):
+                if r != self.rank:
+                    self.peers[r] = ops.ipc_open(h, o, self.device)
+        except Exception:
+            self.close(fence=False)
+            raise
+        self.streams = {r: torch.cuda.Stream(self.device) for r in self.peers}
+        self.nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
+        self._flag = torch.zeros(1, dtype=torch.float32, device=self.device) if self.nccl else None
+
+    def push(self, at, src, after):
+        """Copy device tensor ``src`` to elements [at, at + len(src)) of every peer's buffer once
+        ``after`` (an event on the folding stream) has fired."""
+        from . import ops
+        if at < 0 or at + src.numel() > self.full.numel():
+            raise ValueError("P2PAllGather.push: piece outside the buffer")
+        nbytes = src.numel() * self.esize
+        for r, st in self.streams.items():
+            st.wait_event(after)
+            ops.copy_async(self.peers[r][1] + at * self.esize, src, nbytes, st)
+
+    def fence(self):
+        cur = torch.cuda.current_stream(self.device)
+        for st in self.streams.values():
+            cur.wait_stream(st)
+        if self.world == 1 or not dist.is_initialized():
+            return
+        if self.nccl:
+            dist.all_reduce(self._flag, group=self.group)
+        else:
+            torch.cuda.synchronize(self.device)
+            dist.barrier(group=self.group)
+
+    def close(self, fence=True):
+        """Unmap the peers' buffers (after a fence: no copy into them is in flight)."""
+        from . import ops
+        if fence and self.peers:
+            self.fence()
+            torch.cuda.synchronize(self.device)
+        for r, (base, _) in list(self.peers.items()):
+            ops.ipc_close(base, self.device)
+        self.peers = {}
+        if fence and self.world > 1 and dist.is_initialized():
+            dist.barrier(group=self.group)       # no peer unmaps while another still copies
+
+
+class HostGather:
+    """The node's ONE host copy of a sliced model: every rank D2H's its slice over its own PCIe link
+    straight into it (FEDn's consumer of the aggregate is host serialisation, roundhandler.py:465-468;
+    SURVEY.md §8(e): "each GPU could also D2H its own slice into one pinned host buffer").
+
+    Rank ``dst`` creates a shared-memory file of the model's size (space reserved up front with
+    ``posix_fallocate``: a full /dev/shm raises here, not as a fault later), every rank of the node
+    maps it and page-locks its mapping (``fa_host_register``) once, and the file's name is removed as
+    soon as all ranks hold it, so nothing outlives the processes. :meth:`gather` then costs one
+    D2H per rank plus a barrier, all links at once.
+    """
+
+    def __init__(self, P, dtype, bounds, group=None, dst=0, shm_dir="/dev/shm"):
+        import os
+        import uuid
+        self.P, self.dtype, self.bounds, self.group, self.dst = P, dtype, bounds, group, dst
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        esize = torch.empty((), dtype=dtype).element_size()
+        nbytes = max(1, P) * esize
+        name = [None]
+        if self.rank == dst:
+            path = os.path.join(shm_dir, f"fedn_amd_model_{os.getpid()}_{uuid.uuid4().hex[:12]}")
+            try:
+                fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+                try:
+                    os.posix_fallocate(fd, 0, nbytes)
+                finally:
+                    os.close(fd)
+                name = [path]
+            except OSError as e:
+                try:
+                    os.unlink(path)
+                except OSError:
+                    pass
+                name = [f"error: {e}"]
+        if self.world > 1:
+            dist.broadcast_object_list(name, src=dst, group=self.group)
+        if name[0].startswith("error: "):
+            raise OSError(f"HostGather: shared host model not created ({name[0][7:]})")
+        self.host = torch.from_file(name[0], shared=True, size=max(1, P), dtype=dtype)
+        if self.world > 1:
+            dist.barrier(group=self.group)
+        if self.rank == dst:
+            os.unlink(name[0])
+        self.pinned = False
+        self._stream = None
+
+    def _pin(self, device):
+        from . import ops
+        if not self.pinned:
+            with torch.cuda.device(device):
+                ops.host_register(self.host)
+            self.pinned = True
+            self._stream = torch.cuda.Stream(device)
+
+    def gather(self, local, pieces=None):
+        """``local``: this rank's part of the model (device or CPU tensor). ``pieces``: where it goes,
+        as (global_lo, global_hi, local_lo) triples; default: this rank's contiguous slice of
+        ``bounds`` from local[0]. Returns the host model (a shared-memory tensor, valid until the
+        next gather) on rank ``dst``, None elsewhere."""
+        from . import ops
+        if pieces is None:
+            lo, hi = self.bounds[self.rank]
+            pieces = [(lo, hi, 0)] if hi > lo else []
+        es = self.host.element_size()
+        if local.device.type == "cuda" and pieces:
+            self._pin(local.device)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(local.device))
+            self._stream.wait_event(ev)
+            for lo, hi, l0 in pieces:
+                if l0 + hi - lo > local.numel() or hi > self.P:
+                    raise ValueError("HostGather.gather: piece outside the local buffer or the model")
+                ops.copy_async(self.host.data_ptr() + lo * es, local[l0:], (hi - lo) * es, self._stream)
+            self._stream.synchronize()
+        else:
+            for lo, hi, l0 in pieces:
+                self.host[lo:hi].copy_(local[l0:l0 + hi - lo])
+        if self.world > 1:
+            dist.barrier(group=self.group)
+        return self.host[:self.P] if self.rank == self.dst else None
+
+    def close(self):
+        from . import ops
+        if self.pinned:
+            ops.host_unregister(self.host)
+            self.pinned = False

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 3
+#define FA_ABI_VERSION 4
 
 /* element type codes */
 enum fa_dtype {
@@ -135,6 +135,25 @@ int fa_fedopt_step(const void* old, int old_dtype,
                    int64_t P, void* stream);
 
 /*
+ * fa_fedopt_step with the storage dtypes of the server state explicit: the reference's flow
+ * (state_dtype F64; m_out_dtype = numpy's promote(m_in, pg)) or the fp32-STATE mode (state_dtype
+ * F32): v_out and out are float32 and m_out may be F32. Same arithmetic as the reference step on the
+ * values it is given (f64 server step, numpy's dtype rules for m and the pseudo-gradient); each
+ * stored value is the f64 result rounded once to f32, and f32 state is widened exactly on load.
+ * HBM bytes per round in that mode with fp32 updates, old, m, v: P*(4K + 24) instead of
+ * P*(4K + 48) (plug-in fedn_amd.aggregators.fedopt_f32state).
+ * v_in_dtype: F64 or F32 (either mode may read either: a session can switch).
+ */
+int fa_fedopt_step_ex(const void* old, int old_dtype,
+                      const void* const* updates, int upd_dtype,
+                      const double* n, const double* N, int K,
+                      void* pg, int flags,
+                      const void* m_in, int m_in_dtype, void* m_out, int m_out_dtype,
+                      const void* v_in, int v_in_dtype, void* v_out, void* out, int state_dtype,
+                      int serveropt, double lr, double beta1, double beta2, double tau,
+                      int64_t P, void* stream);
+
+/*
  * Server-function aggregation rules (hooks.py:109-143): the two formulas the reference ships
  * as examples of user aggregation code, on device buffers with numpy's rounding.
  *
@@ -219,6 +238,35 @@ int fa_promote(int a, int b);
  */
 int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, const int64_t* out_shape,
             const int64_t* in_strides, void* stream);
+
+/*
+ * Peer transport of the parameter-sliced all-gather ("prefer ... direct (all 7
+ * links)"; the gathered model's consumer is roundhandler.py:465-468). Replaces the transport of
+ * RCCL's ncclAllGather for fedn_amd/sharded.py P2PAllGather (one process per GPU) and
+ * fedn_amd/multidev.py allgather_devices (one process, several GPUs): every rank copies its folded
+ * slice straight into each peer's model buffer, one copy stream per peer (one xGMI link each).
+ *
+ * fa_ipc_get_handle  FA_IPC_HANDLE_BYTES of handle for the allocation that holds dptr, and dptr's
+ *                    byte offset in it (a caching allocator hands out pieces of one allocation)
+ * fa_ipc_open        map another process's handle: *base = the mapping (pass it to fa_ipc_close),
+ *                    *dptr = base + offset
+ * fa_ipc_close       unmap a mapping fa_ipc_open returned
+ * fa_copy_async      bytes from src to dst on stream; any two device pointers of this process
+ *                    (IPC mappings and other devices' buffers included): the DMA engines move them
+ * fa_peer_enable     let device dev read / write device peer's memory directly (in-process);
+ *                    already enabled is not an error
+ * fa_host_register   page-lock host memory the caller mapped (the node's shared host model that
+ *                    every rank D2H's its slice into: sharded.HostGather), so DMA reaches it directly;
+ * fa_host_unregister undo it before the caller unmaps
+ */
+#define FA_IPC_HANDLE_BYTES 64
+int fa_ipc_get_handle(const void* dptr, void* handle, uint64_t* offset);
+int fa_ipc_open(const void* handle, uint64_t offset, void** base, void** dptr);
+int fa_ipc_close(void* base);
+int fa_copy_async(void* dst, const void* src, int64_t bytes, void* stream);
+int fa_peer_enable(int dev, int peer);
+int fa_host_register(void* p, int64_t bytes);
+int fa_host_unregister(void* p);
 
 #ifdef __cplusplus
 }

@@ -1351,6 +1351,79 @@ def test_sharded_gloo_world2_hip_kernel():
         assert np.array_equal(full.view(np.uint32), want.view(np.uint32)), f"rank {rank}"
 
 
+def _p2p_gloo_worker(rank, world, port, P, K, chunk, q):
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+
+    from fedn_amd.sharded import CyclicShardedFedAvg, P2PAllGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        g = torch.Generator(device="cuda:0").manual_seed(5)
+        base = torch.randn(P, generator=g, device="cuda:0")
+        ups = [torch.randn(P, generator=g, device="cuda:0").mul_(0.01).add_(base) for _ in range(K)]
+        ns = [int(v) for v in np.random.default_rng(5).integers(1, 5001, K)]
+        Ns = [int(v) for v in np.cumsum(ns)]
+        cs = CyclicShardedFedAvg(P, chunk=chunk)
+        aggc = torch.empty(cs.local_len, device="cuda:0")
+        loc = [cs.local(u) for u in ups]
+        full = torch.full((cs.full_len,), float("nan"), device="cuda:0")
+        p2p = P2PAllGather(full)                      # IPC handles of both ranks' buffers, opened once
+        outs = []
+        for step in range(3):                         # the buffer is reused: entry + exit fences
+            if step == 2:                             # a later round of the session: other updates
+                loc = [cs.local(u.add(1.0)) for u in ups]
+            out = cs.fold_allgather(aggc, loc, ns, Ns, init=True, p2p=p2p)
+            torch.cuda.synchronize()
+            outs.append(out.cpu().numpy().copy())
+        p2p.close()
+        q.put((rank, outs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,P,chunk", [(2, 200_003, 8192), (3, 1_000_000, 65536)])
+def test_p2p_allgather_gloo_hip(world, P, chunk):
+    """The direct peer-to-peer all-gather (sharded.P2PAllGather: IPC handles exchanged once,
+    fa_copy_async into every peer's buffer, one copy stream per peer, entry / exit fences) with the
+    HIP fold: ranks share this box's GPU (each maps the others' buffers through IPC), three steps
+    over one buffer, every rank's whole model bit-identical to one single-device fold."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from fedn_amd import ops
+    K = 9
+    s_ = socket.socket()
+    s_.bind(("127.0.0.1", 0))
+    port = s_.getsockname()[1]
+    s_.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pc = mp.start_processes(_p2p_gloo_worker, args=(world, port, P, K, chunk, q), nprocs=world, join=False,
+                            start_method="spawn")
+    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    while not pc.join(timeout=60):
+        pass
+    g = torch.Generator(device=DEV).manual_seed(5)
+    base = torch.randn(P, generator=g, device=DEV)
+    ups = [torch.randn(P, generator=g, device=DEV).mul_(0.01).add_(base) for _ in range(K)]
+    ns = [int(v) for v in np.random.default_rng(5).integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
+    want = torch.empty(P, device=DEV)
+    ops.fedavg_fold(want, ups, ns, Ns, init=True)
+    want2 = torch.empty(P, device=DEV)
+    ops.fedavg_fold(want2, [u.add(1.0) for u in ups], ns, Ns, init=True)
+    want, want2 = want.cpu().numpy(), want2.cpu().numpy()
+    for rank, outs in res:
+        for step, got in enumerate(outs):
+            w = want2 if step == 2 else want
+            assert np.array_equal(got.view(np.uint32), w.view(np.uint32)), f"rank {rank} step {step}"
+
+
 def test_waves_reject_mismatched_updates():
     """WaveFedOpt refuses updates whose dtype / size differ from the first (a copy into the bf16
     wave slots would otherwise round an fp32 update silently) and misplaced old slices."""

@@ -27,6 +27,24 @@ for s in $STEPS; do
         --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --params 20000000 \
         --clients 16 --fedopt-params 20000000 --waves-params 50000000 --waves-clients 32 > "$OUT/rehearsal.log" 2>&1; rc=$?
       echo "rehearsal rc=$rc"; grep -v amdgpu.ids "$OUT/rehearsal.log" | tail -3; [ $rc -eq 0 ] || exit $rc ;;
+    selflaunch)
+      # bench.py --gpus 2 WITHOUT torchrun (its own rank launcher), both ranks on this box's GPU (gloo)
+      FEDN_AMD_BENCH_ONE_GPU=1 timeout -k 10 600 python bench.py --gpus 2 --steps 5 --warmup 2 --params 20000000 \
+        --clients 16 --fedopt-params 20000000 --waves-params 50000000 --waves-clients 32 --cpu-sample 2000000 \
+        --host-clients 4 > "$OUT/selflaunch.log" 2>&1; rc=$?
+      echo "selflaunch rc=$rc"; grep -v amdgpu.ids "$OUT/selflaunch.log" | tail -3; [ $rc -eq 0 ] || exit $rc ;;
+    rccl1)
+      # the N>1 path at world size 1 over a real RCCL communicator (all-gathers as collectives, P2P fences)
+      FEDN_AMD_BENCH_RCCL_WORLD1=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 1 --steps 5 --warmup 2 --params 100000000 \
+        --clients 64 --fedopt-params 50000000 --waves-params 50000000 --waves-clients 32 --cpu-sample 2000000 \
+        > "$OUT/rccl1.log" 2>&1; rc=$?
+      echo "rccl1 rc=$rc"; grep -v amdgpu.ids "$OUT/rccl1.log" | tail -3; [ $rc -eq 0 ] || exit $rc ;;
+    gtest)
+      # a subset of the GPU tests: FEDN_AMD_GTEST = pytest -k expression
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider \
+        -k "$FEDN_AMD_GTEST" > "$OUT/gtest.log" 2>&1; rc=$?
+      echo "gtest rc=$rc"; tail -5 "$OUT/gtest.log"; [ $rc -eq 0 ] || exit $rc ;;
     micro)
       timeout -k 10 600 python tools/microbench.py > "$OUT/micro.log" 2>&1; rc=$?
       echo "micro rc=$rc"; cat "$OUT/micro.log" | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc ;;
