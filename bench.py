@@ -357,6 +357,26 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000, pattern_probe=
     ok2 = bool(np.array_equal(out2[:S].cpu().numpy().view(np.uint64), want2[0].view(np.uint64)) and
                np.array_equal(m_out[:S].cpu().numpy().view(np.uint64), st.m[0].view(np.uint64)) and
                np.array_equal(v_out[:S].cpu().numpy().view(np.uint64), st.v[0].view(np.uint64)))
+    # fp32-state mode (aggregators.fedopt_f32state, fa_fedopt_step_ex state F32): the steady state of a
+    # float32 model with float32 m / v — round 1's results rounded to f32 as the mode stores them
+    old_f, m_f, v_f = out.float(), m32.clone(), v.float()
+    m_o32, v_o32, out32 = (torch.empty(P, dtype=torch.float32, device=device) for _ in range(3))
+
+    def r3():
+        ops.fedopt_step(old_f, ups, ns, Ns, first=True, final=True, m_in=m_f, m_out=m_o32, v_in=v_f, v_out=v_o32,
+                        out=out32, serveropt="adam", stream=stream, **kw)
+
+    for _ in range(warm):
+        r3()
+    _, ms3 = timed_steps(r3, steps, stream, 1, device, False)
+    st3 = ref.FedOptState()
+    st3.m, st3.v = [m_f[:S].cpu().numpy()], [v_f[:S].cpu().numpy()]
+    t0 = time.perf_counter()
+    want3, _ = ref.fedopt_combine_f32state(st3, ups_s, [old_f[:S].cpu().numpy()], params)
+    cpu3 = time.perf_counter() - t0
+    ok3 = bool(np.array_equal(out32[:S].cpu().numpy().view(np.uint32), want3[0].view(np.uint32)) and
+               np.array_equal(m_o32[:S].cpu().numpy().view(np.uint32), st3.m[0].view(np.uint32)) and
+               np.array_equal(v_o32[:S].cpu().numpy().view(np.uint32), st3.v[0].view(np.uint32)))
     # the ceiling of the kernel's own access pattern: the same loads and stores with one add per value
     # (k_fedopt_mix, libfedagg_probe.so; its outputs are not used), timed after the product launches
     pattern = {}
@@ -373,7 +393,8 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000, pattern_probe=
             with _abi.use_probe():
                 ops.tune(opt_mix=0)
     for phase, ms, b, ok, cpu_s in (("round1", ms1, K * P * 4 + P * 4 + P * 20, ok1, cpu1),
-                                    ("steady", ms2, P * (4 * K + 48), ok2, cpu2)):
+                                    ("steady", ms2, P * (4 * K + 48), ok2, cpu2),
+                                    ("steady_f32state", ms3, P * (4 * K + 24), ok3, cpu3)):
         wl = f"fedopt_adam_{phase}_k{K}_p{P}"
         traffic, tsrc = pmc_traffic(wl)
         gbs = b / ms / 1e6
@@ -382,7 +403,10 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000, pattern_probe=
                                    "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
                                    "kernel": "k_fedopt_c (pseudo-gradient fold + Adam step fused; 4 coalesced element pairs per lane)",
                                    "alg_bytes_per_launch": b},
-                      "bit_exact_on_sample": ok, "sample": f"first {S} params of every buffer vs oracle/numpy_ref",
+                      "bit_exact_on_sample": ok,
+                      "sample": f"first {S} params of every buffer vs oracle/numpy_ref" +
+                                (".fedopt_combine_f32state (the mode's definition: the reference step on the "
+                                 "stored f32 state, rounded once to f32)" if phase == "steady_f32state" else ""),
                       "cpu_baseline": {"value": K * S / cpu_s, "unit": "params/s", "cores": 1, "kind": "port",
                                        "sample": f"{K} clients x {S} params: oracle/numpy_ref.fedopt_combine (the "
                                                  "fedopt.py restatement, numpy, single-threaded)", "seconds": cpu_s}}
@@ -394,7 +418,10 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000, pattern_probe=
                         "instead of the arithmetic; the HBM ceiling of this traffic pattern on this box"}
     res["config"] = (f"BASELINE configs[3]: FedAdam, {K} device-resident fp32 updates x {P} params, m / v in HBM "
                      "(fedopt.py:151-185), one fused launch per round")
-    del ups, old32, out, v, m32, old64, m64, v64, m_out, v_out, out2
+    res["steady_f32state"]["vs_steady_ms"] = ms3 / ms2
+    res["steady_f32state"]["note"] = ("fp32-state mode (aggregators.fedopt_f32state): m / v / model stored in "
+                                      "float32, P*(4K+24) bytes; opt-in, not the reference's dtype flow")
+    del ups, old32, out, v, m32, old64, m64, v64, m_out, v_out, out2, old_f, m_f, v_f, m_o32, v_o32, out32
     torch.cuda.empty_cache()
     return res
 

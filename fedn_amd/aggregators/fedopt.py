@@ -37,6 +37,10 @@ PARAMETER_SCHEMA = {"serveropt": str, "learning_rate": float, "beta1": float, "b
 class Aggregator(AggregatorBase):
     """Federated Optimization (FedOpt) on MI355X."""
 
+    #: server state storage: False = the reference's dtype flow (m promoted, v and the model
+    #: float64); True = fp32-state mode (fedopt_f32state.py)
+    fp32_state = False
+
     def __init__(self, update_handler, device=None, devices=None):
         super().__init__(update_handler)
         self.name = "fedopt"
@@ -57,9 +61,9 @@ class Aggregator(AggregatorBase):
                                  len(spread(self.devices, _packed_bytes(model_next))) > 1))
             if self.sharded:
                 from ..multidev import ShardedFedOptState
-                self.state = ShardedFedOptState()
+                self.state = ShardedFedOptState(self.fp32_state)
             else:
-                self.state = FedOptState()
+                self.state = FedOptState(self.fp32_state)
         if self.sharded:
             from ..multidev import ShardedFedOptPipeline
             return ShardedFedOptPipeline(self.devices, model_old, model_next)

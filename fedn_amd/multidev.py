@@ -29,7 +29,8 @@ import torch
 from . import mixed, ops
 from .ingest import ShardedStagedModel, StagedModel
 from .layout import Layout
-from .staging import BATCH, HostStreamer, check_fedopt_dtypes, chunks, fused_fedopt_pair, group_tensors, old_members
+from .staging import (BATCH, HostStreamer, check_fedopt_dtypes, chunks, fused_fedopt_pair, group_tensors, old_members,
+                      state_dtypes)
 
 
 class _DevSlot:
@@ -55,6 +56,42 @@ def gather_group(layout, bounds, devices, per_dev, dt):
     for dv in devices:
         torch.cuda.current_stream(dv).synchronize()
     return flat.numpy()   # a new pinned block owned by the caller (see staging._Pipeline._to_host)
+
+
+def allgather_devices(parts, P):
+    """The in-process form of the sliced all-gather: ``parts`` = [(device, slice
+    tensor on it, lo)] covering [0, P); returns one full P-element model per device. Device d's slice
+    is copied straight into every other device's model by DMA over the d -> e link (``fa_copy_async``
+    after ``fa_peer_enable``), one copy stream per (source, destination) pair, so all links run at
+    once; each destination's current stream then waits for the copies into it. A device listed
+    twice (tests on a one-GPU box) gets its own model buffer per entry."""
+    parts = [(torch.device(dv), t, lo) for dv, t, lo in parts]
+    fulls = []
+    for d, (dv, t, lo) in enumerate(parts):
+        if lo < 0 or lo + t.numel() > P:
+            raise ValueError(f"allgather_devices: part {d} [{lo}, {lo + t.numel()}) outside [0, {P})")
+        fulls.append(torch.empty(P, dtype=t.dtype, device=dv))
+    if sum(t.numel() for _, t, _ in parts) != P:
+        raise ValueError("allgather_devices: the parts do not cover the model")
+    done = [[] for _ in parts]
+    for i, (src_dev, t, lo) in enumerate(parts):
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(src_dev))
+        es = t.element_size()
+        for j, (dst_dev, _, _) in enumerate(parts):
+            if src_dev.index != dst_dev.index:
+                ops.peer_enable(src_dev.index, dst_dev.index)
+            st = torch.cuda.Stream(src_dev)
+            st.wait_event(ready)
+            ops.copy_async(fulls[j].data_ptr() + lo * es, t, t.numel() * es, st)
+            ev = torch.cuda.Event()
+            ev.record(st)
+            done[j].append((ev, st))
+    for j, (dst_dev, _, _) in enumerate(parts):
+        cur = torch.cuda.current_stream(dst_dev)
+        for ev, _ in done[j]:
+            cur.wait_event(ev)
+    return fulls
 
 
 def _same_devices(a, b):
@@ -330,7 +367,7 @@ class ShardedFedOptState:
     round on the per-tensor path the state is per tensor on the first device (``m_t``/``v_t``)
     and is re-sliced over the devices when a later round's layout allows it."""
 
-    def __init__(self):
+    def __init__(self, fp32=False):
         self.m = None
         self.v = None
         self.signature = None
@@ -339,9 +376,10 @@ class ShardedFedOptState:
         self.devices = None
         self.m_t = None
         self.v_t = None
+        self.fp32 = fp32            # fp32-state mode (staging.FedOptState)
 
     def reset(self):
-        self.__init__()
+        self.__init__(self.fp32)
 
     def tensors(self, device=None):
         """(m, v) per tensor (model order) on ``device`` (default: the first device), or (None, None)."""
@@ -535,11 +573,11 @@ class ShardedFedOptPipeline(_ShardedStaging):
                 old = self.old[d][dt]
                 m_in = state.m[d][dt] if state.m is not None else None
                 v_in = state.v[d][dt] if state.v is not None else None
-                _, m_dt = ops.fedopt_dtypes(ops.torch_dtype(dt), old.dtype, None if m_in is None else m_in.dtype)
+                m_dt, sdt = state_dtypes(state, dt, old.dtype, m_in)
                 # new m / v buffers: a failed step leaves the session's state untouched (staging.py)
                 m_out = torch.empty(P, dtype=m_dt, device=dv)
-                v_out = torch.empty(P, dtype=torch.float64, device=dv)
-                out = torch.empty(P, dtype=torch.float64, device=dv)
+                v_out = torch.empty(P, dtype=sdt, device=dv)
+                out = torch.empty(P, dtype=sdt, device=dv)
                 pg = self._pg(d, dt) if (not first or len(entries) > BATCH) else None
                 new_m[d][dt], new_v[d][dt] = m_out, v_out
                 ctx.append((old, pg, m_in, m_out, v_in, v_out, out))
@@ -555,7 +593,7 @@ class ShardedFedOptPipeline(_ShardedStaging):
                                 learning_rate=params["learning_rate"], beta1=params["beta1"],
                                 beta2=params["beta2"], tau=params["tau"], stream=self.compute[d],
                                 upd_dtype=ops.torch_dtype(dt))
-            flats[dt] = self._to_host_chunks(dt, [c[6] for c in ctx], step, torch.float64)
+            flats[dt] = self._to_host_chunks(dt, [c[6] for c in ctx], step, ctx[0][6].dtype)
             self.old_ready.add(dt)
         self.pg_started = True
         self._sync_d2h()

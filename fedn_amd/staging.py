@@ -572,16 +572,19 @@ class FedOptState:
     server step, exactly like the reference's ``self.m``/``self.v``.
     """
 
-    def __init__(self):
+    def __init__(self, fp32=False):
         self.m = None
         self.v = None
         self.signature = None
         self.layout = None
         self.m_t = None
         self.v_t = None
+        # fp32-state mode (aggregators.fedopt_f32state): groups whose global model is float32 keep
+        # m, v and the new model in float32 (fa_fedopt_step_ex, state_dtype F32)
+        self.fp32 = fp32
 
     def reset(self):
-        self.__init__()
+        self.__init__(self.fp32)
 
     def tensors(self):
         """(m, v) as per-tensor device tensors in model order, or (None, None)."""
@@ -707,6 +710,16 @@ def check_fedopt_dtypes(layout):
     for dt in layout.groups:
         if ops.torch_dtype(dt) not in (torch.float16, torch.float32, torch.float64, torch.int32, torch.int64):
             raise TypeError(f"FedOpt supports float16/float32/float64/int32/int64 updates, got {dt}")
+
+
+def state_dtypes(state, upd_dt, old_dt, m_in):
+    """(m dtype, v / new-model dtype) of one group's server step: numpy's flow (m promoted, v and the
+    model float64, fedopt.py:151-258), or in the fp32-state mode, for a float32 global model, float32
+    for all three (fa_fedopt_step_ex)."""
+    _, m_dt = ops.fedopt_dtypes(ops.torch_dtype(upd_dt), old_dt, None if m_in is None else m_in.dtype)
+    if getattr(state, "fp32", False) and old_dt == torch.float32:
+        return torch.float32, torch.float32
+    return m_dt, torch.float64
 
 
 class FedOptPipeline(_Pipeline):
@@ -850,12 +863,12 @@ class FedOptPipeline(_Pipeline):
                 self.old_ready.add(dt)
             m_in = state.m[dt] if state.m is not None else None
             v_in = state.v[dt] if state.v is not None else None
-            _, m_dt = ops.fedopt_dtypes(ops.torch_dtype(dt), old.dtype, None if m_in is None else m_in.dtype)
+            m_dt, sdt = state_dtypes(state, dt, old.dtype, m_in)
             # new m / v buffers (same HBM traffic as in place): a step that fails part-way through
             # its chunks leaves the session's state exactly as the last completed round left it
             m_out = torch.empty(P, dtype=m_dt, device=self.device)
-            v_out = torch.empty(P, dtype=torch.float64, device=self.device)
-            out = torch.empty(P, dtype=torch.float64, device=self.device)
+            v_out = torch.empty(P, dtype=sdt, device=self.device)
+            out = torch.empty(P, dtype=sdt, device=self.device)
             # pg workspace: needed unless this launch starts AND ends the pseudo-gradient in registers
             pg = self._pg(dt) if (not first or len(entries) > BATCH) else None
             ys = [self.group(e[0], dt) for e in entries]

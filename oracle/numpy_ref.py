@@ -217,6 +217,25 @@ def fedopt_combine(state, updates, old, parameters=None):
         return None, nr
 
 
+def fedopt_combine_f32state(state, updates, old, parameters=None):
+    """The fp32-STATE mode's definition (fedn_amd.aggregators.fedopt_f32state, SURVEY.md §7 step 5;
+    a mode of this build, not a reference behaviour): one fedopt.py round (``fedopt_combine``, i.e.
+    fedopt.py:40-121 + 151-258) on the stored float32 state — ``v`` widened exactly to float64, the
+    dtype the reference keeps it in — after which m, v and the model of every tensor whose global
+    model is float32 are rounded once to float32 (other tensors keep the reference's dtypes).
+    ``state`` is updated in place like FedOptState; returns (model or None, nr_aggregated)."""
+    st = FedOptState()
+    st.m = None if state.m is None else [np.asarray(x) for x in state.m]
+    st.v = None if state.v is None else [np.asarray(x).astype(np.float64) for x in state.v]
+    model, nr = fedopt_combine(st, updates, old, parameters)
+    if model is None:
+        return None, nr
+    f32 = [np.asarray(o).dtype == np.float32 for o in old]
+    rnd = lambda xs: [np.asarray(x).astype(np.float32) if f else x for x, f in zip(xs, f32)]  # noqa: E731
+    state.m, state.v = rnd(st.m), rnd(st.v)
+    return rnd(model), nr
+
+
 # --------------------------------------------------------------------------------------
 # Control.reduce — fedn/network/controller/control.py:648-693
 # --------------------------------------------------------------------------------------

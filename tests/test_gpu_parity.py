@@ -1424,6 +1424,33 @@ def test_p2p_allgather_gloo_hip(world, P, chunk):
             assert np.array_equal(got.view(np.uint32), w.view(np.uint32)), f"rank {rank} step {step}"
 
 
+@pytest.mark.parametrize("ndev,P", [(2, 300_001), (3, 1 << 20)])
+def test_allgather_devices_in_process(ndev, P):
+    """multidev.allgather_devices (the in-process form of the direct all-gather: fa_peer_enable +
+    fa_copy_async per (source, destination) pair on its own stream): each "device" (this box's GPU
+    listed ndev times) folds its slice with the HIP kernel, every device ends with the whole model,
+    bit-identical to the oracle."""
+    from fedn_amd import ops
+    from fedn_amd.multidev import allgather_devices
+    from fedn_amd.sharded import shard_bounds
+    rng = np.random.default_rng(9)
+    K = 5
+    base = rng.standard_normal(P).astype(np.float32)
+    ups = [(base + 0.01 * rng.standard_normal(P)).astype(np.float32) for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
+    parts = []
+    for lo, hi in shard_bounds(P, ndev):
+        agg = torch.empty(hi - lo, device=DEV)
+        ops.fedavg_fold(agg, [torch.from_numpy(u[lo:hi]).to(DEV) for u in ups], ns, Ns, init=True)
+        parts.append((DEV, agg, lo))
+    fulls = allgather_devices(parts, P)
+    want = ref.fedavg_flat(ups, ns)
+    assert len(fulls) == ndev
+    for d, f in enumerate(fulls):
+        assert np.array_equal(f.cpu().numpy().view(np.uint32), want.view(np.uint32)), f"device entry {d}"
+
+
 def test_waves_reject_mismatched_updates():
     """WaveFedOpt refuses updates whose dtype / size differ from the first (a copy into the bf16
     wave slots would otherwise round an fp32 update silently) and misplaced old slices."""

@@ -227,9 +227,12 @@ def test_queued_updates_staged_models_read_ahead(monkeypatch):
     for k in range(40):
         uh.submit([np.zeros(1, np.float32)], 1)
     inner = uh.load_model_update
-    uh.load_model_update = lambda mu, helper: (staged(mu.model_update_id), inner(mu, helper)[1])
+    # the UpdateHandler surface WITHOUT load_model_update_byte: no npz size peek can be issued
+    h = types.SimpleNamespace(model_updates=uh.model_updates, next_model_update=uh.next_model_update,
+                              delete_model=uh.delete_model,
+                              load_model_update=lambda mu, helper: (staged(mu.model_update_id), inner(mu, helper)[1]))
     ahead_seen = []
-    for mu, load in queued_updates(uh, None, ahead=8, ahead_bytes=1 << 30):
+    for mu, load in queued_updates(h, None, ahead=8, ahead_bytes=1 << 30):
         load()
         ahead_seen.append(40 - 1 - len(ahead_seen) - uh.model_updates.qsize())
     assert len(ahead_seen) == 40
