@@ -163,6 +163,16 @@ def load_npz(buf, threads=None):
     return outs
 
 
+def npz_layout(buf):
+    """The flat layout an npz archive decodes into (load_npz_into_layout), from its directory
+    and .npy headers alone — no inflate; CodecError if it cannot be decoded that way."""
+    _, ents = open_archive(buf)
+    ents = _ordered(ents)
+    if any(e.fortran_order for e in ents):
+        raise CodecError("fortran-ordered members cannot be decoded into the flat layout")
+    return Layout([_shape(e) for e in ents], [_dtype(e) for e in ents])
+
+
 def load_npz_into_layout(buf, alloc, threads=None):
     """Decode straight into ONE buffer in the grouped flat layout of layout.py.
 

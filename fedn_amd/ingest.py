@@ -22,7 +22,12 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 import torch
 
+from .budget import HbmBudget
 from .layout import Layout, spread
+
+
+class _HostSide(Exception):
+    """The HBM budget cannot hold this update: leave it host-side (folded through the host path)."""
 
 
 class StagedModel:
@@ -31,7 +36,7 @@ class StagedModel:
     ``host`` returns the update as host arrays (needed only when it is the round's sole
     update, fedavg.py:127-128): the decoded arrays if they were kept, else a D2H copy."""
 
-    __slots__ = ("layout", "dev", "ready", "_host")
+    __slots__ = ("layout", "dev", "ready", "_host", "__weakref__")
 
     def __init__(self, layout, dev, ready, host=None):
         self.layout, self.dev, self.ready, self._host = layout, dev, ready, host
@@ -64,7 +69,7 @@ class ShardedStagedModel:
     of every dtype group, ready once ``ready[d]`` has fired. The multi-device pipelines fold it
     in place; ``host`` reassembles host arrays only when needed (a round's sole update)."""
 
-    __slots__ = ("layout", "devices", "bounds", "dev_off", "bufs", "ready", "_host")
+    __slots__ = ("layout", "devices", "bounds", "dev_off", "bufs", "ready", "_host", "__weakref__")
 
     def __init__(self, layout, devices, bufs, ready, host=None):
         self.layout, self.devices, self.bufs, self.ready, self._host = layout, list(devices), bufs, ready, host
@@ -253,6 +258,9 @@ class StagingUpdateHandler:
     devices  several devices (argument or FEDN_AMD_DEVICES, as the aggregators use): every
              update is staged as parameter slices over them (ShardedStagedModel), each device
              receiving only its slice over its own link, for multidev.py's pipelines
+    hbm_budget  budget.HbmBudget (default: FEDN_AMD_HBM_BUDGET, else 3/4 of the free HBM): an
+             update that would exceed it stays host-side and is loaded by the aggregator through
+             the wrapped handler (decoded then, as FEDn does) — never an OOM, never a dropped client
     Every attribute not defined here (``model_updates``, ``next_model_update``, ``load_model``,
     ``waitforit``, ...) is the wrapped handler's.
     """
@@ -260,9 +268,13 @@ class StagingUpdateHandler:
     stages_on_arrival = True       # aggregatorbase.queued_updates: loads are already done
 
     def __init__(self, inner, helper=None, device=None, workers=4, native_decode=True, devices=None,
-                 max_unclaimed_upload_bytes=16 << 30):
+                 max_unclaimed_upload_bytes=16 << 30, hbm_budget=None):
         from .upload import AdoptedUploads
         self.inner = inner
+        # HBM admission control (budget.py): an update the budget cannot hold is not staged; the
+        # aggregator loads and folds it from the host at its place in the FIFO
+        self.budget = hbm_budget if hbm_budget is not None else HbmBudget()
+        self.host_side = 0              # updates left host-side by the budget (or an HBM OOM)
         self._uploads = AdoptedUploads(max_unclaimed_upload_bytes)
         if devices is None:
             from .aggregators.fedavg import env_devices
@@ -329,12 +341,13 @@ class StagingUpdateHandler:
             training_metadata["round_id"] = config["round_id"]
         return training_metadata
 
-    def _stage_sharded(self, model_update):
+    def _stage_sharded(self, model_update, parts):
         """Stage as parameter slices over the devices — or on the first one alone when the model
         is small (layout.spread: the rule the aggregators apply to pick their pipeline)."""
         decoded = self._decoded_upload(model_update)
         if decoded is not None and hasattr(decoded, "arrays"):
             devs = spread(self.devices, Layout.of(decoded.arrays).nbytes)
+            self._admit(Layout.of(decoded.arrays), devs, parts)
             if len(devs) == 1:
                 with torch.cuda.device(devs[0]):
                     return stage_decoded(decoded, devs[0], self._stream(devs[0])), self._metadata(model_update)
@@ -348,6 +361,8 @@ class StagingUpdateHandler:
             if data is not None:
                 from . import codec
                 try:
+                    lay = codec.npz_layout(data)          # directory only: admit before decoding
+                    self._admit(lay, spread(self.devices, lay.nbytes), parts)
                     layout, pinned = codec.load_npz_into_layout(
                         data, lambda nbytes: torch.empty(nbytes, dtype=torch.uint8, pin_memory=True))
                     return self._stage_packed(layout, pinned), metadata
@@ -356,6 +371,8 @@ class StagingUpdateHandler:
         arrays, metadata = self.inner.load_model_update(model_update, self.helper)
         arrays = [np.asarray(a) for a in arrays]
         layout = Layout.of(arrays)
+        if not parts:
+            self._admit(layout, spread(self.devices, layout.nbytes), parts)
         pinned = torch.empty(layout.nbytes, dtype=torch.uint8, pin_memory=True)
         layout.pack(arrays, pinned.numpy())
         return self._stage_packed(layout, pinned, arrays), metadata
@@ -374,12 +391,50 @@ class StagingUpdateHandler:
         return self.native_decode and helper_kind(self.helper) != "binaryhelper" and \
             hasattr(self.inner, "load_model_update_byte")
 
+    def _admit(self, layout, devs, parts):
+        """Reserve HBM for ``layout`` on ``devs`` (its slices when several) or raise _HostSide."""
+        if len(devs) == 1:
+            want = [(devs[0], layout.nbytes)]
+        else:
+            _, _, dev_bytes = layout.shard_geometry(len(devs))
+            want = list(zip(devs, dev_bytes))
+        if not self.budget.reserve(want):
+            raise _HostSide()
+        parts.extend(want)
+
     def _stage(self, model_update):
+        """Stage one update within the HBM budget: (StagedModel, metadata), or None when it stays
+        host-side (the budget is full, or HBM ran out): load_model_update then takes it from the
+        wrapped handler."""
+        parts = []
+        try:
+            staged, metadata = self._stage_device(model_update, parts)
+        except _HostSide:
+            with self._lock:
+                self.host_side += 1
+            return None
+        except torch.cuda.OutOfMemoryError:
+            self.budget.release(parts)
+            with self._lock:
+                self.host_side += 1
+            return None
+        except BaseException:
+            self.budget.release(parts)
+            raise
+        if parts:
+            self.budget.hold(staged, parts)
+        return staged, metadata
+
+    def _stage_device(self, model_update, parts):
         if self.devices:
-            return self._stage_sharded(model_update)
+            return self._stage_sharded(model_update, parts)
         dev = self._device()
         decoded = self._decoded_upload(model_update)
         if decoded is not None:
+            from .upload import DeviceDecodedUpdate
+            lay = (Layout(decoded.shapes, decoded.dtypes) if isinstance(decoded, DeviceDecodedUpdate)
+                   else Layout.of(decoded.arrays))
+            self._admit(lay, [dev], parts)
             with torch.cuda.device(dev):
                 return stage_decoded(decoded, dev, self._stream()), self._metadata(model_update)
         if self._native():
@@ -390,11 +445,14 @@ class StagingUpdateHandler:
             if data is not None:
                 from . import codec
                 try:
+                    self._admit(codec.npz_layout(data), [dev], parts)   # directory only: before decoding
                     with torch.cuda.device(dev):
                         return stage_npz(data, dev, self._stream()), metadata
                 except codec.CodecError:
                     pass     # e.g. Fortran-ordered members: decode through the helper (np.load) below
         arrays, metadata = self.inner.load_model_update(model_update, self.helper)
+        if not parts:
+            self._admit(Layout.of([np.asarray(a) for a in arrays]), [dev], parts)
         with torch.cuda.device(dev):
             return stage_arrays(arrays, dev, self._stream()), metadata
 
@@ -421,7 +479,10 @@ class StagingUpdateHandler:
             fut = self._staged.pop(model_update.model_update_id, None)
         if fut is None:                       # arrived before the wrapper was installed
             return self.inner.load_model_update(model_update, helper)
-        return fut.result()
+        res = fut.result()
+        if res is None:                       # left host-side by the HBM budget: FEDn's own load
+            return self.inner.load_model_update(model_update, helper)
+        return res
 
     def delete_model(self, model_update):
         with self._lock:

@@ -481,3 +481,31 @@ def test_narrow_int_fold_kinds():
     assert not mixed.per_tensor_dtypes([np.float32, np.int64, np.float16])
     plan = mixed.fold_plan([((5,), np.dtype(np.int8))], [((1,), np.dtype(np.int16))], 9, 13)
     assert plan == [(np.dtype(np.int16), np.dtype(np.float64), (5,))]
+
+
+def test_hbm_budget_accounting():
+    """budget.HbmBudget: all-or-nothing reservations per device, release on garbage collection of
+    the staged object, byte-count parsing (no GPU needed with an explicit limit)."""
+    import gc
+
+    from fedn_amd.budget import HbmBudget, parse_bytes
+    assert parse_bytes("0") == 0 and parse_bytes("512") == 512 and parse_bytes("4K") == 4096
+    assert parse_bytes("1.5G") == 3 << 29 and parse_bytes("2GiB") == 2 << 30 and parse_bytes("1T") == 1 << 40
+    with pytest.raises(ValueError):
+        parse_bytes("lots")
+    b = HbmBudget(limit=1000)
+    assert b.reserve([("cuda:0", 600)])
+    assert not b.reserve([("cuda:0", 500)])                 # over the cap: refused, nothing taken
+    assert b.reserve([("cuda:1", 900)])                     # devices are budgeted separately
+    assert not b.reserve([("cuda:0", 100), ("cuda:1", 200)])   # all or nothing
+    assert b.used("cuda:0") == 600 and b.used("cuda:1") == 900 and b.refused == 2
+
+    class Staged:
+        pass
+
+    s = b.hold(Staged(), [("cuda:0", 600)])
+    del s
+    gc.collect()
+    assert b.used("cuda:0") == 0
+    b.release([("cuda:1", 900)])
+    assert b.used("cuda:1") == 0

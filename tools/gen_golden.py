@@ -22,7 +22,8 @@ pull in opentelemetry (not installed). We pre-register a bare ``fedn`` package a
 run from control.py's own source without importing its module (which needs the absent
 ``tenacity``): see ``_control_reduce``.
 
-Usage:  python tools/gen_golden.py            (writes tests/golden/*.npz + manifest.json)
+Usage:  python tools/gen_golden.py            (writes tests/golden/*.npz + manifest.json: every fixture)
+        python tools/gen_golden.py --out DIR  (the same into DIR; tools/verify_golden.py diffs it)
 """
 import io
 import json
@@ -754,7 +755,10 @@ def reduce_cases(ref):
 
 
 def main():
+    global OUT
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
+    if "--out" in sys.argv:          # tools/verify_golden.py regenerates into a scratch directory
+        OUT = sys.argv[sys.argv.index("--out") + 1]
     ref = _import_reference()
     os.makedirs(OUT, exist_ok=True)
     if only == "sf":      # regenerate just these fixtures; the others stay byte-identical
@@ -826,6 +830,7 @@ def main():
     cases += edge_cases(ref)
     cases += numex_cases(ref)
     cases += f16_fedopt_cases(ref)
+    cases += narrow_cases(ref)
     _write(cases, merge=False)
 
 
