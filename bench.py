@@ -206,6 +206,26 @@ def fedopt_waves_side(a, devs, sample=1_000_000):
     t0 = time.perf_counter()
     outs = wf.round(ups, ns, old, params)
     t = time.perf_counter() - t0
+    # per-kernel rooflines: the same round again with HIP events around every launch (round 1 of a
+    # session: FINAL reads old + pg, writes m / v / out; waves read 8 bf16 updates + f64 old and
+    # write the f64 pg workspace, later waves also read it)
+    spans = {}
+    WaveFedOpt(devs, P, wave=8).round(ups, ns, old, params, kernel_times=spans)
+    per_el = {"first": lambda k: 2 * k + 16, "mid": lambda k: 2 * k + 24, "final": lambda k: 40}
+    kern = {}
+    for kind, rows in spans.items():
+        ms = sum(r[3] for r in rows) / len(rows)
+        b = sum(r[1] * per_el[kind](r[2]) for r in rows) / len(rows)
+        traffic, tsrc = pmc_traffic(f"fedyogi_wave_{kind}_p{P // len(devs)}_w8_bf16")
+        kern[kind] = {"launches": len(rows), "ms": ms, "alg_bytes_per_launch": b,
+                      "roofline": {"bound": "hbm", "achieved": b / ms / 1e6, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": b / ms / 1e6 / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc},
+                      "kernel": {"first": "k_fedopt_c<bf16, double, CF64, FIRST, !FINAL>",
+                                 "mid": "k_fedopt_c<bf16, double, CF64, !FIRST, !FINAL>",
+                                 "final": "k_fedopt_c<bf16, double, CF64, !FIRST, FINAL> (K = 0 server step)"}[kind],
+                      "bytes_per_element": {"first": "2W + 16 (W bf16 updates, f64 old, f64 pg written)",
+                                            "mid": "2W + 24 (W bf16 updates, f64 old, f64 pg read + written)",
+                                            "final": "40 (f64 old + pg read; f64 m / v / out written)"}[kind]}
     res = wf.gather(outs)
     S = min(sample, P)
     want, _ = ref.fedopt_combine(ref.FedOptState(), [([ups[k][:S].float().numpy()], n) for k, n in enumerate(ns)],
@@ -216,7 +236,7 @@ def fedopt_waves_side(a, devs, sample=1_000_000):
     torch.cuda.empty_cache()
     return {"s": t, "value": K * P / t, "unit": "params/s", "params": P, "clients": K, "wave": 8, "devices": len(devs),
             "h2d_GBps_total": K * P * 2 / t / 1e9, "h2d_GBps_per_link": K * P * 2 / t / 1e9 / len(devs),
-            "checksum_sha256_16": checksum, "bit_exact_on_sample": exact,
+            "checksum_sha256_16": checksum, "bit_exact_on_sample": exact, "kernels": kern,
             "sample": f"first {S} params vs oracle/numpy_ref.fedopt_combine on the f32 upcasts",
             "note": f"BASELINE configs[4]: {pool} distinct pinned bf16 updates reused cyclically (every one "
                     "crosses PCIe); PCIe-bound by design; not in value"}

@@ -67,9 +67,12 @@ class DeviceSink:
     the whole update, and the H2D runs while later chunks are still arriving. ``finish()``
     records the event that the last copy fired."""
 
-    def __init__(self, device, stream, slot=8 << 20, ring=4):
+    def __init__(self, device, stream, slot=8 << 20, ring=4, budget=None):
         import torch
         self.torch, self.device, self.stream, self.slot = torch, device, stream, slot
+        # HBM admission (budget.HbmBudget of the staging handler): a member the budget cannot hold
+        # ends this decode, and the update takes the normal path (staged or left host-side there)
+        self.budget, self.reserved = budget, 0
         self.ring = [torch.empty(slot, dtype=torch.uint8, pin_memory=True) for _ in range(ring)]
         self.addr = [t.data_ptr() for t in self.ring]
         self.events = [None] * ring
@@ -77,7 +80,12 @@ class DeviceSink:
         self.cur, self.cur_off = None, 0
 
     def open(self, nbytes):
-        return self.torch.empty(max(nbytes, 1), dtype=self.torch.uint8, device=self.device)
+        n = max(nbytes, 1)
+        if self.budget is not None:
+            if not self.budget.reserve([(self.device, n)]):
+                raise MemoryError("HBM budget full: the upload is not decoded into HBM")
+            self.reserved += n
+        return self.torch.empty(n, dtype=self.torch.uint8, device=self.device)
 
     def window(self, blk, offset):
         if self.fill and (self.cur is not blk or self.cur_off + self.fill != offset):
@@ -232,7 +240,7 @@ class DeviceDecodedUpdate:
     """An update decoded during its upload straight into HBM (:class:`DeviceSink`): one
     device block (uint8) per tensor in FEDn's key order, valid once ``ready`` has fired."""
 
-    __slots__ = ("shapes", "dtypes", "blocks", "ready", "device", "nbytes")
+    __slots__ = ("shapes", "dtypes", "blocks", "ready", "device", "nbytes", "__weakref__")
 
     def __init__(self, members, ready, device):
         members = _ordered(members)
@@ -304,9 +312,11 @@ class StreamingUpload:
     def _decode(self, q, fut, device, stop):
         keep = []
         ended = False
+        sink = None
+        budget = getattr(self.handler, "budget", None)
         try:
             if device is not None:
-                sink = DeviceSink(device, self._stream(device), self.slot, self.ring)
+                sink = DeviceSink(device, self._stream(device), self.slot, self.ring, budget)
             else:
                 sink = HostSink(self._alloc(keep))
             dec = NpzStreamDecoder(sink=sink)
@@ -322,9 +332,18 @@ class StreamingUpload:
                 raise RuntimeError("decode abandoned: the upload outpaced the decoder")
             members = dec.finish()
             ready = sink.finish()
-            fut.set_result(DeviceDecodedUpdate(members, ready, device) if device is not None
-                           else DecodedUpdate(members, keep))
+            if device is not None:
+                upd = DeviceDecodedUpdate(members, ready, device)
+                if sink.reserved:
+                    budget.hold(upd, [(device, sink.reserved)])      # returned when the decode is dropped
+                    sink.reserved = 0
+                fut.set_result(upd)
+            else:
+                fut.set_result(DecodedUpdate(members, keep))
         except Exception as e:  # noqa: BLE001 — not adopted: the update takes the normal path
+            if isinstance(sink, DeviceSink) and sink.reserved:
+                budget.release([(device, sink.reserved)])
+                sink.reserved = 0
             keep.clear()
             fut.set_exception(e)
             while not ended:                           # drain to the end of the upload

@@ -35,11 +35,14 @@ class WaveFedOpt:
         self.copy = [torch.cuda.Stream(d) for d in self.devices]
         self.compute = [torch.cuda.current_stream(d) for d in self.devices]
 
-    def round(self, host_updates, ns, old, params):
+    def round(self, host_updates, ns, old, params, kernel_times=None):
         """One aggregation round: ``host_updates`` = K flat CPU tensors (pinned for full-rate
         H2D) in FIFO order, ``ns`` their num_examples, ``old`` the global model as one flat
         tensor per device slice (``old[d]`` on device d, any dtype fa_fedopt_step takes).
-        Returns the new model as per-device f64 slices; m / v stay on the devices."""
+        Returns the new model as per-device f64 slices; m / v stay on the devices.
+        ``kernel_times``: a dict to receive, per launch kind ("first" wave, later "mid" waves, the
+        "final" server step), the list of (device, elements, clients, ms) of every launch (HIP
+        events on the launch stream) — bench.py's per-kernel rooflines."""
         K = len(host_updates)
         if K == 0:
             raise ValueError("no updates")
@@ -83,8 +86,10 @@ class WaveFedOpt:
                             c["slots"][b][j].copy_(host_updates[k][lo:hi], non_blocking=True)
                         c["loaded"][b].record(self.copy[d])
                     self.compute[d].wait_event(c["loaded"][b])
+                    ev = self._span(kernel_times, d)
                     ops.fedopt_step(old[d], c["slots"][b][:len(ks)], [ns[k] for k in ks], [Ns[k] for k in ks],
                                     first=(w == 0), final=False, pg=c["pg"], stream=self.compute[d])
+                    self._end(kernel_times, "first" if w == 0 else "mid", d, ev, c["n"], len(ks))
                     c["used"][b].record(self.compute[d])
         for d, dv in enumerate(self.devices):
             c = ctx[d]
@@ -93,16 +98,35 @@ class WaveFedOpt:
                 v_out = self.v[d] if self.v[d] is not None else torch.empty(c["n"], dtype=torch.float64, device=dv)
                 out = torch.empty(c["n"], dtype=torch.float64, device=dv)
                 if c["n"]:
+                    ev = self._span(kernel_times, d)
                     ops.fedopt_step(old[d], [], [], [], first=False, final=True, pg=c["pg"], m_in=self.m[d], m_out=m_out,
                                     v_in=self.v[d], v_out=v_out, out=out, serveropt=params.get("serveropt", "adam"),
                                     learning_rate=params.get("learning_rate", 1e-3), beta1=params.get("beta1", 0.9),
                                     beta2=params.get("beta2", 0.99), tau=params.get("tau", 1e-4),
                                     stream=self.compute[d], upd_dtype=upd_dt)
+                    self._end(kernel_times, "final", d, ev, c["n"], 0)
                 self.m[d], self.v[d] = m_out, v_out
                 outs.append(out)
         for d, dv in enumerate(self.devices):
             torch.cuda.synchronize(dv)
+        if kernel_times is not None:
+            for kind, spans in list(kernel_times.items()):
+                kernel_times[kind] = [(d, n, k, a.elapsed_time(b)) for d, n, k, a, b in spans]
         return outs
+
+    def _span(self, kernel_times, d):
+        if kernel_times is None:
+            return None
+        a = torch.cuda.Event(enable_timing=True)
+        a.record(self.compute[d])
+        return a
+
+    def _end(self, kernel_times, kind, d, a, n, k):
+        if kernel_times is None:
+            return
+        b = torch.cuda.Event(enable_timing=True)
+        b.record(self.compute[d])
+        kernel_times.setdefault(kind, []).append((d, n, k, a, b))
 
     def slices(self, flat):
         """``flat`` (a host or device tensor of P elements) cut into per-device slices on their devices."""

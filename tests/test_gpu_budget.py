@@ -127,3 +127,36 @@ def test_staging_oom_falls_back_to_host(monkeypatch):
     assert data["nr_aggregated_models"] == 12 and st.host_side == 4
     assert_lists_identical(model, want, "oom fallback")
     st.close()
+
+
+def test_budget_streaming_upload_k20():
+    """Decode-while-uploading under a budget of ~2.5 updates: uploads the budget cannot hold are not
+    decoded into HBM (DeviceSink refuses), stagings beyond it stay host-side; 20 updates, all folded,
+    bit-exact; the budget is empty again once the round's objects are gone."""
+    import gc
+
+    from fedn_amd.updatehandler import MemoryModelService, upload_requests
+    from fedn_amd.upload import StreamingUpload
+    rng = np.random.default_rng(35)
+    base = [rng.standard_normal(s).astype(np.float32) for s in SHAPES]
+    budget = HbmBudget(limit=int(2.5 * Layout.of(base).nbytes))
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=Helper(), device=DEV, workers=2, hbm_budget=budget)
+    svc = StreamingUpload(MemoryModelService(uh.store), st, workers=2, slot=65536, ring=2)
+    ups = []
+    for k in range(20):
+        arrays = [(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base]
+        n = int(rng.integers(1, 5001))
+        svc.Upload(upload_requests(_npz(arrays), f"B{k}", chunk=40_000), None)
+        uh.submit_uploaded(f"B{k}", n, via=st)
+        ups.append((arrays, n))
+    model, data = get_aggregator("fedavg", st).combine_models(helper=Helper())
+    svc.close()
+    want, nr = ref.fedavg_combine(ups)
+    assert data["nr_aggregated_models"] == nr == 20
+    assert_lists_identical(model, want, "upload under budget")
+    assert st.host_side > 0 and budget.refused > 0
+    del model
+    st.close()
+    gc.collect()
+    assert budget.used(DEV) == 0

@@ -92,6 +92,18 @@ for s in $STEPS; do
         done
       done
       echo "pmc: now run  python tools/pmc_traffic.py --session $OUT  in the build container" ;;
+    pmcx)
+      # PMC traffic of the workloads that need a process of their own (tools/pmc_workloads.py): the
+      # fp32-state FedOpt step and configs[4]'s three wave kernels
+      sha256sum fedn_amd/libfedagg.so | cut -c1-16 > "$OUT/lib_sha.txt"
+      for wl in f32state waves; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+          cd /tmp && timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmcx_$wl/pmc_$c" -o run -- \
+            python3 "$GRAFT_REPO_ROOT/tools/pmc_workloads.py" $wl --steps 3 > "$GRAFT_REPO_ROOT/$OUT/pmcx_${wl}_$c.log" 2>&1; rc=$?
+          cd "$GRAFT_REPO_ROOT"; echo "pmcx $wl $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+        done
+      done
+      echo "pmcx: now run  python tools/pmc_traffic.py --x-session $OUT  in the build container" ;;
     pmcrank)
       # HBM traffic of one rank's fold at N = 2, 4, 8 for every fold + all-gather round count bench.py may
       # choose (AG_ROUNDS; bench.py's N > 1 roofline), replayed on this GPU

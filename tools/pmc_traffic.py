@@ -40,7 +40,10 @@ def lib_sha(session=None):
 
 
 def per_launch(path, kernel):
-    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+    """Average counter value per dispatch of the kernels whose name contains ``kernel`` (a string, or
+    a tuple of strings that must all appear)."""
+    parts = (kernel,) if isinstance(kernel, str) else tuple(kernel)
+    rows = [r for r in csv.DictReader(open(path)) if all(p in r["Kernel_Name"] for p in parts)]
     if not rows:
         raise SystemExit(f"no dispatch of {kernel!r} in {path}")
     vals = [float(r["Counter_Value"]) for r in rows]
@@ -72,6 +75,16 @@ SESSION = [
     ("pmc1", f"fedopt_adam_steady_k32_p{Q}", "k_fedopt_c<float, double", Q * (4 * 32 + 48)),
     ("pmc2", f"fedavg_k8_p{P}_f32", "k_fedavg_pipe<float, float", 8 * P * 4 + P * 4),
     ("pmc3", f"fedavg_k64_p{P}_bf16", "bf16, float", 64 * P * 2 + P * 4),
+]
+
+
+# tools/pmc_workloads.py runs (tools/gpu_session.sh step "pmcx"): (subdir, key, kernel, algorithmic bytes)
+WAVE_BF16 = "k_fedopt_c<(anonymous namespace)::bf16, double, (anonymous namespace)::CF64, "
+X_SESSION = [
+    ("pmcx_f32state", f"fedopt_adam_steady_f32state_k32_p{Q}", "k_fedopt_c<float, float", Q * (4 * 32 + 24)),
+    ("pmcx_waves", "fedyogi_wave_first_p1000000000_w8_bf16", (WAVE_BF16 + "true, false,",), 1_000_000_000 * (2 * 8 + 16)),
+    ("pmcx_waves", "fedyogi_wave_mid_p1000000000_w8_bf16", (WAVE_BF16 + "false, false,",), 1_000_000_000 * (2 * 8 + 24)),
+    ("pmcx_waves", "fedyogi_wave_final_p1000000000_w8_bf16", (WAVE_BF16 + "false, true,",), 1_000_000_000 * 40),
 ]
 
 
@@ -110,6 +123,10 @@ def main():
                     record_rank(sys.argv[2], world, R, sub)
             if os.path.isdir(os.path.join(sys.argv[2], f"pmcrank{world}")):   # round-2 sessions: R = 8 only
                 record_rank(sys.argv[2], world)
+        return
+    if sys.argv[1] == "--x-session":
+        for sub, key, kernel, alg in X_SESSION:
+            record(os.path.join(sys.argv[2], sub), key, kernel, alg, session=sys.argv[2])
         return
     if sys.argv[1] == "--session":
         for sub, key, kernel, alg in SESSION:
