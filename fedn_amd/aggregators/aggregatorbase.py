@@ -11,6 +11,7 @@ import importlib
 import io
 import os
 import threading
+import time
 import zipfile
 from abc import ABC, abstractmethod
 from collections import deque
@@ -23,6 +24,9 @@ AGGREGATOR_PLUGIN_PATH = "fedn_amd.aggregators.{}"
 LOAD_AHEAD = int(os.environ.get("FEDN_AMD_LOAD_AHEAD", "8"))
 # host bytes of decoded-but-not-yet-folded updates the read-ahead may hold (FEDn holds one)
 LOAD_AHEAD_BYTES = int(os.environ.get("FEDN_AMD_LOAD_AHEAD_BYTES", str(4 << 30)))
+# loads faster than this (mean over the last round: in-memory handlers, tiny models) are not worth a
+# thread hand-off each; the next round then drains its queue on the calling thread
+CHEAP_LOAD_S = float(os.environ.get("FEDN_AMD_CHEAP_LOAD_S", "100e-6"))
 
 
 _pools = {}
@@ -91,9 +95,11 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
     more than ``ahead_bytes`` of decoded updates (one at least), counting the one being folded. A handler that stages updates
     on arrival (ingest.StagingUpdateHandler) is drained one by one: its loads are already done.
 
-    ``size_box``: a one-element list the caller keeps across rounds (the aggregator instance
-    does): it holds the decoded size of the last update seen, so a later round admits its read-
-    ahead at once instead of decoding its first update alone.
+    ``size_box``: a list the caller keeps across rounds (the aggregator instance does): [0] holds
+    the decoded size of the last update seen, so a later round admits its read-ahead at once
+    instead of decoding its first update alone; [1] the mean time of one load last round — when it
+    is below CHEAP_LOAD_S (an in-memory handler, a tiny model) the round is drained on the calling
+    thread, as the thread hand-off would cost more than the load.
 
     Lossless: if the caller stops early (an exception that escapes its per-update handling,
     e.g. a BaseException, or ``close()``), the updates dequeued ahead but not yet handed out go
@@ -102,19 +108,35 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
     ahead = LOAD_AHEAD if ahead is None else ahead
     ahead_bytes = LOAD_AHEAD_BYTES if ahead_bytes is None else ahead_bytes
     q = update_handler.model_updates
-    if ahead <= 1 or getattr(update_handler, "stages_on_arrival", False):
-        while not q.empty():
-            try:
-                mu = update_handler.next_model_update()
-            except Exception as e:  # noqa: BLE001 — raised inside the caller's try, as FEDn's loop
-                yield None, _raiser(e)
-                continue
-            yield mu, (lambda mu=mu: update_handler.load_model_update(mu, helper))
+    size = size_box if size_box is not None else [None]   # bytes of one decoded update, once known
+    if len(size) < 2:
+        size.append(None)
+    load_times = []                       # this round's loads (s): [1] of the box for the next round
+
+    def timed_load(mu):
+        t0 = time.perf_counter()
+        try:
+            return update_handler.load_model_update(mu, helper)
+        finally:
+            load_times.append(time.perf_counter() - t0)
+
+    cheap = size[1] is not None and size[1] < CHEAP_LOAD_S
+    if ahead <= 1 or cheap or getattr(update_handler, "stages_on_arrival", False):
+        try:
+            while not q.empty():
+                try:
+                    mu = update_handler.next_model_update()
+                except Exception as e:  # noqa: BLE001 — raised inside the caller's try, as FEDn's loop
+                    yield None, _raiser(e)
+                    continue
+                yield mu, (lambda mu=mu: timed_load(mu))
+        finally:
+            if load_times:
+                size[1] = sum(load_times) / len(load_times)
         return
     pool = _load_pool(ahead)
     window = deque()
     issued = []                           # loads submitted this round and not finished
-    size = size_box if size_box is not None else [None]   # bytes of one decoded update, once known
     # with no size yet, the first update's raw bytes (UpdateHandler.load_model_update_byte,
     # updatehandler.py:119-144) show it from the npz directory before its decode ends
     known = threading.Event()
@@ -129,7 +151,7 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
         except Exception:  # noqa: BLE001 — no raw bytes: the first decode shows the size
             pass
         known.set()
-        return update_handler.load_model_update(mu, helper)
+        return timed_load(mu)
 
     def allowed():
         if size[0] is None:
@@ -149,7 +171,7 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
                 peeking[0] = True
                 fut = pool.submit(peek_then_load, mu)
             else:
-                fut = pool.submit(update_handler.load_model_update, mu, helper)
+                fut = pool.submit(timed_load, mu)
             issued[:] = [f for f in issued if not f.done()]   # done loads: their arrays are the caller's
             issued.append(fut)
             window.append((mu, fut, None))
@@ -183,6 +205,8 @@ def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_bo
         window.clear()
         wait_futures([f for f in issued if not f.cancelled()])   # no load of this round outlives it
         requeue_front(q, back)
+        if load_times:
+            size[1] = sum(load_times) / len(load_times)
 
 
 class AggregatorBase(ABC):
@@ -192,7 +216,7 @@ class AggregatorBase(ABC):
     def __init__(self, update_handler):
         self.name = self.__class__.__name__
         self.update_handler = update_handler
-        self._ahead_size = [None]        # decoded update size seen last round (queued_updates)
+        self._ahead_size = [None, None]  # last round's decoded update size and mean load time (queued_updates)
 
     @abstractmethod
     def combine_models(self, helper=None, delete_models=True, parameters=None):

@@ -38,6 +38,27 @@ def _native_gather(jobs):
     return True
 
 
+def run_pack_jobs(jobs):
+    """Run (destination view, flat source) copies: inline below PACK_MIN_PARALLEL bytes in total,
+    else in >= 1 MiB pieces on the native gather's threads (the Python pool if the codec library
+    is not built)."""
+    total = sum(d.nbytes for d, _ in jobs)
+    if PACK_THREADS <= 1 or total < PACK_MIN_PARALLEL:
+        for d, src in jobs:
+            np.copyto(d, src, casting="no")
+        return
+    if _native_gather(jobs):
+        return
+    piece = max(1 << 20, min(PACK_CHUNK, -(-total // PACK_THREADS)))
+    futs = []
+    for d, src in jobs:
+        step = max(1, piece // src.itemsize)
+        for i in range(0, src.size, step):
+            futs.append(_executor().submit(np.copyto, d[i:i + step], src[i:i + step], casting="no"))
+    for f in futs:
+        f.result()
+
+
 def _executor():
     global _pool
     if _pool is None or _pool[0] != os.getpid():     # a forked child starts its own pool
@@ -166,6 +187,11 @@ class Layout:
         for a small update; otherwise every tensor is cut into pieces (>= 1 MiB, at most
         PACK_CHUNK, ~1 per pack thread over the whole update) copied by the pack threads, so a
         model of many mid-size tensors is packed in parallel, not one tensor at a time."""
+        run_pack_jobs(self.pack_jobs(arrays, buf_np_u8))
+
+    def pack_jobs(self, arrays, buf_np_u8):
+        """The (destination view, flat source) copies of :meth:`pack`, not run yet (a caller that
+        packs many small updates runs them together: :func:`run_pack_jobs`)."""
         jobs = []
         for dt in self.groups:
             g = self.group_view(buf_np_u8, dt)
@@ -173,21 +199,7 @@ class Layout:
                 sz = self.sizes[i]
                 if sz:
                     jobs.append((g[off:off + sz], np.ascontiguousarray(arrays[i]).reshape(-1)))
-        total = sum(d.nbytes for d, _ in jobs)
-        if PACK_THREADS <= 1 or total < PACK_MIN_PARALLEL:
-            for d, src in jobs:
-                np.copyto(d, src, casting="no")
-            return
-        if _native_gather(jobs):
-            return
-        piece = max(1 << 20, min(PACK_CHUNK, -(-total // PACK_THREADS)))
-        futs = []
-        for d, src in jobs:
-            step = max(1, piece // src.itemsize)
-            for i in range(0, src.size, step):
-                futs.append(_executor().submit(np.copyto, d[i:i + step], src[i:i + step], casting="no"))
-        for f in futs:
-            f.result()
+        return jobs
 
     def unpack_group(self, flat, dt, out, copy=True):
         """Scatter a group's flat host array back into per-tensor arrays. With copy=False

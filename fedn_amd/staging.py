@@ -27,7 +27,7 @@ import torch
 
 from . import mixed, ops
 from .ingest import StagedModel
-from .layout import Layout, parallel_copy
+from .layout import Layout, parallel_copy, run_pack_jobs
 
 
 BATCH = 64                    # device-resident updates folded per launch (the kernarg client table)
@@ -177,6 +177,8 @@ class _Pipeline:
         # allocated for a single update and never reused)
         self.batch_host = batch and layout.nbytes <= SMALL_UPDATE_BYTES
         self._arenas, self._arena, self._arena_i = (kept["arenas"] if kept else []), None, 0
+        self._pack_jobs = []                     # deferred copies into the arena being filled
+        self._d2h_on_compute = False             # a small result was copied back on the compute stream
         self.streamer = kept["streamer"] if kept else HostStreamer()
 
     def release(self):
@@ -233,7 +235,9 @@ class _Pipeline:
             self._arena = a
         nb, j = self.layout.nbytes, a.count
         tic = time.perf_counter()
-        self.layout.pack(arrays, a.host_np[j * nb:(j + 1) * nb])
+        # the copies run together when the arena is uploaded (one native call, all pack threads):
+        # per update only the jobs are recorded (the source arrays stay referenced until then)
+        self._pack_jobs.extend(self.layout.pack_jobs(arrays, a.host_np[j * nb:(j + 1) * nb]))
         self.time_pack += time.perf_counter() - tic
         a.count += 1
         return _ArenaRef(a.dev[j * nb:(j + 1) * nb])
@@ -247,6 +251,10 @@ class _Pipeline:
         a = self._arena
         if a is None or a.count == 0:
             return
+        tic = time.perf_counter()
+        jobs, self._pack_jobs = self._pack_jobs, []
+        run_pack_jobs(jobs)
+        self.time_pack += time.perf_counter() - tic
         n = a.count * self.layout.nbytes
         start = torch.cuda.Event(enable_timing=True)
         a.done = torch.cuda.Event(enable_timing=True)
@@ -332,6 +340,16 @@ class _Pipeline:
         The caller synchronises the d2h stream."""
         n = src.numel()
         host = torch.empty(n, dtype=src.dtype, pin_memory=True)
+        if n * src.element_size() <= SMALL_UPDATE_BYTES:
+            # one chunk: launch and D2H in order on the compute stream (no cross-stream hand-off);
+            # the caller synchronises the compute stream too
+            if prepare is not None:
+                prepare(0, n)
+            fold_chunk(0, n)
+            with torch.cuda.stream(self.compute):
+                host.copy_(src, non_blocking=True)
+            self._d2h_on_compute = True
+            return host
         for lo, hi in chunks(n, src.element_size()):
             if prepare is not None:
                 prepare(lo, hi)
@@ -371,8 +389,15 @@ class FedAvgPipeline(_Pipeline):
         super().__init__(device, first_arrays.layout if staged else Layout.of(first_arrays), nslots, slots, streams,
                          cache, batch)
         self.first_arrays = first_arrays         # a StagedModel materialises host arrays only if needed
-        self.first = self.acquire(first_arrays) if staged else self.stage(first_arrays)
-        if not staged:
+        if staged:
+            self.first = self.acquire(first_arrays)
+        elif self.batch_host:
+            # a small model: the first update rides in the arena with the round's other updates
+            # (one H2D, everything on the compute stream)
+            self.layout.check(first_arrays)
+            self.first = self.put_small(first_arrays)
+        else:
+            self.first = self.stage(first_arrays)
             self.first.reserved = True
         self.nfolds = 0
         self.agg_started = False                 # agg holds a fold of the first update
@@ -473,8 +498,8 @@ class FedAvgPipeline(_Pipeline):
         self._folded()
 
     def _flush(self):
+        self.upload_arena()                     # also the first update, when it waits in the arena
         if self.pending:
-            self.upload_arena()
             entries, self.pending = self.pending, []
             self._fold_all(entries)
 
@@ -502,6 +527,8 @@ class FedAvgPipeline(_Pipeline):
         if entries:
             self._folded()
         self.d2h.synchronize()
+        if self._d2h_on_compute:
+            self.compute.synchronize()
         self.time_d2h += time.perf_counter() - tic
         out = [None] * len(self.layout.shapes)
         for dt in self.layout.groups:
@@ -886,6 +913,8 @@ class FedOptPipeline(_Pipeline):
         self._end_span(span)
         self.pg_started = True
         self.d2h.synchronize()
+        if self._d2h_on_compute:
+            self.compute.synchronize()
         self.time_d2h += time.perf_counter() - tic
         state.m, state.v, state.signature, state.layout = new_m, new_v, sig, self.layout
         model = [None] * len(self.layout.shapes)
