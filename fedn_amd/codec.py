@@ -19,7 +19,7 @@ from .layout import Layout
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfednpz.so")
 MAX_DIMS = 16
-FNPZ_ABI_VERSION = 2    # include/fednpz.h
+FNPZ_ABI_VERSION = 3    # include/fednpz.h
 THREADS = int(os.environ.get("FEDN_AMD_CODEC_THREADS", str(min(16, os.cpu_count() or 1))))
 
 
@@ -75,6 +75,9 @@ def load_lib():
                                                  ctypes.POINTER(ctypes.c_int64)]
                 lib.fnpz_gather.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+                lib.fnpz_gather_start.restype = ctypes.c_int64
+                lib.fnpz_gather_start.argtypes = lib.fnpz_gather.argtypes
+                lib.fnpz_gather_wait.argtypes = [ctypes.c_int64]
             except AttributeError as e:      # a symbol include/fednpz.h declares is missing
                 raise ImportError(f"{LIB_PATH}: {e}; rebuild it (python -m fedn_amd.build)") from e
             _lib = lib
@@ -84,6 +87,43 @@ def load_lib():
 def _check(rc):
     if rc:
         raise CodecError(f"fednpz status {rc}: {load_lib().fnpz_last_error().decode(errors='replace')}")
+
+
+def _ptrs(pairs):
+    n = len(pairs)
+    dsts, srcs, nb = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)(), (ctypes.c_int64 * n)()
+    for i, (d, src) in enumerate(pairs):
+        if d.nbytes != src.nbytes:
+            raise ValueError("gather: destination and source sizes differ")
+        dsts[i] = d.__array_interface__["data"][0]
+        srcs[i] = src.__array_interface__["data"][0]
+        nb[i] = d.nbytes
+    return n, dsts, srcs, nb
+
+
+def gather_start(pairs, threads):
+    """``dst[:] = src`` for each (dst, src) pair of C-contiguous numpy arrays, queued to the native
+    gather thread (``fnpz_gather_start``); returns the ticket for :func:`gather_wait`. The caller
+    keeps every array alive until then."""
+    lib = load_lib()
+    t = lib.fnpz_gather_start(*_ptrs(pairs), max(1, threads))
+    if t < 0:
+        _check(-t)
+    return t
+
+
+def gather_start_raw(dsts, srcs, nbytes, threads):
+    """:func:`gather_start` on plain addresses and byte counts (lists of ints)."""
+    n = len(dsts)
+    t = load_lib().fnpz_gather_start(n, (ctypes.c_void_p * n)(*dsts), (ctypes.c_void_p * n)(*srcs),
+                                     (ctypes.c_int64 * n)(*nbytes), max(1, threads))
+    if t < 0:
+        _check(-t)
+    return t
+
+
+def gather_wait(ticket):
+    _check(load_lib().fnpz_gather_wait(ticket))
 
 
 def gather(pairs, threads):

@@ -1178,14 +1178,16 @@ k_elementwise(int op, TO* __restrict__ out, const TX* __restrict__ x, const TY* 
 // exponentiation by squaring in the array's integer type (wrapping products).
 template <typename T>
 __global__ void __launch_bounds__(kBlock) k_ipow(T* __restrict__ out, const T* __restrict__ x, uint64_t e, int64_t P) {
+    // products in uint64 (no signed overflow, no promotion of 8/16-bit operands to int): x**e mod
+    // 2**64 taken mod 2**bits(T) is numpy's wrapped result in T
     using U = typename std::make_unsigned<T>::type;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < P; i += (int64_t)gridDim.x * kBlock) {
-        U base = (U)x[i], r = 1;
+        uint64_t base = (uint64_t)(U)x[i], r = 1;
         for (uint64_t k = e; k; k >>= 1) {
             if (k & 1) r *= base;
             base *= base;
         }
-        out[i] = (T)r;
+        out[i] = (T)(U)r;
     }
 }
 
@@ -1299,6 +1301,10 @@ k_cast(TO* __restrict__ out, const TI* __restrict__ in, const CastGeom g, const 
         }
         if constexpr (std::is_same<TO, f16>::value && std::is_integral<TI>::value)
             out[i] = f16{f32_to_f16((float)in[j])};          // int8 / uint8 only: exact in half
+        else if constexpr (std::is_same<TO, f16>::value && std::is_same<TI, float>::value)
+            out[i] = f16{f32_to_f16(in[j])};                 // narrowing: round to nearest even (astype)
+        else if constexpr (std::is_same<TO, float>::value && std::is_same<TI, double>::value)
+            out[i] = (float)in[j];                           // narrowing: round to nearest even (astype)
         else
             out[i] = widen<TI, TO>(in[j]);
     }
@@ -1897,19 +1903,29 @@ int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype,
     if (op == FA_EW_AXPBY && !y) return fail(FA_EINVAL, "fa_elementwise: AXPBY needs y");
     if (P == 0) return FA_OK;
     if (op == FA_EW_IPOW) {
-        if (out_dtype != x_dtype || (x_dtype != FA_I32 && x_dtype != FA_I64))
-            return fail(FA_EDTYPE, "fa_elementwise: IPOW takes an int32/int64 array and returns its dtype");
+        if (out_dtype != x_dtype)
+            return fail(FA_EDTYPE, "fa_elementwise: IPOW returns its input's dtype");
         if (!(a >= 0.0) || a != std::floor(a) || a > 0x1p63)
             return fail(FA_EINVAL, "fa_elementwise: IPOW exponent must be a non-negative integer");
         const dim3 g((unsigned)std::min<int64_t>((P + kBlock - 1) / kBlock, 8192));
         hipStream_t sti = static_cast<hipStream_t>(stream);
-        if (x_dtype == FA_I32)
-            hipLaunchKernelGGL(k_ipow<int32_t>, g, dim3(kBlock), 0, sti, static_cast<int32_t*>(out),
-                               static_cast<const int32_t*>(x), (uint64_t)a, P);
-        else
-            hipLaunchKernelGGL(k_ipow<int64_t>, g, dim3(kBlock), 0, sti, static_cast<int64_t*>(out),
-                               static_cast<const int64_t*>(x), (uint64_t)a, P);
-        return check_launch("fa_elementwise");
+        auto run = [&](auto tag) -> int {
+            using T = decltype(tag);
+            hipLaunchKernelGGL(k_ipow<T>, g, dim3(kBlock), 0, sti, static_cast<T*>(out), static_cast<const T*>(x),
+                               (uint64_t)a, P);
+            return check_launch("fa_elementwise");
+        };
+        switch (x_dtype) {
+            case FA_I8: return run(int8_t{});
+            case FA_I16: return run(int16_t{});
+            case FA_I32: return run(int32_t{});
+            case FA_I64: return run(int64_t{});
+            case FA_U8: return run(uint8_t{});
+            case FA_U16: return run(uint16_t{});
+            case FA_U32: return run(uint32_t{});
+            case FA_U64: return run(uint64_t{});
+            default: return fail(FA_EDTYPE, "fa_elementwise: IPOW takes an integer array, got dtype %d", x_dtype);
+        }
     }
     if (op == FA_EW_IFOLD || op == FA_EW_NFOLD) {
         if (!y || out_dtype != FA_F64 || x_dtype != y_dtype)
@@ -1999,6 +2015,12 @@ int fa_norm1(double* out, const void* x, int dtype, int64_t rows, int64_t cols, 
         case FA_F64: return run(double{});
         case FA_I32: return run(int32_t{});
         case FA_I64: return run(int64_t{});
+        case FA_I8: return run(int8_t{});
+        case FA_I16: return run(int16_t{});
+        case FA_U8: return run(uint8_t{});
+        case FA_U16: return run(uint16_t{});
+        case FA_U32: return run(uint32_t{});
+        case FA_U64: return run(uint64_t{});
         default: return fail(FA_EDTYPE, "fa_norm1: dtype %d", dtype);
     }
 }
@@ -2034,6 +2056,8 @@ int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, co
     }
     FA_CAST(FA_F32, float, FA_F32, float)
     FA_CAST(FA_F64, double, FA_F64, double)
+    FA_CAST(FA_F32, float, FA_F16, f16)      // narrowing float casts (numpy astype: round to nearest even):
+    FA_CAST(FA_F64, double, FA_F32, float)   // the result of a float16 / float32 helper op computed wider
     FA_CAST(FA_F16, f16, FA_F16, f16)
     FA_CAST(FA_BF16, bf16, FA_BF16, bf16)
     FA_CAST(FA_I32, int32_t, FA_I32, int32_t)

@@ -989,6 +989,101 @@ class CopyPool {
 
 }  // namespace
 
+// Asynchronous gathers (fnpz_gather_start / fnpz_gather_wait): a caller that packs many small
+// updates one after the other (staging arenas) hands each update's copies to one background thread
+// and goes on with the next update; the thread takes every queued job at once and copies them on the
+// CopyPool. Jobs complete in submission order, so a ticket is done once the completed count reaches
+// it. One queue per process (fork-safe like CopyPool); its thread parks when idle.
+class GatherQueue {
+   public:
+    struct Piece {
+        uint8_t* d;
+        const uint8_t* s;
+        int64_t len;
+    };
+    static GatherQueue& get() {
+        static std::mutex m;
+        static GatherQueue* q = nullptr;
+        static pid_t owner = 0;
+        std::lock_guard<std::mutex> lk(m);
+        if (!q || owner != getpid()) {
+            q = new GatherQueue();
+            owner = getpid();
+        }
+        return *q;
+    }
+    int64_t submit(std::vector<Piece>&& pieces, int threads) {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!started_) {
+            std::thread([this] { work(); }).detach();
+            started_ = true;
+        }
+        const int64_t t = ++issued_;
+        for (auto& p : pieces) pending_.push_back(p);
+        threads_ = std::max(threads_, threads);
+        last_ = t;
+        cv_.notify_one();
+        return t;
+    }
+    void wait(int64_t t) {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [&] { return done_ >= t; });
+    }
+
+   private:
+    void work() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return !pending_.empty(); });
+            std::vector<Piece> batch;
+            batch.swap(pending_);
+            const int64_t upto = last_;
+            const int threads = threads_;
+            threads_ = 1;
+            lk.unlock();
+            int64_t total = 0;
+            for (auto& p : batch) total += p.len;
+            const int np = (int)batch.size();
+            auto copy = [&](int k) { std::memcpy(batch[k].d, batch[k].s, (size_t)batch[k].len); };
+            const int t = std::min<int64_t>(threads, std::max<int64_t>(1, total >> 18));   // >= 256 KiB per thread
+            if (t <= 1 || np <= 1)
+                for (int k = 0; k < np; ++k) copy(k);
+            else
+                CopyPool::get().run(std::min(t, np), np, copy);
+            lk.lock();
+            done_ = upto;
+            done_cv_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::vector<Piece> pending_;
+    int64_t issued_ = 0, last_ = 0, done_ = 0;
+    int threads_ = 1;
+    bool started_ = false;
+};
+
+extern "C" int64_t fnpz_gather_start(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes,
+                                     int threads) {
+    if (n < 0 || (n > 0 && (!dsts || !srcs || !nbytes)) || threads < 1)
+        return -fail(FNPZ_EINVAL, "fnpz_gather_start: bad arguments");
+    std::vector<GatherQueue::Piece> pieces;
+    for (int i = 0; i < n; ++i) {
+        if (nbytes[i] < 0 || (nbytes[i] > 0 && (!dsts[i] || !srcs[i])))
+            return -fail(FNPZ_EINVAL, "fnpz_gather_start: segment %d", i);
+        for (int64_t o = 0; o < nbytes[i]; o += 1 << 20)
+            pieces.push_back({static_cast<uint8_t*>(dsts[i]) + o, static_cast<const uint8_t*>(srcs[i]) + o,
+                              std::min<int64_t>(1 << 20, nbytes[i] - o)});
+    }
+    return GatherQueue::get().submit(std::move(pieces), threads);
+}
+
+extern "C" int fnpz_gather_wait(int64_t ticket) {
+    if (ticket <= 0) return fail(FNPZ_EINVAL, "fnpz_gather_wait: bad ticket %lld", (long long)ticket);
+    GatherQueue::get().wait(ticket);
+    return FNPZ_OK;
+}
+
 extern "C" int fnpz_gather(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes, int threads) {
     if (n < 0 || (n > 0 && (!dsts || !srcs || !nbytes)) || threads < 1)
         return fail(FNPZ_EINVAL, "fnpz_gather: bad arguments");

@@ -38,9 +38,101 @@ def _to_dev(x, dev):
     if isinstance(x, torch.Tensor):
         return x.contiguous(), False
     a = np.ascontiguousarray(x)
-    if a.dtype not in (np.float32, np.float64):
-        raise TypeError(f"fednamdhelper primitives support float32/float64 arrays, got {a.dtype}")
+    if a.dtype.kind not in "fiu" or a.dtype.itemsize > 8:
+        raise TypeError(f"fednamdhelper primitives support float and integer arrays, got {a.dtype}")
     return torch.from_numpy(a).to(dev), True
+
+
+def _np_result(op, xdt, ydt, a, b):
+    """numpy's result dtype of numpyhelper's expression for these operand dtypes (empty arrays,
+    no data; python scalars are weak): ``x*a + y*b``, ``x*y`` / ``x*a``, ``x/y`` / ``x/a``,
+    ``sqrt``, ``sign``; ``ones`` is float64."""
+    ex = np.empty(0, xdt)
+    ey = None if ydt is None else np.empty(0, ydt)
+    with np.errstate(all="ignore"):
+        if op == "axpby":
+            return (ex * a + ey * b).dtype
+        if op == "mul":
+            return (ex * (a if ey is None else ey)).dtype
+        if op == "div":
+            return (ex / (a if ey is None else ey)).dtype
+        if op == "sqrt":
+            return np.sqrt(ex).dtype
+        if op == "sign":
+            return np.sign(ex).dtype
+    return np.dtype(np.float64)
+
+
+def _ew_one(op, xd, yd, a, b, dev):
+    """One numpyhelper primitive on flat device tensors, numpy's dtypes and rounding.
+
+    float32 / float64 operands run fa_elementwise directly, three float16 arrays in AXPBY its half
+    loop. Otherwise (float16 with a scalar or another dtype, 8 / 16 / 32 / 64-bit integers) the op
+    is computed in a WIDER float and rounded once to numpy's result dtype r: operands are widened
+    exactly (integers to float64 as numpy converts them; float16 to float32), the single op is
+    correctly rounded in the wide type (float32 for an r of float16, float64 otherwise) and
+    narrowed to r by fa_cast — the same value as the op rounded once in r (a correctly rounded op
+    rounded again is innocuous: 24 >= 2*11+2, 53 >= 2*24+2). A python scalar meets a float16 array
+    as a float16 (numpy's weak scalar), so it is rounded to half first. AXPBY with one float16
+    operand rounds that operand's product in half first (numpy's order), then adds in r. Integer
+    results (integer multiply / sign) are not supported (FedAggError)."""
+    import torch
+
+    from . import ops
+    from ._abi import FedAggError
+    kf = (torch.float32, torch.float64)
+    xdt = ops.numpy_dtype(xd.dtype)
+    ydt = None if yd is None else ops.numpy_dtype(yd.dtype)
+    if op == "fill":
+        o = torch.empty(xd.numel(), dtype=torch.float64, device=dev)
+        ops.elementwise("fill", o, None, None, a, b)
+        return o
+    if xd.dtype in kf and (yd is None or yd.dtype in kf):          # the direct kernels
+        odt = ops.promote(xd.dtype, yd.dtype) if (op == "axpby" or (op in ("mul", "div") and yd is not None)) \
+            else xd.dtype
+        o = torch.empty(xd.numel(), dtype=odt, device=dev)
+        ops.elementwise(op, o, xd, yd, a, b)
+        return o
+    if op == "axpby" and xd.dtype == torch.float16 and yd is not None and yd.dtype == torch.float16:
+        o = torch.empty(xd.numel(), dtype=torch.float16, device=dev)
+        ops.elementwise(op, o, xd, yd, a, b)
+        return o
+    r = _np_result(op, xdt, ydt, a, b)
+    if r.kind != "f" or r not in (np.float16, np.float32, np.float64):
+        raise FedAggError(2, f"fednamdhelper: {op} on {xdt}" + (f" / {ydt}" if ydt is not None else "") +
+                             f" gives {r}; integer results are not supported on the GPU helper")
+    rt = ops.torch_dtype(r)
+    wide = torch.float32 if r == np.float16 else torch.float64
+
+    def widen(t, to=None):
+        to = to or wide
+        return t if t.dtype == to else ops.cast(torch.empty(t.numel(), dtype=to, device=dev), t)
+
+    def narrow(t):
+        return t if t.dtype == rt else ops.cast(torch.empty(t.numel(), dtype=rt, device=dev), t)
+
+    half = lambda v: float(np.float16(v))  # noqa: E731  (a python float meeting a half array)
+    if op == "axpby":
+        if rt not in kf:                    # a half result needs three half operands (handled above)
+            raise FedAggError(2, f"fednamdhelper: add on {xdt} / {ydt} is not supported")
+        # numpy's order: each product in its own dtype (operand * weak python float), then the sum
+        # in r. A product whose dtype is r is left to the final kernel (operand widened exactly);
+        # another (float16 or float32 beside a wider r) is rounded in its dtype first
+        parts = []
+        for t, c in ((xd, a), (yd, b)):
+            pd = _np_result("mul", ops.numpy_dtype(t.dtype), None, c, 0)
+            parts.append((t, c) if pd == r else (_ew_one("mul", t, None, c, 0, dev), 1.0))
+        (px, ca), (py, cb) = parts
+        o = torch.empty(xd.numel(), dtype=rt, device=dev)
+        ops.elementwise("axpby", o, widen(px, rt), widen(py, rt), ca, cb)
+        return o
+    if yd is None and op in ("mul", "div") and xd.dtype == torch.float16:
+        a = half(a)
+    wx = widen(xd)
+    wy = None if yd is None else widen(yd)
+    o = torch.empty(xd.numel(), dtype=wide, device=dev)
+    ops.elementwise(op, o, wx, wy, a, b)
+    return narrow(o)
 
 
 def _back(t, host, shape):
@@ -91,6 +183,7 @@ class Helper:
             yd = None
             if isinstance(y, np.generic):          # numpy scalars (0-d results) are arrays here
                 y = np.asarray(y)
+            ai = a
             if y is not None and not isinstance(y, (int, float)):
                 if tuple(y.shape) != shape:
                     raise ValueError(f"operands could not be broadcast together with shapes {shape} {tuple(y.shape)}")
@@ -98,16 +191,8 @@ class Helper:
                 yd = yd.reshape(-1)
                 host = host or yhost
             elif y is not None:
-                a = float(y)                     # multiply/divide by a python scalar (weak)
-            if op == "fill":
-                odt = torch.float64
-            elif op == "axpby" or (op in ("mul", "div") and yd is not None):
-                odt = ops.promote(xd.dtype, yd.dtype)
-            else:
-                odt = xd.dtype
-            o = torch.empty(xd.numel(), dtype=odt, device=dev)
-            ops.elementwise(op, o, xd, yd, a, b)
-            out.append(_back(o, host, shape))
+                ai = float(y)                    # multiply/divide by a python scalar (weak)
+            out.append(_back(_ew_one(op, xd, yd, ai, b, dev), host, shape))
         return out
 
     def add(self, m1, m2, a=1.0, b=1.0):
@@ -151,6 +236,14 @@ class Helper:
             o = torch.empty(xd.numel(), dtype=ops.torch_dtype(rdt), device=dev)
             if rdt.kind in "iu":
                 ops.elementwise("ipow", o, xd, None, float(a))
+            elif o.dtype == torch.float16:
+                # half power: x*x / pow computed in float32 from the exact widening, rounded once to
+                # half (x*x is exact in float32: numpy's result; pow: numpy's libm, 1e-3 relative)
+                w = xd if xd.dtype == torch.float32 else ops.cast(torch.empty(xd.numel(), dtype=torch.float32,
+                                                                               device=dev), xd)
+                t = torch.empty(xd.numel(), dtype=torch.float32, device=dev)
+                ops.elementwise("square" if a == 2 else "pow", t, w, None, float(np.float16(a)))
+                ops.cast(o, t)
             else:
                 if xd.dtype != o.dtype:
                     xd = ops.cast(torch.empty(xd.numel(), dtype=o.dtype, device=dev), xd)
@@ -179,6 +272,8 @@ class Helper:
             if nd == 2 and x.shape[1] == 0:
                 raise ValueError("zero-size array to reduction operation maximum which has no identity")
             xd = torch.from_numpy(np.ascontiguousarray(xa)).to(dev) if host else x.contiguous()
+            if xd.dtype == torch.float16:              # summed from the exact float32 widening
+                xd = ops.cast(torch.empty(tuple(xd.shape), dtype=torch.float32, device=dev), xd)
             val = float(ops.norm1(xd, nd == 2).item())
             rdt = xdt if xdt.kind == "f" else np.dtype(np.float64)   # numpy: non-inexact -> astype(float)
             n += rdt.type(val)

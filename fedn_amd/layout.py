@@ -7,6 +7,7 @@ fp32 tensor back to back, then (if any) the int64 tensors, etc. Each region star
 on a 256-byte boundary so every group base is 16-B aligned for the vector path.
 One H2D copy moves a whole update; one kernel launch per group folds it.
 """
+import ctypes
 import os
 from concurrent.futures import ThreadPoolExecutor
 
@@ -57,6 +58,47 @@ def run_pack_jobs(jobs):
             futs.append(_executor().submit(np.copyto, d[i:i + step], src[i:i + step], casting="no"))
     for f in futs:
         f.result()
+
+
+def start_pack_jobs(jobs):
+    """Queue the copies to the native gather thread and return at once: a ticket for
+    :func:`wait_pack_jobs` (the caller keeps ``jobs`` referenced until then). Without the codec
+    library, or for jobs it cannot take (dtype mismatch, non-contiguous), the copies run now and
+    None is returned."""
+    ok = all(d.dtype == src.dtype and d.flags.c_contiguous and src.flags.c_contiguous for d, src in jobs)
+    if ok and jobs:
+        try:
+            from . import codec
+            return codec.gather_start(jobs, PACK_THREADS)
+        except ImportError:
+            pass
+    run_pack_jobs(jobs)
+    return None
+
+
+def start_pack_into(layout, arrays, dst_ptr):
+    """Queue the pack of ``arrays`` (already checked against ``layout``: shapes and dtypes) into the
+    host bytes at address ``dst_ptr`` to the native gather thread; returns (ticket, the sources to
+    keep referenced until :func:`wait_pack_jobs`). None as ticket: copied already (no codec library,
+    or a non-contiguous source)."""
+    srcs = [arrays[i] for i, _, _ in layout.pack_plan]
+    if all(type(a) is np.ndarray and a.flags.c_contiguous for a in srcs):
+        try:
+            from . import codec
+            return codec.gather_start_raw([dst_ptr + off for _, off, _ in layout.pack_plan],
+                                          [a.ctypes.data for a in srcs], [n for _, _, n in layout.pack_plan],
+                                          PACK_THREADS), srcs
+        except ImportError:
+            pass
+    buf = np.ctypeslib.as_array((ctypes.c_uint8 * layout.nbytes).from_address(dst_ptr))
+    layout.pack(arrays, buf)
+    return None, srcs
+
+
+def wait_pack_jobs(ticket):
+    if ticket is not None:
+        from . import codec
+        codec.gather_wait(ticket)
 
 
 def _executor():
@@ -123,6 +165,10 @@ class Layout:
             off = _round_up(off + self.group_elems[dt] * dt.itemsize, ALIGN)
         self.nbytes = max(off, ALIGN)
         self.nparams = sum(self.sizes)
+        # (tensor index, byte offset in the packed buffer, bytes) of every non-empty tensor: the
+        # copies of a pack as plain integers (staging's arena packs need no numpy views)
+        self.pack_plan = [(i, self.group_byte_offset[dt] + off * dt.itemsize, self.sizes[i] * dt.itemsize)
+                          for dt in self.groups for i, off in self.members[dt] if self.sizes[i]]
 
     def shard_geometry(self, ndev):
         """Parameter-slice sharding over ``ndev`` devices (multidev.py, ingest.py):
@@ -142,10 +188,19 @@ class Layout:
             dev_bytes.append(max(off, ALIGN))
         return bounds, dev_off, dev_bytes
 
+    _by_sig = {}                  # Layout.of: one Layout per (shapes, dtypes) seen (a session's rounds)
+
     @classmethod
     def of(cls, arrays):
         arrays = [np.asarray(a) for a in arrays]
-        return cls([a.shape for a in arrays], [a.dtype for a in arrays])
+        key = tuple((a.shape, a.dtype.str) for a in arrays)
+        lay = cls._by_sig.get(key)
+        if lay is None:
+            lay = cls([a.shape for a in arrays], [a.dtype for a in arrays])
+            if len(cls._by_sig) >= 64:
+                cls._by_sig.clear()
+            cls._by_sig[key] = lay
+        return lay
 
     def signature(self):
         return (tuple(self.shapes), tuple(str(d) for d in self.dtypes))

@@ -27,7 +27,7 @@ import torch
 
 from . import mixed, ops
 from .ingest import StagedModel
-from .layout import Layout, parallel_copy, run_pack_jobs
+from .layout import Layout, parallel_copy, start_pack_into, wait_pack_jobs
 
 
 BATCH = 64                    # device-resident updates folded per launch (the kernarg client table)
@@ -128,11 +128,12 @@ class _Slot:
 
 class _Arena:
     """Pinned host + device bytes for up to ``cap`` packed small updates (see SMALL_UPDATE_BYTES)."""
-    __slots__ = ("host", "host_np", "dev", "cap", "count", "done", "used")
+    __slots__ = ("host", "host_np", "host_ptr", "dev", "cap", "count", "done", "used")
 
     def __init__(self, cap, nbytes, device):
         self.host = torch.empty(cap * nbytes, dtype=torch.uint8, pin_memory=True)
         self.host_np = self.host.numpy()
+        self.host_ptr = self.host.data_ptr()
         self.dev = torch.empty(cap * nbytes, dtype=torch.uint8, device=device)
         self.cap, self.count, self.used = cap, 0, False
         self.done = None
@@ -177,8 +178,19 @@ class _Pipeline:
         # allocated for a single update and never reused)
         self.batch_host = batch and layout.nbytes <= SMALL_UPDATE_BYTES
         self._arenas, self._arena, self._arena_i = (kept["arenas"] if kept else []), None, 0
-        self._pack_jobs = []                     # deferred copies into the arena being filled
+        self._pack_jobs = []                     # copies into the arena being filled (kept referenced)
+        self._pack_ticket = None                 # the last of them queued to the native gather thread
+        # the fused path's fast admission of host updates: exact (shape, dtype) per tensor
+        self._sig = [(tuple(sh), np.dtype(dt)) for sh, dt in zip(layout.shapes, layout.dtypes)]
+        self._plain = not mixed.per_tensor_dtypes(layout.dtypes) and \
+            not any(np.dtype(d).kind == "i" for d in layout.dtypes)
+        try:
+            for dt in layout.groups:
+                ops.fa_dtype(ops.torch_dtype(dt))
+        except (TypeError, KeyError):
+            self._plain = False
         self._d2h_on_compute = False             # a small result was copied back on the compute stream
+        self._synced = False                     # the result is on the host: every recorded event fired
         self.streamer = kept["streamer"] if kept else HostStreamer()
 
     def release(self):
@@ -235,12 +247,25 @@ class _Pipeline:
             self._arena = a
         nb, j = self.layout.nbytes, a.count
         tic = time.perf_counter()
-        # the copies run together when the arena is uploaded (one native call, all pack threads):
-        # per update only the jobs are recorded (the source arrays stay referenced until then)
-        self._pack_jobs.extend(self.layout.pack_jobs(arrays, a.host_np[j * nb:(j + 1) * nb]))
+        # the copies go to the native gather thread and run while the next updates are loaded;
+        # upload_arena waits for them (the source arrays stay referenced until then)
+        ticket, keep = start_pack_into(self.layout, arrays, a.host_ptr + j * nb)
+        self._pack_jobs.append(keep)
+        self._pack_ticket = ticket or self._pack_ticket
         self.time_pack += time.perf_counter() - tic
         a.count += 1
         return _ArenaRef(a.dev[j * nb:(j + 1) * nb])
+
+    def fast_host(self, arrays):
+        """Whether ``arrays`` is a list of numpy arrays with exactly this round's shapes and dtypes on
+        a float-only model batched through the arena: such an update needs none of add()'s other
+        checks (per-tensor path, integer n rules)."""
+        if not (self.batch_host and self._plain) or len(arrays) != len(self._sig):
+            return False
+        for a, (sh, dt) in zip(arrays, self._sig):
+            if type(a) is not np.ndarray or a.shape != sh or a.dtype != dt:
+                return False
+        return True
 
     def arena_full(self):
         return self._arena is not None and self._arena.count >= self._arena.cap
@@ -252,8 +277,8 @@ class _Pipeline:
         if a is None or a.count == 0:
             return
         tic = time.perf_counter()
-        jobs, self._pack_jobs = self._pack_jobs, []
-        run_pack_jobs(jobs)
+        wait_pack_jobs(self._pack_ticket)       # every pack of this arena has landed
+        self._pack_ticket, self._pack_jobs = None, []
         self.time_pack += time.perf_counter() - tic
         n = a.count * self.layout.nbytes
         start = torch.cuda.Event(enable_timing=True)
@@ -375,7 +400,8 @@ class _Pipeline:
 
     def timings(self):
         """GPU-side H2D and kernel time (s, HIP events) plus host pack and D2H wall time."""
-        torch.cuda.synchronize(self.device)
+        if not self._synced:                     # result() synchronised every stream its events are on
+            torch.cuda.synchronize(self.device)
         h2d = sum(a.elapsed_time(b) for a, b in self._h2d) / 1e3
         kern = sum(a.elapsed_time(b) for a, b in self._kern) / 1e3
         return {"time_h2d": h2d, "time_kernel": kern, "time_pack": self.time_pack, "time_d2h": self.time_d2h}
@@ -430,6 +456,12 @@ class FedAvgPipeline(_Pipeline):
         staged and folded on arrival (after any pending batch, keeping FIFO order). An update
         whose dtypes or shapes differ from the first's moves the round to the per-tensor path
         (numpy promotion / broadcasting, mixed.py) — checked before any state changes."""
+        if self.general is None and type(arrays) is list and self.fast_host(arrays):
+            self.pending.append((self.put_small(arrays), n, N))      # a small float model's update
+            if len(self.pending) >= BATCH or self.arena_full():
+                self._flush()
+            self.nfolds += 1
+            return
         if self.general is None and (not self.compatible(arrays) or
                                      mixed.int_float_n(self.layout.dtypes, self.nfolds, n) or
                                      mixed.per_tensor_dtypes(self.layout.dtypes)):
@@ -529,6 +561,8 @@ class FedAvgPipeline(_Pipeline):
         self.d2h.synchronize()
         if self._d2h_on_compute:
             self.compute.synchronize()
+        self.copy.synchronize()
+        self._synced = True
         self.time_d2h += time.perf_counter() - tic
         out = [None] * len(self.layout.shapes)
         for dt in self.layout.groups:
@@ -800,6 +834,12 @@ class FedOptPipeline(_Pipeline):
         join the pending batch, which the server step folds in its fused launch; host arrays
         are staged and folded into pg on arrival (after any pending batch). Updates that differ
         from the first in dtype or shape, or from the global model in shape, run per tensor."""
+        if self.general is None and self.fused_ok and type(arrays) is list and self.fast_host(arrays):
+            self.pending.append((self.put_small(arrays), n, N))      # a small float model's update
+            if len(self.pending) >= BATCH or self.arena_full():
+                self._flush()
+            self.nfolds += 1
+            return
         if self.general is None and not (self.fused_ok and self.compatible(arrays)):
             ym = self.meta_of(arrays)
             splan = mixed.sub_plan(ym, mixed.host_meta(self.old_arrays))          # raises as numpy
@@ -915,6 +955,8 @@ class FedOptPipeline(_Pipeline):
         self.d2h.synchronize()
         if self._d2h_on_compute:
             self.compute.synchronize()
+        self.copy.synchronize()
+        self._synced = True
         self.time_d2h += time.perf_counter() - tic
         state.m, state.v, state.signature, state.layout = new_m, new_v, sig, self.layout
         model = [None] * len(self.layout.shapes)

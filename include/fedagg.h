@@ -188,8 +188,9 @@ int fa_running_mean(void* g, int dtype, const void* m, double a, double b, doubl
  *                                                  power rounded once (numpy's own float power is its
  *                                                  host libm's / SIMD library's: not bit-reproducible
  *                                                  across hosts; parity: 1e-6 relative, f64 1e-15)
- *   FA_EW_IPOW    out = x**a, x I32 | I64, a a non-negative integer: exponentiation by squaring
- *                 with wrapping products, out_dtype = x_dtype (numpy's integer power)
+ *   FA_EW_IPOW    out = x**a, x any integer dtype (I8..I64, U8..U64), a a non-negative integer:
+ *                 exponentiation by squaring with wrapping products, out_dtype = x_dtype (numpy's
+ *                 integer power)
  *   FA_EW_IFOLD   out = x + ((y - x)*a)/b, x and y of one integer dtype (I8..I64, U8..U64), out
  *                 F64: numpyhelper.increment_average (numpyhelper.py:32) on integer arrays with a
  *                 python-float num_examples a and total b — the difference wraps in the integer
@@ -209,7 +210,8 @@ int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype,
 /*
  * numpyhelper.norm (numpyhelper.py:106-117) for one tensor: np.linalg.norm(x, 1), i.e. sum |x| of a
  * vector (matrix = 0; rows*cols elements) or the max column sum of |x| of a C-order rows x cols
- * matrix (matrix = 1). x: F32 | F64 | I32 | I64. Accumulated in f64 in a fixed order (numpy sums f32
+ * matrix (matrix = 1). x: F32 | F64 | any integer dtype (numpy: astype(float) first). Accumulated in
+ * f64 in a fixed order (numpy sums f32
  * pairwise in f32: parity 1e-6 relative). out: DEVICE double (written on `stream`); work: DEVICE
  * scratch of fa_norm1_work(rows, cols, matrix) doubles.
  */
@@ -234,7 +236,10 @@ int fa_promote(int a, int b);
  * Conversions (numpy's casting of the value): identity for every dtype; F16/BF16 -> F32/F64 and
  * F32 -> F64 (exact); I32 -> I64 (exact); I32/I64 -> F64 (round to nearest even); I8 / I16 / U8 /
  * U16 / U32 / U64 to every integer or float dtype numpy casts them to safely (U64 -> F64 rounds to
- * nearest even, the rest are exact). Narrowing conversions are refused (FA_EDTYPE). 1 <= ndim <= 8; out is contiguous.
+ * nearest even, the rest are exact); and two narrowing float casts, F32 -> F16 and F64 -> F32, rounded
+ * to nearest even as numpy's astype (the result of a helper op computed in a wider float: a single
+ * correctly rounded op then rounded again equals the op rounded once, since 24 >= 2*11+2 and
+ * 53 >= 2*24+2). Other narrowing conversions are refused (FA_EDTYPE). 1 <= ndim <= 8; out is contiguous.
  */
 int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, const int64_t* out_shape,
             const int64_t* in_strides, void* stream);
