@@ -49,7 +49,9 @@ class HbmBudget:
             os.environ.get("FEDN_AMD_HBM_FRACTION", DEFAULT_FRACTION))
         self._cap = {}
         self._used = {}
-        self._lock = threading.Lock()
+        # re-entrant: a staged update's finalizer (``hold``) may run — and release — while this thread
+        # is inside reserve() (garbage collection runs at any allocation)
+        self._lock = threading.RLock()
         self.refused = 0              # stagings turned away (reported by the ingest)
 
     def _capacity(self, key, device):

@@ -1034,7 +1034,7 @@ class GatherQueue {
     void work() {
         std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
-            cv_.wait(lk, [&] { return !pending_.empty(); });
+            cv_.wait(lk, [&] { return last_ > done_; });        // a job (possibly with no bytes) is queued
             std::vector<Piece> batch;
             batch.swap(pending_);
             const int64_t upto = last_;

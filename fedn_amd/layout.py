@@ -82,6 +82,8 @@ def start_pack_into(layout, arrays, dst_ptr):
     keep referenced until :func:`wait_pack_jobs`). None as ticket: copied already (no codec library,
     or a non-contiguous source)."""
     srcs = [arrays[i] for i, _, _ in layout.pack_plan]
+    if not srcs:                                  # only empty tensors: nothing to copy
+        return None, srcs
     if all(type(a) is np.ndarray and a.flags.c_contiguous for a in srcs):
         try:
             from . import codec

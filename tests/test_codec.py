@@ -248,3 +248,21 @@ def test_stale_library_is_an_import_error(tmp_path, monkeypatch, version, symbol
     assert layout._native_gather([(dst, srcarr)]) is False
     layout.parallel_copy(dst, srcarr)
     assert np.array_equal(dst, srcarr)
+
+
+def test_async_gather_queue_tickets_and_empty_jobs():
+    """fnpz_gather_start / fnpz_gather_wait: jobs complete in order (waiting on the last ticket
+    covers every earlier one), a job with no bytes completes too (a model of only empty tensors
+    must not hang the pack), and many small jobs land byte-exact."""
+    srcs = [np.arange(i * 1000, i * 1000 + 777 + i, dtype=np.float32) for i in range(50)]
+    dsts = [np.zeros_like(s) for s in srcs]
+    t_empty0 = codec.gather_start_raw([], [], [], 4)
+    codec.gather_wait(t_empty0)
+    tickets = [codec.gather_start_raw([d.ctypes.data], [s.ctypes.data], [s.nbytes], 4) for d, s in zip(dsts, srcs)]
+    t_last = codec.gather_start_raw([], [], [], 4)
+    assert t_last > tickets[-1] > tickets[0] > t_empty0
+    codec.gather_wait(t_last)
+    for d, s in zip(dsts, srcs):
+        assert np.array_equal(d, s)
+    with pytest.raises(codec.CodecError):
+        codec.gather_wait(0)

@@ -13,7 +13,7 @@ python -c "import fedn_amd.build as b; b.build()" > "$OUT/build.log" 2>&1 || { e
 for s in $STEPS; do
   case $s in
     test)
-      timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v --maxfail=20 --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1; rc=$?
       echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu.log"; if fatal $rc; then exit $rc; fi ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$?
