@@ -6,6 +6,8 @@ tensors' current HIP stream, raise :class:`FedAggError` on a nonzero status.
 dtype rules mirror numpy's for the reference expressions:
 see :func:`fold_result_dtype` and :func:`fedopt_dtypes`.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -132,6 +134,25 @@ def fedavg_fold(agg, updates, n, N, init, stream=None):
         st = _stream_handle(agg, stream)
         rc = lib.fa_fedavg_fold(agg.data_ptr(), fa_dtype(agg), _abi.ptr_array([u.data_ptr() for u in updates]),
                                 fa_dtype(upd_dt), _abi.double_array(n), _abi.double_array(N), K, P, int(bool(init)), st)
+    _abi.check(rc)
+    return agg
+
+
+def fedavg_fold_ptrs(agg, ptrs, upd_dtype, n, N, init, stream=None):
+    """:func:`fedavg_fold` with the client table given as device addresses (ints) of ``agg.numel()``
+    elements of ``upd_dtype`` each, on ``agg``'s device: the pipelines' own staging buffers, whose
+    extent they guarantee (no per-update tensor view or check)."""
+    lib = _abi.load()
+    K = len(ptrs)
+    if len(n) != K or len(N) != K:
+        raise ValueError("n and N must have one entry per update")
+    P = agg.numel()
+    _check_dev("agg", agg, P, None)
+    with torch.cuda.device(agg.device):
+        st = _stream_handle(agg, stream)
+        rc = lib.fa_fedavg_fold(agg.data_ptr(), fa_dtype(agg), (ctypes.c_void_p * max(1, K))(*ptrs),
+                                fa_dtype(upd_dtype), (ctypes.c_double * max(1, K))(*n),
+                                (ctypes.c_double * max(1, K))(*N), K, P, int(bool(init)), st)
     _abi.check(rc)
     return agg
 
@@ -439,6 +460,13 @@ def copy_async(dst_ptr, src, nbytes, stream):
         raise ValueError("copy_async: more bytes than the source holds")
     with torch.cuda.device(src.device):
         _abi.check(lib.fa_copy_async(int(dst_ptr), src.data_ptr(), int(nbytes), ctypes_stream(stream)))
+
+
+def copy_ptr_async(dst_ptr, src_ptr, nbytes, stream, device):
+    """``nbytes`` from address ``src_ptr`` to ``dst_ptr`` (host or device) on ``stream``: one
+    hipMemcpyAsync, without a tensor per call."""
+    with torch.cuda.device(device):
+        _abi.check(_abi.load().fa_copy_async(int(dst_ptr), int(src_ptr), int(nbytes), ctypes_stream(stream)))
 
 
 def peer_enable(dev, peer):

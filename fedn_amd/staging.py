@@ -283,9 +283,9 @@ class _Pipeline:
         n = a.count * self.layout.nbytes
         start = torch.cuda.Event(enable_timing=True)
         a.done = torch.cuda.Event(enable_timing=True)
-        with torch.cuda.device(self.device), torch.cuda.stream(self.compute):
+        with torch.cuda.device(self.device):
             start.record(self.compute)
-            a.dev[:n].copy_(a.host[:n], non_blocking=True)
+            ops.copy_ptr_async(a.dev.data_ptr(), a.host_ptr, n, self.compute, self.device)
             a.done.record(self.compute)
         self._h2d.append((start, a.done))
         a.used = True
@@ -496,16 +496,21 @@ class FedAvgPipeline(_Pipeline):
         self.nfolds += 1
 
     def _fold_group(self, dt, entries, init, lo, hi):
-        """Enqueue the fold of ``entries`` over elements [lo, hi) of group ``dt``."""
-        ys = [self.group(e[0], dt)[lo:hi] for e in entries]
+        """Enqueue the fold of ``entries`` over elements [lo, hi) of group ``dt``. Every entry's
+        bytes (a slot, an arena piece or a staged model) are a uint8 buffer on this device in this
+        layout, so the client table is plain addresses (no per-update tensor views: for small models
+        those cost more than the launch)."""
+        off = self.layout.group_byte_offset[dt] + lo * dt.itemsize
+        ptrs = [e[0].dev.data_ptr() + off for e in entries]
         ns = [e[1] for e in entries]
         Ns = [e[2] for e in entries]
         acc = self._agg(dt)[lo:hi]
+        upd_dt = ops.torch_dtype(dt)
         if init:                                # agg := first update, then fold (fedavg.py:127-133)
-            x0 = self.group(self.first, dt)[lo:hi]
-            ops.fedavg_fold(acc, [x0] + ys, [0.0] + ns, [1.0] + Ns, init=True, stream=self.compute)
+            ops.fedavg_fold_ptrs(acc, [self.first.dev.data_ptr() + off] + ptrs, upd_dt, [0.0] + ns, [1.0] + Ns,
+                                 init=True, stream=self.compute)
         else:
-            ops.fedavg_fold(acc, ys, ns, Ns, init=False, stream=self.compute)
+            ops.fedavg_fold_ptrs(acc, ptrs, upd_dt, ns, Ns, init=False, stream=self.compute)
 
     def _agg(self, dt):
         """The running aggregate of group ``dt`` (allocated on first use, numpy's result dtype)."""

@@ -1116,11 +1116,25 @@ def test_cast_strided_source():
     assert torch.equal(out.cpu(), x.cpu().double())
 
 
-def test_cast_refuses_narrowing():
+def test_cast_narrowing_rules():
+    """fa_cast: the two narrowing float casts round to nearest even like numpy's astype (specials,
+    overflow to inf, subnormal results included); every other narrowing conversion is refused."""
     from fedn_amd import _abi, ops
-    x = torch.ones(8, dtype=torch.float64, device=DEV)
-    with pytest.raises(_abi.FedAggError):
-        ops.cast(torch.empty(8, dtype=torch.float32, device=DEV), x)
+    rng = np.random.default_rng(12)
+    x64 = np.concatenate([rng.standard_normal(5000) * 10.0 ** rng.integers(-45, 45, 5000),
+                          [0.0, -0.0, np.inf, -np.inf, np.nan, 3.5e38, 1e-46, 2.0 ** -149, 65520.0]])
+    with np.errstate(all="ignore"):
+        want32 = x64.astype(np.float32)
+        x32 = (rng.standard_normal(5000) * 10.0 ** rng.integers(-9, 6, 5000)).astype(np.float32)
+        x32 = np.concatenate([x32, np.array([65519.0, 65520.0, 6e-8, 3e-8, -0.0, np.inf, np.nan], np.float32)])
+        want16 = x32.astype(np.float16)
+    g32 = ops.cast(torch.empty(x64.size, dtype=torch.float32, device=DEV), torch.from_numpy(x64).to(DEV))
+    assert_lists_identical([g32.cpu().numpy()], [want32], "f64 -> f32")
+    g16 = ops.cast(torch.empty(x32.size, dtype=torch.float16, device=DEV), torch.from_numpy(x32).to(DEV))
+    assert_lists_identical([g16.cpu().numpy()], [want16], "f32 -> f16")
+    for src, dst in ((torch.float64, torch.float16), (torch.int64, torch.int32), (torch.float32, torch.int32)):
+        with pytest.raises(_abi.FedAggError):
+            ops.cast(torch.empty(8, dtype=dst, device=DEV), torch.ones(8, dtype=src, device=DEV))
 
 
 @pytest.mark.parametrize("ndev", [2, 3])
