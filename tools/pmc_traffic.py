@@ -39,20 +39,24 @@ def lib_sha(session=None):
     return file_sha(os.path.join(ROOT, "fedn_amd", "libfedagg.so"))
 
 
-def per_launch(path, kernel):
+def per_launch(path, kernel, take=None):
     """Average counter value per dispatch of the kernels whose name contains ``kernel`` (a string, or
-    a tuple of strings that must all appear)."""
+    a tuple of strings that must all appear); ``take`` = (first, stop): only those dispatches of
+    them, in dispatch order (two phases of one run that share a kernel instantiation)."""
     parts = (kernel,) if isinstance(kernel, str) else tuple(kernel)
     rows = [r for r in csv.DictReader(open(path)) if all(p in r["Kernel_Name"] for p in parts)]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    if take is not None:
+        rows = rows[take[0]:take[1]]
     if not rows:
         raise SystemExit(f"no dispatch of {kernel!r} in {path}")
     vals = [float(r["Counter_Value"]) for r in rows]
     return sum(vals) / len(vals), len(vals)
 
 
-def record(d, key, kernel, alg=None, session=None):
-    fetch, nf = per_launch(os.path.join(d, "pmc_FETCH_SIZE", "run_counter_collection.csv"), kernel)
-    write, nw = per_launch(os.path.join(d, "pmc_WRITE_SIZE", "run_counter_collection.csv"), kernel)
+def record(d, key, kernel, alg=None, session=None, take=None):
+    fetch, nf = per_launch(os.path.join(d, "pmc_FETCH_SIZE", "run_counter_collection.csv"), kernel, take)
+    write, nw = per_launch(os.path.join(d, "pmc_WRITE_SIZE", "run_counter_collection.csv"), kernel, take)
     read_b = 2 * fetch * 1024
     write_b = write * 1024
     out = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -71,7 +75,9 @@ def record(d, key, kernel, alg=None, session=None):
 P, Q = 100_000_000, 350_000_000
 SESSION = [
     ("pmc1", f"fedavg_k64_p{P}_f32", "k_fedavg_pipe<float, float", 64 * P * 4 + P * 4),
-    ("pmc1", f"fedopt_adam_round1_k32_p{Q}", "k_fedopt_c<float, float", 32 * Q * 4 + Q * 24),
+    # bench.py's fedopt field runs round 1 (12 launches) before its fp32-state phase (12 more), both
+    # k_fedopt_c<float, float, CF32, FIRST, FINAL>: round 1 is the first 12 dispatches
+    ("pmc1", f"fedopt_adam_round1_k32_p{Q}", "k_fedopt_c<float, float", 32 * Q * 4 + Q * 24, (0, 12)),
     ("pmc1", f"fedopt_adam_steady_k32_p{Q}", "k_fedopt_c<float, double", Q * (4 * 32 + 48)),
     ("pmc2", f"fedavg_k8_p{P}_f32", "k_fedavg_pipe<float, float", 8 * P * 4 + P * 4),
     ("pmc3", f"fedavg_k64_p{P}_bf16", "bf16, float", 64 * P * 2 + P * 4),
@@ -129,8 +135,8 @@ def main():
             record(os.path.join(sys.argv[2], sub), key, kernel, alg, session=sys.argv[2])
         return
     if sys.argv[1] == "--session":
-        for sub, key, kernel, alg in SESSION:
-            record(os.path.join(sys.argv[2], sub), key, kernel, alg, session=sys.argv[2])
+        for sub, key, kernel, alg, *take in SESSION:
+            record(os.path.join(sys.argv[2], sub), key, kernel, alg, session=sys.argv[2], take=take[0] if take else None)
         return
     d, key = sys.argv[1], sys.argv[2]
     kernel = sys.argv[3] if len(sys.argv) > 3 else "k_fedavg"
