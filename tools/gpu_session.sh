@@ -134,7 +134,7 @@ for s in $STEPS; do
       python tools/pmc_probe_report.py "$OUT/pmcprobe" ;;
     prof)
       cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- \
-        python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 --cpu-sample 0 > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1; rc=$?
+        python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 --cpu-sample 0 --host-clients 0 > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1; rc=$?
       cd "$GRAFT_REPO_ROOT"; echo "prof rc=$rc"; tail -2 "$OUT/prof.log"; [ $rc -eq 0 ] || exit $rc ;;
   esac
 done
