@@ -180,17 +180,24 @@ class _Pipeline:
         self._arenas, self._arena, self._arena_i = (kept["arenas"] if kept else []), None, 0
         self._pack_jobs = []                     # copies into the arena being filled (kept referenced)
         self._pack_ticket = None                 # the last of them queued to the native gather thread
-        # the fused path's fast admission of host updates: exact (shape, dtype) per tensor
-        self._sig = [(tuple(sh), np.dtype(dt)) for sh, dt in zip(layout.shapes, layout.dtypes)]
-        self._plain = not mixed.per_tensor_dtypes(layout.dtypes) and \
-            not any(np.dtype(d).kind == "i" for d in layout.dtypes)
-        try:
-            for dt in layout.groups:
-                ops.fa_dtype(ops.torch_dtype(dt))
-        except (TypeError, KeyError):
-            self._plain = False
+        # the fused path's fast admission of host updates: exact (shape, dtype) per tensor (computed
+        # once per layout: Layout.of returns one object per signature)
+        fast = getattr(layout, "_fast_admission", None)
+        if fast is None:
+            sig = [(tuple(sh), np.dtype(dt)) for sh, dt in zip(layout.shapes, layout.dtypes)]
+            plain = not mixed.per_tensor_dtypes(layout.dtypes) and not any(np.dtype(d).kind == "i"
+                                                                            for d in layout.dtypes)
+            try:
+                for dt in layout.groups:
+                    ops.fa_dtype(ops.torch_dtype(dt))
+            except (TypeError, KeyError):
+                plain = False
+            fast = layout._fast_admission = (sig, plain)
+        self._sig, self._plain = fast
         self._d2h_on_compute = False             # a small result was copied back on the compute stream
         self._synced = False                     # the result is on the host: every recorded event fired
+        self._copy_used = False                  # work was enqueued on the copy stream this round
+        self._d2h_used = False                   # ... on the d2h stream
         self.streamer = kept["streamer"] if kept else HostStreamer()
 
     def release(self):
@@ -219,6 +226,7 @@ class _Pipeline:
         if s.used:
             s.h2d_done.synchronize()            # pinned bytes no longer read by the DMA
             self.copy.wait_event(s.consumed)    # device bytes no longer read by a fold
+        self._copy_used = True
         tic = time.perf_counter()
         self.layout.pack(arrays, s.host_np)
         self.time_pack += time.perf_counter() - tic
@@ -375,6 +383,7 @@ class _Pipeline:
                 host.copy_(src, non_blocking=True)
             self._d2h_on_compute = True
             return host
+        self._d2h_used = True
         for lo, hi in chunks(n, src.element_size()):
             if prepare is not None:
                 prepare(lo, hi)
@@ -563,11 +572,11 @@ class FedAvgPipeline(_Pipeline):
         self._end_span(span)
         if entries:
             self._folded()
-        self.d2h.synchronize()
         if self._d2h_on_compute:
-            self.compute.synchronize()
-        self.copy.synchronize()
-        self._synced = True
+            self.compute.synchronize()          # a small group came back on the compute stream
+        if self._d2h_used or not self._d2h_on_compute:
+            self.d2h.synchronize()
+        self._synced = self._d2h_on_compute and not self._d2h_used and not self._copy_used
         self.time_d2h += time.perf_counter() - tic
         out = [None] * len(self.layout.shapes)
         for dt in self.layout.groups:
@@ -880,6 +889,7 @@ class FedOptPipeline(_Pipeline):
     def _h2d_old(self, dt, lo, hi):
         """Enqueue the H2D of elements [lo, hi) of the global model's group ``dt`` (copy stream)."""
         odt, parts = self.old_host[dt]
+        self._copy_used = True
         return self.streamer.h2d(parts, odt, lo, hi, self.old[dt][lo:hi], self.copy)
 
     def _old_dev(self, dt):
@@ -957,11 +967,11 @@ class FedOptPipeline(_Pipeline):
             new_m[dt], new_v[dt] = m_out, v_out
         self._end_span(span)
         self.pg_started = True
-        self.d2h.synchronize()
         if self._d2h_on_compute:
-            self.compute.synchronize()
-        self.copy.synchronize()
-        self._synced = True
+            self.compute.synchronize()          # a small group came back on the compute stream
+        if self._d2h_used or not self._d2h_on_compute:
+            self.d2h.synchronize()
+        self._synced = self._d2h_on_compute and not self._d2h_used and not self._copy_used
         self.time_d2h += time.perf_counter() - tic
         state.m, state.v, state.signature, state.layout = new_m, new_v, sig, self.layout
         model = [None] * len(self.layout.shapes)
