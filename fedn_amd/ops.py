@@ -148,11 +148,13 @@ def fedavg_fold_ptrs(agg, ptrs, upd_dtype, n, N, init, stream=None):
         raise ValueError("n and N must have one entry per update")
     P = agg.numel()
     _check_dev("agg", agg, P, None)
-    with torch.cuda.device(agg.device):
-        st = _stream_handle(agg, stream)
-        rc = lib.fa_fedavg_fold(agg.data_ptr(), fa_dtype(agg), (ctypes.c_void_p * max(1, K))(*ptrs),
-                                fa_dtype(upd_dtype), (ctypes.c_double * max(1, K))(*n),
-                                (ctypes.c_double * max(1, K))(*N), K, P, int(bool(init)), st)
+    args = (agg.data_ptr(), fa_dtype(agg), (ctypes.c_void_p * max(1, K))(*ptrs), fa_dtype(upd_dtype),
+            (ctypes.c_double * max(1, K))(*n), (ctypes.c_double * max(1, K))(*N), K, P, int(bool(init)))
+    if agg.device.index == torch.cuda.current_device():      # the common case: no device switch
+        rc = lib.fa_fedavg_fold(*args, _stream_handle(agg, stream))
+    else:
+        with torch.cuda.device(agg.device):
+            rc = lib.fa_fedavg_fold(*args, _stream_handle(agg, stream))
     _abi.check(rc)
     return agg
 

@@ -379,8 +379,7 @@ class _Pipeline:
             if prepare is not None:
                 prepare(0, n)
             fold_chunk(0, n)
-            with torch.cuda.stream(self.compute):
-                host.copy_(src, non_blocking=True)
+            ops.copy_ptr_async(host.data_ptr(), src.data_ptr(), n * src.element_size(), self.compute, self.device)
             self._d2h_on_compute = True
             return host
         self._d2h_used = True
@@ -892,8 +891,23 @@ class FedOptPipeline(_Pipeline):
         self._copy_used = True
         return self.streamer.h2d(parts, odt, lo, hi, self.old[dt][lo:hi], self.copy)
 
+    def _h2d_old_small(self, dt):
+        """A small global model's group ``dt`` to HBM: its tensors copied into one pinned block and
+        one H2D enqueued on the compute stream (no ring, no copy-stream hand-off)."""
+        odt, parts = self.old_host[dt]
+        host = torch.empty(self.layout.group_elems[dt], dtype=ops.torch_dtype(odt), pin_memory=True)
+        view = host.numpy()
+        for a, off in parts:
+            np.copyto(view[off:off + a.size], a, casting="no")
+        with torch.cuda.device(self.device), torch.cuda.stream(self.compute):
+            self.old[dt].copy_(host, non_blocking=True)
+        self._hold.append(host)                 # the pinned block lives until the round's sync
+        self.old_ready.add(dt)
+
     def _old_dev(self, dt):
         """The whole global-model group on the device (compute stream ordered after its H2D)."""
+        if dt not in self.old_ready and self.layout.nbytes <= SMALL_UPDATE_BYTES:
+            self._h2d_old_small(dt)
         if dt not in self.old_ready:
             self.compute.wait_event(self._h2d_old(dt, 0, self.layout.group_elems[dt]))
             self.old_ready.add(dt)
@@ -940,7 +954,9 @@ class FedOptPipeline(_Pipeline):
             old = self.old[dt]
             P = self.layout.group_elems[dt]
             prepare = None
-            if dt not in self.old_ready:                # stream the global model in with the chunks
+            if dt not in self.old_ready and self.layout.nbytes <= SMALL_UPDATE_BYTES:
+                self._h2d_old_small(dt)                 # a small model: one copy, on the compute stream
+            elif dt not in self.old_ready:              # stream the global model in with the chunks
                 prepare = lambda lo, hi, dt=dt: self.compute.wait_event(self._h2d_old(dt, lo, hi))  # noqa: E731
                 self.old_ready.add(dt)
             m_in = state.m[dt] if state.m is not None else None
