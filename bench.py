@@ -645,7 +645,8 @@ def main():
         transports = {"collective": None}
         if a.transport in ("auto", "p2p") and (world > 1 or rccl1):
             try:
-                transports["p2p"] = P2PAllGather(full_all)
+                # double-buffered: one fence per step (the exit fence clears the other buffer)
+                transports["p2p"] = P2PAllGather(full_all, spare=torch.empty_like(full_all))
             except Exception as e:  # noqa: BLE001 — reported; the collective stays
                 extra["p2p_error"] = f"{type(e).__name__}: {e}"
         if a.transport == "p2p" and "p2p" in transports:
@@ -716,8 +717,8 @@ def main():
         kernel = (f"{fold_kernel_label(cyc.C, in_bytes, K)} over this rank's {cyc.rounds} chunks of {cyc.C} params "
                   "(fold-only timing; max over ranks)")
         backend = dist.get_backend() if dist.is_initialized() else None
-        transport = (f"direct peer copies (P2PAllGather: IPC-mapped peer buffers, one copy stream per peer, "
-                     f"{backend} fences)" if tname == "p2p" else f"{backend} all_gather_into_tensor on a "
+        transport = (f"direct peer copies (P2PAllGather: IPC-mapped, double-buffered peer buffers, one copy "
+                     f"stream per peer, one {backend} fence per step)" if tname == "p2p" else f"{backend} all_gather_into_tensor on a "
                      "communication stream")
         config = {"workload": f"FedAvg {K} clients x {P_total} params {a.dtype}, param-sharded block-cyclically over "
                               f"{world} GPUs; each folded round gathered to every GPU while the next round folds, "

@@ -195,16 +195,18 @@ class CyclicShardedFedAvg:
 
         ``p2p``: a :class:`P2PAllGather` over this geometry's ``full_len`` buffer — round i is then
         pushed by direct copies into every peer's buffer (one copy stream per peer) instead of an RCCL
-        all-gather, and the result is ``p2p.full[:P]``, which the NEXT call overwrites: it fences on
-        entry (every rank done with the previous result) and on exit (every rank's pushes landed)."""
+        all-gather, and the result is a view of ``p2p``'s buffer: overwritten by the NEXT call (the
+        call fences on entry — every rank done with the previous result — and on exit — every
+        rank's pushes landed), or by the call after next with a double-buffered ``p2p`` (one fence
+        per call)."""
         C, W = self.C, self.world
         if p2p is not None:
             if p2p.full.numel() < self.full_len:
                 raise ValueError(f"p2p buffer has {p2p.full.numel()} elements, this geometry needs {self.full_len}")
             dev = agg_local.device
             cur = torch.cuda.current_stream(dev)
+            p2p.begin()
             out = p2p.full
-            p2p.fence()
             for i in range(self.rounds):
                 sl = slice(i * C, (i + 1) * C)
                 self.fold_fn(agg_local[sl], [u[sl] for u in updates_local], n, N, init)
@@ -260,31 +262,43 @@ class P2PAllGather:
     stream runs past it. Under RCCL it is a one-element all-reduce issued after the copy streams
     (device-side, the host does not block); under gloo (CPU tests, one-GPU rehearsals) a device
     synchronize and a barrier.
+
+    ``spare``: a second buffer of the same size makes the gather double-buffered: the steps
+    alternate between the two, so the exit fence of step t (every rank has entered step t, i.e. is
+    done with step t − 2's result in the same buffer) also clears that buffer for step t + 1's
+    pushes — one fence per step instead of two; a result then stays valid until the step after next.
     """
 
-    def __init__(self, full, group=None):
+    def __init__(self, full, group=None, spare=None):
         from . import ops
-        self.full = full
+        self.bufs = [full] if spare is None else [full, spare]
+        self.cur = 0
+        self.steps = 0
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.device = full.device
         self.esize = full.element_size()
-        handle, off = ops.ipc_handle(full)
-        mine = (handle, off, full.numel(), str(full.dtype))
+        if spare is not None and (spare.numel() != full.numel() or spare.dtype != full.dtype or
+                                  spare.device != full.device):
+            raise ValueError("P2PAllGather: the spare buffer must match the first")
+        mine = [ops.ipc_handle(b) + (b.numel(), str(b.dtype)) for b in self.bufs]
         objs = [None] * self.world
         if self.world > 1:
             dist.all_gather_object(objs, mine, group=group)
         else:
             objs = [mine]
-        for r, (_, _, n, dt) in enumerate(objs):
-            if n != full.numel() or dt != str(full.dtype):
-                raise ValueError(f"P2PAllGather: rank {r} buffer is {n} x {dt}, this rank's {full.numel()} x {full.dtype}")
-        self.peers = {}
+        for r, lst in enumerate(objs):
+            if len(lst) != len(self.bufs) or any(n != full.numel() or dt != str(full.dtype) for _, _, n, dt in lst):
+                raise ValueError(f"P2PAllGather: rank {r} buffers {[(n, dt) for _, _, n, dt in lst]}, this rank's "
+                                 f"{len(self.bufs)} x {full.numel()} x {full.dtype}")
+        self.peers = {}                            # rank -> [(base, pointer) per buffer]
         try:
-            for r, (h, o, _, _) in enumerate(objs):
+            for r, lst in enumerate(objs):
                 if r != self.rank:
-                    self.peers[r] = ops.ipc_open(h, o, self.device)
+                    self.peers[r] = []
+                    for h, o, _, _ in lst:
+                        self.peers[r].append(ops.ipc_open(h, o, self.device))
         except Exception:
             self.close(fence=False)
             raise
@@ -292,16 +306,30 @@ class P2PAllGather:
         self.nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
         self._flag = torch.zeros(1, dtype=torch.float32, device=self.device) if self.nccl else None
 
+    @property
+    def full(self):
+        """The buffer the current step gathers into."""
+        return self.bufs[self.cur]
+
+    def begin(self):
+        """Start a step: double-buffered, switch buffers (the last exit fence cleared this one);
+        single-buffered, fence (every rank is done with the previous result)."""
+        if len(self.bufs) == 2:
+            self.cur = self.steps % 2
+        elif self.steps:
+            self.fence()
+        self.steps += 1
+
     def push(self, at, src, after):
-        """Copy device tensor ``src`` to elements [at, at + len(src)) of every peer's buffer once
-        ``after`` (an event on the folding stream) has fired."""
+        """Copy device tensor ``src`` to elements [at, at + len(src)) of every peer's current buffer
+        once ``after`` (an event on the folding stream) has fired."""
         from . import ops
         if at < 0 or at + src.numel() > self.full.numel():
             raise ValueError("P2PAllGather.push: piece outside the buffer")
         nbytes = src.numel() * self.esize
         for r, st in self.streams.items():
             st.wait_event(after)
-            ops.copy_async(self.peers[r][1] + at * self.esize, src, nbytes, st)
+            ops.copy_async(self.peers[r][self.cur][1] + at * self.esize, src, nbytes, st)
 
     def fence(self):
         cur = torch.cuda.current_stream(self.device)
@@ -321,8 +349,9 @@ class P2PAllGather:
         if fence and self.peers:
             self.fence()
             torch.cuda.synchronize(self.device)
-        for r, (base, _) in list(self.peers.items()):
-            ops.ipc_close(base, self.device)
+        for r, maps in list(self.peers.items()):
+            for base, _ in maps:
+                ops.ipc_close(base, self.device)
         self.peers = {}
         if fence and self.world > 1 and dist.is_initialized():
             dist.barrier(group=self.group)       # no peer unmaps while another still copies

@@ -1365,7 +1365,7 @@ def test_sharded_gloo_world2_hip_kernel():
         assert np.array_equal(full.view(np.uint32), want.view(np.uint32)), f"rank {rank}"
 
 
-def _p2p_gloo_worker(rank, world, port, P, K, chunk, q):
+def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False):
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -1385,10 +1385,11 @@ def _p2p_gloo_worker(rank, world, port, P, K, chunk, q):
         aggc = torch.empty(cs.local_len, device="cuda:0")
         loc = [cs.local(u) for u in ups]
         full = torch.full((cs.full_len,), float("nan"), device="cuda:0")
-        p2p = P2PAllGather(full)                      # IPC handles of both ranks' buffers, opened once
+        spare = torch.full((cs.full_len,), float("nan"), device="cuda:0") if double else None
+        p2p = P2PAllGather(full, spare=spare)         # IPC handles of every rank's buffers, opened once
         outs = []
-        for step in range(3):                         # the buffer is reused: entry + exit fences
-            if step == 2:                             # a later round of the session: other updates
+        for step in range(4):                         # buffers reused: entry + exit fences, or alternation
+            if step >= 2:                             # later rounds of the session: other updates
                 loc = [cs.local(u.add(1.0)) for u in ups]
             out = cs.fold_allgather(aggc, loc, ns, Ns, init=True, p2p=p2p)
             torch.cuda.synchronize()
@@ -1399,8 +1400,9 @@ def _p2p_gloo_worker(rank, world, port, P, K, chunk, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,P,chunk", [(2, 200_003, 8192), (3, 1_000_000, 65536)])
-def test_p2p_allgather_gloo_hip(world, P, chunk):
+@pytest.mark.parametrize("world,P,chunk,double", [(2, 200_003, 8192, False), (3, 1_000_000, 65536, False),
+                                                  (2, 200_003, 8192, True), (3, 1_000_000, 65536, True)])
+def test_p2p_allgather_gloo_hip(world, P, chunk, double):
     """The direct peer-to-peer all-gather (sharded.P2PAllGather: IPC handles exchanged once,
     fa_copy_async into every peer's buffer, one copy stream per peer, entry / exit fences) with the
     HIP fold: ranks share this box's GPU (each maps the others' buffers through IPC), three steps
@@ -1417,8 +1419,8 @@ def test_p2p_allgather_gloo_hip(world, P, chunk):
     s_.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    pc = mp.start_processes(_p2p_gloo_worker, args=(world, port, P, K, chunk, q), nprocs=world, join=False,
-                            start_method="spawn")
+    pc = mp.start_processes(_p2p_gloo_worker, args=(world, port, P, K, chunk, q, double), nprocs=world,
+                            join=False, start_method="spawn")
     res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
     while not pc.join(timeout=60):
         pass
@@ -1434,7 +1436,7 @@ def test_p2p_allgather_gloo_hip(world, P, chunk):
     want, want2 = want.cpu().numpy(), want2.cpu().numpy()
     for rank, outs in res:
         for step, got in enumerate(outs):
-            w = want2 if step == 2 else want
+            w = want2 if step >= 2 else want
             assert np.array_equal(got.view(np.uint32), w.view(np.uint32)), f"rank {rank} step {step}"
 
 
