@@ -1045,7 +1045,7 @@ class GatherQueue {
             for (auto& p : batch) total += p.len;
             const int np = (int)batch.size();
             auto copy = [&](int k) { std::memcpy(batch[k].d, batch[k].s, (size_t)batch[k].len); };
-            const int t = std::min<int64_t>(threads, std::max<int64_t>(1, total >> 18));   // >= 256 KiB per thread
+            const int t = std::min<int64_t>(threads, std::max<int64_t>(1, total >> 16));   // >= 64 KiB per thread
             if (t <= 1 || np <= 1)
                 for (int k = 0; k < np; ++k) copy(k);
             else
@@ -1071,9 +1071,11 @@ extern "C" int64_t fnpz_gather_start(int n, void* const* dsts, const void* const
     for (int i = 0; i < n; ++i) {
         if (nbytes[i] < 0 || (nbytes[i] > 0 && (!dsts[i] || !srcs[i])))
             return -fail(FNPZ_EINVAL, "fnpz_gather_start: segment %d", i);
-        for (int64_t o = 0; o < nbytes[i]; o += 1 << 20)
+        // 64 KiB pieces: a small update (one tensor dominating, e.g. mnist's 200 KB first layer) still
+        // spreads over several threads
+        for (int64_t o = 0; o < nbytes[i]; o += 1 << 16)
             pieces.push_back({static_cast<uint8_t*>(dsts[i]) + o, static_cast<const uint8_t*>(srcs[i]) + o,
-                              std::min<int64_t>(1 << 20, nbytes[i] - o)});
+                              std::min<int64_t>(1 << 16, nbytes[i] - o)});
     }
     return GatherQueue::get().submit(std::move(pieces), threads);
 }

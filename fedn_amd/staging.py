@@ -40,6 +40,7 @@ RING_BYTES = 64 << 20         # pinned ring piece for host -> device streaming o
 # (~0.1 ms of host work each) cost far more than the bytes; larger updates fold on arrival
 SMALL_UPDATE_BYTES = 4 << 20
 ARENA_BYTES = 64 << 20
+ARENA_UPLOAD_EVERY = 16       # an arena's packed updates go to HBM in parts of this many, while later ones load
 
 
 def chunks(n, itemsize):
@@ -127,15 +128,16 @@ class _Slot:
 
 
 class _Arena:
-    """Pinned host + device bytes for up to ``cap`` packed small updates (see SMALL_UPDATE_BYTES)."""
-    __slots__ = ("host", "host_np", "host_ptr", "dev", "cap", "count", "done", "used")
+    """Pinned host + device bytes for up to ``cap`` packed small updates (see SMALL_UPDATE_BYTES);
+    ``uploaded`` of them already sent to HBM (partial uploads every ARENA_UPLOAD_EVERY updates)."""
+    __slots__ = ("host", "host_np", "host_ptr", "dev", "cap", "count", "uploaded", "done", "used")
 
     def __init__(self, cap, nbytes, device):
         self.host = torch.empty(cap * nbytes, dtype=torch.uint8, pin_memory=True)
         self.host_np = self.host.numpy()
         self.host_ptr = self.host.data_ptr()
         self.dev = torch.empty(cap * nbytes, dtype=torch.uint8, device=device)
-        self.cap, self.count, self.used = cap, 0, False
+        self.cap, self.count, self.uploaded, self.used = cap, 0, 0, False
         self.done = None
 
 
@@ -251,7 +253,7 @@ class _Pipeline:
             self._arena_i = (self._arena_i + 1) % len(self._arenas)
             if a.used:
                 a.done.synchronize()            # its previous H2D has read the pinned bytes
-            a.count = 0
+            a.count = a.uploaded = 0
             self._arena = a
         nb, j = self.layout.nbytes, a.count
         tic = time.perf_counter()
@@ -262,7 +264,27 @@ class _Pipeline:
         self._pack_ticket = ticket or self._pack_ticket
         self.time_pack += time.perf_counter() - tic
         a.count += 1
+        if a.count - a.uploaded >= ARENA_UPLOAD_EVERY:
+            self._upload_part(a)                # this part's H2D runs while later updates load
         return _ArenaRef(a.dev[j * nb:(j + 1) * nb])
+
+    def _upload_part(self, a):
+        """The H2D of the arena's updates packed since its last partial upload, on the compute
+        stream, once their packs have landed."""
+        tic = time.perf_counter()
+        wait_pack_jobs(self._pack_ticket)
+        self._pack_ticket, self._pack_jobs = None, []
+        self.time_pack += time.perf_counter() - tic
+        nb = self.layout.nbytes
+        lo, n = a.uploaded * nb, (a.count - a.uploaded) * nb
+        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        start.record(self.compute)
+        ops.copy_ptr_async(a.dev.data_ptr() + lo, a.host_ptr + lo, n, self.compute, self.device)
+        end.record(self.compute)
+        self._h2d.append((start, end))
+        a.uploaded = a.count
+        a.done = end
+        a.used = True
 
     def fast_host(self, arrays):
         """Whether ``arrays`` is a list of numpy arrays with exactly this round's shapes and dtypes on
@@ -284,19 +306,8 @@ class _Pipeline:
         a = self._arena
         if a is None or a.count == 0:
             return
-        tic = time.perf_counter()
-        wait_pack_jobs(self._pack_ticket)       # every pack of this arena has landed
-        self._pack_ticket, self._pack_jobs = None, []
-        self.time_pack += time.perf_counter() - tic
-        n = a.count * self.layout.nbytes
-        start = torch.cuda.Event(enable_timing=True)
-        a.done = torch.cuda.Event(enable_timing=True)
-        with torch.cuda.device(self.device):
-            start.record(self.compute)
-            ops.copy_ptr_async(a.dev.data_ptr(), a.host_ptr, n, self.compute, self.device)
-            a.done.record(self.compute)
-        self._h2d.append((start, a.done))
-        a.used = True
+        if a.count > a.uploaded:                # what the partial uploads have not sent yet
+            self._upload_part(a)
         self._arena = None
 
     def acquire(self, arrays):
