@@ -517,6 +517,17 @@ def global_chunks(geom, K, P_total, dtype, device, seed, sample):
     return loc, host
 
 
+def gathered_bits(full, device, on_cpu):
+    """(min, max) over ranks of the int64 sum of a gathered model's bits: equal when every rank
+    holds the same model."""
+    bits = full.contiguous().view(torch.int32).to(device).sum(dtype=torch.int64).reshape(1)
+    t = torch.cat([bits, -bits])
+    t = t.cpu() if on_cpu else t
+    if dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return -int(t[1]), int(t[0])
+
+
 def sample_check(got, host_sample, ns):
     """Bit-for-bit check of the first params of an aggregate against the oracle (numpy, one core) on
     the same clients' values; returns (equal, oracle seconds)."""
@@ -668,15 +679,29 @@ def main():
         tuned = {}
         if len(cands) * len(transports) > 1:
             scratch = make_updates(K, Lmax, a.dtype, device, a.seed + 1000 * rank + 1)   # timing only
+            sums = {}
             for name, tp in transports.items():
                 for R, c in geoms.items():
-                    st = make_step(c, tp, [u[:c.local_len] for u in scratch])
+                    res = [None]
+                    st = make_step(c, tp, [u[:c.local_len] for u in scratch], res)
                     for _ in range(2):
                         st()
+                    sums[(name, R)] = gathered_bits(res[0], device, rehearsal)
                     el, _ = timed_steps(st, 5, stream, world, device, rehearsal)
                     tuned[f"{name}/R{R}"] = el / 5 * 1e3
             del scratch
             torch.cuda.empty_cache()
+            # a transport whose gathered model differs from another's (same geometry, same data) or
+            # between ranks is not used: every rank computes the same verdict from all-reduced sums
+            bad = set()
+            for (name, R), (lo, hi) in sums.items():
+                ref_sum = sums.get(("collective", R))
+                if lo != hi or (ref_sum is not None and ref_sum != (lo, hi)):
+                    bad.add(name)
+            if bad:
+                extra["transport_disqualified"] = {n: "gathered model differs between ranks or from the RCCL "
+                                                      "all-gather's on the same data" for n in sorted(bad)}
+                tuned = {k: v for k, v in tuned.items() if k.split("/R")[0] not in bad}
             best = min(tuned, key=tuned.get)
             tname, R = best.split("/R")[0], int(best.split("/R")[1])
         else:
@@ -705,10 +730,8 @@ def main():
         elapsed, _ = timed_steps(step, a.steps, stream, world, device, rehearsal)
         full = res[0]
         # every rank ends the step holding the same model: int64 sum of its bits, compared over ranks
-        bits = full.contiguous().view(torch.int32).to(device).sum(dtype=torch.int64).reshape(1)
-        lohi = torch.cat([bits, -bits]).cpu() if rehearsal else torch.cat([bits, -bits])
-        dist.all_reduce(lohi, op=dist.ReduceOp.MAX)
-        consistent = bool(int(lohi[0]) == -int(lohi[1]))
+        lo_bits, hi_bits = gathered_bits(full, device, rehearsal)
+        consistent = lo_bits == hi_bits
         for _ in range(2):
             fold_only()
         _, kern_ms = timed_steps(fold_only, a.steps, stream, world, device, rehearsal)

@@ -89,31 +89,10 @@ def _check(rc):
         raise CodecError(f"fednpz status {rc}: {load_lib().fnpz_last_error().decode(errors='replace')}")
 
 
-def _ptrs(pairs):
-    n = len(pairs)
-    dsts, srcs, nb = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)(), (ctypes.c_int64 * n)()
-    for i, (d, src) in enumerate(pairs):
-        if d.nbytes != src.nbytes:
-            raise ValueError("gather: destination and source sizes differ")
-        dsts[i] = d.__array_interface__["data"][0]
-        srcs[i] = src.__array_interface__["data"][0]
-        nb[i] = d.nbytes
-    return n, dsts, srcs, nb
-
-
-def gather_start(pairs, threads):
-    """``dst[:] = src`` for each (dst, src) pair of C-contiguous numpy arrays, queued to the native
-    gather thread (``fnpz_gather_start``); returns the ticket for :func:`gather_wait`. The caller
-    keeps every array alive until then."""
-    lib = load_lib()
-    t = lib.fnpz_gather_start(*_ptrs(pairs), max(1, threads))
-    if t < 0:
-        _check(-t)
-    return t
-
-
 def gather_start_raw(dsts, srcs, nbytes, threads):
-    """:func:`gather_start` on plain addresses and byte counts (lists of ints)."""
+    """``nbytes[i]`` bytes from address ``srcs[i]`` to ``dsts[i]`` (lists of ints), queued to the native
+    gather thread (``fnpz_gather_start``); returns the ticket for :func:`gather_wait`. The caller keeps
+    every source and destination alive until then."""
     n = len(dsts)
     t = load_lib().fnpz_gather_start(n, (ctypes.c_void_p * n)(*dsts), (ctypes.c_void_p * n)(*srcs),
                                      (ctypes.c_int64 * n)(*nbytes), max(1, threads))

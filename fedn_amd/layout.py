@@ -60,22 +60,6 @@ def run_pack_jobs(jobs):
         f.result()
 
 
-def start_pack_jobs(jobs):
-    """Queue the copies to the native gather thread and return at once: a ticket for
-    :func:`wait_pack_jobs` (the caller keeps ``jobs`` referenced until then). Without the codec
-    library, or for jobs it cannot take (dtype mismatch, non-contiguous), the copies run now and
-    None is returned."""
-    ok = all(d.dtype == src.dtype and d.flags.c_contiguous and src.flags.c_contiguous for d, src in jobs)
-    if ok and jobs:
-        try:
-            from . import codec
-            return codec.gather_start(jobs, PACK_THREADS)
-        except ImportError:
-            pass
-    run_pack_jobs(jobs)
-    return None
-
-
 def start_pack_into(layout, arrays, dst_ptr):
     """Queue the pack of ``arrays`` (already checked against ``layout``: shapes and dtypes) into the
     host bytes at address ``dst_ptr`` to the native gather thread; returns (ticket, the sources to
