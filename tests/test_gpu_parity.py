@@ -1309,7 +1309,7 @@ def _hip_gloo_worker(rank, world, port, P, K, q):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import torch.distributed as dist
 
-    from fedn_amd.sharded import CyclicShardedFedAvg, ShardedFedAvg
+    from fedn_amd.sharded import CyclicShardedFedAvg, ShardedFedAvg, ShardedFedOpt
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -1326,8 +1326,15 @@ def _hip_gloo_worker(rank, world, port, P, K, q):
         cs = CyclicShardedFedAvg(P, chunk=8192)
         aggc = torch.empty(cs.local_len, device="cuda:0")
         full = cs.fold_allgather(aggc, [cs.local(u) for u in ups], ns, Ns, init=True)
+        # FedOpt: each rank's slice of old / m / v on the device, the float64 model gathered to the
+        # node's shared host model (HostGather) on rank 0
+        so = ShardedFedOpt(P)
+        out = so.step(so.local(base), [so.local(u) for u in ups], ns, Ns,
+                      {"serveropt": "adam", "learning_rate": 1e-3, "beta1": 0.9, "beta2": 0.99, "tau": 1e-4})
+        host_opt = so.gather_to_host(out)
         torch.cuda.synchronize()
-        q.put((rank, None if host is None else host.numpy().copy(), full.cpu().numpy().copy()))
+        q.put((rank, None if host is None else host.numpy().copy(), full.cpu().numpy().copy(),
+               None if host_opt is None else host_opt.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -1361,8 +1368,13 @@ def test_sharded_gloo_world2_hip_kernel():
     ops.fedavg_fold(want, ups, ns, [int(v) for v in np.cumsum(ns)], init=True)
     want = want.cpu().numpy()
     assert np.array_equal(res[0][1].view(np.uint32), want.view(np.uint32))
-    for rank, _, full in res:
+    for rank, _, full, _ in res:
         assert np.array_equal(full.view(np.uint32), want.view(np.uint32)), f"rank {rank}"
+    # FedOpt gathered to the host on rank 0 (float64) == the oracle's fedopt.py round
+    want_opt, _ = ref.fedopt_combine(ref.FedOptState(), [([u.cpu().numpy()], n) for u, n in zip(ups, ns)],
+                                     [base.cpu().numpy()], {"serveropt": "adam"})
+    assert res[0][3].dtype == np.float64 and res[1][3] is None
+    assert np.array_equal(res[0][3].view(np.uint64), want_opt[0].view(np.uint64))
 
 
 def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False):
