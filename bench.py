@@ -87,8 +87,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-achievable", dest="achievable", action="store_false",
                     help="N = 1: skip the achievable-peak copy / read reference")
-    ap.add_argument("--transport", choices=["auto", "collective", "p2p"], default="auto",
-                    help="N > 1: how each folded round reaches every GPU (auto = the faster in the untimed warm-up)")
+    ap.add_argument("--transport", choices=["auto", "collective", "p2p", "p2p_kernel"], default="auto",
+                    help="N > 1: how each folded round reaches every GPU — RCCL all-gather, direct peer DMA copies, "
+                         "or one push kernel per round (auto = the fastest in the untimed warm-up)")
     ap.add_argument("--host-clients", type=int, default=16,
                     help="host_resident side field: host numpy updates through the plug-in (0 = skip)")
     ap.add_argument("--launch-check", action="store_true", help="rank set-up only (gloo, no GPU): the launcher's test")
@@ -654,16 +655,25 @@ def main():
         Lmax = max(c.local_len for c in geoms.values())
         full_all = torch.empty(max(c.full_len for c in geoms.values()), dtype=torch.float32, device=device)
         transports = {"collective": None}
-        if a.transport in ("auto", "p2p") and (world > 1 or rccl1):
+        engines = {"p2p": "dma", "p2p_kernel": "kernel"}    # P2PAllGather.engine of each direct transport
+        if a.transport != "collective" and (world > 1 or rccl1):
             try:
-                # double-buffered: one fence per step (the exit fence clears the other buffer)
-                transports["p2p"] = P2PAllGather(full_all, spare=torch.empty_like(full_all))
+                # double-buffered: one fence per step (the exit fence clears the other buffer); ONE set of
+                # IPC mappings serves both engines (the engine is switched between steps)
+                pa = P2PAllGather(full_all, spare=torch.empty_like(full_all))
+                for name in engines:
+                    if a.transport in ("auto", name):
+                        transports[name] = pa
             except Exception as e:  # noqa: BLE001 — reported; the collective stays
                 extra["p2p_error"] = f"{type(e).__name__}: {e}"
-        if a.transport == "p2p" and "p2p" in transports:
+        if a.transport in engines and a.transport in transports:
             del transports["collective"]
-        elif a.transport == "collective":
-            transports.pop("p2p", None)
+
+        def use(name):
+            tp = transports[name]
+            if tp is not None:
+                tp.engine = engines[name]
+            return tp
         agg_all = torch.empty(Lmax, dtype=torch.float32, device=device)
 
         def make_step(c, tp, loc, res=None):
@@ -680,7 +690,8 @@ def main():
         if len(cands) * len(transports) > 1:
             scratch = make_updates(K, Lmax, a.dtype, device, a.seed + 1000 * rank + 1)   # timing only
             sums = {}
-            for name, tp in transports.items():
+            for name in transports:
+                tp = use(name)
                 for R, c in geoms.items():
                     res = [None]
                     st = make_step(c, tp, [u[:c.local_len] for u in scratch], res)
@@ -706,10 +717,11 @@ def main():
             tname, R = best.split("/R")[0], int(best.split("/R")[1])
         else:
             tname, R = next(iter(transports)), cands[0]
+        tp = use(tname)
         for name in list(transports):
-            if name != tname and transports[name] is not None:
+            other = transports[name]
+            if name != tname and other is not None and other is not tp:
                 transports.pop(name).close()
-        tp = transports[tname]
         cyc = geoms[R]
         L = cyc.local_len
         P = L
@@ -740,9 +752,11 @@ def main():
         kernel = (f"{fold_kernel_label(cyc.C, in_bytes, K)} over this rank's {cyc.rounds} chunks of {cyc.C} params "
                   "(fold-only timing; max over ranks)")
         backend = dist.get_backend() if dist.is_initialized() else None
-        transport = (f"direct peer copies (P2PAllGather: IPC-mapped, double-buffered peer buffers, one copy "
-                     f"stream per peer, one {backend} fence per step)" if tname == "p2p" else f"{backend} all_gather_into_tensor on a "
-                     "communication stream")
+        transport = {"p2p": f"direct peer copies (P2PAllGather: IPC-mapped, double-buffered peer buffers, one DMA copy "
+                            f"stream per peer, one {backend} fence per step)",
+                     "p2p_kernel": f"direct peer pushes (P2PAllGather engine 'kernel': IPC-mapped, double-buffered peer "
+                                   f"buffers, one fa_push kernel per round storing into every peer, one {backend} fence "
+                                   "per step)"}.get(tname, f"{backend} all_gather_into_tensor on a communication stream")
         config = {"workload": f"FedAvg {K} clients x {P_total} params {a.dtype}, param-sharded block-cyclically over "
                               f"{world} GPUs; each folded round gathered to every GPU while the next round folds, "
                               "inside the timed step (BASELINE configs[2])",

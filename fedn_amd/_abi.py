@@ -80,7 +80,10 @@ EXPORTS = {
                                    ctypes.POINTER(ctypes.c_void_p)]),
     "fa_ipc_close": (ctypes.c_int, [ctypes.c_void_p]),
     "fa_copy_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "fa_push": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                               ctypes.c_void_p]),
     "fa_peer_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "fa_host_device_ptr": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "fa_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "fa_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
 }
@@ -94,7 +97,7 @@ PROBE_EXPORTS = {
     "fa_stream_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 IPC_HANDLE_BYTES = 64    # FA_IPC_HANDLE_BYTES
 
 

@@ -49,12 +49,35 @@ def build_codec(force=False, verbose=True):
     return NPZ_OUT
 
 
+FASTPACK_SRC = os.path.join(HERE, "csrc", "fastpack.c")
+FASTPACK_OUT = os.path.join(HERE, "_fastpack.so")       # CPython extension: ``fedn_amd._fastpack``
+
+
+def build_fastpack(force=False, verbose=True):
+    """The small-update admission + pack extension (C, CPython and numpy C API; no GPU code)."""
+    if not force and not _stale(FASTPACK_OUT, FASTPACK_SRC):
+        return FASTPACK_OUT
+    import sysconfig
+
+    import numpy
+    cc = os.environ.get("CC") or shutil.which("gcc") or "gcc"
+    tmp = FASTPACK_OUT + ".tmp"
+    cmd = [cc, "-O2", "-fPIC", "-shared", "-Wall", "-I", sysconfig.get_paths()["include"], "-I", numpy.get_include(),
+           "-o", tmp, FASTPACK_SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, FASTPACK_OUT)
+    return FASTPACK_OUT
+
+
 def build(force=False, verbose=True):
-    """Product library, probe library and codec; the two hipcc builds run concurrently."""
+    """Product library, probe library, codec and the pack extension; the two hipcc builds run
+    concurrently."""
     from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(3) as ex:
+    with ThreadPoolExecutor(4) as ex:
         futs = [ex.submit(build_codec, force, verbose), ex.submit(build_hip, force, verbose),
-                ex.submit(build_hip, force, verbose, True)]
+                ex.submit(build_hip, force, verbose, True), ex.submit(build_fastpack, force, verbose)]
         for f in futs:
             f.result()
     return OUT

@@ -1310,6 +1310,49 @@ k_cast(TO* __restrict__ out, const TI* __restrict__ in, const CastGeom g, const 
     }
 }
 
+// ----------------------------------------------------------------------------
+// k_push: one folded piece to every peer's copy of the model (fa_push; sharded.P2PAllGather's
+// "kernel" engine). Each lane loads a 16-B word of the piece ONCE and stores it to every
+// destination: the piece crosses each peer's own xGMI link once, all links at once, and local HBM
+// is read once instead of once per DMA copy. The stores are plain vector stores (non-temporal:
+// nothing here is read back by this GPU); the end-of-grid system-scope release makes them visible
+// to the peers before the stream's next operation (the fence the ranks exchange).
+// ----------------------------------------------------------------------------
+constexpr int kPushMax = 16;
+constexpr int kPushWords = 4;                    // 16-B words per lane per iteration (64 B in flight)
+struct PushTable {
+    u32x4* dst[kPushMax];
+};
+
+__global__ void __launch_bounds__(kBlock) k_push(PushTable t, int nd, const u32x4* __restrict__ src, int64_t n16) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock * kPushWords;
+    for (int64_t base = (int64_t)blockIdx.x * kBlock * kPushWords + threadIdx.x; base < n16; base += stride) {
+        u32x4 v[kPushWords];
+#pragma unroll
+        for (int j = 0; j < kPushWords; ++j) {
+            const int64_t i = base + (int64_t)j * kBlock;
+            if (i < n16) v[j] = __builtin_nontemporal_load(src + i);
+        }
+        for (int d = 0; d < nd; ++d) {
+            u32x4* __restrict__ o = t.dst[d];
+#pragma unroll
+            for (int j = 0; j < kPushWords; ++j) {
+                const int64_t i = base + (int64_t)j * kBlock;
+                if (i < n16) __builtin_nontemporal_store(v[j], o + i);
+            }
+        }
+    }
+    __threadfence_system();
+}
+
+// the < 16 B tail of a piece whose length is not a multiple of 16 (one lane per byte)
+__global__ void k_push_tail(PushTable t, int nd, const uint8_t* __restrict__ src, int64_t off, int rem) {
+    const int b = threadIdx.x;
+    if (b < rem)
+        for (int d = 0; d < nd; ++d) reinterpret_cast<uint8_t*>(t.dst[d])[off + b] = src[off + b];
+    __threadfence_system();
+}
+
 #ifdef FEDAGG_PROBES
 // ----------------------------------------------------------------------------
 // measurement kernels (libfedagg_probe.so only)
@@ -2164,6 +2207,49 @@ int fa_copy_async(void* dst, const void* src, int64_t bytes, void* stream) {
     return FA_OK;
 }
 
+int fa_push(void* const* dsts, int ndst, const void* src, int64_t bytes, void* stream) {
+    g_err[0] = 0;
+    if (ndst < 0 || ndst > kPushMax || bytes < 0 || (bytes > 0 && (!src || (ndst > 0 && !dsts))))
+        return fail(FA_EINVAL, "fa_push: bad arguments (at most %d destinations)", kPushMax);
+    if (bytes == 0 || ndst == 0) return FA_OK;
+    PushTable t{};
+    for (int d = 0; d < ndst; ++d) {
+        if (!dsts[d]) return fail(FA_EINVAL, "fa_push: destination %d is null", d);
+        if (reinterpret_cast<uintptr_t>(dsts[d]) % 16) return fail(FA_EINVAL, "fa_push: destination %d not 16-B aligned", d);
+        t.dst[d] = static_cast<u32x4*>(dsts[d]);
+    }
+    if (reinterpret_cast<uintptr_t>(src) % 16) return fail(FA_EINVAL, "fa_push: source not 16-B aligned");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int64_t n16 = bytes / 16;
+    const int rem = (int)(bytes % 16);
+    if (n16 > 0) {
+        // link-bound, not HBM-bound: a few hundred workgroups keep every link's writes in flight and
+        // leave most of the chip to the fold running beside it
+        const int64_t need = (n16 + (int64_t)kBlock * kPushWords - 1) / ((int64_t)kBlock * kPushWords);
+        const int grid = (int)std::min<int64_t>(need, 512);
+        hipLaunchKernelGGL(k_push, dim3(grid), dim3(kBlock), 0, st, t, ndst, static_cast<const u32x4*>(src), n16);
+    }
+    if (rem > 0)
+        hipLaunchKernelGGL(k_push_tail, dim3(1), dim3(64), 0, st, t, ndst, static_cast<const uint8_t*>(src), n16 * 16,
+                           rem);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(FA_EHIP, "fa_push: %s", hipGetErrorString(e));
+    return FA_OK;
+}
+
+int fa_host_device_ptr(const void* host, void** dptr) {
+    g_err[0] = 0;
+    if (!host || !dptr) return fail(FA_EINVAL, "fa_host_device_ptr: null argument");
+    void* d = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&d, const_cast<void*>(host), 0);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(FA_EHIP, "fa_host_device_ptr: %s (not page-locked host memory?)", hipGetErrorString(e));
+    }
+    *dptr = d;
+    return FA_OK;
+}
+
 int fa_host_register(void* p, int64_t bytes) {
     g_err[0] = 0;
     if (!p || bytes <= 0) return fail(FA_EINVAL, "fa_host_register: bad arguments");
@@ -2188,10 +2274,10 @@ int fa_peer_enable(int dev, int peer) {
     if (e != hipSuccess) return fail(FA_EHIP, "fa_peer_enable: hipDeviceCanAccessPeer: %s", hipGetErrorString(e));
     if (!can) return fail(FA_EHIP, "fa_peer_enable: device %d cannot access device %d", dev, peer);
     int cur = 0;
-    hipGetDevice(&cur);
+    (void)hipGetDevice(&cur);
     e = hipSetDevice(dev);
     if (e == hipSuccess) e = hipDeviceEnablePeerAccess(peer, 0);
-    hipSetDevice(cur);
+    (void)hipSetDevice(cur);
     if (e == hipErrorPeerAccessAlreadyEnabled) {
         (void)hipGetLastError();
         return FA_OK;

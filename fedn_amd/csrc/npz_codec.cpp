@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdint>
@@ -993,7 +994,13 @@ class CopyPool {
 // updates one after the other (staging arenas) hands each update's copies to one background thread
 // and goes on with the next update; the thread takes every queued job at once and copies them on the
 // CopyPool. Jobs complete in submission order, so a ticket is done once the completed count reaches
-// it. One queue per process (fork-safe like CopyPool); its thread parks when idle.
+// it. One queue per process (fork-safe like CopyPool).
+//
+// Latency: a round of a small model queues a few jobs tens of microseconds apart and then waits for
+// the last one right away, so a thread that parks between jobs (a futex wake-up on each side costs
+// ~10-20 us) would cost more than the copies. The worker therefore spins for kSpinUs after a job
+// before parking, and a waiter spins as long for its ticket before blocking; a batch under
+// kThreadBytes per thread is copied by the worker alone (waking pool threads costs more).
 class GatherQueue {
    public:
     struct Piece {
@@ -1001,6 +1008,8 @@ class GatherQueue {
         const uint8_t* s;
         int64_t len;
     };
+    static constexpr int64_t kSpinUs = 200;
+    static constexpr int64_t kThreadBytes = 512 << 10;
     static GatherQueue& get() {
         static std::mutex m;
         static GatherQueue* q = nullptr;
@@ -1021,23 +1030,38 @@ class GatherQueue {
         const int64_t t = ++issued_;
         for (auto& p : pieces) pending_.push_back(p);
         threads_ = std::max(threads_, threads);
-        last_ = t;
+        last_.store(t, std::memory_order_release);
         cv_.notify_one();
         return t;
     }
     void wait(int64_t t) {
+        if (spin_until([&] { return done_.load(std::memory_order_acquire) >= t; })) return;
         std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [&] { return done_ >= t; });
+        done_cv_.wait(lk, [&] { return done_.load(std::memory_order_acquire) >= t; });
     }
 
    private:
+    template <class F>
+    static bool spin_until(F ready) {
+        const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(kSpinUs);
+        for (int i = 0;; ++i) {
+            if (ready()) return true;
+            if ((i & 63) == 63 && std::chrono::steady_clock::now() > end) return false;
+            __builtin_ia32_pause();
+        }
+    }
     void work() {
         std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
-            cv_.wait(lk, [&] { return last_ > done_; });        // a job (possibly with no bytes) is queued
+            if (last_.load(std::memory_order_relaxed) <= done_.load(std::memory_order_relaxed)) {
+                lk.unlock();                                 // idle: spin a while before parking
+                spin_until([&] { return last_.load(std::memory_order_acquire) > done_.load(std::memory_order_relaxed); });
+                lk.lock();
+            }
+            cv_.wait(lk, [&] { return last_.load(std::memory_order_relaxed) > done_.load(std::memory_order_relaxed); });
             std::vector<Piece> batch;
             batch.swap(pending_);
-            const int64_t upto = last_;
+            const int64_t upto = last_.load(std::memory_order_relaxed);
             const int threads = threads_;
             threads_ = 1;
             lk.unlock();
@@ -1045,20 +1069,21 @@ class GatherQueue {
             for (auto& p : batch) total += p.len;
             const int np = (int)batch.size();
             auto copy = [&](int k) { std::memcpy(batch[k].d, batch[k].s, (size_t)batch[k].len); };
-            const int t = std::min<int64_t>(threads, std::max<int64_t>(1, total >> 16));   // >= 64 KiB per thread
+            const int t = (int)std::min<int64_t>(threads, std::max<int64_t>(1, total / kThreadBytes));
             if (t <= 1 || np <= 1)
                 for (int k = 0; k < np; ++k) copy(k);
             else
                 CopyPool::get().run(std::min(t, np), np, copy);
             lk.lock();
-            done_ = upto;
+            done_.store(upto, std::memory_order_release);
             done_cv_.notify_all();
         }
     }
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
     std::vector<Piece> pending_;
-    int64_t issued_ = 0, last_ = 0, done_ = 0;
+    int64_t issued_ = 0;
+    std::atomic<int64_t> last_{0}, done_{0};
     int threads_ = 1;
     bool started_ = false;
 };

@@ -81,6 +81,46 @@ def start_pack_into(layout, arrays, dst_ptr):
     return None, srcs
 
 
+_FAST = None          # (admit, address of fnpz_gather_start) once loaded; False: extension not built
+
+
+def _fast():
+    global _FAST
+    if _FAST is None:
+        try:
+            from . import _fastpack, codec
+            _FAST = (_fastpack.admit, ctypes.cast(codec.load_lib().fnpz_gather_start, ctypes.c_void_p).value)
+        except ImportError:
+            _FAST = False
+    return _FAST
+
+
+def fast_admission(layout):
+    """``admit(arrays, dst_ptr) -> ticket | 0 | -1`` for ``layout`` (cached on it): the exact
+    (shape, dtype, C-contiguous) test of a host update and the queueing of its pack into the pinned
+    bytes at ``dst_ptr`` in ONE native call (``_fastpack``, csrc/fastpack.c); -1 leaves everything
+    untouched (not this layout). None if the extension or the codec library is not built."""
+    f = getattr(layout, "_fast_admit", 0)
+    if f == 0:
+        f = None
+        fast = _fast()
+        if fast:
+            from . import _fastpack
+            admit, gstart = fast
+            offs = {i: off for i, off, _ in layout.pack_plan}
+            plan = _fastpack.plan([(tuple(sh), np.dtype(dt), offs.get(i, 0))
+                                   for i, (sh, dt) in enumerate(zip(layout.shapes, layout.dtypes))])
+
+            def f(arrays, dst_ptr, plan=plan, admit=admit, gstart=gstart):
+                t = admit(plan, arrays, dst_ptr, gstart, PACK_THREADS)
+                if t == -2:
+                    from . import codec
+                    codec.gather_wait(-1)       # raises the codec's last error
+                return t
+        layout._fast_admit = f
+    return f
+
+
 def wait_pack_jobs(ticket):
     if ticket is not None:
         from . import codec

@@ -58,13 +58,17 @@ def gather_group(layout, bounds, devices, per_dev, dt):
     return flat.numpy()   # a new pinned block owned by the caller (see staging._Pipeline._to_host)
 
 
-def allgather_devices(parts, P):
+def allgather_devices(parts, P, engine="dma"):
     """The in-process form of the sliced all-gather: ``parts`` = [(device, slice
     tensor on it, lo)] covering [0, P); returns one full P-element model per device. Device d's slice
-    is copied straight into every other device's model by DMA over the d -> e link (``fa_copy_async``
-    after ``fa_peer_enable``), one copy stream per (source, destination) pair, so all links run at
-    once; each destination's current stream then waits for the copies into it. A device listed
+    goes straight into every other device's model over the d -> e link (after ``fa_peer_enable``),
+    all links at once: ``engine="dma"`` copies it with one ``fa_copy_async`` per (source,
+    destination) pair, each on its own stream; ``engine="kernel"`` with ONE ``fa_push`` launch per
+    source that reads the slice once and stores it into every destination (sharded.P2PAllGather's
+    two engines). Each destination's current stream then waits for what lands in it. A device listed
     twice (tests on a one-GPU box) gets its own model buffer per entry."""
+    if engine not in ("dma", "kernel"):
+        raise ValueError("allgather_devices: engine must be 'dma' or 'kernel'")
     parts = [(torch.device(dv), t, lo) for dv, t, lo in parts]
     fulls = []
     for d, (dv, t, lo) in enumerate(parts):
@@ -78,9 +82,19 @@ def allgather_devices(parts, P):
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(src_dev))
         es = t.element_size()
-        for j, (dst_dev, _, _) in enumerate(parts):
+        for dst_dev, _, _ in parts:
             if src_dev.index != dst_dev.index:
                 ops.peer_enable(src_dev.index, dst_dev.index)
+        if engine == "kernel":
+            st = torch.cuda.Stream(src_dev)
+            st.wait_event(ready)
+            ops.push([f.data_ptr() + lo * es for f in fulls], t, t.numel() * es, st)
+            ev = torch.cuda.Event()
+            ev.record(st)
+            for j in range(len(parts)):
+                done[j].append((ev, st))
+            continue
+        for j in range(len(parts)):
             st = torch.cuda.Stream(src_dev)
             st.wait_event(ready)
             ops.copy_async(fulls[j].data_ptr() + lo * es, t, t.numel() * es, st)

@@ -471,9 +471,43 @@ def copy_ptr_async(dst_ptr, src_ptr, nbytes, stream, device):
         _abi.check(_abi.load().fa_copy_async(int(dst_ptr), int(src_ptr), int(nbytes), ctypes_stream(stream)))
 
 
+def push(dst_ptrs, src, nbytes, stream):
+    """``nbytes`` of device tensor ``src`` (from its start) to every device address in ``dst_ptrs``
+    on ``stream`` with ONE kernel (``fa_push``): the source is read once, each destination written
+    over its own link (IPC mappings of peers' buffers, or other devices' buffers in-process)."""
+    lib = _abi.load()
+    if nbytes > src.numel() * src.element_size():
+        raise ValueError("push: more bytes than the source holds")
+    n = len(dst_ptrs)
+    with torch.cuda.device(src.device):
+        _abi.check(lib.fa_push((ctypes.c_void_p * max(1, n))(*[int(p) for p in dst_ptrs]), n, src.data_ptr(),
+                               int(nbytes), ctypes_stream(stream)))
+
+
 def peer_enable(dev, peer):
     """Direct access of device ``dev`` to device ``peer``'s memory (in-process multi-GPU)."""
     _abi.check(_abi.load().fa_peer_enable(int(dev), int(peer)))
+
+
+def host_device_ptr(host_ptr, device):
+    """Device address of page-locked host memory at ``host_ptr`` (raises for pageable memory)."""
+    out = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        _abi.check(_abi.load().fa_host_device_ptr(int(host_ptr), ctypes.byref(out)))
+    return int(out.value or 0)
+
+
+def fedavg_fold_raw(out_ptr, out_dtype, P, ptrs, upd_dtype, n, N, init, stream, device):
+    """:func:`fedavg_fold_ptrs` into ``P`` elements of ``out_dtype`` at device address ``out_ptr``
+    (e.g. pinned host memory's device address: the model lands on the host with no D2H copy)."""
+    K = len(ptrs)
+    if len(n) != K or len(N) != K:
+        raise ValueError("n and N must have one entry per update")
+    with torch.cuda.device(device):
+        _abi.check(_abi.load().fa_fedavg_fold(int(out_ptr), fa_dtype(out_dtype), (ctypes.c_void_p * max(1, K))(*ptrs),
+                                              fa_dtype(upd_dtype), (ctypes.c_double * max(1, K))(*n),
+                                              (ctypes.c_double * max(1, K))(*N), K, int(P), int(bool(init)),
+                                              ctypes_stream(stream)))
 
 
 def host_register(t):

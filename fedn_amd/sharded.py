@@ -263,14 +263,26 @@ class P2PAllGather:
     (device-side, the host does not block); under gloo (CPU tests, one-GPU rehearsals) a device
     synchronize and a barrier.
 
+    ``engine``: how a piece reaches the peers — ``"dma"``, one ``hipMemcpyAsync`` per peer on that
+    peer's stream (the DMA engines; each copy reads the piece from local HBM again), or
+    ``"kernel"``, ONE ``fa_push`` launch on a push stream that reads the piece once and stores it
+    into every peer's buffer (the CUs drive all links at once; it shares the chip with the next
+    round's fold). Which one moves a node's links faster is measured there (``bench.py`` chooses in
+    its warm-up); the attribute may be switched between steps.
+
     ``spare``: a second buffer of the same size makes the gather double-buffered: the steps
     alternate between the two, so the exit fence of step t (every rank has entered step t, i.e. is
     done with step t − 2's result in the same buffer) also clears that buffer for step t + 1's
     pushes — one fence per step instead of two; a result then stays valid until the step after next.
     """
 
-    def __init__(self, full, group=None, spare=None):
+    ENGINES = ("dma", "kernel")
+
+    def __init__(self, full, group=None, spare=None, engine="dma"):
         from . import ops
+        if engine not in self.ENGINES:
+            raise ValueError(f"P2PAllGather: engine must be one of {self.ENGINES}")
+        self.engine = engine
         self.bufs = [full] if spare is None else [full, spare]
         self.cur = 0
         self.steps = 0
@@ -303,6 +315,7 @@ class P2PAllGather:
             self.close(fence=False)
             raise
         self.streams = {r: torch.cuda.Stream(self.device) for r in self.peers}
+        self.push_stream = torch.cuda.Stream(self.device)       # the "kernel" engine's launches
         self.nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
         self._flag = torch.zeros(1, dtype=torch.float32, device=self.device) if self.nccl else None
 
@@ -327,6 +340,12 @@ class P2PAllGather:
         if at < 0 or at + src.numel() > self.full.numel():
             raise ValueError("P2PAllGather.push: piece outside the buffer")
         nbytes = src.numel() * self.esize
+        if self.engine == "kernel":
+            if self.peers:
+                self.push_stream.wait_event(after)
+                ops.push([maps[self.cur][1] + at * self.esize for maps in self.peers.values()], src, nbytes,
+                         self.push_stream)
+            return
         for r, st in self.streams.items():
             st.wait_event(after)
             ops.copy_async(self.peers[r][self.cur][1] + at * self.esize, src, nbytes, st)
@@ -335,6 +354,7 @@ class P2PAllGather:
         cur = torch.cuda.current_stream(self.device)
         for st in self.streams.values():
             cur.wait_stream(st)
+        cur.wait_stream(self.push_stream)
         if self.world == 1 or not dist.is_initialized():
             return
         if self.nccl:

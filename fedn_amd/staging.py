@@ -20,6 +20,7 @@ P*(4K+48) bytes, instead of ~P*(28K) with pg through HBM per update). The result
 overlaps that final fold chunk by chunk. The fold order, and so every bit, is unchanged:
 a multi-client launch replays the same recurrence (tests/test_gpu_parity.py).
 """
+import os
 import time
 
 import numpy as np
@@ -27,7 +28,7 @@ import torch
 
 from . import mixed, ops
 from .ingest import StagedModel
-from .layout import Layout, parallel_copy, start_pack_into, wait_pack_jobs
+from .layout import Layout, fast_admission, parallel_copy, start_pack_into, wait_pack_jobs
 
 
 BATCH = 64                    # device-resident updates folded per launch (the kernarg client table)
@@ -41,6 +42,10 @@ RING_BYTES = 64 << 20         # pinned ring piece for host -> device streaming o
 SMALL_UPDATE_BYTES = 4 << 20
 ARENA_BYTES = 64 << 20
 ARENA_UPLOAD_EVERY = 16       # an arena's packed updates go to HBM in parts of this many, while later ones load
+# a FedAvg round whose updates all wait in one arena, not yet uploaded, and hold at most this many
+# bytes in total folds them straight from the pinned arena into the caller's pinned result block:
+# the kernel reads and writes host memory over PCIe, with no H2D / D2H copy to enqueue and order
+ZERO_COPY_BYTES = int(os.environ.get("FEDN_AMD_ZERO_COPY_BYTES", str(4 << 20)))
 
 
 def chunks(n, itemsize):
@@ -130,23 +135,37 @@ class _Slot:
 class _Arena:
     """Pinned host + device bytes for up to ``cap`` packed small updates (see SMALL_UPDATE_BYTES);
     ``uploaded`` of them already sent to HBM (partial uploads every ARENA_UPLOAD_EVERY updates)."""
-    __slots__ = ("host", "host_np", "host_ptr", "dev", "cap", "count", "uploaded", "done", "used")
+    __slots__ = ("host", "host_np", "host_ptr", "dev", "dev_ptr", "cap", "count", "uploaded", "done", "used",
+                 "host_dev")
 
     def __init__(self, cap, nbytes, device):
         self.host = torch.empty(cap * nbytes, dtype=torch.uint8, pin_memory=True)
         self.host_np = self.host.numpy()
         self.host_ptr = self.host.data_ptr()
         self.dev = torch.empty(cap * nbytes, dtype=torch.uint8, device=device)
+        self.dev_ptr = self.dev.data_ptr()
         self.cap, self.count, self.uploaded, self.used = cap, 0, 0, False
         self.done = None
+        self.host_dev = None          # device address of ``host`` (zero-copy rounds), once asked for
 
 
 class _ArenaRef:
-    """One update's bytes inside an arena: ``dev`` is the view the batch's fold reads."""
-    __slots__ = ("dev",)
+    """One update's bytes inside an arena: ``ptr`` is the device address the batch's fold reads
+    (``dev``, the tensor view, is made only when a path needs one)."""
+    __slots__ = ("ptr", "_arena", "_lo", "_hi")
 
-    def __init__(self, dev):
-        self.dev = dev
+    def __init__(self, arena, lo, hi):
+        self.ptr = arena.dev_ptr + lo
+        self._arena, self._lo, self._hi = arena, lo, hi
+
+    @property
+    def dev(self):
+        return self._arena.dev[self._lo:self._hi]
+
+
+def _addr(src):
+    """Device address of a staged update's bytes (an arena piece, a slot or a StagedModel)."""
+    return src.ptr if type(src) is _ArenaRef else src.dev.data_ptr()
 
 
 class _Pipeline:
@@ -196,6 +215,8 @@ class _Pipeline:
                 plain = False
             fast = layout._fast_admission = (sig, plain)
         self._sig, self._plain = fast
+        # the same test and the pack's queueing in one native call (layout.fast_admission)
+        self._admit = fast_admission(layout) if self.batch_host and self._plain else None
         self._d2h_on_compute = False             # a small result was copied back on the compute stream
         self._synced = False                     # the result is on the host: every recorded event fired
         self._copy_used = False                  # work was enqueued on the copy stream this round
@@ -241,9 +262,11 @@ class _Pipeline:
         s.used = True
         return s
 
-    def put_small(self, arrays):
+    def put_small(self, arrays, fast=False):
         """Pack a small host update into the arena being filled (no H2D yet); returns the
-        reference the batch's fold reads once ``upload_arena`` has run."""
+        reference the batch's fold reads once ``upload_arena`` has run. ``fast``: admit it through
+        the native test first (``self._admit``); None, with nothing changed, if ``arrays`` is not
+        exactly this layout."""
         a = self._arena
         if a is None:
             if not self._arenas:
@@ -259,14 +282,20 @@ class _Pipeline:
         tic = time.perf_counter()
         # the copies go to the native gather thread and run while the next updates are loaded;
         # upload_arena waits for them (the source arrays stay referenced until then)
-        ticket, keep = start_pack_into(self.layout, arrays, a.host_ptr + j * nb)
+        if fast:
+            ticket = self._admit(arrays, a.host_ptr + j * nb)
+            if ticket < 0:
+                return None
+            keep = arrays
+        else:
+            ticket, keep = start_pack_into(self.layout, arrays, a.host_ptr + j * nb)
         self._pack_jobs.append(keep)
         self._pack_ticket = ticket or self._pack_ticket
         self.time_pack += time.perf_counter() - tic
         a.count += 1
         if a.count - a.uploaded >= ARENA_UPLOAD_EVERY:
             self._upload_part(a)                # this part's H2D runs while later updates load
-        return _ArenaRef(a.dev[j * nb:(j + 1) * nb])
+        return _ArenaRef(a, j * nb, (j + 1) * nb)
 
     def _upload_part(self, a):
         """The H2D of the arena's updates packed since its last partial upload, on the compute
@@ -279,7 +308,7 @@ class _Pipeline:
         lo, n = a.uploaded * nb, (a.count - a.uploaded) * nb
         start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         start.record(self.compute)
-        ops.copy_ptr_async(a.dev.data_ptr() + lo, a.host_ptr + lo, n, self.compute, self.device)
+        ops.copy_ptr_async(a.dev_ptr + lo, a.host_ptr + lo, n, self.compute, self.device)
         end.record(self.compute)
         self._h2d.append((start, end))
         a.uploaded = a.count
@@ -475,7 +504,15 @@ class FedAvgPipeline(_Pipeline):
         staged and folded on arrival (after any pending batch, keeping FIFO order). An update
         whose dtypes or shapes differ from the first's moves the round to the per-tensor path
         (numpy promotion / broadcasting, mixed.py) — checked before any state changes."""
-        if self.general is None and type(arrays) is list and self.fast_host(arrays):
+        if self._admit is not None and self.general is None and type(arrays) is list:
+            ref = self.put_small(arrays, fast=True)                 # a small float model's update
+            if ref is not None:
+                self.pending.append((ref, n, N))
+                if len(self.pending) >= BATCH or self.arena_full():
+                    self._flush()
+                self.nfolds += 1
+                return
+        elif self.general is None and type(arrays) is list and self.fast_host(arrays):
             self.pending.append((self.put_small(arrays), n, N))      # a small float model's update
             if len(self.pending) >= BATCH or self.arena_full():
                 self._flush()
@@ -520,13 +557,13 @@ class FedAvgPipeline(_Pipeline):
         layout, so the client table is plain addresses (no per-update tensor views: for small models
         those cost more than the launch)."""
         off = self.layout.group_byte_offset[dt] + lo * dt.itemsize
-        ptrs = [e[0].dev.data_ptr() + off for e in entries]
+        ptrs = [_addr(e[0]) + off for e in entries]
         ns = [e[1] for e in entries]
         Ns = [e[2] for e in entries]
         acc = self._agg(dt)[lo:hi]
         upd_dt = ops.torch_dtype(dt)
         if init:                                # agg := first update, then fold (fedavg.py:127-133)
-            ops.fedavg_fold_ptrs(acc, [self.first.dev.data_ptr() + off] + ptrs, upd_dt, [0.0] + ns, [1.0] + Ns,
+            ops.fedavg_fold_ptrs(acc, [_addr(self.first) + off] + ptrs, upd_dt, [0.0] + ns, [1.0] + Ns,
                                  init=True, stream=self.compute)
         else:
             ops.fedavg_fold_ptrs(acc, ptrs, upd_dt, ns, Ns, init=False, stream=self.compute)
@@ -568,6 +605,10 @@ class FedAvgPipeline(_Pipeline):
         if self.general is not None:
             return self.general.result()
         tic = time.perf_counter()
+        out = self._zero_copy_result()
+        if out is not None:
+            self.time_d2h += time.perf_counter() - tic
+            return out
         self.upload_arena()
         entries, self.pending = self.pending, []
         init = not self.agg_started
@@ -588,6 +629,53 @@ class FedAvgPipeline(_Pipeline):
             self.d2h.synchronize()
         self._synced = self._d2h_on_compute and not self._d2h_used and not self._copy_used
         self.time_d2h += time.perf_counter() - tic
+        out = [None] * len(self.layout.shapes)
+        for dt in self.layout.groups:
+            self.layout.unpack_group(hosts[dt].numpy(), dt, out, copy=False)
+        return out
+
+    def _zero_copy_result(self):
+        """A small round that never left the host: the first update and every pending one wait in the
+        arena being filled, none uploaded yet, at most ZERO_COPY_BYTES in all. ONE launch per dtype
+        group folds them reading the pinned arena and writing the new pinned result block through
+        their device addresses (fa_host_device_ptr) — the same kernel and client table as the
+        device path, so the same bits — and one synchronize ends the round. None if not such a round."""
+        a = self._arena
+        if (self.agg_started or a is None or a.uploaded or not self.pending or type(self.first) is not _ArenaRef
+                or self.first._arena is not a or a.count * self.layout.nbytes > ZERO_COPY_BYTES):
+            return None
+        entries = self.pending
+        if any(type(e[0]) is not _ArenaRef or e[0]._arena is not a for e in entries):
+            return None
+        try:
+            if a.host_dev is None:
+                a.host_dev = ops.host_device_ptr(a.host_ptr, self.device)
+        except Exception:  # noqa: BLE001 — no device mapping of the arena: the copy path
+            return None
+        wait_pack_jobs(self._pack_ticket)
+        self._pack_ticket, self._pack_jobs = None, []
+        self.pending, self._arena = [], None
+        ns, Ns = [0.0] + [e[1] for e in entries], [1.0] + [e[2] for e in entries]
+        span = self._kernel_span()
+        hosts = {}
+        for dt in self.layout.groups:
+            t = ops.torch_dtype(dt)
+            rdt = ops.fold_result_dtype(t, t)
+            n = self.layout.group_elems[dt]
+            host = torch.empty(n, dtype=rdt, pin_memory=True)
+            off = self.layout.group_byte_offset[dt]
+            ptrs = [a.host_dev + self.first._lo + off] + [a.host_dev + e[0]._lo + off for e in entries]
+            ops.fedavg_fold_raw(ops.host_device_ptr(host.data_ptr(), self.device), rdt, n, ptrs, t, ns, Ns, True,
+                                self.compute, self.device)
+            hosts[dt] = host
+        self._end_span(span)
+        self.agg_started = True
+        a.done = torch.cuda.Event()
+        a.done.record(self.compute)             # the arena's pinned bytes are read until here
+        a.used = True
+        self.compute.synchronize()
+        self._d2h_on_compute = True
+        self._synced = not self._d2h_used and not self._copy_used
         out = [None] * len(self.layout.shapes)
         for dt in self.layout.groups:
             self.layout.unpack_group(hosts[dt].numpy(), dt, out, copy=False)
@@ -858,7 +946,15 @@ class FedOptPipeline(_Pipeline):
         join the pending batch, which the server step folds in its fused launch; host arrays
         are staged and folded into pg on arrival (after any pending batch). Updates that differ
         from the first in dtype or shape, or from the global model in shape, run per tensor."""
-        if self.general is None and self.fused_ok and type(arrays) is list and self.fast_host(arrays):
+        if self._admit is not None and self.general is None and self.fused_ok and type(arrays) is list:
+            ref = self.put_small(arrays, fast=True)                 # a small float model's update
+            if ref is not None:
+                self.pending.append((ref, n, N))
+                if len(self.pending) >= BATCH or self.arena_full():
+                    self._flush()
+                self.nfolds += 1
+                return
+        elif self.general is None and self.fused_ok and type(arrays) is list and self.fast_host(arrays):
             self.pending.append((self.put_small(arrays), n, N))      # a small float model's update
             if len(self.pending) >= BATCH or self.arena_full():
                 self._flush()

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 4
+#define FA_ABI_VERSION 5
 
 /* element type codes */
 enum fa_dtype {
@@ -258,20 +258,32 @@ int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, co
  * fa_ipc_close       unmap a mapping fa_ipc_open returned
  * fa_copy_async      bytes from src to dst on stream; any two device pointers of this process
  *                    (IPC mappings and other devices' buffers included): the DMA engines move them
+ * fa_push            bytes from src to each of ndst (<= 16) destinations on stream, by a kernel: the
+ *                    source is read once and every destination (IPC mappings of the peers' model
+ *                    buffers, or in-process peers' buffers) written by vector stores — each over its
+ *                    own link, all at once; 16-B aligned pointers. The alternative to one
+ *                    fa_copy_async per peer that the all-gather picks between (sharded.P2PAllGather;
+ *                    replaces the all-gather consumed at roundhandler.py:465-468)
  * fa_peer_enable     let device dev read / write device peer's memory directly (in-process);
  *                    already enabled is not an error
  * fa_host_register   page-lock host memory the caller mapped (the node's shared host model that
  *                    every rank D2H's its slice into: sharded.HostGather), so DMA reaches it directly;
  * fa_host_unregister undo it before the caller unmaps
+ * fa_host_device_ptr the device address of page-locked host memory (hipHostGetDevicePointer): a
+ *                    small round's fold reads its clients from the pinned arena and writes the
+ *                    model into the caller's pinned block over PCIe, with no H2D / D2H copy
+ *                    (staging.FedAvgPipeline.result); an error for pageable memory
  */
 #define FA_IPC_HANDLE_BYTES 64
 int fa_ipc_get_handle(const void* dptr, void* handle, uint64_t* offset);
 int fa_ipc_open(const void* handle, uint64_t offset, void** base, void** dptr);
 int fa_ipc_close(void* base);
 int fa_copy_async(void* dst, const void* src, int64_t bytes, void* stream);
+int fa_push(void* const* dsts, int ndst, const void* src, int64_t bytes, void* stream);
 int fa_peer_enable(int dev, int peer);
 int fa_host_register(void* p, int64_t bytes);
 int fa_host_unregister(void* p);
+int fa_host_device_ptr(const void* host, void** dptr);
 
 #ifdef __cplusplus
 }

@@ -1377,7 +1377,7 @@ def test_sharded_gloo_world2_hip_kernel():
     assert np.array_equal(res[0][3].view(np.uint64), want_opt[0].view(np.uint64))
 
 
-def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False):
+def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False, engine="dma"):
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -1398,7 +1398,7 @@ def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False):
         loc = [cs.local(u) for u in ups]
         full = torch.full((cs.full_len,), float("nan"), device="cuda:0")
         spare = torch.full((cs.full_len,), float("nan"), device="cuda:0") if double else None
-        p2p = P2PAllGather(full, spare=spare)         # IPC handles of every rank's buffers, opened once
+        p2p = P2PAllGather(full, spare=spare, engine=engine)   # IPC handles of every rank's buffers, opened once
         outs = []
         for step in range(4):                         # buffers reused: entry + exit fences, or alternation
             if step >= 2:                             # later rounds of the session: other updates
@@ -1412,13 +1412,15 @@ def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("engine", ["dma", "kernel"])
 @pytest.mark.parametrize("world,P,chunk,double", [(2, 200_003, 8192, False), (3, 1_000_000, 65536, False),
                                                   (2, 200_003, 8192, True), (3, 1_000_000, 65536, True)])
-def test_p2p_allgather_gloo_hip(world, P, chunk, double):
+def test_p2p_allgather_gloo_hip(world, P, chunk, double, engine):
     """The direct peer-to-peer all-gather (sharded.P2PAllGather: IPC handles exchanged once,
-    fa_copy_async into every peer's buffer, one copy stream per peer, entry / exit fences) with the
-    HIP fold: ranks share this box's GPU (each maps the others' buffers through IPC), three steps
-    over one buffer, every rank's whole model bit-identical to one single-device fold."""
+    pieces pushed into every peer's buffer — fa_copy_async on one copy stream per peer, or one
+    fa_push kernel per piece — entry / exit fences) with the HIP fold: ranks share this box's GPU
+    (each maps the others' buffers through IPC), four steps, every rank's whole model bit-identical
+    to one single-device fold."""
     import socket
 
     import torch.multiprocessing as mp
@@ -1431,7 +1433,7 @@ def test_p2p_allgather_gloo_hip(world, P, chunk, double):
     s_.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    pc = mp.start_processes(_p2p_gloo_worker, args=(world, port, P, K, chunk, q, double), nprocs=world,
+    pc = mp.start_processes(_p2p_gloo_worker, args=(world, port, P, K, chunk, q, double, engine), nprocs=world,
                             join=False, start_method="spawn")
     res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
     while not pc.join(timeout=60):
@@ -1452,8 +1454,31 @@ def test_p2p_allgather_gloo_hip(world, P, chunk, double):
             assert np.array_equal(got.view(np.uint32), w.view(np.uint32)), f"rank {rank} step {step}"
 
 
+@pytest.mark.parametrize("nbytes", [16, 4004, 1 << 20, (64 << 20) + 12])
+@pytest.mark.parametrize("ndst", [1, 3, 7])
+def test_push_kernel(nbytes, ndst):
+    """fa_push: the source's bytes land in every destination exactly (16-B words plus a ragged
+    tail), nothing past the end is written; misaligned pointers and too many destinations refused."""
+    from fedn_amd import ops
+    from fedn_amd._abi import FedAggError
+    g = torch.Generator(device=DEV).manual_seed(nbytes + ndst)
+    src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=DEV, generator=g)
+    dsts = [torch.full((nbytes + 64,), 0xA5, dtype=torch.uint8, device=DEV) for _ in range(ndst)]
+    st = torch.cuda.current_stream(DEV)
+    ops.push([d.data_ptr() for d in dsts], src, nbytes, st)
+    torch.cuda.synchronize()
+    for d in dsts:
+        assert torch.equal(d[:nbytes], src)
+        assert bool((d[nbytes:] == 0xA5).all())
+    with pytest.raises(FedAggError, match="aligned"):
+        ops.push([dsts[0].data_ptr() + 4], src, 32, st)
+    with pytest.raises(FedAggError, match="destinations"):
+        ops.push([dsts[0].data_ptr()] * 17, src, 32, st)
+
+
+@pytest.mark.parametrize("engine", ["dma", "kernel"])
 @pytest.mark.parametrize("ndev,P", [(2, 300_001), (3, 1 << 20)])
-def test_allgather_devices_in_process(ndev, P):
+def test_allgather_devices_in_process(ndev, P, engine):
     """multidev.allgather_devices (the in-process form of the direct all-gather: fa_peer_enable +
     fa_copy_async per (source, destination) pair on its own stream): each "device" (this box's GPU
     listed ndev times) folds its slice with the HIP kernel, every device ends with the whole model,
@@ -1472,7 +1497,7 @@ def test_allgather_devices_in_process(ndev, P):
         agg = torch.empty(hi - lo, device=DEV)
         ops.fedavg_fold(agg, [torch.from_numpy(u[lo:hi]).to(DEV) for u in ups], ns, Ns, init=True)
         parts.append((DEV, agg, lo))
-    fulls = allgather_devices(parts, P)
+    fulls = allgather_devices(parts, P, engine=engine)
     want = ref.fedavg_flat(ups, ns)
     assert len(fulls) == ndev
     for d, f in enumerate(fulls):
@@ -1534,6 +1559,69 @@ def test_small_host_updates_arena_batches(kind):
             old = want
         assert data["nr_aggregated_models"] == nr == K
         assert_lists_identical(model, want, f"{kind} round {r}")
+
+
+@pytest.mark.parametrize("kind", ["fedavg", "fedopt"])
+def test_small_float_updates_native_admission(kind):
+    """Float-only small models are admitted and packed by the native call (layout.fast_admission,
+    csrc/fastpack.c). K = 70 mnist-shaped updates (the arena flushes at 64) with updates the native
+    test must refuse mixed in: a Fortran-ordered tensor and a tuple (same layout: the Python pack),
+    a float64 tensor late in the round (numpy promotion: the per-tensor path). Two rounds through the
+    plug-in, bit-exact to the oracle, every update counted."""
+    from fedn_amd import layout as L
+    assert L._fast(), "the _fastpack extension is not built"
+    rng = np.random.default_rng(33)
+    shapes = [(64, 784), (64,), (32, 64), (32,), (10, 32), (10,)]
+    base = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    K = 70
+    ups = [[(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base] for _ in range(K)]
+    ups[5] = [np.asfortranarray(ups[5][0])] + ups[5][1:]
+    ups[9] = tuple(ups[9])
+    ups[66] = [ups[66][0].astype(np.float64)] + ups[66][1:]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    uh, agg = _plugin(kind)
+    params = {"serveropt": "adam", "learning_rate": 1e-2, "beta1": 0.9, "beta2": 0.99, "tau": 1e-4}
+    st = ref.FedOptState()
+    old = base
+    for r in range(2):
+        gid = uh.put_global_model(old, f"g{r}") if kind == "fedopt" else "global"
+        for a, n in zip(ups, ns):
+            uh.submit(a, n, model_id=gid)
+        model, data = agg.combine_models(helper=None, delete_models=True,
+                                         parameters=params if kind == "fedopt" else None)
+        if kind == "fedavg":
+            want, nr = ref.fedavg_combine(list(zip(ups, ns)))
+        else:
+            want, nr = ref.fedopt_combine(st, list(zip(ups, ns)), old, params)
+            old = want
+        assert data["nr_aggregated_models"] == nr == K
+        assert_lists_identical(model, want, f"{kind} round {r}")
+
+
+@pytest.mark.parametrize("K", [2, 5, 15, 16, 40])
+def test_small_round_zero_copy(K, monkeypatch):
+    """A small FedAvg round whose updates never left the pinned arena folds straight from it into the
+    pinned result block (staging.ZERO_COPY_BYTES: no H2D / D2H). Bit-exact to the oracle and to the
+    copy path (forced with ZERO_COPY_BYTES = 0), three rounds of one session; the zero-copy rounds
+    enqueue no H2D (time_h2d == 0), larger rounds (partial uploads from 16 updates on) copy as before."""
+    from fedn_amd import staging
+    rng = np.random.default_rng(40 + K)
+    shapes = [(64, 784), (64,), (32, 64), (32,), (10, 32), (10,)]
+    base = [rng.standard_normal(sh).astype(np.float32) for sh in shapes]
+    ups = [[(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base] for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    want, nr = ref.fedavg_combine(list(zip(ups, ns)))
+    for zc in (True, False):
+        monkeypatch.setattr(staging, "ZERO_COPY_BYTES", (4 << 20) if zc else 0)
+        uh, agg = _plugin("fedavg")
+        for r in range(3):
+            for a, n in zip(ups, ns):
+                uh.submit(a, n)
+            model, data = agg.combine_models(helper=None, delete_models=True)
+            assert data["nr_aggregated_models"] == nr == K
+            assert_lists_identical(model, want, f"K={K} zero_copy={zc} round {r}")
+            zero = zc and K < staging.ARENA_UPLOAD_EVERY
+            assert (data["time_h2d"] == 0) == zero, data
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])

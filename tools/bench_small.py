@@ -1,12 +1,17 @@
 """Round latency of the plug-ins for SMALL models (BASELINE configs[0]'s mnist-pytorch shapes and a
 mid-size CNN), host-resident numpy updates through the real combine_models call — the regime most
 FEDn deployments run in, where FEDn's numpy loop is already fast and the GPU path must not add
-latency. Beside it, the numpy restatement of the same rounds (oracle/, bit-equal to FEDn) timed on
-one host core. Every GPU round is checked bit-identical to the oracle.
+latency. Beside it, two CPU columns on one host core: the numpy restatement's arithmetic alone
+(oracle/, bit-equal to FEDn: ``round_ms_numpy_oracle_1core``), and the same arithmetic inside
+FEDn's own combine_models loop restated (fedavg.py:46-80, fedopt.py:107-139: queue, load,
+bookkeeping and per-update log calls) over the same in-memory update handler as the plug-in
+(``round_ms_numpy_fedn_loop``) — what the reference aggregator itself takes for the round. Every GPU
+round is checked bit-identical to the oracle.
 
 Run on the GPU box:  python tools/bench_small.py
 """
 import json
+import logging
 import os
 import sys
 import time
@@ -22,6 +27,7 @@ from oracle import numpy_ref as ref  # noqa: E402  (the checker and the CPU base
 MNIST = [(64, 784), (64,), (32, 64), (32,), (10, 32), (10,)]          # examples/mnist-pytorch model.py:18-32
 CNN = [(64, 3, 3, 3), (64,), (128, 64, 3, 3), (128,), (256, 128, 3, 3), (256,), (512, 256, 3, 3), (512,),
        (4096, 512), (4096,), (10, 4096), (10,)]                        # ~3.7 M params, 12 tensors
+ref_logger = logging.getLogger("fedn")     # the plug-ins log to the same logger, at the same level
 PARAMS = {"serveropt": "adam", "learning_rate": 1e-3, "beta1": 0.9, "beta2": 0.99, "tau": 1e-4}
 
 
@@ -37,40 +43,128 @@ def same(a, b):
                                     for x, y in zip(a, b))
 
 
+def fedn_loop_fedavg(uh, helper=None, delete_models=True):
+    """fedavg.py:46-80 restated with the oracle's arithmetic (the reference's per-update log calls
+    included: their messages are formatted whatever the level)."""
+    log = ref_logger
+    name = "fedavg"
+    data = {"time_model_load": 0.0, "time_model_aggregation": 0.0}
+    model, nr, total = None, 0, 0
+    log.info("AGGREGATOR({}): Aggregating model updates... ".format(name))
+    while not uh.model_updates.empty():
+        try:
+            log.info("AGGREGATOR({}): Getting next model update from queue.".format(name))
+            mu = uh.next_model_update()
+            log.info("AGGREGATOR({}): Loading model metadata {}.".format(name, mu.model_update_id))
+            tic = time.time()
+            model_next, metadata = uh.load_model_update(mu, helper)
+            data["time_model_load"] += time.time() - tic
+            log.info("AGGREGATOR({}): Processing model update {}, metadata: {}  ".format(name, mu.model_update_id,
+                                                                                         metadata))
+            total += metadata["num_examples"]
+            tic = time.time()
+            model = model_next if nr == 0 else ref.increment_average(model, model_next, metadata["num_examples"], total)
+            data["time_model_aggregation"] += time.time() - tic
+            nr += 1
+            if delete_models:
+                uh.delete_model(mu)
+        except Exception as e:  # noqa: BLE001
+            log.error(f"AGGREGATOR({name}): Error encoutered while processing model update: {e}")
+    data["nr_aggregated_models"] = nr
+    return model, data
+
+
+def fedn_loop_fedopt(uh, st, params, helper=None, delete_models=True):
+    """fedopt.py:75-121 restated with the oracle's arithmetic (validation, loop, server step)."""
+    log = ref_logger
+    name = "fedopt"
+    data = {"time_model_load": 0.0, "time_model_aggregation": 0.0, "nr_aggregated_models": 0}
+    p = ref.validate_parameters(params)
+    log.info(f"Aggregator {name} starting model aggregation.")
+    pg, old, nr, total = None, None, 0, 0
+    while not uh.model_updates.empty():
+        try:
+            log.info(f"Aggregator {name}: Fetching next model update.")
+            mu = uh.next_model_update()
+            tic = time.time()
+            model_next, metadata = uh.load_model_update(mu, helper)
+            data["time_model_load"] += time.time() - tic
+            log.info(f"Processing model update {mu.model_update_id}")
+            total += metadata["num_examples"]
+            tic = time.time()
+            if nr == 0:
+                old = uh.load_model(helper, mu.model_id)
+                pg = ref.subtract(model_next, old)
+            else:
+                pg = ref.increment_average(pg, ref.subtract(model_next, old), metadata["num_examples"], total)
+            data["time_model_aggregation"] += time.time() - tic
+            nr += 1
+            if delete_models:
+                uh.delete_model(mu)
+                log.info(f"Deleted model update {mu.model_update_id} from storage.")
+        except Exception as e:  # noqa: BLE001
+            log.error(f"Error processing model update: {e}. Skipping this update.")
+    data["nr_aggregated_models"] = nr
+    model = ref._server_step(st, pg, old, p)
+    log.info(f"Aggregator {name} completed. Aggregated {nr} models.")
+    return model, data
+
+
 def run(kind, shapes, K, rounds=20, warm=3):
+    """Each path runs its warm + timed rounds back to back (GPU plug-in, then the oracle's arithmetic,
+    then FEDn's loop restated), so no path's rounds are interleaved with another's host work; every
+    round of the two other paths is then checked against the oracle's model of the same round."""
     rng = np.random.default_rng(K)
     base, ups, ns = models(rng, shapes, K)
+    params = PARAMS if kind == "fedopt" else None
+
     uh = MemoryUpdateHandler()
     agg = get_aggregator(kind, uh)
     gid = uh.put_global_model(base, "g0")
-    st = ref.FedOptState()
-    old = base
-    times, ok = [], True
-    cpu = []
+    times, got = [], []
     for r in range(warm + rounds):
         for a, n in zip(ups, ns):
             uh.submit(a, n, model_id=gid)
         t0 = time.perf_counter()
-        model, data = agg.combine_models(helper=None, delete_models=True,
-                                         parameters=PARAMS if kind == "fedopt" else None)
-        t = time.perf_counter() - t0
+        model, _ = agg.combine_models(helper=None, delete_models=True, parameters=params)
+        times.append(time.perf_counter() - t0)
+        got.append(model)
+        if kind == "fedopt":                     # the next round starts from the new global model
+            gid = uh.put_global_model(model, f"g{r + 1}")
+
+    st, old = ref.FedOptState(), base
+    cpu, want = [], []
+    for r in range(warm + rounds):
         t1 = time.perf_counter()
         if kind == "fedavg":
-            want, _ = ref.fedavg_combine(list(zip(ups, ns)))
+            w, _ = ref.fedavg_combine(list(zip(ups, ns)))
         else:
-            want, _ = ref.fedopt_combine(st, list(zip(ups, ns)), old, PARAMS)
-        tc = time.perf_counter() - t1
-        ok &= same(model, want)
-        if kind == "fedopt":                     # the next round starts from the new global model
-            old = want
-            gid = uh.put_global_model(model, f"g{r + 1}")
-        if r >= warm:
-            times.append(t)
-            cpu.append(tc)
+            w, _ = ref.fedopt_combine(st, list(zip(ups, ns)), old, PARAMS)
+            old = w
+        cpu.append(time.perf_counter() - t1)
+        want.append(w)
+
+    uh_loop, st_loop = MemoryUpdateHandler(), ref.FedOptState()
+    gid_loop = uh_loop.put_global_model(base, "g0")
+    loop, ok = [], True
+    for r in range(warm + rounds):
+        for a, n in zip(ups, ns):
+            uh_loop.submit(a, n, model_id=gid_loop)
+        t2 = time.perf_counter()
+        if kind == "fedavg":
+            got_loop, _ = fedn_loop_fedavg(uh_loop)
+        else:
+            got_loop, _ = fedn_loop_fedopt(uh_loop, st_loop, PARAMS)
+            gid_loop = uh_loop.put_global_model(got_loop, f"g{r + 1}")
+        loop.append(time.perf_counter() - t2)
+        ok &= same(got[r], want[r]) and same(got_loop, want[r])
+
     P = sum(int(np.prod(s)) for s in shapes)
-    gpu_ms, cpu_ms = float(np.median(times)) * 1e3, float(np.median(cpu)) * 1e3
+    med = lambda xs: float(np.median(xs[warm:])) * 1e3  # noqa: E731
+    gpu_ms, cpu_ms, loop_ms = med(times), med(cpu), med(loop)
     return {"aggregator": kind, "params": P, "tensors": len(shapes), "clients": K,
             "round_ms_gpu_plugin": gpu_ms, "round_ms_numpy_oracle_1core": cpu_ms, "speedup": cpu_ms / gpu_ms,
+            "round_ms_numpy_fedn_loop": loop_ms, "speedup_vs_fedn_loop": loop_ms / gpu_ms,
             "bit_exact_all_rounds": bool(ok), "rounds": rounds}
 
 

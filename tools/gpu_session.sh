@@ -45,6 +45,19 @@ for s in $STEPS; do
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider \
         -k "$FEDN_AMD_GTEST" > "$OUT/gtest.log" 2>&1; rc=$?
       echo "gtest rc=$rc"; tail -5 "$OUT/gtest.log"; [ $rc -eq 0 ] || exit $rc ;;
+    small)
+      # small-model rounds (configs[0]'s mnist shapes): latency vs numpy, phase breakdown, host profile
+      timeout -k 10 600 python tools/bench_small.py > "$OUT/small.log" 2>&1; rc=$?
+      echo "small rc=$rc"; grep -v amdgpu.ids "$OUT/small.log" | tail -10; [ $rc -eq 0 ] || exit $rc
+      for k in 2 10 64; do
+        timeout -k 10 300 python tools/small_breakdown.py --clients $k >> "$OUT/small_breakdown.log" 2>&1; rc=$?
+        [ $rc -eq 0 ] || exit $rc
+        timeout -k 10 300 python tools/small_breakdown.py --clients $k --kind fedopt >> "$OUT/small_breakdown.log" 2>&1; rc=$?
+        [ $rc -eq 0 ] || exit $rc
+      done
+      grep -v amdgpu.ids "$OUT/small_breakdown.log"
+      timeout -k 10 300 python tools/profile_small.py --clients 10 > "$OUT/small_profile.log" 2>&1; rc=$?
+      echo "profile rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     micro)
       timeout -k 10 600 python tools/microbench.py > "$OUT/micro.log" 2>&1; rc=$?
       echo "micro rc=$rc"; cat "$OUT/micro.log" | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc ;;

@@ -53,6 +53,7 @@ def main():
     pr.disable()
     s = io.StringIO()
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(35)
+    pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(45)
     print(s.getvalue())
 
 
