@@ -285,6 +285,36 @@ def fedopt_step(old, updates, n, N, *, first, final, pg=None, m_in=None, m_out=N
     _abi.check(rc)
 
 
+def fedopt_step_raw(old_ptr, old_dt, upd_ptrs, upd_dt, n, N, P, *, first, final, pg_ptr=0, m_in=None, m_out=None,
+                    v_in=None, v_out=None, out_ptr=0, state_dt=torch.float64, serveropt="adam", learning_rate=1e-3,
+                    beta1=0.9, beta2=0.99, tau=1e-4, stream=None, device=None):
+    """:func:`fedopt_step` with the global model, the client table, pg and the new model given as
+    device addresses of ``P`` elements each — pinned host memory's device addresses included (a
+    small round folded zero-copy, staging.FedOptPipeline) — and no tensor view per update; m / v
+    are device tensors as in :func:`fedopt_step`. For the pipelines' own buffers, whose extents
+    and dtypes they guarantee (the dtype rules are the same; the C ABI checks the pairs)."""
+    if serveropt not in _OPTS:
+        raise ValueError(f"Unsupported server optimizer: {serveropt}")
+    K = len(upd_ptrs)
+    if len(n) != K or len(N) != K:
+        raise ValueError("fedopt_step_raw: one n and N per update")
+    if final and (m_out is None or v_out is None or not out_ptr):
+        raise ValueError("final step needs m_out, v_out and out")
+    _, m_np = fedopt_dtypes(upd_dt, old_dt, None if m_in is None else m_in.dtype)
+    flags = (_abi.FA_PG_FIRST if first else 0) | (_abi.FA_PG_FINAL if final else 0)
+    ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+    with torch.cuda.device(device):
+        rc = _abi.load().fa_fedopt_step_ex(
+            int(old_ptr), fa_dtype(old_dt), _abi.ptr_array([int(u) for u in upd_ptrs]), fa_dtype(upd_dt),
+            _abi.double_array(n), _abi.double_array(N), K, int(pg_ptr), flags,
+            ptr(m_in), _abi.FA_NONE if m_in is None else fa_dtype(m_in), ptr(m_out),
+            fa_dtype(m_out.dtype if m_out is not None else m_np),
+            ptr(v_in), _abi.FA_F64 if v_in is None else fa_dtype(v_in), ptr(v_out), int(out_ptr),
+            fa_dtype(state_dt), _OPTS[serveropt], float(learning_rate), float(beta1), float(beta2), float(tau), int(P),
+            ctypes_stream(stream))
+    _abi.check(rc)
+
+
 def cast(out, x, stream=None):
     """``out[...] = x`` broadcast to ``out.shape`` and widened to ``out.dtype`` (``fa_cast``):
     numpy's implicit operand preparation for a binary ufunc whose operands differ in dtype or

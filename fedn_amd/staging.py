@@ -468,8 +468,11 @@ class FedAvgPipeline(_Pipeline):
         elif self.batch_host:
             # a small model: the first update rides in the arena with the round's other updates
             # (one H2D, everything on the compute stream)
-            self.layout.check(first_arrays)
-            self.first = self.put_small(first_arrays)
+            self.first = self.put_small(first_arrays, fast=True) if (
+                self._admit is not None and type(first_arrays) is list) else None
+            if self.first is None:
+                self.layout.check(first_arrays)
+                self.first = self.put_small(first_arrays)
         else:
             self.first = self.stage(first_arrays)
             self.first.reserved = True
@@ -663,11 +666,13 @@ class FedAvgPipeline(_Pipeline):
             rdt = ops.fold_result_dtype(t, t)
             n = self.layout.group_elems[dt]
             host = torch.empty(n, dtype=rdt, pin_memory=True)
+            hosts[dt] = host
+            if n == 0:                          # a group of empty tensors: nothing to fold or map
+                continue
             off = self.layout.group_byte_offset[dt]
             ptrs = [a.host_dev + self.first._lo + off] + [a.host_dev + e[0]._lo + off for e in entries]
             ops.fedavg_fold_raw(ops.host_device_ptr(host.data_ptr(), self.device), rdt, n, ptrs, t, ns, Ns, True,
                                 self.compute, self.device)
-            hosts[dt] = host
         self._end_span(span)
         self.agg_started = True
         a.done = torch.cuda.Event()
@@ -1021,11 +1026,17 @@ class FedOptPipeline(_Pipeline):
         return self.old[dt]
 
     def _fold_pg(self, entries):
+        """Fold ``entries`` into pg (no server step): one launch per group over the entries' device
+        addresses (arena pieces, slots and staged models on this device: no tensor view per update)."""
         span = self._kernel_span()
+        ns, Ns = [e[1] for e in entries], [e[2] for e in entries]
+        addrs = [_addr(e[0]) for e in entries]
         for dt in self.layout.groups:
-            ys = [self.group(e[0], dt) for e in entries]
-            ops.fedopt_step(self._old_dev(dt), ys, [e[1] for e in entries], [e[2] for e in entries],
-                            first=not self.pg_started, final=False, pg=self._pg(dt), stream=self.compute)
+            old = self._old_dev(dt)
+            off = self.layout.group_byte_offset[dt]
+            ops.fedopt_step_raw(old.data_ptr(), old.dtype, [p + off for p in addrs], ops.torch_dtype(dt), ns, Ns,
+                                old.numel(), first=not self.pg_started, final=False, pg_ptr=self._pg(dt).data_ptr(),
+                                stream=self.compute, device=self.device)
         self._end_span(span)
         self.pg_started = True
 
@@ -1034,6 +1045,69 @@ class FedOptPipeline(_Pipeline):
             self.upload_arena()
             entries, self.pending = self.pending, []
             self._fold_pg(entries)
+
+    def _zero_copy_step(self, state, params, opt, sig):
+        """A small round that never left the host (see FedAvgPipeline._zero_copy_result): every update
+        waits in the arena being filled, none uploaded, pg not started, the global model not on the
+        device. ONE fused FIRST + FINAL launch per group reads the clients from the pinned arena and the
+        global model from a pinned block through their device addresses and writes the new model into
+        the caller's pinned block (m / v stay in HBM) — the same kernel, so the same bits — then one
+        synchronize. None if not such a round."""
+        a = self._arena
+        entries = self.pending
+        if (self.pg_started or a is None or a.uploaded or not entries or len(entries) > BATCH
+                or a.count * self.layout.nbytes > ZERO_COPY_BYTES or self.old_ready
+                or any(type(e[0]) is not _ArenaRef or e[0]._arena is not a for e in entries)):
+            return None
+        try:
+            if a.host_dev is None:
+                a.host_dev = ops.host_device_ptr(a.host_ptr, self.device)
+        except Exception:  # noqa: BLE001 — no device mapping of the arena: the copy path
+            return None
+        wait_pack_jobs(self._pack_ticket)
+        self._pack_ticket, self._pack_jobs = None, []
+        self.pending, self._arena = [], None
+        ns, Ns = [e[1] for e in entries], [e[2] for e in entries]
+        new_m, new_v, hosts = {}, {}, {}
+        span = self._kernel_span()
+        for dt in self.layout.groups:
+            P = self.layout.group_elems[dt]
+            odt, parts = self.old_host[dt]
+            old_t = ops.torch_dtype(odt)
+            m_in = state.m[dt] if state.m is not None else None
+            v_in = state.v[dt] if state.v is not None else None
+            m_dt, sdt = state_dtypes(state, dt, old_t, m_in)
+            m_out = torch.empty(P, dtype=m_dt, device=self.device)
+            v_out = torch.empty(P, dtype=sdt, device=self.device)
+            out = torch.empty(P, dtype=sdt, pin_memory=True)
+            new_m[dt], new_v[dt], hosts[dt] = m_out, v_out, out
+            if P == 0:                          # a group of empty tensors: nothing to step or map
+                continue
+            old_h = torch.empty(P, dtype=old_t, pin_memory=True)
+            view = old_h.numpy()
+            for arr, off in parts:
+                np.copyto(view[off:off + arr.size], arr, casting="no")
+            self._hold.append(old_h)            # read by the launch until the round's sync
+            off = self.layout.group_byte_offset[dt]
+            ops.fedopt_step_raw(ops.host_device_ptr(old_h.data_ptr(), self.device), old_t,
+                                [a.host_dev + e[0]._lo + off for e in entries], ops.torch_dtype(dt), ns, Ns, P,
+                                first=True, final=True, m_in=m_in, m_out=m_out, v_in=v_in, v_out=v_out,
+                                out_ptr=ops.host_device_ptr(out.data_ptr(), self.device), state_dt=sdt,
+                                serveropt=opt, learning_rate=params["learning_rate"], beta1=params["beta1"],
+                                beta2=params["beta2"], tau=params["tau"], stream=self.compute, device=self.device)
+        self._end_span(span)
+        self.pg_started = True
+        a.done = torch.cuda.Event()
+        a.done.record(self.compute)             # the arena's pinned bytes are read until here
+        a.used = True
+        self.compute.synchronize()
+        self._d2h_on_compute = True
+        self._synced = not self._d2h_used and not self._copy_used
+        state.m, state.v, state.signature, state.layout = new_m, new_v, sig, self.layout
+        model = [None] * len(self.layout.shapes)
+        for dt in self.layout.groups:
+            self.layout.unpack_group(hosts[dt].numpy(), dt, model, copy=False)
+        return model
 
     def server_step(self, state, params):
         """Apply adam/yogi/adagrad (fedopt.py:139-258); returns the new model (host, f64)."""
@@ -1048,10 +1122,14 @@ class FedOptPipeline(_Pipeline):
             model, m, v = self.general.server_step(m, v, params)
             state.set_tensors(m, v)
             return model
+        tic = time.perf_counter()
+        model = self._zero_copy_step(state, params, opt, sig)
+        if model is not None:
+            self.time_d2h += time.perf_counter() - tic
+            return model
         # one fused launch per group: the pending (device-resident) updates, if any, folded into
         # the pseudo-gradient in registers (FIRST when pg holds nothing yet) and the server
         # step; chunked so that each chunk's D2H of the new model overlaps the next chunk
-        tic = time.perf_counter()
         self.upload_arena()
         entries, self.pending = self.pending, []
         first = not self.pg_started

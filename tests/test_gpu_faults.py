@@ -55,6 +55,8 @@ def test_fedavg_fold_failure_skips_the_update(monkeypatch, shapes, fail_call):
     for u, n in zip(ups, ns):
         uh.submit(u, n)
     _failing(monkeypatch, "fedavg_fold_ptrs", lambda i, kw: i == fail_call)   # the pipelines' launch
+    # a small round held in the arena folds zero-copy (staging.ZERO_COPY_BYTES): its one launch fails too
+    _failing(monkeypatch, "fedavg_fold_raw", lambda i, kw: i == fail_call)
     if shapes[0] == (30, 7):
         from fedn_amd import _abi
         with pytest.raises(_abi.FedAggError):
@@ -117,4 +119,42 @@ def test_fedopt_server_step_failure_returns_none_and_keeps_state(monkeypatch, sh
         assert_lists_identical(agg.v, st.v, f"v r{r}")
         old = want
     assert any(kw.get("final") for kw in calls)
+    torch.cuda.synchronize()
+
+
+def test_fedopt_zero_copy_step_failure_keeps_state(monkeypatch):
+    """A small round folded zero-copy (one fedopt_step_raw launch per group, staging.ZERO_COPY_BYTES)
+    that fails in round 2: ``(None, data)``, m / v stay round 1's, round 3 continues from them."""
+    from fedn_amd import staging
+    from fedn_amd.aggregators.fedopt import Aggregator
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    assert staging.ZERO_COPY_BYTES > 0
+    rng = np.random.default_rng(53)
+    shapes = [(64, 784), (64,), (10, 64), (10,)]
+    uh = MemoryUpdateHandler()
+    agg = Aggregator(uh, device=DEV)
+    st = ref.FedOptState()
+    old = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    fail = [False]
+    calls = _failing(monkeypatch, "fedopt_step_raw", lambda i, kw: fail[0])
+    for r in range(3):
+        fail[0] = r == 1
+        ups = [[(o + 0.01 * rng.standard_normal(o.shape)).astype(o.dtype) for o in old] for _ in range(3)]
+        ns = [int(v) for v in rng.integers(1, 5001, 3)]
+        gid = uh.put_global_model(old, f"global-{r}")
+        for u, n in zip(ups, ns):
+            uh.submit(u, n, model_id=gid)
+        model, data = agg.combine_models(helper=None)
+        assert data["nr_aggregated_models"] == 3
+        if r == 1:
+            assert model is None
+            assert_lists_identical(agg.m, st.m, "m kept")
+            assert_lists_identical(agg.v, st.v, "v kept")
+            continue
+        want, _ = ref.fedopt_combine(st, list(zip(ups, ns)), old)
+        assert_lists_identical(model, want, f"round {r}")
+        assert_lists_identical(agg.m, st.m, f"m r{r}")
+        assert_lists_identical(agg.v, st.v, f"v r{r}")
+        old = want
+    assert len(calls) == 3                      # every round took the zero-copy step
     torch.cuda.synchronize()

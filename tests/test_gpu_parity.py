@@ -1471,9 +1471,9 @@ def test_push_kernel(nbytes, ndst):
         assert torch.equal(d[:nbytes], src)
         assert bool((d[nbytes:] == 0xA5).all())
     with pytest.raises(FedAggError, match="aligned"):
-        ops.push([dsts[0].data_ptr() + 4], src, 32, st)
+        ops.push([dsts[0].data_ptr() + 4], src, 16, st)
     with pytest.raises(FedAggError, match="destinations"):
-        ops.push([dsts[0].data_ptr()] * 17, src, 32, st)
+        ops.push([dsts[0].data_ptr()] * 17, src, 16, st)
 
 
 @pytest.mark.parametrize("engine", ["dma", "kernel"])
@@ -1622,6 +1622,37 @@ def test_small_round_zero_copy(K, monkeypatch):
             assert_lists_identical(model, want, f"K={K} zero_copy={zc} round {r}")
             zero = zc and K < staging.ARENA_UPLOAD_EVERY
             assert (data["time_h2d"] == 0) == zero, data
+
+
+@pytest.mark.parametrize("opt", ["adam", "yogi", "adagrad"])
+@pytest.mark.parametrize("K", [1, 3, 15, 40])
+def test_small_fedopt_zero_copy(K, opt, monkeypatch):
+    """A small FedOpt round whose updates never left the pinned arena runs its fused FIRST + FINAL
+    step zero-copy (clients and global model read from pinned memory, the new model written into the
+    caller's pinned block; m / v in HBM). Three rounds of one session (m / v carried, the global model
+    the previous round's float64 output), bit-exact to the oracle and to the copy path."""
+    from fedn_amd import staging
+    rng = np.random.default_rng(60 + K)
+    shapes = [(64, 784), (64,), (32, 64), (32,), (10, 32), (10,)]
+    base = [rng.standard_normal(sh).astype(np.float32) for sh in shapes]
+    ups = [[(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base] for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    params = {"serveropt": opt, "learning_rate": 1e-2, "beta1": 0.9, "beta2": 0.99, "tau": 1e-4}
+    for zc in (True, False):
+        monkeypatch.setattr(staging, "ZERO_COPY_BYTES", (4 << 20) if zc else 0)
+        uh, agg = _plugin("fedopt")
+        st, old = ref.FedOptState(), base
+        for r in range(3):
+            gid = uh.put_global_model(old, f"g{r}")
+            for a, n in zip(ups, ns):
+                uh.submit(a, n, model_id=gid)
+            model, data = agg.combine_models(helper=None, delete_models=True, parameters=params)
+            want, nr = ref.fedopt_combine(st, list(zip(ups, ns)), old, params)
+            assert data["nr_aggregated_models"] == nr == K
+            assert_lists_identical(model, want, f"K={K} {opt} zero_copy={zc} round {r}")
+            zero = zc and K < staging.ARENA_UPLOAD_EVERY
+            assert (data["time_h2d"] == 0) == zero, data
+            old = model
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
