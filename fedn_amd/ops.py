@@ -427,6 +427,13 @@ def elementwise(op, out, x=None, y=None, a=0.0, b=0.0, stream=None):
     for name, t in (("x", x), ("y", y)):
         if t is not None:
             _check_dev(name, t, P, out.device)
+    if P == 0:                      # an empty tensor: nothing to compute (its buffers may be null)
+        for t in (out, x, y):
+            if t is not None:
+                fa_dtype(t)         # the same dtype refusal as a non-empty call
+        if op not in _EW:
+            raise ValueError(f"unknown elementwise op {op}")
+        return out
     with torch.cuda.device(out.device):
         st = _stream_handle(out, stream)
         rc = lib.fa_elementwise(_EW[op], out.data_ptr(), fa_dtype(out), 0 if x is None else x.data_ptr(),

@@ -2,8 +2,10 @@
 tests/golden): random layouts — 1-7 tensors of rank 0-3, empty and one-element tensors, odd sizes,
 now and then a tensor large enough for the multi-strip tiles — in float32 / float64 / float16, K = 1-24
 clients, now and then a client whose tensor differs in dtype (numpy promotion, the per-tensor path),
-each round through the host path (small rounds: native admission, arena, zero-copy) and through the
-streaming ingest (updates staged into HBM on arrival). FedAvg one round, FedOpt (adam / yogi /
+each round through the host path (small rounds: native admission, arena, zero-copy), through the
+streaming ingest (updates staged into HBM on arrival), as npz bytes inflated by the native codec
+into the ingest, and sliced over two device entries in one process (multidev.py; this box's GPU
+listed twice). FedAvg one round, FedOpt (adam / yogi /
 adagrad, random hyper-parameters) three rounds with m / v carried. Bar: bit-exact values and dtypes,
 every update counted — the same bar as the golden fixtures, on cases no fixture spells out."""
 import numpy as np
@@ -69,23 +71,51 @@ def _clients(rng, shapes, dtypes, K, base, mixed):
     return ups, ns
 
 
+ROUTES = ["host", "staged", "npz", "sliced"]
+
+
 def _submit_all(route, uh, st, ups, ns, model_id="global"):
+    import io
     for a, n in zip(ups, ns):
-        uh.submit(a, n, model_id=model_id, via=st if route == "staged" else None)
+        if route == "npz":
+            b = io.BytesIO()
+            np.savez_compressed(b, **{str(i): t for i, t in enumerate(a)})
+            uh.submit_bytes(b.getvalue(), n, model_id=model_id, via=st)
+        else:
+            uh.submit(a, n, model_id=model_id, via=st if route in ("staged",) else None)
 
 
 def _handlers(route):
+    from fedn_amd.helper import Helper
     from fedn_amd.ingest import StagingUpdateHandler
     from fedn_amd.updatehandler import MemoryUpdateHandler
     uh = MemoryUpdateHandler()
-    st = StagingUpdateHandler(uh, helper=None, device=DEV, workers=2) if route == "staged" else None
+    st = None
+    if route == "staged":
+        st = StagingUpdateHandler(uh, helper=None, device=DEV, workers=2)
+    elif route == "npz":
+        st = StagingUpdateHandler(uh, helper=Helper(), device=DEV, workers=2, native_decode=True)
     return uh, st
 
 
-@pytest.mark.parametrize("route", ["host", "staged"])
-@pytest.mark.parametrize("seed", range(24))
-def test_fuzz_fedavg(seed, route):
-    from fedn_amd.aggregators import get_aggregator
+def _aggregator(kind, route, uh, st, monkeypatch):
+    from fedn_amd.aggregators import fedavg, fedopt
+    mod = fedavg if kind == "fedavg" else fedopt
+    if route == "sliced":
+        from fedn_amd import layout
+        monkeypatch.setattr(layout, "MULTIDEV_MIN_BYTES", 0)     # slice even these small models
+        return mod.Aggregator(uh, devices=[DEV, DEV])
+    return mod.Aggregator(st or uh)
+
+
+def _helper(route):
+    from fedn_amd.helper import Helper
+    return Helper() if route == "npz" else None
+
+
+@pytest.mark.parametrize("route", ROUTES)
+@pytest.mark.parametrize("seed", range(48))
+def test_fuzz_fedavg(seed, route, monkeypatch):
     rng = np.random.default_rng(1000 + seed)
     shapes, dtypes = _layout(rng)
     K = int(rng.integers(1, 25))
@@ -95,8 +125,8 @@ def test_fuzz_fedavg(seed, route):
     uh, st = _handlers(route)
     try:
         _submit_all(route, uh, st, ups, ns)
-        agg = get_aggregator("fedavg", st or uh)
-        model, data = agg.combine_models(helper=None, delete_models=True)
+        agg = _aggregator("fedavg", route, uh, st, monkeypatch)
+        model, data = agg.combine_models(helper=_helper(route), delete_models=True)
     finally:
         if st is not None:
             st.close()
@@ -104,10 +134,9 @@ def test_fuzz_fedavg(seed, route):
     assert_lists_identical(model, want, f"seed {seed} {route} shapes {shapes} dtypes {dtypes} K {K}")
 
 
-@pytest.mark.parametrize("route", ["host", "staged"])
-@pytest.mark.parametrize("seed", range(16))
-def test_fuzz_fedopt(seed, route):
-    from fedn_amd.aggregators import get_aggregator
+@pytest.mark.parametrize("route", ROUTES)
+@pytest.mark.parametrize("seed", range(30))
+def test_fuzz_fedopt(seed, route, monkeypatch):
     rng = np.random.default_rng(2000 + seed)
     shapes, dtypes = _layout(rng)
     opt = ["adam", "yogi", "adagrad"][seed % 3]
@@ -116,7 +145,7 @@ def test_fuzz_fedopt(seed, route):
               "tau": float(10 ** rng.uniform(-6, -2))}
     old = [_values(rng, s, d) for s, d in zip(shapes, dtypes)]
     uh, st = _handlers(route)
-    agg = get_aggregator("fedopt", st or uh)
+    agg = _aggregator("fedopt", route, uh, st, monkeypatch)
     state = ref.FedOptState()
     try:
         for r in range(3):
@@ -124,7 +153,7 @@ def test_fuzz_fedopt(seed, route):
             ups, ns = _clients(rng, shapes, dtypes, K, old, mixed=seed % 4 == 1)
             gid = uh.put_global_model(old, f"g{r}")
             _submit_all(route, uh, st, ups, ns, model_id=gid)
-            model, data = agg.combine_models(helper=None, delete_models=True, parameters=params)
+            model, data = agg.combine_models(helper=_helper(route), delete_models=True, parameters=params)
             want, nr = ref.fedopt_combine(state, list(zip(ups, ns)), old, params)
             what = f"seed {seed} {route} {opt} round {r} shapes {shapes} dtypes {dtypes} K {K}"
             assert data["nr_aggregated_models"] == nr == K, what
