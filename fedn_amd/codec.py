@@ -105,6 +105,18 @@ def gather_wait(ticket):
     _check(load_lib().fnpz_gather_wait(ticket))
 
 
+def gather_raw(jobs, threads):
+    """``(dst address, src address, bytes)`` copies in one native call (``fnpz_gather``: 1 MiB+ pieces
+    on the persistent thread pool, the GIL released); the caller keeps both ends alive."""
+    n = len(jobs)
+    if not n:
+        return
+    dsts, srcs, nb = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)(), (ctypes.c_int64 * n)()
+    for i, (d, src, b) in enumerate(jobs):
+        dsts[i], srcs[i], nb[i] = d, src, b
+    _check(load_lib().fnpz_gather(n, dsts, srcs, nb, int(threads)))
+
+
 def gather(pairs, threads):
     """``dst[:] = src`` for each (dst, src) pair of C-contiguous numpy arrays of equal byte size, in
     one native call (``fnpz_gather``: 1 MiB+ pieces on a persistent thread pool; the GIL is released

@@ -270,6 +270,21 @@ class Layout:
         model of many mid-size tensors is packed in parallel, not one tensor at a time."""
         run_pack_jobs(self.pack_jobs(arrays, buf_np_u8))
 
+    def pack_range(self, arrays, dst_ptr, lo, hi):
+        """(destination address, source address, bytes) copies that write bytes [lo, hi) of the packed
+        update at ``dst_ptr`` (padding between groups untouched, as :meth:`pack`); None if a source
+        overlapping the range is not a C-contiguous ndarray of its layout dtype (the caller packs
+        whole instead). The caller keeps ``arrays`` alive until the copies ran."""
+        out = []
+        for i, off, nb in self.pack_plan:
+            s0, s1 = max(lo, off), min(hi, off + nb)
+            if s0 < s1:
+                a = arrays[i]
+                if type(a) is not np.ndarray or not a.flags.c_contiguous or a.dtype != self.dtypes[i]:
+                    return None
+                out.append((dst_ptr + s0, a.ctypes.data + (s0 - off), s1 - s0))
+        return out
+
     def pack_jobs(self, arrays, buf_np_u8):
         """The (destination view, flat source) copies of :meth:`pack`, not run yet (a caller that
         packs many small updates runs them together: :func:`run_pack_jobs`)."""

@@ -42,10 +42,26 @@ RING_BYTES = 64 << 20         # pinned ring piece for host -> device streaming o
 SMALL_UPDATE_BYTES = 4 << 20
 ARENA_BYTES = 64 << 20
 ARENA_UPLOAD_EVERY = 16       # an arena's packed updates go to HBM in parts of this many, while later ones load
+# a large host update is packed into its pinned slot in pieces of STAGE_PIECE bytes, each piece's
+# H2D enqueued as soon as it is packed: the pack of piece j + 1 overlaps the DMA of piece j, so a
+# round's first update no longer waits for its whole pack, and a FedAvg round's LAST fold runs
+# chunk by chunk behind the pieces with the result's D2H (full duplex) — see FedAvgPipeline.result
+STAGE_PIECE = 32 << 20
+STAGE_PIECES_MIN = 64 << 20
 # a FedAvg round whose updates all wait in one arena, not yet uploaded, and hold at most this many
 # bytes in total folds them straight from the pinned arena into the caller's pinned result block:
 # the kernel reads and writes host memory over PCIe, with no H2D / D2H copy to enqueue and order
 ZERO_COPY_BYTES = int(os.environ.get("FEDN_AMD_ZERO_COPY_BYTES", str(4 << 20)))
+
+
+def _have_codec():
+    """Whether libfednpz (the native gather the piecewise stage packs with) is built."""
+    try:
+        from . import codec
+        codec.load_lib()
+        return True
+    except ImportError:
+        return False
 
 
 def chunks(n, itemsize):
@@ -119,7 +135,7 @@ class StagingCache:
 
 
 class _Slot:
-    __slots__ = ("host", "host_np", "dev", "h2d_start", "h2d_done", "consumed", "used", "reserved")
+    __slots__ = ("host", "host_np", "dev", "h2d_start", "h2d_done", "consumed", "used", "reserved", "pieces")
 
     def __init__(self, nbytes, device):
         self.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
@@ -130,6 +146,7 @@ class _Slot:
         self.consumed = torch.cuda.Event()
         self.used = False
         self.reserved = False
+        self.pieces = None          # [(lo, hi, event after that byte range's H2D)] of a piecewise stage
 
 
 class _Arena:
@@ -243,24 +260,62 @@ class _Pipeline:
                 return s
         raise RuntimeError("no free staging slot")
 
-    def stage(self, arrays):
-        """Pack host ``arrays`` into a pinned slot and start its H2D copy; returns the slot."""
+    def stage(self, arrays, wait=True):
+        """Pack host ``arrays`` into a pinned slot and start its H2D copy; returns the slot. A large
+        update (>= STAGE_PIECES_MIN bytes) is packed and copied piece by piece (``slot.pieces``).
+        ``wait``: the compute stream waits for the whole H2D (else the caller orders its folds)."""
         s = self._take_slot()
         if s.used:
             s.h2d_done.synchronize()            # pinned bytes no longer read by the DMA
             self.copy.wait_event(s.consumed)    # device bytes no longer read by a fold
         self._copy_used = True
         tic = time.perf_counter()
-        self.layout.pack(arrays, s.host_np)
-        self.time_pack += time.perf_counter() - tic
-        with torch.cuda.stream(self.copy):
+        nb = self.layout.nbytes
+        jobs = None
+        if nb >= STAGE_PIECES_MIN and _have_codec():
+            host_ptr = s.host.data_ptr()
+            spans = [(lo, min(nb, lo + STAGE_PIECE)) for lo in range(0, nb, STAGE_PIECE)]
+            jobs = [self.layout.pack_range(arrays, host_ptr, lo, hi) for lo, hi in spans]
+            if any(j is None for j in jobs):
+                jobs = None
+        s.pieces = None
+        if jobs is None:
+            self.layout.pack(arrays, s.host_np)
+            self.time_pack += time.perf_counter() - tic
+            with torch.cuda.stream(self.copy):
+                s.h2d_start.record(self.copy)
+                s.dev.copy_(s.host, non_blocking=True)
+                s.h2d_done.record(self.copy)
+        else:
+            from . import codec
+            from .layout import PACK_THREADS
+            dev_ptr = s.dev.data_ptr()
             s.h2d_start.record(self.copy)
-            s.dev.copy_(s.host, non_blocking=True)
+            s.pieces = []
+            for (lo, hi), job in zip(spans, jobs):
+                t0 = time.perf_counter()
+                codec.gather_raw(job, PACK_THREADS)
+                self.time_pack += time.perf_counter() - t0
+                ops.copy_ptr_async(dev_ptr + lo, host_ptr + lo, hi - lo, self.copy, self.device)
+                ev = torch.cuda.Event()
+                ev.record(self.copy)
+                s.pieces.append((lo, hi, ev))
             s.h2d_done.record(self.copy)
         self._h2d.append((s.h2d_start, s.h2d_done))
-        self.compute.wait_event(s.h2d_done)
+        if wait:
+            self.compute.wait_event(s.h2d_done)
         s.used = True
         return s
+
+    def wait_bytes(self, slot, lo, hi):
+        """The compute stream waits for the H2D of bytes [lo, hi) of ``slot`` (its pieces that overlap
+        the range, or the whole copy)."""
+        if slot.pieces is None:
+            self.compute.wait_event(slot.h2d_done)
+            return
+        for plo, phi, ev in slot.pieces:
+            if plo < hi and lo < phi:
+                self.compute.wait_event(ev)
 
     def put_small(self, arrays, fast=False):
         """Pack a small host update into the arena being filled (no H2D yet); returns the
@@ -405,12 +460,13 @@ class _Pipeline:
         b.record(self.compute)
         self._kern.append((a, b))
 
-    def _fold_then_d2h(self, src, fold_chunk, prepare=None):
+    def _fold_then_d2h(self, src, fold_chunk, prepare=None, ready=None):
         """Copy device tensor ``src`` into a new pinned host tensor chunk by chunk: for each
         chunk [lo, hi), ``prepare(lo, hi)`` (optional: enqueue the chunk's inputs) and
         ``fold_chunk(lo, hi)`` (enqueue the launch that produces ``src[lo:hi]`` on the compute
         stream), then its D2H on the d2h stream, which overlaps the next chunk's work.
-        The caller synchronises the d2h stream."""
+        ``ready(lo, hi)`` (optional): the events the chunk's D2H waits for instead of everything
+        enqueued on the compute stream so far. The caller synchronises the d2h stream."""
         n = src.numel()
         host = torch.empty(n, dtype=src.dtype, pin_memory=True)
         if n * src.element_size() <= SMALL_UPDATE_BYTES:
@@ -427,9 +483,13 @@ class _Pipeline:
             if prepare is not None:
                 prepare(lo, hi)
             fold_chunk(lo, hi)
-            ev = torch.cuda.Event()
-            ev.record(self.compute)
-            self.d2h.wait_event(ev)
+            if ready is not None:
+                for ev in ready(lo, hi):
+                    self.d2h.wait_event(ev)
+            else:
+                ev = torch.cuda.Event()
+                ev.record(self.compute)
+                self.d2h.wait_event(ev)
             with torch.cuda.stream(self.d2h):
                 host[lo:hi].copy_(src[lo:hi], non_blocking=True)
         return host
@@ -480,6 +540,10 @@ class FedAvgPipeline(_Pipeline):
         self.agg_started = False                 # agg holds a fold of the first update
         self.agg = {}
         self.general = None                      # mixed.TensorFedAvg once an update differs in layout
+        # the fold chunks of the latest large host update, (dt, lo, hi, event after the chunk) — valid
+        # while nothing was folded after it: result() then D2H's each chunk of the model as soon as
+        # that chunk is folded, overlapping the rest of the last update's H2D (PCIe is full duplex)
+        self._last_fold = None
 
     def _state_meta(self):
         """(shape, dtype) per tensor of the running model: the first update's before any fold,
@@ -493,6 +557,7 @@ class FedAvgPipeline(_Pipeline):
     def _enter_general(self):
         """Hand the running model to the per-tensor path (mixed.TensorFedAvg)."""
         self._flush()
+        self._last_fold = None
         if self.agg_started:
             views = mixed.tensor_views(self.layout, {dt: self._agg(dt) for dt in self.layout.groups})
             self.general = mixed.TensorFedAvg(self.device, self.compute, views, owned=True)
@@ -549,10 +614,37 @@ class FedAvgPipeline(_Pipeline):
                 self._flush()
         else:
             self._flush()
-            slot = self.acquire(arrays)
-            self._fold_all([(slot, n, N)])
+            slot = self.stage(arrays, wait=False)
+            self._fold_pieces(slot, n, N)
             slot.consumed.record(self.compute)
         self.nfolds += 1
+
+    def _fold_pieces(self, slot, n, N):
+        """Fold one staged host update on arrival, one launch per H2D piece of each group, each
+        waiting only for its piece (the fold of piece j overlaps the DMA of piece j + 1); the chunks'
+        events are kept for result() (``_last_fold``). Same kernel, table and element ranges of one
+        recurrence step: the same bits as one launch."""
+        span = self._kernel_span()
+        init = not self.agg_started
+        done = []
+        for dt in self.layout.groups:
+            off, isz, P = self.layout.group_byte_offset[dt], np.dtype(dt).itemsize, self.layout.group_elems[dt]
+            if slot.pieces is None:
+                bounds = [(0, P)] if P else []
+            else:                               # element ranges of the group inside each piece
+                bounds = [(max(0, (plo - off) // isz), min(P, (phi - off) // isz)) for plo, phi, _ in slot.pieces]
+                bounds = [(lo, hi) for lo, hi in bounds if hi > lo]
+                if bounds:
+                    bounds[-1] = (bounds[-1][0], P)
+            for lo, hi in bounds:
+                self.wait_bytes(slot, off + lo * isz, off + hi * isz)
+                self._fold_group(dt, [(slot, n, N)], init, lo, hi)
+                ev = torch.cuda.Event()
+                ev.record(self.compute)
+                done.append((dt, lo, hi, ev))
+        self._end_span(span)
+        self._folded()
+        self._last_fold = done
 
     def _fold_group(self, dt, entries, init, lo, hi):
         """Enqueue the fold of ``entries`` over elements [lo, hi) of group ``dt``. Every entry's
@@ -586,6 +678,7 @@ class FedAvgPipeline(_Pipeline):
         self.agg_started = True
 
     def _fold_all(self, entries):
+        self._last_fold = None
         span = self._kernel_span()
         init = not self.agg_started
         for dt in self.layout.groups:
@@ -614,15 +707,20 @@ class FedAvgPipeline(_Pipeline):
             return out
         self.upload_arena()
         entries, self.pending = self.pending, []
+        last = self._last_fold if not entries else None
         init = not self.agg_started
         span = self._kernel_span()
         hosts = {}
         for dt in self.layout.groups:
+            ready = None
             if entries:
                 fold = lambda lo, hi, dt=dt: self._fold_group(dt, entries, init, lo, hi)  # noqa: E731
             else:
                 fold = lambda lo, hi: None  # noqa: E731
-            hosts[dt] = self._fold_then_d2h(self._agg(dt), fold)
+                if last is not None:            # each D2H chunk waits only for the folds it reads
+                    mine = [(lo, hi, ev) for d, lo, hi, ev in last if d == dt]
+                    ready = lambda lo, hi, mine=mine: [ev for flo, fhi, ev in mine if flo < hi and lo < fhi]  # noqa: E731
+            hosts[dt] = self._fold_then_d2h(self._agg(dt), fold, ready=ready)
         self._end_span(span)
         if entries:
             self._folded()

@@ -1655,6 +1655,45 @@ def test_small_fedopt_zero_copy(K, opt, monkeypatch):
             old = model
 
 
+@pytest.mark.parametrize("K,staged_at,mixed_last", [(1, (), False), (2, (), False), (3, (), False),
+                                                     (5, (), False), (5, (2,), False), (4, (3,), False),
+                                                     (4, (), True)])
+def test_large_host_updates_piecewise_staging(K, staged_at, mixed_last):
+    """Updates >= STAGE_PIECES_MIN are packed and uploaded piece by piece and folded on arrival one
+    launch per piece (each behind its own H2D piece); after the round's last such update the
+    result's D2H chunks wait only for the fold chunks they read. Two groups (a ~17 M fp32 group,
+    ragged, and a small fp64 one); staged (device-resident) updates interleaved keep FIFO order; a
+    last update of another dtype moves the round to the per-tensor path. Bit-exact to the oracle,
+    two rounds."""
+    from fedn_amd import staging
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rng = np.random.default_rng(70 + K)
+    shapes = [(4099, 4099), (777,), (1001,)]
+    dtypes = [np.float32, np.float32, np.float64]
+    base = [rng.standard_normal(sh).astype(d) for sh, d in zip(shapes, dtypes)]
+    nbytes = sum(b.nbytes for b in base)
+    assert nbytes >= staging.STAGE_PIECES_MIN and nbytes % staging.STAGE_PIECE
+    ups = [[(b + 0.01 * rng.standard_normal(b.shape)).astype(b.dtype) for b in base] for _ in range(K)]
+    if mixed_last:
+        ups[-1] = [ups[-1][0].astype(np.float64)] + ups[-1][1:]
+    ns = [int(v) for v in rng.integers(1, 5001, K)]
+    want, nr = ref.fedavg_combine(list(zip(ups, ns)))
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=None, device=DEV, workers=2)
+    agg = get_aggregator("fedavg", st)
+    try:
+        for r in range(2):
+            for k, (a, n) in enumerate(zip(ups, ns)):
+                uh.submit(a, n, via=st if k in staged_at else None)
+            model, data = agg.combine_models(helper=None, delete_models=True)
+            assert data["nr_aggregated_models"] == nr == K
+            assert_lists_identical(model, want, f"K={K} staged_at={staged_at} mixed_last={mixed_last} round {r}")
+    finally:
+        st.close()
+
+
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("K,P", [(3, 1), (64, 4099), (130, 8192 * 3 + 7), (9, 100_003)])
 def test_fedavg_pipelined_geometry_forced_small(dt, K, P):
