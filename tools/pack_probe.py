@@ -49,6 +49,23 @@ def main():
         out[f"{name}_h2d_GBps"] = nbytes / ((time.perf_counter() - t0) / 20) / 1e9
     ops.host_unregister(reg_t)
     print(json.dumps({"bytes": nbytes, **{k: round(v, 2) for k, v in out.items()}}), flush=True)
+    large()
+
+
+def large(P=100_000_000, reps=5):
+    """The pack of ONE large update (a 100 M-param fp32 model, 400 MB) into a pinned slot with 4..64
+    native threads: what bounds the multi-device plug-in, whose GPUs each take only a slice of every
+    packed update over their own links (multidev.py)."""
+    src = np.random.default_rng(0).standard_normal(P).astype(np.float32)
+    dst = torch.empty(P * 4, dtype=torch.uint8, pin_memory=True).numpy().view(np.float32)
+    res = {}
+    for threads in (4, 8, 16, 24, 32, 48, 64):
+        codec.gather([(dst, src)], threads)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            codec.gather([(dst, src)], threads)
+        res[f"t{threads}_GBps"] = round(P * 4 / ((time.perf_counter() - t0) / reps) / 1e9, 1)
+    print(json.dumps({"large_update_bytes": P * 4, **res}), flush=True)
 
 
 if __name__ == "__main__":
