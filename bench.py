@@ -152,7 +152,33 @@ def cpu_baseline(ups, ns, agg, S):
             "sample": f"{len(ups)} clients x {S} fp32 params (first {S} of each client buffer); "
                       f"numpy {np.__version__} oracle/numpy_ref.fedavg_flat, single-threaded, "
                       f"{os.cpu_count()} host cores present", "seconds": dt,
-            "gpu_bit_exact_on_sample": exact}
+            "gpu_bit_exact_on_sample": exact, "threaded": cpu_threaded(sample, ns, want)}
+
+
+def cpu_threaded(sample, ns, want):
+    """SURVEY §8(d)'s optional labelled line: the same oracle over the same sample sliced by
+    parameters across every core this process may use (numpy ufuncs release the GIL; each element's
+    recurrence is untouched, so the result is the single-threaded one, checked)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import numpy_ref as ref  # test infrastructure: the baseline/checker only
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    S = want.size
+    bounds = [(S * i // cores, S * (i + 1) // cores) for i in range(cores)]
+    out = np.empty_like(want)
+
+    def part(lo, hi):
+        out[lo:hi] = ref.fedavg_flat([u[lo:hi] for u in sample], ns)
+
+    with ThreadPoolExecutor(cores) as ex:
+        t0 = time.perf_counter()
+        for f in [ex.submit(part, lo, hi) for lo, hi in bounds]:
+            f.result()
+        dt = time.perf_counter() - t0
+    return {"value": len(sample) * S / dt, "unit": "params/s", "cores": cores, "seconds": dt,
+            "same_as_single_threaded": bool(np.array_equal(out.view(np.uint32), want.view(np.uint32))),
+            "note": "numpy oracle sliced over parameters on a thread per core; reported beside the 1-core "
+                    "baseline, not instead of it"}
 
 
 def timed_steps(step, steps, stream, world, device, on_cpu):
