@@ -32,7 +32,7 @@ from .layout import Layout, fast_admission, parallel_copy, start_pack_into, wait
 
 
 BATCH = 64                    # device-resident updates folded per launch (the kernarg client table)
-MAX_CHUNKS = 8                # the round's last launch is split into at most this many chunks, each
+MAX_CHUNKS = int(os.environ.get("FEDN_AMD_MAX_CHUNKS", "16"))  # the round's last launch is split into at most this many chunks, each
 MIN_CHUNK_BYTES = 8 << 20     # chunk's D2H (and FedOpt's old-model H2D) overlapping the next chunk
 RING_BYTES = 64 << 20         # pinned ring piece for host -> device streaming of the global model
 # host updates of at most SMALL_UPDATE_BYTES (a packed model) are batched: packed on arrival into a
