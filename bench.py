@@ -155,6 +155,28 @@ def cpu_baseline(ups, ns, agg, S):
             "gpu_bit_exact_on_sample": exact, "threaded": cpu_threaded(sample, ns, want)}
 
 
+def usable_cores():
+    """The cores this process may keep busy: its CPU affinity, capped by a cgroup CPU quota (a GPU box
+    shows every core of the machine but grants a share of them)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:                     # cgroup v2: "<quota> <period>"
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        try:                                                         # cgroup v1
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                quota = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                period = int(f.read())
+            if quota > 0:
+                n = min(n, max(1, -(-quota // period)))
+        except (OSError, ValueError):
+            pass
+    return n
+
+
 def cpu_threaded(sample, ns, want):
     """SURVEY §8(d)'s optional labelled line: the same oracle over the same sample sliced by
     parameters across every core this process may use (numpy ufuncs release the GIL; each element's
@@ -162,7 +184,7 @@ def cpu_threaded(sample, ns, want):
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import numpy_ref as ref  # test infrastructure: the baseline/checker only
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cores = usable_cores()
     S = want.size
     bounds = [(S * i // cores, S * (i + 1) // cores) for i in range(cores)]
     out = np.empty_like(want)
