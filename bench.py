@@ -875,6 +875,14 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
                          "kernel": kernel, "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": base,
+            # the north star's "absolute GB/s and fraction of the HBM roofline" for the whole job: the
+            # algorithmic bytes of the 64-client fold over the GLOBAL model (K*P*s_in + P*4) per wall
+            # step, against N GPUs' peak (at N > 1 the step includes the all-gather)
+            "throughput": {"GBps": (K * P_total * in_bytes + P_total * 4) / (elapsed / a.steps) / 1e9,
+                           "peak_GBps": HBM_PEAK_GBS * world,
+                           "frac": (K * P_total * in_bytes + P_total * 4) / (elapsed / a.steps) / 1e9
+                           / (HBM_PEAK_GBS * world),
+                           "note": "whole job, wall time of a step (fold + gather at N > 1) vs N x 8 TB/s"},
         }
         line.update(extra)
         print(json.dumps(line), flush=True)
