@@ -780,10 +780,11 @@ def main():
         res = [None]
         step = make_step(cyc, tp, ups_local, res)
 
+        fold_round = cyc.round_folder(agg, ups_local, ns, Ns, True, stream)   # the step's own launches
+
         def fold_only():
             for i in range(cyc.rounds):
-                sl = slice(i * cyc.C, (i + 1) * cyc.C)
-                ops.fedavg_fold(agg[sl], [u[sl] for u in ups_local], ns, Ns, init=True, stream=stream)
+                fold_round(i)
 
         for _ in range(a.warmup):
             step()

@@ -1,7 +1,8 @@
 """Time one rank's share of bench.py --gpus N's step on ONE GPU: the R fold launches of 64 clients x C
 fp32 params (sharded.CyclicShardedFedAvg's block-cyclic geometry, the same launches
-tools/pmc_rank_fold.py replays for PMC), for N = 2, 4, 8 and every round count R the warm-up may
-pick, plus a fa_push of each folded round into N - 1 other buffers of this GPU (the push kernel's own
+tools/pmc_rank_fold.py replays for PMC) — issued as the step issues them (client table as device
+addresses, CyclicShardedFedAvg.round_folder) and, for comparison, through 64 tensor slices per
+launch — for N = 2, 4, 8 and every round count R the warm-up may pick, plus a fa_push of each folded round into N - 1 other buffers of this GPU (the push kernel's own
 cost when the links are not the limit). What the fold contributes to the N-GPU step; the gather over
 xGMI is the node's to measure.
 
@@ -50,7 +51,14 @@ def main():
         for R in (1, 2, 4, 8, 16):
             C, rounds, L = rank_geometry(P, world, R)
 
-            def fold():
+            bases = [u.data_ptr() for u in ups]
+
+            def fold():                         # CyclicShardedFedAvg.round_folder's launches
+                for i in range(rounds):
+                    ops.fedavg_fold_ptrs(agg[i * C:(i + 1) * C], [b + i * C * 4 for b in bases], torch.float32,
+                                         ns, Ns, init=True, stream=stream)
+
+            def fold_sliced():                  # the same launches through 64 tensor slices each
                 for i in range(rounds):
                     sl = slice(i * C, (i + 1) * C)
                     ops.fedavg_fold(agg[sl], [u[sl] for u in ups], ns, Ns, init=True, stream=stream)
@@ -61,10 +69,12 @@ def main():
                     ops.push([p[sl].data_ptr() for p in peers], agg[sl], C * 4, stream)
 
             fms = timed(fold, STEPS, stream)
+            sms = timed(fold_sliced, STEPS, stream)
             pms = timed(push, STEPS, stream)
             alg = K * L * 4 + L * 4
             print(json.dumps({"world": world, "rounds": rounds, "chunk": C, "local_len": L,
                               "fold_ms_per_step": round(fms, 4), "fold_frac_of_peak": round(alg / fms / 8e9, 4),
+                              "fold_sliced_ms_per_step": round(sms, 4),
                               "push_local_ms_per_step": round(pms, 4),
                               "push_note": f"fa_push of every round into {world - 1} buffers of this GPU "
                                            "(HBM-local: the kernel's own cost, not the links')"}), flush=True)
