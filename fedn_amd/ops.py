@@ -6,6 +6,7 @@ tensors' current HIP stream, raise :class:`FedAggError` on a nonzero status.
 dtype rules mirror numpy's for the reference expressions:
 see :func:`fold_result_dtype` and :func:`fedopt_dtypes`.
 """
+import contextlib
 import ctypes
 
 import numpy as np
@@ -497,14 +498,14 @@ def copy_async(dst_ptr, src, nbytes, stream):
     lib = _abi.load()
     if nbytes > src.numel() * src.element_size():
         raise ValueError("copy_async: more bytes than the source holds")
-    with torch.cuda.device(src.device):
+    with _on(src.device):
         _abi.check(lib.fa_copy_async(int(dst_ptr), src.data_ptr(), int(nbytes), ctypes_stream(stream)))
 
 
 def copy_ptr_async(dst_ptr, src_ptr, nbytes, stream, device):
     """``nbytes`` from address ``src_ptr`` to ``dst_ptr`` (host or device) on ``stream``: one
     hipMemcpyAsync, without a tensor per call."""
-    with torch.cuda.device(device):
+    with _on(device):
         _abi.check(_abi.load().fa_copy_async(int(dst_ptr), int(src_ptr), int(nbytes), ctypes_stream(stream)))
 
 
@@ -516,9 +517,21 @@ def push(dst_ptrs, src, nbytes, stream):
     if nbytes > src.numel() * src.element_size():
         raise ValueError("push: more bytes than the source holds")
     n = len(dst_ptrs)
-    with torch.cuda.device(src.device):
+    with _on(src.device):
         _abi.check(lib.fa_push((ctypes.c_void_p * max(1, n))(*[int(p) for p in dst_ptrs]), n, src.data_ptr(),
                                int(nbytes), ctypes_stream(stream)))
+
+
+_NULL_CTX = contextlib.nullcontext()
+
+
+def _on(device):
+    """``torch.cuda.device(device)`` unless it is already the current device (the per-round and
+    per-update copy calls of the pipelines pay the context switch only when they need it)."""
+    idx = device.index if isinstance(device, torch.device) else torch.device(device).index
+    if idx is None or idx == torch.cuda.current_device():
+        return _NULL_CTX
+    return torch.cuda.device(device)
 
 
 def peer_enable(dev, peer):
