@@ -84,3 +84,40 @@ def test_admission_missing_extension(monkeypatch):
     monkeypatch.delattr(lay, "_fast_admit", raising=False)
     assert fast_admission(lay) is None
     monkeypatch.delattr(lay, "_fast_admit")                # the next test sees the extension again
+
+
+@pytest.mark.parametrize("piece", [64, 1000, 4096, 1 << 20])
+def test_pack_range_pieces_equal_pack(piece):
+    """Layout.pack_range (the piecewise stage of large host updates): the copies of every piece,
+    run through the native gather, write exactly what Layout.pack writes; a non-contiguous source
+    makes it refuse (None) so the stage packs whole."""
+    from fedn_amd import codec
+    rng = np.random.default_rng(piece)
+    arrays = [rng.standard_normal((37, 41)).astype(np.float32), rng.standard_normal(1001),
+              rng.standard_normal((5, 7)).astype(np.float16), np.zeros(0, np.float32),
+              rng.standard_normal(3000).astype(np.float32)]
+    lay = Layout.of(arrays)
+    want = _packed(lay, arrays)
+    got = np.zeros(lay.nbytes, np.uint8)
+    ptr = got.ctypes.data
+    for lo in range(0, lay.nbytes, piece):
+        jobs = lay.pack_range(arrays, ptr, lo, min(lay.nbytes, lo + piece))
+        assert jobs is not None
+        codec.gather_raw(jobs, 4)
+    for i, off, nb in lay.pack_plan:
+        assert np.array_equal(got[off:off + nb], want[off:off + nb]), i
+    bad = [np.asfortranarray(arrays[0])] + arrays[1:]
+    assert lay.pack_range(bad, ptr, 0, lay.nbytes) is None
+
+
+def test_threaded_cpu_baseline_matches_single_thread():
+    """bench.py's threaded numpy line slices the same oracle over parameters: identical bits."""
+    import bench
+    from oracle import numpy_ref as ref
+    rng = np.random.default_rng(3)
+    sample = [rng.standard_normal(100_003).astype(np.float32) for _ in range(9)]
+    ns = [int(v) for v in rng.integers(1, 5001, 9)]
+    want = ref.fedavg_flat(sample, ns)
+    out = bench.cpu_threaded(sample, ns, want)
+    assert out["same_as_single_threaded"] and out["cores"] >= 1 and out["value"] > 0
+    assert 1 <= bench.usable_cores() <= (__import__("os").cpu_count() or 1)
