@@ -5,7 +5,7 @@ clients, now and then a client whose tensor differs in dtype (numpy promotion, t
 each round through the host path (small rounds: native admission, arena, zero-copy), through the
 streaming ingest (updates staged into HBM on arrival), as npz bytes inflated by the native codec
 into the ingest, and sliced over two device entries in one process (multidev.py; this box's GPU
-listed twice). FedAvg one round, FedOpt (adam / yogi /
+listed twice), from the host or staged on arrival as parameter slices. FedAvg one round, FedOpt (adam / yogi /
 adagrad, random hyper-parameters) three rounds with m / v carried. Bar: bit-exact values and dtypes,
 every update counted — the same bar as the golden fixtures, on cases no fixture spells out."""
 import numpy as np
@@ -71,7 +71,7 @@ def _clients(rng, shapes, dtypes, K, base, mixed):
     return ups, ns
 
 
-ROUTES = ["host", "staged", "npz", "sliced"]
+ROUTES = ["host", "staged", "npz", "sliced", "staged_sliced"]
 
 
 def _submit_all(route, uh, st, ups, ns, model_id="global"):
@@ -82,7 +82,7 @@ def _submit_all(route, uh, st, ups, ns, model_id="global"):
             np.savez_compressed(b, **{str(i): t for i, t in enumerate(a)})
             uh.submit_bytes(b.getvalue(), n, model_id=model_id, via=st)
         else:
-            uh.submit(a, n, model_id=model_id, via=st if route in ("staged",) else None)
+            uh.submit(a, n, model_id=model_id, via=st if route in ("staged", "staged_sliced") else None)
 
 
 def _handlers(route):
@@ -95,16 +95,18 @@ def _handlers(route):
         st = StagingUpdateHandler(uh, helper=None, device=DEV, workers=2)
     elif route == "npz":
         st = StagingUpdateHandler(uh, helper=Helper(), device=DEV, workers=2, native_decode=True)
+    elif route == "staged_sliced":           # staged on arrival as parameter slices over two device entries
+        st = StagingUpdateHandler(uh, helper=None, devices=[DEV, DEV], workers=2)
     return uh, st
 
 
 def _aggregator(kind, route, uh, st, monkeypatch):
     from fedn_amd.aggregators import fedavg, fedopt
     mod = fedavg if kind == "fedavg" else fedopt
-    if route == "sliced":
+    if route in ("sliced", "staged_sliced"):
         from fedn_amd import layout
         monkeypatch.setattr(layout, "MULTIDEV_MIN_BYTES", 0)     # slice even these small models
-        return mod.Aggregator(uh, devices=[DEV, DEV])
+        return mod.Aggregator(st or uh, devices=[DEV, DEV])
     return mod.Aggregator(st or uh)
 
 
@@ -124,8 +126,8 @@ def test_fuzz_fedavg(seed, route, monkeypatch):
     want, nr = ref.fedavg_combine(list(zip(ups, ns)))
     uh, st = _handlers(route)
     try:
+        agg = _aggregator("fedavg", route, uh, st, monkeypatch)      # (the slicing rule set before staging)
         _submit_all(route, uh, st, ups, ns)
-        agg = _aggregator("fedavg", route, uh, st, monkeypatch)
         model, data = agg.combine_models(helper=_helper(route), delete_models=True)
     finally:
         if st is not None:
