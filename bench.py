@@ -87,9 +87,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-achievable", dest="achievable", action="store_false",
                     help="N = 1: skip the achievable-peak copy / read reference")
-    ap.add_argument("--transport", choices=["auto", "collective", "p2p", "p2p_kernel"], default="auto",
+    ap.add_argument("--transport", choices=["auto", "collective", "p2p", "p2p_kernel", "p2p_fused"], default="auto",
                     help="N > 1: how each folded round reaches every GPU — RCCL all-gather, direct peer DMA copies, "
-                         "or one push kernel per round (auto = the fastest in the untimed warm-up)")
+                         "one push kernel per round, or the fold kernel storing into every peer itself (auto = the "
+                         "fastest in the untimed warm-up)")
     ap.add_argument("--host-clients", type=int, default=16,
                     help="host_resident side field: host numpy updates through the plug-in (0 = skip)")
     ap.add_argument("--launch-check", action="store_true", help="rank set-up only (gloo, no GPU): the launcher's test")
@@ -703,7 +704,7 @@ def main():
         Lmax = max(c.local_len for c in geoms.values())
         full_all = torch.empty(max(c.full_len for c in geoms.values()), dtype=torch.float32, device=device)
         transports = {"collective": None}
-        engines = {"p2p": "dma", "p2p_kernel": "kernel"}    # P2PAllGather.engine of each direct transport
+        engines = {"p2p": "dma", "p2p_kernel": "kernel", "p2p_fused": "fused"}   # P2PAllGather.engine of each
         if a.transport != "collective" and (world > 1 or rccl1):
             try:
                 # double-buffered: one fence per step (the exit fence clears the other buffer); ONE set of
@@ -805,7 +806,10 @@ def main():
                             f"stream per peer, one {backend} fence per step)",
                      "p2p_kernel": f"direct peer pushes (P2PAllGather engine 'kernel': IPC-mapped, double-buffered peer "
                                    f"buffers, one fa_push kernel per round storing into every peer, one {backend} fence "
-                                   "per step)"}.get(tname, f"{backend} all_gather_into_tensor on a communication stream")
+                                   "per step)",
+                     "p2p_fused": f"fold + push fused (P2PAllGather engine 'fused': each round's fold kernel, "
+                                  f"fa_fedavg_fold_push, stores its result into this rank's and every peer's IPC-mapped, "
+                                  f"double-buffered model buffer; one {backend} fence per step)"}.get(tname, f"{backend} all_gather_into_tensor on a communication stream")
         config = {"workload": f"FedAvg {K} clients x {P_total} params {a.dtype}, param-sharded block-cyclically over "
                               f"{world} GPUs; each folded round gathered to every GPU while the next round folds, "
                               "inside the timed step (BASELINE configs[2])",

@@ -82,6 +82,9 @@ EXPORTS = {
     "fa_copy_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "fa_push": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
                                ctypes.c_void_p]),
+    "fa_fedavg_fold_push": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p]),
     "fa_peer_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "fa_host_device_ptr": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "fa_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
@@ -97,7 +100,7 @@ PROBE_EXPORTS = {
     "fa_stream_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 IPC_HANDLE_BYTES = 64    # FA_IPC_HANDLE_BYTES
 
 

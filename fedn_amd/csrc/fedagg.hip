@@ -405,6 +405,73 @@ __device__ __forceinline__ void k_fedavg_tail(X* __restrict__ agg, const ClientT
     }
 }
 
+// Destinations a piece is pushed to besides its own buffer (the peers' model buffers, IPC-mapped
+// or in-process): fa_push and the fused fold + push (fa_fedavg_fold_push).
+constexpr int kPushMax = 16;
+struct PushTable {
+    u32x4* dst[kPushMax];
+};
+
+// k_fedavg with the all-gather fused in (fa_fedavg_fold_push; sharded.P2PAllGather engine "fused"):
+// every finished strip is stored to this rank's own copy of the model AND to each peer's copy — the
+// same vector stores a copy kernel would issue, straight from the registers that hold the result, so
+// a round needs no second pass over the piece and no second launch. fp32 updates and aggregate,
+// 16-B aligned buffers, one strip per lane; the fold arithmetic and order are k_fedavg's.
+template <int U, bool INIT>
+__global__ void __launch_bounds__(kBlock)
+k_fedavg_push(float* __restrict__ agg, const ClientTable<CF32::S> tab, const int K, const int64_t P, PushTable t,
+              const int nd) {
+    using V = CF32::V;
+    constexpr int E = 4;
+    const int64_t strip = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t i0 = strip * E;
+    if (i0 + E <= P) {
+        V x[E];
+        int k = strip_start<float, float, CF32, E, INIT, false, false>(x, agg, tab, i0, E);
+        for (; k + U <= K; k += U) {
+            float y[U][E];
+#pragma unroll
+            for (int u = 0; u < U; ++u) strip_load<float, E, false>(static_cast<const float*>(tab.ptr[k + u]) + i0, y[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                V yv[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) yv[e] = widen<float, V>(y[u][e]);
+                fold_strip<CF32, E>(x, yv, tab.n[k + u], tab.N[k + u], tab.r[k + u]);
+            }
+        }
+        for (; k < K; ++k) {
+            float y[E];
+            strip_load<float, E, false>(static_cast<const float*>(tab.ptr[k]) + i0, y);
+            V yv[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) yv[e] = widen<float, V>(y[e]);
+            fold_strip<CF32, E>(x, yv, tab.n[k], tab.N[k], tab.r[k]);
+        }
+        float xo[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) xo[e] = narrow<float, V>(x[e]);
+        u32x4 w;
+        __builtin_memcpy(&w, xo, 16);
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(agg + i0));
+        for (int d = 0; d < nd; ++d) __builtin_nontemporal_store(w, t.dst[d] + strip);
+    } else if (i0 < P) {                                       // the ragged last strip
+        const int rem = (int)(P - i0);
+        V x[E];
+        int k = strip_start<float, float, CF32, E, INIT, false, false>(x, agg, tab, i0, rem);
+        for (; k < K; ++k) {
+            const float* yp = static_cast<const float*>(tab.ptr[k]) + i0;
+            for (int e = 0; e < rem; ++e) x[e] = CF32::fold(x[e], widen<float, V>(yp[e]), tab.n[k], tab.N[k], tab.r[k]);
+        }
+        for (int e = 0; e < rem; ++e) {
+            const float v = narrow<float, V>(x[e]);
+            agg[i0 + e] = v;
+            for (int d = 0; d < nd; ++d) reinterpret_cast<float*>(t.dst[d])[i0 + e] = v;
+        }
+    }
+    __threadfence_system();
+}
+
 // One lane owns S strips of E elements (strip s at lane + s*kBlock within the block's
 // span, so every wave instruction stays a contiguous 1 KiB). U clients' strips are
 // loaded before any of them is folded, so a lane keeps U*S 16-B loads in flight.
@@ -1318,11 +1385,7 @@ k_cast(TO* __restrict__ out, const TI* __restrict__ in, const CastGeom g, const 
 // nothing here is read back by this GPU); the end-of-grid system-scope release makes them visible
 // to the peers before the stream's next operation (the fence the ranks exchange).
 // ----------------------------------------------------------------------------
-constexpr int kPushMax = 16;
 constexpr int kPushWords = 4;                    // 16-B words per lane per iteration (64 B in flight)
-struct PushTable {
-    u32x4* dst[kPushMax];
-};
 
 __global__ void __launch_bounds__(kBlock) k_push(PushTable t, int nd, const u32x4* __restrict__ src, int64_t n16) {
     const int64_t stride = (int64_t)gridDim.x * kBlock * kPushWords;
@@ -2205,6 +2268,45 @@ int fa_copy_async(void* dst, const void* src, int64_t bytes, void* stream) {
     hipError_t e = hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(FA_EHIP, "fa_copy_async: %s", hipGetErrorString(e));
     return FA_OK;
+}
+
+int fa_fedavg_fold_push(float* agg, const void* const* updates, const double* n, const double* N, int K, int64_t P,
+                        int init, void* const* dsts, int ndst, void* stream) {
+    g_err[0] = 0;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (P < 0 || K < 0 || ndst < 0 || ndst > kPushMax)
+        return fail(FA_EINVAL, "fa_fedavg_fold_push: bad sizes (P=%lld, K=%d, ndst=%d <= %d)", (long long)P, K, ndst,
+                    kPushMax);
+    if (init && K < 1) return fail(FA_EINVAL, "fa_fedavg_fold_push: init requires K >= 1");
+    if (K == 0 || P == 0) return FA_OK;
+    if (!agg || !updates || !n || !N || (ndst > 0 && !dsts)) return fail(FA_EINVAL, "fa_fedavg_fold_push: null pointer argument");
+    if (!aligned16(agg)) return fail(FA_EINVAL, "fa_fedavg_fold_push: agg not 16-B aligned");
+    PushTable t{};
+    for (int d = 0; d < ndst; ++d) {
+        if (!dsts[d] || !aligned16(dsts[d])) return fail(FA_EINVAL, "fa_fedavg_fold_push: destination %d null or not 16-B aligned", d);
+        t.dst[d] = static_cast<u32x4*>(dsts[d]);
+    }
+    for (int k = 0; k < K; ++k)
+        if (!updates[k] || !aligned16(updates[k])) return fail(FA_EINVAL, "fa_fedavg_fold_push: updates[%d] null or not 16-B aligned", k);
+    // clients beyond one kernarg table fold first (plain launches); the last table's launch pushes
+    const int last0 = ((K - 1) / kMaxK) * kMaxK;
+    if (last0 > 0) {
+        const int rc = fa_fedavg_fold(agg, FA_F32, updates, FA_F32, n, N, last0, P, init, stream);
+        if (rc) return rc;
+    }
+    ClientTable<CF32::S> tab;
+    const int cnt = K - last0;
+    fill_table<CF32::S>(tab, updates, n, N, last0, cnt);
+    const bool first = init && last0 == 0;
+    const dim3 grid((unsigned)((P + 4 * (int64_t)kBlock - 1) / (4 * (int64_t)kBlock)));
+    if (cnt <= 8) {
+        if (first) hipLaunchKernelGGL((k_fedavg_push<8, true>), grid, dim3(kBlock), 0, st, agg, tab, cnt, P, t, ndst);
+        else hipLaunchKernelGGL((k_fedavg_push<8, false>), grid, dim3(kBlock), 0, st, agg, tab, cnt, P, t, ndst);
+    } else {
+        if (first) hipLaunchKernelGGL((k_fedavg_push<4, true>), grid, dim3(kBlock), 0, st, agg, tab, cnt, P, t, ndst);
+        else hipLaunchKernelGGL((k_fedavg_push<4, false>), grid, dim3(kBlock), 0, st, agg, tab, cnt, P, t, ndst);
+    }
+    return check_launch("fa_fedavg_fold_push: kernel launch");
 }
 
 int fa_push(void* const* dsts, int ndst, const void* src, int64_t bytes, void* stream) {

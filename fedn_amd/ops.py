@@ -509,6 +509,21 @@ def copy_ptr_async(dst_ptr, src_ptr, nbytes, stream, device):
         _abi.check(_abi.load().fa_copy_async(int(dst_ptr), int(src_ptr), int(nbytes), ctypes_stream(stream)))
 
 
+def fedavg_fold_push(agg_ptr, ptrs, n, N, P, init, dst_ptrs, stream, device):
+    """The fp32 fold of ``P`` elements into device address ``agg_ptr`` whose kernel also stores the
+    result to every address in ``dst_ptrs`` (``fa_fedavg_fold_push``: fold and all-gather push in
+    one pass); client table and destinations as device addresses, 16-B aligned."""
+    K = len(ptrs)
+    if len(n) != K or len(N) != K:
+        raise ValueError("n and N must have one entry per update")
+    nd = len(dst_ptrs)
+    with _on(device):
+        _abi.check(_abi.load().fa_fedavg_fold_push(
+            int(agg_ptr), (ctypes.c_void_p * max(1, K))(*ptrs), (ctypes.c_double * max(1, K))(*n),
+            (ctypes.c_double * max(1, K))(*N), K, int(P), int(bool(init)),
+            (ctypes.c_void_p * max(1, nd))(*[int(p) for p in dst_ptrs]), nd, ctypes_stream(stream)))
+
+
 def push(dst_ptrs, src, nbytes, stream):
     """``nbytes`` of device tensor ``src`` (from its start) to every device address in ``dst_ptrs``
     on ``stream`` with ONE kernel (``fa_push``): the source is read once, each destination written

@@ -221,6 +221,14 @@ class CyclicShardedFedAvg:
             self.fold_fn(agg_local[sl], [u[sl] for u in updates_local], n, N, init)
         return fold
 
+    def _fusable(self, updates_local, out):
+        """The fused fold + push applies: the default kernel, fp32 updates and model on one device,
+        contiguous buffers of the geometry's sizes."""
+        return bool(self._kernel and out.dtype == torch.float32 and out.is_cuda and updates_local
+                    and all(u.dtype == torch.float32 and u.device == out.device and u.is_contiguous()
+                            and u.numel() >= self.local_len for u in updates_local)
+                    and out.numel() >= self.full_len)
+
     def fold_allgather(self, agg_local, updates_local, n, N, init, out=None, p2p=None):
         """Fold every round and gather it as soon as it is folded; returns the full model
         (``full[:P]``; on the host for gloo). ``agg_local`` / ``updates_local``: local_len each.
@@ -239,6 +247,15 @@ class CyclicShardedFedAvg:
             cur = torch.cuda.current_stream(dev)
             p2p.begin()
             out = p2p.full
+            if p2p.engine == "fused" and self._fusable(updates_local, out):
+                from . import ops
+                bases = [u.data_ptr() for u in updates_local]
+                for i in range(self.rounds):
+                    at = (i * W + self.rank) * C
+                    ops.fedavg_fold_push(out.data_ptr() + at * 4, [b + i * C * 4 for b in bases], n, N, C, init,
+                                         p2p.peer_ptrs(at), cur, dev)
+                p2p.fence()
+                return out[:self.P]
             fold = self.round_folder(agg_local, updates_local, n, N, init, cur)
             for i in range(self.rounds):
                 sl = slice(i * C, (i + 1) * C)
@@ -302,7 +319,10 @@ class P2PAllGather:
     ``"kernel"``, ONE ``fa_push`` launch on a push stream that reads the piece once and stores it
     into every peer's buffer (the CUs drive all links at once; it shares the chip with the next
     round's fold). Which one moves a node's links faster is measured there (``bench.py`` chooses in
-    its warm-up); the attribute may be switched between steps.
+    its warm-up); the attribute may be switched between steps. ``"fused"``: no separate push at all —
+    ``CyclicShardedFedAvg.fold_allgather`` folds each round with ``fa_fedavg_fold_push``, whose kernel
+    stores every result element into this rank's buffer and every peer's as it is produced (fp32;
+    other dtypes push with the kernel engine).
 
     ``spare``: a second buffer of the same size makes the gather double-buffered: the steps
     alternate between the two, so the exit fence of step t (every rank has entered step t, i.e. is
@@ -310,7 +330,7 @@ class P2PAllGather:
     pushes — one fence per step instead of two; a result then stays valid until the step after next.
     """
 
-    ENGINES = ("dma", "kernel")
+    ENGINES = ("dma", "kernel", "fused")
 
     def __init__(self, full, group=None, spare=None, engine="dma"):
         from . import ops
@@ -376,7 +396,7 @@ class P2PAllGather:
         if at < 0 or at + src.numel() > self.full.numel():
             raise ValueError("P2PAllGather.push: piece outside the buffer")
         nbytes = src.numel() * self.esize
-        if self.engine == "kernel":
+        if self.engine in ("kernel", "fused"):
             dsts = [maps[self.cur][1] + at * self.esize for maps in self.peers.values()]
             if local:
                 dsts.append(self.full.data_ptr() + at * self.esize)
@@ -388,6 +408,11 @@ class P2PAllGather:
             st.wait_event(after)
             ops.copy_async(self.peers[r][self.cur][1] + at * self.esize, src, nbytes, st)
         return False
+
+    def peer_ptrs(self, at):
+        """Device addresses of element ``at`` of every peer's current buffer (the fused engine's
+        destinations)."""
+        return [maps[self.cur][1] + at * self.esize for maps in self.peers.values()]
 
     def fence(self):
         cur = torch.cuda.current_stream(self.device)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 5
+#define FA_ABI_VERSION 6
 
 /* element type codes */
 enum fa_dtype {
@@ -264,6 +264,10 @@ int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, co
  *                    own link, all at once; 16-B aligned pointers. The alternative to one
  *                    fa_copy_async per peer that the all-gather picks between (sharded.P2PAllGather;
  *                    replaces the all-gather consumed at roundhandler.py:465-468)
+ * fa_fedavg_fold_push  fa_fedavg_fold (fp32 updates, fp32 aggregate, 16-B aligned buffers) whose kernel
+ *                    also stores every finished element to each of ndst (<= 16) destinations: the
+ *                    fold and the all-gather push in ONE pass (sharded.P2PAllGather engine "fused";
+ *                    the peers' buffers IPC-mapped or in-process). agg is this rank's own copy.
  * fa_peer_enable     let device dev read / write device peer's memory directly (in-process);
  *                    already enabled is not an error
  * fa_host_register   page-lock host memory the caller mapped (the node's shared host model that
@@ -280,6 +284,8 @@ int fa_ipc_open(const void* handle, uint64_t offset, void** base, void** dptr);
 int fa_ipc_close(void* base);
 int fa_copy_async(void* dst, const void* src, int64_t bytes, void* stream);
 int fa_push(void* const* dsts, int ndst, const void* src, int64_t bytes, void* stream);
+int fa_fedavg_fold_push(float* agg, const void* const* updates, const double* n, const double* N, int K, int64_t P,
+                        int init, void* const* dsts, int ndst, void* stream);
 int fa_peer_enable(int dev, int peer);
 int fa_host_register(void* p, int64_t bytes);
 int fa_host_unregister(void* p);

@@ -1412,7 +1412,7 @@ def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False, engine="dm
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("engine", ["dma", "kernel"])
+@pytest.mark.parametrize("engine", ["dma", "kernel", "fused"])
 @pytest.mark.parametrize("world,P,chunk,double", [(2, 200_003, 8192, False), (3, 1_000_000, 65536, False),
                                                   (2, 200_003, 8192, True), (3, 1_000_000, 65536, True)])
 def test_p2p_allgather_gloo_hip(world, P, chunk, double, engine):
@@ -1452,6 +1452,46 @@ def test_p2p_allgather_gloo_hip(world, P, chunk, double, engine):
         for step, got in enumerate(outs):
             w = want2 if step >= 2 else want
             assert np.array_equal(got.view(np.uint32), w.view(np.uint32)), f"rank {rank} step {step}"
+
+
+@pytest.mark.parametrize("K", [1, 3, 9, 64, 70])
+@pytest.mark.parametrize("P,ndst", [(1, 1), (4099, 0), (4099, 3), (1_000_003, 7)])
+def test_fedavg_fold_push(K, P, ndst):
+    """fa_fedavg_fold_push: the fold written to agg AND to every destination, bit-identical to
+    fa_fedavg_fold (clients beyond one 64-entry table folded first, the last table pushes; a ragged
+    last strip); init and continuation; misaligned addresses refused."""
+    from fedn_amd import ops
+    from fedn_amd._abi import FedAggError
+    g = torch.Generator(device=DEV).manual_seed(K * 7 + ndst)
+    base = torch.randn(P, generator=g, device=DEV)
+    ups = [torch.randn(P, generator=g, device=DEV).mul_(0.01).add_(base) for _ in range(K)]
+    ns = [int(v) for v in np.random.default_rng(K).integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
+    want = torch.empty(P, device=DEV)
+    ops.fedavg_fold(want, ups, ns, Ns, init=True)
+    agg = torch.full((P + 64,), float("nan"), device=DEV)
+    dsts = [torch.full((P + 64,), float("nan"), device=DEV) for _ in range(ndst)]
+    st = torch.cuda.current_stream(DEV)
+    ops.fedavg_fold_push(agg.data_ptr(), [u.data_ptr() for u in ups], ns, Ns, P, True, [d.data_ptr() for d in dsts],
+                         st, DEV)
+    torch.cuda.synchronize()
+    for t in [agg] + dsts:
+        assert torch.equal(t[:P].view(torch.int32), want.view(torch.int32))
+        assert bool(torch.isnan(t[P:]).all())
+    # continuation (init=False): fold the same clients again onto the result, as fa_fedavg_fold does
+    want2 = want.clone()
+    ops.fedavg_fold(want2, ups, ns, [x + Ns[-1] for x in Ns], init=False)
+    ops.fedavg_fold_push(agg.data_ptr(), [u.data_ptr() for u in ups], ns, [x + Ns[-1] for x in Ns], P, False,
+                         [d.data_ptr() for d in dsts], st, DEV)
+    torch.cuda.synchronize()
+    for t in [agg] + dsts:
+        assert torch.equal(t[:P].view(torch.int32), want2.view(torch.int32))
+    if P > 1:
+        with pytest.raises(FedAggError, match="aligned"):
+            ops.fedavg_fold_push(agg.data_ptr() + 4, [u.data_ptr() for u in ups], ns, Ns, P - 1, True, [], st, DEV)
+        with pytest.raises(FedAggError, match="aligned"):
+            ops.fedavg_fold_push(agg.data_ptr(), [u.data_ptr() for u in ups], ns, Ns, P, True, [agg.data_ptr() + 8],
+                                 st, DEV)
 
 
 @pytest.mark.parametrize("nbytes", [16, 4004, 1 << 20, (64 << 20) + 12])
