@@ -469,7 +469,20 @@ k_fedavg_push(float* __restrict__ agg, const ClientTable<CF32::S> tab, const int
             for (int d = 0; d < nd; ++d) reinterpret_cast<float*>(t.dst[d])[i0 + e] = v;
         }
     }
-    __threadfence_system();
+}
+
+// One system-scope release per XCD after a grid that stored into other GPUs' memory (k_fedavg_push,
+// k_push): the stores are visible to the peers before anything later on the stream (the fence the
+// ranks exchange). A release inside every wave of a large grid would write the L2 back hundreds of
+// thousands of times; workgroups are dealt round-robin over the 8 XCDs, so 64 single-wave
+// workgroups cover each XCD's L2 several times over.
+__global__ void __launch_bounds__(64) k_release() {
+    if (threadIdx.x == 0) __threadfence_system();
+}
+
+int launch_release(hipStream_t st) {
+    hipLaunchKernelGGL(k_release, dim3(64), dim3(64), 0, st);
+    return check_launch("release after peer stores");
 }
 
 // One lane owns S strips of E elements (strip s at lane + s*kBlock within the block's
@@ -1382,8 +1395,8 @@ k_cast(TO* __restrict__ out, const TI* __restrict__ in, const CastGeom g, const 
 // "kernel" engine). Each lane loads a 16-B word of the piece ONCE and stores it to every
 // destination: the piece crosses each peer's own xGMI link once, all links at once, and local HBM
 // is read once instead of once per DMA copy. The stores are plain vector stores (non-temporal:
-// nothing here is read back by this GPU); the end-of-grid system-scope release makes them visible
-// to the peers before the stream's next operation (the fence the ranks exchange).
+// nothing here is read back by this GPU); k_release after the grid makes them visible to the peers
+// before the stream's next operation (the fence the ranks exchange).
 // ----------------------------------------------------------------------------
 constexpr int kPushWords = 4;                    // 16-B words per lane per iteration (64 B in flight)
 
@@ -1405,7 +1418,6 @@ __global__ void __launch_bounds__(kBlock) k_push(PushTable t, int nd, const u32x
             }
         }
     }
-    __threadfence_system();
 }
 
 // the < 16 B tail of a piece whose length is not a multiple of 16 (one lane per byte)
@@ -1413,7 +1425,6 @@ __global__ void k_push_tail(PushTable t, int nd, const uint8_t* __restrict__ src
     const int b = threadIdx.x;
     if (b < rem)
         for (int d = 0; d < nd; ++d) reinterpret_cast<uint8_t*>(t.dst[d])[off + b] = src[off + b];
-    __threadfence_system();
 }
 
 #ifdef FEDAGG_PROBES
@@ -2306,7 +2317,8 @@ int fa_fedavg_fold_push(float* agg, const void* const* updates, const double* n,
         if (first) hipLaunchKernelGGL((k_fedavg_push<4, true>), grid, dim3(kBlock), 0, st, agg, tab, cnt, P, t, ndst);
         else hipLaunchKernelGGL((k_fedavg_push<4, false>), grid, dim3(kBlock), 0, st, agg, tab, cnt, P, t, ndst);
     }
-    return check_launch("fa_fedavg_fold_push: kernel launch");
+    const int rc = check_launch("fa_fedavg_fold_push: kernel launch");
+    return rc ? rc : (ndst > 0 ? launch_release(st) : FA_OK);
 }
 
 int fa_push(void* const* dsts, int ndst, const void* src, int64_t bytes, void* stream) {
@@ -2336,7 +2348,7 @@ int fa_push(void* const* dsts, int ndst, const void* src, int64_t bytes, void* s
                            rem);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(FA_EHIP, "fa_push: %s", hipGetErrorString(e));
-    return FA_OK;
+    return launch_release(st);
 }
 
 int fa_host_device_ptr(const void* host, void** dptr) {
