@@ -113,9 +113,9 @@ def fast_admission(layout):
 
             def f(arrays, dst_ptr, plan=plan, admit=admit, gstart=gstart):
                 t = admit(plan, arrays, dst_ptr, gstart, PACK_THREADS)
-                if t == -2:
+                if t == -2:                     # the gather queue refused the job: its reason
                     from . import codec
-                    codec.gather_wait(-1)       # raises the codec's last error
+                    raise codec.CodecError(f"fnpz_gather_start: {codec.load_lib().fnpz_last_error().decode(errors='replace')}")
                 return t
         layout._fast_admit = f
     return f
