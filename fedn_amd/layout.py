@@ -115,7 +115,8 @@ def fast_admission(layout):
                 t = admit(plan, arrays, dst_ptr, gstart, PACK_THREADS)
                 if t == -2:                     # the gather queue refused the job: its reason
                     from . import codec
-                    raise codec.CodecError(f"fnpz_gather_start: {codec.load_lib().fnpz_last_error().decode(errors='replace')}")
+                    why = codec.load_lib().fnpz_last_error().decode(errors="replace")
+                    raise codec.CodecError(f"fnpz_gather_start: {why}")
                 return t
         layout._fast_admit = f
     return f
