@@ -230,7 +230,10 @@ class Layout:
         return lay
 
     def signature(self):
-        return (tuple(self.shapes), tuple(str(d) for d in self.dtypes))
+        sig = self.__dict__.get("_signature")
+        if sig is None:                 # a Layout never changes: computed once
+            sig = self._signature = (tuple(self.shapes), tuple(str(d) for d in self.dtypes))
+        return sig
 
     def check(self, arrays):
         """Raise (as numpy would, on a non-broadcastable mismatch) if ``arrays`` does not match."""
@@ -247,7 +250,7 @@ class Layout:
 
     def check_layout(self, other):
         """Like :meth:`check` for an already-laid-out update (a staged model's Layout)."""
-        if other.signature() == self.signature():
+        if other is self or other.signature() == self.signature():
             return
         if len(other.shapes) != len(self.shapes):
             raise ValueError(f"model has {len(other.shapes)} tensors, expected {len(self.shapes)}")

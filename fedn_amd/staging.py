@@ -586,6 +586,13 @@ class FedAvgPipeline(_Pipeline):
                 self._flush()
             self.nfolds += 1
             return
+        elif self.general is None and self._plain and type(arrays) is StagedModel and arrays.layout is self.layout:
+            # staged on arrival in this very layout (the ingest's round end): nothing else to check
+            self.pending.append((self._resident(arrays), n, N))
+            if len(self.pending) >= BATCH:
+                self._flush()
+            self.nfolds += 1
+            return
         if self.general is None and (not self.compatible(arrays) or
                                      mixed.int_float_n(self.layout.dtypes, self.nfolds, n) or
                                      mixed.per_tensor_dtypes(self.layout.dtypes)):
@@ -1060,6 +1067,13 @@ class FedOptPipeline(_Pipeline):
         elif self.general is None and self.fused_ok and type(arrays) is list and self.fast_host(arrays):
             self.pending.append((self.put_small(arrays), n, N))      # a small float model's update
             if len(self.pending) >= BATCH or self.arena_full():
+                self._flush()
+            self.nfolds += 1
+            return
+        elif self.general is None and self.fused_ok and type(arrays) is StagedModel and arrays.layout is self.layout:
+            # staged on arrival in this very layout (the ingest's round end): nothing else to check
+            self.pending.append((self._resident(arrays), n, N))
+            if len(self.pending) >= BATCH:
                 self._flush()
             self.nfolds += 1
             return
