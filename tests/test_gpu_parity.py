@@ -1377,7 +1377,7 @@ def test_sharded_gloo_world2_hip_kernel():
     assert np.array_equal(res[0][3].view(np.uint64), want_opt[0].view(np.uint64))
 
 
-def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False, engine="dma"):
+def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False, engine="dma", bf16=False):
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -1391,6 +1391,8 @@ def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False, engine="dm
         g = torch.Generator(device="cuda:0").manual_seed(5)
         base = torch.randn(P, generator=g, device="cuda:0")
         ups = [torch.randn(P, generator=g, device="cuda:0").mul_(0.01).add_(base) for _ in range(K)]
+        if bf16:                                      # not fusable: the "fused" engine pushes with the kernel
+            ups = [u.to(torch.bfloat16) for u in ups]
         ns = [int(v) for v in np.random.default_rng(5).integers(1, 5001, K)]
         Ns = [int(v) for v in np.cumsum(ns)]
         cs = CyclicShardedFedAvg(P, chunk=chunk)
@@ -1402,7 +1404,7 @@ def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False, engine="dm
         outs = []
         for step in range(4):                         # buffers reused: entry + exit fences, or alternation
             if step >= 2:                             # later rounds of the session: other updates
-                loc = [cs.local(u.add(1.0)) for u in ups]
+                loc = [cs.local(u.add(1.0).to(u.dtype)) for u in ups]
             out = cs.fold_allgather(aggc, loc, ns, Ns, init=True, p2p=p2p)
             torch.cuda.synchronize()
             outs.append(out.cpu().numpy().copy())
@@ -1410,6 +1412,42 @@ def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False, engine="dm
         q.put((rank, outs))
     finally:
         dist.destroy_process_group()
+
+
+def test_p2p_allgather_fused_engine_bf16_falls_back():
+    """The fused engine applies to fp32 updates; bf16 updates fold with the regular kernel and push
+    with the push kernel — still bit-identical to one single-device fold (2 processes, one GPU)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from fedn_amd import ops
+    P, K, world, chunk = 200_003, 9, 2, 8192
+    s_ = socket.socket()
+    s_.bind(("127.0.0.1", 0))
+    port = s_.getsockname()[1]
+    s_.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pc = mp.start_processes(_p2p_gloo_worker, args=(world, port, P, K, chunk, q, True, "fused", True), nprocs=world,
+                            join=False, start_method="spawn")
+    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    while not pc.join(timeout=60):
+        pass
+    g = torch.Generator(device=DEV).manual_seed(5)
+    base = torch.randn(P, generator=g, device=DEV)
+    ups = [torch.randn(P, generator=g, device=DEV).mul_(0.01).add_(base).to(torch.bfloat16) for _ in range(K)]
+    ns = [int(v) for v in np.random.default_rng(5).integers(1, 5001, K)]
+    Ns = [int(v) for v in np.cumsum(ns)]
+    want = torch.empty(P, device=DEV)
+    ops.fedavg_fold(want, ups, ns, Ns, init=True)
+    want2 = torch.empty(P, device=DEV)
+    ops.fedavg_fold(want2, [u.add(1.0).to(torch.bfloat16) for u in ups], ns, Ns, init=True)
+    want, want2 = want.cpu().numpy(), want2.cpu().numpy()
+    for rank, outs in res:
+        for step, got in enumerate(outs):
+            w = want2 if step >= 2 else want
+            assert np.array_equal(got.view(np.uint32), w.view(np.uint32)), f"rank {rank} step {step}"
 
 
 @pytest.mark.parametrize("engine", ["dma", "kernel", "fused"])
