@@ -53,12 +53,18 @@ def make_fedavg_pipeline(first, device=None, devices=None, helper=None, cache=No
     return FedAvgPipeline(device or (devices[0] if devices else None) or default_device(), first, cache=cache)
 
 
+_HIP_SEEN = False      # torch.cuda.is_available() was True once in this process (it stays so)
+
+
 def default_device():
+    global _HIP_SEEN
     dev = os.environ.get("FEDN_AMD_DEVICE")
     if dev:
         return torch.device(dev)
-    if not torch.cuda.is_available():
-        raise RuntimeError("fedn_amd aggregators need a HIP device (torch.cuda.is_available() is False)")
+    if not _HIP_SEEN:
+        if not torch.cuda.is_available():
+            raise RuntimeError("fedn_amd aggregators need a HIP device (torch.cuda.is_available() is False)")
+        _HIP_SEEN = True
     return torch.device("cuda", torch.cuda.current_device())
 
 

@@ -131,7 +131,7 @@ def fedavg_fold(agg, updates, n, N, init, stream=None):
         _check_dev(f"updates[{i}]", u, P, dev)
         if u.dtype != upd_dt:
             raise TypeError("all updates in one fold call must share a dtype")
-    with torch.cuda.device(dev):        # launch on the tensors' device (multi-GPU processes)
+    with _on(dev):        # launch on the tensors' device (multi-GPU processes)
         st = _stream_handle(agg, stream)
         rc = lib.fa_fedavg_fold(agg.data_ptr(), fa_dtype(agg), _abi.ptr_array([u.data_ptr() for u in updates]),
                                 fa_dtype(upd_dt), _abi.double_array(n), _abi.double_array(N), K, P, int(bool(init)), st)
@@ -154,7 +154,7 @@ def fedavg_fold_ptrs(agg, ptrs, upd_dtype, n, N, init, stream=None):
     if agg.device.index == torch.cuda.current_device():      # the common case: no device switch
         rc = lib.fa_fedavg_fold(*args, _stream_handle(agg, stream))
     else:
-        with torch.cuda.device(agg.device):
+        with _on(agg.device):
             rc = lib.fa_fedavg_fold(*args, _stream_handle(agg, stream))
     _abi.check(rc)
     return agg
@@ -175,7 +175,7 @@ def weighted_sum(acc, updates, w, stream=None):
         _check_dev(f"updates[{i}]", u, P, dev)
         if u.dtype != upd_dt:
             raise TypeError("all updates in one weighted_sum call must share a dtype")
-    with torch.cuda.device(dev):
+    with _on(dev):
         st = _stream_handle(acc, stream)
         rc = lib.fa_weighted_sum(acc.data_ptr(), fa_dtype(acc), _abi.ptr_array([u.data_ptr() for u in updates]),
                                  fa_dtype(upd_dt), _abi.double_array(w), K, P, st)
@@ -192,7 +192,7 @@ def running_mean(g, m, a, b, T, stream=None):
     _check_dev("m", m, P, g.device)
     if m.dtype != g.dtype:
         raise TypeError(f"running_mean: model dtype {m.dtype} differs from the running model's {g.dtype}")
-    with torch.cuda.device(g.device):
+    with _on(g.device):
         st = _stream_handle(g, stream)
         rc = lib.fa_running_mean(g.data_ptr(), fa_dtype(g), m.data_ptr(), float(a), float(b), float(T), P, st)
     _abi.check(rc)
@@ -274,7 +274,7 @@ def fedopt_step(old, updates, n, N, *, first, final, pg=None, m_in=None, m_out=N
                             f", v_out/out {state_dt}")
     flags = (_abi.FA_PG_FIRST if first else 0) | (_abi.FA_PG_FINAL if final else 0)
     ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
-    with torch.cuda.device(dev):
+    with _on(dev):
         st = _stream_handle(old, stream)
         rc = lib.fa_fedopt_step_ex(
             old.data_ptr(), fa_dtype(old), _abi.ptr_array([u.data_ptr() for u in updates]), fa_dtype(upd_dt),
@@ -304,7 +304,7 @@ def fedopt_step_raw(old_ptr, old_dt, upd_ptrs, upd_dt, n, N, P, *, first, final,
     _, m_np = fedopt_dtypes(upd_dt, old_dt, None if m_in is None else m_in.dtype)
     flags = (_abi.FA_PG_FIRST if first else 0) | (_abi.FA_PG_FINAL if final else 0)
     ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
-    with torch.cuda.device(device):
+    with _on(device):
         rc = _abi.load().fa_fedopt_step_ex(
             int(old_ptr), fa_dtype(old_dt), _abi.ptr_array([int(u) for u in upd_ptrs]), fa_dtype(upd_dt),
             _abi.double_array(n), _abi.double_array(N), K, int(pg_ptr), flags,
@@ -353,7 +353,7 @@ def cast(out, x, stream=None):
             mt.append(t)
     if len(ms) > 8:
         raise ValueError(f"cast: {len(ms)} non-mergeable dimensions (kernel limit 8)")
-    with torch.cuda.device(out.device):
+    with _on(out.device):
         st = _stream_handle(out, stream)
         rc = lib.fa_cast(out.data_ptr(), fa_dtype(out), x.data_ptr(), fa_dtype(x), len(ms), _abi.int64_array(ms),
                          _abi.int64_array(mt), st)
@@ -435,7 +435,7 @@ def elementwise(op, out, x=None, y=None, a=0.0, b=0.0, stream=None):
         if op not in _EW:
             raise ValueError(f"unknown elementwise op {op}")
         return out
-    with torch.cuda.device(out.device):
+    with _on(out.device):
         st = _stream_handle(out, stream)
         rc = lib.fa_elementwise(_EW[op], out.data_ptr(), fa_dtype(out), 0 if x is None else x.data_ptr(),
                                 fa_dtype(out) if x is None else fa_dtype(x), 0 if y is None else y.data_ptr(),
@@ -453,7 +453,7 @@ def norm1(x, matrix, stream=None):
     rows, cols = (x.shape[0], x.shape[1]) if matrix else (1, x.numel())
     work = torch.empty(max(1, int(lib.fa_norm1_work(rows, cols, int(matrix)))), dtype=torch.float64, device=x.device)
     out = torch.empty((), dtype=torch.float64, device=x.device)
-    with torch.cuda.device(x.device):
+    with _on(x.device):
         st = _stream_handle(x, stream)
         rc = lib.fa_norm1(out.data_ptr(), x.data_ptr(), fa_dtype(x), rows, cols, int(matrix), work.data_ptr(), st)
     _abi.check(rc)
@@ -468,7 +468,7 @@ def ipc_handle(t):
     lib = _abi.load()
     h = ctypes.create_string_buffer(_abi.IPC_HANDLE_BYTES)
     off = ctypes.c_uint64(0)
-    with torch.cuda.device(t.device):
+    with _on(t.device):
         _abi.check(lib.fa_ipc_get_handle(t.data_ptr(), h, ctypes.byref(off)))
     return h.raw, int(off.value)
 
@@ -480,7 +480,7 @@ def ipc_open(handle, offset, device):
     if len(handle) != _abi.IPC_HANDLE_BYTES:
         raise ValueError(f"IPC handle must be {_abi.IPC_HANDLE_BYTES} bytes")
     base, ptr = ctypes.c_void_p(), ctypes.c_void_p()
-    with torch.cuda.device(device):
+    with _on(device):
         _abi.check(lib.fa_ipc_open(ctypes.create_string_buffer(handle, len(handle)), int(offset), ctypes.byref(base),
                                    ctypes.byref(ptr)))
     return int(base.value or 0), int(ptr.value or 0)
@@ -488,7 +488,7 @@ def ipc_open(handle, offset, device):
 
 def ipc_close(base, device):
     lib = _abi.load()
-    with torch.cuda.device(device):
+    with _on(device):
         _abi.check(lib.fa_ipc_close(base))
 
 
@@ -543,6 +543,8 @@ _NULL_CTX = contextlib.nullcontext()
 def _on(device):
     """``torch.cuda.device(device)`` unless it is already the current device (the per-round and
     per-update copy calls of the pipelines pay the context switch only when they need it)."""
+    if device is None:
+        return _NULL_CTX
     idx = device.index if isinstance(device, torch.device) else torch.device(device).index
     if idx is None or idx == torch.cuda.current_device():
         return _NULL_CTX
@@ -557,7 +559,7 @@ def peer_enable(dev, peer):
 def host_device_ptr(host_ptr, device):
     """Device address of page-locked host memory at ``host_ptr`` (raises for pageable memory)."""
     out = ctypes.c_void_p()
-    with torch.cuda.device(device):
+    with _on(device):
         _abi.check(_abi.load().fa_host_device_ptr(int(host_ptr), ctypes.byref(out)))
     return int(out.value or 0)
 
@@ -568,7 +570,7 @@ def fedavg_fold_raw(out_ptr, out_dtype, P, ptrs, upd_dtype, n, N, init, stream, 
     K = len(ptrs)
     if len(n) != K or len(N) != K:
         raise ValueError("n and N must have one entry per update")
-    with torch.cuda.device(device):
+    with _on(device):
         _abi.check(_abi.load().fa_fedavg_fold(int(out_ptr), fa_dtype(out_dtype), (ctypes.c_void_p * max(1, K))(*ptrs),
                                               fa_dtype(upd_dtype), (ctypes.c_double * max(1, K))(*n),
                                               (ctypes.c_double * max(1, K))(*N), K, int(P), int(bool(init)),
