@@ -55,7 +55,7 @@ def _worker(rank, world, port, P, K, seed, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,P", [(2, 10_000), (2, 4096), (3, 5_003)])
+@pytest.mark.parametrize("world,P", [(2, 10_000), (2, 4096), (3, 5_003), (4, 20_011), (8, 70_001)])
 def test_sharded_fedavg_gloo(world, P):
     from oracle import numpy_ref as ref
     K, seed = 5, 17
@@ -121,10 +121,11 @@ def _fedopt_worker(rank, world, port, P, K, seed, q):
         dist.destroy_process_group()
 
 
-def test_sharded_fedopt_gloo_two_rounds():
+@pytest.mark.parametrize("world,P", [(2, 6000), (8, 40_003)])
+def test_sharded_fedopt_gloo_two_rounds(world, P):
     """FedOpt state (m, v) stays sharded across rounds; gathered models == single-process oracle."""
     from oracle import numpy_ref as ref
-    P, K, seed, world = 6000, 4, 23, 2
+    K, seed = 4, 23
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     pc = mp.start_processes(_fedopt_worker, args=(world, _free_port(), P, K, seed, q), nprocs=world, join=False,
@@ -163,10 +164,13 @@ def _cyclic_worker(rank, world, port, P, K, chunk, seed, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,P,chunk", [(2, 10_000, 1024), (3, 5_003, 1024), (2, 3_000, 4096), (3, 9_216, 1024)])
+@pytest.mark.parametrize("world,P,chunk", [(2, 10_000, 1024), (3, 5_003, 1024), (2, 3_000, 4096), (3, 9_216, 1024),
+                                             (4, 40_001, 2_500), (8, 100_003, 1_571), (8, 2_000, 1_024)])
 def test_cyclic_fold_allgather_gloo(world, P, chunk):
     """Block-cyclic shards, per-round fold + all-gather straight into natural order: every
-    rank ends with the full model, bit-identical to the single-process oracle."""
+    rank ends with the full model, bit-identical to the single-process oracle. World 4 / 8 are
+    the N = 4 / 8 geometries of bench.py --gpus N (ragged last chunk; at (8, 2000, 1024) some
+    ranks own nothing)."""
     from oracle import numpy_ref as ref
     K, seed = 4, 29
     ctx = mp.get_context("spawn")
