@@ -323,9 +323,15 @@ class _Pipeline:
         the native test first (``self._admit``); None, with nothing changed, if ``arrays`` is not
         exactly this layout."""
         a = self._arena
+        if a is not None and a.count >= a.cap:
+            # every caller flushes a full arena right after its put; a full one here is a bug, and
+            # packing into it would write past its pinned block
+            raise RuntimeError(f"staging arena full ({a.count} of {a.cap} updates) before put_small")
         if a is None:
             if not self._arenas:
-                cap = max(1, min(BATCH, ARENA_BYTES // self.layout.nbytes))
+                # >= 2: FedAvg's first update waits in the arena outside ``pending`` (the callers'
+                # full-arena flush follows the NEXT put), so one slot is never enough
+                cap = max(2, min(BATCH, ARENA_BYTES // self.layout.nbytes))
                 self._arenas = [_Arena(cap, self.layout.nbytes, self.device) for _ in range(2)]
             a = self._arenas[self._arena_i]
             self._arena_i = (self._arena_i + 1) % len(self._arenas)
