@@ -4,8 +4,8 @@ production only models of 4 MB to GBs take: piecewise pack + H2D with one fold l
 (STAGE_PIECES_MIN / STAGE_PIECE, piece boundaries at odd byte offsets that split elements), the
 result's chunked D2H (MIN_CHUNK_BYTES), arenas holding one or two updates with partial uploads
 (ARENA_BYTES / ARENA_UPLOAD_EVERY), zero-copy folds of the arena on or off (ZERO_COPY_BYTES),
-small update batches per launch (BATCH), and the large / small split itself
-(SMALL_UPDATE_BYTES). Every threshold is read by staging.py at call time; the values are drawn per
+small update batches per launch (BATCH), FedOpt's pinned ring for the global model (RING_BYTES) and
+the large / small split itself (SMALL_UPDATE_BYTES). Every threshold is read by staging.py at call time; the values are drawn per
 seed. Bar: bit-exact values and dtypes against the oracle, every update counted."""
 import numpy as np
 import pytest
@@ -41,6 +41,10 @@ def _thresholds(seed, monkeypatch):
          "BATCH": pick(1, 3, 64)}
     for k, v in t.items():
         monkeypatch.setattr(staging, k, v)
+    # FedOpt's global model streams through a ring of pinned pieces (HostStreamer, RING_BYTES bound
+    # as its default argument)
+    t["RING_BYTES"] = pick(4096, 6000, 64 << 20)
+    monkeypatch.setattr(staging.HostStreamer.__init__, "__defaults__", (3, t["RING_BYTES"]))
     return t
 
 
