@@ -4,8 +4,9 @@ production only models of 4 MB to GBs take: piecewise pack + H2D with one fold l
 (STAGE_PIECES_MIN / STAGE_PIECE, piece boundaries at odd byte offsets that split elements), the
 result's chunked D2H (MIN_CHUNK_BYTES), arenas holding one or two updates with partial uploads
 (ARENA_BYTES / ARENA_UPLOAD_EVERY), zero-copy folds of the arena on or off (ZERO_COPY_BYTES),
-small update batches per launch (BATCH), FedOpt's pinned ring for the global model (RING_BYTES) and
-the large / small split itself (SMALL_UPDATE_BYTES). Every threshold is read by staging.py at call time; the values are drawn per
+small update batches per launch (BATCH), FedOpt's pinned ring for the global model (RING_BYTES), the host pack inline or on the native
+gather's threads (layout.PACK_MIN_PARALLEL / PACK_CHUNK) and the large / small split itself
+(SMALL_UPDATE_BYTES). Every threshold is read by staging.py at call time; the values are drawn per
 seed. Bar: bit-exact values and dtypes against the oracle, every update counted."""
 import numpy as np
 import pytest
@@ -45,6 +46,12 @@ def _thresholds(seed, monkeypatch):
     # as its default argument)
     t["RING_BYTES"] = pick(4096, 6000, 64 << 20)
     monkeypatch.setattr(staging.HostStreamer.__init__, "__defaults__", (3, t["RING_BYTES"]))
+    # the host pack: inline vs the native gather's threads, and the parallel copy's piece size
+    from fedn_amd import layout
+    t["PACK_MIN_PARALLEL"] = pick(0, 1 << 20)
+    t["PACK_CHUNK"] = pick(4096, 16 << 20)
+    monkeypatch.setattr(layout, "PACK_MIN_PARALLEL", t["PACK_MIN_PARALLEL"])
+    monkeypatch.setattr(layout, "PACK_CHUNK", t["PACK_CHUNK"])
     return t
 
 
