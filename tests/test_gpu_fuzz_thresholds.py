@@ -17,7 +17,7 @@ from oracle import numpy_ref as ref
 from test_gpu_fuzz import _aggregator, _clients, _handlers, _helper, _layout, _submit_all, _values
 
 
-ROUTES = ["host", "staged", "sliced", "staged_sliced"]
+ROUTES = ["host", "staged", "npz", "sliced", "staged_sliced"]
 
 
 @pytest.fixture
