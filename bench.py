@@ -794,6 +794,9 @@ def main():
         # every rank ends the step holding the same model: int64 sum of its bits, compared over ranks
         lo_bits, hi_bits = gathered_bits(full, device, rehearsal)
         consistent = lo_bits == hi_bits
+        if tp is not None:
+            # every release grid after the peer stores covered every XCD (warm-up + timed steps)
+            extra["release_check"] = side(tp.check_release)
         for _ in range(2):
             fold_only()
         _, kern_ms = timed_steps(fold_only, a.steps, stream, world, device, rehearsal)

@@ -81,10 +81,12 @@ EXPORTS = {
     "fa_ipc_close": (ctypes.c_int, [ctypes.c_void_p]),
     "fa_copy_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "fa_push": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
-                               ctypes.c_void_p]),
+                               ctypes.c_void_p, ctypes.c_void_p]),           # ..., release_rec, stream
     "fa_fedavg_fold_push": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int64, ctypes.c_int,
-                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p]),
+                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_void_p]),  # release_rec, stream
+    "fa_device_xccs": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "fa_peer_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "fa_host_device_ptr": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "fa_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
@@ -100,8 +102,10 @@ PROBE_EXPORTS = {
     "fa_stream_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 IPC_HANDLE_BYTES = 64    # FA_IPC_HANDLE_BYTES
+RELEASE_WORDS = 8        # FA_RELEASE_WORDS; enum fa_release_word:
+FA_REL_MASK, FA_REL_ARRIVED, FA_REL_LAUNCHES, FA_REL_MISSES, FA_REL_SEEN, FA_REL_EXPECT = range(6)
 
 
 class FedAggLibraryError(ImportError):

@@ -471,17 +471,59 @@ k_fedavg_push(float* __restrict__ agg, const ClientTable<CF32::S> tab, const int
     }
 }
 
-// One system-scope release per XCD after a grid that stored into other GPUs' memory (k_fedavg_push,
-// k_push): the stores are visible to the peers before anything later on the stream (the fence the
-// ranks exchange). A release inside every wave of a large grid would write the L2 back hundreds of
-// thousands of times; workgroups are dealt round-robin over the 8 XCDs, so 64 single-wave
-// workgroups cover each XCD's L2 several times over.
-__global__ void __launch_bounds__(64) k_release() {
-    if (threadIdx.x == 0) __threadfence_system();
+// A system-scope release on every XCD after a grid that stored into other GPUs' memory
+// (k_fedavg_push, k_push): the stores still held in an XCD's L2 are written back before anything
+// later on the stream (the fence the ranks exchange). A release inside every wave of a large grid
+// would write the L2s back hundreds of thousands of times, so a separate grid of kReleaseBlocks
+// single-wave workgroups releases instead — but HIP does not promise which XCDs a grid's workgroups
+// land on, so each workgroup reads the XCD it runs on (HW_REG_XCC_ID) and ORs it into the caller's
+// release record (FA_REL_*, include/fedagg.h). The launch's last workgroup to arrive (an acq_rel
+// arrival counter: it sees every other workgroup's bit) compares the XCDs covered with the device's
+// XCD count and counts a miss; the record is read by the caller at its next synchronisation
+// (sharded.P2PAllGather.check_release), which fails the session on any miss. The mask and the
+// arrival counter are reset by that last workgroup, so the next launch on the stream starts clean.
+constexpr int kReleaseBlocks = 64;
+constexpr unsigned kXccIdReg = (3u << 11) | 20u;   // s_getreg operand: HW_REG_XCC_ID, offset 0, 4 bits
+
+__global__ void __launch_bounds__(64) k_release(unsigned* __restrict__ rec, unsigned expect) {
+    if (threadIdx.x != 0) return;
+    __threadfence_system();
+    if (rec == nullptr) return;
+    const unsigned xcc = __builtin_amdgcn_s_getreg(kXccIdReg) & 15u;
+    __hip_atomic_fetch_or(rec + FA_REL_MASK, 1u << xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned before = __hip_atomic_fetch_add(rec + FA_REL_ARRIVED, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (before + 1 != gridDim.x) return;
+    const unsigned seen = __hip_atomic_exchange(rec + FA_REL_MASK, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(rec + FA_REL_ARRIVED, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_or(rec + FA_REL_SEEN, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(rec + FA_REL_LAUNCHES, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(rec + FA_REL_EXPECT, expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((seen & expect) != expect) __hip_atomic_fetch_add(rec + FA_REL_MISSES, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-int launch_release(hipStream_t st) {
-    hipLaunchKernelGGL(k_release, dim3(64), dim3(64), 0, st);
+// XCDs of the current device (1 in a partition mode that exposes one XCD per device)
+int device_xccs(int dev, int* n) {
+    int v = 0;
+    hipError_t e = hipDeviceGetAttribute(&v, hipDeviceAttributeNumberOfXccs, dev);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(FA_EHIP, "hipDeviceGetAttribute(NumberOfXccs, %d): %s", dev, hipGetErrorString(e));
+    }
+    if (v < 1 || v > 16) return fail(FA_EHIP, "device %d reports %d XCDs", dev, v);
+    *n = v;
+    return FA_OK;
+}
+
+int launch_release(hipStream_t st, unsigned* rec) {
+    unsigned expect = 0;
+    if (rec) {
+        int dev = 0, nx = 0;
+        (void)hipGetDevice(&dev);
+        const int rc = device_xccs(dev, &nx);
+        if (rc) return rc;
+        expect = (nx >= 32) ? ~0u : ((1u << nx) - 1u);
+    }
+    hipLaunchKernelGGL(k_release, dim3(kReleaseBlocks), dim3(64), 0, st, rec, expect);
     return check_launch("release after peer stores");
 }
 
@@ -2282,7 +2324,7 @@ int fa_copy_async(void* dst, const void* src, int64_t bytes, void* stream) {
 }
 
 int fa_fedavg_fold_push(float* agg, const void* const* updates, const double* n, const double* N, int K, int64_t P,
-                        int init, void* const* dsts, int ndst, void* stream) {
+                        int init, void* const* dsts, int ndst, uint32_t* release_rec, void* stream) {
     g_err[0] = 0;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (P < 0 || K < 0 || ndst < 0 || ndst > kPushMax)
@@ -2318,10 +2360,10 @@ int fa_fedavg_fold_push(float* agg, const void* const* updates, const double* n,
         else hipLaunchKernelGGL((k_fedavg_push<4, false>), grid, dim3(kBlock), 0, st, agg, tab, cnt, P, t, ndst);
     }
     const int rc = check_launch("fa_fedavg_fold_push: kernel launch");
-    return rc ? rc : (ndst > 0 ? launch_release(st) : FA_OK);
+    return rc ? rc : (ndst > 0 ? launch_release(st, release_rec) : FA_OK);
 }
 
-int fa_push(void* const* dsts, int ndst, const void* src, int64_t bytes, void* stream) {
+int fa_push(void* const* dsts, int ndst, const void* src, int64_t bytes, uint32_t* release_rec, void* stream) {
     g_err[0] = 0;
     if (ndst < 0 || ndst > kPushMax || bytes < 0 || (bytes > 0 && (!src || (ndst > 0 && !dsts))))
         return fail(FA_EINVAL, "fa_push: bad arguments (at most %d destinations)", kPushMax);
@@ -2348,7 +2390,13 @@ int fa_push(void* const* dsts, int ndst, const void* src, int64_t bytes, void* s
                            rem);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(FA_EHIP, "fa_push: %s", hipGetErrorString(e));
-    return launch_release(st);
+    return launch_release(st, release_rec);
+}
+
+int fa_device_xccs(int dev, int* n) {
+    g_err[0] = 0;
+    if (!n) return fail(FA_EINVAL, "fa_device_xccs: null argument");
+    return device_xccs(dev, n);
 }
 
 int fa_host_device_ptr(const void* host, void** dptr) {

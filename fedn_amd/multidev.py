@@ -58,7 +58,7 @@ def gather_group(layout, bounds, devices, per_dev, dt):
     return flat.numpy()   # a new pinned block owned by the caller (see staging._Pipeline._to_host)
 
 
-def allgather_devices(parts, P, engine="dma"):
+def allgather_devices(parts, P, engine="dma", records=None):
     """The in-process form of the sliced all-gather: ``parts`` = [(device, slice
     tensor on it, lo)] covering [0, P); returns one full P-element model per device. Device d's slice
     goes straight into every other device's model over the d -> e link (after ``fa_peer_enable``),
@@ -66,7 +66,9 @@ def allgather_devices(parts, P, engine="dma"):
     destination) pair, each on its own stream; ``engine="kernel"`` with ONE ``fa_push`` launch per
     source that reads the slice once and stores it into every destination (sharded.P2PAllGather's
     two engines). Each destination's current stream then waits for what lands in it. A device listed
-    twice (tests on a one-GPU box) gets its own model buffer per entry."""
+    twice (tests on a one-GPU box) gets its own model buffer per entry. ``records``: a list that
+    receives, per kernel push, the release record its XCD-covering release grid wrote (read with
+    ``ops.read_release_record`` once the destinations have synchronised; ``misses`` must be 0)."""
     if engine not in ("dma", "kernel"):
         raise ValueError("allgather_devices: engine must be 'dma' or 'kernel'")
     parts = [(torch.device(dv), t, lo) for dv, t, lo in parts]
@@ -88,7 +90,10 @@ def allgather_devices(parts, P, engine="dma"):
         if engine == "kernel":
             st = torch.cuda.Stream(src_dev)
             st.wait_event(ready)
-            ops.push([f.data_ptr() + lo * es for f in fulls], t, t.numel() * es, st)
+            rec = ops.release_record(src_dev) if records is not None else None
+            ops.push([f.data_ptr() + lo * es for f in fulls], t, t.numel() * es, st, release_rec=rec)
+            if rec is not None:
+                records.append(rec)
             ev = torch.cuda.Event()
             ev.record(st)
             for j in range(len(parts)):

@@ -509,22 +509,24 @@ def copy_ptr_async(dst_ptr, src_ptr, nbytes, stream, device):
         _abi.check(_abi.load().fa_copy_async(int(dst_ptr), int(src_ptr), int(nbytes), ctypes_stream(stream)))
 
 
-def fedavg_fold_push(agg_ptr, ptrs, n, N, P, init, dst_ptrs, stream, device):
+def fedavg_fold_push(agg_ptr, ptrs, n, N, P, init, dst_ptrs, stream, device, release_rec=None):
     """The fp32 fold of ``P`` elements into device address ``agg_ptr`` whose kernel also stores the
     result to every address in ``dst_ptrs`` (``fa_fedavg_fold_push``: fold and all-gather push in
-    one pass); client table and destinations as device addresses, 16-B aligned."""
+    one pass); client table and destinations as device addresses, 16-B aligned. ``release_rec``: a
+    :func:`release_record` tensor on ``device`` the release grid records its XCDs in (or None)."""
     K = len(ptrs)
     if len(n) != K or len(N) != K:
         raise ValueError("n and N must have one entry per update")
     nd = len(dst_ptrs)
+    rec = _release_ptr(release_rec, device)
     with _on(device):
         _abi.check(_abi.load().fa_fedavg_fold_push(
             int(agg_ptr), (ctypes.c_void_p * max(1, K))(*ptrs), (ctypes.c_double * max(1, K))(*n),
             (ctypes.c_double * max(1, K))(*N), K, int(P), int(bool(init)),
-            (ctypes.c_void_p * max(1, nd))(*[int(p) for p in dst_ptrs]), nd, ctypes_stream(stream)))
+            (ctypes.c_void_p * max(1, nd))(*[int(p) for p in dst_ptrs]), nd, rec, ctypes_stream(stream)))
 
 
-def push(dst_ptrs, src, nbytes, stream):
+def push(dst_ptrs, src, nbytes, stream, release_rec=None):
     """``nbytes`` of device tensor ``src`` (from its start) to every device address in ``dst_ptrs``
     on ``stream`` with ONE kernel (``fa_push``): the source is read once, each destination written
     over its own link (IPC mappings of peers' buffers, or other devices' buffers in-process)."""
@@ -532,9 +534,41 @@ def push(dst_ptrs, src, nbytes, stream):
     if nbytes > src.numel() * src.element_size():
         raise ValueError("push: more bytes than the source holds")
     n = len(dst_ptrs)
+    rec = _release_ptr(release_rec, src.device)
     with _on(src.device):
         _abi.check(lib.fa_push((ctypes.c_void_p * max(1, n))(*[int(p) for p in dst_ptrs]), n, src.data_ptr(),
-                               int(nbytes), ctypes_stream(stream)))
+                               int(nbytes), rec, ctypes_stream(stream)))
+
+
+def release_record(device):
+    """A zeroed release record (include/fedagg.h FA_RELEASE_WORDS uint32 on ``device``) for the
+    release grids of :func:`push` / :func:`fedavg_fold_push` on one stream."""
+    return torch.zeros(_abi.RELEASE_WORDS, dtype=torch.int32, device=device)
+
+
+def _release_ptr(rec, device):
+    if rec is None:
+        return None
+    if (rec.dtype != torch.int32 or rec.numel() < _abi.RELEASE_WORDS or not rec.is_contiguous()
+            or rec.device != torch.device(device)):
+        raise ValueError(f"release record must be {_abi.RELEASE_WORDS} contiguous int32 on {device}")
+    return rec.data_ptr()
+
+
+def read_release_record(rec):
+    """The XCD-coverage record of the release grids (synchronises with its device): launches checked,
+    launches that missed an XCD, the XCDs seen (mask) and the device's XCD mask."""
+    v = [int(x) & 0xFFFFFFFF for x in rec.cpu().tolist()]
+    return {"launches": v[_abi.FA_REL_LAUNCHES], "misses": v[_abi.FA_REL_MISSES], "seen_mask": v[_abi.FA_REL_SEEN],
+            "expect_mask": v[_abi.FA_REL_EXPECT], "xcds_seen": bin(v[_abi.FA_REL_SEEN]).count("1")}
+
+
+def device_xccs(device):
+    """XCDs (each with its own L2) of ``device``."""
+    out = ctypes.c_int(0)
+    idx = torch.device(device).index or 0
+    _abi.check(_abi.load().fa_device_xccs(int(idx), ctypes.byref(out)))
+    return int(out.value)
 
 
 _NULL_CTX = contextlib.nullcontext()

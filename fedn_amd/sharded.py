@@ -83,10 +83,20 @@ class ShardedFedAvg:
         if self.world == 1:
             return agg_local.to("cpu")
         if gather is None:
-            if getattr(self, "_host_gather", None) is None or self._host_gather.dst != dst:
-                self._host_gather = HostGather(self.P, agg_local.dtype, self.bounds, group=self.group, dst=dst)
-            gather = self._host_gather
+            gather = self._host_gather = _cached_gather(self, agg_local.dtype, dst, self.bounds)
         return gather.gather(agg_local)
+
+
+def _cached_gather(owner, dtype, dst, bounds):
+    """``owner``'s HostGather for (dst, dtype) — made on first use, replaced (and the old one closed)
+    when a later gather asks for another destination rank or dtype. Every rank of the group makes the
+    same calls, so they replace it together."""
+    hg = getattr(owner, "_host_gather", None)
+    if hg is not None and hg.dst == dst and hg.dtype == dtype and hg.P == owner.P:
+        return hg
+    if hg is not None:
+        hg.close()
+    return HostGather(owner.P, dtype, bounds, group=owner.group, dst=dst)
 
 
 class ShardedFedOpt:
@@ -188,9 +198,7 @@ class CyclicShardedFedAvg:
         collective: every rank D2H's its chunks straight into the node's shared host model
         (:class:`HostGather`, kept for later rounds) — FEDn's consumer (roundhandler.py:465-468)."""
         if gather is None:
-            if getattr(self, "_host_gather", None) is None or self._host_gather.dst != dst:
-                self._host_gather = HostGather(self.P, agg_local.dtype, None, group=self.group, dst=dst)
-            gather = self._host_gather
+            gather = self._host_gather = _cached_gather(self, agg_local.dtype, dst, None)
         return gather.gather(agg_local, self.owned())
 
     def round_folder(self, agg_local, updates_local, n, N, init, stream=None):
@@ -221,12 +229,12 @@ class CyclicShardedFedAvg:
             self.fold_fn(agg_local[sl], [u[sl] for u in updates_local], n, N, init)
         return fold
 
-    def _fusable(self, updates_local, out):
-        """The fused fold + push applies: the default kernel, fp32 updates and model on one device,
-        contiguous buffers of the geometry's sizes."""
+    def _fusable(self, agg_local, updates_local, out):
+        """The fused fold + push applies: the default kernel, fp32 updates, aggregate and model on
+        one device, contiguous buffers of the geometry's sizes."""
         return bool(self._kernel and out.dtype == torch.float32 and out.is_cuda and updates_local
-                    and all(u.dtype == torch.float32 and u.device == out.device and u.is_contiguous()
-                            and u.numel() >= self.local_len for u in updates_local)
+                    and all(t.dtype == torch.float32 and t.device == out.device and t.is_contiguous()
+                            and t.numel() >= self.local_len for t in [agg_local, *updates_local])
                     and out.numel() >= self.full_len)
 
     def fold_allgather(self, agg_local, updates_local, n, N, init, out=None, p2p=None):
@@ -247,13 +255,17 @@ class CyclicShardedFedAvg:
             cur = torch.cuda.current_stream(dev)
             p2p.begin()
             out = p2p.full
-            if p2p.engine == "fused" and self._fusable(updates_local, out):
+            if p2p.engine == "fused" and self._fusable(agg_local, updates_local, out):
                 from . import ops
                 bases = [u.data_ptr() for u in updates_local]
                 for i in range(self.rounds):
                     at = (i * W + self.rank) * C
-                    ops.fedavg_fold_push(out.data_ptr() + at * 4, [b + i * C * 4 for b in bases], n, N, C, init,
-                                         p2p.peer_ptrs(at), cur, dev)
+                    # the running aggregate is agg_local (read back when init is False, and what a later
+                    # gather_to_host(agg_local) copies); this rank's copy in ``out`` is one more store
+                    # destination beside the peers'
+                    ops.fedavg_fold_push(agg_local.data_ptr() + i * C * 4, [b + i * C * 4 for b in bases], n, N, C,
+                                         init, p2p.peer_ptrs(at) + [out.data_ptr() + at * 4], cur, dev,
+                                         release_rec=p2p.release_rec(cur))
                 p2p.fence()
                 return out[:self.P]
             fold = self.round_folder(agg_local, updates_local, n, N, init, cur)
@@ -372,6 +384,39 @@ class P2PAllGather:
         self.push_stream = torch.cuda.Stream(self.device)       # the "kernel" engine's launches
         self.nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
         self._flag = torch.zeros(1, dtype=torch.float32, device=self.device) if self.nccl else None
+        self._release = {}                          # stream handle -> its release record (kernel engines)
+
+    def release_rec(self, stream):
+        """The release record of ``stream`` (one per stream: a record's reset is ordered by the stream)
+        that the kernel engines' release grids fill with the XCDs they ran on (fa_push /
+        fa_fedavg_fold_push, include/fedagg.h); :meth:`check_release` reads them."""
+        key = stream.cuda_stream
+        rec = self._release.get(key)
+        if rec is None:
+            from . import ops
+            rec = self._release[key] = ops.release_record(self.device)
+        return rec
+
+    def check_release(self):
+        """Synchronise and verify that every release grid of the peer-storing kernels so far covered
+        every XCD of the device (each XCD's L2 written back at system scope before the fence).
+        Returns the summed record; raises FedAggError on any launch that missed an XCD — the peers
+        may then have read stale bytes, so the exchange is not trusted."""
+        from . import _abi, ops
+        tot = {"launches": 0, "misses": 0, "seen_mask": 0, "expect_mask": 0}
+        for rec in self._release.values():
+            r = ops.read_release_record(rec)
+            tot["launches"] += r["launches"]
+            tot["misses"] += r["misses"]
+            tot["seen_mask"] |= r["seen_mask"]
+            tot["expect_mask"] |= r["expect_mask"]
+        tot["xcds_seen"] = bin(tot["seen_mask"]).count("1")
+        tot["xcds"] = ops.device_xccs(self.device)
+        if tot["misses"]:
+            raise _abi.FedAggError(_abi.FA_EHIP, f"P2PAllGather: {tot['misses']} of {tot['launches']} release grids "
+                                                 f"did not cover every XCD (seen {tot['seen_mask']:#x}, device "
+                                                 f"{tot['expect_mask']:#x}): peer stores may not have been visible")
+        return tot
 
     @property
     def full(self):
@@ -402,7 +447,7 @@ class P2PAllGather:
                 dsts.append(self.full.data_ptr() + at * self.esize)
             if dsts:
                 self.push_stream.wait_event(after)
-                ops.push(dsts, src, nbytes, self.push_stream)
+                ops.push(dsts, src, nbytes, self.push_stream, release_rec=self.release_rec(self.push_stream))
             return local
         for r, st in self.streams.items():
             st.wait_event(after)
@@ -428,17 +473,25 @@ class P2PAllGather:
             dist.barrier(group=self.group)
 
     def close(self, fence=True):
-        """Unmap the peers' buffers (after a fence: no copy into them is in flight)."""
+        """Unmap the peers' buffers (after a fence: no copy into them is in flight). The release
+        records are checked first (:meth:`check_release`; raised after the unmapping)."""
         from . import ops
+        err = None
         if fence and self.peers:
             self.fence()
             torch.cuda.synchronize(self.device)
+            try:
+                self.check_release()
+            except Exception as e:  # noqa: BLE001 — raised once the peers are unmapped
+                err = e
         for r, maps in list(self.peers.items()):
             for base, _ in maps:
                 ops.ipc_close(base, self.device)
         self.peers = {}
         if fence and self.world > 1 and dist.is_initialized():
             dist.barrier(group=self.group)       # no peer unmaps while another still copies
+        if err is not None:
+            raise err
 
 
 class HostGather:
@@ -500,12 +553,19 @@ class HostGather:
     def gather(self, local, pieces=None):
         """``local``: this rank's part of the model (device or CPU tensor). ``pieces``: where it goes,
         as (global_lo, global_hi, local_lo) triples; default: this rank's contiguous slice of
-        ``bounds`` from local[0]. Returns the host model (a shared-memory tensor, valid until the
-        next gather) on rank ``dst``, None elsewhere."""
+        ``bounds`` from local[0]. Returns the host model (a shared-memory tensor, valid until rank
+        ``dst``'s next gather: every gather starts with a barrier) on rank ``dst``, None elsewhere.
+        ``local`` must have the host model's dtype."""
         from . import ops
+        if local.dtype != self.dtype:
+            raise TypeError(f"HostGather.gather: a {local.dtype} slice into a {self.dtype} host model")
         if pieces is None:
             lo, hi = self.bounds[self.rank]
             pieces = [(lo, hi, 0)] if hi > lo else []
+        if self.world > 1:
+            # the previous result stays valid until rank dst enters the next gather: no rank writes
+            # into the shared model before then
+            dist.barrier(group=self.group)
         es = self.host.element_size()
         if local.device.type == "cuda" and pieces:
             self._pin(local.device)

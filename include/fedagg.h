@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 6
+#define FA_ABI_VERSION 7
 
 /* element type codes */
 enum fa_dtype {
@@ -268,6 +268,18 @@ int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, co
  *                    also stores every finished element to each of ndst (<= 16) destinations: the
  *                    fold and the all-gather push in ONE pass (sharded.P2PAllGather engine "fused";
  *                    the peers' buffers IPC-mapped or in-process). agg is this rank's own copy.
+ *   release_rec      (fa_push, fa_fedavg_fold_push; ABI 7) after a grid that stored into peers, a
+ *                    release grid writes every XCD's L2 back at system scope. HIP does not promise
+ *                    which XCDs a grid's workgroups run on, so each release workgroup records its
+ *                    XCD (HW_REG_XCC_ID) in release_rec: FA_RELEASE_WORDS uint32 of caller-owned
+ *                    DEVICE memory, zeroed once before the first call and then passed to every call
+ *                    on one stream. Per release launch, the last workgroup compares the XCDs covered
+ *                    with the device's XCD count and increments FA_REL_MISSES on a gap; FA_REL_LAUNCHES
+ *                    counts the launches checked, FA_REL_SEEN is the union of the XCDs seen and
+ *                    FA_REL_EXPECT the mask of the device's XCDs. The caller reads the record at a
+ *                    synchronisation point and must treat MISSES > 0 as a failed exchange. NULL:
+ *                    release without the record (in-process peers behind a device synchronize).
+ * fa_device_xccs     *n = the number of XCDs (each with its own L2) of device dev
  * fa_peer_enable     let device dev read / write device peer's memory directly (in-process);
  *                    already enabled is not an error
  * fa_host_register   page-lock host memory the caller mapped (the node's shared host model that
@@ -279,13 +291,17 @@ int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, co
  *                    (staging.FedAvgPipeline.result); an error for pageable memory
  */
 #define FA_IPC_HANDLE_BYTES 64
+#define FA_RELEASE_WORDS 8
+enum fa_release_word { FA_REL_MASK = 0, FA_REL_ARRIVED = 1, FA_REL_LAUNCHES = 2, FA_REL_MISSES = 3, FA_REL_SEEN = 4,
+                       FA_REL_EXPECT = 5 };
 int fa_ipc_get_handle(const void* dptr, void* handle, uint64_t* offset);
 int fa_ipc_open(const void* handle, uint64_t offset, void** base, void** dptr);
 int fa_ipc_close(void* base);
 int fa_copy_async(void* dst, const void* src, int64_t bytes, void* stream);
-int fa_push(void* const* dsts, int ndst, const void* src, int64_t bytes, void* stream);
+int fa_push(void* const* dsts, int ndst, const void* src, int64_t bytes, uint32_t* release_rec, void* stream);
 int fa_fedavg_fold_push(float* agg, const void* const* updates, const double* n, const double* N, int K, int64_t P,
-                        int init, void* const* dsts, int ndst, void* stream);
+                        int init, void* const* dsts, int ndst, uint32_t* release_rec, void* stream);
+int fa_device_xccs(int dev, int* n);
 int fa_peer_enable(int dev, int peer);
 int fa_host_register(void* p, int64_t bytes);
 int fa_host_unregister(void* p);

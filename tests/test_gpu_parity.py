@@ -1408,10 +1408,35 @@ def _p2p_gloo_worker(rank, world, port, P, K, chunk, q, double=False, engine="dm
             out = cs.fold_allgather(aggc, loc, ns, Ns, init=True, p2p=p2p)
             torch.cuda.synchronize()
             outs.append(out.cpu().numpy().copy())
+        # a continuation (init=False) folds onto the running aggregate agg_local, and agg_local holds
+        # this rank's folded chunks afterwards (gather_to_host copies it), whatever the engine
+        out = cs.fold_allgather(aggc, loc, ns, [x + Ns[-1] for x in Ns], init=False, p2p=p2p)
+        torch.cuda.synchronize()
+        outs.append(out.cpu().numpy().copy())
+        host = cs.gather_to_host(aggc)
+        outs.append(None if host is None else host.numpy().copy())
+        rel = p2p.check_release()
         p2p.close()
-        q.put((rank, outs))
+        q.put((rank, outs, rel))
     finally:
         dist.destroy_process_group()
+
+
+def _check_p2p_results(res, want, want2, want3, engine=None):
+    """Steps 0-3 (init, other updates from step 2), the continuation step (init=False, step 4) and
+    rank 0's host model gathered from agg_local (step 5); the release grids covered every XCD."""
+    want, want2, want3 = (w.cpu().numpy() for w in (want, want2, want3))
+    for rank, outs, rel in res:
+        for step, got in enumerate(outs[:5]):
+            w = want3 if step == 4 else (want2 if step >= 2 else want)
+            assert np.array_equal(got.view(np.uint32), w.view(np.uint32)), f"rank {rank} step {step}"
+        if rank == 0:
+            assert np.array_equal(outs[5].view(np.uint32), want3.view(np.uint32)), "gather_to_host(agg_local)"
+        else:
+            assert outs[5] is None
+        assert rel["misses"] == 0
+        if engine in ("kernel", "fused"):
+            assert rel["launches"] > 0 and rel["misses"] == 0 and rel["seen_mask"] == rel["expect_mask"]
 
 
 def test_p2p_allgather_fused_engine_bf16_falls_back():
@@ -1443,11 +1468,9 @@ def test_p2p_allgather_fused_engine_bf16_falls_back():
     ops.fedavg_fold(want, ups, ns, Ns, init=True)
     want2 = torch.empty(P, device=DEV)
     ops.fedavg_fold(want2, [u.add(1.0).to(torch.bfloat16) for u in ups], ns, Ns, init=True)
-    want, want2 = want.cpu().numpy(), want2.cpu().numpy()
-    for rank, outs in res:
-        for step, got in enumerate(outs):
-            w = want2 if step >= 2 else want
-            assert np.array_equal(got.view(np.uint32), w.view(np.uint32)), f"rank {rank} step {step}"
+    want3 = want2.clone()
+    ops.fedavg_fold(want3, [u.add(1.0).to(torch.bfloat16) for u in ups], ns, [x + Ns[-1] for x in Ns], init=False)
+    _check_p2p_results(res, want, want2, want3)
 
 
 @pytest.mark.parametrize("engine", ["dma", "kernel", "fused"])
@@ -1485,11 +1508,9 @@ def test_p2p_allgather_gloo_hip(world, P, chunk, double, engine):
     ops.fedavg_fold(want, ups, ns, Ns, init=True)
     want2 = torch.empty(P, device=DEV)
     ops.fedavg_fold(want2, [u.add(1.0) for u in ups], ns, Ns, init=True)
-    want, want2 = want.cpu().numpy(), want2.cpu().numpy()
-    for rank, outs in res:
-        for step, got in enumerate(outs):
-            w = want2 if step >= 2 else want
-            assert np.array_equal(got.view(np.uint32), w.view(np.uint32)), f"rank {rank} step {step}"
+    want3 = want2.clone()
+    ops.fedavg_fold(want3, [u.add(1.0) for u in ups], ns, [x + Ns[-1] for x in Ns], init=False)
+    _check_p2p_results(res, want, want2, want3, engine)
 
 
 @pytest.mark.parametrize("K", [1, 3, 9, 64, 70])
