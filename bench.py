@@ -97,6 +97,16 @@ def parse():
     return ap.parse_args()
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """A progress line on stderr (rank 0; stdout carries only the JSON line): a long multi-rank run
+    shows where it is."""
+    if os.environ.get("RANK", "0") == "0":
+        print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def make_updates(K, P, dtype, device, seed):
     """Synthetic client updates: base ~ N(0,1), client k = base + 0.01 N(0,1)."""
     g = torch.Generator(device=device).manual_seed(seed)
@@ -741,6 +751,7 @@ def main():
             sums = {}
             for name in transports:
                 tp = use(name)
+                progress(f"warm-up: transport {name}, rounds {list(geoms)}")
                 for R, c in geoms.items():
                     res = [None]
                     st = make_step(c, tp, [u[:c.local_len] for u in scratch], res)
@@ -776,6 +787,7 @@ def main():
         P = L
         # the timed data: this rank's chunks of ONE seeded global model (the N = 1 line's), so that
         # rank 0 checks the gathered model bit-for-bit against the oracle
+        progress(f"chose {tname} R={R}; generating this rank's chunks of the global model")
         ups_local, host_sample = global_chunks(cyc, K, P_total, a.dtype, device, a.seed, S if rank == 0 else 0)
         agg = agg_all[:L]
         res = [None]
@@ -787,6 +799,7 @@ def main():
             for i in range(cyc.rounds):
                 fold_round(i)
 
+        progress("timed steps")
         for _ in range(a.warmup):
             step()
         elapsed, _ = timed_steps(step, a.steps, stream, world, device, rehearsal)
@@ -823,6 +836,7 @@ def main():
         extra["fold_allgather_ms"] = elapsed / a.steps * 1e3
         extra["allgather_consistent_over_ranks"] = consistent
         if rank == 0 and S:
+            progress("oracle check of the gathered model's sample")
             exact, dt = sample_check(full, host_sample, ns)
             base = {"value": K * S / dt, "unit": "params/s", "cores": 1, "kind": "port",
                     "sample": f"{K} clients x {S} fp32 params (the first {S} of the global model's clients); numpy "
@@ -942,7 +956,9 @@ def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, u
         return res
 
     def weak():
-        P = P_total
+        # a rehearsal puts every rank on one GPU: each folds a 1/world slice there, so the ranks'
+        # updates together take the N = 1 line's HBM, not world times it
+        P = -(-P_total // world) if rehearsal else P_total
         ups = make_updates(K, P, a.dtype, device, a.seed + 7 + 1000 * rank)
         agg_w = torch.empty(P, dtype=torch.float32, device=device)
         step = lambda: ops.fedavg_fold(agg_w, ups, ns, Ns, init=True, stream=stream)  # noqa: E731
@@ -953,7 +969,8 @@ def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, u
         torch.cuda.empty_cache()
         return {"value": K * P * world / (el / a.steps), "ms_per_step": el / a.steps * 1e3, "kernel_ms": kms,
                 "params_per_gpu": P, "global_params": P * world,
-                "note": f"every rank folds its own {P}-param slice of a world x {P} model; no collective; not in value"}
+                "note": f"every rank folds its own {P}-param slice of a world x {P} model; no collective; not in value"
+                        + ("; REHEARSAL: all ranks on one GPU, each folding a 1/world slice" if rehearsal else "")}
 
     def in_process():
         """One process (rank 0) drives all N GPUs: each folds its slice of the 64 updates and copies it
@@ -992,6 +1009,7 @@ def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, u
             torch.cuda.empty_cache()
         return res
 
+    progress("side: allgather, gather_to_host, weak_scaling")
     out["allgather"] = side(plain_allgather)
     out["gather_to_host"] = side(gather_to_host)
     out["weak_scaling"] = side(weak)
@@ -1041,8 +1059,10 @@ def multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, u
                         "fp64 model slice's D2H is timed apart; not in value"}
 
     if a.fedopt_params > 0:
+        progress("side: fedopt_sharded")
         out["fedopt_sharded"] = side(fedopt_sharded)
     devs = [torch.device("cuda", 0 if rehearsal else d) for d in range(world)]
+    progress("side (rank 0): in_process, host_resident, fedopt_waves")
     ip = side(in_process) if rank == 0 else None     # the other ranks wait (their GPUs are in use)
     hr = (side(lambda: host_resident_side(a, devs, ns, clients=a.host_clients))
           if rank == 0 and a.host_clients > 0 else None)

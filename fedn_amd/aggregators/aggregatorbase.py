@@ -82,7 +82,7 @@ def requeue_front(q, items):
 
 
 def queued_updates(update_handler, helper, ahead=None, ahead_bytes=None, size_box=None):
-    """The aggregators' drain of ``update_handler.model_updates`` (fedavg.py:109-112,
+    """The aggregators' drain of ``update_handler.model_updates`` (fedavg.py:47-50,
     fedopt.py:76-80): yields ``(model_update, load)`` in FIFO order until the queue is empty,
     where ``load()`` returns ``update_handler.load_model_update(model_update, helper)`` or
     raises its error (``model_update`` is None if dequeuing itself raised). The caller folds

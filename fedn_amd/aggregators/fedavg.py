@@ -1,12 +1,12 @@
 """FedAvg aggregator plug-in — drop-in for fedn/network/combiner/aggregators/fedavg.py.
 
 Same contract and observable behaviour as fedavg.py:8-83:
-  * drains ``update_handler.model_updates`` in FIFO order (fedavg.py:109-112);
-  * ``total_examples`` grows BEFORE the fold (fedavg.py:124), so an update whose fold
+  * drains ``update_handler.model_updates`` in FIFO order (fedavg.py:47-50);
+  * ``total_examples`` grows BEFORE the fold (fedavg.py:62), so an update whose fold
     fails is skipped but still counted; a load failure is skipped uncounted;
-  * the first update is the model (fedavg.py:127-128): K = 1 returns it unchanged;
+  * the first update is the model (fedavg.py:65-66): K = 1 returns it unchanged;
   * returns ``(model, data)`` with ``time_model_load``, ``time_model_aggregation``,
-    ``nr_aggregated_models`` (fedavg.py:99-101, 142), ``(None, data)`` if nothing folded.
+    ``nr_aggregated_models`` (fedavg.py:37-39, 80), ``(None, data)`` if nothing folded.
 The fold ``x + (n*(y-x))/N`` (numpyhelper.py:32; binaryhelper inherits it) runs in libfedagg
 on the GPU, bit-exact; a session on androidhelper folds with ITS rule instead,
 ``(1 - w)*x + w*y`` on one flat array (androidhelper.py:21-39, staging.AndroidFedAvgPipeline);
@@ -105,7 +105,7 @@ class Aggregator(AggregatorBase):
                     nr_aggregated_models += 1
                     if delete_models:
                         self.update_handler.delete_model(model_update)
-                except Exception as e:  # noqa: BLE001 — fedavg.py:137-140: log and continue
+                except Exception as e:  # noqa: BLE001 — fedavg.py:75-78: log and continue
                     logger.error(f"AGGREGATOR({self.name}): Error encoutered while processing model update: {e}")
                     logger.error(traceback.format_exc())
 

@@ -1,7 +1,7 @@
 // fedagg.hip — gfx950 (MI355X) kernels + C ABI for FEDn's combiner-side aggregation.
 //
 // The hot path is an elementwise, HBM-bound recurrence over K client buffers:
-//   FedAvg  (numpyhelper.py:32, fedavg.py:109-133):   x <- x + (n_k*(y_k - x))/N_k
+//   FedAvg  (numpyhelper.py:32, fedavg.py:47-71):   x <- x + (n_k*(y_k - x))/N_k
 //   FedOpt  (fedopt.py:74-118):  pg <- running mean of (y_k - old), then one
 //           Adam/Yogi/AdaGrad server step (fedopt.py:151-258) over (old, m, v).
 // Every output element depends only on the same element of the inputs, and the
@@ -338,7 +338,7 @@ struct ClientTable {
 };
 
 // Start one strip's running value. INIT: x := updates[0] (the `model = model_next`
-// alias, fedavg.py:127-128); else x := agg (continuing a chunked / streamed fold).
+// alias, fedavg.py:65-66); else x := agg (continuing a chunked / streamed fold).
 // INT_FIRST: integer updates; the first fold runs in integer arithmetic (numpy int
 // subtract + multiply wrap), then true_divide to f64 (numpyhelper.py:32 on int arrays).
 // Returns the first client index still to fold.

@@ -4,7 +4,7 @@ ARRIVE, not when the round aggregates.
 In FEDn an update reaches the combiner through ``ModelService.Upload`` (modelservice.py:
 198-221) and ``UpdateHandler.on_model_update`` (updatehandler.py:46-70), which only
 validates and enqueues it; decoding (npz inflate, updatehandler.py:90-117) and all
-arithmetic happen later, serially, inside ``combine_models`` (fedavg.py:118, 130). Here
+arithmetic happen later, serially, inside ``combine_models`` (fedavg.py:56, 68). Here
 :class:`StagingUpdateHandler` wraps the combiner's UpdateHandler: ``on_model_update``
 enqueues the update in arrival order exactly as before AND hands it to a worker pool
 that decodes it (the wrapped handler's own ``load_model_update`` with the round's
@@ -34,7 +34,7 @@ class StagedModel:
     """One decoded client update resident in HBM: flat grouped layout (layout.py) in
     ``dev`` (uint8), ready once ``ready`` (an event on the staging stream) has fired.
     ``host`` returns the update as host arrays (needed only when it is the round's sole
-    update, fedavg.py:127-128): the decoded arrays if they were kept, else a D2H copy."""
+    update, fedavg.py:65-66): the decoded arrays if they were kept, else a D2H copy."""
 
     __slots__ = ("layout", "dev", "ready", "_host", "__weakref__")
 

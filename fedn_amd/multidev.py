@@ -331,7 +331,7 @@ class ShardedFedAvgPipeline(_ShardedStaging):
         ns = [e[1] for e in entries]
         Ns = [e[2] for e in entries]
         acc = self._agg(d, dt)[clo:chi]
-        if init:                                # agg := first update, then fold (fedavg.py:127-133)
+        if init:                                # agg := first update, then fold (fedavg.py:65-71)
             x0 = self._view(d, self.first, dt)[clo:chi]
             ops.fedavg_fold(acc, [x0] + ys, [0.0] + ns, [1.0] + Ns, init=True, stream=self.compute[d])
         else:
@@ -359,7 +359,7 @@ class ShardedFedAvgPipeline(_ShardedStaging):
 
     def result(self):
         if self.nfolds == 0:
-            return _host_arrays(self.first_arrays)     # `model = model_next` alias (fedavg.py:127-128)
+            return _host_arrays(self.first_arrays)     # `model = model_next` alias (fedavg.py:65-66)
         if self.general is not None:
             return self.general.result()
         entries, self.pending = self.pending, []

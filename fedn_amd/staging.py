@@ -522,7 +522,7 @@ class _Pipeline:
 
 
 class FedAvgPipeline(_Pipeline):
-    """Streaming FedAvg on one device: fedavg.py:109-133 with the fold on the GPU."""
+    """Streaming FedAvg on one device: fedavg.py:47-71 with the fold on the GPU."""
 
     def __init__(self, device, first_arrays, nslots=3, slots=None, streams=None, cache=None, batch=True):
         staged = isinstance(first_arrays, StagedModel)
@@ -670,7 +670,7 @@ class FedAvgPipeline(_Pipeline):
         Ns = [e[2] for e in entries]
         acc = self._agg(dt)[lo:hi]
         upd_dt = ops.torch_dtype(dt)
-        if init:                                # agg := first update, then fold (fedavg.py:127-133)
+        if init:                                # agg := first update, then fold (fedavg.py:65-71)
             ops.fedavg_fold_ptrs(acc, [_addr(self.first) + off] + ptrs, upd_dt, [0.0] + ns, [1.0] + Ns,
                                  init=True, stream=self.compute)
         else:
@@ -706,10 +706,10 @@ class FedAvgPipeline(_Pipeline):
             self._fold_all(entries)
 
     def result(self):
-        """The aggregated model as a new host ``list[np.ndarray]`` (fedavg.py:145). A pending
+        """The aggregated model as a new host ``list[np.ndarray]`` (fedavg.py:83). A pending
         batch is folded here, chunk by chunk, each chunk's D2H overlapping the next fold."""
         if self.nfolds == 0:
-            first = self.first_arrays           # `model = model_next` alias (fedavg.py:127-128)
+            first = self.first_arrays           # `model = model_next` alias (fedavg.py:65-66)
             return first.host if isinstance(first, StagedModel) else first
         if self.general is not None:
             return self.general.result()
@@ -848,7 +848,7 @@ class AndroidFedAvgPipeline(_Pipeline):
 
     def result(self):
         if self.nfolds == 0:
-            return self.first_arrays            # `model = model_next` alias (fedavg.py:127-128)
+            return self.first_arrays            # `model = model_next` alias (fedavg.py:65-66)
         return self._to_host(self.g).numpy()
 
 

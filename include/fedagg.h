@@ -13,7 +13,7 @@
  *   fa_fedavg_fold   numpyhelper.Helper.increment_average
  *                    fedn/utils/helpers/plugins/numpyhelper.py:18-32, applied in
  *                    queue order by fedavg.Aggregator.combine_models
- *                    fedn/network/combiner/aggregators/fedavg.py:109-133, and by
+ *                    fedn/network/combiner/aggregators/fedavg.py:47-71, and by
  *                    Control.reduce fedn/network/controller/control.py:678-682
  *   fa_fedopt_step   the pseudo-gradient loop + server optimizer of
  *                    fedopt.Aggregator.combine_models
@@ -84,8 +84,8 @@ const char* fa_last_error(void);
  * agg      device buffer, P elements of agg_dtype (the running model)
  * updates  HOST array of K DEVICE pointers, each P elements of upd_dtype
  * n, N     HOST arrays of K doubles: num_examples of update k and the running
- *          total including it (fedavg.py:124), exact integers
- * init     1: agg := updates[0] (the `model = model_next` alias, fedavg.py:127-128),
+ *          total including it (fedavg.py:62), exact integers
+ * init     1: agg := updates[0] (the `model = model_next` alias, fedavg.py:65-66),
  *             then fold k = 1..K-1;  0: fold k = 0..K-1 into the existing agg
  * stream   hipStream_t (NULL = default stream)
  *

@@ -96,10 +96,10 @@ def android_increment_average(model, model_next, num_examples, total_examples):
 def fedavg_combine(updates, increment=None):
     """Fold ``updates`` = [(arrays, num_examples), ...] in FIFO order.
 
-    Returns (model or None, nr_aggregated_models). Mirrors fedavg.py:109-140: the
-    running total is incremented BEFORE the fold (fedavg.py:124), the first update
-    is aliased (fedavg.py:127-128), and a fold that raises is skipped while its
-    examples stay counted (fedavg.py:137-140).
+    Returns (model or None, nr_aggregated_models). Mirrors fedavg.py:47-78: the
+    running total is incremented BEFORE the fold (fedavg.py:62), the first update
+    is aliased (fedavg.py:65-66), and a fold that raises is skipped while its
+    examples stay counted (fedavg.py:75-78).
     """
     increment = increment or increment_average      # the session helper's rule (fedavg.py:68)
     model, nr, total = None, 0, 0

@@ -1,6 +1,6 @@
 """the kernel path never kills the round. A libfedagg call that fails (nonzero
 status -> FedAggError) is handled by the plug-ins exactly as FEDn handles an update whose fold
-raises: the update is logged and skipped with its examples still counted (fedavg.py:137-140,
+raises: the update is logged and skipped with its examples still counted (fedavg.py:75-78,
 fedopt.py:103-106), and a server step that raises gives ``(None, data)`` (fedopt.py:111-116).
 Failures are injected at the C-ABI wrapper (fedn_amd.ops) before anything is enqueued, which
 is where a real status code surfaces; every result is checked against the oracle."""

@@ -3,7 +3,7 @@ mid-size CNN), host-resident numpy updates through the real combine_models call 
 FEDn deployments run in, where FEDn's numpy loop is already fast and the GPU path must not add
 latency. Beside it, two CPU columns on one host core: the numpy restatement's arithmetic alone
 (oracle/, bit-equal to FEDn: ``round_ms_numpy_oracle_1core``), and the same arithmetic inside
-FEDn's own combine_models loop restated (fedavg.py:46-80, fedopt.py:107-139: queue, load,
+FEDn's own combine_models loop restated (fedavg.py:45-83, fedopt.py:74-121: queue, load,
 bookkeeping and per-update log calls) over the same in-memory update handler as the plug-in
 (``round_ms_numpy_fedn_loop``) — what the reference aggregator itself takes for the round. Every GPU
 round is checked bit-identical to the oracle.
@@ -44,7 +44,7 @@ def same(a, b):
 
 
 def fedn_loop_fedavg(uh, helper=None, delete_models=True):
-    """fedavg.py:46-80 restated with the oracle's arithmetic (the reference's per-update log calls
+    """fedavg.py:45-83 restated with the oracle's arithmetic (the reference's per-update log calls
     included: their messages are formatted whatever the level)."""
     log = ref_logger
     name = "fedavg"
