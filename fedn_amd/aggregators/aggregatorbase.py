@@ -222,6 +222,35 @@ class AggregatorBase(ABC):
     def combine_models(self, helper=None, delete_models=True, parameters=None):
         """Drain the update queue and return ``(model, data)``."""
 
+    def _settle(self, pipe, waiting, delete_models):
+        """Bookkeeping of updates whose fold is deferred to a batched launch. ``waiting``: the admitted
+        updates (``ModelUpdate`` tags, FIFO) not yet deleted from storage. An update the pipeline
+        skipped — its batch's launch failed and its own one-at-a-time fold failed too — is logged as
+        FEDn logs a fold that raises (fedavg.py:75-78, fedopt.py:103-106), is not counted, and stays in
+        storage (FEDn deletes only after a successful fold, fedavg.py:71-74); the others are deleted
+        once folded (the pipeline's ``unsettled()`` newest ones still wait). Returns how many were
+        skipped."""
+        import traceback
+        skipped = pipe.take_skipped() if hasattr(pipe, "take_skipped") else []
+        for tag, exc in skipped:
+            self._log_skip(exc, "".join(traceback.format_exception(type(exc), exc, exc.__traceback__)))
+            for i, mu in enumerate(waiting):
+                if mu is tag:
+                    del waiting[i]
+                    break
+        keep = pipe.unsettled() if hasattr(pipe, "unsettled") else 0
+        while len(waiting) > keep:
+            mu = waiting.popleft()
+            if delete_models:
+                self.update_handler.delete_model(mu)
+        return len(skipped)
+
+    def _log_skip(self, exc, tb):
+        import logging
+        log = logging.getLogger("fedn")
+        log.error(f"AGGREGATOR({self.name}): Error encoutered while processing model update: {exc}")
+        log.error(tb)
+
 
 def get_aggregator(aggregator_module_name, update_handler):
     """aggregatorbase.py:44-62."""

@@ -18,6 +18,7 @@ import logging
 import os
 import time
 import traceback
+from collections import deque
 
 import torch
 
@@ -84,6 +85,7 @@ class Aggregator(AggregatorBase):
         nr_aggregated_models = 0
         total_examples = 0
         pipe = None
+        waiting = deque()       # admitted updates not deleted yet: a batched fold may still skip them
 
         logger.info("AGGREGATOR({}): Aggregating model updates... ".format(self.name))
         with contextlib.closing(queued_updates(self.update_handler, helper, size_box=self._ahead_size)) as updates:
@@ -99,23 +101,26 @@ class Aggregator(AggregatorBase):
                     if nr_aggregated_models == 0:
                         pipe = make_fedavg_pipeline(model_next, self.device, self.devices, helper, self._staging)
                     else:
-                        pipe.add(model_next, metadata["num_examples"], total_examples)
+                        pipe.add(model_next, metadata["num_examples"], total_examples, tag=model_update)
                     data["time_model_aggregation"] += time.time() - tic
 
                     nr_aggregated_models += 1
-                    if delete_models:
-                        self.update_handler.delete_model(model_update)
+                    waiting.append(model_update)
+                    # updates of a batch whose launch failed were refolded one at a time: the ones
+                    # whose own fold failed are skipped (fedavg.py:75-78); the folded ones deleted
+                    nr_aggregated_models -= self._settle(pipe, waiting, delete_models)
                 except Exception as e:  # noqa: BLE001 — fedavg.py:75-78: log and continue
                     logger.error(f"AGGREGATOR({self.name}): Error encoutered while processing model update: {e}")
                     logger.error(traceback.format_exc())
 
-        data["nr_aggregated_models"] = nr_aggregated_models
         if pipe is not None:
             tic = time.time()
             model = pipe.result()
             data["time_model_aggregation"] += time.time() - tic
+            nr_aggregated_models -= self._settle(pipe, waiting, delete_models)
             data.update(pipe.timings())
             if hasattr(pipe, "release"):
                 pipe.release()
+        data["nr_aggregated_models"] = nr_aggregated_models
         logger.info("AGGREGATOR({}): Aggregation completed, aggregated {} models.".format(self.name, nr_aggregated_models))
         return model, data

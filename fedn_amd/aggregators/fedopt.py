@@ -17,6 +17,7 @@ import contextlib
 import logging
 import time
 import traceback
+from collections import deque
 
 from ..exceptions import InvalidParameterError
 from ..parameters import Parameters
@@ -89,6 +90,7 @@ class Aggregator(AggregatorBase):
 
         pipe = None
         nr_aggregated_models, total_examples = 0, 0
+        waiting = deque()       # admitted updates not deleted yet: a batched fold may still skip them
         with contextlib.closing(queued_updates(self.update_handler, helper, size_box=self._ahead_size)) as updates:
             for model_update, load in updates:
                 try:
@@ -105,12 +107,14 @@ class Aggregator(AggregatorBase):
                     if nr_aggregated_models == 0:
                         model_old = self.update_handler.load_model(helper, model_update.model_id)
                         pipe = self._pipeline(model_old, model_next)
-                    pipe.add(model_next, metadata["num_examples"], total_examples)
+                    pipe.add(model_next, metadata["num_examples"], total_examples, tag=model_update)
                     data["time_model_aggregation"] += time.time() - tic
 
                     nr_aggregated_models += 1
-                    if delete_models:
-                        self.update_handler.delete_model(model_update)
+                    waiting.append(model_update)
+                    # a batch whose launch failed was folded one update at a time: skipped ones are
+                    # logged and uncounted (fedopt.py:103-106), folded ones deleted
+                    nr_aggregated_models -= self._settle(pipe, waiting, delete_models)
                 except Exception as e:  # noqa: BLE001 — fedopt.py:103-106
                     logger.error(f"Error processing model update: {e}. Skipping this update.")
                     logger.error(traceback.format_exc())
@@ -129,9 +133,12 @@ class Aggregator(AggregatorBase):
             if hasattr(pipe, "release"):
                 pipe.release()
         except Exception as e:  # noqa: BLE001 — fedopt.py:111-116
+            data["nr_aggregated_models"] = nr_aggregated_models - self._settle(pipe, waiting, delete_models)
             logger.error(f"Error during model aggregation: {e}")
             logger.error(traceback.format_exc())
             return None, data
+        nr_aggregated_models -= self._settle(pipe, waiting, delete_models)
+        data["nr_aggregated_models"] = nr_aggregated_models
         logger.info(f"Aggregator {self.name} completed. Aggregated {nr_aggregated_models} models.")
         return model, data
 

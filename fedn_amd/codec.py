@@ -19,7 +19,7 @@ from .layout import Layout
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfednpz.so")
 MAX_DIMS = 16
-FNPZ_ABI_VERSION = 3    # include/fednpz.h
+FNPZ_ABI_VERSION = 4    # include/fednpz.h
 THREADS = int(os.environ.get("FEDN_AMD_CODEC_THREADS", str(min(16, os.cpu_count() or 1))))
 
 
@@ -74,7 +74,8 @@ def load_lib():
                                                  ctypes.POINTER(ctypes.c_int), ctypes.POINTER(Entry),
                                                  ctypes.POINTER(ctypes.c_int64)]
                 lib.fnpz_gather.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
-                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_int64]          # destination buffer window
                 lib.fnpz_gather_start.restype = ctypes.c_int64
                 lib.fnpz_gather_start.argtypes = lib.fnpz_gather.argtypes
                 lib.fnpz_gather_wait.argtypes = [ctypes.c_int64]
@@ -89,13 +90,15 @@ def _check(rc):
         raise CodecError(f"fednpz status {rc}: {load_lib().fnpz_last_error().decode(errors='replace')}")
 
 
-def gather_start_raw(dsts, srcs, nbytes, threads):
+def gather_start_raw(dsts, srcs, nbytes, threads, window):
     """``nbytes[i]`` bytes from address ``srcs[i]`` to ``dsts[i]`` (lists of ints), queued to the native
-    gather thread (``fnpz_gather_start``); returns the ticket for :func:`gather_wait`. The caller keeps
-    every source and destination alive until then."""
+    gather thread (``fnpz_gather_start``); returns the ticket for :func:`gather_wait`. ``window`` =
+    (address, length) of the destination buffer: a segment outside it raises CodecError (FNPZ_ENOSPC)
+    and nothing is copied. The caller keeps every source and destination alive until the ticket is done."""
     n = len(dsts)
+    lo, ln = window
     t = load_lib().fnpz_gather_start(n, (ctypes.c_void_p * n)(*dsts), (ctypes.c_void_p * n)(*srcs),
-                                     (ctypes.c_int64 * n)(*nbytes), max(1, threads))
+                                     (ctypes.c_int64 * n)(*nbytes), max(1, threads), int(lo), int(ln))
     if t < 0:
         _check(-t)
     return t
@@ -105,31 +108,38 @@ def gather_wait(ticket):
     _check(load_lib().fnpz_gather_wait(ticket))
 
 
-def gather_raw(jobs, threads):
+def gather_raw(jobs, threads, window):
     """``(dst address, src address, bytes)`` copies in one native call (``fnpz_gather``: 1 MiB+ pieces
-    on the persistent thread pool, the GIL released); the caller keeps both ends alive."""
+    on the persistent thread pool, the GIL released); the caller keeps both ends alive. ``window`` =
+    (address, length) of the destination buffer every copy must land in (else CodecError)."""
     n = len(jobs)
     if not n:
         return
     dsts, srcs, nb = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)(), (ctypes.c_int64 * n)()
     for i, (d, src, b) in enumerate(jobs):
         dsts[i], srcs[i], nb[i] = d, src, b
-    _check(load_lib().fnpz_gather(n, dsts, srcs, nb, int(threads)))
+    lo, ln = window
+    _check(load_lib().fnpz_gather(n, dsts, srcs, nb, int(threads), int(lo), int(ln)))
 
 
 def gather(pairs, threads):
     """``dst[:] = src`` for each (dst, src) pair of C-contiguous numpy arrays of equal byte size, in
     one native call (``fnpz_gather``: 1 MiB+ pieces on a persistent thread pool; the GIL is released
-    while it copies)."""
+    while it copies). The destination window is the span the destination arrays cover (numpy bounds
+    each one)."""
     n = len(pairs)
     dsts, srcs, nb = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)(), (ctypes.c_int64 * n)()
+    lo = hi = None
     for i, (d, src) in enumerate(pairs):
         if d.nbytes != src.nbytes:
             raise ValueError(f"gather: {d.nbytes} != {src.nbytes} bytes")
         if not (d.flags.c_contiguous and src.flags.c_contiguous):
             raise ValueError("gather: non-contiguous array")
         dsts[i], srcs[i], nb[i] = d.ctypes.data, src.ctypes.data, d.nbytes
-    _check(load_lib().fnpz_gather(n, dsts, srcs, nb, int(threads)))
+        if d.nbytes:
+            a, b = d.ctypes.data, d.ctypes.data + d.nbytes
+            lo, hi = (a, b) if lo is None else (min(lo, a), max(hi, b))
+    _check(load_lib().fnpz_gather(n, dsts, srcs, nb, int(threads), lo or 0, (hi - lo) if lo is not None else 0))
 
 
 def _as_u8(buf):

@@ -11,12 +11,13 @@
  * function address the caller passes), so the Python thread moves on to the next update.
  *
  *   plan(specs) -> capsule       specs: one (shape tuple, dtype, dst byte offset) per tensor
- *   admit(plan, arrays, dst_addr, gather_start_addr, threads) -> int
+ *   admit(plan, arrays, dst_addr, gather_start_addr, threads, buf_addr, buf_len) -> int
  *       > 0  the gather ticket (wait on it with fnpz_gather_wait before reading dst)
  *         0  admitted, nothing to copy (only empty tensors)
  *        -1  not this layout (wrong length / type / shape / dtype, or not C-contiguous): the
  *            caller takes its general path, which raises numpy's error where numpy would
- *        -2  the gather queue refused the job (fnpz_last_error says why)
+ *        -2  the gather queue refused the job (fnpz_last_error says why: e.g. FNPZ_ENOSPC, a
+ *            destination outside [buf_addr, buf_addr + buf_len), the pinned buffer it packs into)
  * The caller keeps ``arrays`` referenced until the ticket is done.
  */
 #define PY_SSIZE_T_CLEAN
@@ -27,7 +28,7 @@
 #include <string.h>
 
 typedef int64_t (*gather_start_fn)(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes,
-                                   int threads);
+                                   int threads, const void* dst_lo, int64_t dst_len);
 
 typedef struct {
     int ndim;
@@ -96,9 +97,10 @@ static inline int same_dtype(PyArray_Descr* a, PyArray_Descr* b) {
 
 static PyObject* fp_admit(PyObject* self, PyObject* args) {
     PyObject *cap, *arrays;
-    unsigned long long dst, fn;
+    unsigned long long dst, fn, buf;
+    long long buf_len;
     int threads;
-    if (!PyArg_ParseTuple(args, "OOKKi", &cap, &arrays, &dst, &fn, &threads)) return NULL;
+    if (!PyArg_ParseTuple(args, "OOKKiKL", &cap, &arrays, &dst, &fn, &threads, &buf, &buf_len)) return NULL;
     Plan* p = (Plan*)PyCapsule_GetPointer(cap, "fedn_amd._fastpack.plan");
     if (!p) return NULL;
     if (!PyList_CheckExact(arrays) || PyList_GET_SIZE(arrays) != p->n) return PyLong_FromLong(-1);
@@ -137,7 +139,8 @@ static PyObject* fp_admit(PyObject* self, PyObject* args) {
         }
     }
     if (rc == 0 && k > 0) {
-        int64_t ticket = ((gather_start_fn)(uintptr_t)fn)(k, dsts, srcs, nb, threads < 1 ? 1 : threads);
+        int64_t ticket = ((gather_start_fn)(uintptr_t)fn)(k, dsts, srcs, nb, threads < 1 ? 1 : threads,
+                                                           (const void*)(uintptr_t)buf, (int64_t)buf_len);
         rc = ticket > 0 ? (long)ticket : -2;
     }
     if (dsts != dsts_s) PyMem_Free(dsts), PyMem_Free(srcs), PyMem_Free(nb);
@@ -147,7 +150,8 @@ static PyObject* fp_admit(PyObject* self, PyObject* args) {
 static PyMethodDef methods[] = {
     {"plan", fp_plan, METH_VARARGS, "plan([(shape, dtype, dst_offset), ...]) -> capsule"},
     {"admit", fp_admit, METH_VARARGS,
-     "admit(plan, arrays, dst_addr, gather_start_addr, threads) -> ticket | 0 | -1 (not this layout) | -2"},
+     "admit(plan, arrays, dst_addr, gather_start_addr, threads, buf_addr, buf_len) -> ticket | 0 | -1 (not this "
+     "layout) | -2"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_fastpack", NULL, -1, methods};

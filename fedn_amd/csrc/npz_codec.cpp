@@ -1088,14 +1088,32 @@ class GatherQueue {
     bool started_ = false;
 };
 
+// Every destination segment inside the caller's buffer [lo, lo + len): checked before anything is
+// copied or queued, so an accounting slip above (a full arena, a wrong offset) is a status, not a
+// write past a pinned block.
+static int check_window(const char* who, int n, void* const* dsts, const int64_t* nbytes, const void* lo, int64_t len) {
+    if (n > 0 && (!lo || len < 0)) return fail(FNPZ_EINVAL, "%s: no destination window", who);
+    const uintptr_t w0 = reinterpret_cast<uintptr_t>(lo);
+    for (int i = 0; i < n; ++i) {
+        if (nbytes[i] == 0) continue;
+        const uintptr_t d = reinterpret_cast<uintptr_t>(dsts[i]);
+        if (d < w0 || d - w0 > (uint64_t)len || (uint64_t)nbytes[i] > (uint64_t)len - (d - w0))
+            return fail(FNPZ_ENOSPC, "%s: segment %d (%lld bytes at offset %lld) outside the %lld-byte destination buffer",
+                        who, i, (long long)nbytes[i], (long long)((int64_t)d - (int64_t)w0), (long long)len);
+    }
+    return FNPZ_OK;
+}
+
 extern "C" int64_t fnpz_gather_start(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes,
-                                     int threads) {
+                                     int threads, const void* dst_lo, int64_t dst_len) {
     if (n < 0 || (n > 0 && (!dsts || !srcs || !nbytes)) || threads < 1)
         return -fail(FNPZ_EINVAL, "fnpz_gather_start: bad arguments");
-    std::vector<GatherQueue::Piece> pieces;
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n; ++i)
         if (nbytes[i] < 0 || (nbytes[i] > 0 && (!dsts[i] || !srcs[i])))
             return -fail(FNPZ_EINVAL, "fnpz_gather_start: segment %d", i);
+    if (int rc = check_window("fnpz_gather_start", n, dsts, nbytes, dst_lo, dst_len)) return -rc;
+    std::vector<GatherQueue::Piece> pieces;
+    for (int i = 0; i < n; ++i) {
         // 64 KiB pieces: a small update (one tensor dominating, e.g. mnist's 200 KB first layer) still
         // spreads over several threads
         for (int64_t o = 0; o < nbytes[i]; o += 1 << 16)
@@ -1111,7 +1129,8 @@ extern "C" int fnpz_gather_wait(int64_t ticket) {
     return FNPZ_OK;
 }
 
-extern "C" int fnpz_gather(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes, int threads) {
+extern "C" int fnpz_gather(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes, int threads,
+                           const void* dst_lo, int64_t dst_len) {
     if (n < 0 || (n > 0 && (!dsts || !srcs || !nbytes)) || threads < 1)
         return fail(FNPZ_EINVAL, "fnpz_gather: bad arguments");
     int64_t total = 0;
@@ -1119,6 +1138,7 @@ extern "C" int fnpz_gather(int n, void* const* dsts, const void* const* srcs, co
         if (nbytes[i] < 0 || (nbytes[i] > 0 && (!dsts[i] || !srcs[i]))) return fail(FNPZ_EINVAL, "fnpz_gather: segment %d", i);
         total += nbytes[i];
     }
+    if (int rc = check_window("fnpz_gather", n, dsts, nbytes, dst_lo, dst_len)) return rc;
     if (total == 0) return FNPZ_OK;
     struct Piece {
         uint8_t* d;

@@ -60,11 +60,18 @@ def run_pack_jobs(jobs):
         f.result()
 
 
-def start_pack_into(layout, arrays, dst_ptr):
+def _in_window(dst_ptr, nbytes, window):
+    lo, ln = window
+    if dst_ptr < lo or dst_ptr + nbytes > lo + ln:
+        raise ValueError(f"pack: {nbytes} bytes at offset {dst_ptr - lo} do not fit the {ln}-byte destination buffer")
+
+
+def start_pack_into(layout, arrays, dst_ptr, window):
     """Queue the pack of ``arrays`` (already checked against ``layout``: shapes and dtypes) into the
     host bytes at address ``dst_ptr`` to the native gather thread; returns (ticket, the sources to
     keep referenced until :func:`wait_pack_jobs`). None as ticket: copied already (no codec library,
-    or a non-contiguous source)."""
+    or a non-contiguous source). ``window`` = (address, length) of the pinned buffer ``dst_ptr``
+    points into: a pack that would not fit raises (the native gather checks it too, fednpz ABI 4)."""
     srcs = [arrays[i] for i, _, _ in layout.pack_plan]
     if not srcs:                                  # only empty tensors: nothing to copy
         return None, srcs
@@ -73,9 +80,10 @@ def start_pack_into(layout, arrays, dst_ptr):
             from . import codec
             return codec.gather_start_raw([dst_ptr + off for _, off, _ in layout.pack_plan],
                                           [a.ctypes.data for a in srcs], [n for _, _, n in layout.pack_plan],
-                                          PACK_THREADS), srcs
+                                          PACK_THREADS, window), srcs
         except ImportError:
             pass
+    _in_window(dst_ptr, layout.nbytes, window)
     buf = np.ctypeslib.as_array((ctypes.c_uint8 * layout.nbytes).from_address(dst_ptr))
     layout.pack(arrays, buf)
     return None, srcs
@@ -96,10 +104,12 @@ def _fast():
 
 
 def fast_admission(layout):
-    """``admit(arrays, dst_ptr) -> ticket | 0 | -1`` for ``layout`` (cached on it): the exact
+    """``admit(arrays, dst_ptr, window) -> ticket | 0 | -1`` for ``layout`` (cached on it): the exact
     (shape, dtype, C-contiguous) test of a host update and the queueing of its pack into the pinned
     bytes at ``dst_ptr`` in ONE native call (``_fastpack``, csrc/fastpack.c); -1 leaves everything
-    untouched (not this layout). None if the extension or the codec library is not built."""
+    untouched (not this layout). ``window`` = (address, length) of the pinned buffer: a pack outside
+    it raises CodecError (FNPZ_ENOSPC) with nothing copied. None if the extension or the codec
+    library is not built."""
     f = getattr(layout, "_fast_admit", 0)
     if f == 0:
         f = None
@@ -111,8 +121,8 @@ def fast_admission(layout):
             plan = _fastpack.plan([(tuple(sh), np.dtype(dt), offs.get(i, 0))
                                    for i, (sh, dt) in enumerate(zip(layout.shapes, layout.dtypes))])
 
-            def f(arrays, dst_ptr, plan=plan, admit=admit, gstart=gstart):
-                t = admit(plan, arrays, dst_ptr, gstart, PACK_THREADS)
+            def f(arrays, dst_ptr, window, plan=plan, admit=admit, gstart=gstart):
+                t = admit(plan, arrays, dst_ptr, gstart, PACK_THREADS, window[0], window[1])
                 if t == -2:                     # the gather queue refused the job: its reason
                     from . import codec
                     why = codec.load_lib().fnpz_last_error().decode(errors="replace")

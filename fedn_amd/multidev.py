@@ -139,7 +139,40 @@ class _ShardedStaging:
         self.dslots = None
         self._next = 0
         self.reserved = set()
-        self.pending = []                              # resident updates not folded yet: (model, n, N)
+        self.pending = []                              # resident updates not folded yet: (model, n, N, tag)
+        self.skipped = []                              # (tag, exception): see staging._Pipeline.skipped
+        self.broken = None
+
+    def take_skipped(self):
+        out, self.skipped = self.skipped, []
+        return out
+
+    def unsettled(self):
+        return len(self.pending)
+
+    def _check_broken(self):
+        if self.broken is not None:
+            raise RuntimeError(f"a batched fold failed and could not be recovered: {self.broken}") from self.broken
+
+    def _sync_all(self):
+        for st in (*self.compute, *self.copy, *self.d2h):
+            st.synchronize()
+
+    def _copy_aside(self, per_dev):
+        """Device copies of ``per_dev`` ([{group: tensor}] per device) on each compute stream."""
+        out = []
+        for d, dv in enumerate(self.devices):
+            with torch.cuda.device(dv), torch.cuda.stream(self.compute[d]):
+                out.append({dt: t.clone() for dt, t in per_dev[d].items()})
+        return out
+
+    def _copy_back(self, per_dev, snap):
+        if snap is None:
+            return
+        for d, dv in enumerate(self.devices):
+            with torch.cuda.device(dv), torch.cuda.stream(self.compute[d]):
+                for dt, t in snap[d].items():
+                    per_dev[d][dt].copy_(t)
 
     def _ensure_slots(self):
         if self.host is None:
@@ -285,7 +318,8 @@ class ShardedFedAvgPipeline(_ShardedStaging):
         self.general = mixed.TensorFedAvg(self.devices[0], self.compute[0], self.gathered(self.layout, self.bounds, slices),
                                           owned=True)
 
-    def add(self, arrays, n, N):
+    def add(self, arrays, n, N, tag=None):
+        self._check_broken()
         if self.general is None and (not self.compatible(arrays) or
                                      mixed.int_float_n(self.layout.dtypes, self.nfolds, n) or
                                      mixed.per_tensor_dtypes(self.layout.dtypes)):
@@ -305,16 +339,40 @@ class ShardedFedAvgPipeline(_ShardedStaging):
             ops.fa_dtype(ops.torch_dtype(dt))
         if resident:
             self._accept(arrays)
-            self.pending.append((arrays, n, N))
+            self.pending.append((arrays, n, N, tag))
             if len(self.pending) >= BATCH:
                 self._flush()
         else:
             self._flush()
             s = self._stage(arrays)
-            self._fold_all([(s, n, N)])
-            for d in range(len(self.devices)):
-                self.dslots[d][s].consumed.record(self.compute[d])
+            try:
+                self._fold_all([(s, n, N)])     # all-or-nothing: the caller skips the update on failure
+            finally:
+                for d in range(len(self.devices)):
+                    self.dslots[d][s].consumed.record(self.compute[d])
         self.nfolds += 1
+
+    def _snapshot(self):
+        """The aggregate slices copied aside before a continuation fold of several launches (see
+        staging.FedAvgPipeline._snapshot); None when a failed fold cannot leave it half-advanced."""
+        if not self.agg_started or len(self.devices) * len(self.layout.groups) <= 1:
+            return None
+        return self._copy_aside([{dt: self._agg(d, dt) for dt in self.layout.groups} for d in range(len(self.devices))])
+
+    def _restore(self, snap):
+        self._copy_back([{dt: self._agg(d, dt) for dt in self.layout.groups} for d in range(len(self.devices))], snap)
+
+    def _refold_singly(self, entries):
+        """A batched fold over ``entries`` failed: one update at a time (fedavg.py:47-78); an update
+        whose own fold fails is skipped and reported, the aggregate left as before it."""
+        for e in entries:
+            try:
+                self._fold_all([e])
+            except ops.FedAggError as ex:
+                self.skipped.append((e[3] if len(e) > 3 else None, ex))
+
+    def _alias(self):
+        return _host_arrays(self.first_arrays)   # `model = model_next` alias (fedavg.py:65-66)
 
     def _agg(self, d, dt):
         if dt not in self.agg[d]:
@@ -345,33 +403,67 @@ class ShardedFedAvgPipeline(_ShardedStaging):
         self.agg_started = True
 
     def _fold_all(self, entries):
+        """One fold of ``entries`` on every device and group, all-or-nothing: on a failed launch the
+        aggregate is put back (or stays unstarted) and the FedAggError propagates."""
         init = not self.agg_started
-        for d in range(len(self.devices)):
-            for dt in self.layout.groups:
-                lo, hi = self.bounds[dt][d]
-                self._fold_dev(d, dt, entries, init, 0, hi - lo)
+        snap = self._snapshot()
+        try:
+            for d in range(len(self.devices)):
+                for dt in self.layout.groups:
+                    lo, hi = self.bounds[dt][d]
+                    self._fold_dev(d, dt, entries, init, 0, hi - lo)
+        except ops.FedAggError:
+            self._restore(snap)
+            raise
         self._folded()
 
     def _flush(self):
         if self.pending:
             entries, self.pending = self.pending, []
-            self._fold_all(entries)
+            try:
+                try:
+                    self._fold_all(entries)
+                except ops.FedAggError:
+                    self._refold_singly(entries)
+            except BaseException as e:          # the batch is lost: never return a model without it
+                self.broken = e
+                raise
 
     def result(self):
+        self._check_broken()
         if self.nfolds == 0:
-            return _host_arrays(self.first_arrays)     # `model = model_next` alias (fedavg.py:65-66)
+            return self._alias()
         if self.general is not None:
             return self.general.result()
         entries, self.pending = self.pending, []
+        if not entries and not self.agg_started:
+            return self._alias()                # every fold after the first update was skipped
         init = not self.agg_started
         flats = {}
-        for dt in self.layout.groups:
-            t = ops.torch_dtype(dt)
-            fold = None
-            if entries:
-                fold = lambda d, clo, chi, dt=dt: self._fold_dev(d, dt, entries, init, clo, chi)  # noqa: E731
-            per_dev = [self._agg(d, dt) for d in range(len(self.devices))]
-            flats[dt] = self._to_host_chunks(dt, per_dev, fold, ops.fold_result_dtype(t, t))
+        snap = self._snapshot() if entries else None
+        try:
+            for dt in self.layout.groups:
+                t = ops.torch_dtype(dt)
+                fold = None
+                if entries:
+                    fold = lambda d, clo, chi, dt=dt: self._fold_dev(d, dt, entries, init, clo, chi)  # noqa: E731
+                per_dev = [self._agg(d, dt) for d in range(len(self.devices))]
+                flats[dt] = self._to_host_chunks(dt, per_dev, fold, ops.fold_result_dtype(t, t))
+        except ops.FedAggError:
+            if not entries:
+                raise
+            self._sync_all()
+            self._restore(snap)
+            self._refold_singly(entries)
+            entries = []
+            if not self.agg_started:
+                self._sync_all()
+                return self._alias()
+            flats = {}
+            for dt in self.layout.groups:
+                t = ops.torch_dtype(dt)
+                per_dev = [self._agg(d, dt) for d in range(len(self.devices))]
+                flats[dt] = self._to_host_chunks(dt, per_dev, None, ops.fold_result_dtype(t, t))
         if entries:
             self._folded()
         self._sync_d2h()
@@ -498,7 +590,8 @@ class ShardedFedOptPipeline(_ShardedStaging):
         old = mixed.upload(self.old_arrays, self.devices[0], self.compute[0])
         self.general = mixed.TensorFedOpt(self.devices[0], self.compute[0], old, pg)
 
-    def add(self, arrays, n, N):
+    def add(self, arrays, n, N, tag=None):
+        self._check_broken()
         if self.general is None and not (self.fused_ok and self.compatible(arrays)):
             splan = mixed.sub_plan(self.meta_of(arrays), mixed.host_meta(self.old_arrays))   # raises as numpy
             if self.nfolds:
@@ -513,15 +606,17 @@ class ShardedFedOptPipeline(_ShardedStaging):
             arrays = _host_arrays(arrays)
         if resident:
             self._accept(arrays)
-            self.pending.append((arrays, n, N))
+            self.pending.append((arrays, n, N, tag))
             if len(self.pending) >= BATCH:
                 self._flush()
         else:
             self._flush()
             s = self._stage(arrays)
-            self._fold_pg([(s, n, N)])
-            for d in range(len(self.devices)):
-                self.dslots[d][s].consumed.record(self.compute[d])
+            try:
+                self._fold_pg([(s, n, N)])      # all-or-nothing: the caller skips the update on failure
+            finally:
+                for d in range(len(self.devices)):
+                    self.dslots[d][s].consumed.record(self.compute[d])
         self.nfolds += 1
 
     def _pg(self, d, dt):
@@ -545,21 +640,48 @@ class ShardedFedOptPipeline(_ShardedStaging):
             self.old_ready.add(dt)
 
     def _fold_pg(self, entries):
-        for dt in self.layout.groups:
-            self._old_all(dt)
-            for d in range(len(self.devices)):
-                lo, hi = self.bounds[dt][d]
-                pg = self._pg(d, dt)
-                if hi > lo:
-                    ys = [self._view(d, e[0], dt) for e in entries]
-                    ops.fedopt_step(self.old[d][dt], ys, [e[1] for e in entries], [e[2] for e in entries],
-                                    first=not self.pg_started, final=False, pg=pg, stream=self.compute[d])
+        """``entries`` into every device's pg slices, all-or-nothing (pg copied aside first when a
+        started pg is continued by several launches); a failed launch's FedAggError propagates."""
+        snap = None
+        if self.pg_started and len(self.devices) * len(self.layout.groups) > 1:
+            snap = self._copy_aside([{dt: self._pg(d, dt) for dt in self.layout.groups} for d in range(len(self.devices))])
+        try:
+            for dt in self.layout.groups:
+                self._old_all(dt)
+                for d in range(len(self.devices)):
+                    lo, hi = self.bounds[dt][d]
+                    pg = self._pg(d, dt)
+                    if hi > lo:
+                        ys = [self._view(d, e[0], dt) for e in entries]
+                        ops.fedopt_step(self.old[d][dt], ys, [e[1] for e in entries], [e[2] for e in entries],
+                                        first=not self.pg_started, final=False, pg=pg, stream=self.compute[d])
+        except ops.FedAggError:
+            self._copy_back([{dt: self._pg(d, dt) for dt in self.layout.groups} for d in range(len(self.devices))], snap)
+            raise
         self.pg_started = True
+
+    def _fold_pg_isolated(self, entries):
+        """A batch into pg; on a failed launch one update at a time (fedopt.py:74-106), skipping and
+        reporting each update whose own fold fails."""
+        try:
+            self._fold_pg(entries)
+            return
+        except ops.FedAggError:
+            pass
+        for e in entries:
+            try:
+                self._fold_pg([e])
+            except ops.FedAggError as ex:
+                self.skipped.append((e[3] if len(e) > 3 else None, ex))
 
     def _flush(self):
         if self.pending:
             entries, self.pending = self.pending, []
-            self._fold_pg(entries)
+            try:
+                self._fold_pg_isolated(entries)
+            except BaseException as e:          # the batch is lost: never return a model without it
+                self.broken = e
+                raise
 
     def server_step(self, state, params):
         opt = params["serveropt"]
@@ -573,10 +695,26 @@ class ShardedFedOptPipeline(_ShardedStaging):
             model, m, v = self.general.server_step(m, v, params)
             state.set_tensors(m, v)
             return model
+        self._check_broken()
         # per device and group, one fused launch: pending (resident) updates folded into the
         # pseudo-gradient in registers (FIRST when pg holds nothing yet) and the server step,
         # chunked so that the global model's H2D, the step and the result's D2H overlap
         entries, self.pending = self.pending, []
+        if not entries and not self.pg_started:
+            raise ValueError("no update was folded into the pseudo-gradient")   # fedopt.py:110, 117-118
+        old_ready = set(self.old_ready)
+        try:
+            return self._fused_step(state, params, opt, sig, entries)
+        except ops.FedAggError:
+            if not entries:
+                raise                           # the server step itself failed (fedopt.py:111-116)
+        # see staging.FedOptPipeline.server_step: the batch one update at a time, then K = 0
+        self._sync_all()
+        self.old_ready = old_ready
+        self._fold_pg_isolated(entries)
+        return self.server_step(state, params)
+
+    def _fused_step(self, state, params, opt, sig, entries):
         first = not self.pg_started
         ns, Ns = [e[1] for e in entries], [e[2] for e in entries]
         new_m = [dict() for _ in self.devices]

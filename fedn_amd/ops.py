@@ -13,6 +13,7 @@ import numpy as np
 import torch
 
 from . import _abi
+from ._abi import FedAggError  # noqa: F401  (the status exception, re-exported for the pipelines)
 
 _TORCH_TO_FA = {
     torch.float32: _abi.FA_F32,

@@ -110,7 +110,9 @@ def reduce_models(combiners, fetch, load, delete=None, device=None, workers=8):
                     if model_next is None:       # the load itself raised: FEDn loads again (and raises)
                         model_next = load(data)
                     # else the fold raised: FEDn re-decodes the same bytes; the decoded arrays are reused
-                    pipe = FedAvgPipeline(device or default_device(), model_next)
+                    # no deferred batches: a fold that fails must raise here, where FEDn replaces the
+                    # running model with this one (control.py:683-686)
+                    pipe = FedAvgPipeline(device or default_device(), model_next, batch=False)
                     meta["time_aggregate_model"] += time.time() - tic
                 i = i + 1
             if delete is not None:

@@ -239,6 +239,25 @@ class _Pipeline:
         self._copy_used = False                  # work was enqueued on the copy stream this round
         self._d2h_used = False                   # ... on the d2h stream
         self.streamer = kept["streamer"] if kept else HostStreamer()
+        # per-update failure isolation (fedavg.py:75-78, fedopt.py:103-106): updates admitted into a
+        # batch whose multi-client launch failed are refolded one at a time; (tag, exception) of each
+        # one whose own fold failed, for the aggregator to log, uncount and keep in storage
+        self.skipped = []
+        self.broken = None                       # a batch lost beyond recovery: result() raises it
+
+    def take_skipped(self):
+        """(tag, exception) of the updates skipped since the last call (see ``skipped``)."""
+        out, self.skipped = self.skipped, []
+        return out
+
+    def unsettled(self):
+        """How many of the most recently added updates are admitted but not folded yet (the pending
+        batch): their fold may still fail, so the aggregator keeps them in storage until then."""
+        return len(self.pending)
+
+    def _check_broken(self):
+        if self.broken is not None:
+            raise RuntimeError(f"a batched fold failed and could not be recovered: {self.broken}") from self.broken
 
     def release(self):
         """Give the staging resources to the cache for the session's next round (call once the
@@ -294,7 +313,7 @@ class _Pipeline:
             s.pieces = []
             for (lo, hi), job in zip(spans, jobs):
                 t0 = time.perf_counter()
-                codec.gather_raw(job, PACK_THREADS)
+                codec.gather_raw(job, PACK_THREADS, (host_ptr, s.host.numel()))
                 self.time_pack += time.perf_counter() - t0
                 ops.copy_ptr_async(dev_ptr + lo, host_ptr + lo, hi - lo, self.copy, self.device)
                 ev = torch.cuda.Event()
@@ -343,13 +362,15 @@ class _Pipeline:
         tic = time.perf_counter()
         # the copies go to the native gather thread and run while the next updates are loaded;
         # upload_arena waits for them (the source arrays stay referenced until then)
+        # the arena's pinned block as allocated (not as counted): the native pack is checked against it
+        window = (a.host_ptr, a.host.numel())
         if fast:
-            ticket = self._admit(arrays, a.host_ptr + j * nb)
+            ticket = self._admit(arrays, a.host_ptr + j * nb, window)
             if ticket < 0:
                 return None
             keep = arrays
         else:
-            ticket, keep = start_pack_into(self.layout, arrays, a.host_ptr + j * nb)
+            ticket, keep = start_pack_into(self.layout, arrays, a.host_ptr + j * nb, window)
         self._pack_jobs.append(keep)
         self._pack_ticket = ticket or self._pack_ticket
         self.time_pack += time.perf_counter() - tic
@@ -572,29 +593,31 @@ class FedAvgPipeline(_Pipeline):
             views = mixed.tensor_views(self.layout, mixed.u8_flats(self.layout, src))
             self.general = mixed.TensorFedAvg(self.device, self.compute, views, owned=False)
 
-    def add(self, arrays, n, N):
+    def add(self, arrays, n, N, tag=None):
         """Fold one more update (n = its num_examples, N = running total including it).
         A device-resident update (StagedModel) joins the pending batch; host arrays are
         staged and folded on arrival (after any pending batch, keeping FIFO order). An update
         whose dtypes or shapes differ from the first's moves the round to the per-tensor path
-        (numpy promotion / broadcasting, mixed.py) — checked before any state changes."""
+        (numpy promotion / broadcasting, mixed.py) — checked before any state changes.
+        ``tag``: reported back with the update if its batched fold fails later (``skipped``)."""
+        self._check_broken()
         if self._admit is not None and self.general is None and type(arrays) is list:
             ref = self.put_small(arrays, fast=True)                 # a small float model's update
             if ref is not None:
-                self.pending.append((ref, n, N))
+                self.pending.append((ref, n, N, tag))
                 if len(self.pending) >= BATCH or self.arena_full():
                     self._flush()
                 self.nfolds += 1
                 return
         elif self.general is None and type(arrays) is list and self.fast_host(arrays):
-            self.pending.append((self.put_small(arrays), n, N))      # a small float model's update
+            self.pending.append((self.put_small(arrays), n, N, tag))      # a small float model's update
             if len(self.pending) >= BATCH or self.arena_full():
                 self._flush()
             self.nfolds += 1
             return
         elif self.general is None and self._plain and type(arrays) is StagedModel and arrays.layout is self.layout:
             # staged on arrival in this very layout (the ingest's round end): nothing else to check
-            self.pending.append((self._resident(arrays), n, N))
+            self.pending.append((self._resident(arrays), n, N, tag))
             if len(self.pending) >= BATCH:
                 self._flush()
             self.nfolds += 1
@@ -618,19 +641,53 @@ class FedAvgPipeline(_Pipeline):
         for dt in self.layout.groups:           # refuse before touching device state
             ops.fa_dtype(ops.torch_dtype(dt))
         if isinstance(arrays, StagedModel):
-            self.pending.append((self.acquire(arrays), n, N))
+            self.pending.append((self.acquire(arrays), n, N, tag))
             if len(self.pending) >= BATCH:
                 self._flush()
         elif self.batch_host:
-            self.pending.append((self.put_small(arrays), n, N))
+            self.pending.append((self.put_small(arrays), n, N, tag))
             if len(self.pending) >= BATCH or self.arena_full():
                 self._flush()
         else:
             self._flush()
             slot = self.stage(arrays, wait=False)
-            self._fold_pieces(slot, n, N)
-            slot.consumed.record(self.compute)
+            try:
+                self._fold_pieces(slot, n, N)
+            finally:
+                slot.consumed.record(self.compute)   # the slot's next H2D waits for what was enqueued
         self.nfolds += 1
+
+    # ---- per-update failure isolation (fedavg.py:75-78) ---------------------------------------
+    def _snapshot(self, launches):
+        """The running aggregate copied aside before a continuation fold of more than one launch:
+        one that fails part-way leaves it half-advanced, and the recovery needs it back. None when
+        not needed: not started (an init fold rewrites it) or one launch (a failed launch ran nothing)."""
+        if not self.agg_started or launches <= 1:
+            return None
+        with torch.cuda.device(self.device), torch.cuda.stream(self.compute):
+            return {dt: self._agg(dt).clone() for dt in self.layout.groups}
+
+    def _restore(self, snap):
+        if snap is not None:
+            with torch.cuda.device(self.device), torch.cuda.stream(self.compute):
+                for dt, t in snap.items():
+                    self._agg(dt).copy_(t)
+
+    def _refold_singly(self, entries):
+        """A multi-client launch over ``entries`` failed: fold them one at a time in FIFO order as
+        FEDn does (fedavg.py:47-78). An update whose own fold fails is skipped and reported with its
+        tag; its examples stay counted (its N is already in every later entry's running total), and
+        the aggregate is as the previous update left it (each update's launches are all-or-nothing)."""
+        for e in entries:
+            snap = self._snapshot(len(self.layout.groups))
+            try:
+                for dt in self.layout.groups:
+                    self._fold_group(dt, [e], not self.agg_started, 0, self.layout.group_elems[dt])
+            except ops.FedAggError as ex:
+                self._restore(snap)
+                self.skipped.append((e[3] if len(e) > 3 else None, ex))
+                continue
+            self._folded()
 
     def _fold_pieces(self, slot, n, N):
         """Fold one staged host update on arrival, one launch per H2D piece of each group, each
@@ -639,7 +696,7 @@ class FedAvgPipeline(_Pipeline):
         recurrence step: the same bits as one launch."""
         span = self._kernel_span()
         init = not self.agg_started
-        done = []
+        plan = []
         for dt in self.layout.groups:
             off, isz, P = self.layout.group_byte_offset[dt], np.dtype(dt).itemsize, self.layout.group_elems[dt]
             if slot.pieces is None:
@@ -649,12 +706,20 @@ class FedAvgPipeline(_Pipeline):
                 bounds = [(lo, hi) for lo, hi in bounds if hi > lo]
                 if bounds:
                     bounds[-1] = (bounds[-1][0], P)
-            for lo, hi in bounds:
+            plan += [(dt, off, isz, lo, hi) for lo, hi in bounds]
+        snap = self._snapshot(len(plan))        # this update's launches are all-or-nothing
+        done = []
+        try:
+            for dt, off, isz, lo, hi in plan:
                 self.wait_bytes(slot, off + lo * isz, off + hi * isz)
                 self._fold_group(dt, [(slot, n, N)], init, lo, hi)
                 ev = torch.cuda.Event()
                 ev.record(self.compute)
                 done.append((dt, lo, hi, ev))
+        except ops.FedAggError:
+            self._last_fold = None
+            self._restore(snap)                 # the update is skipped by the caller (fedavg.py:75-78)
+            raise
         self._end_span(span)
         self._folded()
         self._last_fold = done
@@ -694,8 +759,15 @@ class FedAvgPipeline(_Pipeline):
         self._last_fold = None
         span = self._kernel_span()
         init = not self.agg_started
-        for dt in self.layout.groups:
-            self._fold_group(dt, entries, init, 0, self.layout.group_elems[dt])
+        snap = self._snapshot(len(self.layout.groups))
+        try:
+            for dt in self.layout.groups:
+                self._fold_group(dt, entries, init, 0, self.layout.group_elems[dt])
+        except ops.FedAggError:
+            self._restore(snap)
+            self._refold_singly(entries)
+            self._end_span(span)
+            return
         self._end_span(span)
         self._folded()
 
@@ -703,14 +775,18 @@ class FedAvgPipeline(_Pipeline):
         self.upload_arena()                     # also the first update, when it waits in the arena
         if self.pending:
             entries, self.pending = self.pending, []
-            self._fold_all(entries)
+            try:
+                self._fold_all(entries)
+            except BaseException as e:          # the batch is lost: never return a model without it
+                self.broken = e
+                raise
 
     def result(self):
         """The aggregated model as a new host ``list[np.ndarray]`` (fedavg.py:83). A pending
         batch is folded here, chunk by chunk, each chunk's D2H overlapping the next fold."""
+        self._check_broken()
         if self.nfolds == 0:
-            first = self.first_arrays           # `model = model_next` alias (fedavg.py:65-66)
-            return first.host if isinstance(first, StagedModel) else first
+            return self._alias()
         if self.general is not None:
             return self.general.result()
         tic = time.perf_counter()
@@ -720,20 +796,38 @@ class FedAvgPipeline(_Pipeline):
             return out
         self.upload_arena()
         entries, self.pending = self.pending, []
+        if not entries and not self.agg_started:
+            return self._alias()                # every fold after the first update was skipped
         last = self._last_fold if not entries else None
         init = not self.agg_started
         span = self._kernel_span()
         hosts = {}
-        for dt in self.layout.groups:
-            ready = None
-            if entries:
-                fold = lambda lo, hi, dt=dt: self._fold_group(dt, entries, init, lo, hi)  # noqa: E731
-            else:
-                fold = lambda lo, hi: None  # noqa: E731
-                if last is not None:            # each D2H chunk waits only for the folds it reads
-                    mine = [(lo, hi, ev) for d, lo, hi, ev in last if d == dt]
-                    ready = lambda lo, hi, mine=mine: [ev for flo, fhi, ev in mine if flo < hi and lo < fhi]  # noqa: E731
-            hosts[dt] = self._fold_then_d2h(self._agg(dt), fold, ready=ready)
+        # the last batch runs chunk by chunk (or per group): a failed chunk needs the aggregate back
+        snap = self._snapshot(2 if (len(self.layout.groups) > 1 or self.layout.nbytes > SMALL_UPDATE_BYTES) else 1) \
+            if entries else None
+        try:
+            for dt in self.layout.groups:
+                ready = None
+                if entries:
+                    fold = lambda lo, hi, dt=dt: self._fold_group(dt, entries, init, lo, hi)  # noqa: E731
+                else:
+                    fold = lambda lo, hi: None  # noqa: E731
+                    if last is not None:            # each D2H chunk waits only for the folds it reads
+                        mine = [(lo, hi, ev) for d, lo, hi, ev in last if d == dt]
+                        ready = lambda lo, hi, mine=mine: [ev for flo, fhi, ev in mine if flo < hi and lo < fhi]  # noqa: E731
+                hosts[dt] = self._fold_then_d2h(self._agg(dt), fold, ready=ready)
+        except ops.FedAggError:
+            if not entries:
+                raise
+            self.compute.synchronize()          # what the failed attempt enqueued has run
+            self.d2h.synchronize()
+            self._restore(snap)
+            self._refold_singly(entries)
+            entries = []
+            if not self.agg_started:
+                self.compute.synchronize()
+                return self._alias()
+            hosts = {dt: self._fold_then_d2h(self._agg(dt), lambda lo, hi: None) for dt in self.layout.groups}
         self._end_span(span)
         if entries:
             self._folded()
@@ -747,6 +841,11 @@ class FedAvgPipeline(_Pipeline):
         for dt in self.layout.groups:
             self.layout.unpack_group(hosts[dt].numpy(), dt, out, copy=False)
         return out
+
+    def _alias(self):
+        """The first update itself: the model when nothing was folded into it (fedavg.py:65-66)."""
+        first = self.first_arrays
+        return first.host if isinstance(first, StagedModel) else first
 
     def _zero_copy_result(self):
         """A small round that never left the host: the first update and every pending one wait in the
@@ -772,18 +871,24 @@ class FedAvgPipeline(_Pipeline):
         ns, Ns = [0.0] + [e[1] for e in entries], [1.0] + [e[2] for e in entries]
         span = self._kernel_span()
         hosts = {}
-        for dt in self.layout.groups:
-            t = ops.torch_dtype(dt)
-            rdt = ops.fold_result_dtype(t, t)
-            n = self.layout.group_elems[dt]
-            host = torch.empty(n, dtype=rdt, pin_memory=True)
-            hosts[dt] = host
-            if n == 0:                          # a group of empty tensors: nothing to fold or map
-                continue
-            off = self.layout.group_byte_offset[dt]
-            ptrs = [a.host_dev + self.first._lo + off] + [a.host_dev + e[0]._lo + off for e in entries]
-            ops.fedavg_fold_raw(ops.host_device_ptr(host.data_ptr(), self.device), rdt, n, ptrs, t, ns, Ns, True,
-                                self.compute, self.device)
+        try:
+            for dt in self.layout.groups:
+                t = ops.torch_dtype(dt)
+                rdt = ops.fold_result_dtype(t, t)
+                n = self.layout.group_elems[dt]
+                host = torch.empty(n, dtype=rdt, pin_memory=True)
+                hosts[dt] = host
+                if n == 0:                          # a group of empty tensors: nothing to fold or map
+                    continue
+                off = self.layout.group_byte_offset[dt]
+                ptrs = [a.host_dev + self.first._lo + off] + [a.host_dev + e[0]._lo + off for e in entries]
+                ops.fedavg_fold_raw(ops.host_device_ptr(host.data_ptr(), self.device), rdt, n, ptrs, t, ns, Ns, True,
+                                    self.compute, self.device)
+        except ops.FedAggError:
+            # the batch goes the device way instead (upload, batched launch, one-at-a-time on failure)
+            self.compute.synchronize()
+            self.pending, self._arena = entries, a
+            return None
         self._end_span(span)
         self.agg_started = True
         a.done = torch.cuda.Event()
@@ -827,7 +932,7 @@ class AndroidFedAvgPipeline(_Pipeline):
         self.nfolds = 0
         self.g = None
 
-    def add(self, arrays, n, N):
+    def add(self, arrays, n, N, tag=None):
         arr = np.asarray(arrays)
         self.layout.check([arr])                # numpy would refuse other lengths too
         dt = self.layout.groups[0]
@@ -1057,28 +1162,30 @@ class FedOptPipeline(_Pipeline):
         old = mixed.upload(self.old_arrays, self.device, self.compute)
         self.general = mixed.TensorFedOpt(self.device, self.compute, old, pg)
 
-    def add(self, arrays, n, N):
+    def add(self, arrays, n, N, tag=None):
         """One more update into the pseudo-gradient (fedopt.py:89-94). Device-resident updates
         join the pending batch, which the server step folds in its fused launch; host arrays
         are staged and folded into pg on arrival (after any pending batch). Updates that differ
-        from the first in dtype or shape, or from the global model in shape, run per tensor."""
+        from the first in dtype or shape, or from the global model in shape, run per tensor.
+        ``tag``: reported back with the update if its batched fold fails later (``skipped``)."""
+        self._check_broken()
         if self._admit is not None and self.general is None and self.fused_ok and type(arrays) is list:
             ref = self.put_small(arrays, fast=True)                 # a small float model's update
             if ref is not None:
-                self.pending.append((ref, n, N))
+                self.pending.append((ref, n, N, tag))
                 if len(self.pending) >= BATCH or self.arena_full():
                     self._flush()
                 self.nfolds += 1
                 return
         elif self.general is None and self.fused_ok and type(arrays) is list and self.fast_host(arrays):
-            self.pending.append((self.put_small(arrays), n, N))      # a small float model's update
+            self.pending.append((self.put_small(arrays), n, N, tag))      # a small float model's update
             if len(self.pending) >= BATCH or self.arena_full():
                 self._flush()
             self.nfolds += 1
             return
         elif self.general is None and self.fused_ok and type(arrays) is StagedModel and arrays.layout is self.layout:
             # staged on arrival in this very layout (the ingest's round end): nothing else to check
-            self.pending.append((self._resident(arrays), n, N))
+            self.pending.append((self._resident(arrays), n, N, tag))
             if len(self.pending) >= BATCH:
                 self._flush()
             self.nfolds += 1
@@ -1094,19 +1201,21 @@ class FedOptPipeline(_Pipeline):
             self.nfolds += 1
             return
         if isinstance(arrays, StagedModel):
-            self.pending.append((self.acquire(arrays), n, N))
+            self.pending.append((self.acquire(arrays), n, N, tag))
             if len(self.pending) >= BATCH:
                 self._flush()
         elif self.batch_host:
             self.layout.check(arrays)
-            self.pending.append((self.put_small(arrays), n, N))
+            self.pending.append((self.put_small(arrays), n, N, tag))
             if len(self.pending) >= BATCH or self.arena_full():
                 self._flush()
         else:
             self._flush()
             slot = self.acquire(arrays)
-            self._fold_pg([(slot, n, N)])
-            slot.consumed.record(self.compute)
+            try:
+                self._fold_pg([(slot, n, N)])   # fails as a whole: the caller skips the update
+            finally:
+                slot.consumed.record(self.compute)
         self.nfolds += 1
 
     def _pg(self, dt):
@@ -1145,24 +1254,56 @@ class FedOptPipeline(_Pipeline):
 
     def _fold_pg(self, entries):
         """Fold ``entries`` into pg (no server step): one launch per group over the entries' device
-        addresses (arena pieces, slots and staged models on this device: no tensor view per update)."""
+        addresses (arena pieces, slots and staged models on this device: no tensor view per update).
+        All-or-nothing: on a failed launch pg is as before the call (copied aside first when the
+        groups' launches continue a started pg) and the FedAggError propagates."""
         span = self._kernel_span()
         ns, Ns = [e[1] for e in entries], [e[2] for e in entries]
         addrs = [_addr(e[0]) for e in entries]
-        for dt in self.layout.groups:
-            old = self._old_dev(dt)
-            off = self.layout.group_byte_offset[dt]
-            ops.fedopt_step_raw(old.data_ptr(), old.dtype, [p + off for p in addrs], ops.torch_dtype(dt), ns, Ns,
-                                old.numel(), first=not self.pg_started, final=False, pg_ptr=self._pg(dt).data_ptr(),
-                                stream=self.compute, device=self.device)
+        snap = None
+        if self.pg_started and len(self.layout.groups) > 1:
+            with torch.cuda.device(self.device), torch.cuda.stream(self.compute):
+                snap = {dt: self._pg(dt).clone() for dt in self.layout.groups}
+        try:
+            for dt in self.layout.groups:
+                old = self._old_dev(dt)
+                off = self.layout.group_byte_offset[dt]
+                ops.fedopt_step_raw(old.data_ptr(), old.dtype, [p + off for p in addrs], ops.torch_dtype(dt), ns, Ns,
+                                    old.numel(), first=not self.pg_started, final=False,
+                                    pg_ptr=self._pg(dt).data_ptr(), stream=self.compute, device=self.device)
+        except ops.FedAggError:
+            if snap is not None:
+                with torch.cuda.device(self.device), torch.cuda.stream(self.compute):
+                    for dt, t in snap.items():
+                        self._pg(dt).copy_(t)
+            raise
         self._end_span(span)
         self.pg_started = True
+
+    def _fold_pg_isolated(self, entries):
+        """Fold a batch into pg; if its launch fails, fold its updates one at a time as FEDn does
+        (fedopt.py:74-106): an update whose own fold fails is skipped and reported with its tag (its
+        examples stay counted), the rest fold in FIFO order."""
+        try:
+            self._fold_pg(entries)
+            return
+        except ops.FedAggError:
+            pass
+        for e in entries:
+            try:
+                self._fold_pg([e])
+            except ops.FedAggError as ex:
+                self.skipped.append((e[3] if len(e) > 3 else None, ex))
 
     def _flush(self):
         if self.pending:
             self.upload_arena()
             entries, self.pending = self.pending, []
-            self._fold_pg(entries)
+            try:
+                self._fold_pg_isolated(entries)
+            except BaseException as e:          # the batch is lost: never return a model without it
+                self.broken = e
+                raise
 
     def _zero_copy_step(self, state, params, opt, sig):
         """A small round that never left the host (see FedAvgPipeline._zero_copy_result): every update
@@ -1207,12 +1348,20 @@ class FedOptPipeline(_Pipeline):
                 np.copyto(view[off:off + arr.size], arr, casting="no")
             self._hold.append(old_h)            # read by the launch until the round's sync
             off = self.layout.group_byte_offset[dt]
-            ops.fedopt_step_raw(ops.host_device_ptr(old_h.data_ptr(), self.device), old_t,
-                                [a.host_dev + e[0]._lo + off for e in entries], ops.torch_dtype(dt), ns, Ns, P,
-                                first=True, final=True, m_in=m_in, m_out=m_out, v_in=v_in, v_out=v_out,
-                                out_ptr=ops.host_device_ptr(out.data_ptr(), self.device), state_dt=sdt,
-                                serveropt=opt, learning_rate=params["learning_rate"], beta1=params["beta1"],
-                                beta2=params["beta2"], tau=params["tau"], stream=self.compute, device=self.device)
+            try:
+                ops.fedopt_step_raw(ops.host_device_ptr(old_h.data_ptr(), self.device), old_t,
+                                    [a.host_dev + e[0]._lo + off for e in entries], ops.torch_dtype(dt), ns, Ns, P,
+                                    first=True, final=True, m_in=m_in, m_out=m_out, v_in=v_in, v_out=v_out,
+                                    out_ptr=ops.host_device_ptr(out.data_ptr(), self.device), state_dt=sdt,
+                                    serveropt=opt, learning_rate=params["learning_rate"], beta1=params["beta1"],
+                                    beta2=params["beta2"], tau=params["tau"], stream=self.compute,
+                                    device=self.device)
+            except ops.FedAggError:
+                # nothing of the session's state was replaced: the round goes the device way (upload,
+                # pseudo-gradient one update at a time if need be, then the server step alone)
+                self.compute.synchronize()
+                self.pending, self._arena = entries, a
+                return None
         self._end_span(span)
         self.pg_started = True
         a.done = torch.cuda.Event()
@@ -1240,6 +1389,7 @@ class FedOptPipeline(_Pipeline):
             model, m, v = self.general.server_step(m, v, params)
             state.set_tensors(m, v)
             return model
+        self._check_broken()
         tic = time.perf_counter()
         model = self._zero_copy_step(state, params, opt, sig)
         if model is not None:
@@ -1250,6 +1400,25 @@ class FedOptPipeline(_Pipeline):
         # step; chunked so that each chunk's D2H of the new model overlaps the next chunk
         self.upload_arena()
         entries, self.pending = self.pending, []
+        if not entries and not self.pg_started:
+            # every update's fold was skipped: no pseudo-gradient (fedopt.py:110, 117-118)
+            raise ValueError("no update was folded into the pseudo-gradient")
+        old_ready = set(self.old_ready)
+        try:
+            return self._fused_step(state, params, opt, sig, entries, tic)
+        except ops.FedAggError:
+            if not entries:
+                raise                           # the server step itself failed (fedopt.py:111-116)
+        # the fused launch failed: the pending updates fold into pg one at a time (a failing one is
+        # skipped), then the server step runs alone (K = 0); its failure is the round's (None, data)
+        self.compute.synchronize()
+        self.copy.synchronize()
+        self.d2h.synchronize()
+        self.old_ready = old_ready              # a global model streamed in part-way is streamed again
+        self._fold_pg_isolated(entries)
+        return self.server_step(state, params)
+
+    def _fused_step(self, state, params, opt, sig, entries, tic):
         first = not self.pg_started
         new_m, new_v, hosts = {}, {}, {}
         span = self._kernel_span()

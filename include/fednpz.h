@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define FNPZ_ABI_VERSION 3
+#define FNPZ_ABI_VERSION 4
 #define FNPZ_MAX_DIMS 16
 
 enum fnpz_status { FNPZ_OK = 0, FNPZ_EFORMAT = 1, FNPZ_ECORRUPT = 2, FNPZ_EINVAL = 3, FNPZ_ENOSPC = 4 };
@@ -95,14 +95,20 @@ int fnpz_stream_next(fnpz_stream* stream, uint8_t* out, int64_t out_cap, int* ev
 /* Host staging (beside the wire format; the aggregators' pack of a decoded update into its pinned
  * staging buffer, fedn_amd/layout.py): dsts[i][0, nbytes[i]) = srcs[i][0, nbytes[i]) for i < n,
  * cut into pieces of at least 1 MiB that up to `threads` threads copy (the calling thread and a
- * pool created once per process: no thread start-up per call). Regions must not overlap. */
-int fnpz_gather(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes, int threads);
+ * pool created once per process: no thread start-up per call). Regions must not overlap.
+ * [dst_lo, dst_lo + dst_len) is the destination buffer the caller allocated (a pinned slot or
+ * arena): every destination segment must lie inside it, else nothing is copied and FNPZ_ENOSPC is
+ * returned (ABI 4) — a caller whose own accounting slipped gets an error, not heap corruption. */
+int fnpz_gather(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes, int threads,
+                const void* dst_lo, int64_t dst_len);
 
 /* The same copies, asynchronously: queued to one background thread (which copies every queued job
- * at once on up to `threads` threads) and returned at once. Returns a ticket > 0, or -status.
+ * at once on up to `threads` threads) and returned at once. Returns a ticket > 0, or -status
+ * (-FNPZ_ENOSPC: a segment outside [dst_lo, dst_lo + dst_len); nothing queued).
  * fnpz_gather_wait(ticket) blocks until that job — and every job submitted before it — is done.
  * The caller keeps the sources and destinations alive until then. */
-int64_t fnpz_gather_start(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes, int threads);
+int64_t fnpz_gather_start(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes, int threads,
+                          const void* dst_lo, int64_t dst_len);
 int fnpz_gather_wait(int64_t ticket);
 
 #ifdef __cplusplus

@@ -256,10 +256,11 @@ def test_async_gather_queue_tickets_and_empty_jobs():
     must not hang the pack), and many small jobs land byte-exact."""
     srcs = [np.arange(i * 1000, i * 1000 + 777 + i, dtype=np.float32) for i in range(50)]
     dsts = [np.zeros_like(s) for s in srcs]
-    t_empty0 = codec.gather_start_raw([], [], [], 4)
+    t_empty0 = codec.gather_start_raw([], [], [], 4, (0, 0))
     codec.gather_wait(t_empty0)
-    tickets = [codec.gather_start_raw([d.ctypes.data], [s.ctypes.data], [s.nbytes], 4) for d, s in zip(dsts, srcs)]
-    t_last = codec.gather_start_raw([], [], [], 4)
+    tickets = [codec.gather_start_raw([d.ctypes.data], [s.ctypes.data], [s.nbytes], 4, (d.ctypes.data, d.nbytes))
+               for d, s in zip(dsts, srcs)]
+    t_last = codec.gather_start_raw([], [], [], 4, (0, 0))
     assert t_last > tickets[-1] > tickets[0] > t_empty0
     codec.gather_wait(t_last)
     for d, s in zip(dsts, srcs):

@@ -37,7 +37,7 @@ def test_admit_packs_like_layout(shapes, dtypes):
     for _ in range(3):
         upd = _model(rng, shapes, dtypes)
         buf = np.full(lay.nbytes, 0xAB, np.uint8)
-        t = admit(upd, buf.ctypes.data)
+        t = admit(upd, buf.ctypes.data, (buf.ctypes.data, buf.nbytes))
         assert t >= 0
         if t:
             wait_pack_jobs(t)
@@ -73,7 +73,7 @@ def test_admit_refuses_other_layouts():
         [m[0].tolist()] + m[1:],                             # not an array
     ]
     for arrays in bad:
-        assert admit(arrays, buf.ctypes.data) == -1
+        assert admit(arrays, buf.ctypes.data, (buf.ctypes.data, buf.nbytes)) == -1
     assert np.array_equal(buf, before)                       # nothing queued, nothing written
 
 
@@ -103,7 +103,7 @@ def test_pack_range_pieces_equal_pack(piece):
     for lo in range(0, lay.nbytes, piece):
         jobs = lay.pack_range(arrays, ptr, lo, min(lay.nbytes, lo + piece))
         assert jobs is not None
-        codec.gather_raw(jobs, 4)
+        codec.gather_raw(jobs, 4, (ptr, got.nbytes))
     for i, off, nb in lay.pack_plan:
         assert np.array_equal(got[off:off + nb], want[off:off + nb]), i
     bad = [np.asfortranarray(arrays[0])] + arrays[1:]
@@ -121,3 +121,58 @@ def test_threaded_cpu_baseline_matches_single_thread():
     out = bench.cpu_threaded(sample, ns, want)
     assert out["same_as_single_threaded"] and out["cores"] >= 1 and out["value"] > 0
     assert 1 <= bench.usable_cores() <= (__import__("os").cpu_count() or 1)
+
+
+def test_admit_refuses_a_pack_past_its_buffer():
+    """The fednpz ABI 4 window: an admission whose destination would run past the pinned buffer it
+    packs into (the class of accounting slip that corrupted the heap in round 3: an arena put one
+    update too far) raises CodecError and writes nothing — past the end, before the start, or one
+    byte short."""
+    from fedn_amd import codec
+    rng = np.random.default_rng(5)
+    m = _model(rng, MNIST, ["f4"] * 6)
+    lay = Layout.of(m)
+    admit = fast_admission(lay)
+    arena = np.full(2 * lay.nbytes + 64, 0x5A, np.uint8)
+    base = arena.ctypes.data
+    window = (base, 2 * lay.nbytes)                            # an arena of two updates
+    t = admit(m, base + lay.nbytes, window)                    # the second slot: fits exactly
+    wait_pack_jobs(t)
+    end = max(off + nb for _, off, nb in lay.pack_plan)       # the last byte a pack writes (+1)
+    for dst, win in ((base + 2 * lay.nbytes, window),          # a third update into a 2-update arena
+                     (base + 2 * lay.nbytes - end + 1, window),   # its last byte one past the arena
+                     (base, (base + 8, 2 * lay.nbytes)),       # before the buffer
+                     (base, (base, end - 1))):                 # one byte short
+        before = arena.copy()
+        with pytest.raises(codec.CodecError, match="outside"):
+            admit(m, dst, win)
+        wait_pack_jobs(codec.gather_start_raw([], [], [], 1, (0, 0)))   # nothing was queued
+        assert np.array_equal(arena, before)
+
+
+def test_gather_raw_and_start_refuse_past_the_window():
+    from fedn_amd import codec
+    src = np.arange(1000, dtype=np.uint8)
+    dst = np.zeros(1000, np.uint8)
+    p = dst.ctypes.data
+    with pytest.raises(codec.CodecError, match="outside"):
+        codec.gather_raw([(p + 1, src.ctypes.data, 1000)], 4, (p, 1000))
+    with pytest.raises(codec.CodecError, match="outside"):
+        codec.gather_start_raw([p - 1], [src.ctypes.data], [10], 4, (p, 1000))
+    with pytest.raises(codec.CodecError, match="window"):
+        codec.gather_raw([(p, src.ctypes.data, 10)], 4, (0, 1000))
+    assert not dst.any()
+    codec.gather_raw([(p, src.ctypes.data, 1000)], 4, (p, 1000))       # exactly the buffer: fine
+    assert np.array_equal(dst, src)
+
+
+def test_start_pack_into_refuses_past_the_window():
+    """The Python-side pack (start_pack_into, the arena's non-fast path) checks the same window."""
+    from fedn_amd import codec
+    lay = Layout.of(_model(np.random.default_rng(6), MNIST, ["f4"] * 6))
+    end = max(off + nb for _, off, nb in lay.pack_plan)
+    buf = np.zeros(end + 3, np.uint8)                      # 4 bytes in, the last tensor's end is 1 byte past
+    with pytest.raises((codec.CodecError, ValueError), match="outside|fit"):
+        L.start_pack_into(lay, _model(np.random.default_rng(7), MNIST, ["f4"] * 6), buf.ctypes.data + 4,
+                          (buf.ctypes.data, buf.nbytes))
+    assert not buf.any()

@@ -1,7 +1,9 @@
 """the kernel path never kills the round. A libfedagg call that fails (nonzero
 status -> FedAggError) is handled by the plug-ins exactly as FEDn handles an update whose fold
 raises: the update is logged and skipped with its examples still counted (fedavg.py:75-78,
-fedopt.py:103-106), and a server step that raises gives ``(None, data)`` (fedopt.py:111-116).
+fedopt.py:103-106) — for batched launches after refolding the batch one update at a time
+(tests/test_gpu_batch_faults.py covers every batching route) — and a server step that raises gives
+``(None, data)`` (fedopt.py:111-116).
 Failures are injected at the C-ABI wrapper (fedn_amd.ops) before anything is enqueued, which
 is where a real status code surfaces; every result is checked against the oracle."""
 import numpy as np
@@ -39,13 +41,33 @@ def _models(rng, K, shapes):
     return base, ups, ns
 
 
-@pytest.mark.parametrize("shapes,fail_call", [([(1000, 1100), (999,)], 2), ([(30, 7), (5,)], 1)],
-                         ids=["large", "small_batched"])
-def test_fedavg_fold_failure_skips_the_update(monkeypatch, shapes, fail_call):
-    """Large host updates fold on arrival (one launch per update): the failing update is skipped and
-    counted. Small ones are batched (one launch per <= 64): a failing batch launch is raised at the
-    round end by ``result()`` and escapes ``combine_models``, as any exception that escapes FEDn's
-    loop aborts the round (roundhandler.py:203-205) — never a silently wrong model."""
+def _poison_update(monkeypatch, n, N):
+    """Every fold launch whose client table holds the update (n, N) raises FedAggError: an update
+    whose fold fails however it is launched (alone, or in a multi-client batch)."""
+    import inspect
+
+    from fedn_amd import _abi, ops
+    for name in ("fedavg_fold_ptrs", "fedavg_fold_raw"):
+        real = getattr(ops, name)
+        sig = inspect.signature(real)
+
+        def wrapper(*a, _real=real, _sig=sig, _name=name, **kw):
+            b = _sig.bind(*a, **kw)
+            if any(float(x) == n and float(y) == N for x, y in zip(b.arguments["n"], b.arguments["N"])):
+                raise _abi.FedAggError(_abi.FA_EHIP, f"{_name}: injected failure")
+            return _real(*a, **kw)
+
+        monkeypatch.setattr(ops, name, wrapper)
+
+
+@pytest.mark.parametrize("shapes", [[(1000, 1100), (999,)], [(30, 7), (5,)]], ids=["large", "small_batched"])
+def test_fedavg_fold_failure_skips_the_update(monkeypatch, shapes):
+    """Update 2's fold fails. Large host updates fold on arrival (one launch per update): the update
+    is skipped right there. Small ones are batched (one zero-copy launch for the round, or one launch
+    per <= 64 updates): the batch's launch fails, its updates are refolded one at a time from their
+    staged copies, and only update 2 — whose own fold fails again — is skipped (fedavg.py:75-78).
+    Either way: logged, uncounted, its examples still in every later running total, the model the
+    oracle's with update 2's fold raising."""
     from fedn_amd.aggregators.fedavg import Aggregator
     from fedn_amd.updatehandler import MemoryUpdateHandler
     rng = np.random.default_rng(51)
@@ -54,14 +76,7 @@ def test_fedavg_fold_failure_skips_the_update(monkeypatch, shapes, fail_call):
     agg = Aggregator(uh, device=DEV)
     for u, n in zip(ups, ns):
         uh.submit(u, n)
-    _failing(monkeypatch, "fedavg_fold_ptrs", lambda i, kw: i == fail_call)   # the pipelines' launch
-    # a small round held in the arena folds zero-copy (staging.ZERO_COPY_BYTES): its one launch fails too
-    _failing(monkeypatch, "fedavg_fold_raw", lambda i, kw: i == fail_call)
-    if shapes[0] == (30, 7):
-        from fedn_amd import _abi
-        with pytest.raises(_abi.FedAggError):
-            agg.combine_models(helper=None)
-        return
+    _poison_update(monkeypatch, float(ns[2]), float(sum(ns[:3])))
     model, data = agg.combine_models(helper=None)
 
     def increment(m1, m2, n, N):                      # the reference fold raising on update 2
@@ -92,10 +107,12 @@ def test_fedopt_server_step_failure_returns_none_and_keeps_state(monkeypatch, sh
     finals = [0]
 
     def fail_on(i, kw):
+        # the server step fails from its at_chunk-th launch on: the fused launch fails, the batch's
+        # updates refold into pg one at a time (no final launch), and the server step alone fails again
         if not kw.get("final") or not fail[0]:
             return False
         finals[0] += 1
-        return finals[0] == at_chunk
+        return finals[0] >= at_chunk
 
     calls = _failing(monkeypatch, "fedopt_step", fail_on)
     for r in range(3):
@@ -136,7 +153,10 @@ def test_fedopt_zero_copy_step_failure_keeps_state(monkeypatch):
     st = ref.FedOptState()
     old = [rng.standard_normal(s).astype(np.float32) for s in shapes]
     fail = [False]
-    calls = _failing(monkeypatch, "fedopt_step_raw", lambda i, kw: fail[0])
+    # the server step fails (the zero-copy FIRST + FINAL launch, then the K = 0 step after the updates
+    # refolded into pg one at a time); the pseudo-gradient folds themselves succeed
+    calls = _failing(monkeypatch, "fedopt_step_raw", lambda i, kw: fail[0] and kw.get("final"))
+    _failing(monkeypatch, "fedopt_step", lambda i, kw: fail[0] and kw.get("final"))
     for r in range(3):
         fail[0] = r == 1
         ups = [[(o + 0.01 * rng.standard_normal(o.shape)).astype(o.dtype) for o in old] for _ in range(3)]
@@ -156,5 +176,5 @@ def test_fedopt_zero_copy_step_failure_keeps_state(monkeypatch):
         assert_lists_identical(agg.m, st.m, f"m r{r}")
         assert_lists_identical(agg.v, st.v, f"v r{r}")
         old = want
-    assert len(calls) == 3                      # every round took the zero-copy step
+    assert sum(1 for kw in calls if kw.get("final")) == 3     # every round took the zero-copy step first
     torch.cuda.synchronize()

@@ -246,7 +246,7 @@ def test_reduce_byte_cap_keeps_order():
     seen = []
 
     class Pipe:
-        def __init__(self, dev, m):
+        def __init__(self, dev, m, batch=True):
             seen.append(("first", int(m[0][0])))
 
         def add(self, m, n, N):
@@ -301,7 +301,7 @@ def test_reduce_admits_by_npz_directory_size():
     import fedn_amd.reduce as red
 
     class Pipe:
-        def __init__(self, dev, m):
+        def __init__(self, dev, m, batch=True):
             pass
 
         def add(self, m, n, N):
