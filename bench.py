@@ -638,8 +638,13 @@ def host_resident_side(a, devs, ns_all, clients=16, sample=1_000_000, rounds=3):
             "devices": len(devs), "GBps_in": nbytes / t / 1e9, "GBps_per_link": nbytes / t / 1e9 / len(devs),
             "rounds_s": times, "bit_exact_on_sample": exact, "sample": f"first {S} params vs oracle/numpy_ref.fedavg_flat",
             "nr_aggregated_models": data.get("nr_aggregated_models"),
-            "note": "FedAvg plug-in over host numpy updates (pack -> pinned -> per-device H2D slice -> fold -> D2H into "
-                    "the host model), median of a session's rounds 2..; PCIe-bound; not in value"}
+            "h2d_path": ("in place: each update's tensors page-locked where they lie (hipHostRegister) and DMA'd "
+                         "slice by slice to every GPU (multidev.INPLACE_MIN_BYTES)" if data.get("bytes_h2d_in_place")
+                         else "packed into pinned slots, then H2D"),
+            "bytes_h2d_in_place": data.get("bytes_h2d_in_place"), "bytes_h2d_packed": data.get("bytes_h2d_packed"),
+            "note": "FedAvg plug-in over host numpy updates (one GPU: pack -> pinned -> H2D; several: page-lock in "
+                    "place -> per-device H2D slice) -> fold -> D2H into the host model, median of a session's rounds "
+                    "2..; PCIe-bound; not in value"}
 
 
 def main():

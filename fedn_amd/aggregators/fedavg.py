@@ -80,6 +80,16 @@ class Aggregator(AggregatorBase):
         self._staging = StagingCache()   # pinned slots, arenas and streams reused by the next round
 
     def combine_models(self, helper=None, delete_models=True, parameters=None):
+        try:
+            return self._combine(helper, delete_models, parameters)
+        finally:
+            # whatever way the round ends, the native gather thread is done with its update arrays
+            # and arenas before they can be freed or reused (staging._Pipeline.quiesce)
+            pipe, self._live = getattr(self, "_live", None), None
+            if pipe is not None and hasattr(pipe, "quiesce"):
+                pipe.quiesce()
+
+    def _combine(self, helper, delete_models, parameters):
         data = {"time_model_load": 0.0, "time_model_aggregation": 0.0}
         model = None
         nr_aggregated_models = 0
@@ -100,6 +110,7 @@ class Aggregator(AggregatorBase):
                     tic = time.time()
                     if nr_aggregated_models == 0:
                         pipe = make_fedavg_pipeline(model_next, self.device, self.devices, helper, self._staging)
+                        self._live = pipe
                     else:
                         pipe.add(model_next, metadata["num_examples"], total_examples, tag=model_update)
                     data["time_model_aggregation"] += time.time() - tic

@@ -81,6 +81,16 @@ class Aggregator(AggregatorBase):
         return None if self.state is None else self.state.v_host()
 
     def combine_models(self, helper=None, delete_models=True, parameters=None):
+        try:
+            return self._combine(helper, delete_models, parameters)
+        finally:
+            # whatever way the round ends, the native gather thread is done with its update arrays
+            # and arenas before they can be freed or reused (staging._Pipeline.quiesce)
+            pipe, self._live = getattr(self, "_live", None), None
+            if pipe is not None and hasattr(pipe, "quiesce"):
+                pipe.quiesce()
+
+    def _combine(self, helper, delete_models, parameters):
         data = {"time_model_load": 0.0, "time_model_aggregation": 0.0}
         try:
             parameters = self._validate_and_merge_parameters(parameters, DEFAULT_PARAMETERS)
@@ -107,6 +117,7 @@ class Aggregator(AggregatorBase):
                     if nr_aggregated_models == 0:
                         model_old = self.update_handler.load_model(helper, model_update.model_id)
                         pipe = self._pipeline(model_old, model_next)
+                        self._live = pipe
                     pipe.add(model_next, metadata["num_examples"], total_examples, tag=model_update)
                     data["time_model_aggregation"] += time.time() - tic
 

@@ -85,8 +85,24 @@ class HbmBudget:
 
     def hold(self, obj, parts):
         """Return the reservation ``parts`` when ``obj`` (a staged update) is garbage collected."""
-        weakref.finalize(obj, self.release, list(parts))
+        fin = weakref.finalize(obj, self.release, list(parts))
+        try:
+            obj.budget_fin = fin      # so that take() can move the reservation to what replaces obj
+        except AttributeError:
+            pass
         return obj
+
+    def take(self, obj):
+        """Move the reservation ``hold`` attached to ``obj`` to the caller (who must ``release`` or
+        ``hold`` it): the parts, or [] if there is none. An update decoded into HBM during its upload
+        hands its reservation to its staged copy this way, instead of both counting against the
+        budget."""
+        fin = getattr(obj, "budget_fin", None)
+        if fin is None:
+            return []
+        det = fin.detach()
+        obj.budget_fin = None
+        return list(det[2][0]) if det is not None else []
 
     def used(self, device):
         with self._lock:

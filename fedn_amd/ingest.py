@@ -398,6 +398,9 @@ class StagingUpdateHandler:
         else:
             _, _, dev_bytes = layout.shard_geometry(len(devs))
             want = list(zip(devs, dev_bytes))
+        self._admit_bytes(want, parts)
+
+    def _admit_bytes(self, want, parts):
         if not self.budget.reserve(want):
             raise _HostSide()
         parts.extend(want)
@@ -410,6 +413,7 @@ class StagingUpdateHandler:
         try:
             staged, metadata = self._stage_device(model_update, parts)
         except _HostSide:
+            self.budget.release(parts)        # a decode's reservation taken over before the refusal
             with self._lock:
                 self.host_side += 1
             return None
@@ -432,9 +436,24 @@ class StagingUpdateHandler:
         decoded = self._decoded_upload(model_update)
         if decoded is not None:
             from .upload import DeviceDecodedUpdate
-            lay = (Layout(decoded.shapes, decoded.dtypes) if isinstance(decoded, DeviceDecodedUpdate)
-                   else Layout.of(decoded.arrays))
-            self._admit(lay, [dev], parts)
+            if isinstance(decoded, DeviceDecodedUpdate):
+                lay = Layout(decoded.shapes, decoded.dtypes)
+                # the decode's own reservation becomes the staged copy's: only the difference (the
+                # layout's alignment padding) is reserved anew, so a decoded update is not counted
+                # twice against the budget while it is copied into the pipelines' layout
+                moved = sum(n for _, n in self.budget.take(decoded))      # reserved on dev by the sink
+                if lay.nbytes > moved:
+                    try:
+                        self._admit_bytes([(dev, lay.nbytes - moved)], [])
+                    except _HostSide:
+                        self.budget.release([(dev, moved)])
+                        raise
+                elif moved > lay.nbytes:
+                    self.budget.release([(dev, moved - lay.nbytes)])
+                parts.append((dev, lay.nbytes))
+            else:
+                lay = Layout.of(decoded.arrays)
+                self._admit(lay, [dev], parts)
             with torch.cuda.device(dev):
                 return stage_decoded(decoded, dev, self._stream()), self._metadata(model_update)
         if self._native():

@@ -277,11 +277,14 @@ class TensorFedOpt:
         else:                                    # fedopt.py:93-94
             self.acc.fold(subs, n, N, plan=fplan)
 
-    def server_step(self, m, v, params):
+    def server_step(self, m, v, params, fp32=False):
         """Apply adam / yogi / adagrad (fedopt.py:139-258) to the pseudo-gradient. ``m``, ``v``:
         the state as per-tensor device tensors or None. Returns (model host arrays, new m, new v).
         Inputs of different broadcastable shapes are broadcast to their common shape first (the
-        state keeps that shape; every value is numpy's)."""
+        state keeps that shape; every value is numpy's). ``fp32``: the fp32-state mode
+        (aggregators.fedopt_f32state): for a tensor whose global model is float32, m, v and the new
+        model are stored in float32 (the f64 step's results rounded once, fa_fedopt_step_ex), as
+        the fused path stores them — the model's dtypes do not change with the round's path."""
         opt = params["serveropt"]
         if opt not in ("adam", "yogi", "adagrad"):
             raise ValueError(f"Unsupported server optimizer: {opt}")
@@ -312,18 +315,21 @@ class TensorFedOpt:
             mdt = None if m is None else m[i].dtype
             if mdt is not None and mdt not in (torch.float16, torch.float32, torch.float64):
                 raise TypeError(f"m dtype {mdt} is not supported")
-            plan.append((B, odt, upd, ops.fedopt_dtypes(upd, odt, mdt)[1]))
+            f32 = fp32 and o.dtype == torch.float32
+            plan.append((B, odt, upd, torch.float32 if f32 else ops.fedopt_dtypes(upd, odt, mdt)[1],
+                         torch.float32 if f32 else torch.float64))
         model, new_m, new_v = [], [], []
         with torch.cuda.device(self.device), torch.cuda.stream(self.stream):
-            for i, (B, odt, upd, m_dt) in enumerate(plan):
+            for i, (B, odt, upd, m_dt, sdt) in enumerate(plan):
                 s = self.stream
                 pb = _as(pg[i], pg[i].dtype, B, s)
                 ob = _as(self.old[i], odt, B, s)
                 mi = None if m is None else _as(m[i], m[i].dtype, B, s)
-                vi = None if v is None else _as(v[i], torch.float64, B, s)
+                vdt = torch.float64 if v is None or v[i].dtype != torch.float32 else torch.float32
+                vi = None if v is None else _as(v[i], vdt, B, s)
                 m_out = torch.empty(B, dtype=m_dt, device=self.device)
-                v_out = torch.empty(B, dtype=torch.float64, device=self.device)
-                out = torch.empty(B, dtype=torch.float64, device=self.device)
+                v_out = torch.empty(B, dtype=sdt, device=self.device)
+                out = torch.empty(B, dtype=sdt, device=self.device)
                 fl = lambda t: None if t is None else t.view(-1)  # noqa: E731
                 ops.fedopt_step(ob.view(-1), [], [], [], first=False, final=True, pg=pb.view(-1), m_in=fl(mi),
                                 m_out=m_out.view(-1), v_in=fl(vi), v_out=v_out.view(-1), out=out.view(-1),

@@ -9,8 +9,11 @@ bit-identical to one device. No xGMI traffic: the consumer of the model is the h
 (roundhandler.py:465-468).
 
 Updates reach the devices two ways:
-* host arrays: packed ONCE into pinned host memory, device d copies only its slice (H2D in
-  parallel across devices), folded on arrival;
+* host arrays: device d copies only its slice (H2D in parallel across devices), folded on
+  arrival. A tensor of at least INPLACE_MIN_BYTES is page-locked where it lies (hipHostRegister,
+  ~330 GB/s on the box) and DMA'd straight from the caller's array; smaller ones are packed once
+  into a pinned slot (~70-110 GB/s, native threads) — the pack of every byte was the bound of a
+  many-GPU round on host updates (tools/pack_probe.py --inplace, profiles/r04_pack_inplace.log);
 * already sliced over these devices by the streaming ingest
   (ingest.StagingUpdateHandler(devices=...) -> ShardedStagedModel): they queue and fold
   together in one multi-client launch per device (flushed at staging.BATCH), and the round's
@@ -27,10 +30,14 @@ import numpy as np
 import torch
 
 from . import mixed, ops
-from .ingest import ShardedStagedModel, StagedModel
+from .ingest import ShardedStagedModel, StagedModel, _member_spans
 from .layout import Layout
 from .staging import (BATCH, HostStreamer, check_fedopt_dtypes, chunks, fused_fedopt_pair, group_tensors, old_members,
                       state_dtypes)
+
+# host tensors at least this large are page-locked in place and DMA'd from where they lie instead of
+# being packed into a pinned slot first (0 disables); smaller ones cost more to register than to copy
+INPLACE_MIN_BYTES = int(__import__("os").environ.get("FEDN_AMD_INPLACE_MIN_BYTES", str(8 << 20)))
 
 
 class _DevSlot:
@@ -136,6 +143,12 @@ class _ShardedStaging:
         self.nslots = nslots
         self.host = None                               # pinned host slots: on the first host update
         self.host_done = [None] * nslots               # per host slot: the H2D events reading it
+        # per host slot: the caller's arrays page-locked in place for its H2D, [(address, array)] —
+        # referenced and registered until those H2D events have fired (then unregistered)
+        self.inplace = [[] for _ in range(nslots)]
+        self._locks = {}                               # address -> [slots using it, registered here]
+        self.inplace_bytes = 0                         # bytes DMA'd from page-locked caller memory
+        self.packed_bytes = 0                          # bytes packed into the pinned slots
         self.dslots = None
         self._next = 0
         self.reserved = set()
@@ -225,6 +238,64 @@ class _ShardedStaging:
                                                  for d in range(len(self.devices))])
         return mixed.upload(_host_arrays(arrays), self.devices[0], self.compute[0])
 
+    def _unlock(self, s):
+        """Release the caller arrays slot ``s``'s last H2D read in place (its events have fired):
+        unregistered when no other slot still uses them and this pipeline registered them."""
+        for ptr, _ in self.inplace[s]:
+            ent = self._locks[ptr]
+            ent[0] -= 1
+            if ent[0] == 0:
+                del self._locks[ptr]
+                if ent[1]:
+                    ops.host_unregister_ptr(ptr)
+        self.inplace[s] = []
+
+    def quiesce(self):
+        """Every host slot's H2D done and its in-place registrations undone (the round is over or
+        abandoned: the caller's arrays may be freed after this)."""
+        for s in range(self.nslots):
+            if self.host_done[s] is not None:
+                for ev in self.host_done[s]:
+                    ev.synchronize()
+            self._unlock(s)
+
+    def __del__(self):
+        try:
+            self.quiesce()                             # a pipeline dropped without its round's end
+        except Exception:  # noqa: BLE001 — interpreter shutdown: the process's pinnings go with it
+            pass
+
+    def _lock_in_place(self, arrays, s):
+        """{tensor index: host address} of the tensors of ``arrays`` DMA'd from where they lie:
+        C-contiguous ndarrays of their layout dtype of at least INPLACE_MIN_BYTES, page-locked here
+        (or already page-locked, e.g. torch pinned blocks); a tensor that cannot be (pages shared
+        with one already registered, ...) is packed instead."""
+        out = {}
+        if INPLACE_MIN_BYTES <= 0:
+            return out
+        for i, _, nb in self.layout.pack_plan:
+            a = arrays[i]
+            if nb < INPLACE_MIN_BYTES or type(a) is not np.ndarray or not a.flags.c_contiguous \
+                    or a.dtype != self.layout.dtypes[i]:
+                continue
+            ptr = a.ctypes.data
+            ent = self._locks.get(ptr)
+            if ent is None:
+                try:                                   # page-locked already (a torch pinned block, or
+                    ops.host_device_ptr(ptr, self.devices[0])     # its owner registered it): use it as is
+                    ent = [0, False]
+                except ops.FedAggError:
+                    try:
+                        ops.host_register_ptr(ptr, nb)
+                        ent = [0, True]
+                    except ops.FedAggError:
+                        continue                       # e.g. pages shared with a registered block: pack it
+                self._locks[ptr] = ent
+            ent[0] += 1                                # the same array handed over twice: registered once
+            self.inplace[s].append((ptr, a))
+            out[i] = ptr
+        return out
+
     def _stage(self, arrays):
         self._ensure_slots()
         for _ in range(self.nslots):
@@ -235,24 +306,45 @@ class _ShardedStaging:
         if self.host_done[s] is not None:
             for ev in self.host_done[s]:
                 ev.synchronize()                       # pinned bytes no longer read by any DMA
-        self.layout.pack(arrays, self.host[s].numpy())
+        self._unlock(s)
+        lay = self.layout
+        inplace = self._lock_in_place(arrays, s)
+        if inplace:                                    # pack only the other tensors
+            host = self.host[s].numpy()
+            for dt in lay.groups:
+                g = lay.group_view(host, dt)
+                for i, off in lay.members[dt]:
+                    if i not in inplace and lay.sizes[i]:
+                        np.copyto(g[off:off + lay.sizes[i]], np.asarray(arrays[i]).reshape(-1), casting="no")
+        else:
+            lay.pack(arrays, self.host[s].numpy())
+        hbase = self.host[s].data_ptr()
         evs = []
         for d, dv in enumerate(self.devices):
             ds = self.dslots[d][s]
             if ds.used:
                 self.copy[d].wait_event(ds.consumed)
             with torch.cuda.device(dv), torch.cuda.stream(self.copy[d]):
-                for dt in self.layout.groups:
+                for dt in lay.groups:
                     lo, hi = self.bounds[dt][d]
-                    if hi > lo:
-                        off = self.layout.group_byte_offset[dt]
-                        src = self.host[s][off + lo * dt.itemsize: off + hi * dt.itemsize]
-                        self._dev_view(d, s, dt).view(torch.uint8).copy_(src, non_blocking=True)
+                    if hi <= lo:
+                        continue
+                    isz, goff = dt.itemsize, lay.group_byte_offset[dt]
+                    dbase = self._dev_view(d, s, dt).data_ptr()
+                    if not inplace:
+                        ops.copy_ptr_async(dbase, hbase + goff + lo * isz, (hi - lo) * isz, self.copy[d], dv)
+                        continue
+                    for i, e0, n, o in _member_spans(lay, dt, lo, hi):
+                        src = inplace[i] + e0 * isz if i in inplace else hbase + goff + (lo + o) * isz
+                        ops.copy_ptr_async(dbase + o * isz, src, n * isz, self.copy[d], dv)
                 ds.h2d_done.record(self.copy[d])
             self.compute[d].wait_event(ds.h2d_done)
             ds.used = True
             evs.append(ds.h2d_done)
         self.host_done[s] = evs
+        nin = sum(lay.sizes[i] * lay.dtypes[i].itemsize for i in inplace)
+        self.inplace_bytes += nin
+        self.packed_bytes += lay.nbytes - nin
         return s
 
     def _to_host_chunks(self, dt, per_dev, fold_chunk, rdtype):
@@ -279,7 +371,7 @@ class _ShardedStaging:
             st.synchronize()
 
     def timings(self):
-        return {}
+        return {"bytes_h2d_in_place": self.inplace_bytes, "bytes_h2d_packed": self.packed_bytes}
 
 
 class ShardedFedAvgPipeline(_ShardedStaging):
@@ -692,7 +784,7 @@ class ShardedFedOptPipeline(_ShardedStaging):
             self._enter_general()               # the state's layout differs from this round's
         if self.general is not None:
             m, v = state.tensors(self.devices[0])
-            model, m, v = self.general.server_step(m, v, params)
+            model, m, v = self.general.server_step(m, v, params, fp32=getattr(state, "fp32", False))
             state.set_tensors(m, v)
             return model
         self._check_broken()

@@ -619,3 +619,13 @@ def host_register(t):
 
 def host_unregister(t):
     _abi.check(_abi.load().fa_host_unregister(t.data_ptr()))
+
+
+def host_register_ptr(ptr, nbytes):
+    """Page-lock ``nbytes`` of host memory at ``ptr`` in place (e.g. a decoded update's numpy array),
+    so DMA reads it directly; undo with :func:`host_unregister_ptr` before the memory is freed."""
+    _abi.check(_abi.load().fa_host_register(int(ptr), int(nbytes)))
+
+
+def host_unregister_ptr(ptr):
+    _abi.check(_abi.load().fa_host_unregister(int(ptr)))

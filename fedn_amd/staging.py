@@ -236,6 +236,7 @@ class _Pipeline:
         self._admit = fast_admission(layout) if self.batch_host and self._plain else None
         self._d2h_on_compute = False             # a small result was copied back on the compute stream
         self._synced = False                     # the result is on the host: every recorded event fired
+        self._kern_wall = 0.0                    # zero-copy rounds: launch-to-sync wall time (no events)
         self._copy_used = False                  # work was enqueued on the copy stream this round
         self._d2h_used = False                   # ... on the d2h stream
         self.streamer = kept["streamer"] if kept else HostStreamer()
@@ -259,9 +260,19 @@ class _Pipeline:
         if self.broken is not None:
             raise RuntimeError(f"a batched fold failed and could not be recovered: {self.broken}") from self.broken
 
+    def quiesce(self):
+        """Wait for the packs still queued to the native gather thread: its copies read the update
+        arrays (kept alive only by ``_pack_jobs``) and write the arenas. A round abandoned between a
+        put and the batch's upload (an exception out of combine_models, a server step refused) must
+        not free either while the thread still copies."""
+        if self._pack_ticket is not None:
+            wait_pack_jobs(self._pack_ticket)
+        self._pack_ticket, self._pack_jobs = None, []
+
     def release(self):
         """Give the staging resources to the cache for the session's next round (call once the
         round's result is on the host; the pipeline stages nothing afterwards)."""
+        self.quiesce()
         if self.cache is not None:
             self.cache.give(self.device, self.layout.nbytes,
                             {"slots": self.slots, "arenas": self._arenas, "streams": (self.copy, self.d2h),
@@ -538,7 +549,7 @@ class _Pipeline:
         if not self._synced:                     # result() synchronised every stream its events are on
             torch.cuda.synchronize(self.device)
         h2d = sum(a.elapsed_time(b) for a, b in self._h2d) / 1e3
-        kern = sum(a.elapsed_time(b) for a, b in self._kern) / 1e3
+        kern = sum(a.elapsed_time(b) for a, b in self._kern) / 1e3 + self._kern_wall
         return {"time_h2d": h2d, "time_kernel": kern, "time_pack": self.time_pack, "time_d2h": self.time_d2h}
 
 
@@ -869,7 +880,7 @@ class FedAvgPipeline(_Pipeline):
         self._pack_ticket, self._pack_jobs = None, []
         self.pending, self._arena = [], None
         ns, Ns = [0.0] + [e[1] for e in entries], [1.0] + [e[2] for e in entries]
-        span = self._kernel_span()
+        t0 = time.perf_counter()                # no event pair: the launch is synchronised right after
         hosts = {}
         try:
             for dt in self.layout.groups:
@@ -889,12 +900,10 @@ class FedAvgPipeline(_Pipeline):
             self.compute.synchronize()
             self.pending, self._arena = entries, a
             return None
-        self._end_span(span)
         self.agg_started = True
-        a.done = torch.cuda.Event()
-        a.done.record(self.compute)             # the arena's pinned bytes are read until here
-        a.used = True
-        self.compute.synchronize()
+        self.compute.synchronize()              # the arena's pinned bytes are read until here: free again
+        a.done, a.used = None, False
+        self._kern_wall += time.perf_counter() - t0
         self._d2h_on_compute = True
         self._synced = not self._d2h_used and not self._copy_used
         out = [None] * len(self.layout.shapes)
@@ -1328,7 +1337,7 @@ class FedOptPipeline(_Pipeline):
         self.pending, self._arena = [], None
         ns, Ns = [e[1] for e in entries], [e[2] for e in entries]
         new_m, new_v, hosts = {}, {}, {}
-        span = self._kernel_span()
+        t0 = time.perf_counter()                # no event pair: the launch is synchronised right after
         for dt in self.layout.groups:
             P = self.layout.group_elems[dt]
             odt, parts = self.old_host[dt]
@@ -1362,12 +1371,10 @@ class FedOptPipeline(_Pipeline):
                 self.compute.synchronize()
                 self.pending, self._arena = entries, a
                 return None
-        self._end_span(span)
         self.pg_started = True
-        a.done = torch.cuda.Event()
-        a.done.record(self.compute)             # the arena's pinned bytes are read until here
-        a.used = True
-        self.compute.synchronize()
+        self.compute.synchronize()              # the arena's pinned bytes are read until here: free again
+        a.done, a.used = None, False
+        self._kern_wall += time.perf_counter() - t0
         self._d2h_on_compute = True
         self._synced = not self._d2h_used and not self._copy_used
         state.m, state.v, state.signature, state.layout = new_m, new_v, sig, self.layout
@@ -1386,7 +1393,7 @@ class FedOptPipeline(_Pipeline):
             self._enter_general()               # the state's layout differs from this round's
         if self.general is not None:
             m, v = state.tensors()
-            model, m, v = self.general.server_step(m, v, params)
+            model, m, v = self.general.server_step(m, v, params, fp32=getattr(state, "fp32", False))
             state.set_tensors(m, v)
             return model
         self._check_broken()

@@ -240,9 +240,10 @@ class DeviceDecodedUpdate:
     """An update decoded during its upload straight into HBM (:class:`DeviceSink`): one
     device block (uint8) per tensor in FEDn's key order, valid once ``ready`` has fired."""
 
-    __slots__ = ("shapes", "dtypes", "blocks", "ready", "device", "nbytes", "__weakref__")
+    __slots__ = ("shapes", "dtypes", "blocks", "ready", "device", "nbytes", "budget_fin", "__weakref__")
 
     def __init__(self, members, ready, device):
+        self.budget_fin = None            # the HBM budget's hold on the decode (budget.HbmBudget.take)
         members = _ordered(members)
         self.shapes = [tuple(shape) for _, _, shape, _ in members]
         self.dtypes = [dtype for _, dtype, _, _ in members]

@@ -27,8 +27,10 @@ int main(void) {
         void* d = dst;
         const void* s = junk;
         int64_t nb = sizeof junk;
-        if (fnpz_gather(1, &d, &s, &nb, 4) != FNPZ_OK || dst[0] != junk[0]) return 7;
-        if (fnpz_gather(1, &d, &s, &nb, 0) != FNPZ_EINVAL) return 8;
+        if (fnpz_gather(1, &d, &s, &nb, 4, dst, sizeof dst) != FNPZ_OK || dst[0] != junk[0]) return 7;
+        if (fnpz_gather(1, &d, &s, &nb, 0, dst, sizeof dst) != FNPZ_EINVAL) return 8;
+        if (fnpz_gather(1, &d, &s, &nb, 4, dst, sizeof dst - 1) != FNPZ_ENOSPC) return 9;
+        if (fnpz_gather_start(1, &d, &s, &nb, 4, dst + 1, sizeof dst) != -FNPZ_ENOSPC) return 10;
     }
     printf("ok %s\n", fnpz_last_error());
     return 0;

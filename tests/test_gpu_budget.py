@@ -160,3 +160,38 @@ def test_budget_streaming_upload_k20():
     st.close()
     gc.collect()
     assert budget.used(DEV) == 0
+
+
+def test_decoded_upload_reservation_moves_to_its_staged_copy():
+    """an update decoded into HBM while it uploaded (DeviceSink, which reserves its payload
+    bytes) hands that reservation to its staged copy instead of both counting against the budget. Under
+    a budget of 1.5 updates every update is staged (none left host-side), one after the other, and the
+    budget holds exactly the staged bytes while they live, nothing once the round is gone."""
+    import gc
+
+    from fedn_amd.updatehandler import MemoryModelService, upload_requests
+    from fedn_amd.upload import StreamingUpload
+    rng = np.random.default_rng(36)
+    base = [rng.standard_normal(s).astype(np.float32) for s in SHAPES]
+    lay = Layout.of(base)
+    budget = HbmBudget(limit=int(1.5 * lay.nbytes))
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=Helper(), device=DEV, workers=1, hbm_budget=budget)
+    svc = StreamingUpload(MemoryModelService(uh.store), st, workers=1, slot=65536, ring=2)
+    ups = []
+    for k in range(3):
+        arrays = [(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base]
+        n = int(rng.integers(1, 5001))
+        svc.Upload(upload_requests(_npz(arrays), f"D{k}", chunk=40_000), None)
+        mu = uh.submit_uploaded(f"D{k}", n, via=st)
+        ups.append((arrays, n))
+        staged, _ = st.load_model_update(mu, Helper())          # waits for its staging
+        assert hasattr(staged, "layout"), "left host-side: the decode's reservation was counted twice"
+        assert budget.used(DEV) == lay.nbytes
+        uh.model_updates.get()                                   # consumed here, not by an aggregator
+        del staged
+        gc.collect()
+        assert budget.used(DEV) == 0
+    svc.close()
+    assert st.host_side == 0 and budget.refused == 0
+    st.close()

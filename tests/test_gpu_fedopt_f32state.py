@@ -128,3 +128,36 @@ def test_f32state_dtype_rules():
         ops.fedopt_step(old, u, [1], [1], first=True, final=True, m_out=f32(), v_out=f32(), out=f64())
     with pytest.raises(TypeError):
         ops.fedopt_step(old.double(), u, [1], [1], first=True, final=True, m_out=f32(), v_out=f64(), out=f64())
+
+
+@pytest.mark.parametrize("opt", ["adam", "yogi"])
+def test_f32state_round_on_the_per_tensor_path_keeps_float32(opt):
+    """a round whose clients differ in dtype (here one float64 client) runs on the per-tensor
+    path (mixed.TensorFedOpt); in the fp32-state mode it must store m, v and the model of float32
+    global tensors in float32 like the fused path — not switch the session to float64 for a round.
+    Three rounds (fused, per-tensor, fused again), bit-exact against the mode's definition."""
+    rng = np.random.default_rng(41)
+    shapes = [(40, 30), (30,), (7,)]
+    base = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    params = {"serveropt": opt, "learning_rate": 1e-2}
+    uh = MemoryUpdateHandler()
+    agg = fedopt_f32state.Aggregator(uh, device=DEV)
+    st = ref.FedOptState()
+    old = base
+    for r in range(3):
+        ups = [([(w + 0.01 * rng.standard_normal(w.shape)).astype(np.float32) for w in old], int(n))
+               for n in rng.integers(1, 5001, 4)]
+        if r == 1:                                       # one client sends its first tensor in float64
+            arrays, n = ups[2]
+            ups[2] = ([arrays[0].astype(np.float64)] + arrays[1:], n)
+        gid = uh.put_global_model(old, f"g{r}")
+        for arrays, n in ups:
+            uh.submit(arrays, n, model_id=gid)
+        model, data = agg.combine_models(helper=None, parameters=params)
+        want, nr = ref.fedopt_combine_f32state(st, ups, old, params)
+        assert data["nr_aggregated_models"] == nr == 4
+        assert all(m.dtype == np.float32 for m in model), [m.dtype for m in model]
+        assert_lists_identical(model, want, f"{opt} round {r} model")
+        assert_lists_identical(agg.m, st.m, f"{opt} round {r} m")
+        assert_lists_identical(agg.v, st.v, f"{opt} round {r} v")
+        old = model

@@ -1,0 +1,90 @@
+"""Host-resident FedAvg rounds through the plug-in on D device entries (one process, multidev.py):
+page-locking each update's tensors in place vs packing them into pinned slots (multidev.
+INPLACE_MIN_BYTES). Same updates, same session shape as bench.py's host_resident
+field; median of rounds 2..; every round bit-exact on a sample against the oracle.
+
+On a one-GPU box the D entries share ONE PCIe link, so the rate there is link-bound whatever the
+host does; what the A/B shows is the host-side cost per update that an N-link node would expose
+(``stage_ms``: the calling thread's time in multidev._stage per update).
+
+    python tools/bench_hostres.py [--devices 1 2 4] [--clients 16] [--params 100000000]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fedn_amd import _abi, multidev  # noqa: E402
+from fedn_amd.aggregators.fedavg import Aggregator  # noqa: E402
+from fedn_amd.updatehandler import MemoryUpdateHandler  # noqa: E402
+from oracle import numpy_ref as ref  # noqa: E402  (the sample checker only)
+
+
+def run(devs, host, ns, rounds, inplace):
+    multidev.INPLACE_MIN_BYTES = (8 << 20) if inplace else 0
+    stage_t = [0.0, 0]
+    real = multidev._ShardedStaging._stage
+
+    def timed(self, arrays):
+        t0 = time.perf_counter()
+        try:
+            return real(self, arrays)
+        finally:
+            stage_t[0] += time.perf_counter() - t0
+            stage_t[1] += 1
+    multidev._ShardedStaging._stage = timed
+    try:
+        uh = MemoryUpdateHandler()
+        agg = Aggregator(uh, devices=list(devs))
+        times, model, data = [], None, None
+        for r in range(rounds + 1):
+            for k, h in enumerate(host):
+                uh.submit([h], ns[k])
+            stage_t[:] = [0.0, 0]
+            t0 = time.perf_counter()
+            model, data = agg.combine_models(helper=None)
+            if r:
+                times.append(time.perf_counter() - t0)
+    finally:
+        multidev._ShardedStaging._stage = real
+    S = 1_000_000
+    want = ref.fedavg_flat([h[:S] for h in host], ns)
+    exact = bool(np.array_equal(model[0][:S].view(np.uint32), want.view(np.uint32)))
+    t = sorted(times)[len(times) // 2]
+    P = host[0].size
+    return {"devices": len(devs), "in_place": inplace, "round_s": round(t, 4),
+            "GBps_in": round(len(host) * P * 4 / t / 1e9, 2), "rounds_s": [round(x, 4) for x in times],
+            "stage_ms_per_update": round(stage_t[0] / max(1, stage_t[1]) * 1e3, 3) if stage_t[1] else None,
+            "bytes_h2d_in_place": data.get("bytes_h2d_in_place"), "bytes_h2d_packed": data.get("bytes_h2d_packed"),
+            "bit_exact_on_sample": exact}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--devices", type=int, nargs="+", default=[2, 4])
+    ap.add_argument("--clients", type=int, default=16)
+    ap.add_argument("--params", type=int, default=100_000_000)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    _abi.load()
+    from fedn_amd import layout
+    layout.MULTIDEV_MIN_BYTES = 0
+    g = torch.Generator(device="cuda:0").manual_seed(11)
+    base = torch.randn(a.params, generator=g, device="cuda:0")
+    host = [torch.randn(a.params, generator=g, device="cuda:0").mul_(0.01).add_(base).cpu().numpy()
+            for _ in range(a.clients)]
+    del base
+    ns = [int(v) for v in np.random.default_rng(0).integers(1, 5001, a.clients)]
+    for D in a.devices:
+        devs = [torch.device("cuda", 0)] * D
+        for inplace in (False, True):
+            print(json.dumps(run(devs, host, ns, a.rounds, inplace)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

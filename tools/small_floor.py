@@ -1,0 +1,124 @@
+"""configs[0]'s K = 2 round against its floor: the mnist-pytorch model (52,650
+params, 6 tensors), two host numpy updates, FedAvg through the plug-in's combine_models — next to
+what the round cannot go below on this box:
+
+  sync_idle        hipStreamSynchronize on an idle stream
+  launch_sync      one 1-element zero-copy fold launch + synchronize (the GPU round trip)
+  fold_zero_copy   the round's own launch: the 3-client fold of 52,650 fp32 params reading the pinned
+                   arena and writing the pinned result over PCIe, + synchronize
+  pack_k2          the two updates' copies into the pinned arena (native gather) + wait
+  plugin           the whole combine_models round (median)
+  fedn_loop        FEDn's own loop restated around the numpy arithmetic (tools/bench_small.py)
+
+and a cProfile of the plug-in's host work. Run on the GPU box: python tools/small_floor.py
+"""
+import cProfile
+import io
+import json
+import os
+import pstats
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fedn_amd import _abi, ops  # noqa: E402
+from fedn_amd.aggregators import get_aggregator  # noqa: E402
+from fedn_amd.updatehandler import MemoryUpdateHandler  # noqa: E402
+from oracle import numpy_ref as ref  # noqa: E402  (the checker only)
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import bench_small  # noqa: E402
+
+MNIST = bench_small.MNIST
+
+
+def med(f, n=400, warm=20):
+    for _ in range(warm):
+        f()
+    ts = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        f()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return round(ts[len(ts) // 2] * 1e6, 2), round(ts[len(ts) // 10] * 1e6, 2)
+
+
+def main():
+    _abi.load()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    st = torch.cuda.current_stream(dev)
+    out = {}
+    out["sync_idle_us"] = med(lambda: st.synchronize())
+    one = torch.ones(64, dtype=torch.float32, pin_memory=True)
+    res = torch.empty(64, dtype=torch.float32, pin_memory=True)
+    p_one = ops.host_device_ptr(one.data_ptr(), dev)
+    p_res = ops.host_device_ptr(res.data_ptr(), dev)
+
+    def launch1():
+        ops.fedavg_fold_raw(p_res, torch.float32, 1, [p_one, p_one], torch.float32, [0.0, 1.0], [1.0, 2.0], True, st, dev)
+        st.synchronize()
+    out["launch_sync_us"] = med(launch1)
+    rng = np.random.default_rng(0)
+    P = sum(int(np.prod(s)) for s in MNIST)
+    arena = torch.empty(3 * P, dtype=torch.float32, pin_memory=True)
+    arena.copy_(torch.from_numpy(rng.standard_normal(3 * P).astype(np.float32)))
+    out_h = torch.empty(P, dtype=torch.float32, pin_memory=True)
+    pa = ops.host_device_ptr(arena.data_ptr(), dev)
+    po = ops.host_device_ptr(out_h.data_ptr(), dev)
+
+    def fold3():
+        ops.fedavg_fold_raw(po, torch.float32, P, [pa, pa + 4 * P, pa + 8 * P], torch.float32, [0.0, 7.0, 9.0],
+                            [1.0, 7.0, 16.0], True, st, dev)
+        st.synchronize()
+    out["fold_zero_copy_us"] = med(fold3)
+    from fedn_amd import codec
+    ups = [rng.standard_normal(P).astype(np.float32) for _ in range(2)]
+    dst = arena.numpy()
+
+    def pack2():
+        t = None
+        for k, u in enumerate(ups):
+            t = codec.gather_start_raw([dst.ctypes.data + (k + 1) * 4 * P], [u.ctypes.data], [4 * P], 8,
+                                       (dst.ctypes.data, dst.nbytes))
+        codec.gather_wait(t)
+    out["pack_k2_us"] = med(pack2)
+
+    base = [rng.standard_normal(s).astype(np.float32) for s in MNIST]
+    cl = [[(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base] for _ in range(2)]
+    ns = [int(v) for v in rng.integers(1, 5001, 2)]
+    uh = MemoryUpdateHandler()
+    agg = get_aggregator("fedavg", uh)
+    box = {}
+
+    def plugin():
+        for u, n in zip(cl, ns):
+            uh.submit(u, n)
+        box["m"], _ = agg.combine_models(helper=None)
+    out["plugin_us"] = med(plugin, n=400)
+    want, _ = ref.fedavg_combine(list(zip(cl, ns)))
+    out["plugin_bit_exact"] = bench_small.same(box["m"], want)
+    uh2 = MemoryUpdateHandler()
+
+    def loop():
+        for u, n in zip(cl, ns):
+            uh2.submit(u, n)
+        bench_small.fedn_loop_fedavg(uh2)
+    out["fedn_loop_us"] = med(loop, n=400)
+    print(json.dumps(out), flush=True)
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(300):
+        plugin()
+    pr.disable()
+    s = io.StringIO()
+    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(30)
+    print(s.getvalue())
+
+
+if __name__ == "__main__":
+    main()
