@@ -26,6 +26,8 @@ model, the pseudo-gradient and the server state m / v resident across rounds
 moves between devices. The global model streams in through a pinned ring (no whole-model
 pinning), chunk by chunk with the server step when every update was device-resident.
 """
+import time
+
 import numpy as np
 import torch
 
@@ -38,6 +40,9 @@ from .staging import (BATCH, HostStreamer, check_fedopt_dtypes, chunks, fused_fe
 # host tensors at least this large are page-locked in place and DMA'd from where they lie instead of
 # being packed into a pinned slot first (0 disables); smaller ones cost more to register than to copy
 INPLACE_MIN_BYTES = int(__import__("os").environ.get("FEDN_AMD_INPLACE_MIN_BYTES", str(8 << 20)))
+# caller arrays kept page-locked (and referenced) after their H2D until the round ends, at most this many
+# bytes: beyond it they are unregistered in one batch (each hipHostUnregister waits for the DMA in flight)
+INPLACE_HOLD_BYTES = int(__import__("os").environ.get("FEDN_AMD_INPLACE_HOLD_BYTES", str(16 << 30)))
 
 
 class _DevSlot:
@@ -146,8 +151,10 @@ class _ShardedStaging:
         # per host slot: the caller's arrays page-locked in place for its H2D, [(address, array)] —
         # referenced and registered until those H2D events have fired (then unregistered)
         self.inplace = [[] for _ in range(nslots)]
-        self._locks = {}                               # address -> [slots using it, registered here]
+        self._locks = {}                               # address -> [slots using it, registered here, array, bytes]
+        self._retired, self._retired_bytes = [], 0     # registered here, no longer read: [(address, array)]
         self.inplace_bytes = 0                         # bytes DMA'd from page-locked caller memory
+        self.time_stage_wait = self.time_stage_host = 0.0
         self.packed_bytes = 0                          # bytes packed into the pinned slots
         self.dslots = None
         self._next = 0
@@ -239,25 +246,39 @@ class _ShardedStaging:
         return mixed.upload(_host_arrays(arrays), self.devices[0], self.compute[0])
 
     def _unlock(self, s):
-        """Release the caller arrays slot ``s``'s last H2D read in place (its events have fired):
-        unregistered when no other slot still uses them and this pipeline registered them."""
+        """Release the caller arrays slot ``s``'s last H2D read in place (its events have fired). One no
+        other slot still uses, and that this pipeline registered, is retired: kept page-locked (and
+        referenced) until the round ends — hipHostUnregister waits for every DMA in flight on the
+        device (7 ms with one 400 MB H2D queued, profiles/r04_pack_inplace.log), so unregistering
+        mid-round would stall the pipeline once per update. Past INPLACE_HOLD_BYTES retired bytes they
+        are unregistered together (one stall per batch) so the host memory held stays bounded."""
         for ptr, _ in self.inplace[s]:
             ent = self._locks[ptr]
             ent[0] -= 1
             if ent[0] == 0:
                 del self._locks[ptr]
                 if ent[1]:
-                    ops.host_unregister_ptr(ptr)
+                    self._retired.append((ptr, ent[2]))
+                    self._retired_bytes += ent[3]
         self.inplace[s] = []
+        if self._retired_bytes > INPLACE_HOLD_BYTES:
+            self._unregister_retired()
+
+    def _unregister_retired(self):
+        for ptr, _ in self._retired:
+            ops.host_unregister_ptr(ptr)
+        self._retired, self._retired_bytes = [], 0
 
     def quiesce(self):
         """Every host slot's H2D done and its in-place registrations undone (the round is over or
-        abandoned: the caller's arrays may be freed after this)."""
+        abandoned: the caller's arrays may be freed after this; the device is idle, so each
+        unregistration is cheap)."""
         for s in range(self.nslots):
             if self.host_done[s] is not None:
                 for ev in self.host_done[s]:
                     ev.synchronize()
             self._unlock(s)
+        self._unregister_retired()
 
     def __del__(self):
         try:
@@ -281,13 +302,13 @@ class _ShardedStaging:
             ptr = a.ctypes.data
             ent = self._locks.get(ptr)
             if ent is None:
-                try:                                   # page-locked already (a torch pinned block, or
-                    ops.host_device_ptr(ptr, self.devices[0])     # its owner registered it): use it as is
-                    ent = [0, False]
+                try:                                   # page-locked already (a torch pinned block, its owner
+                    ops.host_device_ptr(ptr, self.devices[0])     # registered it, or retired here): as is
+                    ent = [0, False, a, nb]
                 except ops.FedAggError:
                     try:
                         ops.host_register_ptr(ptr, nb)
-                        ent = [0, True]
+                        ent = [0, True, a, nb]
                     except ops.FedAggError:
                         continue                       # e.g. pages shared with a registered block: pack it
                 self._locks[ptr] = ent
@@ -303,9 +324,12 @@ class _ShardedStaging:
             self._next = (self._next + 1) % self.nslots
             if s not in self.reserved:
                 break
+        t0 = time.perf_counter()
         if self.host_done[s] is not None:
             for ev in self.host_done[s]:
                 ev.synchronize()                       # pinned bytes no longer read by any DMA
+        t1 = time.perf_counter()
+        self.time_stage_wait += t1 - t0                # backpressure of the links (slot ring full)
         self._unlock(s)
         lay = self.layout
         inplace = self._lock_in_place(arrays, s)
@@ -345,6 +369,7 @@ class _ShardedStaging:
         nin = sum(lay.sizes[i] * lay.dtypes[i].itemsize for i in inplace)
         self.inplace_bytes += nin
         self.packed_bytes += lay.nbytes - nin
+        self.time_stage_host += time.perf_counter() - t1   # page-lock / pack + enqueue: the host's own work
         return s
 
     def _to_host_chunks(self, dt, per_dev, fold_chunk, rdtype):
@@ -371,7 +396,8 @@ class _ShardedStaging:
             st.synchronize()
 
     def timings(self):
-        return {"bytes_h2d_in_place": self.inplace_bytes, "bytes_h2d_packed": self.packed_bytes}
+        return {"bytes_h2d_in_place": self.inplace_bytes, "bytes_h2d_packed": self.packed_bytes,
+                "time_stage_host": self.time_stage_host, "time_stage_wait": self.time_stage_wait}
 
 
 class ShardedFedAvgPipeline(_ShardedStaging):

@@ -25,7 +25,7 @@ from fedn_amd.updatehandler import MemoryUpdateHandler  # noqa: E402
 from oracle import numpy_ref as ref  # noqa: E402  (the sample checker only)
 
 
-def run(devs, host, ns, rounds, inplace):
+def run(devs, host, ns, rounds, inplace, fresh=False):
     multidev.INPLACE_MIN_BYTES = (8 << 20) if inplace else 0
     stage_t = [0.0, 0]
     real = multidev._ShardedStaging._stage
@@ -43,8 +43,12 @@ def run(devs, host, ns, rounds, inplace):
         agg = Aggregator(uh, devices=list(devs))
         times, model, data = [], None, None
         for r in range(rounds + 1):
-            for k, h in enumerate(host):
+            # fresh: every round's updates are new arrays (as FEDn decodes them anew each round), so each
+            # is page-locked for the first time; else the same arrays come back every round
+            ups = [h.copy() for h in host] if fresh else host
+            for k, h in enumerate(ups):
                 uh.submit([h], ns[k])
+            del ups
             stage_t[:] = [0.0, 0]
             t0 = time.perf_counter()
             model, data = agg.combine_models(helper=None)
@@ -57,9 +61,11 @@ def run(devs, host, ns, rounds, inplace):
     exact = bool(np.array_equal(model[0][:S].view(np.uint32), want.view(np.uint32)))
     t = sorted(times)[len(times) // 2]
     P = host[0].size
-    return {"devices": len(devs), "in_place": inplace, "round_s": round(t, 4),
+    return {"devices": len(devs), "in_place": inplace, "fresh_arrays": fresh, "round_s": round(t, 4),
             "GBps_in": round(len(host) * P * 4 / t / 1e9, 2), "rounds_s": [round(x, 4) for x in times],
             "stage_ms_per_update": round(stage_t[0] / max(1, stage_t[1]) * 1e3, 3) if stage_t[1] else None,
+            "stage_host_ms_per_update": round(data.get("time_stage_host", 0.0) / max(1, stage_t[1]) * 1e3, 3),
+            "stage_wait_ms_per_update": round(data.get("time_stage_wait", 0.0) / max(1, stage_t[1]) * 1e3, 3),
             "bytes_h2d_in_place": data.get("bytes_h2d_in_place"), "bytes_h2d_packed": data.get("bytes_h2d_packed"),
             "bit_exact_on_sample": exact}
 
@@ -82,8 +88,8 @@ def main():
     ns = [int(v) for v in np.random.default_rng(0).integers(1, 5001, a.clients)]
     for D in a.devices:
         devs = [torch.device("cuda", 0)] * D
-        for inplace in (False, True):
-            print(json.dumps(run(devs, host, ns, a.rounds, inplace)), flush=True)
+        for inplace, fresh in ((False, False), (True, False), (True, True)):
+            print(json.dumps(run(devs, host, ns, a.rounds, inplace, fresh)), flush=True)
 
 
 if __name__ == "__main__":

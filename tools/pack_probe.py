@@ -119,8 +119,47 @@ def inplace(P=100_000_000, updates=6, threads=24):
     print(json.dumps({"inplace_update_bytes": P * 4, "pack_threads": threads, **res}), flush=True)
 
 
+def busy(P=100_000_000, reps=4):
+    """hipHostRegister / hipHostUnregister of one 400 MB update while the copy engines are busy with
+    another update's H2D (what a pipelined round does): whether either call waits for the DMA."""
+    rng = np.random.default_rng(2)
+    dev = torch.empty(P * 4, dtype=torch.uint8, device="cuda:0")
+    side = torch.empty(P * 4, dtype=torch.uint8, pin_memory=True)
+    cs = torch.cuda.Stream()
+    arrs = [rng.standard_normal(P, dtype=np.float32) for _ in range(2)]
+    res = {"register_idle_ms": [], "register_busy_ms": [], "unregister_idle_ms": [], "unregister_busy_ms": [],
+           "h2d_ms": []}
+    for _ in range(reps):
+        for busy_ in (False, True):
+            a = arrs[0]
+            if busy_:
+                with torch.cuda.stream(cs):
+                    dev.copy_(side, non_blocking=True)          # ~7 ms of DMA in flight
+            t0 = time.perf_counter()
+            ops.host_register_ptr(a.ctypes.data, a.nbytes)
+            res["register_busy_ms" if busy_ else "register_idle_ms"].append((time.perf_counter() - t0) * 1e3)
+            cs.synchronize()
+            if busy_:
+                with torch.cuda.stream(cs):
+                    dev.copy_(side, non_blocking=True)
+            t0 = time.perf_counter()
+            ops.host_unregister_ptr(a.ctypes.data)
+            res["unregister_busy_ms" if busy_ else "unregister_idle_ms"].append((time.perf_counter() - t0) * 1e3)
+            cs.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(cs):
+            dev.copy_(side, non_blocking=True)
+        cs.synchronize()
+        res["h2d_ms"].append((time.perf_counter() - t0) * 1e3)
+    print(json.dumps({"busy_probe_bytes": P * 4, **{k: round(float(np.median(v)), 3) for k, v in res.items()}}),
+          flush=True)
+
+
 if __name__ == "__main__":
-    if "--inplace" in sys.argv:
+    if "--busy" in sys.argv:
+        _abi.load()
+        busy()
+    elif "--inplace" in sys.argv:
         _abi.load()
         inplace()
     else:

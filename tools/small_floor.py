@@ -63,6 +63,14 @@ def main():
         ops.fedavg_fold_raw(p_res, torch.float32, 1, [p_one, p_one], torch.float32, [0.0, 1.0], [1.0, 2.0], True, st, dev)
         st.synchronize()
     out["launch_sync_us"] = med(launch1)
+    ev = torch.cuda.Event()
+
+    def launch1_spin():
+        ops.fedavg_fold_raw(p_res, torch.float32, 1, [p_one, p_one], torch.float32, [0.0, 1.0], [1.0, 2.0], True, st, dev)
+        ev.record(st)
+        while not ev.query():
+            pass
+    out["launch_spin_us"] = med(launch1_spin)
     rng = np.random.default_rng(0)
     P = sum(int(np.prod(s)) for s in MNIST)
     arena = torch.empty(3 * P, dtype=torch.float32, pin_memory=True)
@@ -76,6 +84,14 @@ def main():
                             [1.0, 7.0, 16.0], True, st, dev)
         st.synchronize()
     out["fold_zero_copy_us"] = med(fold3)
+
+    def fold3_spin():
+        ops.fedavg_fold_raw(po, torch.float32, P, [pa, pa + 4 * P, pa + 8 * P], torch.float32, [0.0, 7.0, 9.0],
+                            [1.0, 7.0, 16.0], True, st, dev)
+        ev.record(st)
+        while not ev.query():
+            pass
+    out["fold_zero_copy_spin_us"] = med(fold3_spin)
     from fedn_amd import codec
     ups = [rng.standard_normal(P).astype(np.float32) for _ in range(2)]
     dst = arena.numpy()
