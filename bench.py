@@ -769,14 +769,31 @@ def main():
             torch.cuda.empty_cache()
             # a transport whose gathered model differs from another's (same geometry, same data) or
             # between ranks is not used: every rank computes the same verdict from all-reduced sums
-            bad = set()
+            bad = {}
             for (name, R), (lo, hi) in sums.items():
                 ref_sum = sums.get(("collective", R))
                 if lo != hi or (ref_sum is not None and ref_sum != (lo, hi)):
-                    bad.add(name)
+                    bad[name] = "gathered model differs between ranks or from the RCCL all-gather's on the same data"
+            # a release grid after peer stores that missed an XCD (sharded.P2PAllGather.check_release):
+            # the kernel engines' stores may not have been visible — not used (every rank reads its own
+            # records, so the verdict is all-reduced: MAX of the miss flag)
+            p2p_objs = {id(t): t for t in transports.values() if t is not None}
+            if p2p_objs:
+                miss = 0
+                for t in p2p_objs.values():
+                    try:
+                        t.check_release()
+                    except Exception:  # noqa: BLE001
+                        miss = 1
+                flag = torch.tensor([miss], dtype=torch.int32, device="cpu" if rehearsal else device)
+                if dist.is_initialized():
+                    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+                if int(flag[0]):
+                    for name in ("p2p_kernel", "p2p_fused"):
+                        if name in transports:
+                            bad[name] = "a release grid after its peer stores did not cover every XCD"
             if bad:
-                extra["transport_disqualified"] = {n: "gathered model differs between ranks or from the RCCL "
-                                                      "all-gather's on the same data" for n in sorted(bad)}
+                extra["transport_disqualified"] = dict(sorted(bad.items()))
                 tuned = {k: v for k, v in tuned.items() if k.split("/R")[0] not in bad}
             best = min(tuned, key=tuned.get)
             tname, R = best.split("/R")[0], int(best.split("/R")[1])
@@ -786,7 +803,7 @@ def main():
         for name in list(transports):
             other = transports[name]
             if name != tname and other is not None and other is not tp:
-                transports.pop(name).close()
+                transports.pop(name).close(check=False)    # its release records were read in the warm-up
         cyc = geoms[R]
         L = cyc.local_len
         P = L
@@ -853,7 +870,7 @@ def main():
             extra.update(multi_gpu_side(a, world, rank, device, rehearsal, ns, Ns, K, P_total, agg, ups_local, stream,
                                         rccl1, cyc, host_sample))
         if tp is not None:
-            tp.close()
+            tp.close(check=False)          # the release records are already in the line (release_check)
         if rccl1:
             extra["rccl_world1"] = ("rehearsal: the N>1 path at world size 1 over RCCL (all-gathers issued as "
                                     "collectives); not a reported number")

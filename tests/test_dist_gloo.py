@@ -234,3 +234,51 @@ def test_collective_at_world1_gloo():
     want = ref.fedavg_flat(ups, ns)
     for got in (r_off, r_on, r_sh):
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def _hostgather_worker(rank, world, port, P, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fedn_amd.sharded import HostGather
+        sh = ShardedFedAvg(P, fold_fn=lambda *a: None)
+        out = []
+        for step, dt in enumerate((torch.float32, torch.float32, torch.float64, torch.float32)):
+            full = torch.arange(P, dtype=dt) * (step + 1)
+            got = sh.gather_to_host(sh.local(full).clone(), dst=0)     # cached per (dst, dtype)
+            if rank == 0:
+                out.append((str(dt), np.array_equal(got.numpy(), full.numpy()), got.dtype == dt))
+            else:
+                out.append(got is None)
+        hg = HostGather(P, torch.float32, sh.bounds)
+        try:
+            hg.gather(torch.zeros(sh.hi - sh.lo, dtype=torch.float64))
+            out.append("no error")
+        except TypeError:
+            out.append("TypeError")
+        dist.barrier()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_host_gather_dtype_cache_and_entry_barrier():
+    """the shared host model is cached per (destination rank, dtype) — a float64 gather after
+    float32 ones gets its own buffer, and the float32 one after it is right again — and a slice of the
+    wrong dtype raises instead of copying half its bytes; back-to-back gathers (each entered through a
+    barrier) return the newest model on rank 0."""
+    world, P = 3, 10_007
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pc = mp.start_processes(_hostgather_worker, args=(world, _free_port(), P, q), nprocs=world, join=False,
+                            start_method="spawn")
+    res = dict(q.get(timeout=120) for _ in range(world))
+    while not pc.join(timeout=60):
+        pass
+    for dt, same, dtype_ok in res[0][:4]:
+        assert same and dtype_ok, dt
+    for r in (1, 2):
+        assert res[r][:4] == [True] * 4
+    assert all(res[r][4] == "TypeError" for r in range(world))
