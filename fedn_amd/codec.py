@@ -191,14 +191,18 @@ def _ordered(ents):
     return [by_name[str(i)] for i in range(len(ents))]
 
 
-def load_npz(buf, threads=None):
-    """Decode an npz archive to the list numpyhelper.Helper.load returns (new arrays)."""
+def load_npz(buf, threads=None, alloc=None):
+    """Decode an npz archive to the list numpyhelper.Helper.load returns (new arrays).
+
+    ``alloc(shape, dtype, order)``, when given, returns the array a member is decoded into (e.g. in
+    page-locked memory, helper.pinned_empty) or None for a plain np.empty."""
     a, ents = open_archive(buf)
     ents = _ordered(ents)
     outs = []
     for e in ents:
-        dt = _dtype(e)
-        outs.append(np.empty(_shape(e), dtype=dt, order="F" if e.fortran_order else "C"))
+        dt, shape, order = _dtype(e), _shape(e), "F" if e.fortran_order else "C"
+        o = alloc(shape, dt, order) if alloc is not None else None
+        outs.append(np.empty(shape, dtype=dt, order=order) if o is None else o)
     read_entries(a, ents, [o.reshape(-1, order="A").view(np.uint8) if o.size else o.view(np.uint8).reshape(-1)
                            for o in outs], threads)
     return outs

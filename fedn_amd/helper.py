@@ -6,7 +6,8 @@ FEDn's ``HelperBase`` requires (helperbase.py:4-40) plus its file-type API:
   save(weights, path=None, file_type="npz")   numpyhelper.py:144-169: block-parallel deflate,
                                               output readable by np.load
   load(path, file_type="npz")                 numpyhelper.py:171-189: native inflate (parallel
-                                              for archives this codec wrote); raw_binary as FEDn
+                                              for archives this codec wrote), members of 8 MiB+
+                                              into pinned memory on a GPU host; raw_binary as FEDn
   add / subtract / multiply / divide / sqrt / sign / ones
                                               numpyhelper.py:34-142 on the GPU (fa_elementwise),
                                               numpy's dtype promotion and rounding, so FEDn's
@@ -25,6 +26,31 @@ from io import BytesIO
 import numpy as np
 
 from . import codec
+
+
+# npz members at least this large are decoded into page-locked host memory when a GPU is present
+# (0 disables): the multi-device aggregation pipeline DMAs such a tensor straight from where it lies
+# instead of packing it into a pinned slot first (multidev.INPLACE_MIN_BYTES). The blocks come from
+# torch's caching host allocator, so a session's rounds reuse them without pinning pages again.
+DECODE_PINNED_MIN_BYTES = int(os.environ.get("FEDN_AMD_DECODE_PINNED_MIN_BYTES", str(8 << 20)))
+_pinned_ok = None
+
+
+def pinned_empty(shape, dtype, order="C"):
+    """An uninitialised C-ordered array in page-locked host memory (None: no GPU, a Fortran-ordered
+    or small member — the caller allocates it as usual). The array keeps its pinned block alive."""
+    global _pinned_ok
+    dtype = np.dtype(dtype)
+    nbytes = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+    if order != "C" or DECODE_PINNED_MIN_BYTES <= 0 or nbytes < DECODE_PINNED_MIN_BYTES:
+        return None
+    import torch
+    if _pinned_ok is None:
+        _pinned_ok = torch.cuda.is_available()
+    if not _pinned_ok:
+        return None
+    blk = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    return blk.numpy().view(dtype).reshape(shape)
 
 
 def _device():
@@ -307,13 +333,13 @@ class Helper:
         self.check_supported_file_type(file_type)
         if file_type == "npz":
             if isinstance(path, (bytes, bytearray, memoryview)):
-                return codec.load_npz(path)
+                return codec.load_npz(path, alloc=pinned_empty)
             if hasattr(path, "getbuffer"):
-                return codec.load_npz(path.getbuffer())
+                return codec.load_npz(path.getbuffer(), alloc=pinned_empty)
             if hasattr(path, "read"):
-                return codec.load_npz(path.read())
+                return codec.load_npz(path.read(), alloc=pinned_empty)
             with open(path, "rb") as f:
-                return codec.load_npz(np.fromfile(f, dtype=np.uint8))
+                return codec.load_npz(np.fromfile(f, dtype=np.uint8), alloc=pinned_empty)
         if isinstance(path, BytesIO):
             return [np.frombuffer(path.read(), dtype=np.float64)]
         return [np.fromfile(path, dtype=np.float64)]

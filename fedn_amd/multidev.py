@@ -10,10 +10,11 @@ bit-identical to one device. No xGMI traffic: the consumer of the model is the h
 
 Updates reach the devices two ways:
 * host arrays: device d copies only its slice (H2D in parallel across devices), folded on
-  arrival. A tensor of at least INPLACE_MIN_BYTES is page-locked where it lies (hipHostRegister,
-  ~330 GB/s on the box) and DMA'd straight from the caller's array; smaller ones are packed once
-  into a pinned slot (~70-110 GB/s, native threads) — the pack of every byte was the bound of a
-  many-GPU round on host updates (tools/pack_probe.py --inplace, profiles/r04_pack_inplace.log);
+  arrival. A tensor of at least INPLACE_MIN_BYTES that lies in page-locked memory already (how
+  fedn_amd.helper decodes large npz members) is DMA'd straight from the caller's array; the others
+  are packed once into a pinned slot (~70-110 GB/s, native threads) — the pack of every byte bounds
+  a many-GPU round on pageable host updates (tools/pack_probe.py, tools/bench_hostres.py,
+  profiles/r04_hostres.log; page-locking pageable updates in place instead is INPLACE_REGISTER);
 * already sliced over these devices by the streaming ingest
   (ingest.StagingUpdateHandler(devices=...) -> ShardedStagedModel): they queue and fold
   together in one multi-client launch per device (flushed at staging.BATCH), and the round's
@@ -37,9 +38,15 @@ from .layout import Layout
 from .staging import (BATCH, HostStreamer, check_fedopt_dtypes, chunks, fused_fedopt_pair, group_tensors, old_members,
                       state_dtypes)
 
-# host tensors at least this large are page-locked in place and DMA'd from where they lie instead of
-# being packed into a pinned slot first (0 disables); smaller ones cost more to register than to copy
+# host tensors at least this large that are page-locked already (pinned memory: e.g. what
+# fedn_amd.helper decodes large npz members into) are DMA'd slice by slice straight from where they lie
+# instead of being packed into a pinned slot first (0 disables)
 INPLACE_MIN_BYTES = int(__import__("os").environ.get("FEDN_AMD_INPLACE_MIN_BYTES", str(8 << 20)))
+# page-lock PAGEABLE tensors in place too (hipHostRegister) — only worth it for host buffers a caller
+# reuses round after round: re-registering pages costs ~0.1 ms per 400 MB, but pinning fresh pages
+# ~1 ms and unpinning them (hipHostUnregister) ~13 ms per 400 MB, more than the ~4-6 ms pack
+# (profiles/r04_hostres.log); FEDn decodes every round's updates into new arrays, so off by default
+INPLACE_REGISTER = __import__("os").environ.get("FEDN_AMD_INPLACE_REGISTER", "0") == "1"
 # caller arrays kept page-locked (and referenced) after their H2D until the round ends, at most this many
 # bytes: beyond it they are unregistered in one batch (each hipHostUnregister waits for the DMA in flight)
 INPLACE_HOLD_BYTES = int(__import__("os").environ.get("FEDN_AMD_INPLACE_HOLD_BYTES", str(16 << 30)))
@@ -306,6 +313,8 @@ class _ShardedStaging:
                     ops.host_device_ptr(ptr, self.devices[0])     # registered it, or retired here): as is
                     ent = [0, False, a, nb]
                 except ops.FedAggError:
+                    if not INPLACE_REGISTER:
+                        continue                       # pageable: packing it is cheaper (see INPLACE_REGISTER)
                     try:
                         ops.host_register_ptr(ptr, nb)
                         ent = [0, True, a, nb]
