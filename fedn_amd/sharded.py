@@ -87,6 +87,19 @@ class ShardedFedAvg:
         return gather.gather(agg_local)
 
 
+def _agree(failed, group=None, device=None):
+    """Whether ANY rank of ``group`` failed (``failed`` is this rank's verdict): a one-element MAX
+    all-reduce every rank takes part in — where a barrier would stand — so a step that fails on one
+    rank only fails on every rank at the same point, and no rank is left waiting in a collective the
+    failed one never reaches. On device ``device`` under RCCL, on the CPU under gloo."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return bool(failed)
+    dev = device if (device is not None and dist.get_backend(group) == "nccl") else "cpu"
+    flag = torch.tensor([1 if failed else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    return bool(int(flag[0]))
+
+
 def _cached_gather(owner, dtype, dst, bounds):
     """``owner``'s HostGather for (dst, dtype) — made on first use, replaced (and the old one closed)
     when a later gather asks for another destination rank or dtype. Every rank of the group makes the
@@ -360,26 +373,40 @@ class P2PAllGather:
         if spare is not None and (spare.numel() != full.numel() or spare.dtype != full.dtype or
                                   spare.device != full.device):
             raise ValueError("P2PAllGather: the spare buffer must match the first")
-        mine = [ops.ipc_handle(b) + (b.numel(), str(b.dtype)) for b in self.bufs]
+        # every rank reaches the handle exchange, and every rank sees every rank's export failure
+        # (the same exception everywhere: a caller falls back together, bench.py to the collective)
+        try:
+            mine = [ops.ipc_handle(b) + (b.numel(), str(b.dtype)) for b in self.bufs]
+        except Exception as e:  # noqa: BLE001 — exchanged, then raised on every rank
+            mine = f"{type(e).__name__}: {e}"
         objs = [None] * self.world
         if self.world > 1:
             dist.all_gather_object(objs, mine, group=group)
         else:
             objs = [mine]
+        bad = [(r, o) for r, o in enumerate(objs) if isinstance(o, str)]
+        if bad:
+            raise RuntimeError(f"P2PAllGather: rank {bad[0][0]} could not export its buffers ({bad[0][1]})")
         for r, lst in enumerate(objs):
             if len(lst) != len(self.bufs) or any(n != full.numel() or dt != str(full.dtype) for _, _, n, dt in lst):
                 raise ValueError(f"P2PAllGather: rank {r} buffers {[(n, dt) for _, _, n, dt in lst]}, this rank's "
                                  f"{len(self.bufs)} x {full.numel()} x {full.dtype}")
         self.peers = {}                            # rank -> [(base, pointer) per buffer]
+        err = None
         try:
             for r, lst in enumerate(objs):
                 if r != self.rank:
                     self.peers[r] = []
                     for h, o, _, _ in lst:
                         self.peers[r].append(ops.ipc_open(h, o, self.device))
-        except Exception:
+        except Exception as e:  # noqa: BLE001 — agreed on below
+            err = e
+        # one rank that cannot map a peer fails the transport on every rank
+        if _agree(err is not None, group, self.device):
             self.close(fence=False)
-            raise
+            if err is not None:
+                raise err
+            raise RuntimeError("P2PAllGather: another rank could not map its peers' buffers")
         self.streams = {r: torch.cuda.Stream(self.device) for r in self.peers}
         self.push_stream = torch.cuda.Stream(self.device)       # the "kernel" engine's launches
         self.nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
@@ -569,21 +596,34 @@ class HostGather:
             # into the shared model before then
             dist.barrier(group=self.group)
         es = self.host.element_size()
-        if local.device.type == "cuda" and pieces:
-            self._pin(local.device)
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(local.device))
-            self._stream.wait_event(ev)
+        err = None
+        try:
             for lo, hi, l0 in pieces:
                 if l0 + hi - lo > local.numel() or hi > self.P:
                     raise ValueError("HostGather.gather: piece outside the local buffer or the model")
-                ops.copy_async(self.host.data_ptr() + lo * es, local[l0:], (hi - lo) * es, self._stream)
-            self._stream.synchronize()
-        else:
-            for lo, hi, l0 in pieces:
-                self.host[lo:hi].copy_(local[l0:l0 + hi - lo])
+            if local.device.type == "cuda" and pieces:
+                self._pin(local.device)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(local.device))
+                self._stream.wait_event(ev)
+                for lo, hi, l0 in pieces:
+                    ops.copy_async(self.host.data_ptr() + lo * es, local[l0:], (hi - lo) * es, self._stream)
+                self._stream.synchronize()
+            else:
+                for lo, hi, l0 in pieces:
+                    self.host[lo:hi].copy_(local[l0:l0 + hi - lo])
+        except Exception as e:  # noqa: BLE001 — agreed on below
+            err = e
+        # the exit barrier, as an agreement: a rank whose copy failed fails the gather on every rank
+        # (the host model is incomplete) instead of leaving the others waiting
         if self.world > 1:
-            dist.barrier(group=self.group)
+            failed = _agree(err is not None, self.group, local.device if local.device.type == "cuda" else None)
+        else:
+            failed = err is not None
+        if failed:
+            if err is not None:
+                raise err
+            raise RuntimeError("HostGather.gather: another rank's copy into the host model failed")
         return self.host[:self.P] if self.rank == self.dst else None
 
     def close(self):

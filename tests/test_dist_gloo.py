@@ -282,3 +282,77 @@ def test_host_gather_dtype_cache_and_entry_barrier():
     for r in (1, 2):
         assert res[r][:4] == [True] * 4
     assert all(res[r][4] == "TypeError" for r in range(world))
+
+
+def _one_rank_fails_worker(rank, world, port, P, q):
+    """Rank 1 alone fails: its HostGather copy (a piece outside its buffer), its P2PAllGather buffer
+    export, then its peer mapping. Every rank must raise at the same point — none left waiting in a
+    collective — and the process group must still work afterwards."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fedn_amd import ops, sharded
+        from fedn_amd.sharded import HostGather, P2PAllGather
+        out = []
+        sh = ShardedFedAvg(P, fold_fn=lambda *a: None)
+        hg = HostGather(P, torch.float32, sh.bounds)
+        local = torch.ones(sh.hi - sh.lo, dtype=torch.float32)
+        pieces = [(sh.lo, sh.hi, 5)] if rank == 1 else None        # rank 1: past the end of its slice
+        try:
+            hg.gather(local, pieces)
+            out.append("no error")
+        except (ValueError, RuntimeError) as e:
+            out.append(type(e).__name__)
+        got = hg.gather(local)                                       # the next gather works again
+        out.append(bool(rank != 0 or float(got.sum()) == float(P)))
+
+        def handle(t):
+            if rank == 1:
+                raise OSError("no IPC export here")
+            return b"\0" * 64, 0
+        ops.ipc_handle, real_handle = handle, ops.ipc_handle
+        buf = torch.zeros(8)
+        try:
+            P2PAllGather(buf)
+            out.append("no error")
+        except RuntimeError as e:
+            out.append("export" if "rank 1 could not export" in str(e) else str(e))
+        ops.ipc_handle = lambda t: (b"\0" * 64, 0)
+
+        def ipc_open(h, o, dev):
+            if rank == 1:
+                raise OSError("no peer mapping here")
+            return 4096, 4096
+        closed = []
+        ops.ipc_open, ops.ipc_close = ipc_open, lambda base, dev=None: closed.append(base)
+        try:
+            P2PAllGather(buf)
+            out.append("no error")
+        except (OSError, RuntimeError) as e:
+            out.append(type(e).__name__)
+        out.append(len(closed))                                      # rank 0 unmapped what it had mapped
+        ops.ipc_handle = real_handle
+        out.append(sharded._agree(False))
+        dist.barrier()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_one_rank_failure_fails_every_rank_without_a_hang():
+    """A HostGather copy, a P2P buffer export and a P2P peer mapping that fail on ONE rank raise on
+    every rank (the failing rank its own error, the others RuntimeError) — bench.py then falls back to
+    the collective on all ranks together instead of hanging in mismatched collectives."""
+    world, P = 3, 10_007
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pc = mp.start_processes(_one_rank_fails_worker, args=(world, _free_port(), P, q), nprocs=world, join=False,
+                            start_method="spawn")
+    res = dict(q.get(timeout=120) for _ in range(world))
+    while not pc.join(timeout=60):
+        pass
+    assert res[1] == ["ValueError", True, "export", "OSError", 0, False]
+    assert res[0] == ["RuntimeError", True, "export", "RuntimeError", 2, False]
+    assert res[2] == ["RuntimeError", True, "export", "RuntimeError", 2, False]
