@@ -7,7 +7,8 @@ FEDn's ``HelperBase`` requires (helperbase.py:4-40) plus its file-type API:
                                               output readable by np.load
   load(path, file_type="npz")                 numpyhelper.py:171-189: native inflate (parallel
                                               for archives this codec wrote), members of 8 MiB+
-                                              into pinned memory on a GPU host; raw_binary as FEDn
+                                              into pinned memory for a multi-GPU combiner;
+                                              raw_binary as FEDn
   add / subtract / multiply / divide / sqrt / sign / ones
                                               numpyhelper.py:34-142 on the GPU (fa_elementwise),
                                               numpy's dtype promotion and rounding, so FEDn's
@@ -28,12 +29,24 @@ import numpy as np
 from . import codec
 
 
-# npz members at least this large are decoded into page-locked host memory when a GPU is present
-# (0 disables): the multi-device aggregation pipeline DMAs such a tensor straight from where it lies
-# instead of packing it into a pinned slot first (multidev.INPLACE_MIN_BYTES). The blocks come from
-# torch's caching host allocator, so a session's rounds reuse them without pinning pages again.
+# npz members at least this large are decoded into page-locked host memory (0 disables) when the
+# combiner aggregates on several GPUs in one process (FEDN_AMD_DEVICES lists more than one; or always
+# with FEDN_AMD_DECODE_PINNED=1, never with 0): the multi-device pipeline DMAs such a tensor slice by
+# slice straight from where it lies instead of packing it into a pinned slot first
+# (multidev.INPLACE_MIN_BYTES). The blocks come from torch's caching host allocator, so a session's
+# rounds reuse them without pinning pages again (its blocks round up to a power of two and stay
+# cached for the process). One device packs every update anyway, so plain arrays serve it.
 DECODE_PINNED_MIN_BYTES = int(os.environ.get("FEDN_AMD_DECODE_PINNED_MIN_BYTES", str(8 << 20)))
 _pinned_ok = None
+
+
+def decode_pinned():
+    """Whether :meth:`Helper.load` decodes large members into page-locked memory (see above)."""
+    v = os.environ.get("FEDN_AMD_DECODE_PINNED", "auto")
+    if v in ("0", "1"):
+        return v == "1"
+    from .aggregators.fedavg import env_devices
+    return len(env_devices() or []) > 1
 
 
 def pinned_empty(shape, dtype, order="C"):
@@ -332,14 +345,15 @@ class Helper:
     def load(self, path, file_type="npz"):
         self.check_supported_file_type(file_type)
         if file_type == "npz":
+            alloc = pinned_empty if decode_pinned() else None
             if isinstance(path, (bytes, bytearray, memoryview)):
-                return codec.load_npz(path, alloc=pinned_empty)
+                return codec.load_npz(path, alloc=alloc)
             if hasattr(path, "getbuffer"):
-                return codec.load_npz(path.getbuffer(), alloc=pinned_empty)
+                return codec.load_npz(path.getbuffer(), alloc=alloc)
             if hasattr(path, "read"):
-                return codec.load_npz(path.read(), alloc=pinned_empty)
+                return codec.load_npz(path.read(), alloc=alloc)
             with open(path, "rb") as f:
-                return codec.load_npz(np.fromfile(f, dtype=np.uint8), alloc=pinned_empty)
+                return codec.load_npz(np.fromfile(f, dtype=np.uint8), alloc=alloc)
         if isinstance(path, BytesIO):
             return [np.frombuffer(path.read(), dtype=np.float64)]
         return [np.fromfile(path, dtype=np.float64)]

@@ -38,11 +38,17 @@ def _clients(rng, base, K, pinned=False):
     return ups, [int(v) for v in rng.integers(1, 5001, K)]
 
 
-def test_helper_load_decodes_large_members_pinned():
-    """fedn_amd.helper.load on a GPU host: members of 8 MiB+ land in page-locked memory (a device
-    address exists for them), smaller ones in ordinary arrays; values identical to the archive's."""
+@pytest.mark.parametrize("env", [{"FEDN_AMD_DEVICES": "cuda:0,cuda:0"}, {"FEDN_AMD_DECODE_PINNED": "1"}],
+                         ids=["multi_device_combiner", "forced"])
+def test_helper_load_decodes_large_members_pinned(env, monkeypatch):
+    """fedn_amd.helper.load for a multi-GPU combiner: members of 8 MiB+ land in page-locked memory
+    (a device address exists for them), smaller ones in ordinary arrays; values identical to the
+    archive's."""
     from fedn_amd import ops
     from fedn_amd.helper import Helper
+    monkeypatch.delenv("FEDN_AMD_DECODE_PINNED", raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     rng = np.random.default_rng(7)
     ws = [rng.standard_normal(s).astype(np.float32) for s in SHAPES]
     h = Helper()
@@ -56,6 +62,21 @@ def test_helper_load_decodes_large_members_pinned():
         else:
             with pytest.raises(ops.FedAggError):
                 ops.host_device_ptr(a.ctypes.data, torch.device(DEV))
+
+
+def test_helper_load_one_device_keeps_plain_arrays(monkeypatch):
+    """One device packs every update anyway: no pinned decode unless asked for."""
+    from fedn_amd import ops
+    from fedn_amd.helper import Helper
+    monkeypatch.delenv("FEDN_AMD_DEVICES", raising=False)
+    monkeypatch.delenv("FEDN_AMD_DECODE_PINNED", raising=False)
+    ws = [np.arange(3_000_000, dtype=np.float32)]
+    b = io.BytesIO()
+    Helper().save(ws, b)
+    out = Helper().load(io.BytesIO(b.getvalue()))
+    assert_lists_identical(out, ws, "plain decode")
+    with pytest.raises(ops.FedAggError):
+        ops.host_device_ptr(out[0].ctypes.data, torch.device(DEV))
 
 
 @pytest.mark.parametrize("ndev", [2, 3])
