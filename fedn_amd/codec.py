@@ -19,7 +19,7 @@ from .layout import Layout
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfednpz.so")
 MAX_DIMS = 16
-FNPZ_ABI_VERSION = 4    # include/fednpz.h
+FNPZ_ABI_VERSION = 5    # include/fednpz.h
 THREADS = int(os.environ.get("FEDN_AMD_CODEC_THREADS", str(min(16, os.cpu_count() or 1))))
 
 
@@ -76,6 +76,10 @@ def load_lib():
                 lib.fnpz_gather.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_int64), ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_int64]          # destination buffer window
+                lib.fnpz_inflate_raw.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                                 ctypes.c_int64, ctypes.POINTER(ctypes.c_int)]
+                lib.fnpz_crc32.restype = ctypes.c_uint32
+                lib.fnpz_crc32.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int64]
                 lib.fnpz_gather_start.restype = ctypes.c_int64
                 lib.fnpz_gather_start.argtypes = lib.fnpz_gather.argtypes
                 lib.fnpz_gather_wait.argtypes = [ctypes.c_int64]
@@ -183,6 +187,25 @@ def read_entries(a, ents, dsts, threads=None):
     arr = (Entry * max(1, len(ents)))(*ents)
     ptrs = (ctypes.c_void_p * max(1, len(ents)))(*[d.ctypes.data if d.size else 0 for d in dsts])
     _check(lib.fnpz_read(a.ctypes.data, a.size, arr, len(ents), ptrs, threads or THREADS))
+
+
+def inflate_raw(data, out_len, window=0):
+    """Raw DEFLATE decode of ``data`` (bytes-like) into ``out_len`` bytes with the codec's decoder
+    (fnpz_inflate_raw; ``window``: resume every that many output bytes). (bytes, stream_end);
+    CodecError on an invalid or short stream."""
+    lib = load_lib()
+    src = np.frombuffer(data, dtype=np.uint8)
+    out = np.empty(max(1, out_len), dtype=np.uint8)
+    end = ctypes.c_int(0)
+    _check(lib.fnpz_inflate_raw(src.ctypes.data if src.size else None, src.size, out.ctypes.data, out_len, window,
+                                ctypes.byref(end)))
+    return out[:out_len].tobytes(), bool(end.value)
+
+
+def crc32(data, crc=0):
+    """CRC-32 of ``data`` (zlib.crc32's value) with the codec's folded implementation."""
+    a = np.frombuffer(data, dtype=np.uint8)
+    return int(load_lib().fnpz_crc32(crc, a.ctypes.data if a.size else None, a.size))
 
 
 def _ordered(ents):

@@ -23,12 +23,14 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/fednpz.h"
+#include "inflate.h"
 
 namespace {
 
@@ -294,22 +296,59 @@ int resolve_entry(const uint8_t* a, int64_t len, const CdEntry& c, fnpz_entry* e
     return FNPZ_OK;
 }
 
-int decode_one(const uint8_t* a, const fnpz_entry& e, void* dst, char* err, size_t errlen) {
-    MemberReader r(a + e.data_offset, e.comp_size, e.method);
-    if (!r.ready()) return snprintf(err, errlen, "%s: inflate init failed", e.name), FNPZ_ECORRUPT;
-    std::vector<uint8_t> hdr((size_t)e.npy_header);
-    if (!r.read(hdr.data(), e.npy_header)) return snprintf(err, errlen, "%s: corrupt header", e.name), FNPZ_ECORRUPT;
-    uLong crc = crc32(0L, hdr.data(), (uInt)hdr.size());
-    uint8_t* out = static_cast<uint8_t*>(dst);
-    int64_t left = e.nbytes;
-    while (left > 0) {
-        const int64_t n = std::min<int64_t>(left, kChunk);
-        if (!r.read(out, n)) return snprintf(err, errlen, "%s: corrupt or truncated payload", e.name), FNPZ_ECORRUPT;
-        crc = crc32(crc, out, (uInt)n);
-        out += n;
-        left -= n;
+// Inflate one raw-deflate range whose output is exactly ``hlen`` bytes into ``hdr`` followed by
+// ``dlen`` bytes into ``dst`` (fnpz_fast::Inflate, inflate.h), CRC-32 folded in over 256 KiB
+// pieces while they are in cache. The header and the first 64 KiB of payload are decoded into a
+// scratch buffer first, so that every later back-reference (<= 32 KiB) stays inside ``dst``.
+// Returns 0, or -1 with ``*line`` = the decoder's verdict line (0: the stream ended early).
+int inflate_split(const uint8_t* in, int64_t inlen, uint8_t* hdr, int64_t hlen, uint8_t* dst, int64_t dlen,
+                  uint32_t* crc, int* line) {
+    std::unique_ptr<fnpz_fast::Inflate> dec(new fnpz_fast::Inflate(in, (size_t)inlen));
+    uint32_t c = *crc;
+    *line = 0;
+    auto fill = [&](uint8_t* lo, uint8_t* hi, const uint8_t* win) -> bool {
+        uint8_t* o = lo;
+        const int rc = dec->run(&o, hi, win);
+        if (rc == fnpz_fast::Inflate::kCorrupt) *line = dec->error_line();
+        return rc != fnpz_fast::Inflate::kCorrupt && o == hi;
+    };
+    int64_t done = 0;
+    if (hlen > 0) {
+        const int64_t first = std::min<int64_t>(dlen, 64 << 10);
+        std::vector<uint8_t> tmp((size_t)(hlen + first));
+        if (!fill(tmp.data(), tmp.data() + tmp.size(), tmp.data())) return -1;
+        c = fnpz_fast::crc32(c, tmp.data(), tmp.size());
+        std::memcpy(hdr, tmp.data(), (size_t)hlen);
+        if (first > 0) std::memcpy(dst, tmp.data() + hlen, (size_t)first);
+        done = first;
     }
-    if ((uint32_t)crc != e.crc32) return snprintf(err, errlen, "%s: CRC-32 mismatch", e.name), FNPZ_ECORRUPT;
+    constexpr int64_t kPiece = 256 << 10;
+    while (done < dlen) {
+        const int64_t k = std::min<int64_t>(kPiece, dlen - done);
+        if (!fill(dst + done, dst + done + k, dst)) return -1;
+        c = fnpz_fast::crc32(c, dst + done, (size_t)k);
+        done += k;
+    }
+    *crc = c;
+    return 0;
+}
+
+int decode_one(const uint8_t* a, const fnpz_entry& e, void* dst, char* err, size_t errlen) {
+    uint8_t* out = static_cast<uint8_t*>(dst);
+    std::vector<uint8_t> hdr((size_t)e.npy_header);
+    uint32_t crc = 0;
+    if (e.method == 8) {
+        int line = 0;
+        if (inflate_split(a + e.data_offset, e.comp_size, hdr.data(), e.npy_header, out, e.nbytes, &crc, &line))
+            return snprintf(err, errlen, "%.200s: corrupt or truncated deflate stream (inflate.h:%d)", e.name, line),
+                   FNPZ_ECORRUPT;
+    } else {
+        if (e.npy_header + e.nbytes > e.comp_size) return snprintf(err, errlen, "%s: truncated member", e.name), FNPZ_ECORRUPT;
+        if (e.npy_header > 0) std::memcpy(hdr.data(), a + e.data_offset, (size_t)e.npy_header);
+        if (e.nbytes > 0) std::memcpy(out, a + e.data_offset + e.npy_header, (size_t)e.nbytes);
+        crc = fnpz_fast::crc32(fnpz_fast::crc32(0, hdr.data(), hdr.size()), out, (size_t)e.nbytes);
+    }
+    if (crc != e.crc32) return snprintf(err, errlen, "%s: CRC-32 mismatch", e.name), FNPZ_ECORRUPT;
     return FNPZ_OK;
 }
 
@@ -368,7 +407,7 @@ void deflate_block(const MemberSrc& m, Block& blk, int level) {
         m.gather(blk.begin, blk.len, tmp.data());
         in = tmp.data();
     }
-    blk.crc = crc32(0L, in, (uInt)blk.len);
+    blk.crc = fnpz_fast::crc32(0, in, (size_t)blk.len);
     z_stream zs{};
     if (deflateInit2(&zs, level, Z_DEFLATED, -MAX_WBITS, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
         blk.rc = Z_STREAM_ERROR;
@@ -537,6 +576,33 @@ int stream_npy_header(fnpz_stream* s, fnpz_entry* e) {
 extern "C" {
 
 int fnpz_abi_version(void) { return FNPZ_ABI_VERSION; }
+
+int fnpz_inflate_raw(const uint8_t* in, int64_t in_len, uint8_t* out, int64_t out_len, int64_t window, int* stream_end) {
+    g_err[0] = 0;
+    if (in_len < 0 || out_len < 0 || window < 0 || (in_len > 0 && !in) || (out_len > 0 && !out))
+        return fail(FNPZ_EINVAL, "fnpz_inflate_raw: bad arguments");
+    std::unique_ptr<fnpz_fast::Inflate> dec(new fnpz_fast::Inflate(in, (size_t)in_len));
+    uint8_t* o = out;
+    uint8_t* const end = out + out_len;
+    int rc = fnpz_fast::Inflate::kFull;
+    while (rc == fnpz_fast::Inflate::kFull && o < end) {
+        uint8_t* w = window > 0 ? std::min(end, o + window) : end;
+        rc = dec->run(&o, w, out);
+        if (rc == fnpz_fast::Inflate::kFull && o != w) break;
+    }
+    if (rc == fnpz_fast::Inflate::kFull && o == end) rc = dec->run(&o, end, out);   // the final block's end, if here
+    if (stream_end) *stream_end = rc == fnpz_fast::Inflate::kEnd;
+    if (rc == fnpz_fast::Inflate::kCorrupt)
+        return fail(FNPZ_ECORRUPT, "fnpz_inflate_raw: invalid deflate stream (inflate.h:%d) after %lld bytes",
+                    dec->error_line(), (long long)(o - out));
+    if (o != end) return fail(FNPZ_ECORRUPT, "fnpz_inflate_raw: stream ended after %lld of %lld bytes", (long long)(o - out),
+                              (long long)out_len);
+    return FNPZ_OK;
+}
+
+uint32_t fnpz_crc32(uint32_t crc, const uint8_t* data, int64_t len) {
+    return len > 0 ? fnpz_fast::crc32(crc, data, (size_t)len) : crc;
+}
 const char* fnpz_last_error(void) { return g_err; }
 
 int fnpz_open(const uint8_t* archive, int64_t len, fnpz_entry* entries, int max_entries, int* n_entries) {
@@ -587,29 +653,23 @@ int fnpz_read(const uint8_t* archive, int64_t len, const fnpz_entry* entries, in
                 rcs[t] = FNPZ_ECORRUPT;
                 snprintf(msg, sizeof(msg), "%s: bad block index", e.name);
             } else {
-                Inflater inf(archive + e.data_offset + c0, (int64_t)(c1 - c0));
-                uLong crc = 0;
-                bool ok = inf.ok;
-                uint64_t pos = r0;
-                if (ok && pos < (uint64_t)e.npy_header) {          // block 0 starts with the .npy header
-                    std::vector<uint8_t> hdr((size_t)(e.npy_header - pos));
-                    ok = inf.fill(hdr.data(), (int64_t)hdr.size());
-                    crc = crc32(crc, hdr.data(), (uInt)hdr.size());
-                    pos = (uint64_t)e.npy_header;
-                }
-                uint8_t* out = static_cast<uint8_t*>(dst) + (pos - (uint64_t)e.npy_header);
-                while (ok && pos < r1) {
-                    const int64_t k = (int64_t)std::min<uint64_t>(r1 - pos, kChunk);
-                    ok = inf.fill(out, k);
-                    crc = crc32(crc, out, (uInt)k);
-                    out += k;
-                    pos += (uint64_t)k;
-                }
-                if (!ok) {
+                // block 0 starts with the .npy header; each block is its own deflate history
+                const uint64_t h0 = r0 < (uint64_t)e.npy_header ? (uint64_t)e.npy_header - r0 : 0;
+                if (r0 + h0 > r1) {
                     rcs[t] = FNPZ_ECORRUPT;
-                    snprintf(msg, sizeof(msg), "%s: corrupt block %d", e.name, b);
+                    snprintf(msg, sizeof(msg), "%s: bad block index", e.name);
+                } else {
+                    std::vector<uint8_t> hdr((size_t)h0);
+                    uint8_t* out = static_cast<uint8_t*>(dst) + (r0 + h0 - (uint64_t)e.npy_header);
+                    uint32_t crc = 0;
+                    int line = 0;
+                    if (inflate_split(archive + e.data_offset + c0, (int64_t)(c1 - c0), hdr.data(), (int64_t)h0, out,
+                                      (int64_t)(r1 - r0 - h0), &crc, &line)) {
+                        rcs[t] = FNPZ_ECORRUPT;
+                        snprintf(msg, sizeof(msg), "%s: corrupt block %d (inflate.h:%d)", e.name, b, line);
+                    }
+                    bcrc[t] = crc;
                 }
-                bcrc[t] = crc;
             }
         }
         errs[t] = msg;

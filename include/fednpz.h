@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define FNPZ_ABI_VERSION 4
+#define FNPZ_ABI_VERSION 5
 #define FNPZ_MAX_DIMS 16
 
 enum fnpz_status { FNPZ_OK = 0, FNPZ_EFORMAT = 1, FNPZ_ECORRUPT = 2, FNPZ_EINVAL = 3, FNPZ_ENOSPC = 4 };
@@ -91,6 +91,17 @@ void fnpz_stream_close(fnpz_stream* stream);
 int fnpz_stream_feed(fnpz_stream* stream, const uint8_t* data, int64_t len);
 int fnpz_stream_next(fnpz_stream* stream, uint8_t* out, int64_t out_cap, int* event, fnpz_entry* entry,
                      int64_t* out_len);
+
+/* Raw DEFLATE (RFC 1951) decode of in[0, in_len) into out[0, out_len), in windows of `window`
+ * bytes (0: one window; the decoder resumes at any output position) — the decoder fnpz_read
+ * inflates whole members and blocks with (fedn_amd/csrc/inflate.h; ABI 5). FNPZ_OK once out is
+ * full (*stream_end = 1 if the stream's final block ended there); FNPZ_ECORRUPT on an invalid or
+ * truncated stream, or one that ends before out is full. */
+int fnpz_inflate_raw(const uint8_t* in, int64_t in_len, uint8_t* out, int64_t out_len, int64_t window, int* stream_end);
+
+/* CRC-32 of the zip format with zlib's convention (crc32(0, ...) starts; pass the previous value to
+ * continue), folded with carry-less multiplies where the CPU has them (ABI 5). */
+uint32_t fnpz_crc32(uint32_t crc, const uint8_t* data, int64_t len);
 
 /* Host staging (beside the wire format; the aggregators' pack of a decoded update into its pinned
  * staging buffer, fedn_amd/layout.py): dsts[i][0, nbytes[i]) = srcs[i][0, nbytes[i]) for i < n,

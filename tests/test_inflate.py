@@ -1,0 +1,159 @@
+"""The codec's own raw-DEFLATE decoder and CRC-32 (fedn_amd/csrc/inflate.h, fnpz_inflate_raw /
+fnpz_crc32) against zlib — the library numpy's np.savez_compressed / np.load go through
+(numpyhelper.py:144-189). Every block type (stored, fixed, dynamic), every zlib level and strategy,
+outputs resumed at arbitrary window sizes (the decoder stops at any output byte, inside a match
+included), sync-flushed ranges (fnpz_write's independently inflatable blocks), and corrupted or
+truncated streams: the decoder returns zlib's bytes for what zlib decodes, and rejects what zlib
+rejects before the requested length. CPU only."""
+import zlib
+
+import numpy as np
+import pytest
+
+from fedn_amd import codec
+
+
+def _inputs():
+    rng = np.random.default_rng(5)
+    out = {}
+    for n in (0, 1, 7, 300, 4096, 70_000, 300_000):
+        out[f"random{n}"] = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        out[f"float{n}"] = rng.standard_normal(n // 4).astype(np.float32).tobytes()
+        out[f"text{n}"] = (b"abcabcabd hello world " * (n // 22 + 1))[:n]
+        sparse = np.zeros(n, np.uint8)
+        m = rng.random(n) < 0.05
+        sparse[m] = rng.integers(1, 256, int(m.sum()), dtype=np.uint8)
+        out[f"sparse{n}"] = sparse.tobytes()
+        runs = np.repeat(rng.integers(0, 4, n // 1000 + 1, dtype=np.uint8), 1000)[:n]
+        out[f"runs{n}"] = runs.tobytes()
+    return out
+
+
+INPUTS = _inputs()
+STRATEGIES = [zlib.Z_DEFAULT_STRATEGY, zlib.Z_FILTERED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE, zlib.Z_FIXED]
+
+
+def _deflate(data, level, strategy, flush=zlib.Z_FINISH):
+    c = zlib.compressobj(level, zlib.DEFLATED, -15, 8, strategy)
+    return c.compress(data) + c.flush(flush)
+
+
+@pytest.mark.parametrize("level", [0, 1, 6, 9])
+@pytest.mark.parametrize("strategy", STRATEGIES)
+def test_every_level_and_strategy_against_zlib(level, strategy):
+    for name, data in INPUTS.items():
+        z = _deflate(data, level, strategy)
+        out, end = codec.inflate_raw(z, len(data))
+        assert out == data and end, (name, level, strategy)
+
+
+@pytest.mark.parametrize("window", [1, 3, 258, 259, 4093, 65536])
+def test_resumes_at_any_output_position(window):
+    for name in ("float70000", "text70000", "sparse70000", "runs70000", "random4096"):
+        data = INPUTS[name]
+        for level, strategy in ((1, zlib.Z_DEFAULT_STRATEGY), (6, zlib.Z_RLE), (9, zlib.Z_FIXED), (0, 0)):
+            out, end = codec.inflate_raw(_deflate(data, level, strategy), len(data), window=window)
+            assert out == data and end, (name, window, level, strategy)
+
+
+def test_sync_flushed_range_decodes_without_a_final_block():
+    """fnpz_write's blocks: each a deflate range ending in a sync flush (an empty stored block),
+    read on its own: the output fills, no final block follows, and that is not an error."""
+    for name in ("float300000", "text4096", "random70000"):
+        data = INPUTS[name]
+        z = _deflate(data, 6, zlib.Z_DEFAULT_STRATEGY, zlib.Z_SYNC_FLUSH)
+        assert z.endswith(b"\x00\x00\xff\xff")
+        out, end = codec.inflate_raw(z, len(data))
+        assert out == data and not end
+
+
+def test_short_and_long_outputs_are_errors():
+    data = INPUTS["float4096"]
+    z = _deflate(data, 6, zlib.Z_DEFAULT_STRATEGY)
+    with pytest.raises(codec.CodecError, match="ended after"):
+        codec.inflate_raw(z, len(data) + 1)          # the stream holds fewer bytes
+    out, end = codec.inflate_raw(z, len(data) - 1)   # a prefix: fine, the final block not reached
+    assert out == data[:-1] and not end
+
+
+def test_crc32_matches_zlib():
+    rng = np.random.default_rng(9)
+    for n in (0, 1, 15, 16, 63, 64, 65, 127, 1000, 65536 + 13, 1_000_003):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        for off in (0, 1, 7):
+            chunk = data[off:]
+            assert codec.crc32(chunk) == zlib.crc32(chunk)
+            assert codec.crc32(chunk, 0x12345678) == zlib.crc32(chunk, 0x12345678)
+    a, b = INPUTS["float300000"], INPUTS["text70000"]
+    assert codec.crc32(b, codec.crc32(a)) == zlib.crc32(a + b)
+
+
+def _zlib_prefix(z, n):
+    """zlib's first n output bytes (None if it fails or runs short before them) and whether the
+    stream also ends cleanly right there."""
+    d = zlib.decompressobj(-15)
+    try:
+        out = d.decompress(z, n)
+    except zlib.error:
+        return None, False
+    if len(out) != n:
+        return None, False
+    try:
+        rest = d.decompress(d.unconsumed_tail, 1) if d.unconsumed_tail else b""
+        rest += d.flush()
+    except zlib.error:
+        return out, False
+    return out, d.eof and not rest
+
+
+def test_corrupted_streams_rejected_like_zlib():
+    """Bit flips, random bytes and truncations. A stream zlib decodes completely to the expected
+    length (final block included) decodes identically; one where zlib fails or runs short before
+    that length is rejected; otherwise (zlib reaches the length, the stream is bad after it) the
+    decoder may stop at the full output or reject — but never returns other bytes."""
+    rng = np.random.default_rng(17)
+    names = [k for k, v in INPUTS.items() if 0 < len(v) <= 70_000]
+    agree = rejected = 0
+    for it in range(3000):
+        data = INPUTS[names[rng.integers(len(names))]]
+        z = bytearray(_deflate(data, int(rng.integers(0, 10)), STRATEGIES[rng.integers(len(STRATEGIES))]))
+        mode = it % 3
+        if mode == 0:
+            for _ in range(int(rng.integers(1, 5))):
+                z[rng.integers(len(z))] ^= 1 << int(rng.integers(8))
+        elif mode == 1:
+            del z[int(rng.integers(len(z))):]
+        else:
+            for _ in range(8):
+                z[rng.integers(len(z))] = int(rng.integers(256))
+        prefix, complete = _zlib_prefix(bytes(z), len(data))
+        try:
+            out, end = codec.inflate_raw(bytes(z), len(data))
+        except codec.CodecError:
+            out, end = None, False
+        if complete:
+            assert out == prefix and end, it
+            agree += 1
+        elif out is None:
+            rejected += 1
+        elif prefix is not None:
+            assert out == prefix, it
+        else:
+            # zlib raised; the decoder stopped at the full output first (zlib decodes a length /
+            # distance pair before it checks for room, this decoder checks first): the bytes zlib did
+            # produce before its error must be the decoder's, and no clean end may be claimed
+            assert not end, it
+            part = _zlib_partial(bytes(z))
+            assert out[:len(part)] == part[:len(out)], it
+    assert agree > 100 and rejected > 1000
+
+
+def _zlib_partial(z, piece=16):
+    d = zlib.decompressobj(-15)
+    out = b""
+    for i in range(0, len(z), piece):
+        try:
+            out += d.decompress(z[i:i + piece])
+        except zlib.error:
+            break
+    return out

@@ -21,7 +21,7 @@ import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TESTS = ["tests/test_codec.py", "tests/test_fastpack.py", "tests/test_staging_host.py"]
+TESTS = ["tests/test_codec.py", "tests/test_inflate.py", "tests/test_fastpack.py", "tests/test_staging_host.py"]
 SAN = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined", "-g", "-O1"]
 
 
@@ -62,7 +62,8 @@ def main():
                                 "new_delete_type_mismatch=0:detect_odr_violation=0",
                    UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
                    PYTHONDONTWRITEBYTECODE="1")
-        cmd = [sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider", "-m", "not gpu", *TESTS]
+        # -s: a report printed inside a test reaches the log even when the sanitizer ends the process
+        cmd = [sys.executable, "-m", "pytest", "-q", "-s", "-p", "no:cacheprovider", "-m", "not gpu", *TESTS]
         say(f"$ LD_PRELOAD={env['LD_PRELOAD']} ASAN_OPTIONS={env['ASAN_OPTIONS']} "
             f"UBSAN_OPTIONS={env['UBSAN_OPTIONS']} " + " ".join(cmd))
         t0 = time.time()
