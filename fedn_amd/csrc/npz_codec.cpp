@@ -399,7 +399,30 @@ struct MemberSrc {
     const uint8_t* direct(int64_t b, int64_t n) const { return b >= hlen ? data + (b - hlen) : (b + n <= hlen ? header + b : nullptr); }
 };
 
-void deflate_block(const MemberSrc& m, Block& blk, int level) {
+// one deflate pass of [in, in + n) as a (sync-flushed or final) raw stream; false on a zlib error
+bool deflate_into(const uint8_t* in, int64_t n, bool last, int level, int strategy, std::vector<uint8_t>& out) {
+    z_stream zs{};
+    if (deflateInit2(&zs, level, Z_DEFLATED, -MAX_WBITS, 8, strategy) != Z_OK) return false;
+    // zlib 1.2.11's deflateBound assumes a stored fallback, which Z_FIXED does not take (fixed codes can
+    // expand incompressible bytes by 1/8): size for that too
+    out.resize(std::max<size_t>(deflateBound(&zs, (uLong)n), (size_t)(n + n / 8 + n / 64)) + 64);
+    zs.next_in = const_cast<Bytef*>(in);
+    zs.avail_in = (uInt)n;
+    zs.next_out = out.data();
+    zs.avail_out = (uInt)out.size();
+    const int rc = deflate(&zs, last ? Z_FINISH : Z_SYNC_FLUSH);
+    const bool ok = last ? rc == Z_STREAM_END : (rc == Z_OK && zs.avail_in == 0);
+    out.resize(out.size() - zs.avail_out);
+    deflateEnd(&zs);
+    return ok;
+}
+
+// FNPZ_STRATEGY_AUTO: run-length matching only (zlib's Z_RLE) — on model weights (fp32 / bf16 values,
+// sparse or not) as small as the default strategy or smaller and 3-8x faster, as their bytes hardly
+// repeat beyond runs; a block that shrinks below 60 % (structured data: integer ramps, tiled
+// patterns, where longer matches pay) is deflated again with the default strategy at level 1 and the
+// smaller of the two kept
+void deflate_block(const MemberSrc& m, Block& blk, int level, int strategy) {
     std::vector<uint8_t> tmp;
     const uint8_t* in = m.direct(blk.begin, blk.len);
     if (!in) {
@@ -408,20 +431,18 @@ void deflate_block(const MemberSrc& m, Block& blk, int level) {
         in = tmp.data();
     }
     blk.crc = fnpz_fast::crc32(0, in, (size_t)blk.len);
-    z_stream zs{};
-    if (deflateInit2(&zs, level, Z_DEFLATED, -MAX_WBITS, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
-        blk.rc = Z_STREAM_ERROR;
+    const bool autos = strategy == FNPZ_STRATEGY_AUTO;
+    if (!deflate_into(in, blk.len, blk.last, level, autos && level > 0 ? Z_RLE : (autos ? Z_DEFAULT_STRATEGY : strategy),
+                      blk.out)) {
+        blk.rc = Z_BUF_ERROR;
         return;
     }
-    blk.out.resize(deflateBound(&zs, (uLong)blk.len) + 64);
-    zs.next_in = const_cast<Bytef*>(in);
-    zs.avail_in = (uInt)blk.len;
-    zs.next_out = blk.out.data();
-    zs.avail_out = (uInt)blk.out.size();
-    const int rc = deflate(&zs, blk.last ? Z_FINISH : Z_SYNC_FLUSH);
-    blk.rc = (blk.last ? rc == Z_STREAM_END : (rc == Z_OK && zs.avail_in == 0)) ? Z_OK : Z_BUF_ERROR;
-    blk.out.resize(blk.out.size() - zs.avail_out);
-    deflateEnd(&zs);
+    blk.rc = Z_OK;
+    if (autos && level > 0 && (double)blk.out.size() < 0.6 * (double)blk.len) {
+        std::vector<uint8_t> alt;
+        if (deflate_into(in, blk.len, blk.last, 1, Z_DEFAULT_STRATEGY, alt) && alt.size() < blk.out.size())
+            blk.out.swap(alt);
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -699,19 +720,23 @@ int64_t fnpz_write_bound(int n, const int64_t* header_lens, const int64_t* nbyte
     int64_t total = 22 + 56 + 20;
     for (int i = 0; i < n; ++i) {
         const int64_t raw = header_lens[i] + nbytes[i];
-        // stored-block worst case of deflate: 5 bytes per 16 KiB, plus per-block flush markers
-        total += raw + raw / 16000 * 5 + (raw / 65536 + 2) * 72 + 2 * (30 + 46 + name_lens[i] + 4 + 20 + 28) + 64;
+        // deflate's worst case: fixed codes (Z_FIXED never falls back to stored blocks) expand by up to
+        // 1/8 + block headers; the stored worst case (5 bytes per 16 KiB) is below that; plus per-block
+        // flush markers and the zip records
+        total += raw + raw / 8 + raw / 64 + (raw / 65536 + 2) * 72 + 2 * (30 + 46 + name_lens[i] + 4 + 20 + 28) + 64;
     }
     return total;
 }
 
 int fnpz_write(int n, const char* const* names, const uint8_t* const* headers, const int64_t* header_lens,
-               const void* const* datas, const int64_t* nbytes, int level, int threads, int64_t block,
+               const void* const* datas, const int64_t* nbytes, int level, int strategy, int threads, int64_t block,
                uint8_t* out, int64_t out_cap, int64_t* out_len) {
     g_err[0] = 0;
     if (n < 0 || !out || !out_len || (n > 0 && (!names || !headers || !header_lens || !datas || !nbytes)))
         return fail(FNPZ_EINVAL, "fnpz_write: bad arguments");
     if (level < 0 || level > 9) return fail(FNPZ_EINVAL, "fnpz_write: level must be 0..9");
+    if (strategy != FNPZ_STRATEGY_AUTO && (strategy < Z_DEFAULT_STRATEGY || strategy > Z_FIXED))
+        return fail(FNPZ_EINVAL, "fnpz_write: strategy must be FNPZ_STRATEGY_AUTO or a zlib strategy 0..4");
     if (block <= 0) block = 4 << 20;
     block = std::min<int64_t>(std::max<int64_t>(block, 64 << 10), 1 << 30);
     std::vector<MemberSrc> src((size_t)n);
@@ -732,7 +757,8 @@ int fnpz_write(int n, const char* const* names, const uint8_t* const* headers, c
             if (total == 0) break;
         }
     }
-    parallel_for((int)blocks.size(), threads, [&](int j) { deflate_block(src[blocks[j].member], blocks[j], level); });
+    parallel_for((int)blocks.size(), threads,
+                 [&](int j) { deflate_block(src[blocks[j].member], blocks[j], level, strategy); });
     for (auto& b : blocks)
         if (b.rc != Z_OK) return fail(FNPZ_ECORRUPT, "fnpz_write: deflate failed on member %d", b.member);
 

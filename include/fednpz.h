@@ -66,10 +66,15 @@ int64_t fnpz_write_bound(int n, const int64_t* header_lens, const int64_t* nbyte
 
 /* Write an npz archive: member i is names[i] + ".npy" = headers[i] (a complete .npy
  * preamble + header dict, e.g. from numpy.lib.format.write_array_header_1_0) followed by
- * datas[i] (nbytes[i] bytes). level: zlib level (numpy uses 6); threads: deflate workers;
- * block: bytes per independently deflated block (0 = 4 MiB). *out_len = bytes written. */
+ * datas[i] (nbytes[i] bytes). level: zlib level (numpy uses 6; 0 stores); strategy: a zlib
+ * strategy (Z_DEFAULT_STRATEGY 0 ... Z_FIXED 4) or FNPZ_STRATEGY_AUTO (ABI 5): run-length matching
+ * (Z_RLE) per block — as small or smaller and several times faster on model weights — with the
+ * default strategy at level 1 kept instead where it is smaller on a block that shrinks below 60 %;
+ * threads: deflate workers; block: bytes per independently deflated block (0 = 4 MiB).
+ * *out_len = bytes written. Any deflate stream np.load reads: the arrays are what was written. */
+#define FNPZ_STRATEGY_AUTO (-1)
 int fnpz_write(int n, const char* const* names, const uint8_t* const* headers, const int64_t* header_lens,
-               const void* const* datas, const int64_t* nbytes, int level, int threads, int64_t block,
+               const void* const* datas, const int64_t* nbytes, int level, int strategy, int threads, int64_t block,
                uint8_t* out, int64_t out_cap, int64_t* out_len);
 
 /* Streaming reader — an archive decoded while it arrives (ModelService.Upload chunks,

@@ -267,3 +267,31 @@ def test_async_gather_queue_tickets_and_empty_jobs():
         assert np.array_equal(d, s)
     with pytest.raises(codec.CodecError):
         codec.gather_wait(0)
+
+
+@pytest.mark.parametrize("strategy", ["auto", "default", "filtered", "huffman", "rle", "fixed"])
+def test_every_write_strategy_reads_back_with_numpy(strategy):
+    rng = np.random.default_rng(3)
+    arrays = ARRAYS + [rng.standard_normal(300_001).astype(np.float32), np.arange(200_000, dtype=np.int64),
+                       np.where(rng.random(100_000) < 0.9, 0, rng.standard_normal(100_000)).astype(np.float32)]
+    enc = codec.save_npz(arrays, block=65536, threads=4, strategy=strategy)
+    assert zipfile.ZipFile(io.BytesIO(enc)).testzip() is None
+    z = np.load(io.BytesIO(enc), allow_pickle=False)
+    for i, x in enumerate(arrays):
+        _same(z[str(i)], x)
+    for x, y in zip(arrays, codec.load_npz(enc)):
+        _same(y, x)
+
+
+def test_auto_strategy_size_on_weights_and_structured_data():
+    """FNPZ_STRATEGY_AUTO: on fp32 weights no larger than np.savez_compressed's own level-6 default
+    strategy (run-length matching captures what deflate finds there); on an integer ramp, where
+    long matches pay, the level-1 default-strategy fallback keeps it within 5 % of level 6."""
+    rng = np.random.default_rng(4)
+    w = rng.standard_normal(1_000_000).astype(np.float32)
+    ramp = np.arange(500_000, dtype=np.int64)
+    for x, slack in ((w, 1.0), (ramp, 1.05)):
+        auto = len(codec.save_npz([x], strategy="auto"))
+        ref = io.BytesIO()
+        np.savez_compressed(ref, x)
+        assert auto <= slack * len(ref.getvalue()), (x.dtype, auto, len(ref.getvalue()))

@@ -59,6 +59,15 @@ def main():
         out["speedup"] = out["numpy_load_s"] / out["native_load_s"]
         out["crc32_native_GBps"] = x.nbytes / best(lambda: codec.crc32(x), a.reps) / 1e9
         out["crc32_zlib_GBps"] = x.nbytes / best(lambda: zlib.crc32(x), a.reps) / 1e9
+        # the other direction: the combiner's model serialisation (helper.save)
+        t_np = best(lambda: np.savez_compressed(io.BytesIO(), **{"0": x}), 1)
+        out["encode"] = {"numpy_s": t_np, "numpy_MB": len(raw) / 1e6}
+        for strat in ("default", "auto"):
+            enc = codec.save_npz([x], threads=a.threads, strategy=strat)
+            got = np.load(io.BytesIO(enc))["0"]
+            assert np.array_equal(got.view(np.uint32), x.view(np.uint32))
+            out["encode"][f"native_{strat}_s"] = best(lambda: codec.save_npz([x], threads=a.threads, strategy=strat), a.reps)
+            out["encode"][f"native_{strat}_MB"] = len(enc) / 1e6
         if a.clients > 1 and P <= 25_000_000:
             archives = [raw] * a.clients
             with ThreadPoolExecutor(a.threads) as ex:
