@@ -268,9 +268,22 @@ inline bool build_table(const uint8_t* lens, int n, Alphabet a, int root, uint32
 
 class Inflate {
   public:
-    enum Status { kOk = 0, kFull = 1, kEnd = 2, kCorrupt = -1 };
+    enum Status { kOk = 0, kFull = 1, kEnd = 2, kNeed = 3, kCorrupt = -1 };
 
     Inflate(const uint8_t* in, size_t n) : in_(in), in_end_(in + n), in_start_(in) {}
+
+    // Streaming input (an archive arriving in pieces): the unconsumed input continues at [in, end)
+    // — the bytes after the last call's input_pos(), possibly moved. Not ``final``: more input may
+    // follow, so run() returns kNeed instead of decoding a symbol or block header that might run
+    // past ``end`` (it keeps >= 56 bits, or >= 700 bytes before a block header, buffered ahead).
+    void set_input(const uint8_t* in, const uint8_t* end, bool final) {
+        in_ = in;
+        in_end_ = end;
+        in_start_ = in;
+        more_ = !final;
+    }
+    // the next input byte not loaded into the bit buffer yet
+    const uint8_t* input_pos() const { return in_; }
 
     // Decode into [*out, out_end): returns kFull when the window is full (call again with the next
     // window), kEnd after the final block (the stream's output is complete), kCorrupt on an invalid
@@ -294,6 +307,9 @@ class Inflate {
                 // a full window at the end of a non-final range (a block of a sync-flushed stream,
                 // read on its own): nothing more to decode here
                 if (out == out_end && !input_left(3)) { rc = kFull; break; }
+                // a dynamic header is < 600 bytes: with more input to come, start a block only
+                // when it cannot run past the input at hand
+                if (more_ && !input_left(8 * 700)) { rc = kNeed; break; }
                 if (!need(3)) { rc = corrupt(__LINE__); break; }
                 final_ = (bits_ & 1) != 0;
                 const uint32_t type = (uint32_t)(bits_ >> 1) & 3;
@@ -312,13 +328,17 @@ class Inflate {
                 }
             }
             if (state_ == kStored) {
-                const size_t k = std::min<size_t>(stored_left_, (size_t)(out_end - out));
-                if ((size_t)(in_end_ - in_) < k) { rc = corrupt(__LINE__); break; }
+                const size_t room = (size_t)(out_end - out);
+                const size_t k = std::min<size_t>({stored_left_, room, (size_t)(in_end_ - in_)});
                 std::memcpy(out, in_, k);
                 in_ += k;
                 out += k;
                 stored_left_ -= k;
-                if (stored_left_) { rc = kFull; break; }
+                if (stored_left_) {
+                    if (out == out_end) { rc = kFull; break; }
+                    rc = more_ ? kNeed : corrupt(__LINE__);   // the input ran out inside the block
+                    break;
+                }
                 state_ = kHeader;
                 continue;
             }
@@ -351,6 +371,7 @@ class Inflate {
     unsigned zeros_ = 0;                 // zero bytes fed past the end of the input (<= 8)
     State state_ = kHeader;
     bool final_ = false;
+    bool more_ = false;                  // streaming input: more may follow the current end
     size_t stored_left_ = 0;
     size_t pend_len_ = 0, pend_dist_ = 0;
     int err_line_ = 0;
@@ -376,6 +397,14 @@ class Inflate {
             nbits_ += 8;
         }
         return true;
+    }
+    // load real input bytes up to 56..63 buffered bits; whether that many are there
+    bool fill_real() {
+        while (nbits_ < 56 && in_ < in_end_) {
+            bits_ |= (uint64_t)*in_++ << nbits_;
+            nbits_ += 8;
+        }
+        return nbits_ >= 56;
     }
     // at least n real (not phantom) input bits not consumed yet
     bool input_left(unsigned n) const {
@@ -628,6 +657,7 @@ class Inflate {
             if (f < 0) { rc = kCorrupt; break; }
             // careful path: the input's or the window's last bytes (>= 56 bits buffered: a whole
             // length / distance pair, <= 48 bits, fits)
+            if (more_ && !fill_real()) { rc = kNeed; break; }     // wait for input, nothing consumed
             if (!refill_slow()) { rc = corrupt(__LINE__); break; }
             const uint32_t e = lit_entry();
             const uint32_t k = e_kind(e);

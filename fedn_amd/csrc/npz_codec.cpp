@@ -474,16 +474,60 @@ struct fnpz_stream {
     size_t pend_pos = 0;
     int64_t left = 0;                   // payload bytes still to deliver
     int err = 0;
+    // deflated members whose compressed size the local header gives (no data descriptor): the
+    // codec's own decoder (inflate.h), fed as the archive arrives, decoding into ``hist`` — the last
+    // 32 KiB of output stay there as the back-reference window, the callers' windows are separate
+    std::unique_ptr<fnpz_fast::Inflate> fdec;
+    bool fast = false;
+    bool fend = false;                  // the decoder passed the member's final block
+    uint64_t comp_left = 0;             // compressed bytes of the member not handed to the decoder
+    std::vector<uint8_t> hist;
+    size_t hp = 0, hd = 0;              // hist[0, hp) decoded; [hd, hp) not delivered yet
+    static constexpr size_t kHistCap = (1u << 20) + (32u << 10), kWindow = 32u << 10;
 
     ~fnpz_stream() {
         if (zinit) inflateEnd(&zs);
     }
     size_t avail() const { return in.size() - pos; }
 
+    int64_t produce_fast(uint8_t* dst, int64_t cap) {
+        if (hd == hp && !fend) {
+            if (hp + 512 > hist.size()) {                          // keep the window, make room
+                const size_t keep = std::min(hp, kWindow);
+                std::memmove(hist.data(), hist.data() + hp - keep, keep);
+                hp = hd = keep;
+            }
+            const uint8_t* base = in.data() + pos;
+            const size_t have = (size_t)std::min<uint64_t>(avail(), comp_left);
+            fdec->set_input(base, base + have, have == comp_left);
+            uint8_t* o = hist.data() + hp;
+            const int rc = fdec->run(&o, hist.data() + hist.size(), hist.data());
+            const size_t used = (size_t)(fdec->input_pos() - base);
+            pos += used;
+            comp_left -= used;
+            hp = (size_t)(o - hist.data());
+            if (rc == fnpz_fast::Inflate::kCorrupt) return -1;
+            if (rc == fnpz_fast::Inflate::kEnd) {
+                fend = true;
+                pos += (size_t)comp_left;                          // the member's last (partial) byte
+                comp_left = 0;
+            }
+        }
+        const int64_t n = std::min<int64_t>(cap, (int64_t)(hp - hd));
+        if (n > 0) {
+            std::memcpy(dst, hist.data() + hd, (size_t)n);
+            hd += (size_t)n;
+            crc = fnpz_fast::crc32((uint32_t)crc, dst, (size_t)n);
+        }
+        if (fend && hd == hp) zend = true;
+        return n;
+    }
+
     // Pull up to cap uncompressed bytes of the current member into dst. Returns the count
     // (crc updated); sets zend at the member's end; -1 on a corrupt stream.
     int64_t produce(uint8_t* dst, int64_t cap) {
         if (zend || cap <= 0) return 0;
+        if (fast) return produce_fast(dst, cap);
         if (method == 0) {
             const int64_t n = (int64_t)std::min<uint64_t>({(uint64_t)cap, (uint64_t)avail(), raw_left});
             std::memcpy(dst, in.data() + pos, (size_t)n);
@@ -543,7 +587,14 @@ int stream_local_header(fnpz_stream* s) {
     if (s->method == 0 && (s->flags & 8)) return -sfail(s, FNPZ_EFORMAT, "%s: stored member with a data descriptor", s->name.c_str());
     s->pos += 30u + nlen + xlen;
     s->raw_left = csize;
-    if (s->method == 8) {
+    s->fast = s->method == 8 && !(s->flags & 8);             // compressed size known: the codec's decoder
+    if (s->fast) {
+        s->fdec.reset(new fnpz_fast::Inflate(nullptr, 0));
+        s->fend = false;
+        s->comp_left = csize;
+        if (s->hist.size() < fnpz_stream::kHistCap) s->hist.resize(fnpz_stream::kHistCap);
+        s->hp = s->hd = 0;
+    } else if (s->method == 8) {
         const int rc = s->zinit ? inflateReset(&s->zs) : inflateInit2(&s->zs, -MAX_WBITS);
         if (rc != Z_OK) return -sfail(s, FNPZ_ECORRUPT, "%s: inflate init failed", s->name.c_str());
         s->zinit = true;

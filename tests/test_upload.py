@@ -252,3 +252,35 @@ def test_streaming_upload_tee_is_bounded():
     assert all(store.get(f"c{i}").data == data for i in range(6))
     svc.close()
     assert svc._free._value == 4                        # every decoder slot released
+
+
+def _zip_npz(arrays, level):
+    """An npz written by zipfile at a given deflate level (np.savez_compressed's container, other levels)."""
+    import zipfile
+    b = io.BytesIO()
+    with zipfile.ZipFile(b, "w", compression=zipfile.ZIP_DEFLATED, compresslevel=level) as z:
+        for i, a in enumerate(arrays):
+            with z.open(f"{i}.npy", "w", force_zip64=True) as f:
+                np.lib.format.write_array(f, np.asarray(a), allow_pickle=False)
+    return b.getvalue()
+
+
+@pytest.mark.parametrize("level", [0, 1, 6, 9])
+def test_decoder_streams_across_its_history_window(level):
+    """Members of several MiB (the streaming decoder's output goes through a 1 MiB buffer whose last
+    32 KiB carry the back-references), periodic data with long matches that straddle those
+    compactions, sparse data and fp32 weights, fed in random pieces from 1 byte to 200 KiB:
+    byte-identical to np.load."""
+    rng = np.random.default_rng(11 + level)
+    arrays = [rng.standard_normal(1_500_000).astype(np.float32),
+              np.tile(rng.integers(0, 255, 30_011, dtype=np.uint8), 100),            # matches ~30 KB back
+              np.where(rng.random(800_000) < 0.95, 0, rng.standard_normal(800_000)).astype(np.float32),
+              np.arange(300_000, dtype=np.int64)]
+    data = _zip_npz(arrays, level)
+    dec = NpzStreamDecoder()
+    o = 0
+    while o < len(data):
+        n = int(rng.integers(1, 200_000)) if rng.random() < 0.7 else int(rng.integers(1, 64))
+        dec.feed(data[o:o + n])
+        o += n
+    _same_as_npload(data, DecodedUpdate(dec.finish(), None).arrays)

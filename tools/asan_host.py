@@ -21,7 +21,8 @@ import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TESTS = ["tests/test_codec.py", "tests/test_inflate.py", "tests/test_fastpack.py", "tests/test_staging_host.py"]
+TESTS = ["tests/test_codec.py", "tests/test_inflate.py", "tests/test_upload.py", "tests/test_fastpack.py",
+         "tests/test_staging_host.py"]
 SAN = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined", "-g", "-O1"]
 
 
