@@ -18,6 +18,7 @@ again. Anything the decoder does not handle (non-npz helpers' bytes, Fortran-ord
 object arrays, a corrupt stream) is simply not adopted: the update then takes the normal path.
 """
 import ctypes
+import os
 import queue
 import threading
 import time
@@ -262,13 +263,19 @@ class StreamingUpload:
     ``max_unclaimed_bytes``. Every other attribute is the wrapped service's."""
 
     def __init__(self, inner, handler, workers=4, pinned=True, device_decode=True, slot=8 << 20, ring=4,
-                 upload=None, max_queued_chunks=64):
+                 upload=None, max_queued_chunks=512, max_queued_bytes=None):
         self.inner = inner
         # bounded tee: at most 4 x workers uploads are decoded at once (a decoder waits for a worker
         # with at most max_queued_chunks chunks buffered; one that falls further behind is
-        # abandoned), later ones take the normal path — the host memory the tee holds is bounded
+        # abandoned), later ones take the normal path — the host memory the tee holds is bounded,
+        # per stream and, over all streams, by max_queued_bytes (FEDN_AMD_TEE_MAX_BYTES, 2 GiB). A
+        # decode slower than its upload (an inflate core does ~440 MB/s of input) lags instead of
+        # giving up: the backlog left when the upload ends is much shorter than decoding it all then.
         self._free = threading.Semaphore(4 * workers)
         self.max_queued_chunks = max_queued_chunks
+        self.max_queued_bytes = int(os.environ.get("FEDN_AMD_TEE_MAX_BYTES", str(2 << 30))) \
+            if max_queued_bytes is None else int(max_queued_bytes)
+        self._queued = 0                     # chunk bytes queued to decoders, all streams
         self._upload = upload if upload is not None else inner.Upload
         self.handler = handler
         self.pinned = pinned
@@ -326,6 +333,7 @@ class StreamingUpload:
                 if chunk is None:
                     ended = True
                     break
+                self._dequeued(len(chunk))
                 if stop.is_set():
                     raise RuntimeError("decode abandoned: the upload outpaced the decoder")
                 dec.feed(chunk)
@@ -348,9 +356,29 @@ class StreamingUpload:
             keep.clear()
             fut.set_exception(e)
             while not ended:                           # drain to the end of the upload
-                ended = q.get() is None
+                chunk = q.get()
+                ended = chunk is None
+                if not ended:
+                    self._dequeued(len(chunk))
         finally:
             self._free.release()
+
+    def _dequeued(self, n):
+        with self._lock:
+            self._queued -= n
+
+    def _enqueue(self, q, chunk):
+        """Queue a chunk to its decoder: False (nothing queued) if its queue or the tee's byte
+        budget is full."""
+        with self._lock:
+            if self._queued + len(chunk) > self.max_queued_bytes:
+                return False
+            try:
+                q.put_nowait(chunk)
+            except queue.Full:
+                return False
+            self._queued += len(chunk)
+            return True
 
     def _start(self):
         """A decoder for a new upload, or None when too many are in flight (normal path)."""
@@ -376,18 +404,17 @@ class StreamingUpload:
                         if rid not in streams:
                             streams[rid] = self._start()
                         st = streams[rid]
-                        if st is not None:
-                            try:
-                                st[0].put_nowait(bytes(request.data))
-                            except queue.Full:          # decoder too slow: give this upload up
-                                st[2].set()
-                                try:                        # drop the backlog (never block the upload)
-                                    while True:
-                                        st[0].get_nowait()
-                                except queue.Empty:
-                                    pass
-                                st[0].put_nowait(None)
-                                streams[rid] = None
+                        if st is not None and not self._enqueue(st[0], bytes(request.data)):
+                            st[2].set()                 # decoder too far behind: give this upload up
+                            try:                        # drop the backlog (never block the upload)
+                                while True:
+                                    c = st[0].get_nowait()
+                                    if c is not None:
+                                        self._dequeued(len(c))
+                            except queue.Empty:
+                                pass
+                            st[0].put_nowait(None)
+                            streams[rid] = None
                     if request.status == MODEL_STATUS_OK and not request.data and streams.get(rid) is not None:
                         q, fut, _ = streams.pop(rid)
                         q.put(None)

@@ -284,3 +284,25 @@ def test_decoder_streams_across_its_history_window(level):
         dec.feed(data[o:o + n])
         o += n
     _same_as_npload(data, DecodedUpdate(dec.finish(), None).arrays)
+
+
+def test_streaming_upload_tee_byte_budget():
+    """The tee's byte budget over all streams (max_queued_bytes): an upload whose decoder cannot run
+    is abandoned once its queued chunks would pass it, even with room in its own queue; every
+    queued byte is accounted back once the streams end."""
+    store = MemoryModelStore()
+    h = _Handler()
+    svc = StreamingUpload(MemoryModelService(store), h, workers=1, pinned=False, max_queued_chunks=10_000,
+                          max_queued_bytes=20_000)
+    blocker = threading.Event()
+    svc._pool.submit(blocker.wait)
+    data = _savez([np.arange(40_000, dtype=np.float32)])
+    svc.Upload(upload_requests(data, "big", chunk=1000), None)          # 160 chunks, 160 KB > 20 KB
+    blocker.set()
+    assert store.get("big").data == data
+    assert "big" not in h.adopted or h.adopted["big"].exception(timeout=30) is not None
+    ok = _savez([np.arange(1000, dtype=np.float32)])                   # 4 KB: within the budget
+    svc.Upload(upload_requests(ok, "small", chunk=1000), None)
+    assert h.adopted["small"].result(timeout=30) is not None
+    svc.close()
+    assert svc._queued == 0
