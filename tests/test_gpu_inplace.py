@@ -159,3 +159,32 @@ def test_sharded_fedopt_host_updates_in_place(pinned, monkeypatch):
         assert_lists_identical(agg.m, st.m, f"m {r}")
         assert_lists_identical(agg.v, st.v, f"v {r}")
         old = model
+
+
+def test_fedn_round_on_npz_updates_decodes_pinned_and_dmas_in_place(monkeypatch):
+    """The whole FEDn-shaped path on several devices: npz bytes in storage (ModelService.Upload),
+    FEDn's load_model_update through the plug-in's helper (members of 8 MiB+ decoded into pinned
+    blocks, FEDN_AMD_DEVICES naming two entries), the multi-device FedAvg pipeline DMAing those
+    tensors in place — bit-exact against the oracle on the decoded arrays."""
+    from fedn_amd.aggregators.fedavg import Aggregator
+    from fedn_amd.helper import Helper
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    monkeypatch.setenv("FEDN_AMD_DEVICES", f"{DEV},{DEV}")
+    monkeypatch.delenv("FEDN_AMD_DECODE_PINNED", raising=False)
+    rng = np.random.default_rng(97)
+    base = [rng.standard_normal(s).astype(np.float32) for s in SHAPES]
+    ups, ns = _clients(rng, base, 4)
+    h = Helper()
+    uh = MemoryUpdateHandler()
+    for u, n in zip(ups, ns):
+        b = io.BytesIO()
+        h.save(u, b)
+        uh.submit_bytes(b.getvalue(), n)
+    agg = Aggregator(uh)
+    model, data = agg.combine_models(helper=h)
+    want, nr = ref.fedavg_combine(list(zip(ups, ns)))
+    assert data["nr_aggregated_models"] == nr == 4
+    assert_lists_identical(model, want, "npz -> pinned decode -> in-place H2D")
+    big = sum(int(np.prod(s)) * 4 for s in SHAPES if int(np.prod(s)) * 4 >= (8 << 20))
+    assert data["bytes_h2d_in_place"] >= 3 * big        # the first update may be staged differently
+    torch.cuda.synchronize()
