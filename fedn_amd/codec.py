@@ -79,6 +79,9 @@ def load_lib():
                                             ctypes.c_void_p, ctypes.c_int64]          # destination buffer window
                 lib.fnpz_inflate_raw.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
                                                  ctypes.c_int64, ctypes.POINTER(ctypes.c_int)]
+                lib.fnpz_parallel_config.restype = None
+                lib.fnpz_parallel_config.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                                                     ctypes.POINTER(ctypes.c_int64)]
                 lib.fnpz_crc32.restype = ctypes.c_uint32
                 lib.fnpz_crc32.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int64]
                 lib.fnpz_gather_start.restype = ctypes.c_int64
@@ -201,6 +204,14 @@ def inflate_raw(data, out_len, window=0):
     _check(lib.fnpz_inflate_raw(src.ctypes.data if src.size else None, src.size, out.ctypes.data, out_len, window,
                                 ctypes.byref(end)))
     return out[:out_len].tobytes(), bool(end.value)
+
+
+def parallel_config(min_member=0, min_chunk=0):
+    """Thresholds of the parallel decode of one large deflate stream (fnpz_parallel_config; 0 keeps
+    a value); returns (decodes that went parallel, decodes that fell back) so far."""
+    ok, fb = ctypes.c_int64(0), ctypes.c_int64(0)
+    load_lib().fnpz_parallel_config(int(min_member), int(min_chunk), ctypes.byref(ok), ctypes.byref(fb))
+    return ok.value, fb.value
 
 
 def crc32(data, crc=0):

@@ -17,6 +17,7 @@
 #pragma once
 
 #include <algorithm>
+#include <vector>
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
@@ -268,7 +269,8 @@ inline bool build_table(const uint8_t* lens, int n, Alphabet a, int root, uint32
 
 class Inflate {
   public:
-    enum Status { kOk = 0, kFull = 1, kEnd = 2, kNeed = 3, kCorrupt = -1 };
+    enum Status { kOk = 0, kFull = 1, kEnd = 2, kNeed = 3, kStop = 4, kSwitch = 5, kCorrupt = -1 };
+    static constexpr uint64_t kNoStop = ~(uint64_t)0;
 
     Inflate(const uint8_t* in, size_t n) : in_(in), in_end_(in + n), in_start_(in) {}
 
@@ -284,6 +286,138 @@ class Inflate {
     }
     // the next input byte not loaded into the bit buffer yet
     const uint8_t* input_pos() const { return in_; }
+
+    // ---- parallel decode of one stream (npz_codec.cpp inflate_parallel) ----------------------
+    // Restart at bit ``bit`` of the input (a block header there), every state reset.
+    void restart_at(uint64_t bit) {
+        in_ = in_start_ + bit / 8;
+        bits_ = 0;
+        nbits_ = 0;
+        zeros_ = 0;
+        state_ = kHeader;
+        final_ = false;
+        more_ = false;
+        stored_left_ = 0;
+        pend_len_ = pend_dist_ = 0;
+        err_line_ = 0;
+        last_marker_ = 32767;                                   // run_markers(): the window's markers
+        if (bit % 8) {
+            need((unsigned)(bit % 8));
+            drop((unsigned)(bit % 8));
+        }
+    }
+    // Could a dynamic-Huffman block header start at input bit ``bit``? The cheap field checks only
+    // (type 2, <= 286 literal/length and <= 30 distance codes, a complete precode); the block
+    // finder then parses and trial-decodes the survivors.
+    static bool maybe_dynamic_header(const uint8_t* base, size_t n, uint64_t bit) {
+        const size_t byte = (size_t)(bit / 8);
+        if (byte + 10 > n) return false;
+        uint64_t v;
+        std::memcpy(&v, base + byte, 8);
+        v >>= bit % 8;                                          // >= 56 valid bits
+        if (((v >> 1) & 3) != 2) return false;
+        if (((v >> 3) & 31) > 29 || ((v >> 8) & 31) > 29) return false;
+        const int hclen = (int)((v >> 13) & 15) + 4;
+        static const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+        uint64_t w;
+        std::memcpy(&w, base + byte + 2, 8);                    // the precode lengths: bits 17 ..
+        w >>= (bit % 8) + 1;
+        int count[8] = {0};
+        for (int i = 0; i < hclen; ++i) count[(w >> (3 * i)) & 7]++;
+        (void)order;
+        int left = 1;
+        for (int l = 1; l <= 7; ++l) {
+            left = (left << 1) - count[l];
+            if (left < 0) return false;
+        }
+        return left == 0;                                       // zlib: the precode must be complete
+    }
+
+    // run() / run_markers() return kStop at the block header at input bit ``bit`` (kCorrupt if a
+    // block runs past it: it was not a block boundary of this stream)
+    void stop_at(uint64_t bit) { stop_bit_ = bit; }
+    uint64_t bit_pos() const { return (uint64_t)(in_ - in_start_) * 8 + (uint64_t)zeros_ * 8 - nbits_; }
+
+    // Marker mode: decode with the 32 KiB before the start unknown. ``out`` starts with 32768
+    // markers, value 256 + i standing for byte i of that unknown window; literals append their
+    // byte, copies copy values (markers included), so every output value is a byte or the marker
+    // of the window byte it equals. Returns kSwitch once the last 32 KiB of output hold no marker
+    // (the byte decoder can take over: run() with those bytes as its window), kStop / kEnd /
+    // kCorrupt as run(), kFull past ``max_out`` values.
+    int run_markers(std::vector<uint16_t>& out, size_t max_out) {
+        for (;;) {
+            if (out.size() >= 65536 && out.size() - 1 - last_marker_ >= 32768) return kSwitch;
+            if (out.size() >= max_out) return kFull;
+            if (state_ == kHeader) {
+                if (stop_bit_ != kNoStop) {
+                    const uint64_t b = bit_pos();
+                    if (b == stop_bit_) return kStop;
+                    if (b > stop_bit_) return corrupt(__LINE__);
+                }
+                if (final_) return kEnd;
+                if (!need(3)) return corrupt(__LINE__);
+                final_ = (bits_ & 1) != 0;
+                const uint32_t type = (uint32_t)(bits_ >> 1) & 3;
+                drop(3);
+                if (type == 0) {
+                    if (!start_stored()) return corrupt(__LINE__);
+                } else if (type == 1) {
+                    fixed_tables();
+                    state_ = kHuff;
+                } else if (type == 2) {
+                    if (!dynamic_tables()) return corrupt(__LINE__);
+                    state_ = kHuff;
+                } else {
+                    return corrupt(__LINE__);
+                }
+                continue;
+            }
+            if (state_ == kStored) {
+                while (stored_left_ && in_ < in_end_ && out.size() < max_out) {
+                    out.push_back(*in_++);
+                    --stored_left_;
+                }
+                if (stored_left_) {
+                    if (out.size() >= max_out) return kFull;
+                    return corrupt(__LINE__);
+                }
+                state_ = kHeader;
+                continue;
+            }
+            // one Huffman symbol
+            if (!refill_slow()) return corrupt(__LINE__);
+            const uint32_t e = lit_entry();
+            if (e & F_LIT) {
+                drop(e_len(e));
+                if (overran()) return corrupt(__LINE__);
+                out.push_back((uint16_t)e_value(e));
+                continue;
+            }
+            if (e & F_EOB) {
+                drop(e_len(e));
+                if (overran()) return corrupt(__LINE__);
+                state_ = kHeader;
+                continue;
+            }
+            if (!(e & F_LEN)) return corrupt(__LINE__);
+            drop(e_len(e));
+            const uint32_t xb = e_extra(e);
+            const size_t len = e_value(e) + ((uint32_t)bits_ & ((1u << xb) - 1));
+            drop(xb);
+            const uint32_t d = dist_entry();
+            if (!(d & F_DIST)) return corrupt(__LINE__);
+            drop(e_len(d));
+            const uint32_t db = e_extra(d);
+            const size_t dist = e_value(d) + ((uint32_t)bits_ & ((1u << db) - 1));
+            drop(db);
+            if (overran() || dist > out.size()) return corrupt(__LINE__);
+            for (size_t k = 0; k < len; ++k) {
+                const uint16_t v = out[out.size() - dist];
+                if (v >= 256) last_marker_ = out.size();
+                out.push_back(v);
+            }
+        }
+    }
 
     // Decode into [*out, out_end): returns kFull when the window is full (call again with the next
     // window), kEnd after the final block (the stream's output is complete), kCorrupt on an invalid
@@ -303,6 +437,11 @@ class Inflate {
                 if (pend_len_) { rc = kFull; break; }
             }
             if (state_ == kHeader) {
+                if (stop_bit_ != kNoStop) {
+                    const uint64_t b = bit_pos();
+                    if (b == stop_bit_) { rc = kStop; break; }
+                    if (b > stop_bit_) { rc = corrupt(__LINE__); break; }
+                }
                 if (final_) { rc = kEnd; break; }
                 // a full window at the end of a non-final range (a block of a sync-flushed stream,
                 // read on its own): nothing more to decode here
@@ -375,6 +514,8 @@ class Inflate {
     size_t stored_left_ = 0;
     size_t pend_len_ = 0, pend_dist_ = 0;
     int err_line_ = 0;
+    uint64_t stop_bit_ = kNoStop;
+    size_t last_marker_ = 0;             // run_markers(): index of the last marker written
     uint32_t lit_[kLitTable];
     uint32_t dist_[kDistTable];
 

@@ -333,10 +333,217 @@ int inflate_split(const uint8_t* in, int64_t inlen, uint8_t* hdr, int64_t hlen, 
     return 0;
 }
 
-int decode_one(const uint8_t* a, const fnpz_entry& e, void* dst, char* err, size_t errlen) {
+// ---------------------------------------------------------------------------------------
+// One deflate stream decoded on several threads (FEDn's np.savez_compressed writes one stream
+// per tensor; a model dominated by one large tensor would decode on one core). The compressed
+// bytes are cut into ``threads`` ranges; in each range after the first, the first position where
+// a dynamic-Huffman block header parses and trial-decodes is taken as a chunk start. Chunk t
+// decodes from its start to the next chunk's start — it must arrive EXACTLY at that bit on a block
+// header, which proves by induction from the stream's own start that every chunk start is a real
+// block boundary. A chunk begins in marker mode (its 32 KiB of history unknown: copies from it
+// carry markers, Inflate::run_markers) until its last 32 KiB hold no marker, then runs the byte
+// decoder; once the chunks before it are known its markers are replaced by the bytes they stand
+// for. The member's CRC-32 over the assembled output is the final check. Any failure (no block
+// found, a chunk that does not meet the next start, a marker before the stream's start, a CRC
+// mismatch) returns -1 and the caller decodes the stream sequentially: the result never depends
+// on the speculation.
+// ---------------------------------------------------------------------------------------
+struct GrowBuf {                                  // uninitialised, growable byte buffer
+    std::unique_ptr<uint8_t[]> p;
+    size_t cap = 0;
+    void reserve_keep(size_t need, size_t keep) {
+        if (need <= cap) return;
+        size_t c = std::max(need, cap + cap / 2);
+        std::unique_ptr<uint8_t[]> q(new uint8_t[c]);
+        if (keep) std::memcpy(q.get(), p.get(), keep);
+        p.swap(q);
+        cap = c;
+    }
+};
+
+struct ParChunk {
+    uint64_t start = 0;                          // input bit of the block header it starts at
+    std::vector<uint16_t> mark;                  // marker-mode output; [0, 32768) the unknown window
+    GrowBuf body;                                // byte-mode output; [0, hist) the window it started with
+    size_t hist = 0, body_len = 0;
+    std::vector<uint8_t> prefix;                 // mark's output resolved to bytes
+    int rc = 0;
+    size_t len() const { return prefix.size() + (body_len - hist); }
+    size_t cap_left() const { return body.cap - body_len; }
+};
+
+// byte-mode decode into c.body from c.body_len until a stop / the end
+int par_bytes(fnpz_fast::Inflate& d, ParChunk& c, size_t expect) {
+    for (;;) {
+        if (c.cap_left() < (1u << 20)) c.body.reserve_keep(c.body_len + std::max<size_t>(expect / 4, 4u << 20), c.body_len);
+        uint8_t* o = c.body.p.get() + c.body_len;
+        const int rc = d.run(&o, c.body.p.get() + c.body.cap, c.body.p.get());
+        c.body_len = (size_t)(o - c.body.p.get());
+        if (rc == fnpz_fast::Inflate::kFull) continue;
+        return rc;
+    }
+}
+
+// the ``want`` (<= 32768) bytes of logical output right before chunk t, into the end of win[32768]
+void chunk_tail(const std::vector<ParChunk>& ch, int t, size_t want, uint8_t* win) {
+    size_t got = 0;
+    for (int u = t - 1; u >= 0 && got < want; --u) {
+        const ParChunk& c = ch[u];
+        // chunk u's output: prefix, then body[hist, body_len)
+        const size_t blen = c.body_len - c.hist;
+        size_t k = std::min(want - got, blen);
+        if (k) std::memcpy(win + 32768 - got - k, c.body.p.get() + c.body_len - k, k);
+        got += k;
+        if (got < want) {
+            k = std::min(want - got, c.prefix.size());
+            if (k) std::memcpy(win + 32768 - got - k, c.prefix.data() + c.prefix.size() - k, k);
+            got += k;
+        }
+    }
+}
+
+template <class F>
+void parallel_for(int n, int threads, F&& f);
+
+// fnpz_parallel_config: streams of at least g_par_min compressed bytes, chunks of at least
+// g_par_chunk; counters of the decodes that went parallel / fell back
+std::atomic<int64_t> g_par_min{16 << 20}, g_par_chunk{4 << 20}, g_par_ok{0}, g_par_fallback{0};
+
+int inflate_parallel(const uint8_t* in, int64_t inlen, uint8_t* hdr, int64_t hlen, uint8_t* dst, int64_t dlen,
+                     int threads, uint32_t* crc_out) {
+    using fnpz_fast::Inflate;
+    const int64_t min_chunk = std::max<int64_t>(g_par_chunk.load(), 64 << 10);
+    const int T = (int)std::min<int64_t>(threads, inlen / min_chunk);
+    if (T < 2) return -1;
+    const uint64_t total = (uint64_t)(hlen + dlen);
+    // 1. chunk starts: the first block header in each range that parses and trial-decodes
+    std::vector<uint64_t> starts((size_t)T, 0);
+    std::vector<char> found((size_t)T, 0);
+    parallel_for(T - 1, T - 1, [&](int j) {
+        const int t = j + 1;
+        const uint64_t lo = (uint64_t)inlen * (uint64_t)t / (uint64_t)T * 8;
+        const uint64_t hi = std::min<uint64_t>((uint64_t)inlen * (uint64_t)(t + 1) / (uint64_t)T * 8, lo + (64ull << 20));
+        std::unique_ptr<Inflate> d(new Inflate(in, (size_t)inlen));
+        std::vector<uint16_t> scratch;
+        for (uint64_t b = lo; b < hi; ++b) {
+            if (!Inflate::maybe_dynamic_header(in, (size_t)inlen, b)) continue;
+            d->restart_at(b);
+            scratch.resize(32768);
+            for (int i = 0; i < 32768; ++i) scratch[(size_t)i] = (uint16_t)(256 + i);
+            const int rc = d->run_markers(scratch, 32768 + 16384);
+            if (rc == Inflate::kFull || (rc == Inflate::kEnd && scratch.size() > 32768)) {
+                starts[(size_t)t] = b;
+                found[(size_t)t] = 1;
+                return;
+            }
+        }
+    });
+    std::vector<uint64_t> st(1, 0);
+    for (int t = 1; t < T; ++t)
+        if (found[(size_t)t] && starts[(size_t)t] > st.back()) st.push_back(starts[(size_t)t]);
+    const int C = (int)st.size();
+    if (C < 2) return -1;
+    // 2. every chunk from its start to the next one's
+    std::vector<ParChunk> ch((size_t)C);
+    const size_t expect = (size_t)(total / (uint64_t)C) + (1u << 20);
+    parallel_for(C, C, [&](int t) {
+        ParChunk& c = ch[(size_t)t];
+        std::unique_ptr<Inflate> d(new Inflate(in, (size_t)inlen));
+        d->restart_at(st[(size_t)t]);
+        d->stop_at(t + 1 < C ? st[(size_t)t + 1] : Inflate::kNoStop);
+        if (t == 0) {
+            c.rc = par_bytes(*d, c, expect);
+            return;
+        }
+        c.mark.resize(32768);
+        for (int i = 0; i < 32768; ++i) c.mark[(size_t)i] = (uint16_t)(256 + i);
+        int rc = d->run_markers(c.mark, std::min<size_t>((size_t)total, 64u << 20) + 32768);
+        if (rc == Inflate::kSwitch) {                             // the last 32 KiB hold bytes only
+            c.body.reserve_keep(expect + 32768, 0);
+            const size_t m = c.mark.size();
+            for (size_t i = 0; i < 32768; ++i) c.body.p[i] = (uint8_t)c.mark[m - 32768 + i];
+            c.hist = c.body_len = 32768;
+            rc = par_bytes(*d, c, expect);
+        }
+        c.rc = rc;
+    });
+    uint64_t sum = 0;
+    for (int t = 0; t < C; ++t) {
+        const ParChunk& c = ch[(size_t)t];
+        if (c.rc != (t + 1 < C ? Inflate::kStop : Inflate::kEnd)) return -1;
+        sum += (c.mark.empty() ? 0 : c.mark.size() - 32768) + (c.body_len - c.hist);
+    }
+    if (sum != total) return -1;
+    // 3. markers -> bytes, chunk by chunk (each needs the 32 KiB before it)
+    std::vector<uint64_t> off((size_t)C + 1, 0);
+    std::vector<uint8_t> win(32768);
+    for (int t = 0; t < C; ++t) {
+        ParChunk& c = ch[(size_t)t];
+        if (t > 0) {
+            const size_t avail = (size_t)std::min<uint64_t>(32768, off[(size_t)t]);
+            chunk_tail(ch, t, avail, win.data());
+            // output = mark[32768, m) resolved, then body[hist, body_len) (body[0, hist) repeats the
+            // mark's last 32 KiB as the byte decoder's window)
+            const size_t m = c.mark.size();
+            c.prefix.resize(m - 32768);
+            for (size_t i = 32768; i < m; ++i) {
+                const uint16_t v = c.mark[i];
+                if (v < 256) {
+                    c.prefix[i - 32768] = (uint8_t)v;
+                } else {
+                    const size_t w = (size_t)(v - 256);
+                    if (w < 32768 - avail) return -1;            // a reference before the stream's start
+                    c.prefix[i - 32768] = win[w];
+                }
+            }
+            std::vector<uint16_t>().swap(c.mark);
+        }
+        off[(size_t)t + 1] = off[(size_t)t] + c.len();
+    }
+    // 4. into [hdr | dst], CRC-32 per chunk, combined in order
+    std::vector<uint32_t> crcs((size_t)C, 0);
+    parallel_for(C, C, [&](int t) {
+        const ParChunk& c = ch[(size_t)t];
+        uint64_t o = off[(size_t)t];
+        uint32_t cr = 0;
+        auto put = [&](const uint8_t* src, size_t n) {
+            cr = fnpz_fast::crc32(cr, src, n);
+            while (n) {
+                if (o < (uint64_t)hlen) {
+                    const size_t k = (size_t)std::min<uint64_t>(n, (uint64_t)hlen - o);
+                    std::memcpy(hdr + o, src, k);
+                    o += k, src += k, n -= k;
+                } else {
+                    std::memcpy(dst + (o - (uint64_t)hlen), src, n);
+                    o += n;
+                    n = 0;
+                }
+            }
+        };
+        if (!c.prefix.empty()) put(c.prefix.data(), c.prefix.size());
+        if (c.body_len > c.hist) put(c.body.p.get() + c.hist, c.body_len - c.hist);
+        crcs[(size_t)t] = cr;
+    });
+    uLong crc = crcs[0];
+    for (int t = 1; t < C; ++t) crc = crc32_combine(crc, crcs[(size_t)t], (z_off_t)ch[(size_t)t].len());
+    *crc_out = (uint32_t)crc;
+    return 0;
+}
+
+int decode_one(const uint8_t* a, const fnpz_entry& e, void* dst, char* err, size_t errlen, int threads) {
     uint8_t* out = static_cast<uint8_t*>(dst);
     std::vector<uint8_t> hdr((size_t)e.npy_header);
     uint32_t crc = 0;
+    if (e.method == 8 && threads > 1 && e.comp_size >= g_par_min.load() &&
+        e.comp_size >= 2 * std::max<int64_t>(g_par_chunk.load(), 64 << 10)) {
+        uint32_t pc = 0;
+        if (inflate_parallel(a + e.data_offset, e.comp_size, hdr.data(), e.npy_header, out, e.nbytes, threads, &pc) == 0 &&
+            pc == e.crc32) {
+            g_par_ok++;
+            return FNPZ_OK;
+        }
+        g_par_fallback++;                // the speculation did not hold (or the stream is bad): in order
+    }
     if (e.method == 8) {
         int line = 0;
         if (inflate_split(a + e.data_offset, e.comp_size, hdr.data(), e.npy_header, out, e.nbytes, &crc, &line))
@@ -672,6 +879,13 @@ int fnpz_inflate_raw(const uint8_t* in, int64_t in_len, uint8_t* out, int64_t ou
     return FNPZ_OK;
 }
 
+void fnpz_parallel_config(int64_t min_member, int64_t min_chunk, int64_t* parallel, int64_t* fallback) {
+    if (min_member > 0) g_par_min = min_member;
+    if (min_chunk > 0) g_par_chunk = min_chunk;
+    if (parallel) *parallel = g_par_ok.load();
+    if (fallback) *fallback = g_par_fallback.load();
+}
+
 uint32_t fnpz_crc32(uint32_t crc, const uint8_t* data, int64_t len) {
     return len > 0 ? fnpz_fast::crc32(crc, data, (size_t)len) : crc;
 }
@@ -714,7 +928,8 @@ int fnpz_read(const uint8_t* archive, int64_t len, const fnpz_entry* entries, in
         void* dst = dsts[tasks[t].member];
         char msg[300] = "";
         if (tasks[t].block < 0) {
-            rcs[t] = decode_one(archive, e, dst, msg, sizeof(msg));
+            // threads the other tasks leave idle decode this member's stream in parallel
+            rcs[t] = decode_one(archive, e, dst, msg, sizeof(msg), std::max(1, threads / (int)tasks.size()));
         } else {
             const uint8_t* ix = archive + e.index_offset;
             const uint64_t B = rd64(ix + 8);

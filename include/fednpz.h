@@ -104,6 +104,15 @@ int fnpz_stream_next(fnpz_stream* stream, uint8_t* out, int64_t out_cap, int* ev
  * truncated stream, or one that ends before out is full. */
 int fnpz_inflate_raw(const uint8_t* in, int64_t in_len, uint8_t* out, int64_t out_len, int64_t window, int* stream_end);
 
+/* Parallel decode of ONE large deflate stream (round 4, fnpz_read): a member of at least
+ * min_member compressed bytes (default 16 MiB) is cut into chunks of at least min_chunk bytes
+ * (default 4 MiB) decoded by the threads the other members leave idle — chunk starts found as
+ * block headers, back-references into the unknown history carried as markers, every chunk
+ * verified to end exactly where the next begins, the member's CRC-32 checked; anything that does
+ * not hold falls back to the sequential decode. Values <= 0 keep the current setting.
+ * *parallel / *fallback (may be NULL): decodes that went parallel / fell back so far. */
+void fnpz_parallel_config(int64_t min_member, int64_t min_chunk, int64_t* parallel, int64_t* fallback);
+
 /* CRC-32 of the zip format with zlib's convention (crc32(0, ...) starts; pass the previous value to
  * continue), folded with carry-less multiplies where the CPU has them (ABI 5). */
 uint32_t fnpz_crc32(uint32_t crc, const uint8_t* data, int64_t len);

@@ -157,3 +157,65 @@ def _zlib_partial(z, piece=16):
         except zlib.error:
             break
     return out
+
+
+def _npz_one(x, level=6, strategy=zlib.Z_DEFAULT_STRATEGY):
+    """A one-member npz like np.savez_compressed's (its container; any deflate level / strategy)."""
+    import io
+    import struct
+    bio = io.BytesIO()
+    np.lib.format.write_array(bio, x, allow_pickle=False)
+    npy = bio.getvalue()
+    comp = _deflate(npy, level, strategy)        # zipfile has no strategy knob: the records by hand
+    name = b"0.npy"
+    crc = zlib.crc32(npy)
+    local = struct.pack("<IHHHHHIIIHH", 0x04034B50, 20, 0, 8, 0, 0x21, crc, len(comp), len(npy), len(name), 0) + name
+    central = struct.pack("<IHHHHHHIIIHHHHHII", 0x02014B50, 20, 20, 0, 8, 0, 0x21, crc, len(comp), len(npy),
+                          len(name), 0, 0, 0, 0, 0, 0) + name
+    eocd = struct.pack("<IHHHHIIH", 0x06054B50, 0, 0, 1, 1, len(central), len(local) + len(comp), 0)
+    return local + comp + central + eocd
+
+
+@pytest.fixture
+def _small_parallel():
+    codec.parallel_config(64 << 10, 16 << 10)
+    yield
+    codec.parallel_config(16 << 20, 4 << 20)
+
+
+def test_parallel_decode_of_one_stream_matches_numpy(_small_parallel):
+    """One large deflate stream split over threads: chunk starts found as block headers,
+    back-references across chunk boundaries (a noisy 30,011-byte period: matches reach ~30 KB back)
+    carried as markers, sparse runs, fp32 weights, text; levels 1 / 6 / 9 and the zlib strategies.
+    Every decode equals np.load; streams without findable dynamic blocks (stored, fixed codes) fall
+    back to the sequential decode, with the same result."""
+    rng = np.random.default_rng(21)
+    period = np.tile(rng.integers(0, 255, 30_011, dtype=np.uint8), 80)
+    hit = rng.random(period.size) < 0.15                 # 15 % noise: still matched ~30 KB back
+    period[hit] = rng.integers(0, 255, int(hit.sum()), dtype=np.uint8)
+    xs = {"weights": rng.standard_normal(600_000).astype(np.float32),
+          "period": period,
+          "sparse": np.where(rng.random(2_000_000) < 0.97, 0, rng.integers(1, 255, 2_000_000)).astype(np.uint8),
+          "text": np.frombuffer((b"federated averaging of model updates " * 60_000), dtype=np.uint8).copy()}
+    before = codec.parallel_config()
+    for name, x in xs.items():
+        for level, strategy in ((1, zlib.Z_DEFAULT_STRATEGY), (6, zlib.Z_DEFAULT_STRATEGY), (9, zlib.Z_FILTERED),
+                                (6, zlib.Z_RLE), (6, zlib.Z_HUFFMAN_ONLY), (6, zlib.Z_FIXED), (0, 0)):
+            raw = _npz_one(x, level, strategy)
+            got = codec.load_npz(raw, threads=8)[0]
+            assert got.dtype == x.dtype and np.array_equal(got, x), (name, level, strategy)
+    after = codec.parallel_config()
+    assert after[0] - before[0] >= 10                   # most of them went parallel
+
+
+def test_parallel_decode_rejects_corruption(_small_parallel):
+    """A corrupted large stream fails loudly (CRC-32 or an invalid code), parallel or not."""
+    rng = np.random.default_rng(22)
+    x = rng.standard_normal(600_000).astype(np.float32)
+    raw = bytearray(_npz_one(x))
+    for k in range(20):
+        bad = bytearray(raw)
+        pos = 60 + int(rng.integers(len(raw) // 3, len(raw) - 200))
+        bad[pos] ^= 1 << int(rng.integers(8))
+        with pytest.raises(codec.CodecError):
+            codec.load_npz(bytes(bad), threads=8)
