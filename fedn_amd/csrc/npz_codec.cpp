@@ -408,6 +408,7 @@ void parallel_for(int n, int threads, F&& f);
 // fnpz_parallel_config: streams of at least g_par_min compressed bytes, chunks of at least
 // g_par_chunk; counters of the decodes that went parallel / fell back
 std::atomic<int64_t> g_par_min{16 << 20}, g_par_chunk{4 << 20}, g_par_ok{0}, g_par_fallback{0};
+std::atomic<int> g_par_busy{0};                 // threads held by parallel decodes in flight
 
 int inflate_parallel(const uint8_t* in, int64_t inlen, uint8_t* hdr, int64_t hlen, uint8_t* dst, int64_t dlen,
                      int threads, uint32_t* crc_out) {
@@ -534,11 +535,17 @@ int decode_one(const uint8_t* a, const fnpz_entry& e, void* dst, char* err, size
     uint8_t* out = static_cast<uint8_t*>(dst);
     std::vector<uint8_t> hdr((size_t)e.npy_header);
     uint32_t crc = 0;
-    if (e.method == 8 && threads > 1 && e.comp_size >= g_par_min.load() &&
+    // concurrent reads (the aggregators' read-ahead decodes several updates at once) share the
+    // threads: each parallel decode takes what the others leave of ``threads``
+    const int grant = threads > 1 ? std::max(1, std::min(threads, threads - g_par_busy.load())) : 1;
+    if (e.method == 8 && grant > 1 && e.comp_size >= g_par_min.load() &&
         e.comp_size >= 2 * std::max<int64_t>(g_par_chunk.load(), 64 << 10)) {
+        g_par_busy += grant;
         uint32_t pc = 0;
-        if (inflate_parallel(a + e.data_offset, e.comp_size, hdr.data(), e.npy_header, out, e.nbytes, threads, &pc) == 0 &&
-            pc == e.crc32) {
+        const bool ok = inflate_parallel(a + e.data_offset, e.comp_size, hdr.data(), e.npy_header, out, e.nbytes, grant,
+                                         &pc) == 0 && pc == e.crc32;
+        g_par_busy -= grant;
+        if (ok) {
             g_par_ok++;
             return FNPZ_OK;
         }
