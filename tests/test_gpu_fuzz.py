@@ -8,6 +8,8 @@ into the ingest, and sliced over two device entries in one process (multidev.py;
 listed twice), from the host or staged on arrival as parameter slices. FedAvg one round, FedOpt (adam / yogi /
 adagrad, random hyper-parameters) three rounds with m / v carried. Bar: bit-exact values and dtypes,
 every update counted — the same bar as the golden fixtures, on cases no fixture spells out."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -16,6 +18,15 @@ from golden_io import assert_lists_identical
 from oracle import numpy_ref as ref
 
 pytestmark = pytest.mark.gpu
+
+# extended runs: FEDN_AMD_FUZZ_BASE shifts every seed range, FEDN_AMD_FUZZ_SCALE multiplies its length
+_BASE = int(os.environ.get("FEDN_AMD_FUZZ_BASE", "0"))
+_SCALE = float(os.environ.get("FEDN_AMD_FUZZ_SCALE", "1"))
+
+
+def _seeds(n):
+    return range(_BASE, _BASE + max(1, int(n * _SCALE)))
+
 
 DEV = "cuda:0"
 DTYPES = [np.float32, np.float64, np.float16]
@@ -116,7 +127,7 @@ def _helper(route):
 
 
 @pytest.mark.parametrize("route", ROUTES)
-@pytest.mark.parametrize("seed", range(48))
+@pytest.mark.parametrize("seed", _seeds(48))
 def test_fuzz_fedavg(seed, route, monkeypatch):
     rng = np.random.default_rng(1000 + seed)
     shapes, dtypes = _layout(rng)
@@ -137,7 +148,7 @@ def test_fuzz_fedavg(seed, route, monkeypatch):
 
 
 @pytest.mark.parametrize("route", ROUTES)
-@pytest.mark.parametrize("seed", range(30))
+@pytest.mark.parametrize("seed", _seeds(30))
 def test_fuzz_fedopt(seed, route, monkeypatch):
     rng = np.random.default_rng(2000 + seed)
     shapes, dtypes = _layout(rng)

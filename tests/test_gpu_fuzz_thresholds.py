@@ -14,7 +14,7 @@ import torch
 
 from golden_io import assert_lists_identical
 from oracle import numpy_ref as ref
-from test_gpu_fuzz import _aggregator, _clients, _handlers, _helper, _layout, _submit_all, _values
+from test_gpu_fuzz import _aggregator, _clients, _handlers, _helper, _layout, _seeds, _submit_all, _values
 
 
 ROUTES = ["host", "staged", "npz", "sliced", "staged_sliced"]
@@ -88,7 +88,7 @@ def test_fuzz_thresholds_reach_the_paths():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("route", ROUTES)
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", _seeds(40))
 def test_fuzz_thresholds_fedavg(seed, route, monkeypatch, _gpu):
     t = _thresholds(seed, monkeypatch)
     rng = np.random.default_rng(3000 + seed)
@@ -111,7 +111,7 @@ def test_fuzz_thresholds_fedavg(seed, route, monkeypatch, _gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("route", ROUTES)
-@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("seed", _seeds(24))
 def test_fuzz_thresholds_fedopt(seed, route, monkeypatch, _gpu):
     t = _thresholds(100 + seed, monkeypatch)
     rng = np.random.default_rng(4000 + seed)
