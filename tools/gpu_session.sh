@@ -64,6 +64,16 @@ for s in $STEPS; do
       grep -v amdgpu.ids "$OUT/small_breakdown.log"
       timeout -k 10 300 python tools/profile_small.py --clients 10 > "$OUT/small_profile.log" 2>&1; rc=$?
       echo "profile rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    inflate)
+      # host npz decode / encode (CPU only): numpy vs the codec's decoder, one stream split over threads
+      timeout -k 10 600 python tools/bench_inflate.py > "$OUT/inflate.log" 2>&1; rc=$?
+      echo "inflate rc=$rc"; tail -2 "$OUT/inflate.log" | cut -c1-300; [ $rc -eq 0 ] || exit $rc ;;
+    fuzzx)
+      # the seeded fuzz on fresh seeds, 4x longer (FEDN_AMD_FUZZ_BASE / FEDN_AMD_FUZZ_SCALE override)
+      FEDN_AMD_FUZZ_BASE=${FEDN_AMD_FUZZ_BASE:-100000} FEDN_AMD_FUZZ_SCALE=${FEDN_AMD_FUZZ_SCALE:-4} \
+        timeout -k 10 1000 python -u -m pytest tests/test_gpu_fuzz.py tests/test_gpu_fuzz_thresholds.py -m gpu -q \
+        --timeout 240 --timeout-method thread -p no:cacheprovider > "$OUT/fuzzx.log" 2>&1; rc=$?
+      echo "fuzzx rc=$rc"; tail -2 "$OUT/fuzzx.log"; if fatal $rc; then exit $rc; fi ;;
     micro)
       timeout -k 10 600 python tools/microbench.py > "$OUT/micro.log" 2>&1; rc=$?
       echo "micro rc=$rc"; cat "$OUT/micro.log" | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc ;;
