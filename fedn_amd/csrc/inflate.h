@@ -153,8 +153,11 @@ inline uint32_t crc32(uint32_t crc, const uint8_t* p, size_t n) {
 // end-of-block, 7 length, 12 distance; no flag = an invalid code
 enum : uint32_t { K_INVALID = 0, K_LIT = 1, K_LEN = 2, K_EOB = 3, K_SUB = 4, K_DIST = 5 };
 constexpr uint32_t F_LIT = 1u << 31, F_SUB = 1u << 5, F_EOB = 1u << 6, F_LEN = 1u << 7, F_DIST = 1u << 12;
-constexpr int kLitRoot = 11, kDistRoot = 8, kPreRoot = 7;
-constexpr int kLitTable = (1 << kLitRoot) + 288 * 16, kDistTable = (1 << kDistRoot) + 32 * 128;
+#ifndef FNPZ_LIT_ROOT
+#define FNPZ_LIT_ROOT 11                  // root bits of the literal/length table (tools: build variants)
+#endif
+constexpr int kLitRoot = FNPZ_LIT_ROOT, kDistRoot = 8, kPreRoot = 7;
+constexpr int kLitTable = (1 << kLitRoot) + 288 * (1 << (15 - kLitRoot)), kDistTable = (1 << kDistRoot) + 32 * 128;
 
 inline uint32_t entry(uint32_t len, uint32_t kind, uint32_t extra, uint32_t value) {
     static const uint32_t flag[6] = {0, F_LIT, F_LEN, F_EOB, F_SUB, F_DIST};
