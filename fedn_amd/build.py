@@ -27,6 +27,7 @@ def hipcc():
 
 NPZ_SRC = os.path.join(HERE, "csrc", "npz_codec.cpp")
 NPZ_HDR = os.path.join(ROOT, "include", "fednpz.h")
+NPZ_INFLATE = os.path.join(HERE, "csrc", "inflate.h")      # the codec's DEFLATE decoder + CRC-32
 NPZ_OUT = os.path.join(HERE, "libfednpz.so")
 
 
@@ -36,7 +37,7 @@ def _stale(out, *deps):
 
 def build_codec(force=False, verbose=True):
     """Host-side npz codec (C++17 + zlib, no GPU code)."""
-    if not force and not _stale(NPZ_OUT, NPZ_SRC, NPZ_HDR):
+    if not force and not _stale(NPZ_OUT, NPZ_SRC, NPZ_HDR, NPZ_INFLATE):
         return NPZ_OUT
     cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
     tmp = NPZ_OUT + ".tmp"
