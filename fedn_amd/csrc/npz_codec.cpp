@@ -423,7 +423,9 @@ int inflate_parallel(const uint8_t* in, int64_t inlen, uint8_t* hdr, int64_t hle
     parallel_for(T - 1, T - 1, [&](int j) {
         const int t = j + 1;
         const uint64_t lo = (uint64_t)inlen * (uint64_t)t / (uint64_t)T * 8;
-        const uint64_t hi = std::min<uint64_t>((uint64_t)inlen * (uint64_t)(t + 1) / (uint64_t)T * 8, lo + (64ull << 20));
+        // zlib ends a dynamic block every ~16 K symbols (tens of KB): 1 MiB of search finds one, and
+        // bounds the time lost on a stream without dynamic blocks (stored / fixed codes only)
+        const uint64_t hi = std::min<uint64_t>((uint64_t)inlen * (uint64_t)(t + 1) / (uint64_t)T * 8, lo + (8ull << 20));
         std::unique_ptr<Inflate> d(new Inflate(in, (size_t)inlen));
         std::vector<uint16_t> scratch;
         for (uint64_t b = lo; b < hi; ++b) {
