@@ -416,6 +416,9 @@ int inflate_parallel(const uint8_t* in, int64_t inlen, uint8_t* hdr, int64_t hle
     const int64_t min_chunk = std::max<int64_t>(g_par_chunk.load(), 64 << 10);
     const int T = (int)std::min<int64_t>(threads, inlen / min_chunk);
     if (T < 2) return -1;
+    // a stream that starts with a stored or fixed-code block (deflate's choice for incompressible
+    // bytes, or Z_FIXED) is not split: chunk starts are searched as dynamic-block headers only
+    if (((in[0] >> 1) & 3) != 2) return -1;
     const uint64_t total = (uint64_t)(hlen + dlen);
     // 1. chunk starts: the first block header in each range that parses and trial-decodes
     std::vector<uint64_t> starts((size_t)T, 0);
@@ -423,9 +426,9 @@ int inflate_parallel(const uint8_t* in, int64_t inlen, uint8_t* hdr, int64_t hle
     parallel_for(T - 1, T - 1, [&](int j) {
         const int t = j + 1;
         const uint64_t lo = (uint64_t)inlen * (uint64_t)t / (uint64_t)T * 8;
-        // zlib ends a dynamic block every ~16 K symbols (tens of KB): 1 MiB of search finds one, and
-        // bounds the time lost on a stream without dynamic blocks (stored / fixed codes only)
-        const uint64_t hi = std::min<uint64_t>((uint64_t)inlen * (uint64_t)(t + 1) / (uint64_t)T * 8, lo + (8ull << 20));
+        // zlib ends a block every 16 K symbols (<= ~30 KB of dynamic codes): 128 KiB of search finds
+        // one, and bounds the time lost on stretches without dynamic blocks (stored ones)
+        const uint64_t hi = std::min<uint64_t>((uint64_t)inlen * (uint64_t)(t + 1) / (uint64_t)T * 8, lo + (1ull << 20));
         std::unique_ptr<Inflate> d(new Inflate(in, (size_t)inlen));
         std::vector<uint16_t> scratch;
         for (uint64_t b = lo; b < hi; ++b) {
