@@ -513,14 +513,17 @@ int inflate_parallel(const uint8_t* in, int64_t inlen, uint8_t* hdr, int64_t hle
         uint64_t o = off[(size_t)t];
         uint32_t cr = 0;
         auto put = [&](const uint8_t* src, size_t n) {
+            cr = fnpz_fast::crc32(cr, src, n);
             while (n) {
-                // 64 KiB at a time: copied, then its CRC taken from the copy while it is in cache
-                uint8_t* to = o < (uint64_t)hlen ? hdr + o : dst + (o - (uint64_t)hlen);
-                size_t k = std::min<size_t>(n, 64u << 10);
-                if (o < (uint64_t)hlen) k = (size_t)std::min<uint64_t>(k, (uint64_t)hlen - o);
-                std::memcpy(to, src, k);
-                cr = fnpz_fast::crc32(cr, to, k);
-                o += k, src += k, n -= k;
+                if (o < (uint64_t)hlen) {
+                    const size_t k = (size_t)std::min<uint64_t>(n, (uint64_t)hlen - o);
+                    std::memcpy(hdr + o, src, k);
+                    o += k, src += k, n -= k;
+                } else {
+                    std::memcpy(dst + (o - (uint64_t)hlen), src, n);
+                    o += n;
+                    n = 0;
+                }
             }
         };
         if (!c.prefix.empty()) put(c.prefix.data(), c.prefix.size());
