@@ -194,10 +194,21 @@ inline uint32_t sym_entry(Alphabet a, int sym, uint32_t len) {
     }
 }
 
+struct Rev8 {
+    uint8_t t[256];
+    Rev8() {
+        for (int i = 0; i < 256; ++i) {
+            int r = 0;
+            for (int b = 0; b < 8; ++b) r |= ((i >> b) & 1) << (7 - b);
+            t[i] = (uint8_t)r;
+        }
+    }
+};
+
+// the low n (<= 16) bits of c, reversed (deflate packs Huffman codes most-significant bit first)
 inline uint32_t reverse_bits(uint32_t c, int n) {
-    uint32_t r = 0;
-    for (int i = 0; i < n; ++i) r |= ((c >> i) & 1u) << (n - 1 - i);
-    return r;
+    static const Rev8 rev;
+    return (((uint32_t)rev.t[c & 0xFF] << 8) | rev.t[(c >> 8) & 0xFF]) >> (16 - n);
 }
 
 // Canonical Huffman table of ``n`` code lengths (0 = unused) with a ``root``-bit first level and
@@ -210,8 +221,10 @@ inline bool build_table(const uint8_t* lens, int n, Alphabet a, int root, uint32
         count[lens[s]]++;
         if (lens[s] > maxlen) maxlen = lens[s];
     }
-    std::memset(table, 0, sizeof(uint32_t) * (size_t)(1 << root));       // K_INVALID everywhere
-    if (maxlen == 0) return a != Alphabet::kPre;                          // no codes (an all-literal block's distances)
+    if (maxlen == 0) {                                                    // no codes (an all-literal block's distances)
+        std::memset(table, 0, sizeof(uint32_t) * (size_t)(1 << root));   // K_INVALID everywhere
+        return a != Alphabet::kPre;
+    }
     count[0] = 0;
     int left = 1;
     for (int l = 1; l <= 15; ++l) {
@@ -220,6 +233,9 @@ inline bool build_table(const uint8_t* lens, int n, Alphabet a, int root, uint32
         if (left < 0) return false;                                        // over-subscribed
     }
     if (left > 0 && (a == Alphabet::kPre || maxlen != 1)) return false;   // incomplete (zlib's rule)
+    // a complete code fills every entry below; only the one incomplete case zlib allows (a single
+    // one-bit code) leaves entries that must read as invalid
+    if (left > 0) std::memset(table, 0, sizeof(uint32_t) * (size_t)(1 << root));
     int next[16];
     int code = 0;
     for (int l = 1; l <= 15; ++l) {
@@ -249,8 +265,7 @@ inline bool build_table(const uint8_t* lens, int n, Alphabet a, int root, uint32
             suboff[p] = off;
             off += 1 << sublen[p];
             if (off > cap) return false;
-            std::memset(table + suboff[p], 0, sizeof(uint32_t) * ((size_t)1 << sublen[p]));
-            table[p] = entry(0, K_SUB, sublen[p], (uint32_t)suboff[p]);
+            table[p] = entry(0, K_SUB, sublen[p], (uint32_t)suboff[p]);     // (complete: filled below)
         }
     }
     for (int s = 0; s < n; ++s) {
