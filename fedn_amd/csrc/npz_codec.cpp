@@ -936,7 +936,8 @@ int fnpz_read(const uint8_t* archive, int64_t len, const fnpz_entry* entries, in
     // small model's members (mnist-sized archives decode 1.8x faster on the calling thread alone)
     int64_t comp_total = 0;
     for (int i = 0; i < n; ++i) comp_total += entries[i].comp_size;
-    threads = (int)std::max<int64_t>(1, std::min<int64_t>(threads, comp_total >> 20));
+    const int64_t unit = std::max<int64_t>(1, std::min<int64_t>(1 << 20, g_par_chunk.load()));
+    threads = (int)std::max<int64_t>(1, std::min<int64_t>(threads, comp_total / unit));
     std::vector<int> rcs(tasks.size(), FNPZ_OK);
     std::vector<uLong> bcrc(tasks.size(), 0);
     std::vector<std::string> errs(tasks.size());
