@@ -159,14 +159,22 @@ def _zlib_partial(z, piece=16):
     return out
 
 
-def _npz_one(x, level=6, strategy=zlib.Z_DEFAULT_STRATEGY):
-    """A one-member npz like np.savez_compressed's (its container; any deflate level / strategy)."""
+def _npy(x):
     import io
-    import struct
     bio = io.BytesIO()
     np.lib.format.write_array(bio, x, allow_pickle=False)
-    npy = bio.getvalue()
-    comp = _deflate(npy, level, strategy)        # zipfile has no strategy knob: the records by hand
+    return bio.getvalue()
+
+
+def _npz_one(x, level=6, strategy=zlib.Z_DEFAULT_STRATEGY):
+    """A one-member npz like np.savez_compressed's (its container; any deflate level / strategy)."""
+    npy = _npy(x)
+    return _npz_member(npy, _deflate(npy, level, strategy))   # zipfile has no strategy knob
+
+
+def _npz_member(npy, comp):
+    """The zip records around one deflated .npy member, by hand."""
+    import struct
     name = b"0.npy"
     crc = zlib.crc32(npy)
     local = struct.pack("<IHHHHHIIIHH", 0x04034B50, 20, 0, 8, 0, 0x21, crc, len(comp), len(npy), len(name), 0) + name
@@ -219,3 +227,47 @@ def test_parallel_decode_rejects_corruption(_small_parallel):
         bad[pos] ^= 1 << int(rng.integers(8))
         with pytest.raises(codec.CodecError):
             codec.load_npz(bytes(bad), threads=8)
+
+
+def _spliced(npy, rng):
+    """One deflate stream over `npy` made of runs of segments: each run from its own compressor
+    (random level and strategy, stored included), segments within a run separated by sync / full
+    flushes (so back-references cross some segment boundaries and not others), every run but the
+    last ending on a sync flush — byte-aligned, non-final, so the runs concatenate into one valid
+    stream of mixed block types."""
+    cuts = np.sort(rng.choice(np.arange(1, len(npy)), size=int(rng.integers(3, 12)), replace=False))
+    segs = np.split(np.frombuffer(npy, np.uint8), cuts)
+    out, c = [], None
+    for i, seg in enumerate(segs):
+        if c is None or rng.random() < 0.4:
+            level = int(rng.choice([0, 1, 6, 9]))
+            c = zlib.compressobj(level, zlib.DEFLATED, -15, 8, int(rng.choice(STRATEGIES)))
+        last = i == len(segs) - 1
+        flush = zlib.Z_FINISH if last else (zlib.Z_FULL_FLUSH if rng.random() < 0.3 else zlib.Z_SYNC_FLUSH)
+        out.append(c.compress(seg.tobytes()) + c.flush(flush))
+        if not last and rng.random() < 0.4:
+            c = None                           # the next segment from a fresh compressor
+    return b"".join(out)
+
+
+def test_parallel_decode_of_spliced_streams(_small_parallel):
+    """Streams whose blocks change type and table mid-stream (stored / fixed / dynamic runs,
+    empty sync-flush blocks, back-references across some flush points): the parallel decode, with
+    chunk starts found wherever a dynamic block happens to begin, equals np.load's bytes; streams
+    that open with a stored or fixed block decode in order."""
+    before = codec.parallel_config()
+    for seed in range(16):
+        rng = np.random.default_rng(700 + seed)
+        parts = [rng.standard_normal(int(rng.integers(20_000, 120_000))).astype(np.float32).view(np.uint8),
+                 np.where(rng.random(int(rng.integers(50_000, 300_000))) < 0.95, 0, 7).astype(np.uint8),
+                 np.tile(rng.integers(0, 255, int(rng.integers(500, 40_000)), dtype=np.uint8), 6),
+                 np.frombuffer(b"model update " * int(rng.integers(2_000, 20_000)), np.uint8)]
+        rng.shuffle(parts)
+        x = np.concatenate(parts)
+        npy = _npy(x)
+        comp = _spliced(npy, rng)
+        assert zlib.decompress(comp, -15) == npy
+        got = codec.load_npz(_npz_member(npy, comp), threads=int(rng.integers(2, 9)))[0]
+        assert got.dtype == x.dtype and np.array_equal(got, x), seed
+    after = codec.parallel_config()
+    assert after[0] - before[0] >= 6                    # (10 of the 16 on these seeds)
