@@ -79,7 +79,11 @@ def upload_requests(data, model_id, chunk=CHUNK_SIZE):
 
 class MemoryModelService:
     """``ModelService.Upload`` (modelservice.py:198-221) over the in-memory store: chunks are
-    appended per id; the OK request commits the bytes under that id and ends the call."""
+    kept per id; the OK request commits the bytes under that id and ends the call. FEDn writes
+    each chunk to a temp file (a write that releases the GIL); the stand-in keeps the chunk
+    objects and joins them once (a join of that size releases the GIL too) rather than growing
+    one bytearray, whose reallocations copy the upload over and over under the GIL and starve
+    the threads decoding other uploads."""
 
     def __init__(self, store):
         self.store = store
@@ -88,9 +92,9 @@ class MemoryModelService:
     def Upload(self, request_iterator, context):
         for request in request_iterator:
             if request.status == MODEL_STATUS_IN_PROGRESS:
-                self._parts.setdefault(request.id, bytearray()).extend(request.data)
+                self._parts.setdefault(request.id, []).append(bytes(request.data))
             if request.status == MODEL_STATUS_OK and not request.data:
-                self.store.put(request.id, _NpzBytes(bytes(self._parts.pop(request.id, b""))))
+                self.store.put(request.id, _NpzBytes(b"".join(self._parts.pop(request.id, []))))
                 return ModelResponse(id=request.id, status=MODEL_STATUS_OK, message="Got model successfully.")
         return None
 
