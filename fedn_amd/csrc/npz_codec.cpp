@@ -22,6 +22,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -405,10 +406,101 @@ void chunk_tail(const std::vector<ParChunk>& ch, int t, size_t want, uint8_t* wi
 template <class F>
 void parallel_for(int n, int threads, F&& f);
 
+// The parallel decode's phases run on one process-wide pool: a burst of updates read at once (the
+// staging workers decode every ModelUpdate as it arrives) queues its chunks on the same workers,
+// so no core idles while any decode has chunks left and no decode is left on one thread because an
+// earlier one holds the rest. Jobs are served in arrival order; a caller works on its own job's
+// indices too, so a job always completes (also nested in fnpz_read's member tasks, and in a forked
+// child, which gets a fresh pool like CopyPool).
+class DecodePool {
+   public:
+    static DecodePool& get() {
+        static std::mutex m;
+        static DecodePool* pool = nullptr;
+        static pid_t owner = 0;
+        std::lock_guard<std::mutex> lk(m);
+        if (!pool || owner != getpid()) {
+            pool = new DecodePool();               // never destroyed: parked workers end with the process
+            owner = getpid();
+        }
+        return *pool;
+    }
+    template <class F>
+    void run(int n, int want, F&& f) {
+        if (n <= 0) return;
+        if (want <= 1 || n == 1) {
+            for (int i = 0; i < n; ++i) f(i);
+            return;
+        }
+        auto job = std::make_shared<Job>();
+        job->n = n;
+        job->f = [&f](int i) { f(i); };
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            const int w = std::min(want, kMaxThreads) - 1;
+            for (; workers_ < w; ++workers_) std::thread([this] { work(); }).detach();
+            queue_.push_back(job);
+        }
+        cv_.notify_all();
+        for (int i; (i = claim(job.get())) >= 0;) finish(*job, i);
+        std::unique_lock<std::mutex> lk(job->mu);
+        job->cv.wait(lk, [&] { return job->done == job->n; });
+    }
+
+   private:
+    static constexpr int kMaxThreads = 64;
+    struct Job {
+        int n = 0, next = 0, done = 0;   // next: under the pool's lock; done: under mu
+        std::function<void(int)> f;      // the caller's body, alive until done == n
+        std::mutex mu;
+        std::condition_variable cv;
+    };
+    int claim(Job* j) {                    // the next index of j, or -1; a fully claimed job leaves the queue
+        std::lock_guard<std::mutex> lk(mu_);
+        if (j->next >= j->n) return -1;
+        const int i = j->next++;
+        if (j->next == j->n)
+            for (auto it = queue_.begin(); it != queue_.end(); ++it)
+                if (it->get() == j) {
+                    queue_.erase(it);
+                    break;
+                }
+        return i;
+    }
+    static void finish(Job& j, int i) {
+        j.f(i);
+        std::lock_guard<std::mutex> lk(j.mu);
+        if (++j.done == j.n) j.cv.notify_all();
+    }
+    void work() {
+        for (;;) {
+            std::shared_ptr<Job> j;
+            int i;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return !queue_.empty(); });
+                j = queue_.front();            // holds the job past its caller's wait
+                i = j->next++;
+                if (j->next == j->n) queue_.pop_front();
+            }
+            finish(*j, i);
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::shared_ptr<Job>> queue_;
+    int workers_ = 0;
+};
+
+template <class F>
+void decode_for(int n, int threads, F&& f) {
+    DecodePool::get().run(n, threads, std::forward<F>(f));
+}
+
 // fnpz_parallel_config: streams of at least g_par_min compressed bytes, chunks of at least
 // g_par_chunk; counters of the decodes that went parallel / fell back
 std::atomic<int64_t> g_par_min{16 << 20}, g_par_chunk{4 << 20}, g_par_ok{0}, g_par_fallback{0};
-std::atomic<int> g_par_busy{0};                 // threads held by parallel decodes in flight
+std::atomic<int> g_par_inflight{0};             // large deflated members being decoded
 
 int inflate_parallel(const uint8_t* in, int64_t inlen, uint8_t* hdr, int64_t hlen, uint8_t* dst, int64_t dlen,
                      int threads, uint32_t* crc_out) {
@@ -423,7 +515,7 @@ int inflate_parallel(const uint8_t* in, int64_t inlen, uint8_t* hdr, int64_t hle
     // 1. chunk starts: the first block header in each range that parses and trial-decodes
     std::vector<uint64_t> starts((size_t)T, 0);
     std::vector<char> found((size_t)T, 0);
-    parallel_for(T - 1, T - 1, [&](int j) {
+    decode_for(T - 1, T - 1, [&](int j) {
         const int t = j + 1;
         const uint64_t lo = (uint64_t)inlen * (uint64_t)t / (uint64_t)T * 8;
         // zlib ends a block every 16 K symbols (<= ~30 KB of dynamic codes): 128 KiB of search finds
@@ -452,7 +544,7 @@ int inflate_parallel(const uint8_t* in, int64_t inlen, uint8_t* hdr, int64_t hle
     // 2. every chunk from its start to the next one's
     std::vector<ParChunk> ch((size_t)C);
     const size_t expect = (size_t)(total / (uint64_t)C) + (1u << 20);
-    parallel_for(C, C, [&](int t) {
+    decode_for(C, C, [&](int t) {
         ParChunk& c = ch[(size_t)t];
         std::unique_ptr<Inflate> d(new Inflate(in, (size_t)inlen));
         d->restart_at(st[(size_t)t]);
@@ -508,7 +600,7 @@ int inflate_parallel(const uint8_t* in, int64_t inlen, uint8_t* hdr, int64_t hle
     }
     // 4. into [hdr | dst], CRC-32 per chunk, combined in order
     std::vector<uint32_t> crcs((size_t)C, 0);
-    parallel_for(C, C, [&](int t) {
+    decode_for(C, C, [&](int t) {
         const ParChunk& c = ch[(size_t)t];
         uint64_t o = off[(size_t)t];
         uint32_t cr = 0;
@@ -540,16 +632,21 @@ int decode_one(const uint8_t* a, const fnpz_entry& e, void* dst, char* err, size
     uint8_t* out = static_cast<uint8_t*>(dst);
     std::vector<uint8_t> hdr((size_t)e.npy_header);
     uint32_t crc = 0;
-    // concurrent reads (the aggregators' read-ahead decodes several updates at once) share the
-    // threads: each parallel decode takes what the others leave of ``threads``
-    const int grant = threads > 1 ? std::max(1, std::min(threads, threads - g_par_busy.load())) : 1;
-    if (e.method == 8 && grant > 1 && e.comp_size >= g_par_min.load() &&
-        e.comp_size >= 2 * std::max<int64_t>(g_par_chunk.load(), 64 << 10)) {
-        g_par_busy += grant;
+    // concurrent reads (the staging workers decode several updates at once) share DecodePool's
+    // threads: each parallel decode queues its chunks there. Once ``threads`` large members are
+    // being decoded at once every core has one, and a member decodes in order (the split's search,
+    // markers and copy cost ~15 % more core time than the in-order decode)
+    struct Inflight {
+        const int ahead = g_par_inflight++;
+        ~Inflight() { --g_par_inflight; }
+    };
+    const bool large = e.method == 8 && e.comp_size >= g_par_min.load() &&
+                       e.comp_size >= 2 * std::max<int64_t>(g_par_chunk.load(), 64 << 10);
+    std::unique_ptr<Inflight> inflight(large ? new Inflight() : nullptr);
+    if (large && threads > 1 && inflight->ahead < threads) {
         uint32_t pc = 0;
-        const bool ok = inflate_parallel(a + e.data_offset, e.comp_size, hdr.data(), e.npy_header, out, e.nbytes, grant,
-                                         &pc) == 0 && pc == e.crc32;
-        g_par_busy -= grant;
+        const bool ok = inflate_parallel(a + e.data_offset, e.comp_size, hdr.data(), e.npy_header, out, e.nbytes,
+                                         threads, &pc) == 0 && pc == e.crc32;
         if (ok) {
             g_par_ok++;
             return FNPZ_OK;

@@ -271,3 +271,21 @@ def test_parallel_decode_of_spliced_streams(_small_parallel):
         assert got.dtype == x.dtype and np.array_equal(got, x), seed
     after = codec.parallel_config()
     assert after[0] - before[0] >= 6                    # (10 of the 16 on these seeds)
+
+
+def test_concurrent_parallel_decodes_share_the_pool(_small_parallel):
+    """Several large streams decoded at once from Python threads (the staging workers on a burst
+    of ModelUpdates): their chunks share one decode pool; every result equals np.load's, and more
+    decodes at once than threads take the in-order decode for the surplus."""
+    from concurrent.futures import ThreadPoolExecutor
+    rng = np.random.default_rng(23)
+    xs = [rng.standard_normal(int(rng.integers(150_000, 400_000))).astype(np.float32) for _ in range(12)]
+    raws = [_npz_one(x, level=int(rng.choice([1, 6]))) for x in xs]
+    before = codec.parallel_config()
+    with ThreadPoolExecutor(12) as ex:
+        for _ in range(3):
+            got = list(ex.map(lambda r: codec.load_npz(r, threads=4)[0], raws))
+            for g, x in zip(got, xs):
+                assert g.dtype == x.dtype and np.array_equal(g, x)
+    after = codec.parallel_config()
+    assert after[0] - before[0] >= 6
