@@ -269,7 +269,7 @@ class StreamingUpload:
         # with at most max_queued_chunks chunks buffered; one that falls further behind is
         # abandoned), later ones take the normal path — the host memory the tee holds is bounded,
         # per stream and, over all streams, by max_queued_bytes (FEDN_AMD_TEE_MAX_BYTES, 2 GiB). A
-        # decode slower than its upload (an inflate core does ~440 MB/s of input) lags instead of
+        # decode slower than its upload (an inflate core does ~470 MB/s of input) lags instead of
         # giving up: the backlog left when the upload ends is much shorter than decoding it all then.
         self._free = threading.Semaphore(4 * workers)
         self.max_queued_chunks = max_queued_chunks
