@@ -28,6 +28,8 @@ def hipcc():
 NPZ_SRC = os.path.join(HERE, "csrc", "npz_codec.cpp")
 NPZ_HDR = os.path.join(ROOT, "include", "fednpz.h")
 NPZ_INFLATE = os.path.join(HERE, "csrc", "inflate.h")      # the codec's DEFLATE decoder + CRC-32
+NPZ_SAVEZ = os.path.join(HERE, "csrc", "savez.cpp")        # numpy-identical writer (fnpz_savez)
+NPZ_PDEFLATE = os.path.join(HERE, "csrc", "pdeflate.h")    # its single-stream parallel deflate
 NPZ_OUT = os.path.join(HERE, "libfednpz.so")
 
 
@@ -37,12 +39,13 @@ def _stale(out, *deps):
 
 def build_codec(force=False, verbose=True):
     """Host-side npz codec (C++17 + zlib, no GPU code)."""
-    if not force and not _stale(NPZ_OUT, NPZ_SRC, NPZ_HDR, NPZ_INFLATE):
+    deps = [d for d in (NPZ_SRC, NPZ_HDR, NPZ_INFLATE, NPZ_SAVEZ, NPZ_PDEFLATE) if os.path.exists(d)]
+    if not force and not _stale(NPZ_OUT, *deps):
         return NPZ_OUT
     cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
     tmp = NPZ_OUT + ".tmp"
     cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", "-I", os.path.join(ROOT, "include"),
-           "-o", tmp, NPZ_SRC, "-lz"]
+           "-o", tmp, NPZ_SRC, NPZ_SAVEZ, "-lz"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -4,8 +4,13 @@ FEDn serialises every model with ``np.savez_compressed`` and reads it back throu
 file and ``np.load`` (numpyhelper.py:144-189, modelservice.py:57-75, 110-146). This module
 decodes an archive held in memory straight into caller buffers — optionally one pinned
 host buffer in the grouped flat layout the GPU pipelines stage from (layout.py) — and
-encodes with a block-parallel deflate. Decoded arrays are byte-identical to ``np.load``;
-written archives are valid npz files (``np.load``/``zipfile`` read them, CRCs checked).
+encodes. Decoded arrays are byte-identical to ``np.load``. Two writers:
+
+  save_npz         the bytes np.savez_compressed writes (numpyhelper.py:162), byte for byte
+                   (fnpz_savez): what Helper.save produces by default
+  save_npz_blocks  a block-parallel deflate with a private block index (fnpz_write): valid
+                   npz files np.load reads, several times smaller/faster to write and decode
+                   in parallel, but not numpy's bytes (opt-in: FEDN_AMD_NPZ_WRITER=blocks)
 """
 import ctypes
 import io
@@ -18,8 +23,8 @@ from .layout import Layout
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfednpz.so")
-MAX_DIMS = 16
-FNPZ_ABI_VERSION = 5    # include/fednpz.h
+MAX_DIMS = 64           # numpy 2.x NPY_MAXDIMS (include/fednpz.h FNPZ_MAX_DIMS)
+FNPZ_ABI_VERSION = 6    # include/fednpz.h
 THREADS = int(os.environ.get("FEDN_AMD_CODEC_THREADS", str(min(16, os.cpu_count() or 1))))
 
 
@@ -67,6 +72,10 @@ def load_lib():
                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
                                            ctypes.POINTER(ctypes.c_int64)]
+                lib.fnpz_savez.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_void_p),
+                                           ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_void_p),
+                                           ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
                 lib.fnpz_stream_open.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
                 lib.fnpz_stream_close.argtypes = [ctypes.c_void_p]
                 lib.fnpz_stream_close.restype = None
@@ -277,8 +286,66 @@ def load_npz_into_layout(buf, alloc, threads=None):
 STRATEGIES = {"auto": -1, "default": 0, "filtered": 1, "huffman": 2, "rle": 3, "fixed": 4}
 
 
-def save_npz(arrays, level=6, threads=None, block=0, strategy="auto"):
-    """Encode ``arrays`` like numpyhelper.Helper.save (keys "0", "1", ...); returns bytes.
+class _NumpyOnly(Exception):
+    """A member only numpy itself writes (pickled object arrays, user dtypes, zero itemsize)."""
+
+
+def _npy_member(x):
+    """(npy header bytes, payload array in numpy's write order, numpy's write size in bytes) for one
+    member, as numpy.lib.format.write_array writes it into the zip member (numpy 2.x format.py:
+    _write_array_header with version=None — the oldest version that holds the header — then
+    16 MiB // itemsize elements per write, C order, or F order for a Fortran-contiguous array)."""
+    fmt = np.lib.format
+    if x.dtype.hasobject or not getattr(type(x.dtype), "_legacy", True) or x.itemsize == 0:
+        raise _NumpyOnly
+    bio = io.BytesIO()
+    fmt._write_array_header(bio, fmt.header_data_from_array_1_0(x), None)
+    if x.flags.f_contiguous and not x.flags.c_contiguous:
+        data = x.ravel(order="K")               # memory order == F order (no copy)
+    else:
+        data = np.ascontiguousarray(x).reshape(-1)
+    seg = max(16 * 1024 ** 2 // x.itemsize, 1) * x.itemsize
+    return np.frombuffer(bio.getvalue(), dtype=np.uint8), data, seg
+
+
+def savez_into(arrays, threads=None):
+    """np.savez_compressed's archive of ``arrays`` under keys "0", "1", ... (numpyhelper.Helper.save,
+    numpyhelper.py:158-162) as a uint8 numpy array (no copy out of the native buffer). Byte-identical
+    to numpy's: fnpz_savez replays zipfile's deflate calls on the same libz and its headers. Members
+    only numpy writes (object arrays: pickled) make the whole archive come from np.savez_compressed."""
+    vals = [np.asanyarray(x) for x in arrays]
+    try:
+        members = [_npy_member(x) for x in vals]
+    except _NumpyOnly:
+        bio = io.BytesIO()
+        np.savez_compressed(bio, **{str(i): x for i, x in enumerate(vals)})
+        return np.frombuffer(bio.getbuffer(), dtype=np.uint8)
+    lib = load_lib()
+    n = len(members)
+    m = max(1, n)
+    names = [str(i).encode() for i in range(n)]
+    hl = (ctypes.c_int64 * m)(*[h.size for h, _, _ in members])
+    nb = (ctypes.c_int64 * m)(*[d.nbytes for _, d, _ in members])
+    nl = (ctypes.c_int32 * m)(*[len(s) for s in names])
+    seg = (ctypes.c_int64 * m)(*[s for _, _, s in members])
+    cap = lib.fnpz_write_bound(n, hl, nb, nl)
+    out = np.empty(cap, dtype=np.uint8)
+    out_len = ctypes.c_int64(0)
+    _check(lib.fnpz_savez(n, (ctypes.c_char_p * m)(*names),
+                          (ctypes.c_void_p * m)(*[h.ctypes.data for h, _, _ in members]), hl,
+                          (ctypes.c_void_p * m)(*[d.ctypes.data if d.size else 0 for _, d, _ in members]), nb, seg,
+                          threads or THREADS, out.ctypes.data, cap, ctypes.byref(out_len)))
+    return out[:out_len.value]
+
+
+def save_npz(arrays, threads=None):
+    """np.savez_compressed's bytes for ``arrays`` (keys "0", "1", ...): see :func:`savez_into`."""
+    return savez_into(arrays, threads).tobytes()
+
+
+def save_npz_blocks(arrays, level=6, threads=None, block=0, strategy="auto"):
+    """Encode ``arrays`` with the block-parallel writer (keys "0", "1", ...); returns bytes. np.load
+    reads the archive; its bytes are this codec's own, not numpy's (see :func:`save_npz`).
 
     ``strategy``: "auto" (fnpz_write's FNPZ_STRATEGY_AUTO: run-length matching per block, the default
     strategy at level 1 where that is smaller on very compressible blocks — as small as

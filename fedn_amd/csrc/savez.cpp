@@ -1,0 +1,247 @@
+// savez.cpp — numpy-identical npz writer (fnpz_savez, include/fednpz.h).
+//
+// numpyhelper.Helper.save is np.savez_compressed (fedn/utils/helpers/plugins/numpyhelper.py:
+// 144-169, the call at :162), and that archive is a deterministic byte stream: numpy's _savez
+// opens every member with zipfile.ZipFile.open(key + ".npy", "w", force_zip64=True) and
+// numpy.lib.format.write_array writes the .npy header in one write and then the payload in
+// writes of 16 MiB // itemsize elements; zipfile feeds each write to
+// zlib.compressobj(Z_DEFAULT_COMPRESSION, DEFLATED, -15) (level 6, memLevel 8, default
+// strategy), CRCs it, finishes the stream, seeks back and rewrites the local header with the
+// real sizes. This file replays exactly that byte sequence: the same deflate() calls into
+// the same libz (the process's libz.so.1 — CPython's zlib module links it too), and
+// zipfile's headers field for field (CPython 3.10 zipfile.py: ZipInfo.FileHeader,
+// ZipFile._write_end_record). Members deflate in parallel; each member's stream is
+// sequential, as numpy's is (fnpz_savez's single-stream parallel mode lives in
+// pdeflate.h).
+
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/fednpz.h"
+#include "inflate.h"
+
+namespace fnpz_internal {
+int set_error(int code, const char* fmt, ...);
+}
+
+namespace {
+
+using fnpz_internal::set_error;
+
+void put16(uint8_t*& p, uint32_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p += 2; }
+void put32(uint8_t*& p, uint32_t v) { for (int i = 0; i < 4; ++i) p[i] = (uint8_t)(v >> (8 * i)); p += 4; }
+void put64(uint8_t*& p, uint64_t v) { for (int i = 0; i < 8; ++i) p[i] = (uint8_t)(v >> (8 * i)); p += 8; }
+
+constexpr uint64_t kZip64Limit = (1ull << 31) - 1;   // zipfile.ZIP64_LIMIT
+constexpr uint32_t kFileCountLimit = (1u << 16) - 1; // zipfile.ZIP_FILECOUNT_LIMIT
+constexpr uint16_t kDosDate = (0 << 9) | (1 << 5) | 1; // ZipInfo's default date_time 1980-01-01 00:00:00
+constexpr uint16_t kDefaultVersion = 20, kZip64Version = 45;
+constexpr uint32_t kExternalAttr = 0600u << 16;      // zipfile: "?rw-------"
+
+struct Member {
+    const char* name;
+    const uint8_t* header;
+    int64_t hlen;
+    const uint8_t* data;
+    int64_t nbytes;
+    int64_t seg;                // numpy's write size (bytes); <= 0: one write
+    std::vector<uint8_t> out;   // the raw deflate stream
+    uint32_t crc = 0;
+    int rc = Z_OK;
+};
+
+// zlib.compressobj(-1, DEFLATED, -15).compress(w) for each write w, then .flush()
+void deflate_member(Member& m) {
+    z_stream zs{};
+    if (deflateInit2(&zs, Z_DEFAULT_COMPRESSION, Z_DEFLATED, -MAX_WBITS, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+        m.rc = Z_MEM_ERROR;
+        return;
+    }
+    const uint64_t raw = (uint64_t)(m.hlen + m.nbytes);
+    m.out.resize((size_t)(raw + raw / 1000 + (raw >> 14) * 5 + 1024));   // >= deflateBound's stored worst case
+    size_t used = 0;
+    auto run = [&](const uint8_t* in, uint64_t n, int flush) -> bool {
+        // CPython passes at most UINT_MAX input bytes per deflate() call (arrange_input_buffer)
+        do {
+            const uInt take = (uInt)std::min<uint64_t>(n, 0xFFFFFFFFu);
+            zs.next_in = const_cast<Bytef*>(in);
+            zs.avail_in = take;
+            const bool last_piece = take == n;
+            for (;;) {
+                if (m.out.size() - used < 64) m.out.resize(m.out.size() * 2);
+                zs.next_out = m.out.data() + used;
+                const size_t room = std::min<size_t>(m.out.size() - used, 0xFFFFFFFFu);
+                zs.avail_out = (uInt)room;
+                const int rc = deflate(&zs, last_piece ? flush : Z_NO_FLUSH);
+                used += room - zs.avail_out;
+                if (rc == Z_STREAM_END) return true;
+                if (rc != Z_OK && rc != Z_BUF_ERROR) return false;
+                if (zs.avail_in == 0 && zs.avail_out != 0 && !(last_piece && flush == Z_FINISH)) break;
+            }
+            in += take;
+            n -= take;
+        } while (n > 0);
+        return true;
+    };
+    bool ok = run(m.header, (uint64_t)m.hlen, Z_NO_FLUSH);
+    m.crc = fnpz_fast::crc32(0, m.header, (size_t)m.hlen);
+    const int64_t seg = m.seg > 0 ? m.seg : std::max<int64_t>(m.nbytes, 1);
+    for (int64_t b = 0; ok && b < m.nbytes; b += seg) {
+        const int64_t n = std::min(seg, m.nbytes - b);
+        ok = run(m.data + b, (uint64_t)n, Z_NO_FLUSH);
+        m.crc = fnpz_fast::crc32(m.crc, m.data + b, (size_t)n);
+    }
+    ok = ok && run(nullptr, 0, Z_FINISH);
+    deflateEnd(&zs);
+    m.out.resize(used);
+    m.rc = ok ? Z_OK : Z_STREAM_ERROR;
+}
+
+}  // namespace
+
+extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const* headers, const int64_t* header_lens,
+                          const void* const* datas, const int64_t* nbytes, const int64_t* seg_bytes, int threads,
+                          uint8_t* out, int64_t out_cap, int64_t* out_len) {
+    if (n < 0 || !out || !out_len || (n > 0 && (!names || !headers || !header_lens || !datas || !nbytes)))
+        return set_error(FNPZ_EINVAL, "fnpz_savez: bad arguments");
+    std::vector<Member> ms((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        const size_t nl = std::strlen(names[i]);
+        if (nl + 4 > 0xFFFF || header_lens[i] < 0 || nbytes[i] < 0 || (nbytes[i] > 0 && !datas[i]))
+            return set_error(FNPZ_EINVAL, "fnpz_savez: bad member %d", i);
+        ms[i] = Member{names[i], headers[i], header_lens[i], static_cast<const uint8_t*>(datas[i]), nbytes[i],
+                       seg_bytes ? seg_bytes[i] : 0};
+    }
+    // largest members first so one big stream does not start last
+    std::vector<int> order((size_t)n);
+    for (int i = 0; i < n; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return ms[a].nbytes > ms[b].nbytes; });
+    std::atomic<int> next{0};
+    auto work = [&] {
+        for (int k; (k = next.fetch_add(1)) < n;) deflate_member(ms[order[k]]);
+    };
+    const int nt = std::max(1, std::min(threads, n));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+    for (int i = 0; i < n; ++i)
+        if (ms[i].rc != Z_OK) return set_error(FNPZ_ECORRUPT, "fnpz_savez: deflate failed on member %d", i);
+
+    uint8_t* p = out;
+    uint8_t* const lim = out + out_cap;
+    std::vector<uint64_t> offs((size_t)n);
+    std::vector<uint64_t> comps((size_t)n);
+    std::vector<uint16_t> ver((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        const Member& m = ms[i];
+        const size_t nl = std::strlen(m.name) + 4;
+        const uint64_t raw = (uint64_t)(m.hlen + m.nbytes), comp = m.out.size();
+        if ((int64_t)(30 + nl + 20 + comp) > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
+        // ZipInfo.FileHeader(zip64=True) as _ZipWriteFile.close rewrites it
+        const bool big = raw > kZip64Limit || comp > kZip64Limit;
+        ver[i] = big ? kZip64Version : kDefaultVersion;
+        offs[i] = (uint64_t)(p - out);
+        comps[i] = comp;
+        put32(p, 0x04034b50);
+        put16(p, ver[i]);
+        put16(p, 0);                        // flag bits (seekable output: no data descriptor)
+        put16(p, Z_DEFLATED);
+        put16(p, 0);                        // DOS time
+        put16(p, kDosDate);
+        put32(p, m.crc);
+        put32(p, big ? 0xFFFFFFFFu : (uint32_t)comp);
+        put32(p, big ? 0xFFFFFFFFu : (uint32_t)raw);
+        put16(p, (uint16_t)nl);
+        put16(p, 20);
+        std::memcpy(p, m.name, nl - 4);
+        std::memcpy(p + nl - 4, ".npy", 4);
+        p += nl;
+        put16(p, 1);
+        put16(p, 16);
+        put64(p, raw);
+        put64(p, comp);
+        std::memcpy(p, m.out.data(), comp);
+        p += comp;
+        std::vector<uint8_t>().swap(ms[i].out);
+    }
+    const uint64_t cd_off = (uint64_t)(p - out);
+    for (int i = 0; i < n; ++i) {   // ZipFile._write_end_record
+        const Member& m = ms[i];
+        const size_t nl = std::strlen(m.name) + 4;
+        const uint64_t raw = (uint64_t)(m.hlen + m.nbytes);
+        const uint64_t csize = comps[i];
+        uint64_t extra[3];
+        int ne = 0;
+        const bool big = raw > kZip64Limit || csize > kZip64Limit;
+        if (big) extra[ne++] = raw, extra[ne++] = csize;
+        if (offs[i] > kZip64Limit) extra[ne++] = offs[i];
+        const uint16_t v = ne ? std::max<uint16_t>(kZip64Version, ver[i]) : ver[i];
+        if ((int64_t)(46 + nl + 4 + 8 * ne) > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
+        put32(p, 0x02014b50);
+        put16(p, (uint16_t)(v | (3 << 8)));  // create_version | create_system (unix)
+        put16(p, v);                          // extract_version
+        put16(p, 0);
+        put16(p, Z_DEFLATED);
+        put16(p, 0);
+        put16(p, kDosDate);
+        put32(p, m.crc);
+        put32(p, big ? 0xFFFFFFFFu : (uint32_t)csize);
+        put32(p, big ? 0xFFFFFFFFu : (uint32_t)raw);
+        put16(p, (uint16_t)nl);
+        put16(p, (uint16_t)(ne ? 4 + 8 * ne : 0));
+        put16(p, 0);                          // comment
+        put16(p, 0);                          // disk number start
+        put16(p, 0);                          // internal attributes
+        put32(p, kExternalAttr);
+        put32(p, offs[i] > kZip64Limit ? 0xFFFFFFFFu : (uint32_t)offs[i]);
+        std::memcpy(p, m.name, nl - 4);
+        std::memcpy(p + nl - 4, ".npy", 4);
+        p += nl;
+        if (ne) {
+            put16(p, 1);
+            put16(p, (uint16_t)(8 * ne));
+            for (int k = 0; k < ne; ++k) put64(p, extra[k]);
+        }
+    }
+    const uint64_t pos2 = (uint64_t)(p - out);
+    const uint64_t cd_size = pos2 - cd_off;
+    uint64_t count = (uint64_t)n, size = cd_size, offset = cd_off;
+    if (count > kFileCountLimit || cd_off > kZip64Limit || cd_size > kZip64Limit) {
+        if (56 + 20 > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
+        put32(p, 0x06064b50);
+        put64(p, 44);
+        put16(p, kZip64Version);
+        put16(p, kZip64Version);
+        put32(p, 0);
+        put32(p, 0);
+        put64(p, count);
+        put64(p, count);
+        put64(p, cd_size);
+        put64(p, cd_off);
+        put32(p, 0x07064b50);
+        put32(p, 0);
+        put64(p, pos2);
+        put32(p, 1);
+        count = std::min<uint64_t>(count, 0xFFFF);
+        size = std::min<uint64_t>(size, 0xFFFFFFFFu);
+        offset = std::min<uint64_t>(offset, 0xFFFFFFFFu);
+    }
+    if (22 > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
+    put32(p, 0x06054b50);
+    put16(p, 0);
+    put16(p, 0);
+    put16(p, (uint16_t)count);
+    put16(p, (uint16_t)count);
+    put32(p, (uint32_t)size);
+    put32(p, (uint32_t)offset);
+    put16(p, 0);
+    *out_len = (int64_t)(p - out);
+    return FNPZ_OK;
+}

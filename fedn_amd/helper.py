@@ -3,8 +3,9 @@
 FEDn's ``HelperBase`` requires (helperbase.py:4-40) plus its file-type API:
 
   increment_average(m1, m2, n, N)  numpyhelper.py:18-32, computed by libfedagg (bit-exact)
-  save(weights, path=None, file_type="npz")   numpyhelper.py:144-169: block-parallel deflate,
-                                              output readable by np.load
+  save(weights, path=None, file_type="npz")   numpyhelper.py:144-169: np.savez_compressed's
+                                              bytes exactly (codec.save_npz; the block-parallel
+                                              writer with FEDN_AMD_NPZ_WRITER=blocks)
   load(path, file_type="npz")                 numpyhelper.py:171-189: native inflate (parallel
                                               for archives this codec wrote), members of 8 MiB+
                                               into pinned memory for a multi-GPU combiner;
@@ -64,6 +65,16 @@ def pinned_empty(shape, dtype, order="C"):
         return None
     blk = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
     return blk.numpy().view(dtype).reshape(shape)
+
+
+def npz_writer():
+    """Helper.save's npz writer: "numpy" (default: np.savez_compressed's bytes, numpyhelper.py:162) or
+    "blocks" (FEDN_AMD_NPZ_WRITER=blocks: the codec's block-parallel archive — np.load reads it, but
+    its bytes are not numpy's)."""
+    v = os.environ.get("FEDN_AMD_NPZ_WRITER", "numpy")
+    if v not in ("numpy", "blocks"):
+        raise ValueError(f"FEDN_AMD_NPZ_WRITER={v!r}: expected 'numpy' or 'blocks'")
+    return v
 
 
 def _device():
@@ -330,7 +341,10 @@ class Helper:
         if file_type == "npz":
             if not path:
                 path = self.get_tmp_path()
-            data = codec.save_npz(list(weights))
+            if npz_writer() == "blocks":
+                data = codec.save_npz_blocks(list(weights))
+            else:
+                data = memoryview(codec.savez_into(list(weights)))
             if hasattr(path, "write"):
                 path.write(data)
             else:

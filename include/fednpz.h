@@ -24,8 +24,8 @@
 extern "C" {
 #endif
 
-#define FNPZ_ABI_VERSION 5
-#define FNPZ_MAX_DIMS 16
+#define FNPZ_ABI_VERSION 6
+#define FNPZ_MAX_DIMS 64   /* numpy 2's NPY_MAXDIMS (ABI 6; 16 before) */
 
 enum fnpz_status { FNPZ_OK = 0, FNPZ_EFORMAT = 1, FNPZ_ECORRUPT = 2, FNPZ_EINVAL = 3, FNPZ_ENOSPC = 4 };
 
@@ -75,6 +75,20 @@ int64_t fnpz_write_bound(int n, const int64_t* header_lens, const int64_t* nbyte
 #define FNPZ_STRATEGY_AUTO (-1)
 int fnpz_write(int n, const char* const* names, const uint8_t* const* headers, const int64_t* header_lens,
                const void* const* datas, const int64_t* nbytes, int level, int strategy, int threads, int64_t block,
+               uint8_t* out, int64_t out_cap, int64_t* out_len);
+
+/* numpy-identical writer (ABI 6): the exact bytes np.savez_compressed writes for these members —
+ * numpyhelper.Helper.save (fedn/utils/helpers/plugins/numpyhelper.py:144-169, np.savez_compressed at
+ * :162). Member i is names[i] + ".npy" = headers[i] (the .npy preamble numpy writes for the array:
+ * numpy.lib.format._write_array_header) followed by datas[i] (nbytes[i] bytes in numpy's write order:
+ * C order, or F order for a Fortran-contiguous array), deflated the way zipfile does it — zlib level
+ * 6, raw (wbits -15), memLevel 8, default strategy, the header in one deflate() call and the payload
+ * in calls of seg_bytes[i] bytes (numpy's 16 MiB // itemsize elements; NULL or <= 0: one call) — and
+ * wrapped in zipfile's headers (ZIP64 local extra on every member, 1980-01-01 timestamps, ZIP64
+ * central / end records only past zipfile's limits). Members deflate on up to `threads` threads.
+ * The output bound is fnpz_write_bound's. *out_len = bytes written. */
+int fnpz_savez(int n, const char* const* names, const uint8_t* const* headers, const int64_t* header_lens,
+               const void* const* datas, const int64_t* nbytes, const int64_t* seg_bytes, int threads,
                uint8_t* out, int64_t out_cap, int64_t* out_len);
 
 /* Streaming reader — an archive decoded while it arrives (ModelService.Upload chunks,

@@ -53,7 +53,7 @@ def test_reads_numpy_savez_compressed():
 def test_writes_archives_numpy_reads(block):
     rng = np.random.default_rng(1)
     arrays = ARRAYS + [rng.standard_normal(200_003).astype(np.float32)]
-    enc = codec.save_npz(arrays, block=block, threads=4)
+    enc = codec.save_npz_blocks(arrays, block=block, threads=4)
     assert zipfile.ZipFile(io.BytesIO(enc)).testzip() is None      # every CRC-32 checks out
     z = np.load(io.BytesIO(enc), allow_pickle=False)
     for i, x in enumerate(arrays):
@@ -64,7 +64,7 @@ def test_writes_archives_numpy_reads(block):
 
 def test_big_member_multiblock_roundtrip():
     x = np.random.default_rng(2).standard_normal(3_000_000).astype(np.float32)
-    enc = codec.save_npz([x], block=1 << 20, threads=4)
+    enc = codec.save_npz_blocks([x], block=1 << 20, threads=4)
     a, ents = codec.open_archive(enc)
     assert ents[0].index_count >= 12
     _same(codec.load_npz(enc, threads=8)[0], x)
@@ -73,7 +73,7 @@ def test_big_member_multiblock_roundtrip():
 
 def test_corruption_detected():
     x = np.random.default_rng(3).standard_normal(100_000).astype(np.float32)
-    enc = bytearray(codec.save_npz([x], block=65536))
+    enc = bytearray(codec.save_npz_blocks([x], block=65536))
     enc[len(enc) // 2] ^= 0xFF
     with pytest.raises(codec.CodecError):
         codec.load_npz(bytes(enc))
@@ -274,7 +274,7 @@ def test_every_write_strategy_reads_back_with_numpy(strategy):
     rng = np.random.default_rng(3)
     arrays = ARRAYS + [rng.standard_normal(300_001).astype(np.float32), np.arange(200_000, dtype=np.int64),
                        np.where(rng.random(100_000) < 0.9, 0, rng.standard_normal(100_000)).astype(np.float32)]
-    enc = codec.save_npz(arrays, block=65536, threads=4, strategy=strategy)
+    enc = codec.save_npz_blocks(arrays, block=65536, threads=4, strategy=strategy)
     assert zipfile.ZipFile(io.BytesIO(enc)).testzip() is None
     z = np.load(io.BytesIO(enc), allow_pickle=False)
     for i, x in enumerate(arrays):
@@ -291,7 +291,7 @@ def test_auto_strategy_size_on_weights_and_structured_data():
     w = rng.standard_normal(1_000_000).astype(np.float32)
     ramp = np.arange(500_000, dtype=np.int64)
     for x, slack in ((w, 1.0), (ramp, 1.05)):
-        auto = len(codec.save_npz([x], strategy="auto"))
+        auto = len(codec.save_npz_blocks([x], strategy="auto"))
         ref = io.BytesIO()
         np.savez_compressed(ref, x)
         assert auto <= slack * len(ref.getvalue()), (x.dtype, auto, len(ref.getvalue()))

@@ -59,10 +59,10 @@ def test_decoder_random_chunking():
 
 
 def test_decoder_reads_native_codec_archives():
-    """fedn_amd.codec.save_npz writes block-parallel deflate + a private extra field."""
+    """fedn_amd.codec.save_npz_blocks writes block-parallel deflate + a private extra field."""
     rng = np.random.default_rng(1)
     arrays = [rng.standard_normal(3_000_000).astype(np.float32), np.arange(5, dtype=np.int64)]
-    data = bytes(codec.save_npz(arrays, block=1 << 20))
+    data = bytes(codec.save_npz_blocks(arrays, block=1 << 20))
     _same_as_npload(data, _decode(data, 1 << 20))
 
 

@@ -63,10 +63,10 @@ def main():
         t_np = best(lambda: np.savez_compressed(io.BytesIO(), **{"0": x}), 1)
         out["encode"] = {"numpy_s": t_np, "numpy_MB": len(raw) / 1e6}
         for strat in ("default", "auto"):
-            enc = codec.save_npz([x], threads=a.threads, strategy=strat)
+            enc = codec.save_npz_blocks([x], threads=a.threads, strategy=strat)
             got = np.load(io.BytesIO(enc))["0"]
             assert np.array_equal(got.view(np.uint32), x.view(np.uint32))
-            out["encode"][f"native_{strat}_s"] = best(lambda: codec.save_npz([x], threads=a.threads, strategy=strat), a.reps)
+            out["encode"][f"native_{strat}_s"] = best(lambda: codec.save_npz_blocks([x], threads=a.threads, strategy=strat), a.reps)
             out["encode"][f"native_{strat}_MB"] = len(enc) / 1e6
         if a.clients > 1 and P <= 25_000_000:
             archives = [raw] * a.clients

@@ -754,6 +754,69 @@ def reduce_cases(ref):
             reduce_case(ref, "reduce_single", rng, ODD_SHAPES, ["ok"])]
 
 
+# views save cases hand to numpyhelper.save (rebuilt from the stored base by tests/test_savez_golden.py)
+SAVE_VIEWS = {
+    "T": lambda b: b.T,
+    "cols3": lambda b: b[:, ::3],
+    "rev": lambda b: b[::-1],
+    "perm201": lambda b: b.transpose(2, 0, 1),
+    "bcast": lambda b: np.broadcast_to(b, (7,) + b.shape),
+}
+
+
+def save_case(ref, name, weights, views=None, raw=True):
+    """numpyhelper.Helper.save (numpyhelper.py:144-169, np.savez_compressed at :162): the archive bytes
+    the reference writes for ``weights`` (``views[i]``: weights[i] is SAVE_VIEWS[views[i]] of the
+    stored base), and the raw_binary bytes (:164-169) where the weights concatenate."""
+    helper = ref["Helper"]()
+    views = views or [""] * len(weights)
+    arrays = [SAVE_VIEWS[v](w) if v else w for w, v in zip(weights, views)]
+    d = {"kind": np.array("save"), "name": np.array(name), "views": np.array(json.dumps(views))}
+    _store_list(d, "w", weights)
+    with tempfile.TemporaryDirectory() as tmp:
+        path = helper.save(arrays, os.path.join(tmp, "m.npz"))
+        with open(path, "rb") as f:
+            d["npz"] = np.frombuffer(f.read(), dtype=np.uint8)
+        try:
+            if not raw:
+                raise ValueError
+            path = helper.save(arrays, os.path.join(tmp, "m.bin"), file_type="raw_binary")
+            with open(path, "rb") as f:
+                d["raw_binary"] = np.frombuffer(f.read(), dtype=np.uint8)
+        except ValueError:                  # np.concatenate of 0-d / mismatched ranks
+            pass
+    return d
+
+
+def save_cases(ref):
+    """The reference's model serialisation bytes: mnist shapes, mixed dtypes, 0-d and empty arrays,
+    Fortran order, non-contiguous views, many members, a member past numpy's 16 MiB write size."""
+    rng = np.random.default_rng(21)
+    mixed = [rng.standard_normal((3, 4)).astype(np.float16), rng.standard_normal(9).astype(np.float32),
+             rng.standard_normal((2, 3, 2)), rng.integers(-100, 100, 11).astype(np.int8),
+             rng.integers(-2**31, 2**31 - 1, 6).astype(np.int32), rng.integers(-2**62, 2**62, 5),
+             rng.integers(0, 255, 13).astype(np.uint8), rng.random(10) < 0.5, np.array(3.25), np.array(7),
+             np.zeros((0,), np.float32), np.zeros((2, 0, 3)), (rng.standard_normal(4) + 1j).astype(np.complex64),
+             np.array(["ab", "c", "xyz"]), np.arange(4, dtype=">f8"), np.ones((1,) * 20, np.float32)]
+    sparse = np.where(rng.random(5_000_000) < 0.004, rng.standard_normal(5_000_000), 0).astype(np.float32)
+    return [
+        save_case(ref, "save_mnist", _rng_model(rng, MNIST_SHAPES, np.float32)),
+        save_case(ref, "save_odd", _rng_model(rng, ODD_SHAPES, np.float32)),
+        save_case(ref, "save_mixed_dtypes", mixed),
+        save_case(ref, "save_fortran", [np.asfortranarray(rng.standard_normal((31, 17))),
+                                        np.asfortranarray(rng.integers(0, 9, (5, 6, 7)).astype(np.int32))]),
+        save_case(ref, "save_views", [rng.standard_normal((40, 60)).astype(np.float32),
+                                      rng.standard_normal((30, 9)).astype(np.float32),
+                                      np.arange(50, dtype=np.int64), rng.standard_normal((4, 5, 6)),
+                                      np.arange(5, dtype=np.float32)],
+                  ["T", "cols3", "rev", "perm201", "bcast"]),
+        save_case(ref, "save_70_members", [rng.standard_normal(int(rng.integers(1, 40))).astype(np.float32)
+                                           for _ in range(70)]),
+        save_case(ref, "save_sparse_20MB", [sparse, np.arange(300_000, dtype=np.int64) // 7], raw=False),
+        save_case(ref, "save_empty_model", []),
+    ]
+
+
 def main():
     global OUT
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
@@ -777,6 +840,8 @@ def main():
         return _write(narrow_cases(ref), merge=True)
     if only == "numex":
         return _write(numex_cases(ref), merge=True)
+    if only == "save":
+        return _write(save_cases(ref), merge=True)
     if only == "reduce":
         return _write(reduce_cases(ref) + mixed_cases(ref)[-2:], merge=True)
     cases = []
@@ -831,6 +896,7 @@ def main():
     cases += numex_cases(ref)
     cases += f16_fedopt_cases(ref)
     cases += narrow_cases(ref)
+    cases += save_cases(ref)
     _write(cases, merge=False)
 
 
@@ -841,7 +907,8 @@ def _write(cases, merge):
             manifest = [n for n in json.load(f)["cases"] if n not in {str(c["name"]) for c in cases}]
     for c in cases:
         name = str(c["name"])
-        np.savez(os.path.join(OUT, name + ".npz"), **c)
+        # the save fixtures hold large, compressible inputs: compressed on disk (np.load reads both)
+        (np.savez_compressed if name.startswith("save_") else np.savez)(os.path.join(OUT, name + ".npz"), **c)
         manifest.append(name)
     with open(os.path.join(OUT, "manifest.json"), "w") as f:
         json.dump({"generator": "tools/gen_golden.py", "numpy": np.__version__, "cases": manifest}, f, indent=1)
