@@ -23,7 +23,7 @@ from ..exceptions import InvalidParameterError
 from ..parameters import Parameters
 from ..ingest import ShardedStagedModel
 from ..layout import spread
-from ..staging import FedOptPipeline, FedOptState, StagingCache
+from ..staging import FedOptPipeline, FedOptState, StagingCache, helper_kind
 from .aggregatorbase import AggregatorBase, queued_updates
 from .fedavg import _packed_bytes, default_device, env_devices
 
@@ -110,6 +110,7 @@ class Aggregator(AggregatorBase):
 
                     total_examples += metadata["num_examples"]
                     tic = time.time()
+                    helper_kind(helper)            # UnsupportedHelper for a helper this does not implement
                     if helper is not None and not hasattr(helper, "subtract"):
                         # androidhelper has no numpyhelper primitives: fedopt.py:91 raises here for every
                         # update, each is logged and skipped, and the round returns (None, data)

@@ -36,6 +36,9 @@ class Entry(ctypes.Structure):
                 ("index_offset", ctypes.c_int64), ("index_count", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+FNPZ_EFALLBACK = 5     # fnpz_deflate_exact: the input needs zlib itself (fednpz.h)
+
+
 class CodecError(ValueError):
     pass
 

@@ -66,6 +66,13 @@ inline uint32_t crc32_sb8(uint32_t c, const uint8_t* p, size_t n) {
 }
 
 #if defined(__x86_64__)
+// Attribution: this routine follows the published PCLMULQDQ CRC folding method — V. Gopal et al.,
+// "Fast CRC Computation for Generic Polynomials Using PCLMULQDQ Instruction" (Intel white paper,
+// 2009) — in the form of Chromium's zlib crc32_sse42_simd_() (third_party/zlib/crc32_simd.c,
+// Copyright 2017 The Chromium Authors, BSD-style license: "Use of this source code is governed by
+// a BSD-style license that can be found in the Chromium source repository LICENSE file"), whose
+// constant names (k1k2, k3k4, k5k0, poly, mask32) and fold / Barrett sequence it keeps. The
+// constants are the CRC-32 (0xEDB88320) values that method defines.
 // Fold-by-4 over 128-bit lanes, then 128 -> 64 -> 32 bits by Barrett reduction (the constants are
 // x^(4*128+64) mod P, x^(4*128) mod P, x^(128+64) mod P, x^128 mod P, x^64 mod P, P' and mu for the
 // reflected polynomial). ``n`` is a multiple of 16 and at least 64; ``c`` the bit-inverted state.
@@ -329,7 +336,7 @@ class Inflate {
     // finder then parses and trial-decodes the survivors.
     static bool maybe_dynamic_header(const uint8_t* base, size_t n, uint64_t bit) {
         const size_t byte = (size_t)(bit / 8);
-        if (byte + 10 > n) return false;
+        if (byte + 11 > n) return false;
         uint64_t v;
         std::memcpy(&v, base + byte, 8);
         v >>= bit % 8;                                          // >= 56 valid bits
@@ -337,9 +344,13 @@ class Inflate {
         if (((v >> 3) & 31) > 29 || ((v >> 8) & 31) > 29) return false;
         const int hclen = (int)((v >> 13) & 15) + 4;
         static const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+        // the precode lengths: bits 17 .. 17 + 3 * hclen (up to 57 of them) — one 64-bit load holds
+        // 64 - ((bit % 8) + 1) >= 56, so the 19th length's last bit comes from the next byte then
         uint64_t w;
-        std::memcpy(&w, base + byte + 2, 8);                    // the precode lengths: bits 17 ..
-        w >>= (bit % 8) + 1;
+        std::memcpy(&w, base + byte + 2, 8);
+        const int sh = (int)(bit % 8) + 1;
+        w >>= sh;
+        if (sh > 7) w |= (uint64_t)base[byte + 10] << (64 - sh);
         int count[8] = {0};
         for (int i = 0; i < hclen; ++i) count[(w >> (3 * i)) & 7]++;
         (void)order;

@@ -25,6 +25,7 @@
 
 #include "../../include/fednpz.h"
 #include "inflate.h"
+#include "pdeflate.h"
 
 namespace fnpz_internal {
 int set_error(int code, const char* fmt, ...);
@@ -33,6 +34,19 @@ int set_error(int code, const char* fmt, ...);
 namespace {
 
 using fnpz_internal::set_error;
+
+// members of at least this many bytes take pdeflate.h's single-stream parallel path
+std::atomic<int64_t> g_par_min{32ll << 20}, g_par_chunk{4ll << 20};
+std::atomic<int64_t> g_par_ok{0}, g_par_fallback{0};
+thread_local const char* g_par_reason = nullptr;
+
+// the member's deflate() inputs as cumulative ends: the header, then numpy's writes
+std::vector<int64_t> input_ends(int64_t hlen, int64_t nbytes, int64_t seg) {
+    std::vector<int64_t> ends{hlen};
+    if (seg <= 0) seg = std::max<int64_t>(nbytes, 1);
+    for (int64_t b = 0; b < nbytes; b += seg) ends.push_back(hlen + std::min(nbytes, b + seg));
+    return ends;
+}
 
 void put16(uint8_t*& p, uint32_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p += 2; }
 void put32(uint8_t*& p, uint32_t v) { for (int i = 0; i < 4; ++i) p[i] = (uint8_t)(v >> (8 * i)); p += 4; }
@@ -55,6 +69,36 @@ struct Member {
     uint32_t crc = 0;
     int rc = Z_OK;
 };
+
+// the same stream from pdeflate.h on `threads` threads; false: the caller runs zlib
+bool deflate_member_parallel(Member& m, int threads) {
+    const int64_t L = m.hlen + m.nbytes;
+    std::vector<uint8_t> S((size_t)L);
+    std::memcpy(S.data(), m.header, (size_t)m.hlen);
+    const int64_t piece = 8 << 20;
+    pdef::parallel((int)((m.nbytes + piece - 1) / piece), threads, [&](int i) {
+        const int64_t b = (int64_t)i * piece;
+        std::memcpy(S.data() + m.hlen + b, m.data + b, (size_t)std::min(piece, m.nbytes - b));
+    });
+    pdef::Stats st;
+    const bool ok = pdef::deflate_exact(S.data(), L, input_ends(m.hlen, m.nbytes, m.seg), threads, g_par_chunk.load(),
+                                        m.out, &st);
+    (ok ? g_par_ok : g_par_fallback).fetch_add(1);
+    g_par_reason = st.fallback;
+    if (!ok) return false;
+    // CRC-32 by pieces, combined
+    const int np = (int)((L + piece - 1) / piece);
+    std::vector<uint32_t> crcs((size_t)np);
+    pdef::parallel(np, threads, [&](int i) {
+        const int64_t b = (int64_t)i * piece;
+        crcs[i] = fnpz_fast::crc32(0, S.data() + b, (size_t)std::min(piece, L - b));
+    });
+    uLong crc = crcs[0];
+    for (int i = 1; i < np; ++i) crc = crc32_combine(crc, crcs[i], (z_off_t)std::min(piece, L - (int64_t)i * piece));
+    m.crc = (uint32_t)crc;
+    m.rc = Z_OK;
+    return true;
+}
 
 // zlib.compressobj(-1, DEFLATED, -15).compress(w) for each write w, then .flush()
 void deflate_member(Member& m) {
@@ -118,15 +162,23 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
         ms[i] = Member{names[i], headers[i], header_lens[i], static_cast<const uint8_t*>(datas[i]), nbytes[i],
                        seg_bytes ? seg_bytes[i] : 0};
     }
-    // largest members first so one big stream does not start last
-    std::vector<int> order((size_t)n);
-    for (int i = 0; i < n; ++i) order[i] = i;
+    // big members one after another on every thread (pdeflate.h); the rest member-parallel, largest
+    // first so one long stream does not start last
+    std::vector<int> order;
+    for (int i = 0; i < n; ++i) {
+        if (threads > 1 && ms[i].hlen + ms[i].nbytes >= g_par_min.load()) {
+            if (!deflate_member_parallel(ms[i], threads)) deflate_member(ms[i]);
+        } else {
+            order.push_back(i);
+        }
+    }
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return ms[a].nbytes > ms[b].nbytes; });
+    const int nrest = (int)order.size();
     std::atomic<int> next{0};
     auto work = [&] {
-        for (int k; (k = next.fetch_add(1)) < n;) deflate_member(ms[order[k]]);
+        for (int k; (k = next.fetch_add(1)) < nrest;) deflate_member(ms[order[k]]);
     };
-    const int nt = std::max(1, std::min(threads, n));
+    const int nt = std::max(1, std::min(threads, nrest));
     std::vector<std::thread> pool;
     for (int t = 1; t < nt; ++t) pool.emplace_back(work);
     work();
@@ -244,4 +296,35 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
     put16(p, 0);
     *out_len = (int64_t)(p - out);
     return FNPZ_OK;
+}
+
+extern "C" void fnpz_savez_config(int64_t min_member, int64_t chunk, int64_t* parallel, int64_t* fallback) {
+    if (min_member > 0) g_par_min.store(min_member);
+    if (chunk > 0) g_par_chunk.store(chunk);
+    if (parallel) *parallel = g_par_ok.load();
+    if (fallback) *fallback = g_par_fallback.load();
+}
+
+extern "C" int fnpz_deflate_exact(const uint8_t* in, int64_t len, const int64_t* ends, int nends, int threads,
+                                  int64_t chunk, uint8_t* out, int64_t out_cap, int64_t* out_len) {
+    if (!in || len <= 0 || !ends || nends <= 0 || !out || !out_len || ends[nends - 1] != len)
+        return set_error(FNPZ_EINVAL, "fnpz_deflate_exact: bad arguments");
+    std::vector<int64_t> e(ends, ends + nends);
+    std::vector<uint8_t> res;
+    pdef::Stats st;
+    if (!pdef::deflate_exact(in, len, e, std::max(1, threads), chunk, res, &st))
+        return set_error(FNPZ_EFALLBACK, "fnpz_deflate_exact: %s", st.fallback ? st.fallback : "fallback");
+    if ((int64_t)res.size() > out_cap) return set_error(FNPZ_ENOSPC, "fnpz_deflate_exact: output buffer too small");
+    std::memcpy(out, res.data(), res.size());
+    *out_len = (int64_t)res.size();
+    set_error(FNPZ_OK, "chunks %d fixups %d blocks %d tail_from %lld parse %.3f sync %.3f sched %.3f plan %.3f encode %.3f",
+              st.chunks, st.fixups, st.blocks, (long long)st.tail_from, st.t_parse, st.t_sync, st.t_sched, st.t_plan,
+              st.t_encode);
+    return FNPZ_OK;
+}
+
+// the parallel decoder's block-header pre-check (inflate.h Inflate::maybe_dynamic_header), for tests
+extern "C" int fnpz_probe_dynamic_header(const uint8_t* in, int64_t len, int64_t bit) {
+    if (!in || len < 0 || bit < 0) return 0;
+    return fnpz_fast::Inflate::maybe_dynamic_header(in, (size_t)len, (uint64_t)bit) ? 1 : 0;
 }

@@ -119,8 +119,8 @@ def stage_sharded(layout, pinned, devices, streams, host=None):
     bufs, ready = [], []
     for d, dv in enumerate(devices):
         with torch.cuda.device(dv):
-            buf = torch.empty(dev_bytes[d], dtype=torch.uint8, device=dv)
-            with torch.cuda.stream(streams[d]):
+            with torch.cuda.stream(streams[d]):   # allocated on the stream that writes it
+                buf = torch.empty(dev_bytes[d], dtype=torch.uint8, device=dv)
                 for dt in layout.groups:
                     lo, hi = bounds[dt][d]
                     if hi > lo:
@@ -143,9 +143,9 @@ def stage_arrays(arrays, device, stream):
     layout = Layout.of(arrays)
     pinned = torch.empty(layout.nbytes, dtype=torch.uint8, pin_memory=True)
     layout.pack(arrays, pinned.numpy())
-    dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
     ready = torch.cuda.Event()
-    with torch.cuda.stream(stream):
+    with torch.cuda.stream(stream):                 # allocated on the stream that writes it
+        dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
         dev.copy_(pinned, non_blocking=True)
         ready.record(stream)
     # the pinned block returns to torch's caching host allocator only after the copy
@@ -166,9 +166,9 @@ def stage_npz(data, device, stream):
 
 def stage_pinned(layout, pinned, device, stream, host=None):
     """Copy a pinned, layout-packed update (uint8 tensor) to a new device buffer on ``stream``."""
-    dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
     ready = torch.cuda.Event()
-    with torch.cuda.stream(stream):
+    with torch.cuda.stream(stream):                 # allocated on the stream that writes it
+        dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
         dev.copy_(pinned, non_blocking=True)
         ready.record(stream)
     ready.synchronize()
@@ -194,9 +194,9 @@ def stage_decoded(decoded, device, stream):
     from .upload import DeviceDecodedUpdate
     if isinstance(decoded, DeviceDecodedUpdate):
         layout = Layout(decoded.shapes, decoded.dtypes)
-        dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
         ready = torch.cuda.Event()
         with torch.cuda.stream(stream):
+            dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
             stream.wait_event(decoded.ready)
             for dt in layout.groups:
                 g0 = layout.group_byte_offset[dt]
@@ -207,9 +207,9 @@ def stage_decoded(decoded, device, stream):
         ready.synchronize()               # the per-tensor blocks are released after the copies
         return StagedModel(layout, dev, ready)
     layout = Layout.of(decoded.arrays)
-    dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
     ready = torch.cuda.Event()
     with torch.cuda.stream(stream):
+        dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
         for dt in layout.groups:
             g0 = layout.group_byte_offset[dt]
             for i, e0, n, o in _member_spans(layout, dt, 0, layout.group_elems[dt]):
@@ -229,8 +229,8 @@ def stage_decoded_sharded(decoded, devices, streams):
     bufs, ready = [], []
     for d, dv in enumerate(devices):
         with torch.cuda.device(dv):
-            buf = torch.empty(dev_bytes[d], dtype=torch.uint8, device=dv)
-            with torch.cuda.stream(streams[d]):
+            with torch.cuda.stream(streams[d]):   # allocated on the stream that writes it
+                buf = torch.empty(dev_bytes[d], dtype=torch.uint8, device=dv)
                 for dt in layout.groups:
                     lo, hi = bounds[dt][d]
                     base, isz = dev_off[d][dt], dt.itemsize
@@ -311,7 +311,7 @@ class StagingUpdateHandler:
         """Whether uploads should be decoded as they stream in: npz helpers only (binaryhelper
         holds raw float64 bytes; androidhelper updates are folded from the host)."""
         from .staging import helper_kind
-        return self.native_decode and helper_kind(self.helper) not in ("binaryhelper", "androidhelper")
+        return self.native_decode and helper_kind(self.helper, strict=False) not in ("binaryhelper", "androidhelper", "unknown")
 
     def upload_device(self):
         """The device uploads are decoded into (upload.DeviceSink), or None when updates are
@@ -388,7 +388,7 @@ class StagingUpdateHandler:
         """Raw-bytes decode applies to npz (numpyhelper / fednamdhelper); binaryhelper's raw
         float64 bytes go through the helper's own load."""
         from .staging import helper_kind
-        return self.native_decode and helper_kind(self.helper) != "binaryhelper" and \
+        return self.native_decode and helper_kind(self.helper, strict=False) not in ("binaryhelper", "unknown") and \
             hasattr(self.inner, "load_model_update_byte")
 
     def _admit(self, layout, devs, parts):
@@ -483,8 +483,10 @@ class StagingUpdateHandler:
         except (KeyError, TypeError, ValueError):
             valid = False
         from .staging import helper_kind
-        if valid and helper_kind(self.helper) == "androidhelper":
-            valid = False    # one flat array with its own fold rule: the aggregator takes it from the host
+        if valid and helper_kind(self.helper, strict=False) in ("androidhelper", "unknown"):
+            # one flat array with its own fold rule (or a helper the aggregators refuse): the
+            # aggregator takes it from the host
+            valid = False
         if valid:
             self._device()
             with self._lock:

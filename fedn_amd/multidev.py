@@ -169,6 +169,12 @@ class _ShardedStaging:
         self.pending = []                              # resident updates not folded yet: (model, n, N, tag)
         self.skipped = []                              # (tag, exception): see staging._Pipeline.skipped
         self.broken = None
+        # resident updates read by enqueued launches: kept until the pipeline (the round) ends, as
+        # staging._Pipeline._hold does. Dropped when their fold is merely enqueued, their HBM went
+        # back to torch's allocator and a staging worker could refill it (H2D on its own stream)
+        # before the compute stream had read it — a multi-device round then folded another
+        # update's bytes (GPU test test_multidevice_sharded_ingest_fedavg[3-70], round 5)
+        self._hold = []
 
     def take_skipped(self):
         out, self.skipped = self.skipped, []
@@ -221,9 +227,11 @@ class _ShardedStaging:
         return isinstance(arrays, ShardedStagedModel) and _same_devices(arrays.devices, self.devices)
 
     def _accept(self, model):
-        """Order every device's compute stream after the resident update's H2D."""
+        """Order every device's compute stream after the resident update's H2D; hold its HBM until
+        the round ends (see ``_hold``)."""
         for d in range(len(self.devices)):
             self.compute[d].wait_event(model.ready[d])
+        self._hold.append(model)
 
     # ---- per-tensor path (mixed.py) on the first device: updates that differ in layout ------
     def compatible(self, arrays):

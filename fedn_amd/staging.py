@@ -912,17 +912,34 @@ class FedAvgPipeline(_Pipeline):
         return out
 
 
-def helper_kind(helper):
+class UnsupportedHelper(TypeError):
+    """A helper plug-in whose arithmetic the aggregators do not implement."""
+
+
+KNOWN_HELPERS = ("numpyhelper", "binaryhelper", "androidhelper", "fednamdhelper")
+
+
+def helper_kind(helper, strict=True):
     """Which FEDn helper plug-in a round uses. package.py:24 accepts numpyhelper, binaryhelper
-    and androidhelper; the aggregators fold with the helper's own arithmetic (fedavg.py:68).
-    androidhelper sets ``name`` and HelperBase resets it to the class name, so the plug-in's
-    module decides; None (tests, tools) means numpyhelper."""
+    and androidhelper (plus this package's fednamdhelper); the aggregators fold with the helper's
+    own arithmetic (fedavg.py:68), so each is recognised by its plug-in module (androidhelper sets
+    ``name`` and HelperBase resets it to the class name). None (tests, tools) means numpyhelper.
+    Any other helper: UnsupportedHelper (raised inside combine_models' per-update try, so every
+    update is logged and skipped and the round returns (None, data) — its arithmetic is never
+    guessed), or "unknown" with ``strict=False`` (the ingest then leaves its updates host-side)."""
     if helper is None:
         return "numpyhelper"
     mod = type(helper).__module__.rsplit(".", 1)[-1]
     if mod in ("numpyhelper", "binaryhelper", "androidhelper"):
         return mod
-    return getattr(helper, "name", "numpyhelper")
+    from .helper import Helper as OwnHelper
+    if isinstance(helper, OwnHelper) or mod == "fednamdhelper":
+        return "fednamdhelper"
+    if not strict:
+        return "unknown"
+    raise UnsupportedHelper(f"helper {type(helper).__module__}.{type(helper).__name__} is not supported by the "
+                            f"fedn_amd aggregators (they implement {', '.join(KNOWN_HELPERS)}); its "
+                            f"increment_average is not assumed to be numpyhelper's")
 
 
 class AndroidFedAvgPipeline(_Pipeline):

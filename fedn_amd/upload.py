@@ -86,7 +86,9 @@ class DeviceSink:
             if not self.budget.reserve([(self.device, n)]):
                 raise MemoryError("HBM budget full: the upload is not decoded into HBM")
             self.reserved += n
-        return self.torch.empty(n, dtype=self.torch.uint8, device=self.device)
+        torch = self.torch
+        with torch.cuda.device(self.device), torch.cuda.stream(self.stream):   # allocated where it is written
+            return torch.empty(n, dtype=torch.uint8, device=self.device)
 
     def window(self, blk, offset):
         if self.fill and (self.cur is not blk or self.cur_off + self.fill != offset):

@@ -27,7 +27,7 @@ extern "C" {
 #define FNPZ_ABI_VERSION 6
 #define FNPZ_MAX_DIMS 64   /* numpy 2's NPY_MAXDIMS (ABI 6; 16 before) */
 
-enum fnpz_status { FNPZ_OK = 0, FNPZ_EFORMAT = 1, FNPZ_ECORRUPT = 2, FNPZ_EINVAL = 3, FNPZ_ENOSPC = 4 };
+enum fnpz_status { FNPZ_OK = 0, FNPZ_EFORMAT = 1, FNPZ_ECORRUPT = 2, FNPZ_EINVAL = 3, FNPZ_ENOSPC = 4, FNPZ_EFALLBACK = 5 };
 
 /* One archive member holding a .npy array. */
 typedef struct {
@@ -90,6 +90,24 @@ int fnpz_write(int n, const char* const* names, const uint8_t* const* headers, c
 int fnpz_savez(int n, const char* const* names, const uint8_t* const* headers, const int64_t* header_lens,
                const void* const* datas, const int64_t* nbytes, const int64_t* seg_bytes, int threads,
                uint8_t* out, int64_t out_cap, int64_t* out_len);
+
+/* fnpz_savez's single-stream parallel deflate (fedn_amd/csrc/pdeflate.h): a member of at least
+ * min_member bytes (default 32 MiB) is deflated on every thread in chunks of `chunk` bytes (default
+ * 4 MiB) by a reimplementation of zlib 1.2.11's level-6 parse and trees.c whose output is zlib's,
+ * byte for byte; an input it does not model falls back to zlib itself. Values <= 0 keep a setting.
+ * *parallel / *fallback (may be NULL): members that went parallel / fell back so far. */
+void fnpz_savez_config(int64_t min_member, int64_t chunk, int64_t* parallel, int64_t* fallback);
+
+/* That deflate on its own (tests): in[0, len) fed as deflate(Z_NO_FLUSH) calls ending at ends[0 ..
+ * nends) (ends[nends - 1] == len) and then Z_FINISH, raw (wbits -15), level 6, memLevel 8. FNPZ_OK
+ * with the stream in out, or FNPZ_EFALLBACK (fnpz_last_error says why) where the caller must use
+ * zlib. After FNPZ_OK, fnpz_last_error() describes the run (chunks, fix-ups, blocks). */
+int fnpz_deflate_exact(const uint8_t* in, int64_t len, const int64_t* ends, int nends, int threads, int64_t chunk,
+                       uint8_t* out, int64_t out_cap, int64_t* out_len);
+
+/* Test hook: 1 if in[] holds a plausible dynamic-Huffman block header at input bit `bit` (the
+ * parallel decoder's candidate filter: block type, code counts and a complete precode). */
+int fnpz_probe_dynamic_header(const uint8_t* in, int64_t len, int64_t bit);
 
 /* Streaming reader — an archive decoded while it arrives (ModelService.Upload chunks,
  * fedn/network/combiner/modelservice.py:198-221), members taken from their local headers in

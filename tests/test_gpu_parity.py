@@ -1021,6 +1021,37 @@ def _helper_stub(kind):
     return h
 
 
+@pytest.mark.parametrize("agg_name", ["fedavg", "fedopt"])
+def test_unknown_helper_is_refused_not_guessed(agg_name, caplog):
+    """A helper plug-in the aggregators do not implement: its increment_average is
+    not assumed to be numpyhelper's. Every update's fold raises UnsupportedHelper inside
+    combine_models' per-update try (fedavg.py:75-78 / fedopt.py:103-106: logged and skipped), so
+    the round returns (None, data) with nothing aggregated — never a model computed with another
+    helper's arithmetic."""
+    class HalfHelper:                     # e.g. a user plug-in with its own (different) rule
+        name = "numpyhelper"              # a name alone does not make it numpyhelper
+
+        def increment_average(self, m1, m2, n, N):
+            return [(x + y) / 2 for x, y in zip(m1, m2)]
+
+        def subtract(self, m1, m2, a=1.0, b=1.0):
+            return [x * a - y * b for x, y in zip(m1, m2)]
+
+    uh, agg = _plugin(agg_name)
+    rng = np.random.default_rng(3)
+    base = [rng.standard_normal(40).astype(np.float32)]
+    if agg_name == "fedopt":
+        uh.put_global_model(base, "global")
+    for k in range(3):
+        uh.submit([base[0] + np.float32(0.01 * k)], 10 + k, model_id="global")
+    import logging
+    with caplog.at_level(logging.ERROR, logger="fedn"):
+        model, data = agg.combine_models(helper=HalfHelper())
+    assert model is None
+    assert data["nr_aggregated_models"] == 0
+    assert "not supported by the fedn_amd aggregators" in caplog.text
+
+
 @pytest.mark.parametrize("name", case_names("helper_fedavg"))
 def test_helper_fedavg_plugin(name):
     """The plug-in folds with the session helper's rule: androidhelper's (1 - w)*x + w*y on one

@@ -509,3 +509,22 @@ def test_hbm_budget_accounting():
     assert b.used("cuda:0") == 0
     b.release([("cuda:1", 900)])
     assert b.used("cuda:1") == 0
+
+
+def test_helper_kind_recognises_plugins_and_refuses_others():
+    """staging.helper_kind: FEDn's three helper plug-ins by module, this package's Helper, None as
+    numpyhelper; anything else raises UnsupportedHelper (strict) or reads "unknown" (the ingest's
+    non-strict query) — a ``name`` attribute alone never selects numpyhelper's arithmetic."""
+    from fedn_amd.helper import Helper
+    from fedn_amd.staging import UnsupportedHelper, helper_kind
+    for kind in ("numpyhelper", "binaryhelper", "androidhelper"):
+        cls = type("Helper", (), {"__module__": f"fedn.utils.helpers.plugins.{kind}"})
+        assert helper_kind(cls()) == kind
+    assert helper_kind(None) == "numpyhelper"
+    assert helper_kind(Helper()) == "fednamdhelper"
+
+    class Custom:
+        name = "numpyhelper"
+    with pytest.raises(UnsupportedHelper, match="not supported"):
+        helper_kind(Custom())
+    assert helper_kind(Custom(), strict=False) == "unknown"

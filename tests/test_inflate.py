@@ -5,6 +5,7 @@ outputs resumed at arbitrary window sizes (the decoder stops at any output byte,
 included), sync-flushed ranges (fnpz_write's independently inflatable blocks), and corrupted or
 truncated streams: the decoder returns zlib's bytes for what zlib decodes, and rejects what zlib
 rejects before the requested length. CPU only."""
+import ctypes
 import zlib
 
 import numpy as np
@@ -289,3 +290,32 @@ def test_concurrent_parallel_decodes_share_the_pool(_small_parallel):
                 assert g.dtype == x.dtype and np.array_equal(g, x)
     after = codec.parallel_config()
     assert after[0] - before[0] >= 6
+
+
+def _header_bits(lengths, lead):
+    """A dynamic block header (BFINAL 0, BTYPE 2, HLIT 0, HDIST 0, HCLEN = len(lengths) - 4, then the
+    precode lengths, 3 bits each) behind ``lead`` zero bits, LSB-first as DEFLATE packs them."""
+    bits = [0] * lead + [0] + [0, 1] + [0] * 5 + [0] * 5
+    hclen = len(lengths) - 4
+    bits += [(hclen >> i) & 1 for i in range(4)]
+    for v in lengths:
+        bits += [(v >> i) & 1 for i in range(3)]
+    bits += [0] * (8 * 16)
+    out = bytearray((len(bits) + 7) // 8)
+    for i, b in enumerate(bits):
+        out[i // 8] |= b << (i % 8)
+    return bytes(out)
+
+
+@pytest.mark.parametrize("lead", range(8))
+def test_header_finder_reads_all_57_precode_bits(lead):
+    """with the header at bit offset 7 and HCLEN = 19, the 19th precode length's top bit
+    is the 57th bit after the first load's shift. A complete precode whose 19th length is 4 (0b100):
+    read right it is complete (accepted); that bit read as 0 would leave it incomplete (rejected)."""
+    lib = codec.load_lib()
+    lib.fnpz_probe_dynamic_header.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64]
+    complete = [1, 2, 3, 4] + [0] * 14 + [4]          # 1/2 + 1/4 + 1/8 + 1/16 + 1/16
+    incomplete = [1, 2, 3, 4] + [0] * 15
+    good, bad = _header_bits(complete, lead), _header_bits(incomplete, lead)
+    assert lib.fnpz_probe_dynamic_header(good, len(good), lead) == 1
+    assert lib.fnpz_probe_dynamic_header(bad, len(bad), lead) == 0
