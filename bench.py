@@ -127,8 +127,9 @@ def file_sha(path):
 
 def pmc_traffic(workload):
     """(HBM bytes per launch, provenance) from rocprofv3 PMC runs (tools/gpu_session.sh pmc) — only if
-    that entry was collected on the very libfedagg.so this run loaded (sha256 of the file; the build
-    is deterministic, so probe-only source edits do not invalidate it); else (None, reason)."""
+    the measured kernels' gfx950 code in the loaded libfedagg.so is the code the entry was collected
+    on (``code_sha`` over ``symbols``, fedn_amd/codeobj.py; entries without it: the sha256 of the
+    whole file); else (None, reason)."""
     from fedn_amd import _abi
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -141,6 +142,22 @@ def pmc_traffic(workload):
     src = {"file": "profiles/pmc_traffic.json", "workload": workload, "lib_sha": ent.get("lib_sha"),
            "kernel_src_sha": ent.get("kernel_src_sha"), "collected": ent.get("collected"),
            "read_bytes": ent.get("read_bytes"), "write_bytes": ent.get("write_bytes")}
+    if ent.get("code_sha") and ent.get("symbols"):
+        # keyed on the measured kernels' own gfx950 machine code + descriptors (fedn_amd/codeobj.py):
+        # valid on any build of the library whose those bytes are unchanged (another build path, other
+        # kernels edited), stale as soon as they change
+        from fedn_amd import codeobj
+        try:
+            now = codeobj.kernel_sha(_abi.lib_path(), ent["symbols"])
+        except (OSError, ValueError) as e:
+            now = None
+            src["note"] = f"code object unreadable: {e}"
+        src["code_sha"] = ent["code_sha"]
+        if now != ent["code_sha"]:
+            src.setdefault("note", "stale: the measured kernels' machine code changed since the PMC run; re-run "
+                                   "tools/gpu_session.sh pmc + tools/pmc_traffic.py --session")
+            return None, src
+        return ent["bytes"], src
     if ent.get("lib_sha") != file_sha(_abi.lib_path()):
         src["note"] = ("stale: collected on another build of libfedagg.so; re-run tools/gpu_session.sh pmc + "
                        "tools/pmc_traffic.py --session")
@@ -747,7 +764,7 @@ def main():
             try:
                 # double-buffered: one fence per step (the exit fence clears the other buffer); ONE set of
                 # IPC mappings serves both engines (the engine is switched between steps)
-                pa = P2PAllGather(full_all, spare=torch.empty_like(full_all))
+                pa = P2PAllGather(full_all, spare=torch.empty_like(full_all), verify="close")
                 for name in engines:
                     if a.transport in ("auto", name):
                         transports[name] = pa

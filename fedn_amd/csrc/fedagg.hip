@@ -478,8 +478,8 @@ k_fedavg_push(float* __restrict__ agg, const ClientTable<CF32::S> tab, const int
 // single-wave workgroups releases instead — but HIP does not promise which XCDs a grid's workgroups
 // land on, so each workgroup reads the XCD it runs on (HW_REG_XCC_ID) and ORs it into the caller's
 // release record (FA_REL_*, include/fedagg.h). The launch's last workgroup to arrive (an acq_rel
-// arrival counter: it sees every other workgroup's bit) compares the XCDs covered with the device's
-// XCD count and counts a miss; the record is read by the caller at its next synchronisation
+// arrival counter: it sees every other workgroup's bit) compares the number of distinct XCDs covered
+// with the device's XCD count and counts a miss; the record is read by the caller at its next synchronisation
 // (sharded.P2PAllGather.check_release), which fails the session on any miss. The mask and the
 // arrival counter are reset by that last workgroup, so the next launch on the stream starts clean.
 constexpr int kReleaseBlocks = 64;
@@ -498,7 +498,10 @@ __global__ void __launch_bounds__(64) k_release(unsigned* __restrict__ rec, unsi
     __hip_atomic_fetch_or(rec + FA_REL_SEEN, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(rec + FA_REL_LAUNCHES, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(rec + FA_REL_EXPECT, expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((seen & expect) != expect) __hip_atomic_fetch_add(rec + FA_REL_MISSES, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // distinct XCDs seen vs the device's count (a partition mode may number its XCDs by their
+    // physical index rather than 0 .. n - 1: the mask is reported, the count is what is checked)
+    if (__builtin_popcount(seen) < __builtin_popcount(expect))
+        __hip_atomic_fetch_add(rec + FA_REL_MISSES, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // XCDs of the current device (1 in a partition mode that exposes one XCD per device)

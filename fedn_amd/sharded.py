@@ -357,11 +357,18 @@ class P2PAllGather:
 
     ENGINES = ("dma", "kernel", "fused")
 
-    def __init__(self, full, group=None, spare=None, engine="dma"):
+    def __init__(self, full, group=None, spare=None, engine="dma", verify="round"):
         from . import ops
         if engine not in self.ENGINES:
             raise ValueError(f"P2PAllGather: engine must be one of {self.ENGINES}")
+        if verify not in ("round", "close"):
+            raise ValueError("P2PAllGather: verify must be 'round' or 'close'")
         self.engine = engine
+        # "round": every fence() reads the release records (one small D2H after the fence; under RCCL
+        # the host waits for the round there) and fails that round's exchange on a missed XCD or a
+        # release grid that never ran; "close": only close() / check_release() do (bench.py, whose
+        # timed steps must not block the host; it reads and reports the records itself)
+        self.verify = verify
         self.bufs = [full] if spare is None else [full, spare]
         self.cur = 0
         self.steps = 0
@@ -412,6 +419,7 @@ class P2PAllGather:
         self.nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
         self._flag = torch.zeros(1, dtype=torch.float32, device=self.device) if self.nccl else None
         self._release = {}                          # stream handle -> its release record (kernel engines)
+        self._issued = {}                           # stream handle -> release grids launched with it
 
     def release_rec(self, stream):
         """The release record of ``stream`` (one per stream: a record's reset is ordered by the stream)
@@ -421,7 +429,9 @@ class P2PAllGather:
         rec = self._release.get(key)
         if rec is None:
             from . import ops
-            rec = self._release[key] = ops.release_record(self.device)
+            with torch.cuda.stream(stream):      # zeroed in the order of the stream that fills it
+                rec = self._release[key] = ops.release_record(self.device)
+        self._issued[key] = self._issued.get(key, 0) + 1   # each use is one release grid launch
         return rec
 
     def check_release(self):
@@ -439,6 +449,10 @@ class P2PAllGather:
             tot["expect_mask"] |= r["expect_mask"]
         tot["xcds_seen"] = bin(tot["seen_mask"]).count("1")
         tot["xcds"] = ops.device_xccs(self.device)
+        issued = sum(self._issued.values())
+        if tot["launches"] != issued:
+            raise _abi.FedAggError(_abi.FA_EHIP, f"P2PAllGather: {tot['launches']} release grids recorded, {issued} "
+                                                 f"launched: a release did not run (or its record was reset)")
         if tot["misses"]:
             raise _abi.FedAggError(_abi.FA_EHIP, f"P2PAllGather: {tot['misses']} of {tot['launches']} release grids "
                                                  f"did not cover every XCD (seen {tot['seen_mask']:#x}, device "
@@ -491,13 +505,16 @@ class P2PAllGather:
         for st in self.streams.values():
             cur.wait_stream(st)
         cur.wait_stream(self.push_stream)
-        if self.world == 1 or not dist.is_initialized():
-            return
-        if self.nccl:
-            dist.all_reduce(self._flag, group=self.group)
-        else:
-            torch.cuda.synchronize(self.device)
-            dist.barrier(group=self.group)
+        if self.world > 1 and dist.is_initialized():
+            if self.nccl:
+                dist.all_reduce(self._flag, group=self.group)
+            else:
+                torch.cuda.synchronize(self.device)
+                dist.barrier(group=self.group)
+        if self.verify == "round" and self._release:
+            # this round's release records, read after the fence (check_release's D2H is ordered after
+            # it on the current stream): a miss fails the round's exchange here, not at close()
+            self.check_release()
 
     def close(self, fence=True, check=True):
         """Unmap the peers' buffers (after a fence: no copy into them is in flight). ``check``: the

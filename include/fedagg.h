@@ -273,10 +273,12 @@ int fa_cast(void* out, int out_dtype, const void* in, int in_dtype, int ndim, co
  *                    which XCDs a grid's workgroups run on, so each release workgroup records its
  *                    XCD (HW_REG_XCC_ID) in release_rec: FA_RELEASE_WORDS uint32 of caller-owned
  *                    DEVICE memory, zeroed once before the first call and then passed to every call
- *                    on one stream. Per release launch, the last workgroup compares the XCDs covered
- *                    with the device's XCD count and increments FA_REL_MISSES on a gap; FA_REL_LAUNCHES
- *                    counts the launches checked, FA_REL_SEEN is the union of the XCDs seen and
- *                    FA_REL_EXPECT the mask of the device's XCDs. The caller reads the record at a
+ *                    on one stream. Per release launch, the last workgroup compares the number of
+ *                    distinct XCDs covered with the device's XCD count (IDs are counted, not matched
+ *                    against 0 .. n - 1: a partition mode may report physical indices) and
+ *                    increments FA_REL_MISSES on a gap; FA_REL_LAUNCHES counts the launches checked,
+ *                    FA_REL_SEEN is the union of the XCDs seen and FA_REL_EXPECT the mask
+ *                    (1 << n) - 1 of the device's XCD count. The caller reads the record at a
  *                    synchronisation point and must treat MISSES > 0 as a failed exchange. NULL:
  *                    release without the record (in-process peers behind a device synchronize).
  * fa_device_xccs     *n = the number of XCDs (each with its own L2) of device dev

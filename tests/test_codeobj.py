@@ -1,0 +1,68 @@
+"""PMC evidence is keyed on the measured kernels' machine code, not on the library file (VERDICT r4
+#5). hipcc embeds a ``__hip_cuid_<hash>`` that follows the build paths, so two builds of the same
+source differ as files; fedn_amd/codeobj.py hashes only the gfx950 code and descriptors of the named
+kernels, so bench.py keeps profiles/pmc_traffic.json's ``traffic`` after a fresh build() anywhere —
+and drops it once a measured kernel's code changes."""
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from fedn_amd import codeobj
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = r'''
+#include <hip/hip_runtime.h>
+__global__ void k_scale(float* x, float a, int n) { int i = blockIdx.x * blockDim.x + threadIdx.x; if (i < n) x[i] *= a; }
+__global__ void k_other(float* x, int n) { int i = blockIdx.x * blockDim.x + threadIdx.x; if (i < n) x[i] += OTHER; }
+extern "C" int launch(float* x, int n) { hipLaunchKernelGGL(k_scale, dim3((n + 255) / 256), dim3(256), 0, 0, x, 2.0f, n); return 0; }
+'''
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    pytest.skip("hipcc not found")
+
+
+def _build(tmp, sub, other):
+    d = tmp / sub
+    d.mkdir(parents=True)
+    (d / "k.hip").write_text(SRC)
+    out = d / "libk.so"
+    subprocess.run([_hipcc(), "-O3", "-fPIC", "-shared", "--offload-arch=gfx950", f"-DOTHER={other}", "-o", str(out),
+                    "k.hip"], cwd=d, check=True, capture_output=True)
+    return str(out)
+
+
+def _file_sha(p):
+    return hashlib.sha256(open(p, "rb").read()).hexdigest()[:16]
+
+
+def test_two_build_paths_one_kernel_key(tmp_path):
+    a = _build(tmp_path, "one/deep/path", "1.0f")
+    b = _build(tmp_path, "another", "1.0f")
+    c = _build(tmp_path, "third", "3.0f")          # k_other edited, k_scale untouched
+    assert _file_sha(a) != _file_sha(b)             # the files differ (build-path cuid)
+    na, nb = codeobj.kernels_matching(a, "k_scale"), codeobj.kernels_matching(b, "k_scale")
+    assert na == nb and any(n.endswith(".kd") for n in na)
+    assert codeobj.kernel_sha(a, na) == codeobj.kernel_sha(b, nb) == codeobj.kernel_sha(c, na)
+    no = codeobj.kernels_matching(a, "k_other")
+    assert codeobj.kernel_sha(a, no) == codeobj.kernel_sha(b, no) != codeobj.kernel_sha(c, no)
+    assert codeobj.kernel_sha(a, ["not_a_kernel"]) is None
+
+
+def test_shipped_pmc_entries_match_the_in_tree_library():
+    """Every PMC entry bench.py reports carries a code key, and the in-tree libfedagg.so (whatever
+    path it was built at) still has those kernels' bytes: bench.py keeps its ``traffic``."""
+    lib = os.path.join(ROOT, "fedn_amd", "libfedagg.so")
+    if not os.path.exists(lib):
+        pytest.skip("libfedagg.so not built")
+    db = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    for key, ent in db.items():
+        assert ent.get("symbols") and ent.get("code_sha"), key
+        assert codeobj.kernel_sha(lib, ent["symbols"]) == ent["code_sha"], key

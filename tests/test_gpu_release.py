@@ -139,3 +139,51 @@ def test_p2p_allgather_check_release_world1(engine):
     r = p2p.check_release()
     assert r["launches"] == 3 * cyc.rounds and r["misses"] == 0 and r["xcds_seen"] == r["xcds"]
     p2p.close()
+
+
+def test_p2p_allgather_checks_every_round_and_fails_the_round_on_a_miss():
+    """a session that keeps its P2PAllGather across rounds has each round's release
+    records read at that round's fence (verify="round", the default) — not only at close(). A miss
+    injected into the record after round 2 fails round 3's exchange right there; with
+    verify="close" (bench.py's timed steps) it surfaces at close()."""
+    from fedn_amd import _abi
+    from fedn_amd.sharded import CyclicShardedFedAvg, P2PAllGather
+    P, K = 200_000, 3
+    cyc = CyclicShardedFedAvg(P, chunk=65536)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    ups = [torch.randn(cyc.local_len, generator=g, device=DEV) for _ in range(K)]
+    ns, Ns = [2, 3, 4], [2, 5, 9]
+    agg = torch.empty(cyc.local_len, device=DEV)
+    for verify in ("round", "close"):
+        full = torch.empty(cyc.full_len, device=DEV)
+        p2p = P2PAllGather(full, spare=torch.empty_like(full), engine="kernel", verify=verify)
+        for _ in range(2):
+            cyc.fold_allgather(agg, ups, ns, Ns, True, p2p=p2p)
+        rec = next(iter(p2p._release.values()))
+        rec[_abi.FA_REL_MISSES] += 1                      # a release grid that missed an XCD
+        if verify == "round":
+            with pytest.raises(_abi.FedAggError, match="did not cover every XCD"):
+                cyc.fold_allgather(agg, ups, ns, Ns, True, p2p=p2p)
+            p2p.close(check=False)
+        else:
+            cyc.fold_allgather(agg, ups, ns, Ns, True, p2p=p2p)    # not read until close()
+            with pytest.raises(_abi.FedAggError, match="did not cover every XCD"):
+                p2p.close()
+
+
+def test_p2p_allgather_release_count_must_match_launches():
+    """A release grid that never ran (or a record reset under it) is a failure too: the records'
+    launch count must equal the release grids issued."""
+    from fedn_amd import _abi
+    from fedn_amd.sharded import CyclicShardedFedAvg, P2PAllGather
+    cyc = CyclicShardedFedAvg(100_000, chunk=65536)
+    ups = [torch.ones(cyc.local_len, device=DEV)]
+    full = torch.empty(cyc.full_len, device=DEV)
+    p2p = P2PAllGather(full, engine="kernel", verify="close")
+    agg = torch.empty(cyc.local_len, device=DEV)
+    cyc.fold_allgather(agg, ups, [1], [1], True, p2p=p2p)
+    torch.cuda.synchronize()
+    next(iter(p2p._release.values()))[_abi.FA_REL_LAUNCHES] -= 1
+    with pytest.raises(_abi.FedAggError, match="release grids recorded"):
+        p2p.check_release()
+    p2p.close(check=False)

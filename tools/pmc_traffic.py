@@ -39,6 +39,18 @@ def lib_sha(session=None):
     return file_sha(os.path.join(ROOT, "fedn_amd", "libfedagg.so"))
 
 
+def code_key(kernel, lib=None):
+    """(mangled symbols, sha) of the measured kernels' gfx950 machine code in ``lib`` (default: the
+    in-tree libfedagg.so, built from the source the PMC runs used): bench.py keeps an entry's traffic
+    while the library it loads has the same bytes for those kernels (fedn_amd/codeobj.py)."""
+    from fedn_amd import codeobj
+    lib = lib or os.path.join(ROOT, "fedn_amd", "libfedagg.so")
+    names = codeobj.kernels_matching(lib, kernel)
+    if not names:
+        raise SystemExit(f"no kernel matching {kernel!r} in {lib}")
+    return names, codeobj.kernel_sha(lib, names)
+
+
 def per_launch(path, kernel, take=None):
     """Average counter value per dispatch of the kernels whose name contains ``kernel`` (a string, or
     a tuple of strings that must all appear); ``take`` = (first, stop): only those dispatches of
@@ -67,6 +79,7 @@ def record(d, key, kernel, alg=None, session=None, take=None):
                "alg_bytes": alg, "traffic_over_alg": None if not alg else (read_b + write_b) / alg,
                "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count on 16-B streaming loads); "
                              "write = WRITE_SIZE x 1024"}
+    db[key]["symbols"], db[key]["code_sha"] = code_key(kernel)
     json.dump(db, open(out, "w"), indent=1)
     print(json.dumps({key: db[key]}))
 
@@ -116,11 +129,25 @@ def record_rank(session, world, R=8, sub=None):
                "alg_bytes": alg, "traffic_over_alg": (read_b + write_b) / alg,
                "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count on 16-B streaming loads); "
                              "write = WRITE_SIZE x 1024"}
+    db[key]["symbols"], db[key]["code_sha"] = code_key(kernel)
     json.dump(db, open(out, "w"), indent=1)
     print(json.dumps({key: db[key]}))
 
 
+def annotate(lib):
+    """Key every existing entry on its kernels' machine code in ``lib`` — a build of the fedagg.hip the
+    entries were collected on (their kernel_src_sha), at any path."""
+    out = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    db = json.load(open(out))
+    for key, ent in db.items():
+        ent["symbols"], ent["code_sha"] = code_key(ent["kernel"], lib)
+        print(key, ent["code_sha"], len(ent["symbols"]))
+    json.dump(db, open(out, "w"), indent=1)
+
+
 def main():
+    if sys.argv[1] == "--annotate":
+        return annotate(sys.argv[2])
     if sys.argv[1] == "--rank-session":
         for world in (2, 4, 8):
             for R in (1, 2, 4, 8, 16):   # bench.py AG_ROUNDS
