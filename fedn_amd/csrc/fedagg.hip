@@ -1231,6 +1231,80 @@ k_fedopt_mix(const OptBuffers b, const ClientTable<S> tab, const int K, const in
 }
 #endif
 
+#ifdef FEDAGG_PROBES
+// burst-store probe (FA_TUNE_OPT_BURST = G): k_fedopt_mix's access pattern, but each
+// wave takes G consecutive wave tiles and holds the new v / out / m of all G in registers (LDS
+// staging of several tiles would leave one workgroup per CU), storing them together after the
+// reads of the last one — the writes leave the wave in one burst of 3 x G KiB-lines per stream
+// instead of interleaved with every tile's reads. Whole groups of G tiles only.
+template <typename Y, typename OLD, typename S, bool NT, int G>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_mixg(const OptBuffers b, const ClientTable<S> tab, const int K, const int64_t P) {
+    constexpr int NH = 4, H = 2, E = 2 * NH, U = kUnroll / 2;
+    constexpr int64_t T = 128 * NH;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if ((wave + 1) * G * T > P) return;
+    double vo[G][E], oo[G][E], mo[G][E];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int64_t i0 = (wave * G + g) * T + 2 * (threadIdx.x & 63);
+        auto at = [i0](int h) { return i0 + (int64_t)h * 128; };
+        double acc[E];
+        {
+            OLD old[E];
+#pragma unroll
+            for (int h = 0; h < NH; ++h)
+                strip_load<OLD, H, false>(static_cast<const OLD*>(b.old) + at(h), *reinterpret_cast<OLD(*)[H]>(&old[h * H]));
+#pragma unroll
+            for (int e = 0; e < E; ++e) acc[e] = (double)widen<OLD, double>(old[e]);
+        }
+        auto add_client = [&](int k, Y (&y)[E]) {
+            const Y* yp = static_cast<const Y*>(tab.ptr[k]);
+#pragma unroll
+            for (int h = 0; h < NH; ++h) strip_load<Y, H, NT>(yp + at(h), *reinterpret_cast<Y(*)[H]>(&y[h * H]));
+        };
+        int k = 0;
+        for (; k + U <= K; k += U) {
+            Y y[U][E];
+#pragma unroll
+            for (int u = 0; u < U; ++u) add_client(k + u, y[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int e = 0; e < E; ++e) acc[e] += (double)widen<Y, double>(y[u][e]);
+        }
+        for (; k < K; ++k) {
+            Y y[E];
+            add_client(k, y);
+#pragma unroll
+            for (int e = 0; e < E; ++e) acc[e] += (double)widen<Y, double>(y[e]);
+        }
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            double mi[H] = {}, vv[H] = {};
+            opt_load_state<H>(b, OptScalars{}, at(h), H, mi, vv);
+#pragma unroll
+            for (int e = 0; e < H; ++e) {
+                mo[g][h * H + e] = mi[e] + acc[h * H + e];
+                vo[g][h * H + e] = vv[e] + acc[h * H + e];
+                oo[g][h * H + e] = acc[h * H + e];
+            }
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int64_t i0 = (wave * G + g) * T + 2 * (threadIdx.x & 63);
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            const int64_t o = i0 + (int64_t)h * 128;
+            strip_store<double, H, 1>(static_cast<double*>(b.v_out) + o, *reinterpret_cast<double(*)[H]>(&vo[g][h * H]));
+            strip_store<double, H, 1>(static_cast<double*>(b.out) + o, *reinterpret_cast<double(*)[H]>(&oo[g][h * H]));
+            strip_store<double, H, 1>(static_cast<double*>(b.m_out) + o, *reinterpret_cast<double(*)[H]>(&mo[g][h * H]));
+        }
+    }
+}
+#endif
+
 template <typename Y, typename OLD, class PG, int E, bool FIRST, bool FINAL, bool NT, bool NOST = false, int OSM = 0>
 __global__ void __launch_bounds__(kBlock)
 k_fedopt(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
@@ -1515,7 +1589,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0}, opt_burst{0};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -1760,6 +1834,19 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
     constexpr bool probe_combo = E == 4 && std::is_same<Y, float>::value &&
                                  (std::is_same<OLD, float>::value || std::is_same<OLD, double>::value);
     if constexpr (probe_combo) {
+        if (first && final_ && g_cfg.opt_burst) {
+            if (b.m_out_f64 != 1) return fail(FA_EINVAL, "fa_tune OPT_BURST probe: fp64 m out");
+            const int G = g_cfg.opt_burst;
+            const dim3 gb((unsigned)((P + 4 * 512 * G - 1) / (4 * 512 * G)));   // a ragged last group is skipped
+            switch (G) {
+#define FA_BURST(G_) \
+    case G_: hipLaunchKernelGGL((k_fedopt_mixg<Y, OLD, typename PG::S, NT, G_>), gb, dim3(kBlock), 0, st, b, tab, cnt, P); break;
+                FA_BURST(1) FA_BURST(2) FA_BURST(4)
+#undef FA_BURST
+                default: return fail(FA_EINVAL, "fa_tune OPT_BURST: 1, 2 or 4 tiles per wave");
+            }
+            return check_launch("fa_fedopt_step: kernel launch");
+        }
         if (first && final_ && g_cfg.opt_mix) {
             const dim3 gm((unsigned)((P + 4 * 512 - 1) / (4 * 512)));   // a ragged last tile is skipped
             hipLaunchKernelGGL((k_fedopt_mix<Y, OLD, typename PG::S, NT>), gm, dim3(kBlock), 0, st, b, tab, cnt, P);
@@ -2531,6 +2618,11 @@ int fa_tune(int knob, int value) {
             return FA_OK;
         case FA_TUNE_OPT_MIX:
             g_cfg.opt_mix = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_OPT_BURST:
+            if (value != 0 && value != 1 && value != 2 && value != 4)
+                return fail(FA_EINVAL, "fa_tune: burst-store probe 0 (off), 1, 2 or 4 tiles per wave");
+            g_cfg.opt_burst = value;
             return FA_OK;
         case FA_TUNE_WPE:
             if (value != 0 && value != 5 && value != 6 && value != 8)

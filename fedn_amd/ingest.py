@@ -16,7 +16,9 @@ handling and error semantics are unchanged: a decode that fails re-raises from
 137-140) logs and skips it, as FEDn would.
 """
 import json
+import queue
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -246,6 +248,34 @@ def stage_decoded_sharded(decoded, devices, streams):
     return ShardedStagedModel(layout, devices, bufs, ready)
 
 
+class Reaper:
+    """One daemon thread that drops the references it is handed: a large free (munmap of a host
+    block, hipHostUnregister, the caching allocators' bookkeeping) happens there instead of on the
+    round thread. ``close()`` waits until everything handed over is gone."""
+
+    def __init__(self):
+        self._q = queue.Queue()
+        self._t = None
+        self._lock = threading.Lock()
+
+    def drop(self, obj):
+        with self._lock:
+            if self._t is None:
+                self._t = threading.Thread(target=self._run, name="fedn_amd_reaper", daemon=True)
+                self._t.start()
+        self._q.put(obj)
+
+    def _run(self):
+        while True:
+            obj = self._q.get()
+            del obj
+            self._q.task_done()
+
+    def close(self):
+        if self._t is not None:
+            self._q.join()
+
+
 class StagingUpdateHandler:
     """Drop-in wrapper of a FEDn ``UpdateHandler`` that decodes + stages updates on arrival.
 
@@ -287,6 +317,8 @@ class StagingUpdateHandler:
         self._streams = {}
         self._lock = threading.Lock()
         self._staged = {}
+        self._reaper = Reaper()
+        self.delete_times = {"plugin_s": 0.0, "store_s": 0.0, "count": 0}
 
     def __getattr__(self, name):
         return getattr(self.inner, name)
@@ -506,10 +538,27 @@ class StagingUpdateHandler:
         return res
 
     def delete_model(self, model_update):
+        """FEDn's per-update delete (updatehandler.py:31-33, called in the aggregation loop,
+        fedavg.py:73-74): the wrapped handler's delete runs inline, as in the reference; this
+        handler's own copies of the update (a staged future, a decoded upload) are handed to the
+        reaper thread, so freeing their host / device memory never stalls the round.
+        ``delete_times`` accumulates both parts (seconds) and the count."""
+        t0 = time.perf_counter()
         with self._lock:
-            self._staged.pop(model_update.model_update_id, None)
-        self._uploads.pop(model_update.model_update_id)
-        return self.inner.delete_model(model_update)
+            staged = self._staged.pop(model_update.model_update_id, None)
+        upload = self._uploads.pop(model_update.model_update_id)
+        if staged is not None or upload is not None:
+            self._reaper.drop((staged, upload))
+        del staged, upload
+        t1 = time.perf_counter()
+        ok = self.inner.delete_model(model_update)
+        t2 = time.perf_counter()
+        d = self.delete_times
+        d["plugin_s"] += t1 - t0
+        d["store_s"] += t2 - t1
+        d["count"] += 1
+        return ok
 
     def close(self):
         self._pool.shutdown(wait=True)
+        self._reaper.close()

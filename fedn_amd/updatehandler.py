@@ -10,6 +10,7 @@ gRPC. Behaviour mirrors updatehandler.py:35-117: metadata must carry
 ``round_id`` is copied from the config (:106-116).
 """
 import json
+import os
 import queue
 import uuid
 from dataclasses import dataclass
@@ -46,6 +47,57 @@ class MemoryModelStore:
     def delete(self, model_id):
         return self.models.pop(model_id, None) is not None
 
+
+class TempFileModelStore:
+    """FEDn's TempModelStorage (tempmodelstorage.py:11-76) as far as the round sees it: an update's
+    bytes live in a file under ``directory`` (FEDN_MODEL_DIR), ``get`` reads the whole file back
+    (:27-41), ``delete`` is ``os.remove`` (:66-76). Non-bytes models (global models as arrays, the
+    tests' host updates) stay in memory. With MemoryModelService it is written chunk by chunk as
+    ModelService.Upload writes it (get_ptr, :43-53)."""
+
+    def __init__(self, directory=None):
+        import tempfile
+        self.dir = directory or tempfile.mkdtemp(prefix="fedn_models_")
+        self.models = {}
+        self._files = {}
+
+    def path(self, model_id):
+        return os.path.join(self.dir, str(model_id))
+
+    def open_write(self, model_id):
+        f = self._files.get(model_id)
+        if f is None:
+            f = self._files[model_id] = open(self.path(model_id), "wb")
+        return f
+
+    def commit(self, model_id):
+        f = self._files.pop(model_id, None)
+        if f is not None:
+            f.close()
+        self.models[model_id] = _ON_DISK
+
+    def put(self, model_id, arrays):
+        if isinstance(arrays, _NpzBytes):
+            with open(self.path(model_id), "wb") as f:
+                f.write(arrays.data)
+            arrays = _ON_DISK
+        self.models[model_id] = arrays
+
+    def get(self, model_id):
+        m = self.models.get(model_id)
+        if m is _ON_DISK:
+            with open(self.path(model_id), "rb") as f:
+                return _NpzBytes(f.read())
+        return m
+
+    def delete(self, model_id):
+        m = self.models.pop(model_id, None)
+        if m is _ON_DISK:
+            os.remove(self.path(model_id))
+        return m is not None
+
+
+_ON_DISK = object()
 
 MODEL_STATUS_OK = 0            # fedn.proto:147-153 (ModelStatus)
 MODEL_STATUS_IN_PROGRESS = 1
@@ -90,11 +142,18 @@ class MemoryModelService:
         self._parts = {}
 
     def Upload(self, request_iterator, context):
+        to_file = isinstance(self.store, TempFileModelStore)
         for request in request_iterator:
             if request.status == MODEL_STATUS_IN_PROGRESS:
-                self._parts.setdefault(request.id, []).append(bytes(request.data))
+                if to_file:                     # modelservice.py:208-214: each chunk written to the file
+                    self.store.open_write(request.id).write(request.data)
+                else:
+                    self._parts.setdefault(request.id, []).append(bytes(request.data))
             if request.status == MODEL_STATUS_OK and not request.data:
-                self.store.put(request.id, _NpzBytes(b"".join(self._parts.pop(request.id, []))))
+                if to_file:
+                    self.store.commit(request.id)
+                else:
+                    self.store.put(request.id, _NpzBytes(b"".join(self._parts.pop(request.id, []))))
                 return ModelResponse(id=request.id, status=MODEL_STATUS_OK, message="Got model successfully.")
         return None
 

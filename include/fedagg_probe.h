@@ -74,7 +74,11 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                     FA_TUNE_OPT_MIX = 21 /* FedOpt FIRST|FINAL, access-pattern probe: 1 = k_fedopt_c's exact loads
                                             and stores with one add per value instead of the arithmetic
                                             (results are NOT the reference's; a ragged last 2048-element
-                                            tile is skipped) */ };
+                                            tile is skipped) */,
+                    FA_TUNE_OPT_BURST = 22 /* FedOpt FIRST|FINAL, burst-store probe (fp64 m out): G = 1, 2 or 4
+                                              wave tiles per wave with k_fedopt_mix's loads, the new v / out / m
+                                              of all G held in registers and stored together after the last
+                                              tile's reads (0 = off; a ragged last group is skipped) */ };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);

@@ -528,3 +528,53 @@ def test_helper_kind_recognises_plugins_and_refuses_others():
     with pytest.raises(UnsupportedHelper, match="not supported"):
         helper_kind(Custom())
     assert helper_kind(Custom(), strict=False) == "unknown"
+
+
+def test_temp_file_store_mirrors_tempmodelstorage(tmp_path):
+    """updatehandler.TempFileModelStore: bytes updates on disk (written chunk by chunk through
+    MemoryModelService.Upload), read back whole, deleted with os.remove (tempmodelstorage.py:27-76)."""
+    import os
+
+    from fedn_amd.updatehandler import MemoryModelService, TempFileModelStore, _NpzBytes, upload_requests
+    st = TempFileModelStore(str(tmp_path))
+    svc = MemoryModelService(st)
+    data = bytes(range(256)) * 9000
+    svc.Upload(upload_requests(data, "u1", chunk=4096), None)
+    assert os.path.getsize(st.path("u1")) == len(data)
+    assert st.get("u1").data == data
+    st.put("g", [1, 2])
+    assert st.get("g") == [1, 2]
+    st.put("u2", _NpzBytes(b"abc"))
+    assert st.delete("u1") and not os.path.exists(st.path("u1"))
+    assert st.delete("u2") and st.delete("g") and not st.delete("g")
+
+
+def test_delete_model_hands_own_copies_to_the_reaper():
+    """StagingUpdateHandler.delete_model: the wrapped handler's delete inline (the store's), this
+    handler's own copies of the update dropped on the reaper thread; both parts timed."""
+    import gc
+    import threading
+    import weakref
+
+    from fedn_amd.ingest import StagingUpdateHandler
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    uh = MemoryUpdateHandler()
+    st = StagingUpdateHandler(uh, helper=None, device="cpu", workers=1)
+
+    class Big:
+        nbytes = 1 << 20                 # AdoptedUploads accounts decoded uploads by size
+    obj = Big()
+    freed_on = []
+    weakref.finalize(obj, lambda: freed_on.append(threading.current_thread().name))
+    mu = uh.submit([np.zeros(4, np.float32)], 3)          # not via st: nothing staged
+    from concurrent.futures import Future
+    fut = Future()
+    fut.set_result(obj)
+    st._uploads.put(mu.model_update_id, fut)                  # as if decoded during its upload
+    del obj, fut
+    st.delete_model(mu)
+    st.close()                                               # waits for the reaper
+    gc.collect()
+    assert freed_on == ["fedn_amd_reaper"]
+    assert st.delete_times["count"] == 1 and st.delete_times["store_s"] >= 0 and st.delete_times["plugin_s"] >= 0
+    assert uh.store.get(mu.model_update_id) is None           # the store's delete ran inline

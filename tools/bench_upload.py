@@ -31,15 +31,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fedn_amd import _abi  # noqa: E402
 
 
-def run(mode, blob, ns, rate, workers):
+def run(mode, blob, ns, rate, workers, store="memory"):
     from fedn_amd.aggregators import get_aggregator
     from fedn_amd.helper import Helper
     from fedn_amd.ingest import StagingUpdateHandler
     from fedn_amd.updatehandler import MemoryModelService, MemoryUpdateHandler, upload_requests
     from fedn_amd.upload import StreamingUpload
 
+    from fedn_amd.updatehandler import MemoryModelStore, TempFileModelStore
     K = len(ns)
-    uh = MemoryUpdateHandler()
+    uh = MemoryUpdateHandler(TempFileModelStore() if store == "file" else MemoryModelStore())
     st = StagingUpdateHandler(uh, helper=Helper(), workers=workers)
     svc = MemoryModelService(uh.store)
     if mode.startswith("streaming"):
@@ -93,7 +94,9 @@ def run(mode, blob, ns, rate, workers):
     t_comb = t1 - t_agg
     return model, order, {"round_s": t1 - t0, "tail_s": t1 - last[0], "upload_s": last[0] - t0,
                           "decode_lag_s": (max(decoded_at) - last[0]) if decoded_at else None,
-                          "combine_s": t_comb, "aggregator_init_s": t_init, "delete_s": t_del[0], **{k: v for k, v in data.items() if isinstance(v, float)}}
+                          "combine_s": t_comb, "aggregator_init_s": t_init, "delete_s": t_del[0],
+                          "delete_plugin_s": st.delete_times["plugin_s"], "delete_store_s": st.delete_times["store_s"],
+                          "store": store, **{k: v for k, v in data.items() if isinstance(v, float)}}
 
 
 def main():
@@ -103,6 +106,8 @@ def main():
     ap.add_argument("--client-MBps", type=float, default=250.0)
     ap.add_argument("--workers", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--store", choices=("memory", "file"), default="memory",
+                    help="the update store: in-memory bytes, or files + os.remove as FEDn's TempModelStorage")
     a = ap.parse_args()
     _abi.load()
     torch.cuda.set_device(0)
@@ -118,7 +123,7 @@ def main():
     res = {}
     for rep in range(a.reps):                         # rep 0 warms pinned / device pools
         for mode in ("after-arrival", "streaming-host", "streaming"):
-            model, order, t = run(mode, blob, ns, a.client_MBps * 1e6, a.workers)
+            model, order, t = run(mode, blob, ns, a.client_MBps * 1e6, a.workers, a.store)
             uh = MemoryUpdateHandler()                # the same fold from host arrays
             for k in order:
                 uh.submit([w.copy() for w in tensors], ns[k])
@@ -127,7 +132,10 @@ def main():
             res[mode] = t
             print(json.dumps({"rep": rep, "mode": mode, **{k: (round(v, 4) if isinstance(v, float) else v)
                                                            for k, v in t.items()}}), flush=True)
-    print(json.dumps({"what": "upload", "clients": K, "params": P, "archive_MB": round(len(blob) / 1e6, 1),
+    print(json.dumps({"what": "upload", "store": a.store, "clients": K, "params": P,
+                      "archive_MB": round(len(blob) / 1e6, 1),
+                      "delete_plugin_s": round(res["streaming"]["delete_plugin_s"], 4),
+                      "delete_store_s": round(res["streaming"]["delete_store_s"], 4),
                       "client_MBps": a.client_MBps, "tail_after_arrival_s": round(res["after-arrival"]["tail_s"], 4),
                       "tail_streaming_host_s": round(res["streaming-host"]["tail_s"], 4),
                       "tail_streaming_s": round(res["streaming"]["tail_s"], 4),

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--params", type=int, default=2048 * 170898)      # ~350 M, whole 2048-element tiles
     ap.add_argument("--clients", type=int, default=32)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--burst", default="1,2,4", help="burst-store probe G values (tiles per wave), '' = none")
     a = ap.parse_args()
     _abi.use_probe()
     dev = torch.device("cuda", 0)
@@ -59,12 +60,21 @@ def main():
     src = torch.empty(1 << 30, dtype=torch.float32, device=dev).fill_(1.0)
     dst = torch.empty_like(src)
     res = {}
+    bursts = [int(x) for x in a.burst.split(",") if x]
     for _ in range(a.reps):
         for name, (fn, _) in phases.items():
             for mix in (0, 1):
                 ops.tune(opt_mix=mix)
                 fn()
                 res.setdefault((name, mix), []).append(median_ms(fn))
+            ops.tune(opt_mix=0)
+            for g in bursts:                      # the burst-store probe: G tiles per wave, stores after
+                if name != "steady":
+                    continue
+                ops.tune(opt_burst=g)
+                fn()
+                res.setdefault((name, f"burst{g}"), []).append(median_ms(fn))
+            ops.tune(opt_burst=0)
         ops.tune(opt_mix=0)
         ops.stream_copy(dst, src)
         res.setdefault(("copy", 0), []).append(median_ms(lambda: ops.stream_copy(dst, src)))
@@ -78,7 +88,11 @@ def main():
                           "product_over_pattern": round(mix / prod, 4),
                           "product_frac_of_copy": round(b / prod / 1e6 / copy_gbs, 4),
                           "reps_product": [round(x, 4) for x in res[(name, 0)]],
-                          "reps_pattern": [round(x, 4) for x in res[(name, 1)]]}), flush=True)
+                          "reps_pattern": [round(x, 4) for x in res[(name, 1)]],
+                          **{f"burst{g}_ms": round(float(np.median(res[(name, f'burst{g}')])), 4)
+                             for g in bursts if (name, f"burst{g}") in res},
+                          **{f"burst{g}_frac_of_peak": round(b / float(np.median(res[(name, f'burst{g}')])) / 1e6 / PEAK, 4)
+                             for g in bursts if (name, f"burst{g}") in res}}), flush=True)
     print(json.dumps({"copy_GBps": round(copy_gbs, 1), "reps_ms": [round(x, 4) for x in res[("copy", 0)]]}))
 
 

@@ -104,6 +104,18 @@ for s in $STEPS; do
     upload)
       timeout -k 10 600 python tools/bench_upload.py > "$OUT/upload.log" 2>&1; rc=$?
       echo "upload rc=$rc"; grep -v amdgpu.ids "$OUT/upload.log" | tail -5; [ $rc -eq 0 ] || exit $rc ;;
+    upload100mfile)
+      # the same with FEDn's file store stand-in (TempModelStorage: chunks to a file, delete = os.remove),
+      # 300 and 400 MB/s per client; the delete breakdown (plug-in copies vs the store) is in the lines
+      for r in 300 400; do
+        timeout -k 10 600 python tools/bench_upload.py --params 100000000 --clients 8 --client-MBps $r --store file \
+          >> "$OUT/upload100m_file.log" 2>&1; rc=$?
+        [ $rc -eq 0 ] || { echo "upload100mfile rc=$rc"; exit $rc; }
+      done
+      echo "upload100mfile rc=0"; grep '"what"' "$OUT/upload100m_file.log" | cut -c1-600 ;;
+    mixprobe)
+      timeout -k 10 600 python tools/fedopt_mix_probe.py > "$OUT/mixprobe.log" 2>&1; rc=$?
+      echo "mixprobe rc=$rc"; cut -c1-700 "$OUT/mixprobe.log" | tail -4; [ $rc -eq 0 ] || exit $rc ;;
     upload100m)
       timeout -k 10 600 python tools/bench_upload.py --params 100000000 --clients 8 --client-MBps 400 > "$OUT/upload100m.log" 2>&1; rc=$?
       echo "upload100m rc=$rc"; grep -v amdgpu.ids "$OUT/upload100m.log" | tail -5; [ $rc -eq 0 ] || exit $rc ;;
