@@ -116,16 +116,28 @@ struct Parser {
     const uint8_t* S;
     int64_t L;
     int64_t base = 0;   // a position p is stored as p - base + 1; 0 is NIL (and stream position 0)
-    std::vector<uint32_t> head, prev;
+    // zlib's prev[] ring with each position's first 4 bytes beside its link: a chain step reads one
+    // 8-byte slot, and most candidates (hash collisions, 3-byte matches) are rejected without
+    // touching the stream — the candidates visited and counted are zlib's, only cheaper to reject
+    struct Slot {
+        uint32_t prev, key;
+    };
+    std::vector<uint32_t> head;
+    std::vector<Slot> ring;
     int64_t t = 0, mstart = 0;
     int avail = 0, mlen = kMinMatch - 1;
 
-    Parser(const uint8_t* s, int64_t l) : S(s), L(l), head(kHSize, 0), prev(kWSize, 0) {}
+    Parser(const uint8_t* s, int64_t l) : S(s), L(l), head(kHSize, 0), ring(kWSize, Slot{0, 0}) {}
     inline uint32_t enc(int64_t p) const { return p == 0 ? 0u : (uint32_t)(p - base + 1); }
     inline int64_t dec(uint32_t e) const { return (int64_t)e - 1 + base; }
+    static inline uint32_t load32(const uint8_t* p) {
+        uint32_t v;
+        std::memcpy(&v, p, 4);
+        return v;
+    }
     inline uint32_t insert(int64_t p) {
         const uint32_t h = hash3(S + p), hh = head[h];
-        prev[p & kWMask] = hh;
+        ring[p & kWMask] = Slot{hh, load32(S + p)};
         head[h] = enc(p);
         return hh;
     }
@@ -137,7 +149,7 @@ struct Parser {
             e = p < nb ? 0u : (uint32_t)(p - nb + 1);
         };
         for (auto& e : head) fix(e);
-        for (auto& e : prev) fix(e);
+        for (auto& e : ring) fix(e.prev);
         base = nb;
     }
     void start(int64_t b) {
@@ -158,21 +170,29 @@ struct Parser {
         const uint8_t* scan = S + t;
         int best = prev_len;
         uint8_t e1 = scan[best - 1], e0 = scan[best];
+        const uint32_t skey = load32(scan);
+        // a candidate beats best only if its first min(best + 1, 4) bytes equal scan's (bytes 0..2
+        // agree for every same-hash candidate whose bytes 0..1 do, as zlib's check relies on)
+        uint32_t kmask = best >= 3 ? 0xFFFFFFFFu : 0x00FFFFFFu;
         const int64_t limit = t - kMaxDist;
         int64_t cp = dec(cur);
         for (;;) {
-            const uint8_t* m = S + cp;
-            if (m[best] == e0 && m[best - 1] == e1 && m[0] == scan[0] && m[1] == scan[1]) {
-                const int len = kMinMatch + common255(scan + 3, m + 3);
-                if (len > best) {
-                    mstart = cp;
-                    best = len;
-                    if (len >= kNice) break;
-                    e1 = scan[best - 1];
-                    e0 = scan[best];
+            const Slot sl = ring[cp & kWMask];
+            if (((sl.key ^ skey) & kmask) == 0) {
+                const uint8_t* m = S + cp;
+                if (best < 4 || (m[best] == e0 && m[best - 1] == e1)) {
+                    const int len = kMinMatch + common255(scan + 3, m + 3);
+                    if (len > best) {
+                        mstart = cp;
+                        best = len;
+                        if (len >= kNice) break;
+                        e1 = scan[best - 1];
+                        e0 = scan[best];
+                        kmask = 0xFFFFFFFFu;
+                    }
                 }
             }
-            const uint32_t nx = prev[cp & kWMask];
+            const uint32_t nx = sl.prev;
             if (!nx) break;
             cp = dec(nx);
             if (cp <= limit || --chain == 0) break;
