@@ -1138,6 +1138,171 @@ __device__ __forceinline__ void fedopt_c_body(const OptBuffers& b, const OptScal
     }
 }
 
+#ifdef FEDAGG_PROBES
+// burst-store probe of the product step (FA_TUNE_OPT_G = G): k_fedopt_c's FINAL phase
+// with every wave taking G consecutive 512-element tiles and storing the new v / out / m of all G
+// after the last tile's reads (k_fedopt_mixg measured the access pattern alone). The arithmetic is
+// opt_apply's, duplicated here (opt_compute_p) so that the product kernels' code stays as measured.
+template <class PG, int E>
+__device__ __forceinline__ void opt_compute_p(const OptBuffers& b, const OptScalars& s, const typename PG::V (&pg)[E],
+                                              const typename PG::V (&ov)[E], const double (&mi)[E], double (&v)[E],
+                                              double (&m)[E], double (&o)[E]) {
+    using V = typename PG::V;
+    constexpr bool PG32 = std::is_same<PG, CF32>::value;
+    // ---- m (fedopt.py:173-176 and the two twins)
+    constexpr bool PG64 = std::is_same<PG, CF64>::value;
+    if (b.m_in_f64 < 0) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) m[e] = mul_pg<PG>((double)pg[e], s.c1, s.c1f, s.c1h);
+    } else {
+        // m*beta1 in m's dtype, pg*(1-beta1) in pg's dtype, their sum in the promoted dtype
+        // (f16 < f32 < f64); each operand is exact in its dtype, so the float sum rounds once
+        if (b.m_in_f64 == 1) {                     // f64 m: an f64 sum
+#pragma unroll
+            for (int e = 0; e < E; ++e) m[e] = mi[e] * s.b1 + mul_pg<PG>((double)pg[e], s.c1, s.c1f, s.c1h);
+        } else if (b.m_in_f64 == 0) {              // f32 m (mi is an exact f32)
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float a = (float)mi[e] * s.b1f;
+                const double pm = mul_pg<PG>((double)pg[e], s.c1, s.c1f, s.c1h);
+                if constexpr (PG64) m[e] = (double)a + pm;          // f32 + f64
+                else m[e] = (double)(a + (float)pm);                // f32 + f32 (or f16) in f32
+            }
+        } else {                                   // f16 m (a float16 session's first rounds)
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float a = CF16::rh((float)mi[e] * s.b1h);
+                const double pm = mul_pg<PG>((double)pg[e], s.c1, s.c1f, s.c1h);
+                if constexpr (PG64) m[e] = (double)a + pm;
+                else if constexpr (PG32) m[e] = (double)(a + (float)pm);
+                else m[e] = (double)CF16::rh(a + (float)pm);
+            }
+        }
+    }
+    // ---- v (fedopt.py:178-179 / 214-217 / 251-252)
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const V pv = pg[e];
+        const double p = (double)pg_sq<PG>(pv);   // power(pg, 2) in the pg dtype
+        if (s.opt == FA_ADAM) {
+            v[e] = v[e] * s.b2 + mul_pg<PG>(p, s.c2, s.c2f, s.c2h);
+        } else if (s.opt == FA_YOGI) {
+            const double sg = np_sign(v[e] - p);
+            v[e] = v[e] + (sg * p) * s.nc2;
+        } else {
+            v[e] = v[e] + p;
+        }
+        const double sv = __builtin_sqrt(v[e]) + s.tau;
+        const double t = m[e] / sv;
+        o[e] = (double)ov[e] + t * s.lr;
+    }
+}
+
+template <typename Y, typename OLD, class PG, bool FIRST, bool NT, int G>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_cg(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
+    using V = typename PG::V;
+    constexpr int NH = 4, H = 2, E = H * NH, U = kUnroll / 2;
+    constexpr int64_t T = 128 * NH;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if ((wave + 1) * G * T > P) {                 // a partial group: the product kernel's per-tile path
+        for (int g = 0; g < G; ++g) {
+            const int64_t base = (wave * G + g) * T;
+            if (base >= P) break;
+            if (base + T <= P) fedopt_strip_split<Y, OLD, PG, FIRST, true, NT, 1, NH, U>(b, s, tab, K, base + 2 * lane);
+            else
+                for (int j = 0; j < NH / 2; ++j) {
+                    const int64_t i0 = base + j * 256 + 4 * lane;
+                    if (i0 < P) fedopt_strip<Y, OLD, PG, 4, FIRST, true, NT, false, 1>(b, s, tab, K, P, i0);
+                }
+        }
+        return;
+    }
+    double mo[G][E], vo[G][E], oo[G][E];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int64_t i0 = (wave * G + g) * T + 2 * lane;
+        auto half = [](auto& a, int h) -> auto& {
+            using TT = std::remove_reference_t<decltype(a[0])>;
+            return *reinterpret_cast<TT(*)[H]>(&a[h * H]);
+        };
+        auto at = [i0](int h) { return i0 + (int64_t)h * 128; };
+        OLD old[E];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) strip_load<OLD, H, false>(static_cast<const OLD*>(b.old) + at(h), half(old, h));
+        V ov[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) ov[e] = widen<OLD, V>(old[e]);
+        V pg[E];
+        int k = 0;
+        if constexpr (FIRST) {
+            Y y[E];
+            const Y* yp = static_cast<const Y*>(tab.ptr[0]);
+#pragma unroll
+            for (int h = 0; h < NH; ++h) strip_load<Y, H, NT>(yp + at(h), half(y, h));
+#pragma unroll
+            for (int e = 0; e < E; ++e) pg[e] = pg_sub<PG>(widen<Y, V>(y[e]), ov[e]);
+            k = 1;
+        } else {
+            using TT = typename PG::T;
+            TT t[E];
+#pragma unroll
+            for (int h = 0; h < NH; ++h) strip_load<TT, H, false>(static_cast<const TT*>(b.pg) + at(h), half(t, h));
+#pragma unroll
+            for (int e = 0; e < E; ++e) pg[e] = widen<TT, V>(t[e]);
+        }
+        for (; k + U <= K; k += U) {
+            Y y[U][E];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const Y* yp = static_cast<const Y*>(tab.ptr[k + u]);
+#pragma unroll
+                for (int h = 0; h < NH; ++h) strip_load<Y, H, NT>(yp + at(h), half(y[u], h));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                V d[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) d[e] = pg_sub<PG>(widen<Y, V>(y[u][e]), ov[e]);
+                fold_strip<PG, E>(pg, d, tab.n[k + u], tab.N[k + u], tab.r[k + u]);
+            }
+        }
+        for (; k < K; ++k) {
+            const Y* yp = static_cast<const Y*>(tab.ptr[k]);
+            Y y[E];
+#pragma unroll
+            for (int h = 0; h < NH; ++h) strip_load<Y, H, NT>(yp + at(h), half(y, h));
+            V d[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) d[e] = pg_sub<PG>(widen<Y, V>(y[e]), ov[e]);
+            fold_strip<PG, E>(pg, d, tab.n[k], tab.N[k], tab.r[k]);
+        }
+        double mi[E];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) opt_load_state<H>(b, s, at(h), H, half(mi, h), half(vo[g], h));
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+            opt_compute_p<PG, H>(b, s, half(pg, h), half(ov, h), half(mi, h), half(vo[g], h), half(mo[g], h), half(oo[g], h));
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int64_t i0 = (wave * G + g) * T + 2 * lane;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            const int64_t o = i0 + (int64_t)h * 128;
+            double* vp = &vo[g][h * H];
+            double* op = &oo[g][h * H];
+            double* mp = &mo[g][h * H];
+            // fp64 state and model (the steady state of configs[3]; other dtypes refused at launch)
+            strip_store<double, H, 1>(static_cast<double*>(b.v_out) + o, *reinterpret_cast<double(*)[H]>(vp));
+            strip_store<double, H, 1>(static_cast<double*>(b.out) + o, *reinterpret_cast<double(*)[H]>(op));
+            strip_store<double, H, 1>(static_cast<double*>(b.m_out) + o, *reinterpret_cast<double(*)[H]>(mp));
+        }
+    }
+}
+#endif
+
 template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM = 0, int NH = 2,
           int U = kUnroll / 2>
 __global__ void __launch_bounds__(kBlock)
@@ -1589,7 +1754,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0}, opt_burst{0};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0}, opt_burst{0}, opt_g{0};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -1834,6 +1999,21 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
     constexpr bool probe_combo = E == 4 && std::is_same<Y, float>::value &&
                                  (std::is_same<OLD, float>::value || std::is_same<OLD, double>::value);
     if constexpr (probe_combo) {
+        if (final_ && g_cfg.opt_g && std::is_same<OLD, double>::value) {
+            if (b.m_out_f64 != 1 || b.v_out_f32 || b.out_f32 || !b.v_in || b.v_in_f32)
+                return fail(FA_EINVAL, "fa_tune OPT_G probe: fp64 m / v / model out, fp64 v in");
+            const int G = g_cfg.opt_g;
+            const dim3 gg((unsigned)((P + 4 * 512 * G - 1) / (4 * 512 * G)));
+            switch (G) {
+#define FA_OPTG(G_) \
+    case G_: if (first) hipLaunchKernelGGL((k_fedopt_cg<Y, OLD, PG, true, NT, G_>), gg, dim3(kBlock), 0, st, b, s, tab, cnt, P); \
+             else hipLaunchKernelGGL((k_fedopt_cg<Y, OLD, PG, false, NT, G_>), gg, dim3(kBlock), 0, st, b, s, tab, cnt, P); break;
+                FA_OPTG(1) FA_OPTG(2) FA_OPTG(4)
+#undef FA_OPTG
+                default: return fail(FA_EINVAL, "fa_tune OPT_G: 1, 2 or 4 tiles per wave");
+            }
+            return check_launch("fa_fedopt_step: kernel launch");
+        }
         if (first && final_ && g_cfg.opt_burst) {
             if (b.m_out_f64 != 1) return fail(FA_EINVAL, "fa_tune OPT_BURST probe: fp64 m out");
             const int G = g_cfg.opt_burst;
@@ -2618,6 +2798,11 @@ int fa_tune(int knob, int value) {
             return FA_OK;
         case FA_TUNE_OPT_MIX:
             g_cfg.opt_mix = value ? 1 : 0;
+            return FA_OK;
+        case FA_TUNE_OPT_G:
+            if (value != 0 && value != 1 && value != 2 && value != 4)
+                return fail(FA_EINVAL, "fa_tune: burst-store product probe 0 (off), 1, 2 or 4 tiles per wave");
+            g_cfg.opt_g = value;
             return FA_OK;
         case FA_TUNE_OPT_BURST:
             if (value != 0 && value != 1 && value != 2 && value != 4)

@@ -192,14 +192,24 @@ class _ShardedStaging:
             st.synchronize()
 
     def _copy_aside(self, per_dev):
-        """Device copies of ``per_dev`` ([{group: tensor}] per device) on each compute stream."""
+        """Device copies of ``per_dev`` ([{group: tensor}] per device) on each compute stream
+        (staging.NO_SNAPSHOT when HBM cannot hold them: see staging._Pipeline._snapshot)."""
+        from .staging import NO_SNAPSHOT
         out = []
-        for d, dv in enumerate(self.devices):
-            with torch.cuda.device(dv), torch.cuda.stream(self.compute[d]):
-                out.append({dt: t.clone() for dt, t in per_dev[d].items()})
+        try:
+            for d, dv in enumerate(self.devices):
+                with torch.cuda.device(dv), torch.cuda.stream(self.compute[d]):
+                    out.append({dt: t.clone() for dt, t in per_dev[d].items()})
+        except torch.cuda.OutOfMemoryError:
+            return NO_SNAPSHOT
         return out
 
     def _copy_back(self, per_dev, snap):
+        from .staging import NO_SNAPSHOT
+        if snap is NO_SNAPSHOT:
+            self.broken = RuntimeError("a multi-launch fold failed part-way and the aggregate could not be "
+                                       "copied aside beforehand (HBM full): the round is lost")
+            raise self.broken
         if snap is None:
             return
         for d, dv in enumerate(self.devices):
@@ -541,8 +551,9 @@ class ShardedFedAvgPipeline(_ShardedStaging):
         """One fold of ``entries`` on every device and group, all-or-nothing: on a failed launch the
         aggregate is put back (or stays unstarted) and the FedAggError propagates."""
         init = not self.agg_started
-        snap = self._snapshot()
+        snap = None
         try:
+            snap = self._snapshot()
             for d in range(len(self.devices)):
                 for dt in self.layout.groups:
                     lo, hi = self.bounds[dt][d]

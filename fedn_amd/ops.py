@@ -406,7 +406,8 @@ _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _a
           "opt_store": _abi.FA_TUNE_OPT_STORE, "opt_coal": _abi.FA_TUNE_OPT_COAL, "narrow": _abi.FA_TUNE_NARROW,
           "lds": _abi.FA_TUNE_LDS, "wpe": _abi.FA_TUNE_WPE,
           "opt_mv": _abi.FA_TUNE_OPT_MV, "auto_geom": _abi.FA_TUNE_AUTO_GEOM,
-          "opt_mix": _abi.FA_TUNE_OPT_MIX, "opt_burst": _abi.FA_TUNE_OPT_BURST}
+          "opt_mix": _abi.FA_TUNE_OPT_MIX, "opt_burst": _abi.FA_TUNE_OPT_BURST,
+          "opt_g": _abi.FA_TUNE_OPT_G}
 
 
 def tune(**knobs):

@@ -500,7 +500,11 @@ class P2PAllGather:
         destinations)."""
         return [maps[self.cur][1] + at * self.esize for maps in self.peers.values()]
 
-    def fence(self):
+    def fence(self, check=None):
+        """Order the ranks (see the class doc); ``check`` (default: ``verify == "round"``) then reads
+        the release records and raises on a missed XCD or a release grid that did not run."""
+        if check is None:
+            check = self.verify == "round"
         cur = torch.cuda.current_stream(self.device)
         for st in self.streams.values():
             cur.wait_stream(st)
@@ -511,7 +515,7 @@ class P2PAllGather:
             else:
                 torch.cuda.synchronize(self.device)
                 dist.barrier(group=self.group)
-        if self.verify == "round" and self._release:
+        if check and self._release:
             # this round's release records, read after the fence (check_release's D2H is ordered after
             # it on the current stream): a miss fails the round's exchange here, not at close()
             self.check_release()
@@ -522,8 +526,8 @@ class P2PAllGather:
         caller that already read them (bench.py reports them in its line) passes False."""
         from . import ops
         err = None
-        if fence and self.peers:
-            self.fence()
+        if fence and (self.peers or self._release):
+            self.fence(check=False)             # checked below, raised once the peers are unmapped
             torch.cuda.synchronize(self.device)
             if check:
                 try:

@@ -185,6 +185,9 @@ def _addr(src):
     return src.ptr if type(src) is _ArenaRef else src.dev.data_ptr()
 
 
+NO_SNAPSHOT = object()   # _snapshot could not copy the aggregate aside (HBM full)
+
+
 class _Pipeline:
     def __init__(self, device, layout, nslots, slots=None, streams=None, cache=None, batch=True):
         self.device = torch.device(device)
@@ -675,10 +678,23 @@ class FedAvgPipeline(_Pipeline):
         not needed: not started (an init fold rewrites it) or one launch (a failed launch ran nothing)."""
         if not self.agg_started or launches <= 1:
             return None
-        with torch.cuda.device(self.device), torch.cuda.stream(self.compute):
-            return {dt: self._agg(dt).clone() for dt in self.layout.groups}
+        try:                                    # a model-sized clone for the fold's duration (the HBM
+            with torch.cuda.device(self.device), torch.cuda.stream(self.compute):   # budget's headroom)
+                return {dt: self._agg(dt).clone() for dt in self.layout.groups}
+        except torch.cuda.OutOfMemoryError:
+            return NO_SNAPSHOT                  # the fold goes ahead; only a failure part-way is fatal
 
-    def _restore(self, snap):
+    def _restore(self, snap, ran=1):
+        """Put the aggregate back after a failed multi-launch fold of which ``ran`` launches had been
+        enqueued (0: the aggregate is untouched, nothing to put back)."""
+        if ran == 0:
+            return
+        if snap is NO_SNAPSHOT:
+            # a launch failed after earlier ones advanced the aggregate, and HBM held no copy of it:
+            # the round cannot go on with this update skipped (ADVICE r4) — result() raises
+            self.broken = RuntimeError("a multi-launch fold failed part-way and the aggregate could not be "
+                                       "copied aside beforehand (HBM full): the round is lost")
+            raise self.broken
         if snap is not None:
             with torch.cuda.device(self.device), torch.cuda.stream(self.compute):
                 for dt, t in snap.items():
@@ -690,12 +706,14 @@ class FedAvgPipeline(_Pipeline):
         tag; its examples stay counted (its N is already in every later entry's running total), and
         the aggregate is as the previous update left it (each update's launches are all-or-nothing)."""
         for e in entries:
-            snap = self._snapshot(len(self.layout.groups))
+            snap, ran = None, 0
             try:
+                snap = self._snapshot(len(self.layout.groups))
                 for dt in self.layout.groups:
                     self._fold_group(dt, [e], not self.agg_started, 0, self.layout.group_elems[dt])
+                    ran += 1
             except ops.FedAggError as ex:
-                self._restore(snap)
+                self._restore(snap, ran)
                 self.skipped.append((e[3] if len(e) > 3 else None, ex))
                 continue
             self._folded()
@@ -718,9 +736,10 @@ class FedAvgPipeline(_Pipeline):
                 if bounds:
                     bounds[-1] = (bounds[-1][0], P)
             plan += [(dt, off, isz, lo, hi) for lo, hi in bounds]
-        snap = self._snapshot(len(plan))        # this update's launches are all-or-nothing
         done = []
+        snap = None
         try:
+            snap = self._snapshot(len(plan))    # this update's launches are all-or-nothing
             for dt, off, isz, lo, hi in plan:
                 self.wait_bytes(slot, off + lo * isz, off + hi * isz)
                 self._fold_group(dt, [(slot, n, N)], init, lo, hi)
@@ -729,7 +748,7 @@ class FedAvgPipeline(_Pipeline):
                 done.append((dt, lo, hi, ev))
         except ops.FedAggError:
             self._last_fold = None
-            self._restore(snap)                 # the update is skipped by the caller (fedavg.py:75-78)
+            self._restore(snap, len(done))      # the update is skipped by the caller (fedavg.py:75-78)
             raise
         self._end_span(span)
         self._folded()
@@ -770,12 +789,14 @@ class FedAvgPipeline(_Pipeline):
         self._last_fold = None
         span = self._kernel_span()
         init = not self.agg_started
-        snap = self._snapshot(len(self.layout.groups))
+        snap, ran = None, 0
         try:
+            snap = self._snapshot(len(self.layout.groups))
             for dt in self.layout.groups:
                 self._fold_group(dt, entries, init, 0, self.layout.group_elems[dt])
+                ran += 1
         except ops.FedAggError:
-            self._restore(snap)
+            self._restore(snap, ran)
             self._refold_singly(entries)
             self._end_span(span)
             return
@@ -814,13 +835,18 @@ class FedAvgPipeline(_Pipeline):
         span = self._kernel_span()
         hosts = {}
         # the last batch runs chunk by chunk (or per group): a failed chunk needs the aggregate back
-        snap = self._snapshot(2 if (len(self.layout.groups) > 1 or self.layout.nbytes > SMALL_UPDATE_BYTES) else 1) \
-            if entries else None
+        snap, ran = None, [0]
         try:
+            snap = self._snapshot(2 if (len(self.layout.groups) > 1 or self.layout.nbytes > SMALL_UPDATE_BYTES) else 1) \
+                if entries else None
+
+            def fold_counted(dt, lo, hi):
+                self._fold_group(dt, entries, init, lo, hi)
+                ran[0] += 1
             for dt in self.layout.groups:
                 ready = None
                 if entries:
-                    fold = lambda lo, hi, dt=dt: self._fold_group(dt, entries, init, lo, hi)  # noqa: E731
+                    fold = lambda lo, hi, dt=dt: fold_counted(dt, lo, hi)  # noqa: E731
                 else:
                     fold = lambda lo, hi: None  # noqa: E731
                     if last is not None:            # each D2H chunk waits only for the folds it reads
@@ -832,7 +858,7 @@ class FedAvgPipeline(_Pipeline):
                 raise
             self.compute.synchronize()          # what the failed attempt enqueued has run
             self.d2h.synchronize()
-            self._restore(snap)
+            self._restore(snap, ran[0])
             self._refold_singly(entries)
             entries = []
             if not self.agg_started:

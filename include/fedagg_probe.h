@@ -78,7 +78,10 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                     FA_TUNE_OPT_BURST = 22 /* FedOpt FIRST|FINAL, burst-store probe (fp64 m out): G = 1, 2 or 4
                                               wave tiles per wave with k_fedopt_mix's loads, the new v / out / m
                                               of all G held in registers and stored together after the last
-                                              tile's reads (0 = off; a ragged last group is skipped) */ };
+                                              tile's reads (0 = off; a ragged last group is skipped) */,
+                    FA_TUNE_OPT_G = 23 /* FedOpt FINAL launches over an fp64 model with fp64 state out: the
+                                          product arithmetic with G = 1, 2 or 4 wave tiles per wave and their
+                                          v / out / m stored after the last tile's reads (0 = off) */ };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);

@@ -214,3 +214,69 @@ def test_fedopt_server_step_failure_after_batch_refold_returns_none(monkeypatch)
     assert model is None and data["nr_aggregated_models"] == 4
     assert_lists_identical(agg.m, state.m, "m kept")
     assert_lists_identical(agg.v, state.v, "v kept")
+
+
+MIXED = [(300, 7), (5,)]                      # + an int64 counter per update: two dtype groups
+
+
+def _mixed_updates(rng, K):
+    base = [rng.standard_normal(s).astype(np.float32) for s in MIXED]
+    ups = [[(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base] +
+           [np.array([int(rng.integers(0, 1000))], dtype=np.int64)] for _ in range(K)]
+    ns = [int(v) for v in rng.choice(np.arange(1, 5001), K, replace=False)]
+    return ups, ns
+
+
+@pytest.mark.parametrize("route", ["host_flush", "staged"])
+def test_snapshot_that_cannot_be_taken_only_matters_on_failure(route, monkeypatch):
+    """the all-or-nothing snapshot of a multi-launch fold is taken inside the fold's try,
+    and an HBM-full clone (simulated: every snapshot reports staging.NO_SNAPSHOT) does not skip a
+    valid update — the folds go ahead and the round is bit-exact; a launch that then fails part-way
+    cannot be undone, so the round is lost loudly (combine_models raises) instead of returning a
+    model with a half-applied update."""
+    from fedn_amd import staging
+    from fedn_amd.aggregators.fedavg import Aggregator
+    _setup(route, monkeypatch)
+    monkeypatch.setattr(staging, "BATCH", 3)   # u1-u3 fold as the init batch, u4-u5 continue it
+    real = staging._Pipeline._snapshot
+    taken = []
+
+    def no_room(self, launches):
+        snap = real(self, launches)
+        if snap is None:
+            return None
+        taken.append(launches)
+        return staging.NO_SNAPSHOT
+    monkeypatch.setattr(staging._Pipeline, "_snapshot", no_room)
+    for poisoned in (False, True):
+        rng = np.random.default_rng(77)
+        ups, ns = _mixed_updates(rng, 6)
+        uh, st = _handlers(route)
+        try:
+            agg = Aggregator(st or uh, device=DEV)
+            for u, n in zip(ups, ns):
+                uh.submit(u, n, via=st)
+            if not poisoned:
+                model, data = agg.combine_models(helper=None)
+                want, nr = ref.fedavg_combine(list(zip(ups, ns)))
+                assert data["nr_aggregated_models"] == nr == 6
+                assert_lists_identical(model, want, f"{route} without a snapshot")
+                assert taken, "no multi-launch fold ran: the case does not exercise the snapshot"
+            else:
+                # the update's int64-group launch fails AFTER its float32-group launch ran: that
+                # half-applied fold could only be undone from the snapshot it could not take
+                from fedn_amd import _abi, ops
+                Ns = np.cumsum(ns)
+                bad = (float(ns[4]), float(Ns[4]))
+                real_fold = ops.fedavg_fold_ptrs
+
+                def fold(acc, ptrs, upd_dt, n, N, *a, **kw):
+                    if upd_dt == torch.int64 and any((float(x), float(y)) == bad for x, y in zip(n, N)):
+                        raise _abi.FedAggError(_abi.FA_EHIP, "injected failure of the second launch")
+                    return real_fold(acc, ptrs, upd_dt, n, N, *a, **kw)
+                monkeypatch.setattr(ops, "fedavg_fold_ptrs", fold)
+                with pytest.raises(RuntimeError, match="could not be copied aside"):
+                    agg.combine_models(helper=None)
+        finally:
+            if st is not None:
+                st.close()

@@ -62,8 +62,15 @@ def main():
         # the other direction: the combiner's model serialisation (helper.save)
         t_np = best(lambda: np.savez_compressed(io.BytesIO(), **{"0": x}), 1)
         out["encode"] = {"numpy_s": t_np, "numpy_MB": len(raw) / 1e6}
+        # helper.save's default: numpy's exact bytes (fnpz_savez; one big member -> pdeflate.h)
+        exact = codec.save_npz([x], threads=a.threads)
+        out["encode"]["exact_identical_to_numpy"] = exact == raw
+        out["encode"]["exact_s"] = best(lambda: codec.save_npz([x], threads=a.threads), a.reps)
+        out["encode"]["exact_speedup"] = t_np / out["encode"]["exact_s"]
+        # a helper-written archive is numpy's: the decoder's single-stream split applies to it
+        out["native_load_helper_written_s"] = best(lambda: codec.load_npz(exact), a.reps)
         for strat in ("default", "auto"):
-            enc = codec.save_npz_blocks([x], threads=a.threads, strategy=strat)
+            enc = codec.save_npz_blocks([x], threads=a.threads, strategy=strat)   # FEDN_AMD_NPZ_WRITER=blocks
             got = np.load(io.BytesIO(enc))["0"]
             assert np.array_equal(got.view(np.uint32), x.view(np.uint32))
             out["encode"][f"native_{strat}_s"] = best(lambda: codec.save_npz_blocks([x], threads=a.threads, strategy=strat), a.reps)

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--clients", type=int, default=32)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--burst", default="1,2,4", help="burst-store probe G values (tiles per wave), '' = none")
+    ap.add_argument("--opt-g", default="1,2,4", help="product step with G tiles per wave (fa_tune OPT_G), '' = none")
     a = ap.parse_args()
     _abi.use_probe()
     dev = torch.device("cuda", 0)
@@ -61,13 +62,36 @@ def main():
     dst = torch.empty_like(src)
     res = {}
     bursts = [int(x) for x in a.burst.split(",") if x]
+    gs = [int(x) for x in a.opt_g.split(",") if x]
+    # the product arithmetic with G tiles per wave (fa_tune OPT_G): bit-identical to k_fedopt_c?
+    exact = {}
+    if gs:
+        fn = phases["steady"][0]
+        ops.tune(opt_g=0)
+        fn()
+        torch.cuda.synchronize()
+        ref_out = (o2.clone(), m_o.clone(), v_o.clone())
+        for g in gs:
+            ops.tune(opt_g=g)
+            o2.zero_(); m_o.zero_(); v_o.zero_()
+            fn()
+            torch.cuda.synchronize()
+            exact[g] = all(torch.equal(x.view(torch.int64), y.view(torch.int64)) for x, y in zip((o2, m_o, v_o), ref_out))
+        ops.tune(opt_g=0)
     for _ in range(a.reps):
-        for name, (fn, _) in phases.items():
+        for name, (fn, _b) in phases.items():
             for mix in (0, 1):
                 ops.tune(opt_mix=mix)
                 fn()
                 res.setdefault((name, mix), []).append(median_ms(fn))
             ops.tune(opt_mix=0)
+            for g in gs:                          # the product step with G tiles per wave
+                if name != "steady":
+                    continue
+                ops.tune(opt_g=g)
+                fn()
+                res.setdefault((name, f"g{g}"), []).append(median_ms(fn))
+            ops.tune(opt_g=0)
             for g in bursts:                      # the burst-store probe: G tiles per wave, stores after
                 if name != "steady":
                     continue
@@ -92,7 +116,12 @@ def main():
                           **{f"burst{g}_ms": round(float(np.median(res[(name, f'burst{g}')])), 4)
                              for g in bursts if (name, f"burst{g}") in res},
                           **{f"burst{g}_frac_of_peak": round(b / float(np.median(res[(name, f'burst{g}')])) / 1e6 / PEAK, 4)
-                             for g in bursts if (name, f"burst{g}") in res}}), flush=True)
+                             for g in bursts if (name, f"burst{g}") in res},
+                          **{f"g{g}_ms": round(float(np.median(res[(name, f'g{g}')])), 4)
+                             for g in gs if (name, f"g{g}") in res},
+                          **{f"g{g}_reps": [round(x, 4) for x in res[(name, f'g{g}')]]
+                             for g in gs if (name, f"g{g}") in res},
+                          **({f"g{g}_bit_exact": exact[g] for g in gs} if name == "steady" else {})}), flush=True)
     print(json.dumps({"copy_GBps": round(copy_gbs, 1), "reps_ms": [round(x, 4) for x in res[("copy", 0)]]}))
 
 
