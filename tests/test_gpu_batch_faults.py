@@ -238,7 +238,7 @@ def test_snapshot_that_cannot_be_taken_only_matters_on_failure(route, monkeypatc
     from fedn_amd.aggregators.fedavg import Aggregator
     _setup(route, monkeypatch)
     monkeypatch.setattr(staging, "BATCH", 3)   # u1-u3 fold as the init batch, u4-u5 continue it
-    real = staging._Pipeline._snapshot
+    real = staging.FedAvgPipeline._snapshot
     taken = []
 
     def no_room(self, launches):
@@ -247,7 +247,7 @@ def test_snapshot_that_cannot_be_taken_only_matters_on_failure(route, monkeypatc
             return None
         taken.append(launches)
         return staging.NO_SNAPSHOT
-    monkeypatch.setattr(staging._Pipeline, "_snapshot", no_room)
+    monkeypatch.setattr(staging.FedAvgPipeline, "_snapshot", no_room)
     for poisoned in (False, True):
         rng = np.random.default_rng(77)
         ups, ns = _mixed_updates(rng, 6)
