@@ -64,6 +64,10 @@ for s in $STEPS; do
       grep -v amdgpu.ids "$OUT/small_breakdown.log"
       timeout -k 10 300 python tools/profile_small.py --clients 10 > "$OUT/small_profile.log" 2>&1; rc=$?
       echo "profile rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    floor)
+      # configs[0]'s K = 2 round against the GPU round trip's floor and FEDn's own loop overhead
+      timeout -k 10 300 python tools/small_floor.py > "$OUT/floor.log" 2>&1; rc=$?
+      echo "floor rc=$rc"; grep -v amdgpu.ids "$OUT/floor.log" | head -2 | cut -c1-900; [ $rc -eq 0 ] || exit $rc ;;
     inflate)
       # host npz decode / encode (CPU only): numpy vs the codec's decoder, one stream split over threads
       timeout -k 10 600 python tools/bench_inflate.py > "$OUT/inflate.log" 2>&1; rc=$?

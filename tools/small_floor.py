@@ -9,6 +9,9 @@ what the round cannot go below on this box:
   pack_k2          the two updates' copies into the pinned arena (native gather) + wait
   plugin           the whole combine_models round (median)
   fedn_loop        FEDn's own loop restated around the numpy arithmetic (tools/bench_small.py)
+  fedn_loop_no_arith  the same loop with increment_average made the identity: the queue / load /
+                   log / delete share every aggregator pays; budget = fedn_loop - this is what a
+                   plug-in has for its arithmetic, against gpu_floor = pack_k2 + the K = 2 fold
 
 and a cProfile of the plug-in's host work. Run on the GPU box: python tools/small_floor.py
 """
@@ -92,6 +95,14 @@ def main():
         while not ev.query():
             pass
     out["fold_zero_copy_spin_us"] = med(fold3_spin)
+
+    def fold2_spin():          # K = 2 needs only the two updates: x1 + n2 (x2 - x1) / N
+        ops.fedavg_fold_raw(po, torch.float32, P, [pa + 4 * P, pa + 8 * P], torch.float32, [7.0, 9.0],
+                            [7.0, 16.0], True, st, dev)
+        ev.record(st)
+        while not ev.query():
+            pass
+    out["fold2_zero_copy_spin_us"] = med(fold2_spin)
     from fedn_amd import codec
     ups = [rng.standard_normal(P).astype(np.float32) for _ in range(2)]
     dst = arena.numpy()
@@ -125,6 +136,18 @@ def main():
             uh2.submit(u, n)
         bench_small.fedn_loop_fedavg(uh2)
     out["fedn_loop_us"] = med(loop, n=400)
+    # the loop's own share that any plug-in pays as well (queue, load, logging, delete): the same
+    # loop with the arithmetic taken out; FEDn's arithmetic alone is the rest
+    real = ref.increment_average
+    ref.increment_average = lambda m, mn, n, N: m
+    try:
+        out["fedn_loop_no_arith_us"] = med(loop, n=400)
+    finally:
+        ref.increment_average = real
+    out["fedn_arith_us"] = med(lambda: real(cl[0], cl[1], ns[1], ns[0] + ns[1]))
+    gpu_floor = out["pack_k2_us"][0] + min(out["fold2_zero_copy_spin_us"][0], out["fold_zero_copy_us"][0])
+    out["budget_us"] = round(out["fedn_loop_us"][0] - out["fedn_loop_no_arith_us"][0], 2)
+    out["gpu_floor_us"] = round(gpu_floor, 2)
     print(json.dumps(out), flush=True)
     pr = cProfile.Profile()
     pr.enable()
