@@ -163,10 +163,16 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
                        seg_bytes ? seg_bytes[i] : 0};
     }
     // big members one after another on every thread (pdeflate.h); the rest member-parallel, largest
-    // first so one long stream does not start last
+    // first so one long stream does not start last. Big: at least min_member bytes, or at least four
+    // chunks and more than an even share of the archive per thread (member-parallel, that member
+    // alone would outlast the rest of the archive spread over the other threads)
+    int64_t total = 0;
+    for (const Member& m : ms) total += m.hlen + m.nbytes;
+    const int64_t floor = 4 * g_par_chunk.load();
     std::vector<int> order;
     for (int i = 0; i < n; ++i) {
-        if (threads > 1 && ms[i].hlen + ms[i].nbytes >= g_par_min.load()) {
+        const int64_t sz = ms[i].hlen + ms[i].nbytes;
+        if (threads > 1 && (sz >= g_par_min.load() || (sz >= floor && sz * threads > total))) {
             if (!deflate_member_parallel(ms[i], threads)) deflate_member(ms[i]);
         } else {
             order.push_back(i);

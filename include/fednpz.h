@@ -92,8 +92,8 @@ int fnpz_savez(int n, const char* const* names, const uint8_t* const* headers, c
                uint8_t* out, int64_t out_cap, int64_t* out_len);
 
 /* fnpz_savez's single-stream parallel deflate (fedn_amd/csrc/pdeflate.h): a member of at least
- * min_member bytes (default 32 MiB) is deflated on every thread in chunks of `chunk` bytes (default
- * 4 MiB) by a reimplementation of zlib 1.2.11's level-6 parse and trees.c whose output is zlib's,
+ * min_member bytes (default 32 MiB), or of at least 4 chunks and more than 1/threads of the archive,
+ * is deflated on every thread in chunks of `chunk` bytes (default 4 MiB) by a reimplementation of zlib 1.2.11's level-6 parse and trees.c whose output is zlib's,
  * byte for byte; an input it does not model falls back to zlib itself. Values <= 0 keep a setting.
  * *parallel / *fallback (may be NULL): members that went parallel / fell back so far. */
 void fnpz_savez_config(int64_t min_member, int64_t chunk, int64_t* parallel, int64_t* fallback);

@@ -135,3 +135,24 @@ def test_save_npz_big_member_parallel_is_numpys(threads):
     ref = io.BytesIO()
     np.savez_compressed(ref, **{str(i): w for i, w in enumerate(ws)})
     assert got == ref.getvalue()
+
+
+def test_save_npz_member_over_its_thread_share_goes_parallel():
+    """Below min_member, a member of >= 4 chunks holding more than 1/threads of the archive is
+    deflated on every thread (member-parallel it would outlast the rest); smaller ones stay zlib's."""
+    lib = _lib()
+    rng = np.random.default_rng(11)
+    ws = [rng.standard_normal(n).astype(np.float32) for n in (400_000, 300_000, 60_000, 1000)]
+    before, fb0 = ctypes.c_int64(), ctypes.c_int64()
+    lib.fnpz_savez_config(0, 0, ctypes.byref(before), ctypes.byref(fb0))
+    lib.fnpz_savez_config(1 << 40, CHUNK, None, None)           # min_member out of reach
+    try:
+        got = codec.save_npz(ws, threads=4)                     # 1.6 MB and 1.2 MB of 3.0 MB: > 1/4 each
+    finally:
+        lib.fnpz_savez_config(32 << 20, 4 << 20, None, None)
+    after, fb1 = ctypes.c_int64(), ctypes.c_int64()
+    lib.fnpz_savez_config(0, 0, ctypes.byref(after), ctypes.byref(fb1))
+    assert after.value - before.value == 2 and fb1.value == fb0.value
+    ref = io.BytesIO()
+    np.savez_compressed(ref, **{str(i): w for i, w in enumerate(ws)})
+    assert got == ref.getvalue()
