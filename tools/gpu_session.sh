@@ -39,6 +39,10 @@ for s in $STEPS; do
         --clients 16 --fedopt-params 20000000 --waves-params 50000000 --waves-clients 32 --cpu-sample 2000000 \
         --host-clients 4 > "$OUT/selflaunch4.log" 2>&1; rc=$?
       echo "selflaunch4 rc=$rc"; grep -v amdgpu.ids "$OUT/selflaunch4.log" | tail -2 | cut -c1-400; [ $rc -eq 0 ] || exit $rc ;;
+    selflaunch8)
+      # bench.py --gpus 8 at DEFAULT sizes, self-launched, all 8 ranks on this box's one GPU
+      FEDN_AMD_BENCH_ONE_GPU=1 timeout -k 10 900 python bench.py --gpus 8 > "$OUT/selflaunch8.log" 2>&1; rc=$?
+      echo "selflaunch8 rc=$rc"; grep -v amdgpu.ids "$OUT/selflaunch8.log" | tail -2 | cut -c1-600; [ $rc -eq 0 ] || exit $rc ;;
     rccl1)
       # the N>1 path at world size 1 over a real RCCL communicator (all-gathers as collectives, P2P fences)
       FEDN_AMD_BENCH_RCCL_WORLD1=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
