@@ -53,7 +53,10 @@ void put32(uint8_t*& p, uint32_t v) { for (int i = 0; i < 4; ++i) p[i] = (uint8_
 void put64(uint8_t*& p, uint64_t v) { for (int i = 0; i < 8; ++i) p[i] = (uint8_t)(v >> (8 * i)); p += 8; }
 
 constexpr uint64_t kZip64Limit = (1ull << 31) - 1;   // zipfile.ZIP64_LIMIT
-constexpr uint32_t kFileCountLimit = (1u << 16) - 1; // zipfile.ZIP_FILECOUNT_LIMIT
+constexpr uint64_t kFileCountLimit = (1u << 16) - 1; // zipfile.ZIP_FILECOUNT_LIMIT
+// the limits fnpz_savez applies (fnpz_savez_zip_limits: tests compare the ZIP64 branches with numpy
+// run under a zipfile whose limits are patched to the same small values)
+std::atomic<uint64_t> g_zip64_limit{kZip64Limit}, g_filecount_limit{kFileCountLimit};
 constexpr uint16_t kDosDate = (0 << 9) | (1 << 5) | 1; // ZipInfo's default date_time 1980-01-01 00:00:00
 constexpr uint16_t kDefaultVersion = 20, kZip64Version = 45;
 constexpr uint32_t kExternalAttr = 0600u << 16;      // zipfile: "?rw-------"
@@ -194,6 +197,7 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
 
     uint8_t* p = out;
     uint8_t* const lim = out + out_cap;
+    const uint64_t zip64_limit = g_zip64_limit.load(), filecount_limit = g_filecount_limit.load();
     std::vector<uint64_t> offs((size_t)n);
     std::vector<uint64_t> comps((size_t)n);
     std::vector<uint16_t> ver((size_t)n);
@@ -203,7 +207,7 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
         const uint64_t raw = (uint64_t)(m.hlen + m.nbytes), comp = m.out.size();
         if ((int64_t)(30 + nl + 20 + comp) > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
         // ZipInfo.FileHeader(zip64=True) as _ZipWriteFile.close rewrites it
-        const bool big = raw > kZip64Limit || comp > kZip64Limit;
+        const bool big = raw > zip64_limit || comp > zip64_limit;
         ver[i] = big ? kZip64Version : kDefaultVersion;
         offs[i] = (uint64_t)(p - out);
         comps[i] = comp;
@@ -237,9 +241,9 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
         const uint64_t csize = comps[i];
         uint64_t extra[3];
         int ne = 0;
-        const bool big = raw > kZip64Limit || csize > kZip64Limit;
+        const bool big = raw > zip64_limit || csize > zip64_limit;
         if (big) extra[ne++] = raw, extra[ne++] = csize;
-        if (offs[i] > kZip64Limit) extra[ne++] = offs[i];
+        if (offs[i] > zip64_limit) extra[ne++] = offs[i];
         const uint16_t v = ne ? std::max<uint16_t>(kZip64Version, ver[i]) : ver[i];
         if ((int64_t)(46 + nl + 4 + 8 * ne) > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
         put32(p, 0x02014b50);
@@ -258,7 +262,7 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
         put16(p, 0);                          // disk number start
         put16(p, 0);                          // internal attributes
         put32(p, kExternalAttr);
-        put32(p, offs[i] > kZip64Limit ? 0xFFFFFFFFu : (uint32_t)offs[i]);
+        put32(p, offs[i] > zip64_limit ? 0xFFFFFFFFu : (uint32_t)offs[i]);
         std::memcpy(p, m.name, nl - 4);
         std::memcpy(p + nl - 4, ".npy", 4);
         p += nl;
@@ -271,7 +275,7 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
     const uint64_t pos2 = (uint64_t)(p - out);
     const uint64_t cd_size = pos2 - cd_off;
     uint64_t count = (uint64_t)n, size = cd_size, offset = cd_off;
-    if (count > kFileCountLimit || cd_off > kZip64Limit || cd_size > kZip64Limit) {
+    if (count > filecount_limit || cd_off > zip64_limit || cd_size > zip64_limit) {
         if (56 + 20 > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
         put32(p, 0x06064b50);
         put64(p, 44);
@@ -309,6 +313,11 @@ extern "C" void fnpz_savez_config(int64_t min_member, int64_t chunk, int64_t* pa
     if (chunk > 0) g_par_chunk.store(chunk);
     if (parallel) *parallel = g_par_ok.load();
     if (fallback) *fallback = g_par_fallback.load();
+}
+
+extern "C" void fnpz_savez_zip_limits(int64_t zip64_limit, int64_t filecount_limit) {
+    g_zip64_limit.store(zip64_limit > 0 ? (uint64_t)zip64_limit : kZip64Limit);
+    g_filecount_limit.store(filecount_limit > 0 ? (uint64_t)filecount_limit : kFileCountLimit);
 }
 
 extern "C" int fnpz_deflate_exact(const uint8_t* in, int64_t len, const int64_t* ends, int nends, int threads,

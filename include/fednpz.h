@@ -93,10 +93,17 @@ int fnpz_savez(int n, const char* const* names, const uint8_t* const* headers, c
 
 /* fnpz_savez's single-stream parallel deflate (fedn_amd/csrc/pdeflate.h): a member of at least
  * min_member bytes (default 32 MiB), or of at least 4 chunks and more than 1/threads of the archive,
- * is deflated on every thread in chunks of `chunk` bytes (default 4 MiB) by a reimplementation of zlib 1.2.11's level-6 parse and trees.c whose output is zlib's,
- * byte for byte; an input it does not model falls back to zlib itself. Values <= 0 keep a setting.
+ * is deflated on every thread in chunks of `chunk` bytes (default 4 MiB) by a reimplementation of
+ * zlib 1.2.11's level-6 parse and trees.c whose output is zlib's, byte for byte; an input it does not model falls back to zlib itself. Values <= 0 keep a setting.
  * *parallel / *fallback (may be NULL): members that went parallel / fell back so far. */
 void fnpz_savez_config(int64_t min_member, int64_t chunk, int64_t* parallel, int64_t* fallback);
+
+/* zipfile's ZIP64_LIMIT ((1 << 31) - 1) and ZIP_FILECOUNT_LIMIT ((1 << 16) - 1) as fnpz_savez applies
+ * them (sizes / offsets past the first: ZIP64 fields and version 45; more members than the second,
+ * or a central directory past the first: ZIP64 end records). Values <= 0 restore those defaults.
+ * For tests: with smaller limits, and CPython's zipfile patched to the same, the ZIP64 branches are
+ * compared with np.savez_compressed at kilobyte sizes. */
+void fnpz_savez_zip_limits(int64_t zip64_limit, int64_t filecount_limit);
 
 /* That deflate on its own (tests): in[0, len) fed as deflate(Z_NO_FLUSH) calls ending at ends[0 ..
  * nends) (ends[nends - 1] == len) and then Z_FINISH, raw (wbits -15), level 6, memLevel 8. FNPZ_OK
