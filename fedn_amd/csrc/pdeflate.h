@@ -1121,7 +1121,15 @@ inline bool deflate_exact(const uint8_t* S, int64_t L, const std::vector<int64_t
         st->fallback = "too small";
         return false;
     }
-    const int T = (int)std::min<int64_t>(L / chunk, 1 << 20);
+    // a whole number of chunks per thread (the parse is most of the time: a last round with a few
+    // chunks would leave the other threads idle), each near the requested size
+    int64_t T0 = std::min<int64_t>(L / chunk, 1 << 20);
+    if (threads > 1 && T0 > threads) {
+        const int64_t k = std::max<int64_t>(1, (T0 + threads / 2) / threads);
+        const int64_t Tk = std::min<int64_t>(k * threads, L / kMinChunk);
+        if (Tk >= 2 && 2 * kTailRec <= L / Tk * Tk) T0 = Tk, chunk = L / Tk;
+    }
+    const int T = (int)T0;
     std::vector<Chunk> C((size_t)T);
     for (int i = 0; i < T; ++i) {
         C[i].b = (int64_t)i * chunk;

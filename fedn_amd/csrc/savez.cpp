@@ -20,6 +20,7 @@
 #include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -76,15 +77,16 @@ struct Member {
 // the same stream from pdeflate.h on `threads` threads; false: the caller runs zlib
 bool deflate_member_parallel(Member& m, int threads) {
     const int64_t L = m.hlen + m.nbytes;
-    std::vector<uint8_t> S((size_t)L);
-    std::memcpy(S.data(), m.header, (size_t)m.hlen);
+    std::unique_ptr<uint8_t[]> buf(new uint8_t[(size_t)L]);   // no zero fill: every byte is copied in
+    uint8_t* const S = buf.get();
+    std::memcpy(S, m.header, (size_t)m.hlen);
     const int64_t piece = 8 << 20;
     pdef::parallel((int)((m.nbytes + piece - 1) / piece), threads, [&](int i) {
         const int64_t b = (int64_t)i * piece;
-        std::memcpy(S.data() + m.hlen + b, m.data + b, (size_t)std::min(piece, m.nbytes - b));
+        std::memcpy(S + m.hlen + b, m.data + b, (size_t)std::min(piece, m.nbytes - b));
     });
     pdef::Stats st;
-    const bool ok = pdef::deflate_exact(S.data(), L, input_ends(m.hlen, m.nbytes, m.seg), threads, g_par_chunk.load(),
+    const bool ok = pdef::deflate_exact(S, L, input_ends(m.hlen, m.nbytes, m.seg), threads, g_par_chunk.load(),
                                         m.out, &st);
     (ok ? g_par_ok : g_par_fallback).fetch_add(1);
     g_par_reason = st.fallback;
@@ -94,7 +96,7 @@ bool deflate_member_parallel(Member& m, int threads) {
     std::vector<uint32_t> crcs((size_t)np);
     pdef::parallel(np, threads, [&](int i) {
         const int64_t b = (int64_t)i * piece;
-        crcs[i] = fnpz_fast::crc32(0, S.data() + b, (size_t)std::min(piece, L - b));
+        crcs[i] = fnpz_fast::crc32(0, S + b, (size_t)std::min(piece, L - b));
     });
     uLong crc = crcs[0];
     for (int i = 1; i < np; ++i) crc = crc32_combine(crc, crcs[i], (z_off_t)std::min(piece, L - (int64_t)i * piece));
