@@ -72,6 +72,11 @@ for s in $STEPS; do
       # configs[0]'s K = 2 round against the GPU round trip's floor and FEDn's own loop overhead
       timeout -k 10 300 python tools/small_floor.py > "$OUT/floor.log" 2>&1; rc=$?
       echo "floor rc=$rc"; grep -v amdgpu.ids "$OUT/floor.log" | head -2 | cut -c1-900; [ $rc -eq 0 ] || exit $rc ;;
+    roundblob)
+      # a combiner's round end down to the stored global-model blob: FEDn (numpy loop + np.savez_compressed)
+      # vs the plug-in (GPU fold + exact writer), blobs compared byte for byte
+      timeout -k 10 600 python tools/bench_round_e2e.py > "$OUT/roundblob.log" 2>&1; rc=$?
+      echo "roundblob rc=$rc"; grep -v amdgpu.ids "$OUT/roundblob.log" | tail -2 | cut -c1-700; [ $rc -eq 0 ] || exit $rc ;;
     inflate)
       # host npz decode / encode (CPU only): numpy vs the codec's decoder, one stream split over threads
       timeout -k 10 600 python tools/bench_inflate.py > "$OUT/inflate.log" 2>&1; rc=$?
