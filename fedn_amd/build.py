@@ -30,6 +30,7 @@ NPZ_HDR = os.path.join(ROOT, "include", "fednpz.h")
 NPZ_INFLATE = os.path.join(HERE, "csrc", "inflate.h")      # the codec's DEFLATE decoder + CRC-32
 NPZ_SAVEZ = os.path.join(HERE, "csrc", "savez.cpp")        # numpy-identical writer (fnpz_savez)
 NPZ_PDEFLATE = os.path.join(HERE, "csrc", "pdeflate.h")    # its single-stream parallel deflate
+NPZ_GUARD = os.path.join(HERE, "csrc", "fnpz_guard.h")      # no exception across the C ABI
 NPZ_OUT = os.path.join(HERE, "libfednpz.so")
 
 
@@ -39,7 +40,7 @@ def _stale(out, *deps):
 
 def build_codec(force=False, verbose=True):
     """Host-side npz codec (C++17 + zlib, no GPU code)."""
-    deps = [d for d in (NPZ_SRC, NPZ_HDR, NPZ_INFLATE, NPZ_SAVEZ, NPZ_PDEFLATE) if os.path.exists(d)]
+    deps = [d for d in (NPZ_SRC, NPZ_HDR, NPZ_INFLATE, NPZ_SAVEZ, NPZ_PDEFLATE, NPZ_GUARD) if os.path.exists(d)]
     if not force and not _stale(NPZ_OUT, *deps):
         return NPZ_OUT
     cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"

@@ -37,6 +37,7 @@ class Entry(ctypes.Structure):
 
 
 FNPZ_EFALLBACK = 5     # fnpz_deflate_exact: the input needs zlib itself (fednpz.h)
+FNPZ_ENOMEM = 6        # memory or a worker thread ran out inside the call: raised as MemoryError
 
 
 class CodecError(ValueError):
@@ -107,7 +108,10 @@ def load_lib():
 
 def _check(rc):
     if rc:
-        raise CodecError(f"fednpz status {rc}: {load_lib().fnpz_last_error().decode(errors='replace')}")
+        msg = f"fednpz status {rc}: {load_lib().fnpz_last_error().decode(errors='replace')}"
+        if rc == FNPZ_ENOMEM:
+            raise MemoryError(msg)
+        raise CodecError(msg)
 
 
 def gather_start_raw(dsts, srcs, nbytes, threads, window):

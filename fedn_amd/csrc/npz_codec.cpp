@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../../include/fednpz.h"
+#include "fnpz_guard.h"
 #include "inflate.h"
 
 namespace {
@@ -452,13 +453,18 @@ class DecodePool {
         {
             std::lock_guard<std::mutex> lk(mu_);
             const int w = std::min(want, kMaxThreads) - 1;
-            for (; workers_ < w; ++workers_) std::thread([this] { work(); }).detach();
+            try {
+                for (; workers_ < w; ++workers_) std::thread([this] { work(); }).detach();
+            } catch (...) {
+                // no more threads: the pool's and the caller's finish the job
+            }
             queue_.push_back(job);
         }
         cv_.notify_all();
         for (int i; (i = claim(job.get())) >= 0;) finish(*job, i);
         std::unique_lock<std::mutex> lk(job->mu);
         job->cv.wait(lk, [&] { return job->done == job->n; });
+        job->err.rethrow();   // a worker's exception, on the calling thread
     }
 
    private:
@@ -466,6 +472,7 @@ class DecodePool {
     struct Job {
         int n = 0, next = 0, done = 0;   // next: under the pool's lock; done: under mu
         std::function<void(int)> f;      // the caller's body, alive until done == n
+        fnpz_internal::FirstError err;   // the first exception of any index (the rest still run)
         std::mutex mu;
         std::condition_variable cv;
     };
@@ -482,7 +489,11 @@ class DecodePool {
         return i;
     }
     static void finish(Job& j, int i) {
-        j.f(i);
+        try {
+            j.f(i);
+        } catch (...) {
+            j.err.capture();
+        }
         std::lock_guard<std::mutex> lk(j.mu);
         if (++j.done == j.n) j.cv.notify_all();
     }
@@ -684,18 +695,7 @@ int decode_one(const uint8_t* a, const fnpz_entry& e, void* dst, char* err, size
 
 template <class F>
 void parallel_for(int n, int threads, F&& f) {
-    threads = std::max(1, std::min(threads, n));
-    if (threads == 1) {
-        for (int i = 0; i < n; ++i) f(i);
-        return;
-    }
-    std::atomic<int> next{0};
-    std::vector<std::thread> pool;
-    for (int t = 0; t < threads; ++t)
-        pool.emplace_back([&] {
-            for (int i; (i = next.fetch_add(1)) < n;) f(i);
-        });
-    for (auto& th : pool) th.join();
+    fnpz_internal::run_parallel(n, threads, std::forward<F>(f));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -980,26 +980,28 @@ extern "C" {
 int fnpz_abi_version(void) { return FNPZ_ABI_VERSION; }
 
 int fnpz_inflate_raw(const uint8_t* in, int64_t in_len, uint8_t* out, int64_t out_len, int64_t window, int* stream_end) {
-    g_err[0] = 0;
-    if (in_len < 0 || out_len < 0 || window < 0 || (in_len > 0 && !in) || (out_len > 0 && !out))
-        return fail(FNPZ_EINVAL, "fnpz_inflate_raw: bad arguments");
-    std::unique_ptr<fnpz_fast::Inflate> dec(new fnpz_fast::Inflate(in, (size_t)in_len));
-    uint8_t* o = out;
-    uint8_t* const end = out + out_len;
-    int rc = fnpz_fast::Inflate::kFull;
-    while (rc == fnpz_fast::Inflate::kFull && o < end) {
-        uint8_t* w = window > 0 ? std::min(end, o + window) : end;
-        rc = dec->run(&o, w, out);
-        if (rc == fnpz_fast::Inflate::kFull && o != w) break;
-    }
-    if (rc == fnpz_fast::Inflate::kFull && o == end) rc = dec->run(&o, end, out);   // the final block's end, if here
-    if (stream_end) *stream_end = rc == fnpz_fast::Inflate::kEnd;
-    if (rc == fnpz_fast::Inflate::kCorrupt)
-        return fail(FNPZ_ECORRUPT, "fnpz_inflate_raw: invalid deflate stream (inflate.h:%d) after %lld bytes",
-                    dec->error_line(), (long long)(o - out));
-    if (o != end) return fail(FNPZ_ECORRUPT, "fnpz_inflate_raw: stream ended after %lld of %lld bytes", (long long)(o - out),
-                              (long long)out_len);
-    return FNPZ_OK;
+    return fnpz_internal::guard("fnpz_inflate_raw", [&]() -> int {
+        g_err[0] = 0;
+        if (in_len < 0 || out_len < 0 || window < 0 || (in_len > 0 && !in) || (out_len > 0 && !out))
+            return fail(FNPZ_EINVAL, "fnpz_inflate_raw: bad arguments");
+        std::unique_ptr<fnpz_fast::Inflate> dec(new fnpz_fast::Inflate(in, (size_t)in_len));
+        uint8_t* o = out;
+        uint8_t* const end = out + out_len;
+        int rc = fnpz_fast::Inflate::kFull;
+        while (rc == fnpz_fast::Inflate::kFull && o < end) {
+            uint8_t* w = window > 0 ? std::min(end, o + window) : end;
+            rc = dec->run(&o, w, out);
+            if (rc == fnpz_fast::Inflate::kFull && o != w) break;
+        }
+        if (rc == fnpz_fast::Inflate::kFull && o == end) rc = dec->run(&o, end, out);   // the final block's end, if here
+        if (stream_end) *stream_end = rc == fnpz_fast::Inflate::kEnd;
+        if (rc == fnpz_fast::Inflate::kCorrupt)
+            return fail(FNPZ_ECORRUPT, "fnpz_inflate_raw: invalid deflate stream (inflate.h:%d) after %lld bytes",
+                        dec->error_line(), (long long)(o - out));
+        if (o != end) return fail(FNPZ_ECORRUPT, "fnpz_inflate_raw: stream ended after %lld of %lld bytes", (long long)(o - out),
+                                  (long long)out_len);
+        return FNPZ_OK;
+    });
 }
 
 void fnpz_parallel_config(int64_t min_member, int64_t min_chunk, int64_t* parallel, int64_t* fallback) {
@@ -1015,100 +1017,104 @@ uint32_t fnpz_crc32(uint32_t crc, const uint8_t* data, int64_t len) {
 const char* fnpz_last_error(void) { return g_err; }
 
 int fnpz_open(const uint8_t* archive, int64_t len, fnpz_entry* entries, int max_entries, int* n_entries) {
-    g_err[0] = 0;
-    if (!archive || len < 0 || !n_entries || (max_entries > 0 && !entries)) return fail(FNPZ_EINVAL, "fnpz_open: bad arguments");
-    std::vector<CdEntry> cd;
-    int rc = read_central(archive, len, cd);
-    if (rc) return rc;
-    *n_entries = (int)cd.size();
-    if ((int)cd.size() > max_entries) return fail(FNPZ_ENOSPC, "fnpz_open: archive has %d members, room for %d", (int)cd.size(), max_entries);
-    for (size_t i = 0; i < cd.size(); ++i)
-        if ((rc = resolve_entry(archive, len, cd[i], &entries[i]))) return rc;
-    return FNPZ_OK;
+    return fnpz_internal::guard("fnpz_open", [&]() -> int {
+        g_err[0] = 0;
+        if (!archive || len < 0 || !n_entries || (max_entries > 0 && !entries)) return fail(FNPZ_EINVAL, "fnpz_open: bad arguments");
+        std::vector<CdEntry> cd;
+        int rc = read_central(archive, len, cd);
+        if (rc) return rc;
+        *n_entries = (int)cd.size();
+        if ((int)cd.size() > max_entries) return fail(FNPZ_ENOSPC, "fnpz_open: archive has %d members, room for %d", (int)cd.size(), max_entries);
+        for (size_t i = 0; i < cd.size(); ++i)
+            if ((rc = resolve_entry(archive, len, cd[i], &entries[i]))) return rc;
+        return FNPZ_OK;
+    });
 }
 
 int fnpz_read(const uint8_t* archive, int64_t len, const fnpz_entry* entries, int n, void* const* dsts, int threads) {
-    g_err[0] = 0;
-    if (!archive || n < 0 || (n > 0 && (!entries || !dsts))) return fail(FNPZ_EINVAL, "fnpz_read: bad arguments");
-    for (int i = 0; i < n; ++i) {
-        if (entries[i].data_offset + entries[i].comp_size > len) return fail(FNPZ_EINVAL, "fnpz_read: entry %d out of range", i);
-        if (entries[i].nbytes > 0 && !dsts[i]) return fail(FNPZ_EINVAL, "fnpz_read: dsts[%d] is NULL", i);
-    }
-    // tasks: one per member, or one per block of members that carry a block index
-    struct Task { int member, block; };
-    std::vector<Task> tasks;
-    for (int i = 0; i < n; ++i) {
-        if (entries[i].method == 8 && entries[i].index_count > 0)
-            for (int b = 0; b < entries[i].index_count; ++b) tasks.push_back({i, b});
-        else
-            tasks.push_back({i, -1});
-    }
-    // a thread per MiB of compressed input at most: starting threads costs more than inflating a
-    // small model's members (mnist-sized archives decode 1.8x faster on the calling thread alone)
-    int64_t comp_total = 0;
-    for (int i = 0; i < n; ++i) comp_total += entries[i].comp_size;
-    const int64_t unit = std::max<int64_t>(1, std::min<int64_t>(1 << 20, g_par_chunk.load()));
-    threads = (int)std::max<int64_t>(1, std::min<int64_t>(threads, comp_total / unit));
-    std::vector<int> rcs(tasks.size(), FNPZ_OK);
-    std::vector<uLong> bcrc(tasks.size(), 0);
-    std::vector<std::string> errs(tasks.size());
-    parallel_for((int)tasks.size(), threads, [&](int t) {
-        const fnpz_entry& e = entries[tasks[t].member];
-        void* dst = dsts[tasks[t].member];
-        char msg[300] = "";
-        if (tasks[t].block < 0) {
-            // threads the other tasks leave idle decode this member's stream in parallel
-            rcs[t] = decode_one(archive, e, dst, msg, sizeof(msg), std::max(1, threads / (int)tasks.size()));
-        } else {
-            const uint8_t* ix = archive + e.index_offset;
-            const uint64_t B = rd64(ix + 8);
-            const int b = tasks[t].block;
-            const uint64_t c0 = rd64(ix + 16 + 8ull * b), c1 = rd64(ix + 16 + 8ull * (b + 1));
-            const uint64_t r0 = B * (uint64_t)b, r1 = std::min<uint64_t>(r0 + B, (uint64_t)e.uncomp_size);
-            if (c1 < c0 || c1 > (uint64_t)e.comp_size || r0 >= r1) {
-                rcs[t] = FNPZ_ECORRUPT;
-                snprintf(msg, sizeof(msg), "%s: bad block index", e.name);
+    return fnpz_internal::guard("fnpz_read", [&]() -> int {
+        g_err[0] = 0;
+        if (!archive || n < 0 || (n > 0 && (!entries || !dsts))) return fail(FNPZ_EINVAL, "fnpz_read: bad arguments");
+        for (int i = 0; i < n; ++i) {
+            if (entries[i].data_offset + entries[i].comp_size > len) return fail(FNPZ_EINVAL, "fnpz_read: entry %d out of range", i);
+            if (entries[i].nbytes > 0 && !dsts[i]) return fail(FNPZ_EINVAL, "fnpz_read: dsts[%d] is NULL", i);
+        }
+        // tasks: one per member, or one per block of members that carry a block index
+        struct Task { int member, block; };
+        std::vector<Task> tasks;
+        for (int i = 0; i < n; ++i) {
+            if (entries[i].method == 8 && entries[i].index_count > 0)
+                for (int b = 0; b < entries[i].index_count; ++b) tasks.push_back({i, b});
+            else
+                tasks.push_back({i, -1});
+        }
+        // a thread per MiB of compressed input at most: starting threads costs more than inflating a
+        // small model's members (mnist-sized archives decode 1.8x faster on the calling thread alone)
+        int64_t comp_total = 0;
+        for (int i = 0; i < n; ++i) comp_total += entries[i].comp_size;
+        const int64_t unit = std::max<int64_t>(1, std::min<int64_t>(1 << 20, g_par_chunk.load()));
+        threads = (int)std::max<int64_t>(1, std::min<int64_t>(threads, comp_total / unit));
+        std::vector<int> rcs(tasks.size(), FNPZ_OK);
+        std::vector<uLong> bcrc(tasks.size(), 0);
+        std::vector<std::string> errs(tasks.size());
+        parallel_for((int)tasks.size(), threads, [&](int t) {
+            const fnpz_entry& e = entries[tasks[t].member];
+            void* dst = dsts[tasks[t].member];
+            char msg[300] = "";
+            if (tasks[t].block < 0) {
+                // threads the other tasks leave idle decode this member's stream in parallel
+                rcs[t] = decode_one(archive, e, dst, msg, sizeof(msg), std::max(1, threads / (int)tasks.size()));
             } else {
-                // block 0 starts with the .npy header; each block is its own deflate history
-                const uint64_t h0 = r0 < (uint64_t)e.npy_header ? (uint64_t)e.npy_header - r0 : 0;
-                if (r0 + h0 > r1) {
+                const uint8_t* ix = archive + e.index_offset;
+                const uint64_t B = rd64(ix + 8);
+                const int b = tasks[t].block;
+                const uint64_t c0 = rd64(ix + 16 + 8ull * b), c1 = rd64(ix + 16 + 8ull * (b + 1));
+                const uint64_t r0 = B * (uint64_t)b, r1 = std::min<uint64_t>(r0 + B, (uint64_t)e.uncomp_size);
+                if (c1 < c0 || c1 > (uint64_t)e.comp_size || r0 >= r1) {
                     rcs[t] = FNPZ_ECORRUPT;
                     snprintf(msg, sizeof(msg), "%s: bad block index", e.name);
                 } else {
-                    std::vector<uint8_t> hdr((size_t)h0);
-                    uint8_t* out = static_cast<uint8_t*>(dst) + (r0 + h0 - (uint64_t)e.npy_header);
-                    uint32_t crc = 0;
-                    int line = 0;
-                    if (inflate_split(archive + e.data_offset + c0, (int64_t)(c1 - c0), hdr.data(), (int64_t)h0, out,
-                                      (int64_t)(r1 - r0 - h0), &crc, &line)) {
+                    // block 0 starts with the .npy header; each block is its own deflate history
+                    const uint64_t h0 = r0 < (uint64_t)e.npy_header ? (uint64_t)e.npy_header - r0 : 0;
+                    if (r0 + h0 > r1) {
                         rcs[t] = FNPZ_ECORRUPT;
-                        snprintf(msg, sizeof(msg), "%s: corrupt block %d (inflate.h:%d)", e.name, b, line);
+                        snprintf(msg, sizeof(msg), "%s: bad block index", e.name);
+                    } else {
+                        std::vector<uint8_t> hdr((size_t)h0);
+                        uint8_t* out = static_cast<uint8_t*>(dst) + (r0 + h0 - (uint64_t)e.npy_header);
+                        uint32_t crc = 0;
+                        int line = 0;
+                        if (inflate_split(archive + e.data_offset + c0, (int64_t)(c1 - c0), hdr.data(), (int64_t)h0, out,
+                                          (int64_t)(r1 - r0 - h0), &crc, &line)) {
+                            rcs[t] = FNPZ_ECORRUPT;
+                            snprintf(msg, sizeof(msg), "%s: corrupt block %d (inflate.h:%d)", e.name, b, line);
+                        }
+                        bcrc[t] = crc;
                     }
-                    bcrc[t] = crc;
                 }
             }
+            errs[t] = msg;
+        });
+        for (size_t t = 0; t < tasks.size(); ++t)
+            if (rcs[t]) return fail(rcs[t], "%s", errs[t].c_str());
+        // combine the block CRCs of indexed members, in order
+        for (size_t t = 0; t < tasks.size();) {
+            const int i = tasks[t].member;
+            if (tasks[t].block < 0) {
+                ++t;
+                continue;
+            }
+            const fnpz_entry& e = entries[i];
+            const uint64_t B = rd64(archive + e.index_offset + 8);
+            uLong crc = 0;
+            for (int b = 0; b < e.index_count; ++b, ++t) {
+                const uint64_t r0 = B * (uint64_t)b, r1 = std::min<uint64_t>(r0 + B, (uint64_t)e.uncomp_size);
+                crc = b == 0 ? bcrc[t] : crc32_combine(crc, bcrc[t], (z_off_t)(r1 - r0));
+            }
+            if ((uint32_t)crc != e.crc32) return fail(FNPZ_ECORRUPT, "%s: CRC-32 mismatch", e.name);
         }
-        errs[t] = msg;
+        return FNPZ_OK;
     });
-    for (size_t t = 0; t < tasks.size(); ++t)
-        if (rcs[t]) return fail(rcs[t], "%s", errs[t].c_str());
-    // combine the block CRCs of indexed members, in order
-    for (size_t t = 0; t < tasks.size();) {
-        const int i = tasks[t].member;
-        if (tasks[t].block < 0) {
-            ++t;
-            continue;
-        }
-        const fnpz_entry& e = entries[i];
-        const uint64_t B = rd64(archive + e.index_offset + 8);
-        uLong crc = 0;
-        for (int b = 0; b < e.index_count; ++b, ++t) {
-            const uint64_t r0 = B * (uint64_t)b, r1 = std::min<uint64_t>(r0 + B, (uint64_t)e.uncomp_size);
-            crc = b == 0 ? bcrc[t] : crc32_combine(crc, bcrc[t], (z_off_t)(r1 - r0));
-        }
-        if ((uint32_t)crc != e.crc32) return fail(FNPZ_ECORRUPT, "%s: CRC-32 mismatch", e.name);
-    }
-    return FNPZ_OK;
 }
 
 int64_t fnpz_write_bound(int n, const int64_t* header_lens, const int64_t* nbytes, const int32_t* name_lens) {
@@ -1126,273 +1132,281 @@ int64_t fnpz_write_bound(int n, const int64_t* header_lens, const int64_t* nbyte
 int fnpz_write(int n, const char* const* names, const uint8_t* const* headers, const int64_t* header_lens,
                const void* const* datas, const int64_t* nbytes, int level, int strategy, int threads, int64_t block,
                uint8_t* out, int64_t out_cap, int64_t* out_len) {
-    g_err[0] = 0;
-    if (n < 0 || !out || !out_len || (n > 0 && (!names || !headers || !header_lens || !datas || !nbytes)))
-        return fail(FNPZ_EINVAL, "fnpz_write: bad arguments");
-    if (level < 0 || level > 9) return fail(FNPZ_EINVAL, "fnpz_write: level must be 0..9");
-    if (strategy != FNPZ_STRATEGY_AUTO && (strategy < Z_DEFAULT_STRATEGY || strategy > Z_FIXED))
-        return fail(FNPZ_EINVAL, "fnpz_write: strategy must be FNPZ_STRATEGY_AUTO or a zlib strategy 0..4");
-    if (block <= 0) block = 4 << 20;
-    block = std::min<int64_t>(std::max<int64_t>(block, 64 << 10), 1 << 30);
-    std::vector<MemberSrc> src((size_t)n);
-    std::vector<Block> blocks;
-    std::vector<int64_t> mblock((size_t)n);
-    for (int i = 0; i < n; ++i) {
-        src[i] = MemberSrc{headers[i], header_lens[i], static_cast<const uint8_t*>(datas[i]), nbytes[i]};
-        const int64_t total = header_lens[i] + nbytes[i];
-        const int64_t B = std::max<int64_t>(block, (total + kMaxIndexBlocks - 1) / kMaxIndexBlocks);
-        mblock[i] = B;
-        for (int64_t b = 0; b < total || b == 0; b += B) {
-            Block blk;
-            blk.member = i;
-            blk.begin = b;
-            blk.len = std::min(B, total - b);
-            blk.last = b + B >= total;
-            blocks.push_back(std::move(blk));
-            if (total == 0) break;
+    return fnpz_internal::guard("fnpz_write", [&]() -> int {
+        g_err[0] = 0;
+        if (n < 0 || !out || !out_len || (n > 0 && (!names || !headers || !header_lens || !datas || !nbytes)))
+            return fail(FNPZ_EINVAL, "fnpz_write: bad arguments");
+        if (level < 0 || level > 9) return fail(FNPZ_EINVAL, "fnpz_write: level must be 0..9");
+        if (strategy != FNPZ_STRATEGY_AUTO && (strategy < Z_DEFAULT_STRATEGY || strategy > Z_FIXED))
+            return fail(FNPZ_EINVAL, "fnpz_write: strategy must be FNPZ_STRATEGY_AUTO or a zlib strategy 0..4");
+        if (block <= 0) block = 4 << 20;
+        block = std::min<int64_t>(std::max<int64_t>(block, 64 << 10), 1 << 30);
+        std::vector<MemberSrc> src((size_t)n);
+        std::vector<Block> blocks;
+        std::vector<int64_t> mblock((size_t)n);
+        for (int i = 0; i < n; ++i) {
+            src[i] = MemberSrc{headers[i], header_lens[i], static_cast<const uint8_t*>(datas[i]), nbytes[i]};
+            const int64_t total = header_lens[i] + nbytes[i];
+            const int64_t B = std::max<int64_t>(block, (total + kMaxIndexBlocks - 1) / kMaxIndexBlocks);
+            mblock[i] = B;
+            for (int64_t b = 0; b < total || b == 0; b += B) {
+                Block blk;
+                blk.member = i;
+                blk.begin = b;
+                blk.len = std::min(B, total - b);
+                blk.last = b + B >= total;
+                blocks.push_back(std::move(blk));
+                if (total == 0) break;
+            }
         }
-    }
-    parallel_for((int)blocks.size(), threads,
-                 [&](int j) { deflate_block(src[blocks[j].member], blocks[j], level, strategy); });
-    for (auto& b : blocks)
-        if (b.rc != Z_OK) return fail(FNPZ_ECORRUPT, "fnpz_write: deflate failed on member %d", b.member);
+        parallel_for((int)blocks.size(), threads,
+                     [&](int j) { deflate_block(src[blocks[j].member], blocks[j], level, strategy); });
+        for (auto& b : blocks)
+            if (b.rc != Z_OK) return fail(FNPZ_ECORRUPT, "fnpz_write: deflate failed on member %d", b.member);
 
-    uint8_t* p = out;
-    uint8_t* const lim = out + out_cap;
-    std::vector<uint64_t> offs((size_t)n), comps((size_t)n);
-    std::vector<uint32_t> crcs((size_t)n);
-    size_t bi = 0;
-    for (int i = 0; i < n; ++i) {
-        const size_t nl = std::strlen(names[i]) + 4;
-        uint64_t comp = 0;
-        uLong crc = 0;
-        size_t bj = bi;
-        for (; bj < blocks.size() && blocks[bj].member == i; ++bj) {
-            comp += blocks[bj].out.size();
-            crc = bj == bi ? blocks[bj].crc : crc32_combine(crc, blocks[bj].crc, (z_off_t)blocks[bj].len);
+        uint8_t* p = out;
+        uint8_t* const lim = out + out_cap;
+        std::vector<uint64_t> offs((size_t)n), comps((size_t)n);
+        std::vector<uint32_t> crcs((size_t)n);
+        size_t bi = 0;
+        for (int i = 0; i < n; ++i) {
+            const size_t nl = std::strlen(names[i]) + 4;
+            uint64_t comp = 0;
+            uLong crc = 0;
+            size_t bj = bi;
+            for (; bj < blocks.size() && blocks[bj].member == i; ++bj) {
+                comp += blocks[bj].out.size();
+                crc = bj == bi ? blocks[bj].crc : crc32_combine(crc, blocks[bj].crc, (z_off_t)blocks[bj].len);
+            }
+            const uint64_t raw = (uint64_t)(header_lens[i] + nbytes[i]);
+            const int nblk = (int)(bj - bi);
+            const int xl = 20 + 4 + 16 + 8 * (nblk + 1);
+            if (p + 30 + nl + xl + comp > lim) return fail(FNPZ_ENOSPC, "fnpz_write: output buffer too small");
+            offs[i] = (uint64_t)(p - out);
+            comps[i] = comp;
+            crcs[i] = (uint32_t)crc;
+            wr32(p, kLocalSig);
+            wr16(p + 4, 45);
+            wr16(p + 6, 0);
+            wr16(p + 8, 8);
+            wr16(p + 10, 0);        // DOS time 00:00
+            wr16(p + 12, 0x21);     // DOS date 1980-01-01
+            wr32(p + 14, (uint32_t)crc);
+            wr32(p + 18, 0xFFFFFFFFu);
+            wr32(p + 22, 0xFFFFFFFFu);
+            wr16(p + 26, (uint16_t)nl);
+            wr16(p + 28, (uint16_t)xl);
+            std::memcpy(p + 30, names[i], nl - 4);
+            std::memcpy(p + 30 + nl - 4, ".npy", 4);
+            uint8_t* x = p + 30 + nl;
+            wr16(x, 1);
+            wr16(x + 2, 16);
+            wr64(x + 4, raw);
+            wr64(x + 12, comp);
+            x += 20;
+            wr16(x, kIndexId);
+            wr16(x + 2, (uint16_t)(16 + 8 * (nblk + 1)));
+            wr32(x + 4, (uint32_t)nblk);
+            wr32(x + 8, 0);
+            wr64(x + 12, (uint64_t)mblock[i]);
+            uint64_t off = 0;
+            for (int b = 0; b <= nblk; ++b) {
+                wr64(x + 20 + 8 * b, off);
+                if (b < nblk) off += blocks[bi + b].out.size();
+            }
+            p = x + 20 + 8 * (nblk + 1);
+            for (; bi < bj; ++bi) {
+                std::memcpy(p, blocks[bi].out.data(), blocks[bi].out.size());
+                p += blocks[bi].out.size();
+                std::vector<uint8_t>().swap(blocks[bi].out);
+            }
         }
-        const uint64_t raw = (uint64_t)(header_lens[i] + nbytes[i]);
-        const int nblk = (int)(bj - bi);
-        const int xl = 20 + 4 + 16 + 8 * (nblk + 1);
-        if (p + 30 + nl + xl + comp > lim) return fail(FNPZ_ENOSPC, "fnpz_write: output buffer too small");
-        offs[i] = (uint64_t)(p - out);
-        comps[i] = comp;
-        crcs[i] = (uint32_t)crc;
-        wr32(p, kLocalSig);
-        wr16(p + 4, 45);
+        const uint64_t cd_off = (uint64_t)(p - out);
+        for (int i = 0; i < n; ++i) {
+            const size_t nl = std::strlen(names[i]) + 4;
+            if (p + 46 + nl + 28 > lim) return fail(FNPZ_ENOSPC, "fnpz_write: output buffer too small");
+            const uint64_t raw = (uint64_t)(header_lens[i] + nbytes[i]);
+            wr32(p, kCentralSig);
+            wr16(p + 4, 45);
+            wr16(p + 6, 45);
+            wr16(p + 8, 0);
+            wr16(p + 10, 8);
+            wr16(p + 12, 0);
+            wr16(p + 14, 0x21);
+            wr32(p + 16, crcs[i]);
+            wr32(p + 20, 0xFFFFFFFFu);
+            wr32(p + 24, 0xFFFFFFFFu);
+            wr16(p + 28, (uint16_t)nl);
+            wr16(p + 30, 28);
+            wr16(p + 32, 0);
+            wr16(p + 34, 0);
+            wr16(p + 36, 0);
+            wr32(p + 38, 0x01800000u);   // -rw------- (what zipfile writes for numpy)
+            wr32(p + 42, 0xFFFFFFFFu);
+            std::memcpy(p + 46, names[i], nl - 4);
+            std::memcpy(p + 46 + nl - 4, ".npy", 4);
+            uint8_t* x = p + 46 + nl;
+            wr16(x, 1);
+            wr16(x + 2, 24);
+            wr64(x + 4, raw);
+            wr64(x + 12, comps[i]);
+            wr64(x + 20, offs[i]);
+            p = x + 28;
+        }
+        const uint64_t cd_size = (uint64_t)(p - out) - cd_off;
+        if (p + 56 + 20 + 22 > lim) return fail(FNPZ_ENOSPC, "fnpz_write: output buffer too small");
+        const uint64_t z64 = (uint64_t)(p - out);
+        wr32(p, kZ64EocdSig);
+        wr64(p + 4, 44);
+        wr16(p + 12, 45);
+        wr16(p + 14, 45);
+        wr32(p + 16, 0);
+        wr32(p + 20, 0);
+        wr64(p + 24, (uint64_t)n);
+        wr64(p + 32, (uint64_t)n);
+        wr64(p + 40, cd_size);
+        wr64(p + 48, cd_off);
+        p += 56;
+        wr32(p, kZ64LocSig);
+        wr32(p + 4, 0);
+        wr64(p + 8, z64);
+        wr32(p + 16, 1);
+        p += 20;
+        wr32(p, kEocdSig);
+        wr16(p + 4, 0);
         wr16(p + 6, 0);
-        wr16(p + 8, 8);
-        wr16(p + 10, 0);        // DOS time 00:00
-        wr16(p + 12, 0x21);     // DOS date 1980-01-01
-        wr32(p + 14, (uint32_t)crc);
-        wr32(p + 18, 0xFFFFFFFFu);
-        wr32(p + 22, 0xFFFFFFFFu);
-        wr16(p + 26, (uint16_t)nl);
-        wr16(p + 28, (uint16_t)xl);
-        std::memcpy(p + 30, names[i], nl - 4);
-        std::memcpy(p + 30 + nl - 4, ".npy", 4);
-        uint8_t* x = p + 30 + nl;
-        wr16(x, 1);
-        wr16(x + 2, 16);
-        wr64(x + 4, raw);
-        wr64(x + 12, comp);
-        x += 20;
-        wr16(x, kIndexId);
-        wr16(x + 2, (uint16_t)(16 + 8 * (nblk + 1)));
-        wr32(x + 4, (uint32_t)nblk);
-        wr32(x + 8, 0);
-        wr64(x + 12, (uint64_t)mblock[i]);
-        uint64_t off = 0;
-        for (int b = 0; b <= nblk; ++b) {
-            wr64(x + 20 + 8 * b, off);
-            if (b < nblk) off += blocks[bi + b].out.size();
-        }
-        p = x + 20 + 8 * (nblk + 1);
-        for (; bi < bj; ++bi) {
-            std::memcpy(p, blocks[bi].out.data(), blocks[bi].out.size());
-            p += blocks[bi].out.size();
-            std::vector<uint8_t>().swap(blocks[bi].out);
-        }
-    }
-    const uint64_t cd_off = (uint64_t)(p - out);
-    for (int i = 0; i < n; ++i) {
-        const size_t nl = std::strlen(names[i]) + 4;
-        if (p + 46 + nl + 28 > lim) return fail(FNPZ_ENOSPC, "fnpz_write: output buffer too small");
-        const uint64_t raw = (uint64_t)(header_lens[i] + nbytes[i]);
-        wr32(p, kCentralSig);
-        wr16(p + 4, 45);
-        wr16(p + 6, 45);
-        wr16(p + 8, 0);
-        wr16(p + 10, 8);
-        wr16(p + 12, 0);
-        wr16(p + 14, 0x21);
-        wr32(p + 16, crcs[i]);
-        wr32(p + 20, 0xFFFFFFFFu);
-        wr32(p + 24, 0xFFFFFFFFu);
-        wr16(p + 28, (uint16_t)nl);
-        wr16(p + 30, 28);
-        wr16(p + 32, 0);
-        wr16(p + 34, 0);
-        wr16(p + 36, 0);
-        wr32(p + 38, 0x01800000u);   // -rw------- (what zipfile writes for numpy)
-        wr32(p + 42, 0xFFFFFFFFu);
-        std::memcpy(p + 46, names[i], nl - 4);
-        std::memcpy(p + 46 + nl - 4, ".npy", 4);
-        uint8_t* x = p + 46 + nl;
-        wr16(x, 1);
-        wr16(x + 2, 24);
-        wr64(x + 4, raw);
-        wr64(x + 12, comps[i]);
-        wr64(x + 20, offs[i]);
-        p = x + 28;
-    }
-    const uint64_t cd_size = (uint64_t)(p - out) - cd_off;
-    if (p + 56 + 20 + 22 > lim) return fail(FNPZ_ENOSPC, "fnpz_write: output buffer too small");
-    const uint64_t z64 = (uint64_t)(p - out);
-    wr32(p, kZ64EocdSig);
-    wr64(p + 4, 44);
-    wr16(p + 12, 45);
-    wr16(p + 14, 45);
-    wr32(p + 16, 0);
-    wr32(p + 20, 0);
-    wr64(p + 24, (uint64_t)n);
-    wr64(p + 32, (uint64_t)n);
-    wr64(p + 40, cd_size);
-    wr64(p + 48, cd_off);
-    p += 56;
-    wr32(p, kZ64LocSig);
-    wr32(p + 4, 0);
-    wr64(p + 8, z64);
-    wr32(p + 16, 1);
-    p += 20;
-    wr32(p, kEocdSig);
-    wr16(p + 4, 0);
-    wr16(p + 6, 0);
-    wr16(p + 8, (uint16_t)std::min(n, 0xFFFF));
-    wr16(p + 10, (uint16_t)std::min(n, 0xFFFF));
-    wr32(p + 12, (uint32_t)std::min<uint64_t>(cd_size, 0xFFFFFFFFu));
-    wr32(p + 16, (uint32_t)std::min<uint64_t>(cd_off, 0xFFFFFFFFu));
-    wr16(p + 20, 0);
-    p += 22;
-    *out_len = (int64_t)(p - out);
-    return FNPZ_OK;
+        wr16(p + 8, (uint16_t)std::min(n, 0xFFFF));
+        wr16(p + 10, (uint16_t)std::min(n, 0xFFFF));
+        wr32(p + 12, (uint32_t)std::min<uint64_t>(cd_size, 0xFFFFFFFFu));
+        wr32(p + 16, (uint32_t)std::min<uint64_t>(cd_off, 0xFFFFFFFFu));
+        wr16(p + 20, 0);
+        p += 22;
+        *out_len = (int64_t)(p - out);
+        return FNPZ_OK;
+    });
 }
 
 int fnpz_stream_open(fnpz_stream** s) {
-    if (!s) return fail(FNPZ_EINVAL, "fnpz_stream_open: bad arguments");
-    *s = new fnpz_stream();
-    return FNPZ_OK;
+    return fnpz_internal::guard("fnpz_stream_open", [&]() -> int {
+        if (!s) return fail(FNPZ_EINVAL, "fnpz_stream_open: bad arguments");
+        *s = new fnpz_stream();
+        return FNPZ_OK;
+    });
 }
 
 void fnpz_stream_close(fnpz_stream* s) { delete s; }
 
 int fnpz_stream_feed(fnpz_stream* s, const uint8_t* data, int64_t len) {
-    if (!s || len < 0 || (len > 0 && !data)) return fail(FNPZ_EINVAL, "fnpz_stream_feed: bad arguments");
-    if (s->pos > 0 && s->pos >= s->in.size() / 2) {      // drop consumed input
-        s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)s->pos);
-        s->pos = 0;
-    }
-    s->in.insert(s->in.end(), data, data + len);
-    return FNPZ_OK;
+    return fnpz_internal::guard("fnpz_stream_feed", [&]() -> int {
+        if (!s || len < 0 || (len > 0 && !data)) return fail(FNPZ_EINVAL, "fnpz_stream_feed: bad arguments");
+        if (s->pos > 0 && s->pos >= s->in.size() / 2) {      // drop consumed input
+            s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)s->pos);
+            s->pos = 0;
+        }
+        s->in.insert(s->in.end(), data, data + len);
+        return FNPZ_OK;
+    });
 }
 
 int fnpz_stream_next(fnpz_stream* s, uint8_t* out, int64_t out_cap, int* event, fnpz_entry* entry, int64_t* out_len) {
-    if (!s || !event || !out_len || (out_cap > 0 && !out)) return fail(FNPZ_EINVAL, "fnpz_stream_next: bad arguments");
-    *out_len = 0;
-    if (s->err) return fail(s->err, "fnpz_stream_next: the stream already failed");
-    for (;;) {
-        switch (s->st) {
-        case fnpz_stream::HDR: {
-            if (s->avail() < 4) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
-            const uint32_t sig = rd32(s->in.data() + s->pos);
-            if (sig == kCentralSig || sig == kEocdSig || sig == kZ64EocdSig || sig == kZ64LocSig) {
-                s->st = fnpz_stream::END;
+    return fnpz_internal::guard("fnpz_stream_next", [&]() -> int {
+        if (!s || !event || !out_len || (out_cap > 0 && !out)) return fail(FNPZ_EINVAL, "fnpz_stream_next: bad arguments");
+        *out_len = 0;
+        if (s->err) return fail(s->err, "fnpz_stream_next: the stream already failed");
+        for (;;) {
+            switch (s->st) {
+            case fnpz_stream::HDR: {
+                if (s->avail() < 4) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+                const uint32_t sig = rd32(s->in.data() + s->pos);
+                if (sig == kCentralSig || sig == kEocdSig || sig == kZ64EocdSig || sig == kZ64LocSig) {
+                    s->st = fnpz_stream::END;
+                    continue;
+                }
+                if (sig != kLocalSig) return sfail(s, FNPZ_EFORMAT, "%s", "not a zip local file header");
+                const int rc = stream_local_header(s);
+                if (rc < 0) return -rc;
+                if (rc == 0) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+                s->st = fnpz_stream::NPY;
                 continue;
             }
-            if (sig != kLocalSig) return sfail(s, FNPZ_EFORMAT, "%s", "not a zip local file header");
-            const int rc = stream_local_header(s);
-            if (rc < 0) return -rc;
-            if (rc == 0) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
-            s->st = fnpz_stream::NPY;
-            continue;
-        }
-        case fnpz_stream::NPY: {
-            if (!entry) return fail(FNPZ_EINVAL, "fnpz_stream_next: a member header needs an entry");
-            const int rc = stream_npy_header(s, entry);
-            if (rc < 0) return -rc;
-            if (rc == 1) {
-                s->st = fnpz_stream::DATA;
-                return *event = FNPZ_EV_MEMBER, FNPZ_OK;
-            }
-            if (s->zend) return sfail(s, FNPZ_ECORRUPT, "%s: truncated .npy header", s->name.c_str());
-            const size_t old = s->pend.size();
-            s->pend.resize(old + 4096);
-            const size_t pos0 = s->pos;
-            const int64_t n = s->produce(s->pend.data() + old, 4096);
-            if (n < 0) return sfail(s, FNPZ_ECORRUPT, "%s: corrupt deflate stream", s->name.c_str());
-            s->pend.resize(old + (size_t)n);
-            if (n == 0 && s->pos == pos0 && !s->zend) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
-            continue;
-        }
-        case fnpz_stream::DATA: {
-            if (s->pend_pos < s->pend.size()) {                // payload inflated with the header
-                const int64_t have = (int64_t)(s->pend.size() - s->pend_pos);
-                if (have > s->left) return sfail(s, FNPZ_EFORMAT, "%s: more data than its .npy header declares", s->name.c_str());
-                const int64_t n = std::min(have, out_cap);
-                if (n == 0) return fail(FNPZ_EINVAL, "fnpz_stream_next: payload pending and no output window");
-                std::memcpy(out, s->pend.data() + s->pend_pos, (size_t)n);
-                s->pend_pos += (size_t)n;
-                s->left -= n;
-                *out_len = n;
-                return *event = FNPZ_EV_DATA, FNPZ_OK;
-            }
-            const size_t pos0 = s->pos;
-            if (s->left > 0) {
-                if (out_cap <= 0) return fail(FNPZ_EINVAL, "fnpz_stream_next: payload pending and no output window");
-                if (s->zend) return sfail(s, FNPZ_ECORRUPT, "%s: member shorter than its .npy header declares", s->name.c_str());
-                const int64_t n = s->produce(out, std::min(out_cap, s->left));
+            case fnpz_stream::NPY: {
+                if (!entry) return fail(FNPZ_EINVAL, "fnpz_stream_next: a member header needs an entry");
+                const int rc = stream_npy_header(s, entry);
+                if (rc < 0) return -rc;
+                if (rc == 1) {
+                    s->st = fnpz_stream::DATA;
+                    return *event = FNPZ_EV_MEMBER, FNPZ_OK;
+                }
+                if (s->zend) return sfail(s, FNPZ_ECORRUPT, "%s: truncated .npy header", s->name.c_str());
+                const size_t old = s->pend.size();
+                s->pend.resize(old + 4096);
+                const size_t pos0 = s->pos;
+                const int64_t n = s->produce(s->pend.data() + old, 4096);
                 if (n < 0) return sfail(s, FNPZ_ECORRUPT, "%s: corrupt deflate stream", s->name.c_str());
-                if (n > 0) {
+                s->pend.resize(old + (size_t)n);
+                if (n == 0 && s->pos == pos0 && !s->zend) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+                continue;
+            }
+            case fnpz_stream::DATA: {
+                if (s->pend_pos < s->pend.size()) {                // payload inflated with the header
+                    const int64_t have = (int64_t)(s->pend.size() - s->pend_pos);
+                    if (have > s->left) return sfail(s, FNPZ_EFORMAT, "%s: more data than its .npy header declares", s->name.c_str());
+                    const int64_t n = std::min(have, out_cap);
+                    if (n == 0) return fail(FNPZ_EINVAL, "fnpz_stream_next: payload pending and no output window");
+                    std::memcpy(out, s->pend.data() + s->pend_pos, (size_t)n);
+                    s->pend_pos += (size_t)n;
                     s->left -= n;
                     *out_len = n;
                     return *event = FNPZ_EV_DATA, FNPZ_OK;
                 }
-                if (s->pos == pos0 && !s->zend) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
-                continue;
-            }
-            if (!s->zend) {                                    // payload complete: the stream must end here
-                uint8_t extra;
-                const int64_t n = s->produce(&extra, 1);
-                if (n < 0) return sfail(s, FNPZ_ECORRUPT, "%s: corrupt deflate stream", s->name.c_str());
-                if (n > 0) return sfail(s, FNPZ_EFORMAT, "%s: more data than its .npy header declares", s->name.c_str());
-                if (!s->zend) {
-                    if (s->pos == pos0) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+                const size_t pos0 = s->pos;
+                if (s->left > 0) {
+                    if (out_cap <= 0) return fail(FNPZ_EINVAL, "fnpz_stream_next: payload pending and no output window");
+                    if (s->zend) return sfail(s, FNPZ_ECORRUPT, "%s: member shorter than its .npy header declares", s->name.c_str());
+                    const int64_t n = s->produce(out, std::min(out_cap, s->left));
+                    if (n < 0) return sfail(s, FNPZ_ECORRUPT, "%s: corrupt deflate stream", s->name.c_str());
+                    if (n > 0) {
+                        s->left -= n;
+                        *out_len = n;
+                        return *event = FNPZ_EV_DATA, FNPZ_OK;
+                    }
+                    if (s->pos == pos0 && !s->zend) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
                     continue;
                 }
+                if (!s->zend) {                                    // payload complete: the stream must end here
+                    uint8_t extra;
+                    const int64_t n = s->produce(&extra, 1);
+                    if (n < 0) return sfail(s, FNPZ_ECORRUPT, "%s: corrupt deflate stream", s->name.c_str());
+                    if (n > 0) return sfail(s, FNPZ_EFORMAT, "%s: more data than its .npy header declares", s->name.c_str());
+                    if (!s->zend) {
+                        if (s->pos == pos0) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+                        continue;
+                    }
+                }
+                if (s->flags & 8) {
+                    s->st = fnpz_stream::DESC;
+                    continue;
+                }
+                if ((uint32_t)s->crc != s->crc_want) return sfail(s, FNPZ_ECORRUPT, "%s: CRC-32 mismatch", s->name.c_str());
+                s->st = fnpz_stream::HDR;
+                return *event = FNPZ_EV_MEMBER_END, FNPZ_OK;
             }
-            if (s->flags & 8) {
-                s->st = fnpz_stream::DESC;
-                continue;
+            case fnpz_stream::DESC: {
+                if (s->avail() < 4) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+                const bool has_sig = rd32(s->in.data() + s->pos) == kDescSig;
+                const size_t size = (has_sig ? 4 : 0) + 4 + (s->zip64 ? 16 : 8);
+                if (s->avail() < size) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
+                const uint32_t crc = rd32(s->in.data() + s->pos + (has_sig ? 4 : 0));
+                s->pos += size;
+                if ((uint32_t)s->crc != crc) return sfail(s, FNPZ_ECORRUPT, "%s: CRC-32 mismatch", s->name.c_str());
+                s->st = fnpz_stream::HDR;
+                return *event = FNPZ_EV_MEMBER_END, FNPZ_OK;
             }
-            if ((uint32_t)s->crc != s->crc_want) return sfail(s, FNPZ_ECORRUPT, "%s: CRC-32 mismatch", s->name.c_str());
-            s->st = fnpz_stream::HDR;
-            return *event = FNPZ_EV_MEMBER_END, FNPZ_OK;
+            case fnpz_stream::END:
+                return *event = FNPZ_EV_END, FNPZ_OK;
+            }
         }
-        case fnpz_stream::DESC: {
-            if (s->avail() < 4) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
-            const bool has_sig = rd32(s->in.data() + s->pos) == kDescSig;
-            const size_t size = (has_sig ? 4 : 0) + 4 + (s->zip64 ? 16 : 8);
-            if (s->avail() < size) return *event = FNPZ_EV_NEED_INPUT, FNPZ_OK;
-            const uint32_t crc = rd32(s->in.data() + s->pos + (has_sig ? 4 : 0));
-            s->pos += size;
-            if ((uint32_t)s->crc != crc) return sfail(s, FNPZ_ECORRUPT, "%s: CRC-32 mismatch", s->name.c_str());
-            s->st = fnpz_stream::HDR;
-            return *event = FNPZ_EV_MEMBER_END, FNPZ_OK;
-        }
-        case fnpz_stream::END:
-            return *event = FNPZ_EV_END, FNPZ_OK;
-        }
-    }
+    });
 }
 
 }  // extern "C"
@@ -1427,7 +1441,11 @@ class CopyPool {
         Job job{&f, n, &next};
         {
             std::lock_guard<std::mutex> lk(mu_);
-            while ((int)workers_.size() < threads - 1) workers_.emplace_back([this] { work(); });
+            try {
+                while ((int)workers_.size() < threads - 1) workers_.emplace_back([this] { work(); });
+            } catch (...) {
+                // no more threads: the parked ones and the caller copy
+            }
             job_ = &job;
             ++gen_;
         }
@@ -1585,8 +1603,8 @@ static int check_window(const char* who, int n, void* const* dsts, const int64_t
     return FNPZ_OK;
 }
 
-extern "C" int64_t fnpz_gather_start(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes,
-                                     int threads, const void* dst_lo, int64_t dst_len) {
+static int64_t gather_start(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes, int threads,
+                            const void* dst_lo, int64_t dst_len) {
     if (n < 0 || (n > 0 && (!dsts || !srcs || !nbytes)) || threads < 1)
         return -fail(FNPZ_EINVAL, "fnpz_gather_start: bad arguments");
     for (int i = 0; i < n; ++i)
@@ -1604,41 +1622,55 @@ extern "C" int64_t fnpz_gather_start(int n, void* const* dsts, const void* const
     return GatherQueue::get().submit(std::move(pieces), threads);
 }
 
+extern "C" int64_t fnpz_gather_start(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes,
+                                     int threads, const void* dst_lo, int64_t dst_len) {
+    int64_t ticket = 0;
+    const int rc = fnpz_internal::guard("fnpz_gather_start", [&]() -> int {
+        ticket = gather_start(n, dsts, srcs, nbytes, threads, dst_lo, dst_len);
+        return ticket < 0 ? (int)-ticket : FNPZ_OK;
+    });
+    return rc ? -(int64_t)rc : ticket;
+}
+
 extern "C" int fnpz_gather_wait(int64_t ticket) {
-    if (ticket <= 0) return fail(FNPZ_EINVAL, "fnpz_gather_wait: bad ticket %lld", (long long)ticket);
-    GatherQueue::get().wait(ticket);
-    return FNPZ_OK;
+    return fnpz_internal::guard("fnpz_gather_wait", [&]() -> int {
+        if (ticket <= 0) return fail(FNPZ_EINVAL, "fnpz_gather_wait: bad ticket %lld", (long long)ticket);
+        GatherQueue::get().wait(ticket);
+        return FNPZ_OK;
+    });
 }
 
 extern "C" int fnpz_gather(int n, void* const* dsts, const void* const* srcs, const int64_t* nbytes, int threads,
                            const void* dst_lo, int64_t dst_len) {
-    if (n < 0 || (n > 0 && (!dsts || !srcs || !nbytes)) || threads < 1)
-        return fail(FNPZ_EINVAL, "fnpz_gather: bad arguments");
-    int64_t total = 0;
-    for (int i = 0; i < n; ++i) {
-        if (nbytes[i] < 0 || (nbytes[i] > 0 && (!dsts[i] || !srcs[i]))) return fail(FNPZ_EINVAL, "fnpz_gather: segment %d", i);
-        total += nbytes[i];
-    }
-    if (int rc = check_window("fnpz_gather", n, dsts, nbytes, dst_lo, dst_len)) return rc;
-    if (total == 0) return FNPZ_OK;
-    struct Piece {
-        uint8_t* d;
-        const uint8_t* s;
-        int64_t len;
-    };
-    const int64_t piece = std::max<int64_t>(1 << 20, (total + 2 * threads - 1) / (2 * threads));
-    std::vector<Piece> pieces;
-    for (int i = 0; i < n; ++i)
-        for (int64_t o = 0; o < nbytes[i]; o += piece)
-            pieces.push_back({static_cast<uint8_t*>(dsts[i]) + o, static_cast<const uint8_t*>(srcs[i]) + o,
-                              std::min(piece, nbytes[i] - o)});
-    const int np = (int)pieces.size();
-    auto copy = [&](int k) { std::memcpy(pieces[k].d, pieces[k].s, (size_t)pieces[k].len); };
-    const int t = std::min(threads, np);
-    if (t <= 1) {
-        for (int k = 0; k < np; ++k) copy(k);
+    return fnpz_internal::guard("fnpz_gather", [&]() -> int {
+        if (n < 0 || (n > 0 && (!dsts || !srcs || !nbytes)) || threads < 1)
+            return fail(FNPZ_EINVAL, "fnpz_gather: bad arguments");
+        int64_t total = 0;
+        for (int i = 0; i < n; ++i) {
+            if (nbytes[i] < 0 || (nbytes[i] > 0 && (!dsts[i] || !srcs[i]))) return fail(FNPZ_EINVAL, "fnpz_gather: segment %d", i);
+            total += nbytes[i];
+        }
+        if (int rc = check_window("fnpz_gather", n, dsts, nbytes, dst_lo, dst_len)) return rc;
+        if (total == 0) return FNPZ_OK;
+        struct Piece {
+            uint8_t* d;
+            const uint8_t* s;
+            int64_t len;
+        };
+        const int64_t piece = std::max<int64_t>(1 << 20, (total + 2 * threads - 1) / (2 * threads));
+        std::vector<Piece> pieces;
+        for (int i = 0; i < n; ++i)
+            for (int64_t o = 0; o < nbytes[i]; o += piece)
+                pieces.push_back({static_cast<uint8_t*>(dsts[i]) + o, static_cast<const uint8_t*>(srcs[i]) + o,
+                                  std::min(piece, nbytes[i] - o)});
+        const int np = (int)pieces.size();
+        auto copy = [&](int k) { std::memcpy(pieces[k].d, pieces[k].s, (size_t)pieces[k].len); };
+        const int t = std::min(threads, np);
+        if (t <= 1) {
+            for (int k = 0; k < np; ++k) copy(k);
+            return FNPZ_OK;
+        }
+        CopyPool::get().run(t, np, copy);
         return FNPZ_OK;
-    }
-    CopyPool::get().run(t, np, copy);
-    return FNPZ_OK;
+    });
 }

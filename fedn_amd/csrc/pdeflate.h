@@ -38,6 +38,8 @@
 #include <thread>
 #include <vector>
 
+#include "fnpz_guard.h"
+
 namespace pdef {
 
 // ---- zlib 1.2.11 constants (deflate.h, deflate.c configuration_table[6], trees.c) ----------------
@@ -1090,16 +1092,8 @@ struct Encoder {
 
 // ---- driver ----------------------------------------------------------------------------------------
 template <class F>
-inline void parallel(int n, int threads, F&& f) {
-    threads = std::max(1, std::min(threads, n));
-    std::atomic<int> next{0};
-    auto work = [&] {
-        for (int i; (i = next.fetch_add(1)) < n;) f(i);
-    };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < threads; ++t) pool.emplace_back(work);
-    work();
-    for (auto& th : pool) th.join();
+inline void parallel(int n, int threads, F&& f) {   // a worker's exception is rethrown here
+    fnpz_internal::run_parallel(n, threads, std::forward<F>(f));
 }
 
 struct Stats {

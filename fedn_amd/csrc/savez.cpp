@@ -25,12 +25,10 @@
 #include <vector>
 
 #include "../../include/fednpz.h"
+#include "fnpz_guard.h"
 #include "inflate.h"
 #include "pdeflate.h"
 
-namespace fnpz_internal {
-int set_error(int code, const char* fmt, ...);
-}
 
 namespace {
 
@@ -157,157 +155,150 @@ void deflate_member(Member& m) {
 extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const* headers, const int64_t* header_lens,
                           const void* const* datas, const int64_t* nbytes, const int64_t* seg_bytes, int threads,
                           uint8_t* out, int64_t out_cap, int64_t* out_len) {
-    if (n < 0 || !out || !out_len || (n > 0 && (!names || !headers || !header_lens || !datas || !nbytes)))
-        return set_error(FNPZ_EINVAL, "fnpz_savez: bad arguments");
-    std::vector<Member> ms((size_t)n);
-    for (int i = 0; i < n; ++i) {
-        const size_t nl = std::strlen(names[i]);
-        if (nl + 4 > 0xFFFF || header_lens[i] < 0 || nbytes[i] < 0 || (nbytes[i] > 0 && !datas[i]))
-            return set_error(FNPZ_EINVAL, "fnpz_savez: bad member %d", i);
-        ms[i] = Member{names[i], headers[i], header_lens[i], static_cast<const uint8_t*>(datas[i]), nbytes[i],
-                       seg_bytes ? seg_bytes[i] : 0};
-    }
-    // big members one after another on every thread (pdeflate.h); the rest member-parallel, largest
-    // first so one long stream does not start last. Big: at least min_member bytes, or at least four
-    // chunks and more than an even share of the archive per thread (member-parallel, that member
-    // alone would outlast the rest of the archive spread over the other threads)
-    int64_t total = 0;
-    for (const Member& m : ms) total += m.hlen + m.nbytes;
-    const int64_t floor = 4 * g_par_chunk.load();
-    std::vector<int> order;
-    for (int i = 0; i < n; ++i) {
-        const int64_t sz = ms[i].hlen + ms[i].nbytes;
-        if (threads > 1 && (sz >= g_par_min.load() || (sz >= floor && sz * threads > total))) {
-            if (!deflate_member_parallel(ms[i], threads)) deflate_member(ms[i]);
-        } else {
-            order.push_back(i);
+    return fnpz_internal::guard("fnpz_savez", [&]() -> int {
+        if (n < 0 || !out || !out_len || (n > 0 && (!names || !headers || !header_lens || !datas || !nbytes)))
+            return set_error(FNPZ_EINVAL, "fnpz_savez: bad arguments");
+        std::vector<Member> ms((size_t)n);
+        for (int i = 0; i < n; ++i) {
+            const size_t nl = std::strlen(names[i]);
+            if (nl + 4 > 0xFFFF || header_lens[i] < 0 || nbytes[i] < 0 || (nbytes[i] > 0 && !datas[i]))
+                return set_error(FNPZ_EINVAL, "fnpz_savez: bad member %d", i);
+            ms[i] = Member{names[i], headers[i], header_lens[i], static_cast<const uint8_t*>(datas[i]), nbytes[i],
+                           seg_bytes ? seg_bytes[i] : 0};
         }
-    }
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return ms[a].nbytes > ms[b].nbytes; });
-    const int nrest = (int)order.size();
-    std::atomic<int> next{0};
-    auto work = [&] {
-        for (int k; (k = next.fetch_add(1)) < nrest;) deflate_member(ms[order[k]]);
-    };
-    const int nt = std::max(1, std::min(threads, nrest));
-    std::vector<std::thread> pool;
-    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
-    work();
-    for (auto& th : pool) th.join();
-    for (int i = 0; i < n; ++i)
-        if (ms[i].rc != Z_OK) return set_error(FNPZ_ECORRUPT, "fnpz_savez: deflate failed on member %d", i);
+        // big members one after another on every thread (pdeflate.h); the rest member-parallel, largest
+        // first so one long stream does not start last. Big: at least min_member bytes, or at least four
+        // chunks and more than an even share of the archive per thread (member-parallel, that member
+        // alone would outlast the rest of the archive spread over the other threads)
+        int64_t total = 0;
+        for (const Member& m : ms) total += m.hlen + m.nbytes;
+        const int64_t floor = 4 * g_par_chunk.load();
+        std::vector<int> order;
+        for (int i = 0; i < n; ++i) {
+            const int64_t sz = ms[i].hlen + ms[i].nbytes;
+            if (threads > 1 && (sz >= g_par_min.load() || (sz >= floor && sz * threads > total))) {
+                if (!deflate_member_parallel(ms[i], threads)) deflate_member(ms[i]);
+            } else {
+                order.push_back(i);
+            }
+        }
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return ms[a].nbytes > ms[b].nbytes; });
+        fnpz_internal::run_parallel((int)order.size(), std::max(1, threads), [&](int k) { deflate_member(ms[order[k]]); });
+        for (int i = 0; i < n; ++i)
+            if (ms[i].rc != Z_OK) return set_error(FNPZ_ECORRUPT, "fnpz_savez: deflate failed on member %d", i);
 
-    uint8_t* p = out;
-    uint8_t* const lim = out + out_cap;
-    const uint64_t zip64_limit = g_zip64_limit.load(), filecount_limit = g_filecount_limit.load();
-    std::vector<uint64_t> offs((size_t)n);
-    std::vector<uint64_t> comps((size_t)n);
-    std::vector<uint16_t> ver((size_t)n);
-    for (int i = 0; i < n; ++i) {
-        const Member& m = ms[i];
-        const size_t nl = std::strlen(m.name) + 4;
-        const uint64_t raw = (uint64_t)(m.hlen + m.nbytes), comp = m.out.size();
-        if ((int64_t)(30 + nl + 20 + comp) > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
-        // ZipInfo.FileHeader(zip64=True) as _ZipWriteFile.close rewrites it
-        const bool big = raw > zip64_limit || comp > zip64_limit;
-        ver[i] = big ? kZip64Version : kDefaultVersion;
-        offs[i] = (uint64_t)(p - out);
-        comps[i] = comp;
-        put32(p, 0x04034b50);
-        put16(p, ver[i]);
-        put16(p, 0);                        // flag bits (seekable output: no data descriptor)
-        put16(p, Z_DEFLATED);
-        put16(p, 0);                        // DOS time
-        put16(p, kDosDate);
-        put32(p, m.crc);
-        put32(p, big ? 0xFFFFFFFFu : (uint32_t)comp);
-        put32(p, big ? 0xFFFFFFFFu : (uint32_t)raw);
-        put16(p, (uint16_t)nl);
-        put16(p, 20);
-        std::memcpy(p, m.name, nl - 4);
-        std::memcpy(p + nl - 4, ".npy", 4);
-        p += nl;
-        put16(p, 1);
-        put16(p, 16);
-        put64(p, raw);
-        put64(p, comp);
-        std::memcpy(p, m.out.data(), comp);
-        p += comp;
-        std::vector<uint8_t>().swap(ms[i].out);
-    }
-    const uint64_t cd_off = (uint64_t)(p - out);
-    for (int i = 0; i < n; ++i) {   // ZipFile._write_end_record
-        const Member& m = ms[i];
-        const size_t nl = std::strlen(m.name) + 4;
-        const uint64_t raw = (uint64_t)(m.hlen + m.nbytes);
-        const uint64_t csize = comps[i];
-        uint64_t extra[3];
-        int ne = 0;
-        const bool big = raw > zip64_limit || csize > zip64_limit;
-        if (big) extra[ne++] = raw, extra[ne++] = csize;
-        if (offs[i] > zip64_limit) extra[ne++] = offs[i];
-        const uint16_t v = ne ? std::max<uint16_t>(kZip64Version, ver[i]) : ver[i];
-        if ((int64_t)(46 + nl + 4 + 8 * ne) > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
-        put32(p, 0x02014b50);
-        put16(p, (uint16_t)(v | (3 << 8)));  // create_version | create_system (unix)
-        put16(p, v);                          // extract_version
-        put16(p, 0);
-        put16(p, Z_DEFLATED);
-        put16(p, 0);
-        put16(p, kDosDate);
-        put32(p, m.crc);
-        put32(p, big ? 0xFFFFFFFFu : (uint32_t)csize);
-        put32(p, big ? 0xFFFFFFFFu : (uint32_t)raw);
-        put16(p, (uint16_t)nl);
-        put16(p, (uint16_t)(ne ? 4 + 8 * ne : 0));
-        put16(p, 0);                          // comment
-        put16(p, 0);                          // disk number start
-        put16(p, 0);                          // internal attributes
-        put32(p, kExternalAttr);
-        put32(p, offs[i] > zip64_limit ? 0xFFFFFFFFu : (uint32_t)offs[i]);
-        std::memcpy(p, m.name, nl - 4);
-        std::memcpy(p + nl - 4, ".npy", 4);
-        p += nl;
-        if (ne) {
+        uint8_t* p = out;
+        uint8_t* const lim = out + out_cap;
+        const uint64_t zip64_limit = g_zip64_limit.load(), filecount_limit = g_filecount_limit.load();
+        std::vector<uint64_t> offs((size_t)n);
+        std::vector<uint64_t> comps((size_t)n);
+        std::vector<uint16_t> ver((size_t)n);
+        for (int i = 0; i < n; ++i) {
+            const Member& m = ms[i];
+            const size_t nl = std::strlen(m.name) + 4;
+            const uint64_t raw = (uint64_t)(m.hlen + m.nbytes), comp = m.out.size();
+            if ((int64_t)(30 + nl + 20 + comp) > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
+            // ZipInfo.FileHeader(zip64=True) as _ZipWriteFile.close rewrites it
+            const bool big = raw > zip64_limit || comp > zip64_limit;
+            ver[i] = big ? kZip64Version : kDefaultVersion;
+            offs[i] = (uint64_t)(p - out);
+            comps[i] = comp;
+            put32(p, 0x04034b50);
+            put16(p, ver[i]);
+            put16(p, 0);                        // flag bits (seekable output: no data descriptor)
+            put16(p, Z_DEFLATED);
+            put16(p, 0);                        // DOS time
+            put16(p, kDosDate);
+            put32(p, m.crc);
+            put32(p, big ? 0xFFFFFFFFu : (uint32_t)comp);
+            put32(p, big ? 0xFFFFFFFFu : (uint32_t)raw);
+            put16(p, (uint16_t)nl);
+            put16(p, 20);
+            std::memcpy(p, m.name, nl - 4);
+            std::memcpy(p + nl - 4, ".npy", 4);
+            p += nl;
             put16(p, 1);
-            put16(p, (uint16_t)(8 * ne));
-            for (int k = 0; k < ne; ++k) put64(p, extra[k]);
+            put16(p, 16);
+            put64(p, raw);
+            put64(p, comp);
+            std::memcpy(p, m.out.data(), comp);
+            p += comp;
+            std::vector<uint8_t>().swap(ms[i].out);
         }
-    }
-    const uint64_t pos2 = (uint64_t)(p - out);
-    const uint64_t cd_size = pos2 - cd_off;
-    uint64_t count = (uint64_t)n, size = cd_size, offset = cd_off;
-    if (count > filecount_limit || cd_off > zip64_limit || cd_size > zip64_limit) {
-        if (56 + 20 > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
-        put32(p, 0x06064b50);
-        put64(p, 44);
-        put16(p, kZip64Version);
-        put16(p, kZip64Version);
-        put32(p, 0);
-        put32(p, 0);
-        put64(p, count);
-        put64(p, count);
-        put64(p, cd_size);
-        put64(p, cd_off);
-        put32(p, 0x07064b50);
-        put32(p, 0);
-        put64(p, pos2);
-        put32(p, 1);
-        count = std::min<uint64_t>(count, 0xFFFF);
-        size = std::min<uint64_t>(size, 0xFFFFFFFFu);
-        offset = std::min<uint64_t>(offset, 0xFFFFFFFFu);
-    }
-    if (22 > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
-    put32(p, 0x06054b50);
-    put16(p, 0);
-    put16(p, 0);
-    put16(p, (uint16_t)count);
-    put16(p, (uint16_t)count);
-    put32(p, (uint32_t)size);
-    put32(p, (uint32_t)offset);
-    put16(p, 0);
-    *out_len = (int64_t)(p - out);
-    return FNPZ_OK;
+        const uint64_t cd_off = (uint64_t)(p - out);
+        for (int i = 0; i < n; ++i) {   // ZipFile._write_end_record
+            const Member& m = ms[i];
+            const size_t nl = std::strlen(m.name) + 4;
+            const uint64_t raw = (uint64_t)(m.hlen + m.nbytes);
+            const uint64_t csize = comps[i];
+            uint64_t extra[3];
+            int ne = 0;
+            const bool big = raw > zip64_limit || csize > zip64_limit;
+            if (big) extra[ne++] = raw, extra[ne++] = csize;
+            if (offs[i] > zip64_limit) extra[ne++] = offs[i];
+            const uint16_t v = ne ? std::max<uint16_t>(kZip64Version, ver[i]) : ver[i];
+            if ((int64_t)(46 + nl + 4 + 8 * ne) > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
+            put32(p, 0x02014b50);
+            put16(p, (uint16_t)(v | (3 << 8)));  // create_version | create_system (unix)
+            put16(p, v);                          // extract_version
+            put16(p, 0);
+            put16(p, Z_DEFLATED);
+            put16(p, 0);
+            put16(p, kDosDate);
+            put32(p, m.crc);
+            put32(p, big ? 0xFFFFFFFFu : (uint32_t)csize);
+            put32(p, big ? 0xFFFFFFFFu : (uint32_t)raw);
+            put16(p, (uint16_t)nl);
+            put16(p, (uint16_t)(ne ? 4 + 8 * ne : 0));
+            put16(p, 0);                          // comment
+            put16(p, 0);                          // disk number start
+            put16(p, 0);                          // internal attributes
+            put32(p, kExternalAttr);
+            put32(p, offs[i] > zip64_limit ? 0xFFFFFFFFu : (uint32_t)offs[i]);
+            std::memcpy(p, m.name, nl - 4);
+            std::memcpy(p + nl - 4, ".npy", 4);
+            p += nl;
+            if (ne) {
+                put16(p, 1);
+                put16(p, (uint16_t)(8 * ne));
+                for (int k = 0; k < ne; ++k) put64(p, extra[k]);
+            }
+        }
+        const uint64_t pos2 = (uint64_t)(p - out);
+        const uint64_t cd_size = pos2 - cd_off;
+        uint64_t count = (uint64_t)n, size = cd_size, offset = cd_off;
+        if (count > filecount_limit || cd_off > zip64_limit || cd_size > zip64_limit) {
+            if (56 + 20 > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
+            put32(p, 0x06064b50);
+            put64(p, 44);
+            put16(p, kZip64Version);
+            put16(p, kZip64Version);
+            put32(p, 0);
+            put32(p, 0);
+            put64(p, count);
+            put64(p, count);
+            put64(p, cd_size);
+            put64(p, cd_off);
+            put32(p, 0x07064b50);
+            put32(p, 0);
+            put64(p, pos2);
+            put32(p, 1);
+            count = std::min<uint64_t>(count, 0xFFFF);
+            size = std::min<uint64_t>(size, 0xFFFFFFFFu);
+            offset = std::min<uint64_t>(offset, 0xFFFFFFFFu);
+        }
+        if (22 > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
+        put32(p, 0x06054b50);
+        put16(p, 0);
+        put16(p, 0);
+        put16(p, (uint16_t)count);
+        put16(p, (uint16_t)count);
+        put32(p, (uint32_t)size);
+        put32(p, (uint32_t)offset);
+        put16(p, 0);
+        *out_len = (int64_t)(p - out);
+        return FNPZ_OK;
+    });
 }
 
 extern "C" void fnpz_savez_config(int64_t min_member, int64_t chunk, int64_t* parallel, int64_t* fallback) {
@@ -324,20 +315,22 @@ extern "C" void fnpz_savez_zip_limits(int64_t zip64_limit, int64_t filecount_lim
 
 extern "C" int fnpz_deflate_exact(const uint8_t* in, int64_t len, const int64_t* ends, int nends, int threads,
                                   int64_t chunk, uint8_t* out, int64_t out_cap, int64_t* out_len) {
-    if (!in || len <= 0 || !ends || nends <= 0 || !out || !out_len || ends[nends - 1] != len)
-        return set_error(FNPZ_EINVAL, "fnpz_deflate_exact: bad arguments");
-    std::vector<int64_t> e(ends, ends + nends);
-    std::vector<uint8_t> res;
-    pdef::Stats st;
-    if (!pdef::deflate_exact(in, len, e, std::max(1, threads), chunk, res, &st))
-        return set_error(FNPZ_EFALLBACK, "fnpz_deflate_exact: %s", st.fallback ? st.fallback : "fallback");
-    if ((int64_t)res.size() > out_cap) return set_error(FNPZ_ENOSPC, "fnpz_deflate_exact: output buffer too small");
-    std::memcpy(out, res.data(), res.size());
-    *out_len = (int64_t)res.size();
-    set_error(FNPZ_OK, "chunks %d fixups %d blocks %d tail_from %lld parse %.3f sync %.3f sched %.3f plan %.3f encode %.3f",
-              st.chunks, st.fixups, st.blocks, (long long)st.tail_from, st.t_parse, st.t_sync, st.t_sched, st.t_plan,
-              st.t_encode);
-    return FNPZ_OK;
+    return fnpz_internal::guard("fnpz_deflate_exact", [&]() -> int {
+        if (!in || len <= 0 || !ends || nends <= 0 || !out || !out_len || ends[nends - 1] != len)
+            return set_error(FNPZ_EINVAL, "fnpz_deflate_exact: bad arguments");
+        std::vector<int64_t> e(ends, ends + nends);
+        std::vector<uint8_t> res;
+        pdef::Stats st;
+        if (!pdef::deflate_exact(in, len, e, std::max(1, threads), chunk, res, &st))
+            return set_error(FNPZ_EFALLBACK, "fnpz_deflate_exact: %s", st.fallback ? st.fallback : "fallback");
+        if ((int64_t)res.size() > out_cap) return set_error(FNPZ_ENOSPC, "fnpz_deflate_exact: output buffer too small");
+        std::memcpy(out, res.data(), res.size());
+        *out_len = (int64_t)res.size();
+        set_error(FNPZ_OK, "chunks %d fixups %d blocks %d tail_from %lld parse %.3f sync %.3f sched %.3f plan %.3f encode %.3f",
+                  st.chunks, st.fixups, st.blocks, (long long)st.tail_from, st.t_parse, st.t_sync, st.t_sched, st.t_plan,
+                  st.t_encode);
+        return FNPZ_OK;
+    });
 }
 
 // the parallel decoder's block-header pre-check (inflate.h Inflate::maybe_dynamic_header), for tests

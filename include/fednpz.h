@@ -27,7 +27,11 @@ extern "C" {
 #define FNPZ_ABI_VERSION 6
 #define FNPZ_MAX_DIMS 64   /* numpy 2's NPY_MAXDIMS (ABI 6; 16 before) */
 
-enum fnpz_status { FNPZ_OK = 0, FNPZ_EFORMAT = 1, FNPZ_ECORRUPT = 2, FNPZ_EINVAL = 3, FNPZ_ENOSPC = 4, FNPZ_EFALLBACK = 5 };
+/* Every entry point returns a status; no C++ exception leaves the library. FNPZ_ENOMEM (ABI 6):
+ * memory or a worker thread could not be had inside the call — nothing was returned, and the
+ * library stays usable (fnpz_last_error() says which). */
+enum fnpz_status { FNPZ_OK = 0, FNPZ_EFORMAT = 1, FNPZ_ECORRUPT = 2, FNPZ_EINVAL = 3, FNPZ_ENOSPC = 4, FNPZ_EFALLBACK = 5,
+                   FNPZ_ENOMEM = 6 };
 
 /* One archive member holding a .npy array. */
 typedef struct {
