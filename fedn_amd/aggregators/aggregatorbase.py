@@ -242,8 +242,23 @@ class AggregatorBase(ABC):
         while len(waiting) > keep:
             mu = waiting.popleft()
             if delete_models:
-                self.update_handler.delete_model(mu)
+                try:
+                    self.update_handler.delete_model(mu)
+                except Exception as e:  # noqa: BLE001 — inside the per-update try in the reference
+                    self._log_skip(e, traceback.format_exc())   # (fedavg.py:73-78): logged, still counted
         return len(skipped)
+
+    def _finish_deletes(self):
+        """Wait for the store deletes an update handler runs side by side
+        (ingest.StagingUpdateHandler.finish_deletes): every folded update is deleted when
+        combine_models returns, as in the reference; one that raised is logged as fedavg.py:75-78
+        logs it."""
+        fin = getattr(self.update_handler, "finish_deletes", None)
+        if fin is None:
+            return
+        import traceback
+        for _mu, exc in fin():
+            self._log_skip(exc, "".join(traceback.format_exception(type(exc), exc, exc.__traceback__)))
 
     def _log_skip(self, exc, tb):
         import logging

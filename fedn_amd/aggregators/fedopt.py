@@ -89,6 +89,8 @@ class Aggregator(AggregatorBase):
             pipe, self._live = getattr(self, "_live", None), None
             if pipe is not None and hasattr(pipe, "quiesce"):
                 pipe.quiesce()
+            # the round's store deletes (run side by side by the staging handler) are all done
+            self._finish_deletes()
 
     def _combine(self, helper, delete_models, parameters):
         data = {"time_model_load": 0.0, "time_model_aggregation": 0.0}

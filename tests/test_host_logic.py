@@ -550,8 +550,9 @@ def test_temp_file_store_mirrors_tempmodelstorage(tmp_path):
 
 
 def test_delete_model_hands_own_copies_to_the_reaper():
-    """StagingUpdateHandler.delete_model: the wrapped handler's delete inline (the store's), this
-    handler's own copies of the update dropped on the reaper thread; both parts timed."""
+    """StagingUpdateHandler.delete_model: this handler's own copies of the update dropped on the
+    reaper thread; the wrapped handler's delete (the store's) done by close() at the latest; both
+    parts timed."""
     import gc
     import threading
     import weakref
@@ -577,4 +578,84 @@ def test_delete_model_hands_own_copies_to_the_reaper():
     gc.collect()
     assert freed_on == ["fedn_amd_reaper"]
     assert st.delete_times["count"] == 1 and st.delete_times["store_s"] >= 0 and st.delete_times["plugin_s"] >= 0
-    assert uh.store.get(mu.model_update_id) is None           # the store's delete ran inline
+    assert uh.store.get(mu.model_update_id) is None           # the store's delete has run
+
+
+class _SlowStoreHandler:
+    """A wrapped UpdateHandler whose store delete takes ``delay`` seconds (os.remove of a large
+    file) and raises for the ids in ``bad``."""
+
+    def __init__(self, delay, bad=()):
+        import threading
+        self.delay, self.bad = delay, set(bad)
+        self.deleted, self.threads = [], set()
+        self._lock = threading.Lock()
+
+    def delete_model(self, mu):
+        import threading
+        import time
+        time.sleep(self.delay)
+        if mu.model_update_id in self.bad:
+            raise OSError(f"cannot delete {mu.model_update_id}")
+        with self._lock:
+            self.deleted.append(mu.model_update_id)
+            self.threads.add(threading.current_thread().name)
+
+
+def _mus(n):
+    from types import SimpleNamespace
+    return [SimpleNamespace(model_update_id=f"u{i}") for i in range(n)]
+
+
+@pytest.mark.parametrize("workers", [0, 4])
+def test_store_deletes_run_side_by_side_and_finish_before_the_round_ends(workers):
+    """delete_workers > 0: the round's store deletes (tempmodelstorage.py:66-76, inline in
+    fedavg.py:73-74) run concurrently; finish_deletes — what the aggregators call before
+    combine_models returns — waits for every one, so the storage state at return is the
+    reference's. delete_workers = 0: one after another inside delete_model, as the reference."""
+    import time
+
+    from fedn_amd.ingest import StagingUpdateHandler
+    inner = _SlowStoreHandler(0.15)
+    st = StagingUpdateHandler(inner, helper=None, device="cpu", workers=1, delete_workers=workers)
+    mus = _mus(4)
+    t0 = time.perf_counter()
+    for mu in mus:
+        st.delete_model(mu)
+    issued = time.perf_counter() - t0
+    assert st.finish_deletes() == []
+    total = time.perf_counter() - t0
+    assert sorted(inner.deleted) == ["u0", "u1", "u2", "u3"]      # all done at "return"
+    if workers:
+        assert issued < 0.1 and total < 0.45 and all(t.startswith("fedn_amd_delete") for t in inner.threads)
+    else:
+        assert issued >= 0.6 and inner.threads == {"MainThread"}
+    assert st.delete_times["count"] == 4 and st.delete_times["store_s"] >= 0.6
+    st.close()
+
+
+def test_a_failed_store_delete_is_logged_as_the_reference_logs_it(caplog):
+    """A store delete that raises: the reference's per-update try logs it (fedavg.py:75-78) and the
+    update stays counted; here finish_deletes hands it to the aggregator, which logs the same."""
+    import logging
+
+    from fedn_amd.aggregators.aggregatorbase import AggregatorBase
+    from fedn_amd.ingest import StagingUpdateHandler
+    inner = _SlowStoreHandler(0.0, bad={"u1"})
+    st = StagingUpdateHandler(inner, helper=None, device="cpu", workers=1, delete_workers=2)
+    class Agg(AggregatorBase):
+        def __init__(self, uh):
+            super().__init__(uh)
+            self.name = "fedavg"
+
+        def combine_models(self, helper=None, delete_models=True, parameters=None):
+            return None, {}
+    agg = Agg(st)
+    for mu in _mus(3):
+        st.delete_model(mu)
+    with caplog.at_level(logging.ERROR, logger="fedn"):
+        agg._finish_deletes()
+    assert sorted(inner.deleted) == ["u0", "u2"]
+    assert any("Error encoutered while processing model update: cannot delete u1" in r.getMessage()
+               for r in caplog.records)
+    st.close()

@@ -31,7 +31,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fedn_amd import _abi  # noqa: E402
 
 
-def run(mode, blob, ns, rate, workers, store="memory"):
+def run(mode, blob, ns, rate, workers, store="memory", delete_workers=None):
     from fedn_amd.aggregators import get_aggregator
     from fedn_amd.helper import Helper
     from fedn_amd.ingest import StagingUpdateHandler
@@ -41,7 +41,7 @@ def run(mode, blob, ns, rate, workers, store="memory"):
     from fedn_amd.updatehandler import MemoryModelStore, TempFileModelStore
     K = len(ns)
     uh = MemoryUpdateHandler(TempFileModelStore() if store == "file" else MemoryModelStore())
-    st = StagingUpdateHandler(uh, helper=Helper(), workers=workers)
+    st = StagingUpdateHandler(uh, helper=Helper(), workers=workers, delete_workers=delete_workers)
     svc = MemoryModelService(uh.store)
     if mode.startswith("streaming"):
         svc = StreamingUpload(svc, st, workers=K, device_decode=mode == "streaming")
@@ -96,6 +96,7 @@ def run(mode, blob, ns, rate, workers, store="memory"):
                           "decode_lag_s": (max(decoded_at) - last[0]) if decoded_at else None,
                           "combine_s": t_comb, "aggregator_init_s": t_init, "delete_s": t_del[0],
                           "delete_plugin_s": st.delete_times["plugin_s"], "delete_store_s": st.delete_times["store_s"],
+                          "delete_wait_s": st.delete_times["wait_s"], "delete_workers": st.delete_workers,
                           "store": store, **{k: v for k, v in data.items() if isinstance(v, float)}}
 
 
@@ -106,6 +107,8 @@ def main():
     ap.add_argument("--client-MBps", type=float, default=250.0)
     ap.add_argument("--workers", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--delete-workers", type=int, default=None,
+                    help="store deletes side by side on this many threads (0: inline, one after another)")
     ap.add_argument("--store", choices=("memory", "file"), default="memory",
                     help="the update store: in-memory bytes, or files + os.remove as FEDn's TempModelStorage")
     a = ap.parse_args()
@@ -123,7 +126,7 @@ def main():
     res = {}
     for rep in range(a.reps):                         # rep 0 warms pinned / device pools
         for mode in ("after-arrival", "streaming-host", "streaming"):
-            model, order, t = run(mode, blob, ns, a.client_MBps * 1e6, a.workers, a.store)
+            model, order, t = run(mode, blob, ns, a.client_MBps * 1e6, a.workers, a.store, a.delete_workers)
             uh = MemoryUpdateHandler()                # the same fold from host arrays
             for k in order:
                 uh.submit([w.copy() for w in tensors], ns[k])
@@ -136,6 +139,8 @@ def main():
                       "archive_MB": round(len(blob) / 1e6, 1),
                       "delete_plugin_s": round(res["streaming"]["delete_plugin_s"], 4),
                       "delete_store_s": round(res["streaming"]["delete_store_s"], 4),
+                      "delete_wait_s": round(res["streaming"]["delete_wait_s"], 4),
+                      "delete_workers": res["streaming"]["delete_workers"],
                       "client_MBps": a.client_MBps, "tail_after_arrival_s": round(res["after-arrival"]["tail_s"], 4),
                       "tail_streaming_host_s": round(res["streaming-host"]["tail_s"], 4),
                       "tail_streaming_s": round(res["streaming"]["tail_s"], 4),

@@ -120,10 +120,13 @@ for s in $STEPS; do
     upload100mfile)
       # the same with FEDn's file store stand-in (TempModelStorage: chunks to a file, delete = os.remove),
       # 300 and 400 MB/s per client; the delete breakdown (plug-in copies vs the store) is in the lines
+      # (store deletes side by side, then inline one after another: FEDN_AMD_DELETE_WORKERS=0)
       for r in 300 400; do
-        timeout -k 10 600 python tools/bench_upload.py --params 100000000 --clients 8 --client-MBps $r --store file \
-          >> "$OUT/upload100m_file.log" 2>&1; rc=$?
-        [ $rc -eq 0 ] || { echo "upload100mfile rc=$rc"; exit $rc; }
+        for dw in 8 0; do
+          timeout -k 10 600 python tools/bench_upload.py --params 100000000 --clients 8 --client-MBps $r --store file \
+            --delete-workers $dw >> "$OUT/upload100m_file.log" 2>&1; rc=$?
+          [ $rc -eq 0 ] || { echo "upload100mfile rc=$rc"; exit $rc; }
+        done
       done
       echo "upload100mfile rc=0"; grep '"what"' "$OUT/upload100m_file.log" | cut -c1-600 ;;
     mixprobe)
