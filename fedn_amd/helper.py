@@ -337,18 +337,38 @@ class Helper:
         return self._ew("fill", m1, None, a)
 
     def save(self, weights, path=None, file_type="npz"):
+        """numpyhelper.save (numpyhelper.py:144-169): np.savez_compressed's archive, written by the
+        native writer (codec.savez_into: the same bytes). numpy's own file handling is kept: a path
+        gets ".npz" appended unless it ends in it (the given path is returned, as the reference
+        returns it); a file object is written from where it stands. zipfile's records hold offsets
+        from the stream's start and switch to data descriptors on a stream it cannot seek, so a
+        file object not at offset 0, not seekable or without ``read`` is handed to np.savez_compressed
+        itself (which writes it, or raises, as the reference would)."""
         self.check_supported_file_type(file_type)
         if file_type == "npz":
             if not path:
                 path = self.get_tmp_path()
+            weights = list(weights)
+            if hasattr(path, "write"):
+                at = None
+                if hasattr(path, "read"):           # numpy's zipfile_factory takes it as a file only then
+                    try:
+                        at = path.tell()
+                        path.seek(at)
+                    except (AttributeError, OSError):
+                        at = None
+                if at != 0 and npz_writer() != "blocks":
+                    np.savez_compressed(path, **{str(i): w for i, w in enumerate(weights)})
+                    return path
             if npz_writer() == "blocks":
-                data = codec.save_npz_blocks(list(weights))
+                data = codec.save_npz_blocks(weights)
             else:
-                data = memoryview(codec.savez_into(list(weights)))
+                data = memoryview(codec.savez_into(weights))
             if hasattr(path, "write"):
                 path.write(data)
             else:
-                with open(path, "wb") as f:
+                fn = os.fspath(path)
+                with open(fn if fn.endswith(".npz") else fn + ".npz", "wb") as f:
                     f.write(data)
             return path
         if not path:

@@ -5,6 +5,7 @@ byte for byte — zip headers, member order, .npy headers and the deflate stream
 mixed dtypes (f16 ... complex64, bool, unicode, big-endian), 0-d and empty arrays, Fortran order,
 non-contiguous views, 70 members, and a member past numpy's 16 MiB write size."""
 import io
+import os
 import json
 
 import numpy as np
@@ -104,3 +105,58 @@ def test_object_arrays_fall_back_to_numpy():
     ref = io.BytesIO()
     np.savez_compressed(ref, **{"0": ws[0]})
     assert codec.save_npz(ws) == ref.getvalue()
+
+
+def test_file_handling_is_numpys(tmp_path):
+    """numpy's own target handling around the bytes (np.savez_compressed, numpy/lib/_npyio_impl.py
+    _savez): a path without ".npz" gets it appended (the reference then returns the path it was
+    given), a path-like is accepted, a file object is written from its current offset (zipfile's
+    header offsets count from the stream's start), and an unseekable stream gets zipfile's
+    data-descriptor records — byte-equal to what numpy writes to the same kind of target."""
+    import pathlib
+
+    rng = np.random.default_rng(1)
+    ws = [rng.standard_normal((30, 7)).astype(np.float32), np.arange(5)]
+    ref = io.BytesIO()
+    np.savez_compressed(ref, **{str(i): w for i, w in enumerate(ws)})
+    want = ref.getvalue()
+
+    p = str(tmp_path / "model")                      # no suffix: numpy writes model.npz
+    assert Helper().save(ws, p) == p
+    assert not os.path.exists(p) and open(p + ".npz", "rb").read() == want
+    pl = tmp_path / "pl.npz"
+    assert Helper().save(ws, pl) == pl and pl.read_bytes() == want
+
+    def numpy_into(target):
+        np.savez_compressed(target, **{str(i): w for i, w in enumerate(ws)})
+        return target
+
+    a, b = io.BytesIO(b"prefix-bytes"), io.BytesIO(b"prefix-bytes")
+    a.seek(0, io.SEEK_END)
+    b.seek(0, io.SEEK_END)
+    Helper().save(ws, a)
+    assert a.getvalue() == numpy_into(b).getvalue() and a.getvalue() != b"prefix-bytes" + want
+
+    class Unseekable(io.RawIOBase):                 # a pipe: write only, no tell / seek
+        def __init__(self):
+            self.chunks = []
+
+        def writable(self):
+            return True
+
+        def write(self, d):
+            self.chunks.append(bytes(d))
+            return len(d)
+    u, v = Unseekable(), Unseekable()
+    Helper().save(ws, u)
+    got = b"".join(u.chunks)
+    assert got == b"".join(numpy_into(v).chunks) and got != want
+    assert [np.array_equal(x, y) for x, y in zip(np.load(io.BytesIO(got)).values(), ws)] == [True, True]
+
+    class WriteOnly:                                # no read: numpy refuses it (os.fspath), so do we
+        def write(self, d):
+            return len(d)
+    with pytest.raises(TypeError):
+        np.savez_compressed(WriteOnly(), a=ws[0])
+    with pytest.raises(TypeError):
+        Helper().save(ws, WriteOnly())

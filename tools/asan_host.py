@@ -1,13 +1,15 @@
 """Host native code under AddressSanitizer + UndefinedBehaviorSanitizer (CPU only, build container).
 
-Builds ``libfednpz.so`` (csrc/npz_codec.cpp: the npz codec and the native pack / gather) and the
+Builds ``libfednpz.so`` (csrc/npz_codec.cpp: the npz codec and the native pack / gather;
+csrc/savez.cpp + pdeflate.h: the numpy-identical writer and its parallel deflate) and the
 ``_fastpack`` extension (csrc/fastpack.c: admission + pack of small updates) with
 ``-fsanitize=address,undefined`` into a scratch copy of the package, then runs the CPU tests that
-drive them — ``tests/test_codec.py``, ``tests/test_fastpack.py``, ``tests/test_staging_host.py`` —
+drive them — the codec, decoder, upload, writer (golden bytes, ZIP64, zlib-exact parallel
+deflate), pack and staging-host tests —
 inside that copy with the sanitizer runtimes preloaded into the (uninstrumented) Python. Any
 sanitizer report aborts the run (``halt_on_error``); the summary goes to stdout.
 
-    python tools/asan_host.py [--out profiles/r04_asan_host.log]
+    python tools/asan_host.py [--out profiles/r05_asan_host.log]
 
 GPU code is not sanitized here (no GPU sanitizer on this pool); libfedagg.so is copied as built.
 """
@@ -21,8 +23,9 @@ import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# (not tests/test_codec_nomem.py: it caps the address space, which ASan's shadow memory cannot live in)
 TESTS = ["tests/test_codec.py", "tests/test_inflate.py", "tests/test_upload.py", "tests/test_fastpack.py",
-         "tests/test_staging_host.py"]
+         "tests/test_staging_host.py", "tests/test_savez_golden.py", "tests/test_savez_zip64.py", "tests/test_pdeflate.py"]
 SAN = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined", "-g", "-O1"]
 
 
@@ -51,7 +54,8 @@ def main():
         shutil.copy(os.path.join(ROOT, "bench.py"), tmp)
         pkg = os.path.join(tmp, "fedn_amd")
         cmds = [["g++", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", *SAN, "-I", os.path.join(tmp, "include"),
-                 "-o", os.path.join(pkg, "libfednpz.so"), os.path.join(pkg, "csrc", "npz_codec.cpp"), "-lz"],
+                 "-o", os.path.join(pkg, "libfednpz.so"), os.path.join(pkg, "csrc", "npz_codec.cpp"),
+                 os.path.join(pkg, "csrc", "savez.cpp"), "-lz"],
                 ["gcc", "-fPIC", "-shared", "-Wall", *SAN, "-I", sysconfig.get_paths()["include"], "-I",
                  numpy.get_include(), "-o", os.path.join(pkg, "_fastpack.so"), os.path.join(pkg, "csrc", "fastpack.c")]]
         for c in cmds:
