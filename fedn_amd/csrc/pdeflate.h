@@ -27,6 +27,29 @@
 //     makes it; blocks are sized, placed at their bit offsets and encoded in parallel.
 // Anything outside what this models makes the caller run zlib itself (FNPZ's exact fallback), so
 // the output is zlib's bytes either way; tests/test_pdeflate.py compares against libz directly.
+//
+// Attribution. Byte-identical output means zlib's decisions reproduced exactly, so parts of this
+// file follow zlib 1.2.11 closely: the tree construction (TreeBuilder::pqdownheap / gen_bitlen /
+// build_tree, scan_tree, send_tree, the static tables and gen_codes: trees.c) and the tail replay
+// (Tail::longest_match / fill_window / run: deflate.c's longest_match, fill_window and
+// deflate_slow). Those parts are altered versions of zlib code — restructured for the chunked,
+// stream-offset parse and parallel block encoding, not the original software — and carry zlib's
+// notice:
+//
+//   Copyright (C) 1995-2017 Jean-loup Gailly and Mark Adler
+//
+//   This software is provided 'as-is', without any express or implied warranty. In no event will
+//   the authors be held liable for any damages arising from the use of this software.
+//
+//   Permission is granted to anyone to use this software for any purpose, including commercial
+//   applications, and to alter it and redistribute it freely, subject to the following
+//   restrictions:
+//   1. The origin of this software must not be misrepresented; you must not claim that you wrote
+//      the original software. If you use this software in a product, an acknowledgment in the
+//      product documentation would be appreciated but is not required.
+//   2. Altered source versions must be plainly marked as such, and must not be misrepresented as
+//      being the original software.
+//   3. This notice may not be removed or altered from any source distribution.
 #pragma once
 
 #include <algorithm>
