@@ -224,8 +224,27 @@ struct Parser {
         }
         return best;
     }
+    // the chain walks a few positions ahead, started early: the first slot of t + 4's chain and the
+    // second of t + 2's are fetched while this position is parsed (a walk is a chain of dependent
+    // L2 loads, and the branch that ends each walk is hard to predict, so out-of-order execution
+    // rarely gets to the next one on its own); addresses only, the parse is unchanged
+    inline void prefetch_ahead() {
+        const int64_t a = t + 4, b = t + 2;
+        if (a + 3 <= L) {
+            const uint32_t e = head[hash3(S + a)];
+            if (e) __builtin_prefetch(&ring[(size_t)(dec(e) & kWMask)]);
+        }
+        if (b + 3 <= L) {
+            const uint32_t e = head[hash3(S + b)];
+            if (e) {
+                const uint32_t n2 = ring[(size_t)(dec(e) & kWMask)].prev;
+                if (n2) __builtin_prefetch(&ring[(size_t)(dec(n2) & kWMask)]);
+            }
+        }
+    }
     // one deflate_slow iteration at top t (lookahead >= MIN_LOOKAHEAD)
     inline void step(Syms& out) {
+        prefetch_ahead();
         const uint32_t hh = insert(t);
         const int prev_len = mlen;
         const int64_t prev_match = mstart;
