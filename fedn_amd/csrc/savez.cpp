@@ -185,7 +185,8 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
         std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return ms[a].nbytes > ms[b].nbytes; });
         fnpz_internal::run_parallel((int)order.size(), std::max(1, threads), [&](int k) { deflate_member(ms[order[k]]); });
         for (int i = 0; i < n; ++i)
-            if (ms[i].rc != Z_OK) return set_error(FNPZ_ECORRUPT, "fnpz_savez: deflate failed on member %d", i);
+            if (ms[i].rc == Z_MEM_ERROR) return set_error(FNPZ_ENOMEM, "fnpz_savez: zlib out of memory on member %d", i);
+            else if (ms[i].rc != Z_OK) return set_error(FNPZ_ECORRUPT, "fnpz_savez: deflate failed on member %d", i);
 
         uint8_t* p = out;
         uint8_t* const lim = out + out_cap;
