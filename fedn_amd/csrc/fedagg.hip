@@ -1470,6 +1470,95 @@ k_fedopt_mixg(const OptBuffers b, const ClientTable<S> tab, const int K, const i
 }
 #endif
 
+#ifdef FEDAGG_PROBES
+// clock-windowed store probe (FA_TUNE_OPT_WIN_*): k_fedopt_mix's access pattern with the whole chip's
+// stores confined to a common time window. Every wave reads the GPU's 100 MHz reference clock
+// (s_memrealtime, one counter for all XCDs) and issues its v / out / m stores only while
+// clock mod 2^win_log < win_w, and (mode >= 1) starts a tile's reads, or (mode 2) each client batch's
+// reads, only outside that window — so the DRAM sees read-only stretches and write bursts instead of
+// 36 streams with 14 % writes interleaved everywhere, without a grid barrier. Waits are bounded by
+// one period; results are k_fedopt_mix's.
+__device__ __forceinline__ bool in_write_window(uint32_t win_log, uint32_t win_w) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    return (t & ((1ull << win_log) - 1)) < win_w;
+}
+// (a wait gives up after 2^18 polls, far past one period, should the clock ever stand still)
+__device__ __forceinline__ void wait_write_window(uint32_t win_log, uint32_t win_w) {
+    for (int n = 0; n < (1 << 18) && !in_write_window(win_log, win_w); ++n) __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void wait_read_window(uint32_t win_log, uint32_t win_w) {
+    for (int n = 0; n < (1 << 18) && in_write_window(win_log, win_w); ++n) __builtin_amdgcn_s_sleep(1);
+}
+
+template <typename Y, typename OLD, typename S, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_mixw(const OptBuffers b, const ClientTable<S> tab, const int K, const int64_t P, const uint32_t win_log,
+              const uint32_t win_w, const int mode) {
+    constexpr int NH = 4, H = 2, E = 2 * NH, U = kUnroll / 2;
+    constexpr int64_t T = 128 * NH;
+    const int64_t base = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * T;
+    if (base + T > P) return;
+    const int64_t i0 = base + 2 * (threadIdx.x & 63);
+    auto at = [i0](int h) { return i0 + (int64_t)h * 128; };
+    if (mode >= 1) wait_read_window(win_log, win_w);
+    double acc[E];
+    {
+        OLD old[E];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) strip_load<OLD, H, false>(static_cast<const OLD*>(b.old) + at(h), *reinterpret_cast<OLD(*)[H]>(&old[h * H]));
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = (double)widen<OLD, double>(old[e]);
+    }
+    auto add_client = [&](int k, Y (&y)[E]) {
+        const Y* yp = static_cast<const Y*>(tab.ptr[k]);
+#pragma unroll
+        for (int h = 0; h < NH; ++h) strip_load<Y, H, NT>(yp + at(h), *reinterpret_cast<Y(*)[H]>(&y[h * H]));
+    };
+    int k = 0;
+    {
+        Y y[E];
+        add_client(0, y);
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] += (double)widen<Y, double>(y[e]);
+        k = 1;
+    }
+    for (; k + U <= K; k += U) {
+        if (mode >= 2) wait_read_window(win_log, win_w);
+        Y y[U][E];
+#pragma unroll
+        for (int u = 0; u < U; ++u) add_client(k + u, y[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int e = 0; e < E; ++e) acc[e] += (double)widen<Y, double>(y[u][e]);
+    }
+    for (; k < K; ++k) {
+        Y y[E];
+        add_client(k, y);
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] += (double)widen<Y, double>(y[e]);
+    }
+    double mo[E], vo[E];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        double mi[H] = {}, vv[H] = {};
+        opt_load_state<H>(b, OptScalars{}, at(h), H, mi, vv);
+#pragma unroll
+        for (int e = 0; e < H; ++e) {
+            mo[h * H + e] = mi[e] + acc[h * H + e];
+            vo[h * H + e] = vv[e] + acc[h * H + e];
+        }
+    }
+    wait_write_window(win_log, win_w);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        strip_store<double, H, 1>(static_cast<double*>(b.v_out) + at(h), *reinterpret_cast<double(*)[H]>(&vo[h * H]));
+        strip_store<double, H, 1>(static_cast<double*>(b.out) + at(h), *reinterpret_cast<double(*)[H]>(&acc[h * H]));
+        strip_store<double, H, 1>(static_cast<double*>(b.m_out) + at(h), *reinterpret_cast<double(*)[H]>(&mo[h * H]));
+    }
+}
+#endif
+
 template <typename Y, typename OLD, class PG, int E, bool FIRST, bool FINAL, bool NT, bool NOST = false, int OSM = 0>
 __global__ void __launch_bounds__(kBlock)
 k_fedopt(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
@@ -1754,7 +1843,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0}, opt_burst{0}, opt_g{0};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0}, opt_burst{0}, opt_g{0}, opt_win_log{0}, opt_win_w{0}, opt_win_mode{0};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -2025,6 +2114,13 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
 #undef FA_BURST
                 default: return fail(FA_EINVAL, "fa_tune OPT_BURST: 1, 2 or 4 tiles per wave");
             }
+            return check_launch("fa_fedopt_step: kernel launch");
+        }
+        if (first && final_ && g_cfg.opt_win_log) {
+            if (b.m_out_f64 != 1) return fail(FA_EINVAL, "fa_tune OPT_WIN probe: fp64 m out");
+            const dim3 gw((unsigned)((P + 4 * 512 - 1) / (4 * 512)));   // a ragged last tile is skipped
+            hipLaunchKernelGGL((k_fedopt_mixw<Y, OLD, typename PG::S, NT>), gw, dim3(kBlock), 0, st, b, tab, cnt, P,
+                               (uint32_t)g_cfg.opt_win_log.load(), (uint32_t)g_cfg.opt_win_w.load(), g_cfg.opt_win_mode.load());
             return check_launch("fa_fedopt_step: kernel launch");
         }
         if (first && final_ && g_cfg.opt_mix) {
@@ -2803,6 +2899,19 @@ int fa_tune(int knob, int value) {
             if (value != 0 && value != 1 && value != 2 && value != 4)
                 return fail(FA_EINVAL, "fa_tune: burst-store product probe 0 (off), 1, 2 or 4 tiles per wave");
             g_cfg.opt_g = value;
+            return FA_OK;
+        case FA_TUNE_OPT_WIN_LOG:
+            if (value != 0 && (value < 6 || value > 24))
+                return fail(FA_EINVAL, "fa_tune: store-window period 2^6 .. 2^24 ticks of 10 ns (0 = off)");
+            g_cfg.opt_win_log = value;
+            return FA_OK;
+        case FA_TUNE_OPT_WIN_W:
+            if (value < 0) return fail(FA_EINVAL, "fa_tune: store-window length in ticks >= 0");
+            g_cfg.opt_win_w = value;
+            return FA_OK;
+        case FA_TUNE_OPT_WIN_MODE:
+            if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: store-window mode 0, 1 or 2");
+            g_cfg.opt_win_mode = value;
             return FA_OK;
         case FA_TUNE_OPT_BURST:
             if (value != 0 && value != 1 && value != 2 && value != 4)

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--burst", default="1,2,4", help="burst-store probe G values (tiles per wave), '' = none")
     ap.add_argument("--opt-g", default="1,2,4", help="product step with G tiles per wave (fa_tune OPT_G), '' = none")
+    ap.add_argument("--win", default="", help="clock-windowed store probe: log2period:window_ticks:mode,... "
+                    "(fa_tune OPT_WIN_*: stores only while the 100 MHz clock mod 2^log2period < window)")
     a = ap.parse_args()
     _abi.use_probe()
     dev = torch.device("cuda", 0)
@@ -62,6 +64,7 @@ def main():
     dst = torch.empty_like(src)
     res = {}
     bursts = [int(x) for x in a.burst.split(",") if x]
+    wins = [tuple(int(v) for v in x.split(":")) for x in a.win.split(",") if x]
     gs = [int(x) for x in a.opt_g.split(",") if x]
     # the product arithmetic with G tiles per wave (fa_tune OPT_G): bit-identical to k_fedopt_c?
     exact = {}
@@ -99,6 +102,13 @@ def main():
                 fn()
                 res.setdefault((name, f"burst{g}"), []).append(median_ms(fn))
             ops.tune(opt_burst=0)
+            for lg, w, mode in wins:              # stores confined to a chip-wide clock window
+                if name != "steady":
+                    continue
+                ops.tune(opt_win_log=lg, opt_win_w=w, opt_win_mode=mode)
+                fn()
+                res.setdefault((name, f"win{lg}_{w}_{mode}"), []).append(median_ms(fn))
+            ops.tune(opt_win_log=0)
         ops.tune(opt_mix=0)
         ops.stream_copy(dst, src)
         res.setdefault(("copy", 0), []).append(median_ms(lambda: ops.stream_copy(dst, src)))
@@ -121,6 +131,8 @@ def main():
                              for g in gs if (name, f"g{g}") in res},
                           **{f"g{g}_reps": [round(x, 4) for x in res[(name, f'g{g}')]]
                              for g in gs if (name, f"g{g}") in res},
+                          **{f"win{lg}_{w}_{m}_ms": round(float(np.median(res[(name, f'win{lg}_{w}_{m}')])), 4)
+                             for lg, w, m in wins if (name, f"win{lg}_{w}_{m}") in res},
                           **({f"g{g}_bit_exact": exact[g] for g in gs} if name == "steady" else {})}), flush=True)
     print(json.dumps({"copy_GBps": round(copy_gbs, 1), "reps_ms": [round(x, 4) for x in res[("copy", 0)]]}))
 

@@ -129,6 +129,12 @@ for s in $STEPS; do
         done
       done
       echo "upload100mfile rc=0"; grep '"what"' "$OUT/upload100m_file.log" | cut -c1-600 ;;
+    winprobe)
+      # FedAdam steady state with the chip's stores confined to a common clock window (probe library)
+      timeout -k 10 600 python tools/fedopt_mix_probe.py --burst "" --opt-g "" \
+        --win "11:300:0,11:300:1,11:300:2,11:450:2,10:150:2,12:600:2,12:900:2,13:1200:2,9:80:2" \
+        > "$OUT/winprobe.log" 2>&1; rc=$?
+      echo "winprobe rc=$rc"; cut -c1-1200 "$OUT/winprobe.log" | tail -3; [ $rc -eq 0 ] || exit $rc ;;
     mixprobe)
       timeout -k 10 600 python tools/fedopt_mix_probe.py > "$OUT/mixprobe.log" 2>&1; rc=$?
       echo "mixprobe rc=$rc"; cut -c1-700 "$OUT/mixprobe.log" | tail -4; [ $rc -eq 0 ] || exit $rc ;;
