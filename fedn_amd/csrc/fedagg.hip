@@ -631,6 +631,24 @@ struct LaneTable {
     }
 };
 
+// Chip-wide store windows (probe kernels: fa_tune OPT_WIN_* / AVG_WIN_*). Every wave reads the GPU's
+// 100 MHz reference clock (s_memrealtime: one counter for all XCDs) and stores only while
+// clock mod period < win_w, reads (optionally) only outside that window: the DRAM then sees
+// read-only stretches and write bursts instead of writes interleaved everywhere, with no grid
+// barrier. A wait gives up after 2^18 polls, far past one period, should the clock stand still.
+[[maybe_unused]] __device__ __forceinline__ bool in_write_window(uint32_t period, uint32_t win_w) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    return (uint32_t)(t % period) < win_w;
+}
+// (a wait gives up after 2^18 polls, far past one period, should the clock ever stand still)
+[[maybe_unused]] __device__ __forceinline__ void wait_write_window(uint32_t period, uint32_t win_w) {
+    for (int n = 0; n < (1 << 18) && !in_write_window(period, win_w); ++n) __builtin_amdgcn_s_sleep(1);
+}
+[[maybe_unused]] __device__ __forceinline__ void wait_read_window(uint32_t period, uint32_t win_w) {
+    for (int n = 0; n < (1 << 18) && in_write_window(period, win_w); ++n) __builtin_amdgcn_s_sleep(1);
+}
+
+
 // Workgroup -> tile order for the one-tile-per-workgroup grid (fa_tune FA_TUNE_TILEMAP).
 // Workgroups are dealt round-robin to the 8 XCDs, so with MAP 0 consecutive tiles run on
 // different XCDs. MAP = R > 0 gives each XCD runs of R consecutive tiles (groups of 8R tiles,
@@ -650,9 +668,10 @@ __device__ __forceinline__ int64_t map_tile(int64_t t, int64_t ntiles) {
 }
 
 template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK, int NTS,
-          int MAP>
+          int MAP, bool WIN = false>
 __device__ __forceinline__ void fedavg_pipe_body(X* __restrict__ agg, const ClientTable<typename CP::S>& tab, const int K,
-                                                 const int64_t P) {
+                                                 const int64_t P, const uint32_t period = 0, const uint32_t win_w = 0,
+                                                 const int win_mode = 0) {
     using V = typename CP::V;
     const LaneTable<CP> lt(tab);
     const int64_t ntiles = ((P + E - 1) / E + (int64_t)BLK * S - 1) / ((int64_t)BLK * S);
@@ -664,6 +683,9 @@ __device__ __forceinline__ void fedavg_pipe_body(X* __restrict__ agg, const Clie
         if ((strip0 + (int64_t)(S - 1) * BLK) * E + E > P) {
             k_fedavg_tail<Y, X, CP, E, S, INIT, INT_FIRST, BLK>(agg, tab, K, P, strip0);
             continue;
+        }
+        if constexpr (WIN) {
+            if (win_mode >= 1) wait_read_window(period, win_w);
         }
         V x[S][E];
         int k = 0;
@@ -690,6 +712,9 @@ __device__ __forceinline__ void fedavg_pipe_body(X* __restrict__ agg, const Clie
         Y a[S][E], b[S][E];
         if (k < K) load(k, a);
         while (k + 1 < K) {
+            if constexpr (WIN) {
+                if (win_mode >= 2) wait_read_window(period, win_w);
+            }
             load(k + 1, b);
             fold(k, a);
             if (k + 2 < K) load(k + 2, a);
@@ -697,6 +722,7 @@ __device__ __forceinline__ void fedavg_pipe_body(X* __restrict__ agg, const Clie
             k += 2;
         }
         if (k < K) fold(k, a);
+        if constexpr (WIN) wait_write_window(period, win_w);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             X xo[E];
@@ -718,6 +744,15 @@ k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const 
 }
 
 #ifdef FEDAGG_PROBES
+// store-window probe (FA_TUNE_AVG_WIN_*): the same body with the stores in a chip-wide clock window
+template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK, int NTS,
+          int MAP>
+__global__ void __launch_bounds__(BLK)
+k_fedavg_pipe_win(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const int K, const int64_t P,
+                  const uint32_t period, const uint32_t win_w, const int win_mode) {
+    fedavg_pipe_body<Y, X, CP, E, S, INIT, INT_FIRST, NT, LT, BLK, NTS, MAP, true>(agg, tab, K, P, period, win_w, win_mode);
+}
+
 // occupancy probe (FA_TUNE_WPE): the same body compiled for at least W waves per SIMD
 template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK, int NTS,
           int MAP, int W>
@@ -1474,25 +1509,13 @@ k_fedopt_mixg(const OptBuffers b, const ClientTable<S> tab, const int K, const i
 // clock-windowed store probe (FA_TUNE_OPT_WIN_*): k_fedopt_mix's access pattern with the whole chip's
 // stores confined to a common time window. Every wave reads the GPU's 100 MHz reference clock
 // (s_memrealtime, one counter for all XCDs) and issues its v / out / m stores only while
-// clock mod 2^win_log < win_w, and (mode >= 1) starts a tile's reads, or (mode 2) each client batch's
+// clock mod period < win_w, and (mode >= 1) starts a tile's reads, or (mode 2) each client batch's
 // reads, only outside that window — so the DRAM sees read-only stretches and write bursts instead of
 // 36 streams with 14 % writes interleaved everywhere, without a grid barrier. Waits are bounded by
 // one period; results are k_fedopt_mix's.
-__device__ __forceinline__ bool in_write_window(uint32_t win_log, uint32_t win_w) {
-    const uint64_t t = __builtin_amdgcn_s_memrealtime();
-    return (t & ((1ull << win_log) - 1)) < win_w;
-}
-// (a wait gives up after 2^18 polls, far past one period, should the clock ever stand still)
-__device__ __forceinline__ void wait_write_window(uint32_t win_log, uint32_t win_w) {
-    for (int n = 0; n < (1 << 18) && !in_write_window(win_log, win_w); ++n) __builtin_amdgcn_s_sleep(1);
-}
-__device__ __forceinline__ void wait_read_window(uint32_t win_log, uint32_t win_w) {
-    for (int n = 0; n < (1 << 18) && in_write_window(win_log, win_w); ++n) __builtin_amdgcn_s_sleep(1);
-}
-
 template <typename Y, typename OLD, typename S, bool NT>
 __global__ void __launch_bounds__(kBlock)
-k_fedopt_mixw(const OptBuffers b, const ClientTable<S> tab, const int K, const int64_t P, const uint32_t win_log,
+k_fedopt_mixw(const OptBuffers b, const ClientTable<S> tab, const int K, const int64_t P, const uint32_t period,
               const uint32_t win_w, const int mode) {
     constexpr int NH = 4, H = 2, E = 2 * NH, U = kUnroll / 2;
     constexpr int64_t T = 128 * NH;
@@ -1500,7 +1523,7 @@ k_fedopt_mixw(const OptBuffers b, const ClientTable<S> tab, const int K, const i
     if (base + T > P) return;
     const int64_t i0 = base + 2 * (threadIdx.x & 63);
     auto at = [i0](int h) { return i0 + (int64_t)h * 128; };
-    if (mode >= 1) wait_read_window(win_log, win_w);
+    if (mode >= 1) wait_read_window(period, win_w);
     double acc[E];
     {
         OLD old[E];
@@ -1523,7 +1546,7 @@ k_fedopt_mixw(const OptBuffers b, const ClientTable<S> tab, const int K, const i
         k = 1;
     }
     for (; k + U <= K; k += U) {
-        if (mode >= 2) wait_read_window(win_log, win_w);
+        if (mode >= 2) wait_read_window(period, win_w);
         Y y[U][E];
 #pragma unroll
         for (int u = 0; u < U; ++u) add_client(k + u, y[u]);
@@ -1549,7 +1572,7 @@ k_fedopt_mixw(const OptBuffers b, const ClientTable<S> tab, const int K, const i
             vo[h * H + e] = vv[e] + acc[h * H + e];
         }
     }
-    wait_write_window(win_log, win_w);
+    wait_write_window(period, win_w);
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
         strip_store<double, H, 1>(static_cast<double*>(b.v_out) + at(h), *reinterpret_cast<double(*)[H]>(&vo[h * H]));
@@ -1843,7 +1866,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0}, opt_burst{0}, opt_g{0}, opt_win_log{0}, opt_win_w{0}, opt_win_mode{0};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0}, opt_burst{0}, opt_g{0}, opt_win_period{0}, opt_win_w{0}, opt_win_mode{0}, avg_win_period{0}, avg_win_w{0}, avg_win_mode{0};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -1914,6 +1937,13 @@ void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, i
     shm = (unsigned)g_cfg.lds_kib * 1024u;     // occupancy probe: LDS the kernel never touches
     if constexpr (std::is_same<CP, CF32>::value && std::is_same<X, float>::value && S * E * (int)sizeof(Y) == 64 &&
                   BLK == kBlock && MAP == 0 && !LT && !NT && NTS == 1) {
+        if (g_cfg.avg_win_period && !int_first) {
+            const uint32_t wl = (uint32_t)g_cfg.avg_win_period.load(), ww = (uint32_t)g_cfg.avg_win_w.load();
+            const int wm = g_cfg.avg_win_mode.load();
+            if (first) hipLaunchKernelGGL((k_fedavg_pipe_win<Y, X, CP, E, S, true, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), shm, st, a, tab, cnt, P, wl, ww, wm);
+            else hipLaunchKernelGGL((k_fedavg_pipe_win<Y, X, CP, E, S, false, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), shm, st, a, tab, cnt, P, wl, ww, wm);
+            return;
+        }
         const int w = g_cfg.wpe;
         if (w > 0 && !int_first) {
 #define FA_WPE(W_)                                                                                                      \
@@ -2116,11 +2146,11 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
             }
             return check_launch("fa_fedopt_step: kernel launch");
         }
-        if (first && final_ && g_cfg.opt_win_log) {
+        if (first && final_ && g_cfg.opt_win_period) {
             if (b.m_out_f64 != 1) return fail(FA_EINVAL, "fa_tune OPT_WIN probe: fp64 m out");
             const dim3 gw((unsigned)((P + 4 * 512 - 1) / (4 * 512)));   // a ragged last tile is skipped
             hipLaunchKernelGGL((k_fedopt_mixw<Y, OLD, typename PG::S, NT>), gw, dim3(kBlock), 0, st, b, tab, cnt, P,
-                               (uint32_t)g_cfg.opt_win_log.load(), (uint32_t)g_cfg.opt_win_w.load(), g_cfg.opt_win_mode.load());
+                               (uint32_t)g_cfg.opt_win_period.load(), (uint32_t)g_cfg.opt_win_w.load(), g_cfg.opt_win_mode.load());
             return check_launch("fa_fedopt_step: kernel launch");
         }
         if (first && final_ && g_cfg.opt_mix) {
@@ -2900,10 +2930,10 @@ int fa_tune(int knob, int value) {
                 return fail(FA_EINVAL, "fa_tune: burst-store product probe 0 (off), 1, 2 or 4 tiles per wave");
             g_cfg.opt_g = value;
             return FA_OK;
-        case FA_TUNE_OPT_WIN_LOG:
-            if (value != 0 && (value < 6 || value > 24))
-                return fail(FA_EINVAL, "fa_tune: store-window period 2^6 .. 2^24 ticks of 10 ns (0 = off)");
-            g_cfg.opt_win_log = value;
+        case FA_TUNE_OPT_WIN_PERIOD:
+            if (value != 0 && (value < 64 || value > (1 << 24)))
+                return fail(FA_EINVAL, "fa_tune: store-window period 64 .. 2^24 ticks of 10 ns (0 = off)");
+            g_cfg.opt_win_period = value;
             return FA_OK;
         case FA_TUNE_OPT_WIN_W:
             if (value < 0) return fail(FA_EINVAL, "fa_tune: store-window length in ticks >= 0");
@@ -2912,6 +2942,19 @@ int fa_tune(int knob, int value) {
         case FA_TUNE_OPT_WIN_MODE:
             if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: store-window mode 0, 1 or 2");
             g_cfg.opt_win_mode = value;
+            return FA_OK;
+        case FA_TUNE_AVG_WIN_PERIOD:
+            if (value != 0 && (value < 64 || value > (1 << 24)))
+                return fail(FA_EINVAL, "fa_tune: store-window period 64 .. 2^24 ticks of 10 ns (0 = off)");
+            g_cfg.avg_win_period = value;
+            return FA_OK;
+        case FA_TUNE_AVG_WIN_W:
+            if (value < 0) return fail(FA_EINVAL, "fa_tune: store-window length in ticks >= 0");
+            g_cfg.avg_win_w = value;
+            return FA_OK;
+        case FA_TUNE_AVG_WIN_MODE:
+            if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: store-window mode 0, 1 or 2");
+            g_cfg.avg_win_mode = value;
             return FA_OK;
         case FA_TUNE_OPT_BURST:
             if (value != 0 && value != 1 && value != 2 && value != 4)

@@ -407,8 +407,9 @@ _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _a
           "lds": _abi.FA_TUNE_LDS, "wpe": _abi.FA_TUNE_WPE,
           "opt_mv": _abi.FA_TUNE_OPT_MV, "auto_geom": _abi.FA_TUNE_AUTO_GEOM,
           "opt_mix": _abi.FA_TUNE_OPT_MIX, "opt_burst": _abi.FA_TUNE_OPT_BURST,
-          "opt_g": _abi.FA_TUNE_OPT_G, "opt_win_log": _abi.FA_TUNE_OPT_WIN_LOG, "opt_win_w": _abi.FA_TUNE_OPT_WIN_W,
-          "opt_win_mode": _abi.FA_TUNE_OPT_WIN_MODE}
+          "opt_g": _abi.FA_TUNE_OPT_G, "opt_win_period": _abi.FA_TUNE_OPT_WIN_PERIOD, "opt_win_w": _abi.FA_TUNE_OPT_WIN_W,
+          "opt_win_mode": _abi.FA_TUNE_OPT_WIN_MODE, "avg_win_period": _abi.FA_TUNE_AVG_WIN_PERIOD,
+          "avg_win_w": _abi.FA_TUNE_AVG_WIN_W, "avg_win_mode": _abi.FA_TUNE_AVG_WIN_MODE}
 
 
 def tune(**knobs):

@@ -82,12 +82,17 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                     FA_TUNE_OPT_G = 23 /* FedOpt FINAL launches over an fp64 model with fp64 state out: the
                                           product arithmetic with G = 1, 2 or 4 wave tiles per wave and their
                                           v / out / m stored after the last tile's reads (0 = off) */,
-                    FA_TUNE_OPT_WIN_LOG = 24 /* FedOpt FIRST|FINAL, clock-windowed store probe (fp64 m out):
+                    FA_TUNE_OPT_WIN_PERIOD = 24 /* FedOpt FIRST|FINAL, clock-windowed store probe (fp64 m out):
                                                 k_fedopt_mix's pattern with every store issued only while the
-                                                100 MHz reference clock mod 2^value < OPT_WIN_W (6..24; 0 = off) */,
+                                                100 MHz reference clock mod value < OPT_WIN_W
+                                                (period in 10-ns ticks, 64 .. 2^24; 0 = off) */,
                     FA_TUNE_OPT_WIN_W = 25 /* the store window in 10-ns ticks */,
                     FA_TUNE_OPT_WIN_MODE = 26 /* 0: gate the stores only; 1: also start a tile's reads outside
-                                                 the window; 2: also every client batch's reads */ };
+                                                 the window; 2: also every client batch's reads */,
+                    FA_TUNE_AVG_WIN_PERIOD = 27 /* FedAvg fp32 k_fedavg_pipe (the headline instantiation): the same
+                                                store window for its stores (bit-identical results) */,
+                    FA_TUNE_AVG_WIN_W = 28,
+                    FA_TUNE_AVG_WIN_MODE = 29 };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);

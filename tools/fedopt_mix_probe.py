@@ -35,8 +35,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--burst", default="1,2,4", help="burst-store probe G values (tiles per wave), '' = none")
     ap.add_argument("--opt-g", default="1,2,4", help="product step with G tiles per wave (fa_tune OPT_G), '' = none")
-    ap.add_argument("--win", default="", help="clock-windowed store probe: log2period:window_ticks:mode,... "
-                    "(fa_tune OPT_WIN_*: stores only while the 100 MHz clock mod 2^log2period < window)")
+    ap.add_argument("--win", default="", help="clock-windowed store probe: period_ticks:window_ticks:mode,... "
+                    "(fa_tune OPT_WIN_*: stores only while the 100 MHz clock mod period < window)")
     a = ap.parse_args()
     _abi.use_probe()
     dev = torch.device("cuda", 0)
@@ -105,10 +105,10 @@ def main():
             for lg, w, mode in wins:              # stores confined to a chip-wide clock window
                 if name != "steady":
                     continue
-                ops.tune(opt_win_log=lg, opt_win_w=w, opt_win_mode=mode)
+                ops.tune(opt_win_period=lg, opt_win_w=w, opt_win_mode=mode)
                 fn()
                 res.setdefault((name, f"win{lg}_{w}_{mode}"), []).append(median_ms(fn))
-            ops.tune(opt_win_log=0)
+            ops.tune(opt_win_period=0)
         ops.tune(opt_mix=0)
         ops.stream_copy(dst, src)
         res.setdefault(("copy", 0), []).append(median_ms(lambda: ops.stream_copy(dst, src)))

@@ -132,7 +132,7 @@ for s in $STEPS; do
     winprobe)
       # FedAdam steady state with the chip's stores confined to a common clock window (probe library)
       timeout -k 10 600 python tools/fedopt_mix_probe.py --burst "" --opt-g "" \
-        --win "${FEDN_AMD_WIN:-13:1200:0,13:1200:2,13:800:2,13:1600:2,14:1600:2,14:2400:2,14:3200:2,15:3200:2,15:4800:2,16:9600:2}" \
+        --win "${FEDN_AMD_WIN:-8192:1200:0,9000:1200:0,10000:1400:0,11000:1500:0,12000:1600:0,13000:1800:0,14000:2000:0,12000:1000:0,12000:2400:0,12000:1600:2}" \
         > "$OUT/winprobe.log" 2>&1; rc=$?
       echo "winprobe rc=$rc"; cut -c1-1200 "$OUT/winprobe.log" | tail -3; [ $rc -eq 0 ] || exit $rc ;;
     mixprobe)
