@@ -636,9 +636,19 @@ struct LaneTable {
 // clock mod period < win_w, reads (optionally) only outside that window: the DRAM then sees
 // read-only stretches and write bursts instead of writes interleaved everywhere, with no grid
 // barrier. A wait gives up after 2^18 polls, far past one period, should the clock stand still.
+// (the clock's low 32 bits: one irregular period every 43 s where they wrap; the remainder by a
+// power-of-two period is a mask, otherwise a multiply-high by floor(2^32 / period) and one correction)
 [[maybe_unused]] __device__ __forceinline__ bool in_write_window(uint32_t period, uint32_t win_w) {
-    const uint64_t t = __builtin_amdgcn_s_memrealtime();
-    return (uint32_t)(t % period) < win_w;
+    const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    uint32_t r;
+    if ((period & (period - 1)) == 0) {
+        r = t & (period - 1);
+    } else {
+        const uint32_t recip = 0xFFFFFFFFu / period;   // uniform: the compiler keeps it out of the poll loop
+        r = t - __umulhi(t, recip) * period;
+        if (r >= period) r -= period;
+    }
+    return r < win_w;
 }
 // (a wait gives up after 2^18 polls, far past one period, should the clock ever stand still)
 [[maybe_unused]] __device__ __forceinline__ void wait_write_window(uint32_t period, uint32_t win_w) {

@@ -132,9 +132,13 @@ for s in $STEPS; do
     winprobe)
       # FedAdam steady state with the chip's stores confined to a common clock window (probe library)
       timeout -k 10 600 python tools/fedopt_mix_probe.py --burst "" --opt-g "" \
-        --win "${FEDN_AMD_WIN:-8192:1200:0,9000:1200:0,10000:1400:0,11000:1500:0,12000:1600:0,13000:1800:0,14000:2000:0,12000:1000:0,12000:2400:0,12000:1600:2}" \
+        --win "${FEDN_AMD_WIN:-8192:1200:0,8191:1200:0,8192:1200:2,10000:1400:0,12000:1600:0,14000:2000:0,16384:2400:0,12000:1000:0,12000:2400:0}" \
         > "$OUT/winprobe.log" 2>&1; rc=$?
       echo "winprobe rc=$rc"; cut -c1-1200 "$OUT/winprobe.log" | tail -3; [ $rc -eq 0 ] || exit $rc ;;
+    avgwin)
+      # FedAvg's fold (64 and 8 x 100 M fp32) with its stores in a chip-wide clock window (probe library)
+      timeout -k 10 600 python tools/window_probe.py ${FEDN_AMD_AVGWIN:+--win "$FEDN_AMD_AVGWIN"} > "$OUT/avgwin.log" 2>&1; rc=$?
+      echo "avgwin rc=$rc"; cut -c1-1500 "$OUT/avgwin.log" | grep -v amdgpu.ids | tail -3; [ $rc -eq 0 ] || exit $rc ;;
     mixprobe)
       timeout -k 10 600 python tools/fedopt_mix_probe.py > "$OUT/mixprobe.log" 2>&1; rc=$?
       echo "mixprobe rc=$rc"; cut -c1-700 "$OUT/mixprobe.log" | tail -4; [ $rc -eq 0 ] || exit $rc ;;
