@@ -102,13 +102,27 @@ def kernels_matching(lib_path, kernel):
     return sorted(picked + [m + ".kd" for m in picked if m + ".kd" in syms])
 
 
+# amd_kernel_code_t / kernel descriptor: bytes 16-23 hold kernel_code_entry_byte_offset, the distance
+# from the descriptor to the kernel's code — where the linker placed the two, not the kernel (adding a
+# kernel elsewhere in the library moves it). The rest (segment sizes, register and mode settings)
+# describe the kernel and stay in the key.
+_KD_ENTRY_OFFSET = slice(16, 24)
+
+
+def _keyed(name, data):
+    if name.endswith(".kd") and len(data) >= _KD_ENTRY_OFFSET.stop:
+        data = data[:_KD_ENTRY_OFFSET.start] + bytes(8) + data[_KD_ENTRY_OFFSET.stop:]
+    return data
+
+
 def kernel_sha(lib_path, names):
     """sha256 (16 hex) over the machine code and descriptors of ``names`` (mangled, as
-    :func:`kernels_matching` lists them) in the gfx950 code object; None if one is missing."""
+    :func:`kernels_matching` lists them) in the gfx950 code object — the descriptors without their
+    layout-dependent code offset; None if one is missing."""
     syms = symbols(gfx950_code_object(lib_path))
     h = hashlib.sha256()
     for n in sorted(names):
         if n not in syms:
             return None
-        h.update(n.encode() + b"\0" + syms[n])
+        h.update(n.encode() + b"\0" + _keyed(n, syms[n]))
     return h.hexdigest()[:16]

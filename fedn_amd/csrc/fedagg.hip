@@ -1076,10 +1076,11 @@ __device__ __forceinline__ void fedopt_strip(const OptBuffers& b, const OptScala
 // contiguous 1 KiB per wave instruction (full 128-B lines, no half-line stores) and the client loads
 // are contiguous 512-B dwordx2 wave instructions. Whole wave tiles only.
 template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM = 0, int NH = 2,
-          int U = kUnroll / 2>
+          int U = kUnroll / 2, bool WIN = false>
 __device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const OptScalars& s,
                                                    const ClientTable<typename PG::S>& tab, const int K,
-                                                   const int64_t i0) {
+                                                   const int64_t i0, const uint32_t period = 0,
+                                                   const uint32_t win_w = 0) {
     using V = typename PG::V;
     constexpr int H = 2, E = H * NH;
     auto half = [](auto& a, int h) -> auto& {
@@ -1148,15 +1149,18 @@ __device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const Op
         double mi[E], vv[E];
 #pragma unroll
         for (int h = 0; h < NH; ++h) opt_load_state<H>(b, s, at(h), H, half(mi, h), half(vv, h));
+        if constexpr (WIN) wait_write_window(period, win_w);   // the state loads land meanwhile
 #pragma unroll
         for (int h = 0; h < NH; ++h)
             opt_apply<PG, H, false, OSM>(b, s, half(pg, h), half(ov, h), half(mi, h), half(vv, h), at(h), H);
     }
 }
 
-template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM, int NH, int U, bool MV = false>
+template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM, int NH, int U, bool MV = false,
+          bool WIN = false>
 __device__ __forceinline__ void fedopt_c_body(const OptBuffers& b, const OptScalars& s, const ClientTable<typename PG::S>& tab,
-                                              const int K, const int64_t P) {
+                                              const int K, const int64_t P, const uint32_t period = 0,
+                                              const uint32_t win_w = 0) {
     constexpr int64_t T = 128 * NH;                                     // elements per wave tile
     const int64_t base = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * T;
     const int lane = threadIdx.x & 63;
@@ -1173,7 +1177,7 @@ __device__ __forceinline__ void fedopt_c_body(const OptBuffers& b, const OptScal
         return;
     }
     if (base + T <= P) {
-        fedopt_strip_split<Y, OLD, PG, FIRST, FINAL, NT, OSM, NH, U>(b, s, tab, K, base + 2 * lane);
+        fedopt_strip_split<Y, OLD, PG, FIRST, FINAL, NT, OSM, NH, U, WIN>(b, s, tab, K, base + 2 * lane, period, win_w);
     } else {                                      // the ragged last tile: the per-lane strip map
 #pragma unroll
         for (int j = 0; j < NH / 2; ++j) {
@@ -1353,6 +1357,19 @@ template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, i
 __global__ void __launch_bounds__(kBlock)
 k_fedopt_c(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
     fedopt_c_body<Y, OLD, PG, FIRST, FINAL, NT, OSM, NH, U>(b, s, tab, K, P);
+}
+
+// The same single-launch step (all K clients, FIRST | FINAL) with every wave's v / out / m stores
+// issued inside a chip-wide window of the GPU's 100 MHz reference clock (clock mod period < win_w;
+// opt_window() sizes both from the launch's bytes per round of resident waves). Reads continue
+// throughout; the stores of all waves bunch into common bursts instead of interleaving with 36
+// read streams everywhere — fewer DRAM read/write turnarounds (profiles/r05_fedopt_window.log).
+// Arithmetic and element map are k_fedopt_c's: bit-identical results.
+template <typename Y, typename OLD, class PG, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_cw(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P,
+            const uint32_t period, const uint32_t win_w) {
+    fedopt_c_body<Y, OLD, PG, true, true, NT, 1, 4, kUnroll / 2, false, true>(b, s, tab, K, P, period, win_w);
 }
 
 #ifdef FEDAGG_PROBES
@@ -1876,7 +1893,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0}, opt_burst{0}, opt_g{0}, opt_win_period{0}, opt_win_w{0}, opt_win_mode{0}, avg_win_period{0}, avg_win_w{0}, avg_win_mode{0};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0}, opt_burst{0}, opt_g{0}, opt_win_period{0}, opt_win_w{0}, opt_win_mode{0}, avg_win_period{0}, avg_win_w{0}, avg_win_mode{0}, opt_win_prod{0};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -1931,6 +1948,42 @@ int device_cus() {
         cus = 256;
     return cus > 0 ? cus : 256;
 }
+
+// The chip-wide store window of a single-launch FedOpt step (k_fedopt_cw), in 10-ns ticks of the
+// reference clock. The period is 0.65 of the time one round of resident waves takes to stream its
+// tiles at 6.4 TB/s — shorter than a round, so no wave idles a whole period for its window (periods
+// past ~1.5 rounds leave waves waiting: 1.3-2x slower, profiles/r05_fedopt_window.log) — and the
+// window is the launch's write share plus 15 % of it (8-30 %). {0, 0}: no window — under 8 clients,
+// models under 2^24 elements, or write shares over 25 %, where it was not measured.
+struct StoreWindow {
+    uint32_t period = 0, w = 0;
+};
+template <typename Y, typename OLD, class PG, bool NT>
+StoreWindow opt_store_window(const OptBuffers& b, int K, int64_t P) {
+    if (K < 8 || P < ((int64_t)1 << 24)) return {};
+    static std::atomic<int> blocks_per_cu{-1};            // resident workgroups per CU, per instantiation
+    int nb = blocks_per_cu.load(std::memory_order_relaxed);
+    if (nb < 0) {
+        nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_fedopt_cw<Y, OLD, PG, NT>, kBlock, 0) != hipSuccess) nb = 0;
+        blocks_per_cu.store(nb, std::memory_order_relaxed);
+    }
+    if (nb <= 0) return {};
+    const double waves = (double)nb * (kBlock / 64) * device_cus();
+    const double m_in = b.m_in_f64 == 1 ? 8 : b.m_in_f64 == 0 ? 4 : b.m_in_f64 < 0 ? 0 : 2;
+    const double m_out = b.m_out_f64 == 1 ? 8 : b.m_out_f64 == 0 ? 4 : 2;
+    const double rd = (double)K * sizeof(Y) + sizeof(OLD) + m_in + (b.v_in ? (b.v_in_f32 ? 4 : 8) : 0);
+    const double wr = (b.out_f32 ? 4 : 8) + (b.v_out_f32 ? 4 : 8) + m_out;
+    const double frac = wr / (rd + wr);
+    if (frac > 0.25) return {};
+    const double period = 0.65 * waves * 512.0 * (rd + wr) / 6.4e12 * 1e8;
+    if (period < 1000 || period > 20000) return {};
+    StoreWindow sw;
+    sw.period = (uint32_t)period;
+    sw.w = (uint32_t)(period * std::min(0.30, std::max(0.08, 1.15 * frac)));
+    return sw;
+}
+
 
 template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT, int BLK = kBlock, int NTS = 0, int MAP = 0>
 void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
@@ -2156,7 +2209,7 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
             }
             return check_launch("fa_fedopt_step: kernel launch");
         }
-        if (first && final_ && g_cfg.opt_win_period) {
+        if (first && final_ && g_cfg.opt_win_period > 0 && !g_cfg.opt_win_prod) {
             if (b.m_out_f64 != 1) return fail(FA_EINVAL, "fa_tune OPT_WIN probe: fp64 m out");
             const dim3 gw((unsigned)((P + 4 * 512 - 1) / (4 * 512)));   // a ragged last tile is skipped
             hipLaunchKernelGGL((k_fedopt_mixw<Y, OLD, typename PG::S, NT>), gw, dim3(kBlock), 0, st, b, tab, cnt, P,
@@ -2210,12 +2263,27 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
                 FA_WPE(6) FA_WPE(8)
 #undef FA_WPE
                 default:
-                    hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1, 4>), g4, dim3(kBlock), shm, st, b, s, tab, cnt, P);
-                    return check_launch("fa_fedopt_step: kernel launch");
+                    if (shm) {
+                        hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1, 4>), g4, dim3(kBlock), shm, st, b, s, tab, cnt, P);
+                        return check_launch("fa_fedopt_step: kernel launch");
+                    }
+                    break;                                  // the product's own choice below
             }
         }
         }
 #endif
+        if (first && final_) {
+            StoreWindow sw = opt_store_window<Y, OLD, PG, NT>(b, cnt, P);
+#ifdef FEDAGG_PROBES
+            if (g_cfg.opt_win_period < 0) sw = StoreWindow{};                                 // A/B: no window
+            else if (g_cfg.opt_win_period > 0 && g_cfg.opt_win_prod) sw = StoreWindow{(uint32_t)g_cfg.opt_win_period.load(),
+                                                                                          (uint32_t)g_cfg.opt_win_w.load()};
+#endif
+            if (sw.period) {
+                hipLaunchKernelGGL((k_fedopt_cw<Y, OLD, PG, NT>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P, sw.period, sw.w);
+                return check_launch("fa_fedopt_step: kernel launch");
+            }
+        }
         if (first && final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
         else if (first) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, false, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
         else if (final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, false, true, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
@@ -2941,8 +3009,8 @@ int fa_tune(int knob, int value) {
             g_cfg.opt_g = value;
             return FA_OK;
         case FA_TUNE_OPT_WIN_PERIOD:
-            if (value != 0 && (value < 64 || value > (1 << 24)))
-                return fail(FA_EINVAL, "fa_tune: store-window period 64 .. 2^24 ticks of 10 ns (0 = off)");
+            if (value != 0 && value != -1 && (value < 64 || value > (1 << 24)))
+                return fail(FA_EINVAL, "fa_tune: store-window period 64 .. 2^24 ticks of 10 ns (0 = the product's own, -1 = none)");
             g_cfg.opt_win_period = value;
             return FA_OK;
         case FA_TUNE_OPT_WIN_W:
@@ -2952,6 +3020,9 @@ int fa_tune(int knob, int value) {
         case FA_TUNE_OPT_WIN_MODE:
             if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: store-window mode 0, 1 or 2");
             g_cfg.opt_win_mode = value;
+            return FA_OK;
+        case FA_TUNE_OPT_WIN_PROD:
+            g_cfg.opt_win_prod = value ? 1 : 0;
             return FA_OK;
         case FA_TUNE_AVG_WIN_PERIOD:
             if (value != 0 && (value < 64 || value > (1 << 24)))

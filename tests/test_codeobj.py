@@ -16,6 +16,9 @@ from fedn_amd import codeobj
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = r'''
 #include <hip/hip_runtime.h>
+#ifdef EXTRA
+__global__ void k_extra(double* x, int n) { int i = blockIdx.x * blockDim.x + threadIdx.x; if (i < n) x[i] = x[i] * x[i] + 1.0; }
+#endif
 __global__ void k_scale(float* x, float a, int n) { int i = blockIdx.x * blockDim.x + threadIdx.x; if (i < n) x[i] *= a; }
 __global__ void k_other(float* x, int n) { int i = blockIdx.x * blockDim.x + threadIdx.x; if (i < n) x[i] += OTHER; }
 extern "C" int launch(float* x, int n) { hipLaunchKernelGGL(k_scale, dim3((n + 255) / 256), dim3(256), 0, 0, x, 2.0f, n); return 0; }
@@ -29,13 +32,13 @@ def _hipcc():
     pytest.skip("hipcc not found")
 
 
-def _build(tmp, sub, other):
+def _build(tmp, sub, other, extra=False):
     d = tmp / sub
     d.mkdir(parents=True)
     (d / "k.hip").write_text(SRC)
     out = d / "libk.so"
-    subprocess.run([_hipcc(), "-O3", "-fPIC", "-shared", "--offload-arch=gfx950", f"-DOTHER={other}", "-o", str(out),
-                    "k.hip"], cwd=d, check=True, capture_output=True)
+    subprocess.run([_hipcc(), "-O3", "-fPIC", "-shared", "--offload-arch=gfx950", f"-DOTHER={other}", "-o", str(out)]
+                   + (["-DEXTRA"] if extra else []) + ["k.hip"], cwd=d, check=True, capture_output=True)
     return str(out)
 
 
@@ -54,6 +57,14 @@ def test_two_build_paths_one_kernel_key(tmp_path):
     no = codeobj.kernels_matching(a, "k_other")
     assert codeobj.kernel_sha(a, no) == codeobj.kernel_sha(b, no) != codeobj.kernel_sha(c, no)
     assert codeobj.kernel_sha(a, ["not_a_kernel"]) is None
+    # a kernel added elsewhere moves the others in the code object (their descriptors' code offset),
+    # not their code: the measured kernels keep their key
+    e = _build(tmp_path, "extra", "1.0f", extra=True)
+    assert codeobj.kernels_matching(e, "k_scale") == na and codeobj.kernels_matching(e, "k_extra")
+    kd = [n for n in na if n.endswith(".kd")][0]
+    raw = [codeobj.symbols(codeobj.gfx950_code_object(x))[kd] for x in (a, e)]
+    assert all(raw[0][i] == raw[1][i] for i in range(len(raw[0])) if not 16 <= i < 24)
+    assert codeobj.kernel_sha(e, na) == codeobj.kernel_sha(a, na)
 
 
 def test_shipped_pmc_entries_match_the_in_tree_library():

@@ -135,6 +135,10 @@ for s in $STEPS; do
         --win "${FEDN_AMD_WIN:-8192:1200:0,8191:1200:0,8192:1200:2,10000:1400:0,12000:1600:0,14000:2000:0,16384:2400:0,12000:1000:0,12000:2400:0}" \
         > "$OUT/winprobe.log" 2>&1; rc=$?
       echo "winprobe rc=$rc"; cut -c1-1200 "$OUT/winprobe.log" | tail -3; [ $rc -eq 0 ] || exit $rc ;;
+    optwin)
+      # FedAdam through the product step with / without the chip-wide store window (probe library)
+      timeout -k 10 900 python tools/fedopt_window_probe.py ${FEDN_AMD_OPTWIN:+--winprod "$FEDN_AMD_OPTWIN"} > "$OUT/optwin.log" 2>&1; rc=$?
+      echo "optwin rc=$rc"; cut -c1-900 "$OUT/optwin.log" | grep -v amdgpu.ids | tail -6; [ $rc -eq 0 ] || exit $rc ;;
     avgwin)
       # FedAvg's fold (64 and 8 x 100 M fp32) with its stores in a chip-wide clock window (probe library)
       timeout -k 10 600 python tools/window_probe.py ${FEDN_AMD_AVGWIN:+--win "$FEDN_AMD_AVGWIN"} > "$OUT/avgwin.log" 2>&1; rc=$?
