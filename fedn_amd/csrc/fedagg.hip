@@ -1247,9 +1247,10 @@ __device__ __forceinline__ void opt_compute_p(const OptBuffers& b, const OptScal
     }
 }
 
-template <typename Y, typename OLD, class PG, bool FIRST, bool NT, int G>
-__global__ void __launch_bounds__(kBlock)
-k_fedopt_cg(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
+template <typename Y, typename OLD, class PG, bool FIRST, bool NT, int G, bool WIN = false>
+__device__ __forceinline__ void fedopt_cg_body(const OptBuffers& b, const OptScalars& s, const ClientTable<typename PG::S>& tab,
+                                               const int K, const int64_t P, const uint32_t period = 0,
+                                               const uint32_t win_w = 0) {
     using V = typename PG::V;
     constexpr int NH = 4, H = 2, E = H * NH, U = kUnroll / 2;
     constexpr int64_t T = 128 * NH;
@@ -1334,6 +1335,7 @@ k_fedopt_cg(const OptBuffers b, const OptScalars s, const ClientTable<typename P
         for (int h = 0; h < NH; ++h)
             opt_compute_p<PG, H>(b, s, half(pg, h), half(ov, h), half(mi, h), half(vo[g], h), half(mo[g], h), half(oo[g], h));
     }
+    if constexpr (WIN) wait_write_window(period, win_w);      // everything computed: only the stores wait
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         const int64_t i0 = (wave * G + g) * T + 2 * lane;
@@ -1349,6 +1351,22 @@ k_fedopt_cg(const OptBuffers b, const OptScalars s, const ClientTable<typename P
             strip_store<double, H, 1>(static_cast<double*>(b.m_out) + o, *reinterpret_cast<double(*)[H]>(mp));
         }
     }
+}
+
+template <typename Y, typename OLD, class PG, bool FIRST, bool NT, int G>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_cg(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
+    fedopt_cg_body<Y, OLD, PG, FIRST, NT, G>(b, s, tab, K, P);
+}
+
+// store-window probe on the compute-then-store order (OPT_WIN_PROD = 2): one tile per wave, its
+// v / out / m computed first and stored inside the window (k_fedopt_cw waits before opt_apply, so
+// its fp64 square roots and divisions run inside the window)
+template <typename Y, typename OLD, class PG, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_cgw(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P,
+             const uint32_t period, const uint32_t win_w) {
+    fedopt_cg_body<Y, OLD, PG, true, NT, 1, true>(b, s, tab, K, P, period, win_w);
 }
 #endif
 
@@ -2279,6 +2297,16 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
             else if (g_cfg.opt_win_period > 0 && g_cfg.opt_win_prod) sw = StoreWindow{(uint32_t)g_cfg.opt_win_period.load(),
                                                                                           (uint32_t)g_cfg.opt_win_w.load()};
 #endif
+#ifdef FEDAGG_PROBES
+            if constexpr (probe_combo) {
+                if (sw.period && g_cfg.opt_win_prod == 2) {
+                    if (b.m_out_f64 != 1 || b.v_out_f32 || b.out_f32 || (b.v_in && b.v_in_f32))
+                        return fail(FA_EINVAL, "fa_tune OPT_WIN_PROD 2: fp64 m / v / model out");
+                    hipLaunchKernelGGL((k_fedopt_cgw<Y, OLD, PG, NT>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P, sw.period, sw.w);
+                    return check_launch("fa_fedopt_step: kernel launch");
+                }
+            }
+#endif
             if (sw.period) {
                 hipLaunchKernelGGL((k_fedopt_cw<Y, OLD, PG, NT>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P, sw.period, sw.w);
                 return check_launch("fa_fedopt_step: kernel launch");
@@ -3022,7 +3050,8 @@ int fa_tune(int knob, int value) {
             g_cfg.opt_win_mode = value;
             return FA_OK;
         case FA_TUNE_OPT_WIN_PROD:
-            g_cfg.opt_win_prod = value ? 1 : 0;
+            if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: OPT_WIN_PROD 0 (pattern probe), 1 (k_fedopt_cw), 2 (k_fedopt_cgw)");
+            g_cfg.opt_win_prod = value;
             return FA_OK;
         case FA_TUNE_AVG_WIN_PERIOD:
             if (value != 0 && (value < 64 || value > (1 << 24)))

@@ -36,11 +36,13 @@ def main():
     ap.add_argument("--clients", default="32,16,8")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--winprod", default="3000:450,4500:680,6000:900,8192:1200")
+    ap.add_argument("--wincg", default="", help="the compute-then-store kernel k_fedopt_cgw (OPT_WIN_PROD 2): period:w,...")
     a = ap.parse_args()
     _abi.use_probe()
     dev = torch.device("cuda", 0)
     P = a.params
     explicit = [tuple(int(v) for v in x.split(":")) for x in a.winprod.split(",") if x]
+    cg = [tuple(int(v) for v in x.split(":")) for x in a.wincg.split(",") if x]
     g = torch.Generator(device=dev).manual_seed(4)
     old32 = torch.randn(P, generator=g, device=dev)
     Kmax = max(int(k) for k in a.clients.split(","))
@@ -57,6 +59,8 @@ def main():
         yield "product", dict(opt_win_period=0, opt_win_prod=0)
         for p_, w_ in explicit:
             yield f"win{p_}_{w_}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=1)
+        for p_, w_ in cg:
+            yield f"cgw{p_}_{w_}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=2)
 
     for K in (int(k) for k in a.clients.split(",")):
         ns = [int(x) for x in np.random.default_rng(K).integers(1, 5001, K)]
