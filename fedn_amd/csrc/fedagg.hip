@@ -1970,15 +1970,18 @@ int device_cus() {
 // The chip-wide store window of a single-launch FedOpt step (k_fedopt_cw), in 10-ns ticks of the
 // reference clock. The period is 0.65 of the time one round of resident waves takes to stream its
 // tiles at 6.4 TB/s — shorter than a round, so no wave idles a whole period for its window (periods
-// past ~1.5 rounds leave waves waiting: 1.3-2x slower, profiles/r05_fedopt_window.log) — and the
-// window is the launch's write share plus 15 % of it (8-30 %). {0, 0}: no window — under 8 clients,
-// models under 2^24 elements, or write shares over 25 %, where it was not measured.
+// past ~1.5 rounds leave waves waiting: 1.3-2x slower) — and the window is the launch's write share
+// plus 15 % of it (8-30 %). Measured (profiles/r05_fedopt_window_product.log, bit-exact): a launch
+// that reads no optimizer state (a session's first round) runs 10-11 % faster at K = 32 and 4 % at
+// K = 16; one that reads m and v (the steady state) gains at most 5 % at K = 32 with a hand-picked
+// period and loses at K = 16, so it keeps k_fedopt_c. {0, 0}: no window — state read, under 8
+// clients, models under 2^24 elements, or write shares over 25 %.
 struct StoreWindow {
     uint32_t period = 0, w = 0;
 };
 template <typename Y, typename OLD, class PG, bool NT>
 StoreWindow opt_store_window(const OptBuffers& b, int K, int64_t P) {
-    if (K < 8 || P < ((int64_t)1 << 24)) return {};
+    if (K < 8 || P < ((int64_t)1 << 24) || b.m_in_f64 >= 0 || b.v_in) return {};
     static std::atomic<int> blocks_per_cu{-1};            // resident workgroups per CU, per instantiation
     int nb = blocks_per_cu.load(std::memory_order_relaxed);
     if (nb < 0) {

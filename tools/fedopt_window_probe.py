@@ -54,12 +54,12 @@ def main():
     v_o = torch.empty(P, dtype=torch.float64, device=dev)
     o2 = torch.empty(P, dtype=torch.float64, device=dev)
 
-    def variants():
+    def variants(phase=None):
         yield "nowin", dict(opt_win_period=-1, opt_win_prod=0)
         yield "product", dict(opt_win_period=0, opt_win_prod=0)
         for p_, w_ in explicit:
             yield f"win{p_}_{w_}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=1)
-        for p_, w_ in cg:
+        for p_, w_ in cg if phase == "steady" else ():      # fp64 m / v / model out only
             yield f"cgw{p_}_{w_}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=2)
 
     for K in (int(k) for k in a.clients.split(",")):
@@ -80,7 +80,7 @@ def main():
             torch.cuda.synchronize()
             ref = [t.clone() for t in outs]
             exact = {}
-            for vn, kn in variants():
+            for vn, kn in variants(name):
                 ops.tune(**kn)
                 for t in outs:
                     t.zero_()
@@ -89,7 +89,7 @@ def main():
                 exact[vn] = all(torch.equal(x.view(torch.uint8), y.view(torch.uint8)) for x, y in zip(outs, ref))
             res = {}
             for _ in range(a.reps):
-                for vn, kn in variants():
+                for vn, kn in variants(name):
                     ops.tune(**kn)
                     fn()
                     res.setdefault(vn, []).append(median_ms(fn))

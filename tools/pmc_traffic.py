@@ -88,9 +88,9 @@ def record(d, key, kernel, alg=None, session=None, take=None):
 P, Q = 100_000_000, 350_000_000
 SESSION = [
     ("pmc1", f"fedavg_k64_p{P}_f32", "k_fedavg_pipe<float, float", 64 * P * 4 + P * 4),
-    # bench.py's fedopt field runs round 1 (12 launches) before its fp32-state phase (12 more), both
-    # k_fedopt_c<float, float, CF32, FIRST, FINAL>: round 1 is the first 12 dispatches
-    ("pmc1", f"fedopt_adam_round1_k32_p{Q}", "k_fedopt_c<float, float", 32 * Q * 4 + Q * 24, (0, 12)),
+    # bench.py's fedopt field: round 1 (12 launches) is k_fedopt_cw<float, float, CF32> (no state read:
+    # the store window), its fp32-state phase k_fedopt_c<float, float, CF32>
+    ("pmc1", f"fedopt_adam_round1_k32_p{Q}", "k_fedopt_cw<float, float", 32 * Q * 4 + Q * 24),
     ("pmc1", f"fedopt_adam_steady_k32_p{Q}", "k_fedopt_c<float, double", Q * (4 * 32 + 48)),
     ("pmc2", f"fedavg_k8_p{P}_f32", "k_fedavg_pipe<float, float", 8 * P * 4 + P * 4),
     ("pmc3", f"fedavg_k64_p{P}_bf16", "bf16, float", 64 * P * 2 + P * 4),
