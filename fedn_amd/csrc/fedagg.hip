@@ -1359,6 +1359,15 @@ k_fedopt_cg(const OptBuffers b, const OptScalars s, const ClientTable<typename P
     fedopt_cg_body<Y, OLD, PG, FIRST, NT, G>(b, s, tab, K, P);
 }
 
+// the windowed product step compiled for at least W waves per SIMD (FA_TUNE_WPE with a window): the
+// waves idling for their window need other waves resident to keep the reads flowing
+template <typename Y, typename OLD, class PG, bool NT, int W>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W)))
+k_fedopt_cw_w(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P,
+              const uint32_t period, const uint32_t win_w) {
+    fedopt_c_body<Y, OLD, PG, true, true, NT, 1, 4, kUnroll / 2, false, true>(b, s, tab, K, P, period, win_w);
+}
+
 // store-window probe on the compute-then-store order (OPT_WIN_PROD = 2): one tile per wave, its
 // v / out / m computed first and stored inside the window (k_fedopt_cw waits before opt_apply, so
 // its fp64 square roots and divisions run inside the window)
@@ -2276,7 +2285,7 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
             hipLaunchKernelGGL((k_fedopt_c_mv<Y, OLD, PG, NT>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
             return check_launch("fa_fedopt_step: kernel launch");
         }
-        if (first && final_) {
+        if (first && final_ && !(g_cfg.opt_win_period > 0 && g_cfg.opt_win_prod)) {   // (a window: below)
             switch (g_cfg.wpe) {
 #define FA_WPE(W_) \
     case W_: hipLaunchKernelGGL((k_fedopt_c_w<Y, OLD, PG, true, true, NT, 1, 4, kUnroll / 2, W_>), g4, dim3(kBlock), shm, st, b, s, tab, cnt, P); \
@@ -2302,6 +2311,13 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
 #endif
 #ifdef FEDAGG_PROBES
             if constexpr (probe_combo) {
+                if (sw.period && g_cfg.opt_win_prod == 1 && (g_cfg.wpe == 6 || g_cfg.wpe == 7)) {
+                    if (g_cfg.wpe == 6)
+                        hipLaunchKernelGGL((k_fedopt_cw_w<Y, OLD, PG, NT, 6>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P, sw.period, sw.w);
+                    else
+                        hipLaunchKernelGGL((k_fedopt_cw_w<Y, OLD, PG, NT, 7>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P, sw.period, sw.w);
+                    return check_launch("fa_fedopt_step: kernel launch");
+                }
                 if (sw.period && g_cfg.opt_win_prod == 2) {
                     if (b.m_out_f64 != 1 || b.v_out_f32 || b.out_f32 || (b.v_in && b.v_in_f32))
                         return fail(FA_EINVAL, "fa_tune OPT_WIN_PROD 2: fp64 m / v / model out");
@@ -3075,8 +3091,8 @@ int fa_tune(int knob, int value) {
             g_cfg.opt_burst = value;
             return FA_OK;
         case FA_TUNE_WPE:
-            if (value != 0 && value != 5 && value != 6 && value != 8)
-                return fail(FA_EINVAL, "fa_tune: waves per SIMD 0 (compiler's choice), 5, 6 or 8");
+            if (value != 0 && value != 5 && value != 6 && value != 7 && value != 8)
+                return fail(FA_EINVAL, "fa_tune: waves per SIMD 0 (compiler's choice), 5, 6, 7 or 8");
             g_cfg.wpe = value;
             return FA_OK;
         default:

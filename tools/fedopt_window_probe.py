@@ -37,12 +37,14 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--winprod", default="3000:450,4500:680,6000:900,8192:1200")
     ap.add_argument("--wincg", default="", help="the compute-then-store kernel k_fedopt_cgw (OPT_WIN_PROD 2): period:w,...")
+    ap.add_argument("--wpe", default="", help="also the --winprod windows compiled for W waves per SIMD: W,...")
     a = ap.parse_args()
     _abi.use_probe()
     dev = torch.device("cuda", 0)
     P = a.params
     explicit = [tuple(int(v) for v in x.split(":")) for x in a.winprod.split(",") if x]
     cg = [tuple(int(v) for v in x.split(":")) for x in a.wincg.split(",") if x]
+    wpes = [int(x) for x in a.wpe.split(",") if x]
     g = torch.Generator(device=dev).manual_seed(4)
     old32 = torch.randn(P, generator=g, device=dev)
     Kmax = max(int(k) for k in a.clients.split(","))
@@ -55,12 +57,14 @@ def main():
     o2 = torch.empty(P, dtype=torch.float64, device=dev)
 
     def variants(phase=None):
-        yield "nowin", dict(opt_win_period=-1, opt_win_prod=0)
-        yield "product", dict(opt_win_period=0, opt_win_prod=0)
+        yield "nowin", dict(opt_win_period=-1, opt_win_prod=0, wpe=0)
+        yield "product", dict(opt_win_period=0, opt_win_prod=0, wpe=0)
         for p_, w_ in explicit:
-            yield f"win{p_}_{w_}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=1)
+            yield f"win{p_}_{w_}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=1, wpe=0)
+            for W in wpes:
+                yield f"win{p_}_{w_}_wpe{W}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=1, wpe=W)
         for p_, w_ in cg if phase == "steady" else ():      # fp64 m / v / model out only
-            yield f"cgw{p_}_{w_}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=2)
+            yield f"cgw{p_}_{w_}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=2, wpe=0)
 
     for K in (int(k) for k in a.clients.split(",")):
         ns = [int(x) for x in np.random.default_rng(K).integers(1, 5001, K)]
@@ -93,7 +97,7 @@ def main():
                     ops.tune(**kn)
                     fn()
                     res.setdefault(vn, []).append(median_ms(fn))
-            ops.tune(opt_win_period=0, opt_win_prod=0)
+            ops.tune(opt_win_period=0, opt_win_prod=0, wpe=0)
             line = {"clients": K, "phase": name, "params": P, "alg_bytes": alg}
             for vn in res:
                 ms = float(np.median(res[vn]))
