@@ -1977,20 +1977,22 @@ int device_cus() {
 }
 
 // The chip-wide store window of a single-launch FedOpt step (k_fedopt_cw), in 10-ns ticks of the
-// reference clock. The period is 0.65 of the time one round of resident waves takes to stream its
-// tiles at 6.4 TB/s — shorter than a round, so no wave idles a whole period for its window (periods
-// past ~1.5 rounds leave waves waiting: 1.3-2x slower) — and the window is the launch's write share
-// plus 15 % of it (8-30 %). Measured (profiles/r05_fedopt_window_product.log, bit-exact): a launch
-// that reads no optimizer state (a session's first round) runs 10-11 % faster at K = 32 and 4 % at
-// K = 16; one that reads m and v (the steady state) gains at most 5 % at K = 32 with a hand-picked
-// period and loses at K = 16, so it keeps k_fedopt_c. {0, 0}: no window — state read, under 8
-// clients, models under 2^24 elements, or write shares over 25 %.
+// reference clock, from the time one round of resident waves takes to stream its tiles at 6.4 TB/s
+// (periods past ~1.5 rounds leave waves waiting for their window: 1.3-2x slower). Measured
+// (profiles/r05_fedopt_window_product.log, 350 M params, every variant bit-exact):
+//  - a launch that reads no optimizer state (a session's first round): period 0.65 round, window the
+//    write share + 15 % of it: -8...-11 % at K = 32-64, -4...-5 % at K = 16;
+//  - one that reads m and v (the steady state): period 0.35 round, window 15 %: -4...-9 % at K = 32,
+//    -8...-10 % at K = 48 and 64 — but slower at K = 16 at every period tried, so only K >= 32.
+// {0, 0}: no window — under 8 clients (under 32 with state), models under 2^24 elements, write
+// shares over 25 %.
 struct StoreWindow {
     uint32_t period = 0, w = 0;
 };
 template <typename Y, typename OLD, class PG, bool NT>
 StoreWindow opt_store_window(const OptBuffers& b, int K, int64_t P) {
-    if (K < 8 || P < ((int64_t)1 << 24) || b.m_in_f64 >= 0 || b.v_in) return {};
+    const bool state = b.m_in_f64 >= 0 || b.v_in;
+    if (K < (state ? 32 : 8) || P < ((int64_t)1 << 24)) return {};
     static std::atomic<int> blocks_per_cu{-1};            // resident workgroups per CU, per instantiation
     int nb = blocks_per_cu.load(std::memory_order_relaxed);
     if (nb < 0) {
@@ -2006,11 +2008,11 @@ StoreWindow opt_store_window(const OptBuffers& b, int K, int64_t P) {
     const double wr = (b.out_f32 ? 4 : 8) + (b.v_out_f32 ? 4 : 8) + m_out;
     const double frac = wr / (rd + wr);
     if (frac > 0.25) return {};
-    const double period = 0.65 * waves * 512.0 * (rd + wr) / 6.4e12 * 1e8;
+    const double period = (state ? 0.35 : 0.65) * waves * 512.0 * (rd + wr) / 6.4e12 * 1e8;
     if (period < 1000 || period > 20000) return {};
     StoreWindow sw;
     sw.period = (uint32_t)period;
-    sw.w = (uint32_t)(period * std::min(0.30, std::max(0.08, 1.15 * frac)));
+    sw.w = (uint32_t)(period * (state ? 0.15 : std::min(0.30, std::max(0.08, 1.15 * frac))));
     return sw;
 }
 
