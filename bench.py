@@ -499,9 +499,7 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000, pattern_probe=
                       "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
                                    "kernel": ("k_fedopt_cw (pseudo-gradient fold + Adam step fused; 4 coalesced element pairs per "
-                                              "lane; the stores of all waves in a common window of the GPU's 100 MHz clock)"
-                                              if phase == "round1" else
-                                              "k_fedopt_c (pseudo-gradient fold + Adam step fused; 4 coalesced element pairs per lane)"),
+                                              "lane; the stores of all waves in a common window of the GPU's 100 MHz clock)"),
                                    "alg_bytes_per_launch": b},
                       "bit_exact_on_sample": ok,
                       "sample": f"first {S} params of every buffer vs oracle/numpy_ref" +
@@ -515,8 +513,8 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000, pattern_probe=
                 "ms": pattern[phase], "frac": b / pattern[phase] / 1e6 / HBM_PEAK_GBS,
                 "kernel_over_pattern": pattern[phase] / ms,
                 "note": "k_fedopt_mix (libfedagg_probe.so): k_fedopt_c's exact loads and stores with one add per value "
-                        "instead of the arithmetic; the HBM ceiling of this traffic pattern on this box (round 1's "
-                        "k_fedopt_cw times its stores into a chip-wide window the pattern kernel does not: it can beat it)"}
+                        "instead of the arithmetic and no store window; the HBM ceiling of the unwindowed pattern on "
+                        "this box (k_fedopt_cw times its stores into a chip-wide window: it can beat it)"}
     res["config"] = (f"BASELINE configs[3]: FedAdam, {K} device-resident fp32 updates x {P} params, m / v in HBM "
                      "(fedopt.py:151-185), one fused launch per round")
     res["steady_f32state"]["vs_steady_ms"] = ms3 / ms2

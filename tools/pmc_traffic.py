@@ -88,10 +88,11 @@ def record(d, key, kernel, alg=None, session=None, take=None):
 P, Q = 100_000_000, 350_000_000
 SESSION = [
     ("pmc1", f"fedavg_k64_p{P}_f32", "k_fedavg_pipe<float, float", 64 * P * 4 + P * 4),
-    # bench.py's fedopt field: round 1 (12 launches) is k_fedopt_cw<float, float, CF32> (no state read:
-    # the store window), its fp32-state phase k_fedopt_c<float, float, CF32>
-    ("pmc1", f"fedopt_adam_round1_k32_p{Q}", "k_fedopt_cw<float, float", 32 * Q * 4 + Q * 24),
-    ("pmc1", f"fedopt_adam_steady_k32_p{Q}", "k_fedopt_c<float, double", Q * (4 * 32 + 48)),
+    # bench.py's fedopt field: every phase is one windowed launch per round (k_fedopt_cw, K = 32); round 1
+    # (12 launches) and the fp32-state phase (12 more) are both k_fedopt_cw<float, float, CF32>: round 1
+    # is the first 12 dispatches
+    ("pmc1", f"fedopt_adam_round1_k32_p{Q}", "k_fedopt_cw<float, float", 32 * Q * 4 + Q * 24, (0, 12)),
+    ("pmc1", f"fedopt_adam_steady_k32_p{Q}", "k_fedopt_cw<float, double", Q * (4 * 32 + 48)),
     ("pmc2", f"fedavg_k8_p{P}_f32", "k_fedavg_pipe<float, float", 8 * P * 4 + P * 4),
     ("pmc3", f"fedavg_k64_p{P}_bf16", "bf16, float", 64 * P * 2 + P * 4),
 ]
@@ -100,7 +101,7 @@ SESSION = [
 # tools/pmc_workloads.py runs (tools/gpu_session.sh step "pmcx"): (subdir, key, kernel, algorithmic bytes)
 WAVE_BF16 = "k_fedopt_c<(anonymous namespace)::bf16, double, (anonymous namespace)::CF64, "
 X_SESSION = [
-    ("pmcx_f32state", f"fedopt_adam_steady_f32state_k32_p{Q}", "k_fedopt_c<float, float", Q * (4 * 32 + 24)),
+    ("pmcx_f32state", f"fedopt_adam_steady_f32state_k32_p{Q}", "k_fedopt_cw<float, float", Q * (4 * 32 + 24)),
     ("pmcx_waves", "fedyogi_wave_first_p1000000000_w8_bf16", (WAVE_BF16 + "true, false,",), 1_000_000_000 * (2 * 8 + 16)),
     ("pmcx_waves", "fedyogi_wave_mid_p1000000000_w8_bf16", (WAVE_BF16 + "false, false,",), 1_000_000_000 * (2 * 8 + 24)),
     ("pmcx_waves", "fedyogi_wave_final_p1000000000_w8_bf16", (WAVE_BF16 + "false, true,",), 1_000_000_000 * 40),
