@@ -753,8 +753,8 @@ k_fedavg_pipe(X* __restrict__ agg, const ClientTable<typename CP::S> tab, const 
     fedavg_pipe_body<Y, X, CP, E, S, INIT, INT_FIRST, NT, LT, BLK, NTS, MAP>(agg, tab, K, P);
 }
 
-#ifdef FEDAGG_PROBES
-// store-window probe (FA_TUNE_AVG_WIN_*): the same body with the stores in a chip-wide clock window
+// The same fold with every wave's stores inside a chip-wide window of the GPU's 100 MHz clock
+// (avg_store_window): bit-identical, the stores bunched into common bursts.
 template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK, int NTS,
           int MAP>
 __global__ void __launch_bounds__(BLK)
@@ -763,6 +763,7 @@ k_fedavg_pipe_win(X* __restrict__ agg, const ClientTable<typename CP::S> tab, co
     fedavg_pipe_body<Y, X, CP, E, S, INIT, INT_FIRST, NT, LT, BLK, NTS, MAP, true>(agg, tab, K, P, period, win_w, win_mode);
 }
 
+#ifdef FEDAGG_PROBES
 // occupancy probe (FA_TUNE_WPE): the same body compiled for at least W waves per SIMD
 template <typename Y, typename X, class CP, int E, int S, bool INIT, bool INT_FIRST, bool NT, bool LT, int BLK, int NTS,
           int MAP, int W>
@@ -2017,6 +2018,36 @@ StoreWindow opt_store_window(const OptBuffers& b, int K, int64_t P) {
 }
 
 
+// The store window of a first FedAvg launch (k_fedavg_pipe_win), in 10-ns ticks of the reference
+// clock: period 0.35 of the time one round of resident workgroups streams its tiles at 6.4 TB/s,
+// window 15 % — measured (profiles/r05_fedavg_window.log, 100 M fp32, bit-exact) at K = 64: 0.25-0.47
+// round -5...-6 %, one round and longer +2...+22 %; K = 8: 0.34-0.42 round -6 %. {0, 0}: no window
+// (models under 2^24 elements, periods under 500 ticks).
+struct AvgWindow {
+    uint32_t period = 0, w = 0;
+};
+template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT, int BLK, int NTS, int MAP>
+AvgWindow avg_store_window(int K, int64_t P) {
+    if (P < ((int64_t)1 << 24) || K < 2) return {};
+    static std::atomic<int> blocks_per_cu{-1};
+    int nb = blocks_per_cu.load(std::memory_order_relaxed);
+    if (nb < 0) {
+        nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_fedavg_pipe_win<Y, X, CP, E, S, true, false, NT, LT, BLK, NTS, MAP>,
+                                                         BLK, 0) != hipSuccess)
+            nb = 0;
+        blocks_per_cu.store(nb, std::memory_order_relaxed);
+    }
+    if (nb <= 0) return {};
+    const double round_bytes = (double)nb * device_cus() * BLK * S * E * ((double)K * sizeof(Y) + sizeof(X));
+    const double period = 0.35 * round_bytes / 6.4e12 * 1e8;
+    if (period < 500 || period > 20000) return {};
+    AvgWindow w;
+    w.period = (uint32_t)period;
+    w.w = (uint32_t)(0.15 * period);
+    return w;
+}
+
 template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT, int BLK = kBlock, int NTS = 0, int MAP = 0>
 void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
                         hipStream_t st) {
@@ -2028,15 +2059,35 @@ void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, i
     }
     const dim3 grid((unsigned)ntiles);
     unsigned shm = 0;
+    // the fp32 fold with a first launch (the BASELINE workload's shape): its stores in the chip-wide
+    // window; other dtypes / continuation launches were not measured with one
+    if constexpr (std::is_same<CP, CF32>::value && std::is_same<X, float>::value && std::is_same<Y, float>::value &&
+                  S * E == 16 && BLK == kBlock && MAP == 0 && !LT && !NT && NTS == 1) {
+        if (first && !int_first && cfg_grid_per_cu() == 0) {
+            AvgWindow w = avg_store_window<Y, X, CP, E, S, NT, LT, BLK, NTS, MAP>(cnt, P);
+            int wm = 0;
+#ifdef FEDAGG_PROBES
+            if (g_cfg.avg_win_period < 0 || g_cfg.wpe > 0 || g_cfg.lds_kib > 0) w = AvgWindow{};   // A/B and the other probes
+            else if (g_cfg.avg_win_period > 0) {
+                w = AvgWindow{(uint32_t)g_cfg.avg_win_period.load(), (uint32_t)g_cfg.avg_win_w.load()};
+                wm = g_cfg.avg_win_mode.load();
+            }
+#endif
+            if (w.period) {
+                hipLaunchKernelGGL((k_fedavg_pipe_win<Y, X, CP, E, S, true, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), 0, st, a,
+                                   tab, cnt, P, w.period, w.w, wm);
+                return;
+            }
+        }
+    }
 #ifdef FEDAGG_PROBES
     shm = (unsigned)g_cfg.lds_kib * 1024u;     // occupancy probe: LDS the kernel never touches
     if constexpr (std::is_same<CP, CF32>::value && std::is_same<X, float>::value && S * E * (int)sizeof(Y) == 64 &&
                   BLK == kBlock && MAP == 0 && !LT && !NT && NTS == 1) {
-        if (g_cfg.avg_win_period && !int_first) {
+        if (g_cfg.avg_win_period > 0 && !int_first && !first) {
             const uint32_t wl = (uint32_t)g_cfg.avg_win_period.load(), ww = (uint32_t)g_cfg.avg_win_w.load();
-            const int wm = g_cfg.avg_win_mode.load();
-            if (first) hipLaunchKernelGGL((k_fedavg_pipe_win<Y, X, CP, E, S, true, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), shm, st, a, tab, cnt, P, wl, ww, wm);
-            else hipLaunchKernelGGL((k_fedavg_pipe_win<Y, X, CP, E, S, false, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), shm, st, a, tab, cnt, P, wl, ww, wm);
+            hipLaunchKernelGGL((k_fedavg_pipe_win<Y, X, CP, E, S, false, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), shm, st, a, tab,
+                               cnt, P, wl, ww, g_cfg.avg_win_mode.load());
             return;
         }
         const int w = g_cfg.wpe;
@@ -3075,8 +3126,8 @@ int fa_tune(int knob, int value) {
             g_cfg.opt_win_prod = value;
             return FA_OK;
         case FA_TUNE_AVG_WIN_PERIOD:
-            if (value != 0 && (value < 64 || value > (1 << 24)))
-                return fail(FA_EINVAL, "fa_tune: store-window period 64 .. 2^24 ticks of 10 ns (0 = off)");
+            if (value != 0 && value != -1 && (value < 64 || value > (1 << 24)))
+                return fail(FA_EINVAL, "fa_tune: store-window period 64 .. 2^24 ticks of 10 ns (0 = the product's own, -1 = none)");
             g_cfg.avg_win_period = value;
             return FA_OK;
         case FA_TUNE_AVG_WIN_W:

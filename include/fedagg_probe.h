@@ -89,8 +89,9 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                     FA_TUNE_OPT_WIN_W = 25 /* the store window in 10-ns ticks */,
                     FA_TUNE_OPT_WIN_MODE = 26 /* 0: gate the stores only; 1: also start a tile's reads outside
                                                  the window; 2: also every client batch's reads */,
-                    FA_TUNE_AVG_WIN_PERIOD = 27 /* FedAvg fp32 k_fedavg_pipe (the headline instantiation): the same
-                                                store window for its stores (bit-identical results) */,
+                    FA_TUNE_AVG_WIN_PERIOD = 27 /* FedAvg fp32 k_fedavg_pipe (the headline instantiation): its
+                                                   store window — 0 = the product's own (avg_store_window),
+                                                   -1 = none, > 0 = this period with AVG_WIN_W / _MODE */,
                     FA_TUNE_AVG_WIN_W = 28,
                     FA_TUNE_AVG_WIN_MODE = 29,
                     FA_TUNE_OPT_WIN_PROD = 30 /* 1: OPT_WIN_PERIOD / _W apply to the product step (k_fedopt_cw,
