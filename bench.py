@@ -331,7 +331,8 @@ def fedavg_pattern(ups, agg, stream, device, alg_bytes, kern_ms, a):
         _, ms = timed_steps(fn, a.steps, stream, 1, device, False)
     return {"ms": ms, "frac": alg_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, "kernel_over_pattern": ms / kern_ms,
             "kernel": "k_fedavg_pipe<CADD> (fa_stream_sum, libfedagg_probe.so)",
-            "note": "the fold's exact traversal with x + y instead of x + n(y - x)/N; not in value"}
+            "note": "the fold's exact traversal with x + y instead of x + n(y - x)/N and no store window; "
+                    "not in value (the windowed fold can beat it)"}
 
 
 def achieved_of(alg_bytes, kern_ms):
@@ -373,6 +374,9 @@ def side(fn):
 
 def fold_kernel_label(P, in_bytes, K):
     if P * in_bytes >= 160 << 20:          # fedagg.hip kPipeMinClientBytes
+        if in_bytes == 4 and P >= 1 << 24:  # fedagg.hip avg_store_window: the first fp32 launch
+            return ("k_fedavg_pipe_win (fp32, 4 x 16-B strips per lane, next client prefetched; every wave's "
+                    "stores inside a chip-wide window of the GPU's 100 MHz clock)")
         return ("k_fedavg_pipe (fp32, 4 x 16-B strips per lane, next client prefetched)" if in_bytes == 4 else
                 "k_fedavg_pipe (bf16 -> f32, 8 strips of 4 elements per lane, next client prefetched)")
     return f"k_fedavg (1 x 16-B strip per lane, {8 if in_bytes < 4 or K <= 8 else 4} clients loaded ahead)"

@@ -87,13 +87,14 @@ def record(d, key, kernel, alg=None, session=None, take=None):
 # the workloads bench.py reports (tools/gpu_session.sh step "pmc" runs the passes into pmc1..3)
 P, Q = 100_000_000, 350_000_000
 SESSION = [
-    ("pmc1", f"fedavg_k64_p{P}_f32", "k_fedavg_pipe<float, float", 64 * P * 4 + P * 4),
+    # the fp32 fold's first launch stores inside the chip-wide clock window (k_fedavg_pipe_win)
+    ("pmc1", f"fedavg_k64_p{P}_f32", "k_fedavg_pipe_win<float, float", 64 * P * 4 + P * 4),
     # bench.py's fedopt field: every phase is one windowed launch per round (k_fedopt_cw, K = 32); round 1
     # (12 launches) and the fp32-state phase (12 more) are both k_fedopt_cw<float, float, CF32>: round 1
     # is the first 12 dispatches
     ("pmc1", f"fedopt_adam_round1_k32_p{Q}", "k_fedopt_cw<float, float", 32 * Q * 4 + Q * 24, (0, 12)),
     ("pmc1", f"fedopt_adam_steady_k32_p{Q}", "k_fedopt_cw<float, double", Q * (4 * 32 + 48)),
-    ("pmc2", f"fedavg_k8_p{P}_f32", "k_fedavg_pipe<float, float", 8 * P * 4 + P * 4),
+    ("pmc2", f"fedavg_k8_p{P}_f32", "k_fedavg_pipe_win<float, float", 8 * P * 4 + P * 4),
     ("pmc3", f"fedavg_k64_p{P}_bf16", "bf16, float", 64 * P * 2 + P * 4),
 ]
 
