@@ -1369,6 +1369,15 @@ k_fedopt_cw_w(const OptBuffers b, const OptScalars s, const ClientTable<typename
     fedopt_c_body<Y, OLD, PG, true, true, NT, 1, 4, kUnroll / 2, false, true>(b, s, tab, K, P, period, win_w);
 }
 
+// the windowed step on 256-element wave tiles (2 pairs per lane; OPT_WIN_PROD = 3): fewer registers
+// held per wave, so more waves resident to keep reading while others wait for their window
+template <typename Y, typename OLD, class PG, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_cw2(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P,
+             const uint32_t period, const uint32_t win_w) {
+    fedopt_c_body<Y, OLD, PG, true, true, NT, 1, 2, kUnroll / 2, false, true>(b, s, tab, K, P, period, win_w);
+}
+
 // store-window probe on the compute-then-store order (OPT_WIN_PROD = 2): one tile per wave, its
 // v / out / m computed first and stored inside the window (k_fedopt_cw waits before opt_apply, so
 // its fp64 square roots and divisions run inside the window)
@@ -2371,6 +2380,11 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
                         hipLaunchKernelGGL((k_fedopt_cw_w<Y, OLD, PG, NT, 7>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P, sw.period, sw.w);
                     return check_launch("fa_fedopt_step: kernel launch");
                 }
+                if (sw.period && g_cfg.opt_win_prod == 3) {
+                    const dim3 g2((unsigned)((P + 4 * 256 - 1) / (4 * 256)));
+                    hipLaunchKernelGGL((k_fedopt_cw2<Y, OLD, PG, NT>), g2, dim3(kBlock), 0, st, b, s, tab, cnt, P, sw.period, sw.w);
+                    return check_launch("fa_fedopt_step: kernel launch");
+                }
                 if (sw.period && g_cfg.opt_win_prod == 2) {
                     if (b.m_out_f64 != 1 || b.v_out_f32 || b.out_f32 || (b.v_in && b.v_in_f32))
                         return fail(FA_EINVAL, "fa_tune OPT_WIN_PROD 2: fp64 m / v / model out");
@@ -3122,7 +3136,8 @@ int fa_tune(int knob, int value) {
             g_cfg.opt_win_mode = value;
             return FA_OK;
         case FA_TUNE_OPT_WIN_PROD:
-            if (value < 0 || value > 2) return fail(FA_EINVAL, "fa_tune: OPT_WIN_PROD 0 (pattern probe), 1 (k_fedopt_cw), 2 (k_fedopt_cgw)");
+            if (value < 0 || value > 3)
+                return fail(FA_EINVAL, "fa_tune: OPT_WIN_PROD 0 (pattern probe), 1 (k_fedopt_cw), 2 (k_fedopt_cgw), 3 (k_fedopt_cw2)");
             g_cfg.opt_win_prod = value;
             return FA_OK;
         case FA_TUNE_AVG_WIN_PERIOD:

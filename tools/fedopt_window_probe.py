@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--winprod", default="3000:450,4500:680,6000:900,8192:1200")
     ap.add_argument("--wincg", default="", help="the compute-then-store kernel k_fedopt_cgw (OPT_WIN_PROD 2): period:w,...")
     ap.add_argument("--wpe", default="", help="also the --winprod windows compiled for W waves per SIMD: W,...")
+    ap.add_argument("--wincw2", default="", help="the windowed step on 256-element wave tiles (OPT_WIN_PROD 3): period:w,...")
     a = ap.parse_args()
     _abi.use_probe()
     dev = torch.device("cuda", 0)
@@ -45,6 +46,7 @@ def main():
     explicit = [tuple(int(v) for v in x.split(":")) for x in a.winprod.split(",") if x]
     cg = [tuple(int(v) for v in x.split(":")) for x in a.wincg.split(",") if x]
     wpes = [int(x) for x in a.wpe.split(",") if x]
+    cw2 = [tuple(int(v) for v in x.split(":")) for x in a.wincw2.split(",") if x]
     g = torch.Generator(device=dev).manual_seed(4)
     old32 = torch.randn(P, generator=g, device=dev)
     Kmax = max(int(k) for k in a.clients.split(","))
@@ -63,6 +65,8 @@ def main():
             yield f"win{p_}_{w_}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=1, wpe=0)
             for W in wpes:
                 yield f"win{p_}_{w_}_wpe{W}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=1, wpe=W)
+        for p_, w_ in cw2:
+            yield f"cw2_{p_}_{w_}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=3, wpe=0)
         for p_, w_ in cg if phase == "steady" else ():      # fp64 m / v / model out only
             yield f"cgw{p_}_{w_}", dict(opt_win_period=p_, opt_win_w=w_, opt_win_prod=2, wpe=0)
 

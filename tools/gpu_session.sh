@@ -138,7 +138,7 @@ for s in $STEPS; do
     optwin)
       # FedAdam through the product step with / without the chip-wide store window (probe library)
       timeout -k 10 900 python tools/fedopt_window_probe.py ${FEDN_AMD_OPTWIN:+--winprod "$FEDN_AMD_OPTWIN"} \
-        ${FEDN_AMD_OPTWINCG:+--wincg "$FEDN_AMD_OPTWINCG"} ${FEDN_AMD_OPTWINK:+--clients "$FEDN_AMD_OPTWINK"} ${FEDN_AMD_OPTWPE:+--wpe "$FEDN_AMD_OPTWPE"} > "$OUT/optwin.log" 2>&1; rc=$?
+        ${FEDN_AMD_OPTWINCG:+--wincg "$FEDN_AMD_OPTWINCG"} ${FEDN_AMD_OPTWINK:+--clients "$FEDN_AMD_OPTWINK"} ${FEDN_AMD_OPTWPE:+--wpe "$FEDN_AMD_OPTWPE"} ${FEDN_AMD_OPTCW2:+--wincw2 "$FEDN_AMD_OPTCW2"} > "$OUT/optwin.log" 2>&1; rc=$?
       echo "optwin rc=$rc"; cut -c1-900 "$OUT/optwin.log" | grep -v amdgpu.ids | tail -6; [ $rc -eq 0 ] || exit $rc ;;
     avgwin)
       # FedAvg's fold (64 and 8 x 100 M fp32) with its stores in a chip-wide clock window (probe library)
