@@ -2070,8 +2070,9 @@ void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, i
     unsigned shm = 0;
     // the fp32 fold with a first launch (the BASELINE workload's shape): its stores in the chip-wide
     // window; other dtypes / continuation launches were not measured with one
-    if constexpr (std::is_same<CP, CF32>::value && std::is_same<X, float>::value && std::is_same<Y, float>::value &&
-                  S * E == 16 && BLK == kBlock && MAP == 0 && !LT && !NT && NTS == 1) {
+    if constexpr (std::is_same<CP, CF32>::value && std::is_same<X, float>::value &&
+                  ((std::is_same<Y, float>::value && S * E == 16) || (std::is_same<Y, bf16>::value && S * E == 32)) &&
+                  BLK == kBlock && MAP == 0 && !LT && !NT && NTS == 1) {
         if (first && !int_first && cfg_grid_per_cu() == 0) {
             AvgWindow w = avg_store_window<Y, X, CP, E, S, NT, LT, BLK, NTS, MAP>(cnt, P);
             int wm = 0;

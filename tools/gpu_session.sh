@@ -142,7 +142,7 @@ for s in $STEPS; do
       echo "optwin rc=$rc"; cut -c1-900 "$OUT/optwin.log" | grep -v amdgpu.ids | tail -6; [ $rc -eq 0 ] || exit $rc ;;
     avgwin)
       # FedAvg's fold (64 and 8 x 100 M fp32) with its stores in a chip-wide clock window (probe library)
-      timeout -k 10 600 python tools/window_probe.py ${FEDN_AMD_AVGWIN:+--win "$FEDN_AMD_AVGWIN"} > "$OUT/avgwin.log" 2>&1; rc=$?
+      timeout -k 10 600 python tools/window_probe.py ${FEDN_AMD_AVGWIN:+--win "$FEDN_AMD_AVGWIN"} ${FEDN_AMD_AVGDT:+--dtype "$FEDN_AMD_AVGDT"} > "$OUT/avgwin.log" 2>&1; rc=$?
       echo "avgwin rc=$rc"; cut -c1-1500 "$OUT/avgwin.log" | grep -v amdgpu.ids | tail -3; [ $rc -eq 0 ] || exit $rc ;;
     mixprobe)
       timeout -k 10 600 python tools/fedopt_mix_probe.py > "$OUT/mixprobe.log" 2>&1; rc=$?

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--params", type=int, default=100_000_000)
     ap.add_argument("--clients", default="64,8")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--dtype", default="f32", choices=("f32", "bf16"), help="the client updates' dtype")
     # K:period:window:mode (ticks of 10 ns); a round of resident workgroups reads ~K x 16 KiB each
     ap.add_argument("--win", default="64:14000:700:0,64:17000:850:0,64:20000:1000:0,64:24000:1200:0,64:17000:1700:0,"
                                      "64:17000:850:2,8:2000:250:0,8:2600:320:0,8:3200:400:0,8:4000:500:0,8:2600:520:0")
@@ -46,6 +47,8 @@ def main():
     base = torch.randn(P, generator=g, device=dev)
     Kmax = max(int(k) for k in a.clients.split(","))
     ups = [torch.randn(P, generator=g, device=dev).mul_(0.01).add_(base) for _ in range(Kmax)]
+    if a.dtype == "bf16":
+        ups = [u.to(torch.bfloat16) for u in ups]
     del base
     allwins = [tuple(int(v) for v in x.split(":")) for x in a.win.split(",") if x]
     agg = torch.empty(P, device=dev)
@@ -54,7 +57,7 @@ def main():
         ns = [int(v) for v in np.random.default_rng(K).integers(1, 5001, K)]
         Ns = [int(v) for v in np.cumsum(ns)]
         fn = lambda: ops.fedavg_fold(agg, ups[:K], ns, Ns, True)  # noqa: E731
-        alg = (K + 1) * P * 4
+        alg = K * P * ups[0].element_size() + P * 4
         ops.tune(avg_win_period=-1)                       # no window: the reference bits and times
         fn()
         torch.cuda.synchronize()
@@ -80,7 +83,7 @@ def main():
             ops.tune(avg_win_period=0)
         ops.tune(avg_win_period=0)
         prod = float(np.median(res["product"]))
-        out = {"clients": K, "params": P, "alg_bytes": alg, "nowin_ms": round(prod, 4),
+        out = {"clients": K, "params": P, "dtype": a.dtype, "alg_bytes": alg, "nowin_ms": round(prod, 4),
                "nowin_frac_of_peak": round(alg / prod / 1e6 / PEAK, 4)}
         for w in wins:
             ms = float(np.median(res[w]))
