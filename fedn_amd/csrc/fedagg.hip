@@ -2031,7 +2031,8 @@ StoreWindow opt_store_window(const OptBuffers& b, int K, int64_t P) {
 // clock: period 0.45 of the time one round of resident workgroups streams its tiles at 6.4 TB/s,
 // window 15 % — measured (profiles/r05_fedavg_window.log, 100 M fp32, bit-exact, two boxes) at
 // K = 64: 0.24-0.47 round -5...-7 %, 0.6 round and longer +2...+22 %; K = 8: 0.34-0.42 round -6 %,
-// 0.64 round 0 %. {0, 0}: no window (models under 2^24 elements, periods under 500 ticks).
+// 0.64 round 0 %; bf16 updates at K = 64 -5 %, at K = 8 (a 20 % write share) +4 %. {0, 0}: no window
+// (write shares over 15 %, models under 2^24 elements, periods under 500 ticks).
 struct AvgWindow {
     uint32_t period = 0, w = 0;
 };
@@ -2048,6 +2049,7 @@ AvgWindow avg_store_window(int K, int64_t P) {
         blocks_per_cu.store(nb, std::memory_order_relaxed);
     }
     if (nb <= 0) return {};
+    if ((double)sizeof(X) / ((double)K * sizeof(Y) + sizeof(X)) > 0.15) return {};
     const double round_bytes = (double)nb * device_cus() * BLK * S * E * ((double)K * sizeof(Y) + sizeof(X));
     const double period = 0.45 * round_bytes / 6.4e12 * 1e8;
     if (period < 500 || period > 20000) return {};
