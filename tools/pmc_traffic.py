@@ -95,7 +95,7 @@ SESSION = [
     ("pmc1", f"fedopt_adam_round1_k32_p{Q}", "k_fedopt_cw<float, float", 32 * Q * 4 + Q * 24, (0, 12)),
     ("pmc1", f"fedopt_adam_steady_k32_p{Q}", "k_fedopt_cw<float, double", Q * (4 * 32 + 48)),
     ("pmc2", f"fedavg_k8_p{P}_f32", "k_fedavg_pipe_win<float, float", 8 * P * 4 + P * 4),
-    ("pmc3", f"fedavg_k64_p{P}_bf16", "bf16, float", 64 * P * 2 + P * 4),
+    ("pmc3", f"fedavg_k64_p{P}_bf16", "k_fedavg_pipe_win<(anonymous namespace)::bf16, float", 64 * P * 2 + P * 4),
 ]
 
 
