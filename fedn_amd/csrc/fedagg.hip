@@ -1144,6 +1144,7 @@ __device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const Op
         T t[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) t[e] = narrow<T, V>(pg[e]);
+        if constexpr (WIN) wait_write_window(period, win_w);
 #pragma unroll
         for (int h = 0; h < NH; ++h) strip_store<T, H>(static_cast<T*>(b.pg) + at(h), half(t, h));
     } else {
@@ -1408,6 +1409,20 @@ k_fedopt_cw(const OptBuffers b, const OptScalars s, const ClientTable<typename P
             const uint32_t period, const uint32_t win_w) {
     fedopt_c_body<Y, OLD, PG, true, true, NT, 1, 4, kUnroll / 2, false, true>(b, s, tab, K, P, period, win_w);
 }
+
+#ifdef FEDAGG_PROBES
+// store-window probe on a wave of a multi-launch round (staging.FedOptPipeline: the first or a middle
+// launch, pg written back to the workspace; fa_tune OPT_WIN_PERIOD > 0 with OPT_WIN_PROD = 1):
+// k_fedopt_c's bits. Null for the product: 8 bf16 updates over fp64 pg, 250 M params, every period
+// 400-2500 ticks slower than no window (first +7...+76 %, middle +1...+34 %;
+// profiles/r05_wave_window.log) — the 20-25 % write share of the FedAvg bf16 K = 8 case.
+template <typename Y, typename OLD, class PG, bool FIRST, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_cwp(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P,
+             const uint32_t period, const uint32_t win_w) {
+    fedopt_c_body<Y, OLD, PG, FIRST, false, NT, 1, 4, kUnroll / 2, false, true>(b, s, tab, K, P, period, win_w);
+}
+#endif
 
 #ifdef FEDAGG_PROBES
 template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM, int NH, int U, int W>
@@ -2401,6 +2416,16 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
                 return check_launch("fa_fedopt_step: kernel launch");
             }
         }
+#ifdef FEDAGG_PROBES
+        if (!final_ && g_cfg.opt_win_period > 0 && g_cfg.opt_win_prod) {
+            const uint32_t per = (uint32_t)g_cfg.opt_win_period.load(), w = (uint32_t)g_cfg.opt_win_w.load();
+            if (first)
+                hipLaunchKernelGGL((k_fedopt_cwp<Y, OLD, PG, true, NT>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P, per, w);
+            else
+                hipLaunchKernelGGL((k_fedopt_cwp<Y, OLD, PG, false, NT>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P, per, w);
+            return check_launch("fa_fedopt_step: kernel launch");
+        }
+#endif
         if (first && final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, true, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
         else if (first) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, true, false, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
         else if (final_) hipLaunchKernelGGL((k_fedopt_c<Y, OLD, PG, false, true, NT, 1, 4>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);

@@ -75,3 +75,28 @@ def test_fedopt_window_is_bit_identical(dev, phase):
         finally:
             ops.tune(opt_win_period=0)
     assert all(_same(a, b) for a, b in zip(res[-1], res[0]))
+
+
+@pytest.mark.parametrize("first", [True, False])
+def test_pipeline_wave_window_is_bit_identical(dev, first):
+    """k_fedopt_cwp (probe: a pipeline wave's pg stores in the window) vs k_fedopt_c: bf16 updates, fp64 pg."""
+    W = 8
+    g = torch.Generator(device=dev).manual_seed(11)
+    old = torch.randn(P, generator=g, device=dev, dtype=torch.float64)
+    ups = [(old.float() + 0.01 * torch.randn(P, generator=g, device=dev)).to(torch.bfloat16) for _ in range(W)]
+    ns = [float(v) for v in np.random.default_rng(5).integers(1, 5001, W)]
+    Ns = [float(v) for v in np.cumsum(ns)]
+    pg0 = torch.empty(P, dtype=torch.float64, device=dev)
+    ops.fedopt_step(old, ups, ns, Ns, first=True, final=False, pg=pg0)
+    res = {}
+    with _abi.use_probe():
+        try:
+            for mode, w in ((-1, 0), (0, 0), (600, 150)):
+                ops.tune(opt_win_period=mode, opt_win_w=w if mode > 0 else 0, opt_win_prod=1 if mode > 0 else 0)
+                pg = pg0.clone()
+                ops.fedopt_step(old, ups, ns, Ns, first=first, final=False, pg=pg)
+                torch.cuda.synchronize()
+                res[mode] = pg
+        finally:
+            ops.tune(opt_win_period=0, opt_win_prod=0)
+    assert _same(res[-1], res[0]) and _same(res[-1], res[600])

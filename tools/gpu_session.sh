@@ -144,6 +144,10 @@ for s in $STEPS; do
       # FedAvg's fold (64 and 8 x 100 M fp32) with its stores in a chip-wide clock window (probe library)
       timeout -k 10 600 python tools/window_probe.py ${FEDN_AMD_AVGWIN:+--win "$FEDN_AMD_AVGWIN"} ${FEDN_AMD_AVGDT:+--dtype "$FEDN_AMD_AVGDT"} > "$OUT/avgwin.log" 2>&1; rc=$?
       echo "avgwin rc=$rc"; cut -c1-1500 "$OUT/avgwin.log" | grep -v amdgpu.ids | tail -3; [ $rc -eq 0 ] || exit $rc ;;
+    wavewin)
+      # FedOpt pipeline waves (8 bf16 updates, fp64 model / pg) with their pg stores in the clock window (probe library)
+      timeout -k 10 600 python tools/wave_window_probe.py ${FEDN_AMD_WAVEWIN:+--win "$FEDN_AMD_WAVEWIN"} > "$OUT/wavewin.log" 2>&1; rc=$?
+      echo "wavewin rc=$rc"; grep -v amdgpu.ids "$OUT/wavewin.log" | tail -4; [ $rc -eq 0 ] || exit $rc ;;
     mixprobe)
       timeout -k 10 600 python tools/fedopt_mix_probe.py > "$OUT/mixprobe.log" 2>&1; rc=$?
       echo "mixprobe rc=$rc"; cut -c1-700 "$OUT/mixprobe.log" | tail -4; [ $rc -eq 0 ] || exit $rc ;;
