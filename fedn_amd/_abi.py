@@ -41,6 +41,11 @@ EXPORTS = {
         ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,       # updates, upd_dtype
         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int,  # n, N, K
         ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),     # P, init, stream
+    "fa_fedavg_fold_host": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_int,                       # agg (pinned host), agg_dtype
+        ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,       # updates (pinned host), upd_dtype
+        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int,  # n, N, K
+        ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),     # P, init, stream
     "fa_fedopt_step": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int,                       # old, old_dtype
         ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,       # updates, upd_dtype
@@ -103,7 +108,7 @@ PROBE_EXPORTS = {
     "fa_stream_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 IPC_HANDLE_BYTES = 64    # FA_IPC_HANDLE_BYTES
 RELEASE_WORDS = 8        # FA_RELEASE_WORDS; enum fa_release_word:
 FA_REL_MASK, FA_REL_ARRIVED, FA_REL_LAUNCHES, FA_REL_MISSES, FA_REL_SEEN, FA_REL_EXPECT = range(6)

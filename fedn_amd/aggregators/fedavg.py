@@ -22,8 +22,10 @@ from collections import deque
 
 import torch
 
+from .. import ops
 from ..ingest import ShardedStagedModel
 from ..layout import Layout, spread
+from ..smallround import SmallSessions
 from ..staging import AndroidFedAvgPipeline, FedAvgPipeline, StagingCache, helper_kind
 from .aggregatorbase import AggregatorBase, queued_updates
 
@@ -78,6 +80,7 @@ class Aggregator(AggregatorBase):
         self.device = torch.device(device) if device is not None else None
         self.devices = devices   # several devices: parameter-slice sharding in this process (multidev.py)
         self._staging = StagingCache()   # pinned slots, arenas and streams reused by the next round
+        self._small = SmallSessions()    # configs[0]-sized rounds: arena, plans, result blocks (smallround.py)
 
     def combine_models(self, helper=None, delete_models=True, parameters=None):
         try:
@@ -91,12 +94,23 @@ class Aggregator(AggregatorBase):
             # the round's store deletes (run side by side by the staging handler) are all done
             self._finish_deletes()
 
+    def _small_round(self, first, helper):
+        """configs[0]'s one-call round (smallround.py) when ``first`` is a small float model's update
+        on one device with numpyhelper's arithmetic; None: the general pipeline."""
+        if self.devices or os.environ.get("FEDN_AMD_DEVICES") or helper_kind(helper) == "androidhelper":
+            return None
+        return self._small.round(first, self.device or default_device())
+
+    def _general(self, helper):
+        return lambda first: make_fedavg_pipeline(first, self.device, self.devices, helper, self._staging)
+
     def _combine(self, helper, delete_models, parameters):
         data = {"time_model_load": 0.0, "time_model_aggregation": 0.0}
         model = None
         nr_aggregated_models = 0
         total_examples = 0
         pipe = None
+        small = False           # pipe is a SmallRound: nothing launched or deleted before its result
         waiting = deque()       # admitted updates not deleted yet: a batched fold may still skip them
 
         logger.info("AGGREGATOR({}): Aggregating model updates... ".format(self.name))
@@ -111,9 +125,15 @@ class Aggregator(AggregatorBase):
 
                     tic = time.time()
                     if nr_aggregated_models == 0:
-                        pipe = make_fedavg_pipeline(model_next, self.device, self.devices, helper, self._staging)
+                        pipe = self._small_round(model_next, helper)
+                        small = pipe is not None
+                        if not small:
+                            pipe = self._general(helper)(model_next)
                         self._live = pipe
-                    else:
+                    elif not (small and pipe.add(model_next, metadata["num_examples"], total_examples, model_update)):
+                        if small:       # not this layout, or the arena is full: the general path from here
+                            pipe, small = pipe.general(self._general(helper)), False
+                            self._live = pipe
                         pipe.add(model_next, metadata["num_examples"], total_examples, tag=model_update)
                     data["time_model_aggregation"] += time.time() - tic
 
@@ -121,14 +141,22 @@ class Aggregator(AggregatorBase):
                     waiting.append(model_update)
                     # updates of a batch whose launch failed were refolded one at a time: the ones
                     # whose own fold failed are skipped (fedavg.py:75-78); the folded ones deleted
-                    nr_aggregated_models -= self._settle(pipe, waiting, delete_models)
+                    if not small:
+                        nr_aggregated_models -= self._settle(pipe, waiting, delete_models)
                 except Exception as e:  # noqa: BLE001 — fedavg.py:75-78: log and continue
                     logger.error(f"AGGREGATOR({self.name}): Error encoutered while processing model update: {e}")
                     logger.error(traceback.format_exc())
 
         if pipe is not None:
             tic = time.time()
-            model = pipe.result()
+            if small:
+                try:
+                    model = pipe.result()
+                except ops.FedAggError:      # the launch failed: the general path's per-update recovery
+                    pipe, small = pipe.general(self._general(helper)), False
+                    self._live = pipe
+            if not small:
+                model = pipe.result()
             data["time_model_aggregation"] += time.time() - tic
             nr_aggregated_models -= self._settle(pipe, waiting, delete_models)
             data.update(pipe.timings())

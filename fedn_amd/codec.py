@@ -16,6 +16,7 @@ import ctypes
 import io
 import os
 import threading
+import zlib
 
 import numpy as np
 
@@ -24,7 +25,7 @@ from .layout import Layout
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfednpz.so")
 MAX_DIMS = 64           # numpy 2.x NPY_MAXDIMS (include/fednpz.h FNPZ_MAX_DIMS)
-FNPZ_ABI_VERSION = 6    # include/fednpz.h
+FNPZ_ABI_VERSION = 7    # include/fednpz.h
 THREADS = int(os.environ.get("FEDN_AMD_CODEC_THREADS", str(min(16, os.cpu_count() or 1))))
 
 
@@ -100,6 +101,13 @@ def load_lib():
                 lib.fnpz_gather_start.restype = ctypes.c_int64
                 lib.fnpz_gather_start.argtypes = lib.fnpz_gather.argtypes
                 lib.fnpz_gather_wait.argtypes = [ctypes.c_int64]
+                lib.fnpz_savez_zlib_expect.restype = None
+                lib.fnpz_savez_zlib_expect.argtypes = [ctypes.c_char_p, ctypes.c_int]
+                lib.fnpz_savez_zlib_status.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+                lib.fnpz_savez_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+                # numpy's archive comes from the libz Python's zlib module runs: the exact writer's
+                # parallel path is allowed only while this library's libz is that one (fednpz.h)
+                lib.fnpz_savez_zlib_expect(zlib.ZLIB_RUNTIME_VERSION.encode(), -1)
             except AttributeError as e:      # a symbol include/fednpz.h declares is missing
                 raise ImportError(f"{LIB_PATH}: {e}; rebuild it (python -m fedn_amd.build)") from e
             _lib = lib
@@ -343,6 +351,31 @@ def savez_into(arrays, threads=None):
                           (ctypes.c_void_p * m)(*[d.ctypes.data if d.size else 0 for _, d, _ in members]), nb, seg,
                           threads or THREADS, out.ctypes.data, cap, ctypes.byref(out_len)))
     return out[:out_len.value]
+
+
+def savez_zlib_status():
+    """(True, reason) when the exact writer's big members may take its parallel deflate (pdeflate.h,
+    zlib 1.2.11's stream recomputed on every thread), else (False, reason): every member then goes
+    through the process's libz, the bytes numpy writes with it (include/fednpz.h, ABI 7)."""
+    buf = ctypes.create_string_buffer(512)
+    on = load_lib().fnpz_savez_zlib_status(buf, len(buf))
+    return bool(on), buf.value.decode(errors="replace")
+
+
+def savez_force_zlib(force):
+    """Test hook: ``True`` makes the exact writer act as on a libz it does not model (every member
+    through libz); ``False`` restores the check."""
+    load_lib().fnpz_savez_zlib_expect(None, 1 if force else 0)
+
+
+SAVEZ_PHASES = ("copy", "parse", "sync", "sched", "plan", "encode", "crc", "assemble", "total")
+
+
+def savez_stats():
+    """Phase times (s) of the exact writer's last big member and its last call (fnpz_savez_stats)."""
+    out = (ctypes.c_double * len(SAVEZ_PHASES))()
+    k = load_lib().fnpz_savez_stats(out, len(SAVEZ_PHASES))
+    return {name: out[i] for i, name in enumerate(SAVEZ_PHASES[:k])}
 
 
 def save_npz(arrays, threads=None):

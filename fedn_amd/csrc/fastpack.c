@@ -147,7 +147,159 @@ static PyObject* fp_admit(PyObject* self, PyObject* args) {
     return PyLong_FromLong(rc);
 }
 
+/* ---- a small model's round end: pack wait + fold + wait in one call (smallround.py) --------------
+ *
+ *   fold_plan([(agg_dtype, upd_dtype, byte_offset, elems), ...]) -> capsule   one entry per dtype group
+ *   fold_host(fold_plan, fold_addr, wait_addr, ticket, arena_addr, stride, K, out_addr, n, N, stream)
+ *       -> status
+ * fold_host waits for the gather ticket (the updates' packs into the pinned arena, fnpz_gather_wait),
+ * then for each group calls fa_fedavg_fold_host (include/fedagg.h: the fold of K pinned host updates
+ * into pinned host memory, synchronous) with updates[k] = arena + k * stride + offset, the result at
+ * out + offset; n / N are sequences of K floats (n[0] = 0, N[0] = 1: agg := the first update). The GIL
+ * is released throughout. Returns fa_fedavg_fold_host's status (0 = the model is in out), or -1 if
+ * the pack failed (fnpz_last_error says why). */
+typedef int (*fold_host_fn)(void* agg, int agg_dtype, const void* const* updates, int upd_dtype, const double* n,
+                            const double* N, int K, int64_t P, int init, void* stream);
+typedef int (*gather_wait_fn)(int64_t ticket);
+
+typedef struct {
+    int agg_dtype, upd_dtype;
+    int64_t off, elems;
+} Group;
+
+typedef struct {
+    Py_ssize_t n;
+    Group g[];
+} FoldPlan;
+
+#define MAX_FOLD_K 64
+
+static void fold_plan_free(PyObject* cap) {
+    PyMem_Free(PyCapsule_GetPointer(cap, "fedn_amd._fastpack.fold_plan"));
+}
+
+static PyObject* fp_fold_plan(PyObject* self, PyObject* args) {
+    PyObject* specs;
+    if (!PyArg_ParseTuple(args, "O!", &PyList_Type, &specs)) return NULL;
+    Py_ssize_t n = PyList_GET_SIZE(specs);
+    FoldPlan* p = (FoldPlan*)PyMem_Calloc(1, sizeof(FoldPlan) + (size_t)n * sizeof(Group));
+    if (!p) return PyErr_NoMemory();
+    p->n = n;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        long long off, elems;
+        if (!PyArg_ParseTuple(PyList_GET_ITEM(specs, i), "iiLL", &p->g[i].agg_dtype, &p->g[i].upd_dtype, &off, &elems)) {
+            PyMem_Free(p);
+            return NULL;
+        }
+        if (off < 0 || elems < 0) {
+            PyMem_Free(p);
+            PyErr_SetString(PyExc_ValueError, "negative offset or size");
+            return NULL;
+        }
+        p->g[i].off = off;
+        p->g[i].elems = elems;
+    }
+    PyObject* cap = PyCapsule_New(p, "fedn_amd._fastpack.fold_plan", fold_plan_free);
+    if (!cap) PyMem_Free(p);
+    return cap;
+}
+
+static int read_doubles(PyObject* seq, double* out, Py_ssize_t K) {
+    PyObject* f = PySequence_Fast(seq, "n and N must be sequences");
+    if (!f) return -1;
+    if (PySequence_Fast_GET_SIZE(f) != K) {
+        Py_DECREF(f);
+        PyErr_SetString(PyExc_ValueError, "n and N need one entry per update");
+        return -1;
+    }
+    for (Py_ssize_t k = 0; k < K; ++k) {
+        out[k] = PyFloat_AsDouble(PySequence_Fast_GET_ITEM(f, k));
+        if (out[k] == -1.0 && PyErr_Occurred()) {
+            Py_DECREF(f);
+            return -1;
+        }
+    }
+    Py_DECREF(f);
+    return 0;
+}
+
+static PyObject* fp_fold_host(PyObject* self, PyObject* args) {
+    PyObject *cap, *ns, *Ns;
+    unsigned long long fold, wait, arena, out, stream;
+    long long ticket, stride;
+    int K;
+    if (!PyArg_ParseTuple(args, "OKKLKLiKOOK", &cap, &fold, &wait, &ticket, &arena, &stride, &K, &out, &ns, &Ns,
+                          &stream))
+        return NULL;
+    FoldPlan* p = (FoldPlan*)PyCapsule_GetPointer(cap, "fedn_amd._fastpack.fold_plan");
+    if (!p) return NULL;
+    if (K < 1 || K > MAX_FOLD_K || stride < 0 || !arena || !out || !fold) {
+        PyErr_SetString(PyExc_ValueError, "fold_host: bad arguments");
+        return NULL;
+    }
+    double n[MAX_FOLD_K], N[MAX_FOLD_K];
+    if (read_doubles(ns, n, K) || read_doubles(Ns, N, K)) return NULL;
+    int rc = 0;
+    Py_BEGIN_ALLOW_THREADS
+    if (ticket > 0 && wait) rc = ((gather_wait_fn)(uintptr_t)wait)((int64_t)ticket) ? -1 : 0;
+    for (Py_ssize_t i = 0; rc == 0 && i < p->n; ++i) {
+        const Group* g = &p->g[i];
+        if (!g->elems) continue;
+        const void* ups[MAX_FOLD_K];
+        for (int k = 0; k < K; ++k) ups[k] = (const void*)(uintptr_t)(arena + (unsigned long long)k * stride + g->off);
+        rc = ((fold_host_fn)(uintptr_t)fold)((void*)(uintptr_t)(out + g->off), g->agg_dtype, ups, g->upd_dtype, n, N, K,
+                                              g->elems, 1, (void*)(uintptr_t)stream);
+    }
+    Py_END_ALLOW_THREADS
+    return PyLong_FromLong(rc);
+}
+
+/*   views(plan, base) -> list    the model's arrays as views of ``base`` (a C-contiguous numpy array whose
+ * bytes hold the packed layout ``plan`` describes: the admission plan), each keeping ``base`` alive */
+static PyObject* fp_views(PyObject* self, PyObject* args) {
+    PyObject *cap, *base;
+    if (!PyArg_ParseTuple(args, "OO!", &cap, &PyArray_Type, &base)) return NULL;
+    Plan* p = (Plan*)PyCapsule_GetPointer(cap, "fedn_amd._fastpack.plan");
+    if (!p) return NULL;
+    PyArrayObject* b = (PyArrayObject*)base;
+    if (!PyArray_IS_C_CONTIGUOUS(b)) {
+        PyErr_SetString(PyExc_ValueError, "views: base must be C-contiguous");
+        return NULL;
+    }
+    const int64_t cap_bytes = (int64_t)PyArray_NBYTES(b);
+    char* data = (char*)PyArray_DATA(b);
+    PyObject* out = PyList_New(p->n);
+    if (!out) return NULL;
+    for (Py_ssize_t i = 0; i < p->n; ++i) {
+        const Tensor* t = &p->t[i];
+        if (t->dst_off < 0 || t->dst_off + t->nbytes > cap_bytes) {
+            Py_DECREF(out);
+            PyErr_SetString(PyExc_ValueError, "views: the plan does not fit the base array");
+            return NULL;
+        }
+        Py_INCREF(t->dtype);   /* stolen by PyArray_NewFromDescr */
+        PyObject* v = PyArray_NewFromDescr(&PyArray_Type, t->dtype, t->ndim, (npy_intp*)t->shape, NULL,
+                                           data + t->dst_off, NPY_ARRAY_CARRAY, NULL);
+        if (!v) {
+            Py_DECREF(out);
+            return NULL;
+        }
+        Py_INCREF(base);
+        if (PyArray_SetBaseObject((PyArrayObject*)v, base) < 0) {
+            Py_DECREF(v);
+            Py_DECREF(out);
+            return NULL;
+        }
+        PyList_SET_ITEM(out, i, v);
+    }
+    return out;
+}
+
 static PyMethodDef methods[] = {
+    {"fold_plan", fp_fold_plan, METH_VARARGS, "fold_plan([(agg_dtype, upd_dtype, byte_offset, elems), ...]) -> capsule"},
+    {"fold_host", fp_fold_host, METH_VARARGS,
+     "fold_host(fold_plan, fold_addr, wait_addr, ticket, arena_addr, stride, K, out_addr, n, N, stream) -> status"},
+    {"views", fp_views, METH_VARARGS, "views(plan, base) -> list of arrays viewing base"},
     {"plan", fp_plan, METH_VARARGS, "plan([(shape, dtype, dst_offset), ...]) -> capsule"},
     {"admit", fp_admit, METH_VARARGS,
      "admit(plan, arrays, dst_addr, gather_start_addr, threads, buf_addr, buf_len) -> ticket | 0 | -1 (not this "

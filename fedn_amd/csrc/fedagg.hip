@@ -2535,6 +2535,38 @@ int fa_fedavg_fold(void* agg, int agg_dtype, const void* const* updates, int upd
     return fail(FA_EDTYPE, "fa_fedavg_fold: unsupported dtype pair (update %d, aggregate %d)", upd_dtype, agg_dtype);
 }
 
+// A small model's whole round in one call: the fold reads the packed updates and writes the model
+// straight in page-locked host memory, through their device mappings, and the call returns with the
+// model on the host. For mnist-sized models the copies, events and extra launches of the device path
+// cost more than the bytes (configs[0]); the kernel and client table are fa_fedavg_fold's, so the bits
+// are too.
+int fa_fedavg_fold_host(void* agg, int agg_dtype, const void* const* updates, int upd_dtype, const double* n,
+                        const double* N, int K, int64_t P, int init, void* stream) {
+    g_err[0] = 0;
+    if (P < 0 || K < 0) return fail(FA_EINVAL, "fa_fedavg_fold_host: negative size (P=%lld, K=%d)", (long long)P, K);
+    if (K > kMaxK) return fail(FA_EINVAL, "fa_fedavg_fold_host: K=%d exceeds one launch (%d)", K, kMaxK);
+    if (K == 0 || P == 0) return FA_OK;
+    if (!agg || !updates) return fail(FA_EINVAL, "fa_fedavg_fold_host: null pointer argument");
+    void* dev_agg = nullptr;
+    const void* dev_upd[kMaxK];
+    hipError_t e = hipHostGetDevicePointer(&dev_agg, agg, 0);
+    for (int k = 0; e == hipSuccess && k < K; ++k) {
+        void* d = nullptr;
+        if (!updates[k]) return fail(FA_EINVAL, "fa_fedavg_fold_host: updates[%d] is NULL", k);
+        e = hipHostGetDevicePointer(&d, const_cast<void*>(updates[k]), 0);
+        dev_upd[k] = d;
+    }
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(FA_EINVAL, "fa_fedavg_fold_host: %s (not page-locked host memory?)", hipGetErrorString(e));
+    }
+    const int rc = fa_fedavg_fold(dev_agg, agg_dtype, dev_upd, upd_dtype, n, N, K, P, init, stream);
+    if (rc != FA_OK) return rc;
+    e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(FA_EHIP, "fa_fedavg_fold_host: hipStreamSynchronize: %s", hipGetErrorString(e));
+    return FA_OK;
+}
+
 int fa_weighted_sum(void* acc, int acc_dtype, const void* const* updates, int upd_dtype, const double* w, int K,
                     int64_t P, void* stream) {
     g_err[0] = 0;

@@ -18,9 +18,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstring>
 #include <memory>
+#include <mutex>
+#include <new>
+#include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -38,6 +43,30 @@ using fnpz_internal::set_error;
 std::atomic<int64_t> g_par_min{32ll << 20}, g_par_chunk{4ll << 20};
 std::atomic<int64_t> g_par_ok{0}, g_par_fallback{0};
 thread_local const char* g_par_reason = nullptr;
+
+// ---- which libz pdeflate.h may stand in for ------------------------------------------------------
+// pdeflate.h reproduces zlib 1.2.11's level-6 stream. Small members always go through the process's
+// libz (deflate_member); a big member's bytes come from pdeflate.h only while that libz is one
+// pdeflate.h is known to match: its zlibVersion() is a modelled version, it is the libz Python's zlib
+// module runs (zlib.ZLIB_RUNTIME_VERSION, handed in by codec.py: numpy's archive comes from THAT
+// libz), and a self-test — one 1.5 MiB member through both, compared byte for byte — agrees. Any
+// other libz (zlib-ng-compat, Chromium's, a later release) sends every member through deflate_member,
+// so an archive never mixes two deflaters. Evaluated once, at the first big member.
+const char* const kModelledZlib[] = {"1.2.11"};
+std::mutex g_zl_mu;
+std::atomic<int> g_zl_state{-1};   // -1 not evaluated, 0 off (zlib for every member), 1 pdeflate.h allowed
+std::string g_zl_expect;           // Python's zlib.ZLIB_RUNTIME_VERSION ("" = not told)
+int g_zl_force = 0;                // test hook: 1 = as if the check failed
+std::string g_zl_reason = "not evaluated";
+
+// the last big member's phases (s), for fnpz_savez_stats: the input copy, pdeflate.h's five phases,
+// the CRC, and (per call) the archive assembly
+enum { kStCopy, kStParse, kStSync, kStSched, kStPlan, kStEncode, kStCrc, kStAssemble, kStTotal, kStN };
+std::mutex g_st_mu;
+double g_st[kStN] = {0};
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 // the member's deflate() inputs as cumulative ends: the header, then numpy's writes
 std::vector<int64_t> input_ends(int64_t hlen, int64_t nbytes, int64_t seg) {
@@ -72,8 +101,11 @@ struct Member {
     int rc = Z_OK;
 };
 
-// the same stream from pdeflate.h on `threads` threads; false: the caller runs zlib
-bool deflate_member_parallel(Member& m, int threads) {
+// the same stream from pdeflate.h on `threads` threads; false: the caller runs zlib (also when the
+// extra memory this path holds — a copy of the member and its symbol streams — cannot be had: the
+// streaming zlib path needs only its output)
+bool deflate_member_parallel_unchecked(Member& m, int threads) try {
+    const double t_start = now_s();
     const int64_t L = m.hlen + m.nbytes;
     std::unique_ptr<uint8_t[]> buf(new uint8_t[(size_t)L]);   // no zero fill: every byte is copied in
     uint8_t* const S = buf.get();
@@ -83,12 +115,14 @@ bool deflate_member_parallel(Member& m, int threads) {
         const int64_t b = (int64_t)i * piece;
         std::memcpy(S + m.hlen + b, m.data + b, (size_t)std::min(piece, m.nbytes - b));
     });
+    const double t_copied = now_s();
     pdef::Stats st;
     const bool ok = pdef::deflate_exact(S, L, input_ends(m.hlen, m.nbytes, m.seg), threads, g_par_chunk.load(),
                                         m.out, &st);
     (ok ? g_par_ok : g_par_fallback).fetch_add(1);
     g_par_reason = st.fallback;
     if (!ok) return false;
+    const double t_deflated = now_s();
     // CRC-32 by pieces, combined
     const int np = (int)((L + piece - 1) / piece);
     std::vector<uint32_t> crcs((size_t)np);
@@ -100,7 +134,26 @@ bool deflate_member_parallel(Member& m, int threads) {
     for (int i = 1; i < np; ++i) crc = crc32_combine(crc, crcs[i], (z_off_t)std::min(piece, L - (int64_t)i * piece));
     m.crc = (uint32_t)crc;
     m.rc = Z_OK;
+    const double t_end = now_s();
+    std::lock_guard<std::mutex> lk(g_st_mu);
+    g_st[kStCopy] = t_copied - t_start;
+    g_st[kStParse] = st.t_parse;
+    g_st[kStSync] = st.t_sync;
+    g_st[kStSched] = st.t_sched;
+    g_st[kStPlan] = st.t_plan;
+    g_st[kStEncode] = st.t_encode;
+    g_st[kStCrc] = t_end - t_deflated;
     return true;
+} catch (const std::bad_alloc&) {
+    std::vector<uint8_t>().swap(m.out);
+    g_par_fallback.fetch_add(1);
+    g_par_reason = "out of memory";
+    return false;
+} catch (const std::system_error&) {   // a worker thread could not be started
+    std::vector<uint8_t>().swap(m.out);
+    g_par_fallback.fetch_add(1);
+    g_par_reason = "no thread";
+    return false;
 }
 
 // zlib.compressobj(-1, DEFLATED, -15).compress(w) for each write w, then .flush()
@@ -150,11 +203,83 @@ void deflate_member(Member& m) {
     m.rc = ok ? Z_OK : Z_STREAM_ERROR;
 }
 
+// Why this process's libz may not be replaced by pdeflate.h ("" = it may). The self-test member is a
+// .npy-like header and 1.5 MiB written in 256 KiB pieces: float32-like noise, a zero run (258-byte
+// matches), a short period (lazy matches, chains at their limit) and repeated text, so the chunked
+// parse, the syncs, the tail replay and all three block types are exercised against this libz.
+std::string zlib_check_locked() {
+    const char* v = zlibVersion();
+    bool known = false;
+    for (const char* k : kModelledZlib) known = known || std::strcmp(v, k) == 0;
+    if (!known) return std::string("libz ") + v + " is not a version pdeflate.h models (1.2.11)";
+    if (!g_zl_expect.empty() && g_zl_expect != v)
+        return "Python's zlib runs libz " + g_zl_expect + ", this library links " + v;
+    const int64_t n = 3 << 19;
+    const char* dict = "{'descr': '<f4', 'fortran_order': False, 'shape': (393216,), }";
+    std::vector<uint8_t> hdr(128, ' ');
+    std::memcpy(hdr.data(), dict, std::strlen(dict));
+    hdr.back() = '\n';
+    std::vector<uint8_t> data((size_t)n);
+    uint32_t x = 2463534242u;
+    const char* text = "federated averaging of client updates, round after round; ";
+    for (int64_t i = 0; i < n; i += 4) {
+        x ^= x << 13, x ^= x >> 17, x ^= x << 5;
+        const int64_t part = i / (n / 8);
+        uint32_t w;
+        if (part == 2) w = 0;                                              // zero run
+        else if (part == 5) w = 0x3c000000u | (uint32_t)((i / 4) % 7) << 8; // short period
+        else if (part == 6) std::memcpy(&w, text + (i % 56), 4);           // text
+        else w = 0x3c000000u | (x & 0x01ffffffu);                          // small float32 weights
+        std::memcpy(&data[(size_t)i], &w, 4);
+    }
+    Member z{"t", hdr.data(), (int64_t)hdr.size(), data.data(), n, 256 << 10};
+    deflate_member(z);
+    if (z.rc != Z_OK) return "self-test: this libz failed to deflate";
+    const int64_t L = z.hlen + n;
+    std::vector<uint8_t> S((size_t)L);
+    std::memcpy(S.data(), hdr.data(), hdr.size());
+    std::memcpy(S.data() + hdr.size(), data.data(), (size_t)n);
+    std::vector<uint8_t> out;
+    pdef::Stats st;
+    if (!pdef::deflate_exact(S.data(), L, input_ends(z.hlen, n, z.seg), 4, pdef::kMinChunk, out, &st))
+        return std::string("self-test: pdeflate.h fell back (") + (st.fallback ? st.fallback : "?") + ")";
+    if (out != z.out) return std::string("self-test: pdeflate.h's stream differs from libz ") + v + "'s";
+    return "";
+}
+
+// whether big members may take pdeflate.h (evaluated once; re-evaluated after fnpz_savez_zlib_expect)
+bool zlib_modelled() {
+    const int s = g_zl_state.load(std::memory_order_acquire);
+    if (s >= 0) return s == 1;
+    std::lock_guard<std::mutex> lk(g_zl_mu);
+    if (g_zl_state.load() < 0) {
+        std::string why;
+        try {
+            why = g_zl_force ? std::string("forced off (fnpz_savez_zlib_expect test hook)") : zlib_check_locked();
+        } catch (const std::exception&) {   // no memory for the self-test: zlib this time, ask again later
+            return false;
+        }
+        g_zl_reason = why.empty() ? std::string("libz ") + zlibVersion() + ": pdeflate.h matches it (self-test passed)"
+                                  : why;
+        g_zl_state.store(why.empty() ? 1 : 0, std::memory_order_release);
+    }
+    return g_zl_state.load() == 1;
+}
+
+bool deflate_member_parallel(Member& m, int threads) {
+    if (!zlib_modelled()) {
+        g_par_reason = "libz not modelled";
+        return false;
+    }
+    return deflate_member_parallel_unchecked(m, threads);
+}
+
 }  // namespace
 
 extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const* headers, const int64_t* header_lens,
                           const void* const* datas, const int64_t* nbytes, const int64_t* seg_bytes, int threads,
                           uint8_t* out, int64_t out_cap, int64_t* out_len) {
+    const double t_call = now_s();
     return fnpz_internal::guard("fnpz_savez", [&]() -> int {
         if (n < 0 || !out || !out_len || (n > 0 && (!names || !headers || !header_lens || !datas || !nbytes)))
             return set_error(FNPZ_EINVAL, "fnpz_savez: bad arguments");
@@ -194,6 +319,8 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
         std::vector<uint64_t> offs((size_t)n);
         std::vector<uint64_t> comps((size_t)n);
         std::vector<uint16_t> ver((size_t)n);
+        std::vector<uint8_t*> dst((size_t)n);
+        const double t_asm = now_s();
         for (int i = 0; i < n; ++i) {
             const Member& m = ms[i];
             const size_t nl = std::strlen(m.name) + 4;
@@ -222,9 +349,22 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
             put16(p, 16);
             put64(p, raw);
             put64(p, comp);
-            std::memcpy(p, m.out.data(), comp);
+            dst[i] = p;
             p += comp;
-            std::vector<uint8_t>().swap(ms[i].out);
+        }
+        // the deflate streams into place, in 8 MiB pieces on every thread (one 370 MB member copied
+        // by one thread, page faults on the fresh output included, was a serial ~0.1 s of the save)
+        {
+            const int64_t piece = 8 << 20;
+            std::vector<std::pair<int, int64_t>> pieces;
+            for (int i = 0; i < n; ++i)
+                for (int64_t b = 0; b < (int64_t)ms[i].out.size(); b += piece) pieces.emplace_back(i, b);
+            fnpz_internal::run_parallel((int)pieces.size(), std::max(1, threads), [&](int k) {
+                const int i = pieces[k].first;
+                const int64_t b = pieces[k].second;
+                std::memcpy(dst[i] + b, ms[i].out.data() + b, (size_t)std::min<int64_t>(piece, ms[i].out.size() - b));
+            });
+            for (Member& m : ms) std::vector<uint8_t>().swap(m.out);
         }
         const uint64_t cd_off = (uint64_t)(p - out);
         for (int i = 0; i < n; ++i) {   // ZipFile._write_end_record
@@ -298,8 +438,40 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
         put32(p, (uint32_t)offset);
         put16(p, 0);
         *out_len = (int64_t)(p - out);
+        {
+            std::lock_guard<std::mutex> lk(g_st_mu);
+            g_st[kStAssemble] = now_s() - t_asm;
+            g_st[kStTotal] = now_s() - t_call;
+        }
         return FNPZ_OK;
     });
+}
+
+extern "C" void fnpz_savez_zlib_expect(const char* runtime_version, int force_zlib) {
+    std::lock_guard<std::mutex> lk(g_zl_mu);
+    if (runtime_version) g_zl_expect = runtime_version;
+    if (force_zlib >= 0) g_zl_force = force_zlib ? 1 : 0;
+    g_zl_state.store(-1);
+    g_zl_reason = "not evaluated";
+}
+
+extern "C" int fnpz_savez_zlib_status(char* reason, int64_t cap) {
+    const bool on = zlib_modelled();
+    if (reason && cap > 0) {
+        std::lock_guard<std::mutex> lk(g_zl_mu);
+        const size_t k = std::min<size_t>(g_zl_reason.size(), (size_t)cap - 1);
+        std::memcpy(reason, g_zl_reason.data(), k);
+        reason[k] = 0;
+    }
+    return on ? 1 : 0;
+}
+
+extern "C" int fnpz_savez_stats(double* out, int n) {
+    if (!out || n <= 0) return kStN;
+    std::lock_guard<std::mutex> lk(g_st_mu);
+    const int k = std::min(n, (int)kStN);
+    for (int i = 0; i < k; ++i) out[i] = g_st[i];
+    return k;
 }
 
 extern "C" void fnpz_savez_config(int64_t min_member, int64_t chunk, int64_t* parallel, int64_t* fallback) {

@@ -363,7 +363,14 @@ class Helper:
             if npz_writer() == "blocks":
                 data = codec.save_npz_blocks(weights)
             else:
-                data = memoryview(codec.savez_into(weights))
+                try:
+                    data = memoryview(codec.savez_into(weights))
+                except MemoryError:
+                    # the native writer holds the archive in memory (and, for a big member, a copy of
+                    # it): where that does not fit, numpy itself streams the same bytes to the target
+                    # in 16 MiB writes, as the reference does
+                    np.savez_compressed(path, **{str(i): w for i, w in enumerate(weights)})
+                    return path
             if hasattr(path, "write"):
                 path.write(data)
             else:

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 7
+#define FA_ABI_VERSION 8
 
 /* element type codes */
 enum fa_dtype {
@@ -100,6 +100,19 @@ int fa_fedavg_fold(void* agg, int agg_dtype,
                    const void* const* updates, int upd_dtype,
                    const double* n, const double* N, int K,
                    int64_t P, int init, void* stream);
+
+/*
+ * fa_fedavg_fold_host (ABI 8): fa_fedavg_fold for a small model whose round never leaves the host
+ * (configs[0]: FEDn's mnist-pytorch example, fedavg.py:47-83 over 52,650 parameters). agg and every
+ * updates[k] are PAGE-LOCKED HOST addresses (e.g. the pinned arena the updates were packed into and a
+ * pinned result block); the kernel reads and writes them over PCIe through their device mappings
+ * (hipHostGetDevicePointer), and the call returns once `stream` has drained, with the model in agg.
+ * No H2D / D2H copy and no event: the round's GPU work is one launch and one wait. Same kernel,
+ * client table and dtype pairs as fa_fedavg_fold, so the same bits. K <= 64 (one launch).
+ * FA_EINVAL for memory that is not page-locked.
+ */
+int fa_fedavg_fold_host(void* agg, int agg_dtype, const void* const* updates, int upd_dtype,
+                        const double* n, const double* N, int K, int64_t P, int init, void* stream);
 
 /*
  * FedOpt (fedopt.py:74-118, 151-258), fused: pseudo-gradient running mean over the

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define FNPZ_ABI_VERSION 6
+#define FNPZ_ABI_VERSION 7
 #define FNPZ_MAX_DIMS 64   /* numpy 2's NPY_MAXDIMS (ABI 6; 16 before) */
 
 /* Every entry point returns a status; no C++ exception leaves the library. FNPZ_ENOMEM (ABI 6):
@@ -101,6 +101,23 @@ int fnpz_savez(int n, const char* const* names, const uint8_t* const* headers, c
  * zlib 1.2.11's level-6 parse and trees.c whose output is zlib's, byte for byte; an input it does not model falls back to zlib itself. Values <= 0 keep a setting.
  * *parallel / *fallback (may be NULL): members that went parallel / fell back so far. */
 void fnpz_savez_config(int64_t min_member, int64_t chunk, int64_t* parallel, int64_t* fallback);
+
+/* Which libz fnpz_savez's big members may bypass (ABI 7). pdeflate.h reproduces zlib 1.2.11's
+ * level-6 stream only; a big member takes it while the process's libz reports a modelled version,
+ * equals the libz Python's zlib runs (zlib.ZLIB_RUNTIME_VERSION: numpy's archive comes from it) and
+ * passes a self-test (one 1.5 MiB member through both, byte for byte), checked once, at the first
+ * big member. Otherwise EVERY member goes through the process's libz, so an archive never mixes two
+ * deflaters. fnpz_savez_zlib_expect records Python's runtime version (NULL keeps it) and, for tests,
+ * force_zlib = 1 acts as a failed check (0 clears it, < 0 keeps it); the check is then redone.
+ * fnpz_savez_zlib_status returns 1 when big members may take pdeflate.h, else 0, and copies the
+ * reason into reason[0, cap). */
+void fnpz_savez_zlib_expect(const char* runtime_version, int force_zlib);
+int fnpz_savez_zlib_status(char* reason, int64_t cap);
+
+/* Phase times (s) of fnpz_savez's last big member (ABI 7): out[0..8) = input copy, parse, sync,
+ * window schedule + tail replay, block plan, encode, CRC, archive assembly, and out[8] the last
+ * call's total. Returns how many were written (9 at most; with out NULL, how many there are). */
+int fnpz_savez_stats(double* out, int n);
 
 /* zipfile's ZIP64_LIMIT ((1 << 31) - 1) and ZIP_FILECOUNT_LIMIT ((1 << 16) - 1) as fnpz_savez applies
  * them (sizes / offsets past the first: ZIP64 fields and version 45; more members than the second,

@@ -156,3 +156,77 @@ def test_save_npz_member_over_its_thread_share_goes_parallel():
     ref = io.BytesIO()
     np.savez_compressed(ref, **{str(i): w for i, w in enumerate(ws)})
     assert got == ref.getvalue()
+
+
+def _counts(lib):
+    par, fb = ctypes.c_int64(), ctypes.c_int64()
+    lib.fnpz_savez_config(0, 0, ctypes.byref(par), ctypes.byref(fb))
+    return par.value, fb.value
+
+
+def test_writer_checks_the_libz_it_stands_in_for():
+    """The parallel path is allowed only on a libz it models, which is the one Python's zlib runs and
+    which passes the self-test (fednpz.h ABI 7): true here (zlib 1.2.11, numpy's libz)."""
+    on, why = codec.savez_zlib_status()
+    assert zlib.ZLIB_RUNTIME_VERSION == "1.2.11"
+    assert on, why
+    assert "self-test passed" in why
+
+
+def test_unmodelled_libz_sends_every_member_through_libz():
+    """on a libz pdeflate.h does not model, a big member is NOT computed by pdeflate.h
+    (its bytes would be 1.2.11's next to small members from the host's libz): every member goes through
+    the process's libz, and the archive still equals np.savez_compressed on this host. The mismatch is
+    forced through the test hook, with the parallel threshold lowered so the member would qualify."""
+    lib = _lib()
+    rng = np.random.default_rng(21)
+    ws = [rng.standard_normal(1_200_000).astype(np.float32), np.arange(1000, dtype=np.int16)]
+    ref = io.BytesIO()
+    np.savez_compressed(ref, **{str(i): w for i, w in enumerate(ws)})
+    codec.savez_force_zlib(True)
+    lib.fnpz_savez_config(1 << 20, CHUNK, None, None)
+    try:
+        on, why = codec.savez_zlib_status()
+        assert not on and "forced off" in why
+        p0, f0 = _counts(lib)
+        got = codec.save_npz(ws, threads=4)
+        p1, f1 = _counts(lib)
+    finally:
+        lib.fnpz_savez_config(32 << 20, 4 << 20, None, None)
+        codec.savez_force_zlib(False)
+    assert (p1, f1) == (p0, f0)                  # no member went to pdeflate.h
+    assert got == ref.getvalue()
+    assert codec.savez_zlib_status()[0]           # the check is redone once the hook is cleared
+    p2, _ = _counts(lib)
+    lib.fnpz_savez_config(1 << 20, CHUNK, None, None)
+    try:
+        assert codec.save_npz(ws, threads=4) == ref.getvalue()
+    finally:
+        lib.fnpz_savez_config(32 << 20, 4 << 20, None, None)
+    assert _counts(lib)[0] == p2 + 1             # and the same member goes parallel again
+
+
+def test_python_running_another_libz_turns_the_parallel_path_off():
+    """The version Python's zlib reports is the one numpy's archive comes from: a different one (as when
+    CPython is linked against zlib-ng or a bundled zlib) turns the parallel path off."""
+    lib = codec.load_lib()
+    lib.fnpz_savez_zlib_expect(b"1.3.1", -1)
+    try:
+        on, why = codec.savez_zlib_status()
+        assert not on and "1.3.1" in why
+    finally:
+        lib.fnpz_savez_zlib_expect(zlib.ZLIB_RUNTIME_VERSION.encode(), -1)
+    assert codec.savez_zlib_status()[0]
+
+
+def test_savez_stats_report_the_phases():
+    lib = _lib()
+    x = np.random.default_rng(3).standard_normal(600_000).astype(np.float32)
+    lib.fnpz_savez_config(1 << 20, CHUNK, None, None)
+    try:
+        codec.save_npz([x], threads=3)
+    finally:
+        lib.fnpz_savez_config(32 << 20, 4 << 20, None, None)
+    st = codec.savez_stats()
+    assert list(st) == list(codec.SAVEZ_PHASES)
+    assert all(v >= 0 for v in st.values()) and st["parse"] > 0 and st["total"] >= st["parse"]

@@ -33,6 +33,32 @@ def _weights(z):
     return [SAVE_VIEWS[v](w) if v else w for w, v in zip(ws, views)]
 
 
+@pytest.mark.parametrize("name", CASES)
+def test_fixture_big_members_through_the_parallel_deflate(name):
+    """the same fixtures with the parallel threshold lowered to pdeflate.h's
+    smallest input (two 256 KiB chunks), so every member it can take — the sparse fixture's 2.4 MB and
+    20 MB members; the other fixtures' members are all under 512 KiB — is computed by it instead of
+    libz, with no fallback: the archive is still the reference's."""
+    import ctypes
+    z = golden_io.load_case(name)["raw"]
+    ws = _weights(z)
+    lib = codec.load_lib()
+    lib.fnpz_savez_config.restype = None
+    lib.fnpz_savez_config.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                                      ctypes.POINTER(ctypes.c_int64)]
+    par0, par1, fb0, fb1 = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    lib.fnpz_savez_config(0, 0, ctypes.byref(par0), ctypes.byref(fb0))
+    lib.fnpz_savez_config(512 << 10, 256 << 10, None, None)
+    try:
+        got = codec.save_npz(ws, threads=4)
+    finally:
+        lib.fnpz_savez_config(32 << 20, 4 << 20, None, None)
+    lib.fnpz_savez_config(0, 0, ctypes.byref(par1), ctypes.byref(fb1))
+    assert got == z["npz"].tobytes()
+    big = sum(1 for w in ws if np.asarray(w).nbytes >= 512 << 10)
+    assert (par1.value - par0.value, fb1.value - fb0.value) == (big, 0)
+
+
 def test_save_fixtures_present():
     assert len(CASES) >= 8
 

@@ -145,6 +145,35 @@ def main():
     finally:
         ref.increment_average = real
     out["fedn_arith_us"] = med(lambda: real(cl[0], cl[1], ns[1], ns[0] + ns[1]))
+    # round 6: the one-call round's own floor (smallround.py): the native wait + fold_host + stream wait
+    # over an arena already packed, into a pooled pinned block — no Python between launch and wait
+    from fedn_amd import smallround
+    from fedn_amd.layout import Layout
+    sess = smallround.SmallSession(dev, Layout.of(cl[0]))
+    for k, u in enumerate(cl):
+        sess.wait(sess.admit(u, k))
+    blk = sess.result_block()
+    out["fold_host_k2_us"] = med(lambda: sess.fold(blk, 2, [0.0, float(ns[1])], [1.0, float(ns[0] + ns[1])], 0))
+    out["admit_us"] = med(lambda: sess.wait(sess.admit(cl[1], 1)))
+    # FedOpt K = 2 (adam) through the plug-in and FEDn's loop restated, the same updates
+    uh3 = MemoryUpdateHandler()
+    gid = uh3.put_global_model(base, "g0")
+    opt = get_aggregator("fedopt", uh3)
+
+    def plugin_opt():
+        for u, n in zip(cl, ns):
+            uh3.submit(u, n, model_id=gid)
+        box["o"], _ = opt.combine_models(helper=None, parameters=bench_small.PARAMS)
+    out["plugin_fedopt_us"] = med(plugin_opt, n=400)
+    uh4 = MemoryUpdateHandler()
+    gid4 = uh4.put_global_model(base, "g0")
+    st4 = ref.FedOptState()
+
+    def loop_opt():
+        for u, n in zip(cl, ns):
+            uh4.submit(u, n, model_id=gid4)
+        bench_small.fedn_loop_fedopt(uh4, st4, bench_small.PARAMS)
+    out["fedn_loop_fedopt_us"] = med(loop_opt, n=400)
     gpu_floor = out["pack_k2_us"][0] + min(out["fold2_zero_copy_spin_us"][0], out["fold_zero_copy_us"][0])
     out["budget_us"] = round(out["fedn_loop_us"][0] - out["fedn_loop_no_arith_us"][0], 2)
     out["gpu_floor_us"] = round(gpu_floor, 2)
