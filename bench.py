@@ -372,14 +372,29 @@ def side(fn):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
-def fold_kernel_label(P, in_bytes, K):
-    if P * in_bytes >= 160 << 20:          # fedagg.hip kPipeMinClientBytes
-        if in_bytes == 4 and P >= 1 << 24:  # fedagg.hip avg_store_window: the first fp32 launch
-            return ("k_fedavg_pipe_win (fp32, 4 x 16-B strips per lane, next client prefetched; every wave's "
-                    "stores inside a chip-wide window of the GPU's 100 MHz clock)")
-        return ("k_fedavg_pipe (fp32, 4 x 16-B strips per lane, next client prefetched)" if in_bytes == 4 else
-                "k_fedavg_pipe (bf16 -> f32, 8 strips of 4 elements per lane, next client prefetched)")
-    return f"k_fedavg (1 x 16-B strip per lane, {8 if in_bytes < 4 or K <= 8 else 4} clients loaded ahead)"
+def fold_kernel_label(P, in_bytes, K, ran=None):
+    """The fold kernel's description; ``ran`` = the family the library reports it launched last on this
+    thread (ops.last_kernel(), fa_last_kernel) — what ran, not what the size rules suggest."""
+    from fedn_amd import ops
+    ran = ran or ops.last_kernel()
+    strips = ("4 x 16-B strips per lane" if in_bytes == 4 else "8 strips of 4 elements per lane, bf16 -> f32")
+    if ran == "k_fedavg_pipe_win":
+        return (f"k_fedavg_pipe_win ({strips}, next client prefetched; every wave's stores inside a chip-wide "
+                "window of the GPU's 100 MHz clock)")
+    if ran == "k_fedavg_pipe":
+        return f"k_fedavg_pipe ({strips}, next client prefetched; no store window)"
+    if ran == "k_fedavg":
+        return f"k_fedavg (1 x 16-B strip per lane, {8 if in_bytes < 4 or K <= 8 else 4} clients loaded ahead)"
+    return ran or "unknown (no fold launched on this thread)"
+
+
+OPT_KERNELS = {
+    "k_fedopt_cw": ("k_fedopt_cw (pseudo-gradient fold + Adam step fused; 4 coalesced element pairs per lane; the "
+                    "stores of all waves in a common window of the GPU's 100 MHz clock)"),
+    "k_fedopt_c": ("k_fedopt_c (pseudo-gradient fold + Adam step fused; 4 coalesced element pairs per lane; no "
+                   "store window)"),
+    "k_fedopt": "k_fedopt (pseudo-gradient fold + Adam step fused; per-lane strips)",
+}
 
 
 def configs1_side(ups, ns, agg, stream, device, in_bytes, a):
@@ -428,6 +443,7 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000, pattern_probe=
     for _ in range(warm):
         r1()
     _, ms1 = timed_steps(r1, steps, stream, 1, device, False)
+    ran = {"round1": ops.last_kernel()}
     # checker: round 1 on a sample, then the steady-state inputs of the sample
     S = min(sample, P)
     old_s = old32[:S].cpu().numpy()
@@ -451,6 +467,7 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000, pattern_probe=
     for _ in range(warm):
         r2()
     _, ms2 = timed_steps(r2, steps, stream, 1, device, False)
+    ran["steady"] = ops.last_kernel()
     st.m = [st.m[0].astype(np.float64)]           # the GPU's steady state takes m in float64 (round >= 3)
     t0 = time.perf_counter()
     want2, _ = ref.fedopt_combine(st, ups_s, want1, params)
@@ -470,6 +487,7 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000, pattern_probe=
     for _ in range(warm):
         r3()
     _, ms3 = timed_steps(r3, steps, stream, 1, device, False)
+    ran["steady_f32state"] = ops.last_kernel()
     st3 = ref.FedOptState()
     st3.m, st3.v = [m_f[:S].cpu().numpy()], [v_f[:S].cpu().numpy()]
     t0 = time.perf_counter()
@@ -502,8 +520,7 @@ def fedopt_side(P, K, device, steps=10, warm=2, sample=1_000_000, pattern_probe=
         res[phase] = {"ms": ms, "params_per_s": K * P / (ms / 1e3),
                       "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-                                   "kernel": ("k_fedopt_cw (pseudo-gradient fold + Adam step fused; 4 coalesced element pairs per "
-                                              "lane; the stores of all waves in a common window of the GPU's 100 MHz clock)"),
+                                   "kernel": OPT_KERNELS.get(ran[phase], ran[phase]),
                                    "alg_bytes_per_launch": b},
                       "bit_exact_on_sample": ok,
                       "sample": f"first {S} params of every buffer vs oracle/numpy_ref" +

@@ -35,6 +35,7 @@ EXPORTS = {
     # name: (restype, argtypes)
     "fa_abi_version": (ctypes.c_int, []),
     "fa_last_error": (ctypes.c_char_p, []),
+    "fa_last_kernel": (ctypes.c_char_p, []),
     "fa_promote": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "fa_fedavg_fold": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int,                       # agg, agg_dtype

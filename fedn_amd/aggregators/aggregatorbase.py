@@ -248,6 +248,27 @@ class AggregatorBase(ABC):
                     self._log_skip(e, traceback.format_exc())   # (fedavg.py:73-78): logged, still counted
         return len(skipped)
 
+    def _begin_deletes(self):
+        """The round's store deletes may run side by side (ingest.StagingUpdateHandler.begin_deletes)
+        until :meth:`_finish_deletes`."""
+        begin = getattr(self.update_handler, "begin_deletes", None)
+        if begin is not None:
+            begin()
+
+    def _end_round(self, pipe):
+        """However a round ends: the native gather thread is done with the round's update arrays and
+        arenas before they can be freed or reused (staging._Pipeline.quiesce), and — even when that
+        wait raises — the round's store deletes are all done, their failures logged."""
+        try:
+            if pipe is not None and hasattr(pipe, "quiesce"):
+                pipe.quiesce()
+        finally:
+            try:
+                self._finish_deletes()
+            except Exception as e:  # noqa: BLE001 — logged; never masks the round's own exception
+                import traceback
+                self._log_skip(e, traceback.format_exc())
+
     def _finish_deletes(self):
         """Wait for the store deletes an update handler runs side by side
         (ingest.StagingUpdateHandler.finish_deletes): every folded update is deleted when

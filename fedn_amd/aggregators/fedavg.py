@@ -83,16 +83,12 @@ class Aggregator(AggregatorBase):
         self._small = SmallSessions()    # configs[0]-sized rounds: arena, plans, result blocks (smallround.py)
 
     def combine_models(self, helper=None, delete_models=True, parameters=None):
+        self._begin_deletes()
         try:
             return self._combine(helper, delete_models, parameters)
         finally:
-            # whatever way the round ends, the native gather thread is done with its update arrays
-            # and arenas before they can be freed or reused (staging._Pipeline.quiesce)
             pipe, self._live = getattr(self, "_live", None), None
-            if pipe is not None and hasattr(pipe, "quiesce"):
-                pipe.quiesce()
-            # the round's store deletes (run side by side by the staging handler) are all done
-            self._finish_deletes()
+            self._end_round(pipe)
 
     def _small_round(self, first, helper):
         """configs[0]'s one-call round (smallround.py) when ``first`` is a small float model's update

@@ -81,16 +81,12 @@ class Aggregator(AggregatorBase):
         return None if self.state is None else self.state.v_host()
 
     def combine_models(self, helper=None, delete_models=True, parameters=None):
+        self._begin_deletes()
         try:
             return self._combine(helper, delete_models, parameters)
         finally:
-            # whatever way the round ends, the native gather thread is done with its update arrays
-            # and arenas before they can be freed or reused (staging._Pipeline.quiesce)
             pipe, self._live = getattr(self, "_live", None), None
-            if pipe is not None and hasattr(pipe, "quiesce"):
-                pipe.quiesce()
-            # the round's store deletes (run side by side by the staging handler) are all done
-            self._finish_deletes()
+            self._end_round(pipe)
 
     def _combine(self, helper, delete_models, parameters):
         data = {"time_model_load": 0.0, "time_model_aggregation": 0.0}

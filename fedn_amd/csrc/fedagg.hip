@@ -43,6 +43,9 @@ namespace {
 // error plumbing
 // ----------------------------------------------------------------------------
 thread_local char g_err[512] = "";
+// the kernel family the calling thread's last fold / FedOpt launch used (fa_last_kernel): a diagnostic
+// like g_err, so a benchmark names the kernel that ran, not one it infers
+thread_local const char* g_kernel = "";
 
 int fail(int code, const char* fmt, ...) {
     va_list ap;
@@ -2077,6 +2080,7 @@ AvgWindow avg_store_window(int K, int64_t P) {
 template <typename Y, typename X, class CP, int E, int S, bool NT, bool LT, int BLK = kBlock, int NTS = 0, int MAP = 0>
 void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
                         hipStream_t st) {
+    g_kernel = "k_fedavg_pipe";
     const int64_t strips = (P + E - 1) / E;
     int64_t ntiles = (strips + (int64_t)BLK * S - 1) / ((int64_t)BLK * S);
     if (cfg_grid_per_cu() > 0) {
@@ -2101,6 +2105,7 @@ void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, i
             }
 #endif
             if (w.period) {
+                g_kernel = "k_fedavg_pipe_win";
                 hipLaunchKernelGGL((k_fedavg_pipe_win<Y, X, CP, E, S, true, false, NT, LT, BLK, NTS, MAP>), grid, dim3(BLK), 0, st, a,
                                    tab, cnt, P, w.period, w.w, wm);
                 return;
@@ -2142,6 +2147,7 @@ void launch_fedavg_pipe(X* a, const ClientTable<typename CP::S>& tab, int cnt, i
 template <typename Y, typename X, class CP, int E, int S, int U, bool NT>
 void launch_fedavg_geom(X* a, const ClientTable<typename CP::S>& tab, int cnt, int64_t P, bool first, bool int_first,
                         hipStream_t st) {
+    g_kernel = "k_fedavg";
     const int64_t strips = (P + E - 1) / E;
     const dim3 grid((unsigned)((strips + (int64_t)kBlock * S - 1) / ((int64_t)kBlock * S)));
     if (first && int_first) {
@@ -2284,6 +2290,7 @@ int launch_fedavg(void* agg, const void* const* ups, const double* n, const doub
 template <typename Y, typename OLD, class PG, int E, bool NT>
 int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTable<typename PG::S>& tab, int cnt,
                       int64_t P, bool first, bool final_, hipStream_t st) {
+    g_kernel = E == 4 ? "k_fedopt_c" : "k_fedopt";
     const dim3 grid((unsigned)grid_for(P, E));
 #ifdef FEDAGG_PROBES
     // the probe variants exist for the configs[3] shapes only (fp32 updates over an fp32 or fp64
@@ -2412,6 +2419,7 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
             }
 #endif
             if (sw.period) {
+                g_kernel = "k_fedopt_cw";
                 hipLaunchKernelGGL((k_fedopt_cw<Y, OLD, PG, NT>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P, sw.period, sw.w);
                 return check_launch("fa_fedopt_step: kernel launch");
             }
@@ -2490,6 +2498,7 @@ extern "C" {
 int fa_abi_version(void) { return FA_ABI_VERSION; }
 
 const char* fa_last_error(void) { return g_err; }
+const char* fa_last_kernel(void) { return g_kernel; }
 
 int fa_promote(int a, int b) {
     auto fl = [](int d) { return d == FA_BF16 ? FA_F32 : d; };

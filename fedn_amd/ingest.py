@@ -25,6 +25,7 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 import torch
 
+from . import reuse
 from .budget import HbmBudget
 from .layout import Layout, spread
 
@@ -123,7 +124,7 @@ def stage_sharded(layout, pinned, devices, streams, host=None):
     for d, dv in enumerate(devices):
         with torch.cuda.device(dv):
             with torch.cuda.stream(streams[d]):   # allocated on the stream that writes it
-                buf = torch.empty(dev_bytes[d], dtype=torch.uint8, device=dv)
+                buf = reuse.watch(torch.empty(dev_bytes[d], dtype=torch.uint8, device=dv), streams[d])
                 for dt in layout.groups:
                     lo, hi = bounds[dt][d]
                     if hi > lo:
@@ -148,7 +149,7 @@ def stage_arrays(arrays, device, stream):
     layout.pack(arrays, pinned.numpy())
     ready = torch.cuda.Event()
     with torch.cuda.stream(stream):                 # allocated on the stream that writes it
-        dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
+        dev = reuse.watch(torch.empty(layout.nbytes, dtype=torch.uint8, device=device), stream)
         dev.copy_(pinned, non_blocking=True)
         ready.record(stream)
     # the pinned block returns to torch's caching host allocator only after the copy
@@ -171,7 +172,7 @@ def stage_pinned(layout, pinned, device, stream, host=None):
     """Copy a pinned, layout-packed update (uint8 tensor) to a new device buffer on ``stream``."""
     ready = torch.cuda.Event()
     with torch.cuda.stream(stream):                 # allocated on the stream that writes it
-        dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
+        dev = reuse.watch(torch.empty(layout.nbytes, dtype=torch.uint8, device=device), stream)
         dev.copy_(pinned, non_blocking=True)
         ready.record(stream)
     ready.synchronize()
@@ -199,7 +200,7 @@ def stage_decoded(decoded, device, stream):
         layout = Layout(decoded.shapes, decoded.dtypes)
         ready = torch.cuda.Event()
         with torch.cuda.stream(stream):
-            dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
+            dev = reuse.watch(torch.empty(layout.nbytes, dtype=torch.uint8, device=device), stream)
             stream.wait_event(decoded.ready)
             for dt in layout.groups:
                 g0 = layout.group_byte_offset[dt]
@@ -212,7 +213,7 @@ def stage_decoded(decoded, device, stream):
     layout = Layout.of(decoded.arrays)
     ready = torch.cuda.Event()
     with torch.cuda.stream(stream):
-        dev = torch.empty(layout.nbytes, dtype=torch.uint8, device=device)
+        dev = reuse.watch(torch.empty(layout.nbytes, dtype=torch.uint8, device=device), stream)
         for dt in layout.groups:
             g0 = layout.group_byte_offset[dt]
             for i, e0, n, o in _member_spans(layout, dt, 0, layout.group_elems[dt]):
@@ -233,7 +234,7 @@ def stage_decoded_sharded(decoded, devices, streams):
     for d, dv in enumerate(devices):
         with torch.cuda.device(dv):
             with torch.cuda.stream(streams[d]):   # allocated on the stream that writes it
-                buf = torch.empty(dev_bytes[d], dtype=torch.uint8, device=dv)
+                buf = reuse.watch(torch.empty(dev_bytes[d], dtype=torch.uint8, device=dv), streams[d])
                 for dt in layout.groups:
                     lo, hi = bounds[dt][d]
                     base, isz = dev_off[d][dt], dt.itemsize
@@ -326,6 +327,7 @@ class StagingUpdateHandler:
         self.delete_workers = max(0, int(delete_workers))
         self._deleter = None
         self._deletes = []                # (model_update, future) not waited for yet
+        self._in_round = False            # begin_deletes .. finish_deletes: store deletes side by side
         self.delete_times = {"plugin_s": 0.0, "store_s": 0.0, "wait_s": 0.0, "count": 0}
 
     def __getattr__(self, name):
@@ -567,7 +569,9 @@ class StagingUpdateHandler:
         d = self.delete_times
         d["plugin_s"] += t1 - t0
         d["count"] += 1
-        if self.delete_workers == 0:
+        if self.delete_workers == 0 or not self._in_round:
+            # inline (as the reference) unless inside an aggregator's round: a delete made outside
+            # combine_models (a hook's own loop) would otherwise be waited for by nobody
             ok = self.inner.delete_model(model_update)
             d["store_s"] += time.perf_counter() - t1
             return ok
@@ -584,9 +588,16 @@ class StagingUpdateHandler:
             with self._lock:
                 self.delete_times["store_s"] += time.perf_counter() - t
 
+    def begin_deletes(self):
+        """An aggregator's round starts: its store deletes may run side by side until
+        :meth:`finish_deletes` (which the aggregator calls however the round ends)."""
+        self._in_round = True
+
     def finish_deletes(self):
         """Wait for every store delete handed to the pool; returns [(model_update, exception)] of
-        the ones that raised (the aggregator logs them as the reference logs a failed update)."""
+        the ones that raised (the aggregator logs them as the reference logs a failed update).
+        Deletes after this run inline again until the next :meth:`begin_deletes`."""
+        self._in_round = False
         pending, self._deletes = self._deletes, []
         t = time.perf_counter()
         failed = []

@@ -26,7 +26,7 @@ as the reference's list comprehension either completes or raises before the assi
 import numpy as np
 import torch
 
-from . import ops
+from . import ops, reuse
 
 _NARROW = {np.dtype(t) for t in (np.int8, np.int16, np.uint8, np.uint16, np.uint32, np.uint64)}
 _SUPPORTED = {np.dtype(t) for t in (np.float16, np.float32, np.float64, np.int32, np.int64)} | _NARROW
@@ -150,7 +150,7 @@ def upload(arrays, device, stream):
             a = np.asarray(a)
             if a.dtype not in _SUPPORTED:
                 raise TypeError(f"unsupported dtype {a.dtype}")
-            out.append(torch.from_numpy(a if a.flags.c_contiguous else a.copy()).to(device))   # keeps 0-d shapes
+            out.append(reuse.watch(torch.from_numpy(a if a.flags.c_contiguous else a.copy()).to(device)))   # keeps 0-d shapes
     return out
 
 

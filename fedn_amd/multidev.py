@@ -32,7 +32,7 @@ import time
 import numpy as np
 import torch
 
-from . import mixed, ops
+from . import mixed, ops, reuse
 from .ingest import ShardedStagedModel, StagedModel, _member_spans
 from .layout import Layout
 from .staging import (BATCH, HostStreamer, check_fedopt_dtypes, chunks, fused_fedopt_pair, group_tensors, old_members,
@@ -56,7 +56,7 @@ class _DevSlot:
     __slots__ = ("dev", "h2d_done", "consumed", "used")
 
     def __init__(self, nbytes, device):
-        self.dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        self.dev = reuse.watch(torch.empty(nbytes, dtype=torch.uint8, device=device))
         self.h2d_done = torch.cuda.Event()
         self.consumed = torch.cuda.Event()
         self.used = False

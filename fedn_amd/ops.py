@@ -518,7 +518,8 @@ def fedavg_fold_push(agg_ptr, ptrs, n, N, P, init, dst_ptrs, stream, device, rel
     """The fp32 fold of ``P`` elements into device address ``agg_ptr`` whose kernel also stores the
     result to every address in ``dst_ptrs`` (``fa_fedavg_fold_push``: fold and all-gather push in
     one pass); client table and destinations as device addresses, 16-B aligned. ``release_rec``: a
-    :func:`release_record` tensor on ``device`` the release grid records its XCDs in (or None)."""
+    :func:`release_record` tensor on ``device`` the release grid records its XCDs in (or None).
+    Returns whether a release grid was launched (there were destinations and something to fold)."""
     K = len(ptrs)
     if len(n) != K or len(N) != K:
         raise ValueError("n and N must have one entry per update")
@@ -529,12 +530,14 @@ def fedavg_fold_push(agg_ptr, ptrs, n, N, P, init, dst_ptrs, stream, device, rel
             int(agg_ptr), (ctypes.c_void_p * max(1, K))(*ptrs), (ctypes.c_double * max(1, K))(*n),
             (ctypes.c_double * max(1, K))(*N), K, int(P), int(bool(init)),
             (ctypes.c_void_p * max(1, nd))(*[int(p) for p in dst_ptrs]), nd, rec, ctypes_stream(stream)))
+    return K > 0 and P > 0 and nd > 0    # a release grid ran after the peer stores
 
 
 def push(dst_ptrs, src, nbytes, stream, release_rec=None):
     """``nbytes`` of device tensor ``src`` (from its start) to every device address in ``dst_ptrs``
     on ``stream`` with ONE kernel (``fa_push``): the source is read once, each destination written
-    over its own link (IPC mappings of peers' buffers, or other devices' buffers in-process)."""
+    over its own link (IPC mappings of peers' buffers, or other devices' buffers in-process).
+    Returns whether a release grid was launched (something was stored)."""
     lib = _abi.load()
     if nbytes > src.numel() * src.element_size():
         raise ValueError("push: more bytes than the source holds")
@@ -543,6 +546,8 @@ def push(dst_ptrs, src, nbytes, stream, release_rec=None):
     with _on(src.device):
         _abi.check(lib.fa_push((ctypes.c_void_p * max(1, n))(*[int(p) for p in dst_ptrs]), n, src.data_ptr(),
                                int(nbytes), rec, ctypes_stream(stream)))
+    return n > 0 and nbytes > 0          # a release grid ran after the stores (fa_push returns before one
+    #                                      when there is nothing to store)
 
 
 def release_record(device):
@@ -593,6 +598,12 @@ def _on(device):
 def peer_enable(dev, peer):
     """Direct access of device ``dev`` to device ``peer``'s memory (in-process multi-GPU)."""
     _abi.check(_abi.load().fa_peer_enable(int(dev), int(peer)))
+
+
+def last_kernel():
+    """The kernel family the calling thread's last fold / FedOpt launch ran (fa_last_kernel)."""
+    v = _abi.load().fa_last_kernel()
+    return v.decode() if v else ""
 
 
 def host_device_ptr(host_ptr, device):

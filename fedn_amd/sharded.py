@@ -276,9 +276,9 @@ class CyclicShardedFedAvg:
                     # the running aggregate is agg_local (read back when init is False, and what a later
                     # gather_to_host(agg_local) copies); this rank's copy in ``out`` is one more store
                     # destination beside the peers'
-                    ops.fedavg_fold_push(agg_local.data_ptr() + i * C * 4, [b + i * C * 4 for b in bases], n, N, C,
-                                         init, p2p.peer_ptrs(at) + [out.data_ptr() + at * 4], cur, dev,
-                                         release_rec=p2p.release_rec(cur))
+                    p2p.count_release(cur, ops.fedavg_fold_push(
+                        agg_local.data_ptr() + i * C * 4, [b + i * C * 4 for b in bases], n, N, C, init,
+                        p2p.peer_ptrs(at) + [out.data_ptr() + at * 4], cur, dev, release_rec=p2p.release_rec(cur)))
                 p2p.fence()
                 return out[:self.P]
             fold = self.round_folder(agg_local, updates_local, n, N, init, cur)
@@ -431,8 +431,15 @@ class P2PAllGather:
             from . import ops
             with torch.cuda.stream(stream):      # zeroed in the order of the stream that fills it
                 rec = self._release[key] = ops.release_record(self.device)
-        self._issued[key] = self._issued.get(key, 0) + 1   # each use is one release grid launch
         return rec
+
+    def count_release(self, stream, launched):
+        """One release grid was launched on ``stream`` (``launched``: what ops.push /
+        ops.fedavg_fold_push returned — counted only after the call succeeded and only when it did
+        launch one, so a call that stored nothing or failed its checks leaves the count right)."""
+        if launched:
+            key = stream.cuda_stream
+            self._issued[key] = self._issued.get(key, 0) + 1
 
     def check_release(self):
         """Synchronise and verify that every release grid of the peer-storing kernels so far covered
@@ -488,7 +495,8 @@ class P2PAllGather:
                 dsts.append(self.full.data_ptr() + at * self.esize)
             if dsts:
                 self.push_stream.wait_event(after)
-                ops.push(dsts, src, nbytes, self.push_stream, release_rec=self.release_rec(self.push_stream))
+                self.count_release(self.push_stream, ops.push(dsts, src, nbytes, self.push_stream,
+                                                              release_rec=self.release_rec(self.push_stream)))
             return local
         for r, st in self.streams.items():
             st.wait_event(after)

@@ -187,8 +187,13 @@ class SmallRound:
         added in order (same n, N and tags), as if they had gone that way from the start."""
         self.quiesce()
         pipe = make_pipeline(self.first)
-        for arrays, n, N, tag in self.held:
-            pipe.add(arrays, n, N, tag=tag)
+        try:
+            for arrays, n, N, tag in self.held:
+                pipe.add(arrays, n, N, tag=tag)
+        except BaseException:
+            if hasattr(pipe, "quiesce"):        # its packs in flight end before the arrays can go
+                pipe.quiesce()
+            raise
         return pipe
 
     def result(self):

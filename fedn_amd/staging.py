@@ -26,7 +26,7 @@ import time
 import numpy as np
 import torch
 
-from . import mixed, ops
+from . import mixed, ops, reuse
 from .ingest import StagedModel
 from .layout import Layout, fast_admission, parallel_copy, start_pack_into, wait_pack_jobs
 
@@ -140,7 +140,7 @@ class _Slot:
     def __init__(self, nbytes, device):
         self.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
         self.host_np = self.host.numpy()
-        self.dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        self.dev = reuse.watch(torch.empty(nbytes, dtype=torch.uint8, device=device))
         self.h2d_start = torch.cuda.Event(enable_timing=True)
         self.h2d_done = torch.cuda.Event(enable_timing=True)
         self.consumed = torch.cuda.Event()
@@ -159,7 +159,7 @@ class _Arena:
         self.host = torch.empty(cap * nbytes, dtype=torch.uint8, pin_memory=True)
         self.host_np = self.host.numpy()
         self.host_ptr = self.host.data_ptr()
-        self.dev = torch.empty(cap * nbytes, dtype=torch.uint8, device=device)
+        self.dev = reuse.watch(torch.empty(cap * nbytes, dtype=torch.uint8, device=device))
         self.dev_ptr = self.dev.data_ptr()
         self.cap, self.count, self.uploaded, self.used = cap, 0, 0, False
         self.done = None
@@ -450,7 +450,7 @@ class _Pipeline:
         if arrays.dev.device != self.device:         # staged on another GPU: one D2D copy
             arrays.ready.synchronize()               # (rare) order the copy after its H2D
             with torch.cuda.device(self.device):
-                dev = arrays.dev.to(self.device)
+                dev = reuse.watch(arrays.dev.to(self.device))
                 ready = torch.cuda.Event()
                 ready.record(torch.cuda.current_stream(self.device))
             arrays = StagedModel(arrays.layout, dev, ready, None)

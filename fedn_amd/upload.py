@@ -87,8 +87,9 @@ class DeviceSink:
                 raise MemoryError("HBM budget full: the upload is not decoded into HBM")
             self.reserved += n
         torch = self.torch
+        from . import reuse
         with torch.cuda.device(self.device), torch.cuda.stream(self.stream):   # allocated where it is written
-            return torch.empty(n, dtype=torch.uint8, device=self.device)
+            return reuse.watch(torch.empty(n, dtype=torch.uint8, device=self.device), self.stream)
 
     def window(self, blk, offset):
         if self.fill and (self.cur is not blk or self.cur_off + self.fill != offset):

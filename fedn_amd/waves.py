@@ -15,7 +15,7 @@ and the same kernel, so the result is bit-identical for any device count and any
 import numpy as np
 import torch
 
-from . import ops
+from . import ops, reuse
 from .sharded import shard_bounds
 
 
@@ -65,7 +65,7 @@ class WaveFedOpt:
             with torch.cuda.device(dv):
                 n = hi - lo
                 pg_dt, m_dt = ops.fedopt_dtypes(upd_dt, old[d].dtype, None if self.m[d] is None else self.m[d].dtype)
-                slots = [[torch.empty(n, dtype=upd_dt, device=dv) for _ in range(W)] for _ in range(2)]
+                slots = [[reuse.watch(torch.empty(n, dtype=upd_dt, device=dv)) for _ in range(W)] for _ in range(2)]
                 ctx.append({"n": n, "slots": slots, "pg": torch.empty(n, dtype=pg_dt, device=dv), "m_dt": m_dt,
                             "loaded": [torch.cuda.Event() for _ in range(2)],
                             "used": [torch.cuda.Event() for _ in range(2)]})

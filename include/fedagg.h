@@ -76,6 +76,10 @@ enum fa_serveropt { FA_ADAM = 0, FA_YOGI = 1, FA_ADAGRAD = 2 };
 
 int fa_abi_version(void);
 const char* fa_last_error(void);
+/* ABI 8: the kernel family the calling thread's last fold / FedOpt launch ran ("k_fedavg",
+ * "k_fedavg_pipe", "k_fedavg_pipe_win", "k_fedopt", "k_fedopt_c", "k_fedopt_cw"; "" before any), so a
+ * benchmark reports the kernel that ran — e.g. whether the store window was used — not a guess. */
+const char* fa_last_kernel(void);
 
 /*
  * FedAvg incremental weighted fold (numpyhelper.py:32):

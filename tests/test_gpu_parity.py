@@ -344,11 +344,12 @@ def test_fedopt_configs3_size_sampled():
 
 
 def test_fedopt_waves_1b_sampled():
-    """BASELINE configs[4]'s model size: 1 B-param bf16 updates streamed from pinned host memory in
-    waves of 8 over 2 parameter slices, FedYogi. 16 updates (8 distinct pinned buffers, each sent
-    twice, as bench.py's fedopt_waves does); the oracle checks 3 slices of 100 K elements."""
+    """BASELINE configs[4] as defined: 1 B-param bf16 updates, 128 of them, streamed
+    from pinned host memory in 16 waves of 8 over 2 parameter slices, FedYogi. 8 distinct pinned
+    buffers, each sent 16 times, as bench.py's fedopt_waves does; the oracle checks 3 slices of 100 K
+    elements (one straddling the two slices). ~10 s on the box (16 x 8 x 2 GB of H2D)."""
     from fedn_amd.waves import WaveFedOpt
-    P, K, pool = 1_000_000_000, 16, 8
+    P, K, pool = 1_000_000_000, 128, 8
     g = torch.Generator(device=DEV).manual_seed(6)
     base = torch.randn(P, generator=g, device=DEV)
     host = []

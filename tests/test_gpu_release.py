@@ -187,3 +187,27 @@ def test_p2p_allgather_release_count_must_match_launches():
     with pytest.raises(_abi.FedAggError, match="release grids recorded"):
         p2p.check_release()
     p2p.close(check=False)
+
+
+def test_p2p_push_that_stores_nothing_or_fails_leaves_the_count_right():
+    """a release is counted only once the ops call succeeded AND launched one. A push of 0
+    bytes (fa_push returns before any release grid) and a push refused by its checks (unaligned
+    source: FA_EINVAL before launching) must not make every later fence raise 'a release did not run'."""
+    from fedn_amd import _abi
+    from fedn_amd.sharded import CyclicShardedFedAvg, P2PAllGather
+    cyc = CyclicShardedFedAvg(100_000, chunk=65536)
+    ups = [torch.ones(cyc.local_len, device=DEV)]
+    full = torch.empty(cyc.full_len, device=DEV)
+    p2p = P2PAllGather(full, engine="kernel", verify="round")
+    agg = torch.empty(cyc.local_len, device=DEV)
+    cyc.fold_allgather(agg, ups, [1], [1], True, p2p=p2p)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(DEV))
+    src = torch.ones(64, device=DEV)
+    p2p.push(0, src[:0], ev, local=True)              # nothing to store: no release grid
+    with pytest.raises(_abi.FedAggError):
+        p2p.push(0, src[1:5], ev, local=True)         # 4-B offset source: refused before any launch
+    cyc.fold_allgather(agg, ups, [1], [1], True, p2p=p2p)   # the next round's fence checks the counts
+    r = p2p.check_release()
+    assert r["launches"] == 2 * cyc.rounds and r["misses"] == 0
+    p2p.close()

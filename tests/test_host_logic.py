@@ -619,6 +619,7 @@ def test_store_deletes_run_side_by_side_and_finish_before_the_round_ends(workers
     inner = _SlowStoreHandler(0.15)
     st = StagingUpdateHandler(inner, helper=None, device="cpu", workers=1, delete_workers=workers)
     mus = _mus(4)
+    st.begin_deletes()                       # what combine_models does first
     t0 = time.perf_counter()
     for mu in mus:
         st.delete_model(mu)
@@ -651,6 +652,7 @@ def test_a_failed_store_delete_is_logged_as_the_reference_logs_it(caplog):
         def combine_models(self, helper=None, delete_models=True, parameters=None):
             return None, {}
     agg = Agg(st)
+    agg._begin_deletes()
     for mu in _mus(3):
         st.delete_model(mu)
     with caplog.at_level(logging.ERROR, logger="fedn"):
@@ -658,4 +660,44 @@ def test_a_failed_store_delete_is_logged_as_the_reference_logs_it(caplog):
     assert sorted(inner.deleted) == ["u0", "u2"]
     assert any("Error encoutered while processing model update: cannot delete u1" in r.getMessage()
                for r in caplog.records)
+    st.close()
+
+
+def test_deletes_outside_a_round_run_inline_and_a_failed_wait_still_finishes_them(caplog):
+    """a delete_model made outside combine_models runs inline (nobody would wait for a
+    background one), and the round's deletes are waited for even when the pipeline's quiesce raises —
+    their failures logged, the round's own exception not masked."""
+    import logging
+
+    from fedn_amd.aggregators.aggregatorbase import AggregatorBase
+    from fedn_amd.ingest import StagingUpdateHandler
+    inner = _SlowStoreHandler(0.0, bad={"u2"})
+    st = StagingUpdateHandler(inner, helper=None, device="cpu", workers=1, delete_workers=2)
+    mus = _mus(4)
+    st.delete_model(mus[0])                  # no round: inline, on this thread
+    assert inner.deleted == ["u0"] and inner.threads == {"MainThread"}
+    with pytest.raises(OSError):
+        st.delete_model(mus[2])              # inline: the store's error reaches the caller
+
+    class Agg(AggregatorBase):
+        def __init__(self, uh):
+            super().__init__(uh)
+            self.name = "fedavg"
+
+        def combine_models(self, helper=None, delete_models=True, parameters=None):
+            return None, {}
+
+    class Stuck:
+        def quiesce(self):
+            raise RuntimeError("gather thread failed")
+    agg = Agg(st)
+    agg._begin_deletes()
+    st.delete_model(mus[1])
+    st.delete_model(mus[2])
+    with caplog.at_level(logging.ERROR, logger="fedn"), pytest.raises(RuntimeError, match="gather thread"):
+        agg._end_round(Stuck())
+    assert sorted(inner.deleted) == ["u0", "u1"] and not st._deletes
+    assert any("cannot delete u2" in r.getMessage() for r in caplog.records)
+    st.delete_model(mus[3])                  # the round is over: inline again
+    assert "u3" in inner.deleted
     st.close()
