@@ -627,6 +627,20 @@ def fedavg_fold_raw(out_ptr, out_dtype, P, ptrs, upd_dtype, n, N, init, stream, 
                                               ctypes_stream(stream)))
 
 
+def fedavg_fold_host(call, n, N):
+    """A small round's whole fold (smallround.py): ``call(n, N)`` runs the native pack wait +
+    ``fa_fedavg_fold_host`` + stream wait (``_fastpack.fold_host``) with the client table's ``n`` /
+    ``N`` and returns its status; FedAggError on a failed one (the C-ABI wrapper level, as every
+    fold op here), CodecError if the pack it waited for failed."""
+    if len(n) != len(N):
+        raise ValueError("n and N must have one entry per update")
+    rc = call(n, N)
+    if rc == -1:
+        from . import codec
+        raise codec.CodecError(f"fnpz_gather_wait: {codec.load_lib().fnpz_last_error().decode(errors='replace')}")
+    _abi.check(rc)
+
+
 def host_register(t):
     """Page-lock the memory of host tensor ``t`` (mapped by the caller, e.g. shared memory)."""
     _abi.check(_abi.load().fa_host_register(t.data_ptr(), t.numel() * t.element_size()))

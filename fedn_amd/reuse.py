@@ -9,7 +9,7 @@ before the read. Whether that corrupts a round is a matter of timing, so a test 
 With the knob on, every buffer registered with :func:`watch` (the staging allocations of ingest.py,
 upload.py, staging.py, multidev.py, mixed.py) is watched: the moment its tensor is freed, a poison
 thread allocates blocks of the same size on the same stream until the allocator hands it that very
-block (or 2 ms pass) and fills it with 0xFF bytes — a NaN in every float dtype — on that stream. A
+block (or 0.3 ms pass) and fills it with 0xFF bytes — a NaN in every float dtype — on that stream. A
 buffer still read by an enqueued launch and not protected (held until the reader ran, or
 ``record_stream``'d) is then overwritten right away, and the round's result is wrong; a protected one
 is either not handed out until its reader finished (the poison lands after the read: harmless) or not
@@ -24,7 +24,7 @@ import weakref
 import torch
 
 ENABLED = os.environ.get("FEDN_AMD_POISON_REUSE", "") == "1"
-RETRY_S = 2e-3
+RETRY_S = 300e-6   # an unprotected block comes back at once; a protected one is safe whenever it does
 
 _q = queue.Queue()
 _stats = {"watched": 0, "poisoned": 0, "not_reissued": 0}
@@ -86,7 +86,7 @@ def _poison(ptr, nbytes, device, stream):
                 return
             if len(held) % 8 == 0:
                 held.clear()             # give the block time to come back (its free may still run)
-                time.sleep(50e-6)
+                time.sleep(20e-6)
 
 
 def drain():

@@ -28,11 +28,17 @@ import time
 import numpy as np
 import torch
 
-from . import _abi
+from . import _abi, ops
 from .layout import PACK_THREADS, Layout
 
-# a round's updates, packed, at most this many bytes (and one launch: 64 updates) go the one-call way
-ZERO_COPY_BYTES = 4 << 20
+# a round's updates, packed, at most staging.ZERO_COPY_BYTES (read at each round: one knob for both
+# zero-copy forms, FEDN_AMD_ZERO_COPY_BYTES; 0 turns them off) and 64 of them (one launch) go the
+# one-call way
+
+
+def _zero_copy_bytes():
+    from . import staging
+    return staging.ZERO_COPY_BYTES
 _FOLDABLE = {np.dtype(np.float32): _abi.FA_F32, np.dtype(np.float64): _abi.FA_F64,
              np.dtype(np.float16): _abi.FA_F16}   # dtypes whose fold result is their own dtype (numpy)
 _POOL = 4                     # pinned result blocks kept per session (a block a caller still holds is skipped)
@@ -62,8 +68,9 @@ def eligible(layout, K_hint=2):
     """Whether a round over ``layout`` can take the one-call path: float16/32/64 tensors only (numpy's
     fold keeps their dtype, so the result block has the arena's layout), and at least two updates
     (the first and one more) fit the arena."""
-    return (all(dt in _FOLDABLE for dt in layout.groups) and 2 * layout.nbytes <= ZERO_COPY_BYTES
-            and K_hint * layout.nbytes <= ZERO_COPY_BYTES and bool(_entry_points()))
+    zc = _zero_copy_bytes()
+    return (all(dt in _FOLDABLE for dt in layout.groups) and max(2, K_hint) * layout.nbytes <= zc
+            and bool(_entry_points()))
 
 
 class SmallSession:
@@ -76,7 +83,7 @@ class SmallSession:
         self.layout = layout
         nb = layout.nbytes
         self.stride = nb
-        self.cap = max(2, min(64, ZERO_COPY_BYTES // nb))
+        self.cap = max(2, min(64, _zero_copy_bytes() // nb))
         self.arena = torch.empty(self.cap * nb, dtype=torch.uint8, pin_memory=True)
         self.arena_ptr = self.arena.data_ptr()
         self.window = (self.arena_ptr, self.cap * nb)
@@ -121,12 +128,10 @@ class SmallSession:
 
     def fold(self, block, K, ns, Ns, ticket):
         """Wait for the packs, fold arena slots 0..K-1 into ``block`` (pinned) and wait: one call."""
-        rc = self._fp.fold_host(self.fold_plan, self._fold, self._wait, ticket or 0, self.arena_ptr, self.stride, K,
-                                block.ctypes.data, ns, Ns, self.stream_ptr)
-        if rc == -1:
-            from . import codec
-            raise codec.CodecError(f"fnpz_gather_wait: {codec.load_lib().fnpz_last_error().decode(errors='replace')}")
-        _abi.check(rc)
+        fp, plan, fold, wait, arena, stride, stream = (self._fp, self.fold_plan, self._fold, self._wait,
+                                                       self.arena_ptr, self.stride, self.stream_ptr)
+        ops.fedavg_fold_host(lambda n, N: fp.fold_host(plan, fold, wait, ticket or 0, arena, stride, K,
+                                                       block.ctypes.data, n, N, stream), ns, Ns)
 
     def views(self, block):
         return self._fp.views(self.plan, block)
@@ -243,7 +248,7 @@ class SmallSessions:
         if type(first) is not list or not first:
             return None
         last = self._last
-        if last is not None and last.device == device:
+        if last is not None and last.device == device and last.cap * last.stride <= _zero_copy_bytes():
             r = SmallRound.start(last, first)
             if r is not None:
                 return r
@@ -253,9 +258,11 @@ class SmallSessions:
             return None
         key = (str(device), id(layout))
         s = self._by_key.get(key)
-        if s is None or s.layout is not layout:
-            if not eligible(layout):
-                return None
+        if s is not None and s.layout is not layout:   # a recycled id (Layout.of's cache was cleared)
+            s = None
+        if not eligible(layout):
+            return None
+        if s is None or s.cap * s.stride > _zero_copy_bytes():
             s = SmallSession(device, layout)
             self._by_key[key] = s
             while len(self._by_key) > self.keep:

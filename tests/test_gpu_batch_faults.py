@@ -23,7 +23,7 @@ from oracle import numpy_ref as ref
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
-FOLD_OPS = ("fedavg_fold", "fedavg_fold_ptrs", "fedavg_fold_raw", "fedopt_step", "fedopt_step_raw")
+FOLD_OPS = ("fedavg_fold", "fedavg_fold_ptrs", "fedavg_fold_raw", "fedavg_fold_host", "fedopt_step", "fedopt_step_raw")
 
 
 @pytest.fixture(scope="module", autouse=True)

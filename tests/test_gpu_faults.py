@@ -47,7 +47,7 @@ def _poison_update(monkeypatch, n, N):
     import inspect
 
     from fedn_amd import _abi, ops
-    for name in ("fedavg_fold_ptrs", "fedavg_fold_raw"):
+    for name in ("fedavg_fold_ptrs", "fedavg_fold_raw", "fedavg_fold_host"):
         real = getattr(ops, name)
         sig = inspect.signature(real)
 

@@ -1732,9 +1732,11 @@ def test_small_float_updates_native_admission(kind):
 @pytest.mark.parametrize("K", [2, 5, 15, 16, 40])
 def test_small_round_zero_copy(K, monkeypatch):
     """A small FedAvg round whose updates never left the pinned arena folds straight from it into the
-    pinned result block (staging.ZERO_COPY_BYTES: no H2D / D2H). Bit-exact to the oracle and to the
-    copy path (forced with ZERO_COPY_BYTES = 0), three rounds of one session; the zero-copy rounds
-    enqueue no H2D (time_h2d == 0), larger rounds (partial uploads from 16 updates on) copy as before."""
+    pinned result block (staging.ZERO_COPY_BYTES: no H2D / D2H) — since round 6 through the one-call
+    round (smallround.py) while the round fits its arena (19 mnist updates in 4 MiB), through the
+    general pipeline's arena beyond. Bit-exact to the oracle and to the copy path (forced with
+    ZERO_COPY_BYTES = 0), three rounds of one session; the zero-copy rounds enqueue no H2D
+    (time_h2d == 0), larger rounds (partial uploads from 16 updates on) copy as before."""
     from fedn_amd import staging
     rng = np.random.default_rng(40 + K)
     shapes = [(64, 784), (64,), (32, 64), (32,), (10, 32), (10,)]
@@ -1751,7 +1753,7 @@ def test_small_round_zero_copy(K, monkeypatch):
             model, data = agg.combine_models(helper=None, delete_models=True)
             assert data["nr_aggregated_models"] == nr == K
             assert_lists_identical(model, want, f"K={K} zero_copy={zc} round {r}")
-            zero = zc and K < staging.ARENA_UPLOAD_EVERY
+            zero = zc and K <= staging.ZERO_COPY_BYTES // 210_688     # the one-call round's arena
             assert (data["time_h2d"] == 0) == zero, data
 
 

@@ -22,6 +22,7 @@ def _knob():
     _abi.load()
     was = reuse.enabled()
     reuse.set_enabled(True)
+    reuse.drain()                      # earlier tests' frees (a knob-on suite run) handled first
     yield reuse
     reuse.drain()
     reuse.set_enabled(was)

@@ -75,8 +75,8 @@ def test_small_round_is_the_oracle(K, dtype, monkeypatch):
     updates = _models(rng, MNIST, K, dtype)
     uh, agg = _agg()
     seen = _spy(agg, monkeypatch)
-    from fedn_amd import smallround
-    cap = smallround.ZERO_COPY_BYTES // sum(int(np.prod(s)) * np.dtype(dtype).itemsize for s in MNIST)
+    from fedn_amd import staging
+    cap = staging.ZERO_COPY_BYTES // sum(int(np.prod(s)) * np.dtype(dtype).itemsize for s in MNIST)
     for _ in range(3):                       # a session: the arena, plans and blocks are reused
         model, data = _round(uh, agg, updates)
         want, nr = ref.fedavg_combine(updates)
@@ -136,8 +136,8 @@ def test_other_dtype_or_shape_goes_general_in_fifo_order(monkeypatch):
 
 
 def test_more_updates_than_the_arena_goes_general(monkeypatch):
-    from fedn_amd import smallround
-    monkeypatch.setattr(smallround, "ZERO_COPY_BYTES", 3 * 212_992)   # a 3-update arena for mnist
+    from fedn_amd import staging
+    monkeypatch.setattr(staging, "ZERO_COPY_BYTES", 3 * 210_688)      # a 3-update arena for mnist
     rng = np.random.default_rng(6)
     ups = _models(rng, MNIST, 7)
     uh, agg = _agg()
