@@ -58,7 +58,9 @@
 #include <cstdint>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "fnpz_guard.h"
@@ -79,6 +81,29 @@ constexpr int64_t kMinChunk = 1 << 18;                     // smallest chunk a m
 constexpr int64_t kTailStop = 1024;                        // speculative parses stop this far before the end
 constexpr int64_t kTailRec = 192 << 10;                    // recorded tops before the end (last chunk)
 constexpr int kCkEvery = 256;                              // symbol checkpoints
+
+// byte buffers whose resize leaves new bytes uninitialised: a deflate stream's output is written
+// in full by the parallel encode (and a zlib stream's by zlib), so zero-filling it first — a serial
+// pass that also takes every page fault on one thread — is wasted (round 6, profiles/r06_save_phases.log)
+template <class T>
+struct NoInit : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInit<U>;
+    };
+    NoInit() = default;
+    template <class U>
+    NoInit(const NoInit<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+using Bytes = std::vector<uint8_t, NoInit<uint8_t>>;
 
 inline uint32_t hash3(const uint8_t* p) { return (((uint32_t)p[0] << 10) ^ ((uint32_t)p[1] << 5) ^ p[2]) & kHMask; }
 
@@ -1138,6 +1163,17 @@ inline void parallel(int n, int threads, F&& f) {   // a worker's exception is r
     fnpz_internal::run_parallel(n, threads, std::forward<F>(f));
 }
 
+// Release big buffers off the caller's critical path: returning 1-2 GB to the OS (munmap, serial under
+// the process's mmap lock) took ~0.1 s at the end of a 100 M-param save (profiles/r06_save_phases.log).
+// The object is moved into a detached thread that drops it; if no thread can be had, it is dropped here.
+template <class T>
+inline void free_later(T&& obj) {
+    try {
+        std::thread([o = std::move(obj)]() mutable { T().swap(o); }).detach();
+    } catch (const std::exception&) {
+    }
+}
+
 struct Stats {
     int chunks = 0, fixups = 0, blocks = 0;
     double t_parse = 0, t_sync = 0, t_sched = 0, t_plan = 0, t_encode = 0;
@@ -1149,7 +1185,7 @@ struct Stats {
 // S[0, L) fed as deflate(Z_NO_FLUSH) calls ending at `ends` and then deflate(Z_FINISH). False (with
 // st->fallback set) if this input needs zlib itself.
 inline bool deflate_exact(const uint8_t* S, int64_t L, const std::vector<int64_t>& ends, int threads, int64_t chunk,
-                          std::vector<uint8_t>& out, Stats* st) {
+                          Bytes& out, Stats* st) {
     Stats dummy;
     if (!st) st = &dummy;
     if (chunk < kMinChunk) chunk = kMinChunk;
@@ -1343,7 +1379,7 @@ inline bool deflate_exact(const uint8_t* S, int64_t L, const std::vector<int64_t
     }
     const int64_t total_bits = off;
     std::atomic<int> bad{0};
-    out.assign((size_t)((total_bits + 7) / 8), 0);
+    out.resize((size_t)((total_bits + 7) / 8));   // every byte is written below (no zero fill)
     parallel((int)B.size(), threads, [&](int i) {
         Block& b = B[i];
         const int64_t got = E.encode(b, plans[i]);
@@ -1363,6 +1399,11 @@ inline bool deflate_exact(const uint8_t* S, int64_t L, const std::vector<int64_t
         std::vector<uint8_t>().swap(b.bytes);
     }
     st->t_encode = now() - t0;
+    for (auto& x : C) {                 // the parsers (small), then the symbol streams off the critical path
+        delete x.P;
+        x.P = nullptr;
+    }
+    free_later(std::move(C));
     return true;
 }
 

@@ -17,6 +17,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <atomic>
 #include <chrono>
 #include <cstdint>
@@ -96,7 +97,7 @@ struct Member {
     const uint8_t* data;
     int64_t nbytes;
     int64_t seg;                // numpy's write size (bytes); <= 0: one write
-    std::vector<uint8_t> out;   // the raw deflate stream
+    pdef::Bytes out;            // the raw deflate stream
     uint32_t crc = 0;
     int rc = Z_OK;
 };
@@ -134,6 +135,7 @@ bool deflate_member_parallel_unchecked(Member& m, int threads) try {
     for (int i = 1; i < np; ++i) crc = crc32_combine(crc, crcs[i], (z_off_t)std::min(piece, L - (int64_t)i * piece));
     m.crc = (uint32_t)crc;
     m.rc = Z_OK;
+    pdef::free_later(std::move(buf));   // the member's copy is returned to the OS off the critical path
     const double t_end = now_s();
     std::lock_guard<std::mutex> lk(g_st_mu);
     g_st[kStCopy] = t_copied - t_start;
@@ -145,12 +147,12 @@ bool deflate_member_parallel_unchecked(Member& m, int threads) try {
     g_st[kStCrc] = t_end - t_deflated;
     return true;
 } catch (const std::bad_alloc&) {
-    std::vector<uint8_t>().swap(m.out);
+    pdef::Bytes().swap(m.out);
     g_par_fallback.fetch_add(1);
     g_par_reason = "out of memory";
     return false;
 } catch (const std::system_error&) {   // a worker thread could not be started
-    std::vector<uint8_t>().swap(m.out);
+    pdef::Bytes().swap(m.out);
     g_par_fallback.fetch_add(1);
     g_par_reason = "no thread";
     return false;
@@ -239,7 +241,7 @@ std::string zlib_check_locked() {
     std::vector<uint8_t> S((size_t)L);
     std::memcpy(S.data(), hdr.data(), hdr.size());
     std::memcpy(S.data() + hdr.size(), data.data(), (size_t)n);
-    std::vector<uint8_t> out;
+    pdef::Bytes out;
     pdef::Stats st;
     if (!pdef::deflate_exact(S.data(), L, input_ends(z.hlen, n, z.seg), 4, pdef::kMinChunk, out, &st))
         return std::string("self-test: pdeflate.h fell back (") + (st.fallback ? st.fallback : "?") + ")";
@@ -266,9 +268,31 @@ bool zlib_modelled() {
     return g_zl_state.load() == 1;
 }
 
+// MemAvailable from /proc/meminfo (bytes), or -1 if it cannot be read
+int64_t mem_available() {
+    FILE* f = std::fopen("/proc/meminfo", "r");
+    if (!f) return -1;
+    char line[256];
+    long long kb = -1;
+    while (std::fgets(line, sizeof(line), f))
+        if (std::sscanf(line, "MemAvailable: %lld kB", &kb) == 1) break;
+    std::fclose(f);
+    return kb < 0 ? -1 : (int64_t)kb * 1024;
+}
+
 bool deflate_member_parallel(Member& m, int threads) {
     if (!zlib_modelled()) {
         g_par_reason = "libz not modelled";
+        return false;
+    }
+    // the parallel path holds a copy of the member and its symbol streams (2 bytes per input byte on
+    // weights) besides the output both paths hold — ~4x the member at its peak, 5.3x with the caller's
+    // archive buffer (tools/big_save_check.py): where that would not fit in the host's available
+    // memory, the streaming zlib path writes the same bytes (the reference streams too)
+    const int64_t avail = mem_available();
+    if (avail >= 0 && 5 * (m.hlen + m.nbytes) > avail) {
+        g_par_fallback.fetch_add(1);
+        g_par_reason = "memory";
         return false;
     }
     return deflate_member_parallel_unchecked(m, threads);
@@ -364,7 +388,7 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
                 const int64_t b = pieces[k].second;
                 std::memcpy(dst[i] + b, ms[i].out.data() + b, (size_t)std::min<int64_t>(piece, ms[i].out.size() - b));
             });
-            for (Member& m : ms) std::vector<uint8_t>().swap(m.out);
+            for (Member& m : ms) pdef::Bytes().swap(m.out);
         }
         const uint64_t cd_off = (uint64_t)(p - out);
         for (int i = 0; i < n; ++i) {   // ZipFile._write_end_record
@@ -492,7 +516,7 @@ extern "C" int fnpz_deflate_exact(const uint8_t* in, int64_t len, const int64_t*
         if (!in || len <= 0 || !ends || nends <= 0 || !out || !out_len || ends[nends - 1] != len)
             return set_error(FNPZ_EINVAL, "fnpz_deflate_exact: bad arguments");
         std::vector<int64_t> e(ends, ends + nends);
-        std::vector<uint8_t> res;
+        pdef::Bytes res;
         pdef::Stats st;
         if (!pdef::deflate_exact(in, len, e, std::max(1, threads), chunk, res, &st))
             return set_error(FNPZ_EFALLBACK, "fnpz_deflate_exact: %s", st.fallback ? st.fallback : "fallback");
