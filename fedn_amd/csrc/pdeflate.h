@@ -1178,14 +1178,17 @@ struct Stats {
     int chunks = 0, fixups = 0, blocks = 0;
     double t_parse = 0, t_sync = 0, t_sched = 0, t_plan = 0, t_encode = 0;
     int64_t tail_from = 0;
+    int64_t out_len = 0;               // bytes of the stream (in out, or at dst)
     const char* fallback = nullptr;   // why the caller must run zlib itself
 };
 
 // The raw deflate stream zlib 1.2.11 (level 6, memLevel 8, default strategy, wbits -15) produces for
 // S[0, L) fed as deflate(Z_NO_FLUSH) calls ending at `ends` and then deflate(Z_FINISH). False (with
-// st->fallback set) if this input needs zlib itself.
+// st->fallback set) if this input needs zlib itself. The stream goes to `out`, or — with dst — straight
+// to dst[0, st->out_len) (false, "no room", if it needs more than dst_cap bytes): the archive writer
+// encodes a big member in place, with no copy of the stream afterwards.
 inline bool deflate_exact(const uint8_t* S, int64_t L, const std::vector<int64_t>& ends, int threads, int64_t chunk,
-                          Bytes& out, Stats* st) {
+                          Bytes& out, Stats* st, uint8_t* dst = nullptr, int64_t dst_cap = 0) {
     Stats dummy;
     if (!st) st = &dummy;
     if (chunk < kMinChunk) chunk = kMinChunk;
@@ -1379,14 +1382,21 @@ inline bool deflate_exact(const uint8_t* S, int64_t L, const std::vector<int64_t
     }
     const int64_t total_bits = off;
     std::atomic<int> bad{0};
-    out.resize((size_t)((total_bits + 7) / 8));   // every byte is written below (no zero fill)
+    const int64_t nbytes = (total_bits + 7) / 8;
+    if (dst && nbytes > dst_cap) {
+        st->fallback = "no room";
+        return false;
+    }
+    if (!dst) out.resize((size_t)nbytes);       // every byte is written below (no zero fill)
+    uint8_t* const O = dst ? dst : out.data();
+    st->out_len = nbytes;
     parallel((int)B.size(), threads, [&](int i) {
         Block& b = B[i];
         const int64_t got = E.encode(b, plans[i]);
         if (got != b.bits) bad.fetch_add(1);
         // bytes after the first go straight out; the shared first byte is merged below
         const int64_t first = b.off >> 3, lastb = (b.off + b.bits - 1) >> 3;
-        if (lastb > first) std::memcpy(out.data() + first + 1, b.bytes.data() + 1, (size_t)(lastb - first));
+        if (lastb > first) std::memcpy(O + first + 1, b.bytes.data() + 1, (size_t)(lastb - first));
     });
     if (bad.load()) {
         st->fallback = "internal size mismatch";
@@ -1394,8 +1404,8 @@ inline bool deflate_exact(const uint8_t* S, int64_t L, const std::vector<int64_t
     }
     for (auto& b : B) {
         const int64_t first = b.off >> 3;
-        if ((b.off & 7) == 0) out[(size_t)first] = b.bytes[0];
-        else out[(size_t)first] |= b.bytes[0];
+        if ((b.off & 7) == 0) O[first] = b.bytes[0];
+        else O[first] |= b.bytes[0];
         std::vector<uint8_t>().swap(b.bytes);
     }
     st->t_encode = now() - t0;

@@ -97,15 +97,17 @@ struct Member {
     const uint8_t* data;
     int64_t nbytes;
     int64_t seg;                // numpy's write size (bytes); <= 0: one write
-    pdef::Bytes out;            // the raw deflate stream
+    pdef::Bytes out;            // the raw deflate stream (empty when it was encoded in place)
     uint32_t crc = 0;
     int rc = Z_OK;
+    int64_t comp = -1;          // the stream's length once encoded in place (>= 0), else out.size()
+    int64_t stream_len() const { return comp >= 0 ? comp : (int64_t)out.size(); }
 };
 
 // the same stream from pdeflate.h on `threads` threads; false: the caller runs zlib (also when the
 // extra memory this path holds — a copy of the member and its symbol streams — cannot be had: the
 // streaming zlib path needs only its output)
-bool deflate_member_parallel_unchecked(Member& m, int threads) try {
+bool deflate_member_parallel_unchecked(Member& m, int threads, uint8_t* dst, int64_t dst_cap) try {
     const double t_start = now_s();
     const int64_t L = m.hlen + m.nbytes;
     std::unique_ptr<uint8_t[]> buf(new uint8_t[(size_t)L]);   // no zero fill: every byte is copied in
@@ -119,10 +121,11 @@ bool deflate_member_parallel_unchecked(Member& m, int threads) try {
     const double t_copied = now_s();
     pdef::Stats st;
     const bool ok = pdef::deflate_exact(S, L, input_ends(m.hlen, m.nbytes, m.seg), threads, g_par_chunk.load(),
-                                        m.out, &st);
+                                        m.out, &st, dst, dst_cap);
     (ok ? g_par_ok : g_par_fallback).fetch_add(1);
     g_par_reason = st.fallback;
     if (!ok) return false;
+    if (dst) m.comp = st.out_len;
     const double t_deflated = now_s();
     // CRC-32 by pieces, combined
     const int np = (int)((L + piece - 1) / piece);
@@ -280,7 +283,7 @@ int64_t mem_available() {
     return kb < 0 ? -1 : (int64_t)kb * 1024;
 }
 
-bool deflate_member_parallel(Member& m, int threads) {
+bool deflate_member_parallel(Member& m, int threads, uint8_t* dst, int64_t dst_cap) {
     if (!zlib_modelled()) {
         g_par_reason = "libz not modelled";
         return false;
@@ -295,7 +298,7 @@ bool deflate_member_parallel(Member& m, int threads) {
         g_par_reason = "memory";
         return false;
     }
-    return deflate_member_parallel_unchecked(m, threads);
+    return deflate_member_parallel_unchecked(m, threads, dst, dst_cap);
 }
 
 }  // namespace
@@ -315,27 +318,31 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
             ms[i] = Member{names[i], headers[i], header_lens[i], static_cast<const uint8_t*>(datas[i]), nbytes[i],
                            seg_bytes ? seg_bytes[i] : 0};
         }
-        // big members one after another on every thread (pdeflate.h); the rest member-parallel, largest
-        // first so one long stream does not start last. Big: at least min_member bytes, or at least four
-        // chunks and more than an even share of the archive per thread (member-parallel, that member
-        // alone would outlast the rest of the archive spread over the other threads)
+        // big members take pdeflate.h's stream on every thread; the rest are deflated member-parallel
+        // FIRST (largest first, so one long stream does not start last), so that when the archive is laid
+        // out in order every big member's place is known and its stream is encoded straight into it (no
+        // copy of the stream afterwards). Big: at least min_member bytes, or at least four chunks and more
+        // than an even share of the archive per thread (member-parallel, that member alone would outlast
+        // the rest of the archive spread over the other threads)
         int64_t total = 0;
         for (const Member& m : ms) total += m.hlen + m.nbytes;
         const int64_t floor = 4 * g_par_chunk.load();
         std::vector<int> order;
+        std::vector<char> is_big((size_t)n, 0);
         for (int i = 0; i < n; ++i) {
             const int64_t sz = ms[i].hlen + ms[i].nbytes;
-            if (threads > 1 && (sz >= g_par_min.load() || (sz >= floor && sz * threads > total))) {
-                if (!deflate_member_parallel(ms[i], threads)) deflate_member(ms[i]);
-            } else {
-                order.push_back(i);
-            }
+            if (threads > 1 && (sz >= g_par_min.load() || (sz >= floor && sz * threads > total))) is_big[i] = 1;
+            else order.push_back(i);
         }
         std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return ms[a].nbytes > ms[b].nbytes; });
         fnpz_internal::run_parallel((int)order.size(), std::max(1, threads), [&](int k) { deflate_member(ms[order[k]]); });
-        for (int i = 0; i < n; ++i)
+        auto check = [&](int i) -> int {
             if (ms[i].rc == Z_MEM_ERROR) return set_error(FNPZ_ENOMEM, "fnpz_savez: zlib out of memory on member %d", i);
-            else if (ms[i].rc != Z_OK) return set_error(FNPZ_ECORRUPT, "fnpz_savez: deflate failed on member %d", i);
+            if (ms[i].rc != Z_OK) return set_error(FNPZ_ECORRUPT, "fnpz_savez: deflate failed on member %d", i);
+            return FNPZ_OK;
+        };
+        for (int i : order)
+            if (const int rc = check(i)) return rc;
 
         uint8_t* p = out;
         uint8_t* const lim = out + out_cap;
@@ -344,11 +351,19 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
         std::vector<uint64_t> comps((size_t)n);
         std::vector<uint16_t> ver((size_t)n);
         std::vector<uint8_t*> dst((size_t)n);
-        const double t_asm = now_s();
+        double t_asm = now_s(), t_big = 0;
         for (int i = 0; i < n; ++i) {
-            const Member& m = ms[i];
+            Member& m = ms[i];
             const size_t nl = std::strlen(m.name) + 4;
-            const uint64_t raw = (uint64_t)(m.hlen + m.nbytes), comp = m.out.size();
+            if ((int64_t)(30 + nl + 20) > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
+            if (is_big[i]) {                    // encoded in place behind its local header, else zlib's stream
+                const double t0 = now_s();
+                uint8_t* at = p + 30 + nl + 20;
+                if (!deflate_member_parallel(m, threads, at, lim - at)) deflate_member(m);
+                if (const int rc = check(i)) return rc;
+                t_big += now_s() - t0;
+            }
+            const uint64_t raw = (uint64_t)(m.hlen + m.nbytes), comp = (uint64_t)m.stream_len();
             if ((int64_t)(30 + nl + 20 + comp) > lim - p) return set_error(FNPZ_ENOSPC, "fnpz_savez: output buffer too small");
             // ZipInfo.FileHeader(zip64=True) as _ZipWriteFile.close rewrites it
             const bool big = raw > zip64_limit || comp > zip64_limit;
@@ -381,7 +396,7 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
         {
             const int64_t piece = 8 << 20;
             std::vector<std::pair<int, int64_t>> pieces;
-            for (int i = 0; i < n; ++i)
+            for (int i = 0; i < n; ++i)   // (a stream encoded in place has no bytes here)
                 for (int64_t b = 0; b < (int64_t)ms[i].out.size(); b += piece) pieces.emplace_back(i, b);
             fnpz_internal::run_parallel((int)pieces.size(), std::max(1, threads), [&](int k) {
                 const int i = pieces[k].first;
@@ -464,7 +479,7 @@ extern "C" int fnpz_savez(int n, const char* const* names, const uint8_t* const*
         *out_len = (int64_t)(p - out);
         {
             std::lock_guard<std::mutex> lk(g_st_mu);
-            g_st[kStAssemble] = now_s() - t_asm;
+            g_st[kStAssemble] = now_s() - t_asm - t_big;   // the big members' deflates are their own phases
             g_st[kStTotal] = now_s() - t_call;
         }
         return FNPZ_OK;
