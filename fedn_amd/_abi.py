@@ -47,6 +47,14 @@ EXPORTS = {
         ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,       # updates (pinned host), upd_dtype
         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int,  # n, N, K
         ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),     # P, init, stream
+    "fa_fedopt_step_host": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_int,                       # old (pinned host), old_dtype
+        ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,       # updates (pinned host), upd_dtype
+        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int,  # n, N, K
+        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,  # m_in, m_in_dtype, m_out, m_out_dtype
+        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,  # v_in, v_in_dt, v_out, out, state_dt
+        ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,  # opt, lr, b1, b2, tau
+        ctypes.c_int64, ctypes.c_void_p]),                   # P, stream
     "fa_fedopt_step": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int,                       # old, old_dtype
         ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,       # updates, upd_dtype

@@ -23,6 +23,7 @@ from ..exceptions import InvalidParameterError
 from ..parameters import Parameters
 from ..ingest import ShardedStagedModel
 from ..layout import spread
+from ..smallround import SmallFedOptSessions
 from ..staging import FedOptPipeline, FedOptState, StagingCache, helper_kind
 from .aggregatorbase import AggregatorBase, queued_updates
 from .fedavg import _packed_bytes, default_device, env_devices
@@ -54,6 +55,7 @@ class Aggregator(AggregatorBase):
         self.state = None
         self.sharded = None
         self._staging = StagingCache()   # pinned slots, arenas, streams and ring reused by the next round
+        self._small = SmallFedOptSessions()   # configs[0]-sized rounds in one native call (smallround.py)
 
     def _pipeline(self, model_old, model_next):
         if self.sharded is None:
@@ -70,6 +72,18 @@ class Aggregator(AggregatorBase):
             return ShardedFedOptPipeline(self.devices, model_old, model_next)
         dev = self.device or (self.devices[0] if self.devices else None) or default_device()
         return FedOptPipeline(dev, model_old, model_next, cache=self._staging)
+
+    def _small_round(self, model_old, model_next):
+        """The one-call round (smallround.SmallFedOptRound) for a small single-dtype model on one
+        device; None: the general pipeline."""
+        if self.devices or self.sharded:
+            return None
+        dev = self.device or default_device()
+        r = self._small.round(model_old, model_next, dev, self._pipeline)
+        if r is not None and self.sharded is None:
+            self.sharded = False                 # what _pipeline decides for a one-device session
+            self.state = FedOptState(self.fp32_state)
+        return r
 
     # reference attribute names (fedopt.py:37-38): host copies of the HBM-resident state
     @property
@@ -97,6 +111,7 @@ class Aggregator(AggregatorBase):
             return None, data
 
         pipe = None
+        small = False           # pipe is a SmallFedOptRound: nothing launched or deleted before its step
         nr_aggregated_models, total_examples = 0, 0
         waiting = deque()       # admitted updates not deleted yet: a batched fold may still skip them
         with contextlib.closing(queued_updates(self.update_handler, helper, size_box=self._ahead_size)) as updates:
@@ -115,21 +130,31 @@ class Aggregator(AggregatorBase):
                         raise AttributeError(f"'{type(helper).__name__}' object has no attribute 'subtract'")
                     if nr_aggregated_models == 0:
                         model_old = self.update_handler.load_model(helper, model_update.model_id)
-                        pipe = self._pipeline(model_old, model_next)
+                        pipe = self._small_round(model_old, model_next)
+                        small = pipe is not None
+                        if not small:
+                            pipe = self._pipeline(model_old, model_next)
                         self._live = pipe
-                    pipe.add(model_next, metadata["num_examples"], total_examples, tag=model_update)
+                    if not (small and pipe.add(model_next, metadata["num_examples"], total_examples, model_update)):
+                        if small:       # not this layout, or the arena is full: the general path from here
+                            pipe, small = pipe.general(), False
+                            self._live = pipe
+                        pipe.add(model_next, metadata["num_examples"], total_examples, tag=model_update)
                     data["time_model_aggregation"] += time.time() - tic
 
                     nr_aggregated_models += 1
                     waiting.append(model_update)
                     # a batch whose launch failed was folded one update at a time: skipped ones are
                     # logged and uncounted (fedopt.py:103-106), folded ones deleted
-                    nr_aggregated_models -= self._settle(pipe, waiting, delete_models)
+                    if not small:
+                        nr_aggregated_models -= self._settle(pipe, waiting, delete_models)
                 except Exception as e:  # noqa: BLE001 — fedopt.py:103-106
                     logger.error(f"Error processing model update: {e}. Skipping this update.")
                     logger.error(traceback.format_exc())
                     if nr_aggregated_models == 0:
-                        pipe = None
+                        if pipe is not None and hasattr(pipe, "quiesce"):
+                            pipe.quiesce()          # its pack of the global model reads model_old
+                        pipe, small = None, False
                     continue
 
         data["nr_aggregated_models"] = nr_aggregated_models
@@ -137,6 +162,8 @@ class Aggregator(AggregatorBase):
             return None, data
         try:
             tic = time.time()
+            # (a one-call round whose launch fails hands its step to the general pipeline, which it then
+            # reports through: skipped updates, timings)
             model = pipe.server_step(self.state, parameters)
             data["time_model_aggregation"] += time.time() - tic
             data.update(pipe.timings())

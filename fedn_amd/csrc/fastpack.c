@@ -254,6 +254,50 @@ static PyObject* fp_fold_host(PyObject* self, PyObject* args) {
     return PyLong_FromLong(rc);
 }
 
+/*   fedopt_host(fn, wait, ticket, old, arena, stride, K, upd_dtype, old_dtype, P, out, n, N, stream,
+ *               (m_in, m_in_dtype, m_out, m_out_dtype, v_in, v_in_dtype, v_out, state_dtype),
+ *               serveropt, lr, beta1, beta2, tau) -> status
+ * A small model's FedOpt round (one dtype group): the global model packed into the pinned block at
+ * ``old`` and the K updates at arena slots 0..K-1; waits for the packs (``ticket``: the last), then fa_fedopt_step_host (include/fedagg.h: FIRST |
+ * FINAL, the new model into pinned ``out``, m / v device buffers) — the GIL released throughout.
+ * -1 if the pack failed (fnpz_last_error says why). */
+typedef int (*fedopt_host_fn)(const void* old, int old_dtype, const void* const* updates, int upd_dtype,
+                              const double* n, const double* N, int K, const void* m_in, int m_in_dtype, void* m_out,
+                              int m_out_dtype, const void* v_in, int v_in_dtype, void* v_out, void* out,
+                              int state_dtype, int serveropt, double lr, double beta1, double beta2, double tau,
+                              int64_t P, void* stream);
+
+static PyObject* fp_fedopt_host(PyObject* self, PyObject* args) {
+    PyObject *ns, *Ns;
+    unsigned long long fn, wait, old, arena, out, stream, m_in, m_out, v_in, v_out;
+    long long ticket, stride, P;
+    int K, upd_dt, old_dt, m_in_dt, m_out_dt, v_in_dt, state_dt, opt;
+    double lr, b1, b2, tau;
+    if (!PyArg_ParseTuple(args, "KKLKKLiiiLKOOK(KiKiKiKi)idddd", &fn, &wait, &ticket, &old, &arena, &stride, &K, &upd_dt,
+                          &old_dt, &P, &out, &ns, &Ns, &stream, &m_in, &m_in_dt, &m_out, &m_out_dt, &v_in, &v_in_dt,
+                          &v_out, &state_dt, &opt, &lr, &b1, &b2, &tau))
+        return NULL;
+    if (K < 1 || K > MAX_FOLD_K || stride < 0 || P < 0 || !old || !arena || !out || !fn) {
+        PyErr_SetString(PyExc_ValueError, "fedopt_host: bad arguments");
+        return NULL;
+    }
+    double n[MAX_FOLD_K], N[MAX_FOLD_K];
+    if (read_doubles(ns, n, K) || read_doubles(Ns, N, K)) return NULL;
+    const void* ups[MAX_FOLD_K];
+    for (int k = 0; k < K; ++k) ups[k] = (const void*)(uintptr_t)(arena + (unsigned long long)k * stride);
+    int rc = 0;
+    Py_BEGIN_ALLOW_THREADS
+    if (ticket > 0 && wait) rc = ((gather_wait_fn)(uintptr_t)wait)((int64_t)ticket) ? -1 : 0;
+    if (rc == 0)
+        rc = ((fedopt_host_fn)(uintptr_t)fn)((const void*)(uintptr_t)old, old_dt, ups, upd_dt, n, N, K,
+                                             (const void*)(uintptr_t)m_in, m_in_dt, (void*)(uintptr_t)m_out, m_out_dt,
+                                             (const void*)(uintptr_t)v_in, v_in_dt, (void*)(uintptr_t)v_out,
+                                             (void*)(uintptr_t)out, state_dt, opt, lr, b1, b2, tau, (int64_t)P,
+                                             (void*)(uintptr_t)stream);
+    Py_END_ALLOW_THREADS
+    return PyLong_FromLong(rc);
+}
+
 /*   views(plan, base) -> list    the model's arrays as views of ``base`` (a C-contiguous numpy array whose
  * bytes hold the packed layout ``plan`` describes: the admission plan), each keeping ``base`` alive */
 static PyObject* fp_views(PyObject* self, PyObject* args) {
@@ -300,6 +344,9 @@ static PyMethodDef methods[] = {
     {"fold_host", fp_fold_host, METH_VARARGS,
      "fold_host(fold_plan, fold_addr, wait_addr, ticket, arena_addr, stride, K, out_addr, n, N, stream) -> status"},
     {"views", fp_views, METH_VARARGS, "views(plan, base) -> list of arrays viewing base"},
+    {"fedopt_host", fp_fedopt_host, METH_VARARGS,
+     "fedopt_host(fn, wait, ticket, old, arena, stride, K, upd_dtype, old_dtype, P, out, n, N, stream, state, serveropt, "
+     "lr, beta1, beta2, tau) -> status"},
     {"plan", fp_plan, METH_VARARGS, "plan([(shape, dtype, dst_offset), ...]) -> capsule"},
     {"admit", fp_admit, METH_VARARGS,
      "admit(plan, arrays, dst_addr, gather_start_addr, threads, buf_addr, buf_len) -> ticket | 0 | -1 (not this "

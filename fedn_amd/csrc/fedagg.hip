@@ -2711,6 +2711,44 @@ int fa_fedopt_step_ex(const void* old, int old_dtype, const void* const* updates
     return fail(FA_EDTYPE, "fa_fedopt_step: unsupported dtype pair (update %d, old %d)", upd_dtype, old_dtype);
 }
 
+// A small model's whole FedOpt round in one call (the FedOpt form of fa_fedavg_fold_host): the global
+// model, the packed updates and the new model in page-locked host memory, read and written through
+// their device mappings; m / v in HBM. One FIRST | FINAL launch (the pseudo-gradient in registers,
+// then the server step), then the stream wait.
+int fa_fedopt_step_host(const void* old, int old_dtype, const void* const* updates, int upd_dtype, const double* n,
+                        const double* N, int K, const void* m_in, int m_in_dtype, void* m_out, int m_out_dtype,
+                        const void* v_in, int v_in_dtype, void* v_out, void* out, int state_dtype, int serveropt,
+                        double lr, double beta1, double beta2, double tau, int64_t P, void* stream) {
+    g_err[0] = 0;
+    if (P < 0 || K < 1 || K > kMaxK)
+        return fail(FA_EINVAL, "fa_fedopt_step_host: 1 <= K <= %d updates in one launch (K=%d, P=%lld)", kMaxK, K,
+                    (long long)P);
+    if (P == 0) return FA_OK;
+    if (!old || !updates || !out) return fail(FA_EINVAL, "fa_fedopt_step_host: null pointer argument");
+    void* dev_old = nullptr;
+    void* dev_out = nullptr;
+    const void* dev_upd[kMaxK];
+    hipError_t e = hipHostGetDevicePointer(&dev_old, const_cast<void*>(old), 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&dev_out, out, 0);
+    for (int k = 0; e == hipSuccess && k < K; ++k) {
+        void* d = nullptr;
+        if (!updates[k]) return fail(FA_EINVAL, "fa_fedopt_step_host: updates[%d] is NULL", k);
+        e = hipHostGetDevicePointer(&d, const_cast<void*>(updates[k]), 0);
+        dev_upd[k] = d;
+    }
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(FA_EINVAL, "fa_fedopt_step_host: %s (not page-locked host memory?)", hipGetErrorString(e));
+    }
+    const int rc = fa_fedopt_step_ex(dev_old, old_dtype, dev_upd, upd_dtype, n, N, K, nullptr, FA_PG_FIRST | FA_PG_FINAL,
+                                     m_in, m_in_dtype, m_out, m_out_dtype, v_in, v_in_dtype, v_out, dev_out, state_dtype,
+                                     serveropt, lr, beta1, beta2, tau, P, stream);
+    if (rc != FA_OK) return rc;
+    e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(FA_EHIP, "fa_fedopt_step_host: hipStreamSynchronize: %s", hipGetErrorString(e));
+    return FA_OK;
+}
+
 int fa_elementwise(int op, void* out, int out_dtype, const void* x, int x_dtype, const void* y, int y_dtype,
                    double a, double b, int64_t P, void* stream) {
     g_err[0] = 0;

@@ -641,6 +641,22 @@ def fedavg_fold_host(call, n, N):
     _abi.check(rc)
 
 
+def fedopt_step_host(call, n, N, *, first=True, final=True):
+    """A small FedOpt round's whole step (smallround.SmallFedOptRound): ``call(n, N)`` runs the native
+    pack wait + ``fa_fedopt_step_host`` (FIRST | FINAL) + stream wait with the client table's ``n`` /
+    ``N``; FedAggError on a failed one (the state untouched: the step writes the buffers the state
+    does not hold), CodecError if a pack failed."""
+    if len(n) != len(N):
+        raise ValueError("n and N must have one entry per update")
+    if not (first and final):
+        raise ValueError("fedopt_step_host: the one-call round is a FIRST | FINAL step")
+    rc = call(n, N)
+    if rc == -1:
+        from . import codec
+        raise codec.CodecError(f"fnpz_gather_wait: {codec.load_lib().fnpz_last_error().decode(errors='replace')}")
+    _abi.check(rc)
+
+
 def host_register(t):
     """Page-lock the memory of host tensor ``t`` (mapped by the caller, e.g. shared memory)."""
     _abi.check(_abi.load().fa_host_register(t.data_ptr(), t.numel() * t.element_size()))

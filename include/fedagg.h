@@ -119,6 +119,19 @@ int fa_fedavg_fold_host(void* agg, int agg_dtype, const void* const* updates, in
                         const double* n, const double* N, int K, int64_t P, int init, void* stream);
 
 /*
+ * fa_fedopt_step_host (ABI 8): the FedOpt round of a small model in one call — fa_fedopt_step_ex with
+ * flags FA_PG_FIRST | FA_PG_FINAL and no pg workspace, where `old`, every updates[k] and `out` are
+ * PAGE-LOCKED HOST addresses (the global model and the updates packed into a pinned arena, a pinned
+ * result block), mapped inside; m_in / m_out / v_in / v_out are device buffers as in
+ * fa_fedopt_step_ex (the session's state stays in HBM). Returns once `stream` has drained. 1 <= K <= 64.
+ */
+int fa_fedopt_step_host(const void* old, int old_dtype, const void* const* updates, int upd_dtype,
+                        const double* n, const double* N, int K,
+                        const void* m_in, int m_in_dtype, void* m_out, int m_out_dtype,
+                        const void* v_in, int v_in_dtype, void* v_out, void* out, int state_dtype,
+                        int serveropt, double lr, double beta1, double beta2, double tau, int64_t P, void* stream);
+
+/*
  * FedOpt (fedopt.py:74-118, 151-258), fused: pseudo-gradient running mean over the
  * K updates followed (FA_PG_FINAL) by one Adam / Yogi / AdaGrad server step.
  *

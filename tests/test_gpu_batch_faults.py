@@ -23,7 +23,8 @@ from oracle import numpy_ref as ref
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
-FOLD_OPS = ("fedavg_fold", "fedavg_fold_ptrs", "fedavg_fold_raw", "fedavg_fold_host", "fedopt_step", "fedopt_step_raw")
+FOLD_OPS = ("fedavg_fold", "fedavg_fold_ptrs", "fedavg_fold_raw", "fedavg_fold_host", "fedopt_step", "fedopt_step_raw",
+            "fedopt_step_host")
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -197,7 +198,7 @@ def test_fedopt_server_step_failure_after_batch_refold_returns_none(monkeypatch)
     model, _ = agg.combine_models(helper=None)
     want, _ = ref.fedopt_combine(state, list(zip(ups, ns)), old)
     assert_lists_identical(model, want, "round 1")
-    for name in ("fedopt_step", "fedopt_step_raw"):
+    for name in ("fedopt_step", "fedopt_step_raw", "fedopt_step_host"):
         real = getattr(ops, name)
 
         def wrapper(*a, _real=real, **kw):

@@ -140,8 +140,9 @@ def test_fedopt_server_step_failure_returns_none_and_keeps_state(monkeypatch, sh
 
 
 def test_fedopt_zero_copy_step_failure_keeps_state(monkeypatch):
-    """A small round folded zero-copy (one fedopt_step_raw launch per group, staging.ZERO_COPY_BYTES)
-    that fails in round 2: ``(None, data)``, m / v stay round 1's, round 3 continues from them."""
+    """A small round folded zero-copy (the one-call step, smallround.py, then the pipeline's
+    fedopt_step_raw launch per group: staging.ZERO_COPY_BYTES) that fails in round 2: ``(None, data)``,
+    m / v stay round 1's, round 3 continues from them."""
     from fedn_amd import staging
     from fedn_amd.aggregators.fedopt import Aggregator
     from fedn_amd.updatehandler import MemoryUpdateHandler
@@ -157,6 +158,8 @@ def test_fedopt_zero_copy_step_failure_keeps_state(monkeypatch):
     # refolded into pg one at a time); the pseudo-gradient folds themselves succeed
     calls = _failing(monkeypatch, "fedopt_step_raw", lambda i, kw: fail[0] and kw.get("final"))
     _failing(monkeypatch, "fedopt_step", lambda i, kw: fail[0] and kw.get("final"))
+    # since round 6 a small round's first try is the one-call step (smallround.py, fedopt_step_host)
+    host_calls = _failing(monkeypatch, "fedopt_step_host", lambda i, kw: fail[0] and kw.get("final"))
     for r in range(3):
         fail[0] = r == 1
         ups = [[(o + 0.01 * rng.standard_normal(o.shape)).astype(o.dtype) for o in old] for _ in range(3)]
@@ -176,5 +179,6 @@ def test_fedopt_zero_copy_step_failure_keeps_state(monkeypatch):
         assert_lists_identical(agg.m, st.m, f"m r{r}")
         assert_lists_identical(agg.v, st.v, f"v r{r}")
         old = want
-    assert sum(1 for kw in calls if kw.get("final")) == 3     # every round took the zero-copy step first
+    assert sum(1 for kw in host_calls if kw.get("final")) == 3    # every round took the one-call step first
+    assert sum(1 for kw in calls if kw.get("final")) == 1         # round 2 then the general zero-copy step
     torch.cuda.synchronize()

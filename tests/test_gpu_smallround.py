@@ -176,3 +176,94 @@ def test_fold_host_refuses_pageable_memory():
     N = (ctypes.c_double * 2)(1.0, 2.0)
     rc = lib.fa_fedavg_fold_host(a.ctypes.data, _abi.FA_F32, ptrs, _abi.FA_F32, n, N, 2, 1024, 1, None)
     assert rc == _abi.FA_EINVAL and b"page-locked" in lib.fa_last_error()
+
+
+# ---------------------------------------------------------------- FedOpt (fedopt.py:74-121, 151-258)
+def _opt_agg():
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    uh = MemoryUpdateHandler()
+    return uh, get_aggregator("fedopt", uh)
+
+
+def _opt_spy(monkeypatch):
+    from fedn_amd import smallround
+    seen = {"small": 0, "general": 0}
+    real_step, real_general = smallround.SmallFedOptRound.server_step, smallround.SmallFedOptRound.general
+
+    def step(self, state, params):
+        seen["small"] += 1
+        return real_step(self, state, params)
+
+    def general(self):
+        seen["general"] += 1
+        return real_general(self)
+    monkeypatch.setattr(smallround.SmallFedOptRound, "server_step", step)
+    monkeypatch.setattr(smallround.SmallFedOptRound, "general", general)
+    return seen
+
+
+@pytest.mark.parametrize("opt", ["adam", "yogi", "adagrad"])
+@pytest.mark.parametrize("K", [1, 2, 5, 19])
+def test_small_fedopt_round_is_the_oracle(K, opt, monkeypatch):
+    """Three rounds of a session: fp32 clients over the fp32 global model, then over the float64 model
+    the previous round returned (FEDn stores FedOpt's float64 output as the next global model); m / v
+    carried in HBM, every round and the state bit-exact to the oracle."""
+    rng = np.random.default_rng(90 + K)
+    base = [rng.standard_normal(s).astype(np.float32) for s in MNIST]
+    params = {"serveropt": opt, "learning_rate": 1e-2, "beta1": 0.9, "beta2": 0.99, "tau": 1e-4}
+    uh, agg = _opt_agg()
+    seen = _opt_spy(monkeypatch)
+    st, old = ref.FedOptState(), base
+    for r in range(3):
+        ups = [[(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base] for _ in range(K)]
+        ns = [int(v) for v in rng.integers(1, 5001, K)]
+        gid = uh.put_global_model(old, f"g{r}")
+        for a, n in zip(ups, ns):
+            uh.submit(a, n, model_id=gid)
+        model, data = agg.combine_models(helper=None, parameters=params)
+        want, nr = ref.fedopt_combine(st, list(zip(ups, ns)), old, params)
+        assert data["nr_aggregated_models"] == nr == K
+        _same(model, want)
+        _same(agg.m, st.m)
+        _same(agg.v, st.v)
+        assert uh.model_updates.qsize() == 0 and list(uh.store.models) == [gid]
+        old = model                          # held by the caller: its block must not be reused
+    assert seen == {"small": 3, "general": 0}
+
+
+def test_small_fedopt_goes_general_on_another_layout(monkeypatch):
+    rng = np.random.default_rng(95)
+    base = [rng.standard_normal(s).astype(np.float32) for s in MNIST]
+    uh, agg = _opt_agg()
+    seen = _opt_spy(monkeypatch)
+    ups = [[(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base] for _ in range(4)]
+    ups[2] = [a.astype(np.float64) for a in ups[2]]               # numpy promotes from here on
+    ns = [int(v) for v in rng.integers(1, 5001, 4)]
+    gid = uh.put_global_model(base, "g0")
+    for a, n in zip(ups, ns):
+        uh.submit(a, n, model_id=gid)
+    model, data = agg.combine_models(helper=None)
+    st = ref.FedOptState()
+    want, nr = ref.fedopt_combine(st, list(zip(ups, ns)), base)
+    assert data["nr_aggregated_models"] == nr == 4
+    _same(model, want)
+    _same(agg.m, st.m)
+    assert seen["general"] == 1
+
+
+def test_fedopt_step_host_refuses_pageable_memory():
+    from fedn_amd import _abi
+    import ctypes
+    lib = _abi.load()
+    old = np.zeros(256, np.float32)
+    upd = np.ones(256, np.float32)
+    out = np.zeros(256, np.float64)
+    m = torch.empty(256, dtype=torch.float64, device="cuda:0")
+    v = torch.empty(256, dtype=torch.float64, device="cuda:0")
+    ptrs = (ctypes.c_void_p * 1)(upd.ctypes.data)
+    n = (ctypes.c_double * 1)(1.0)
+    rc = lib.fa_fedopt_step_host(old.ctypes.data, _abi.FA_F32, ptrs, _abi.FA_F32, n, n, 1, None, _abi.FA_NONE,
+                                 m.data_ptr(), _abi.FA_F64, None, _abi.FA_F64, v.data_ptr(), out.ctypes.data,
+                                 _abi.FA_F64, _abi.FA_ADAM, 1e-3, 0.9, 0.99, 1e-4, 256, None)
+    assert rc == _abi.FA_EINVAL and b"page-locked" in lib.fa_last_error()
