@@ -227,7 +227,7 @@ def test_small_fedopt_round_is_the_oracle(K, opt, monkeypatch):
         _same(model, want)
         _same(agg.m, st.m)
         _same(agg.v, st.v)
-        assert uh.model_updates.qsize() == 0 and list(uh.store.models) == [gid]
+        assert uh.model_updates.qsize() == 0 and all(k.startswith("g") for k in uh.store.models)   # updates deleted
         old = model                          # held by the caller: its block must not be reused
     assert seen == {"small": 3, "general": 0}
 
