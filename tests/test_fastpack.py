@@ -176,3 +176,63 @@ def test_start_pack_into_refuses_past_the_window():
         L.start_pack_into(lay, _model(np.random.default_rng(7), MNIST, ["f4"] * 6), buf.ctypes.data + 4,
                           (buf.ctypes.data, buf.nbytes))
     assert not buf.any()
+
+
+def test_views_rebuild_the_model_from_its_packed_block():
+    """_fastpack.views (the one-call round's result, smallround.py): every tensor a C-contiguous,
+    writable view of the block at its packed offset, keeping the block alive."""
+    import sys
+
+    from fedn_amd import _fastpack
+    rng = np.random.default_rng(3)
+    arrays = _model(rng, [(3, 5), (0,), (7,), (2, 3, 4), (1,)], ["f4"] * 5)
+    lay = Layout.of(arrays)
+    offs = {i: off for i, off, _ in lay.pack_plan}
+    plan = _fastpack.plan([(tuple(sh), np.dtype(dt), offs.get(i, 0)) for i, (sh, dt) in
+                           enumerate(zip(lay.shapes, lay.dtypes))])
+    block = _packed(lay, arrays)
+    before = sys.getrefcount(block)
+    views = _fastpack.views(plan, block)
+    assert sys.getrefcount(block) == before + len(arrays)        # each view holds the block
+    for v, a in zip(views, arrays):
+        assert v.dtype == a.dtype and v.shape == a.shape and v.flags.c_contiguous and v.flags.writeable
+        assert np.array_equal(v, a) and (v.size == 0 or v.base is block)
+    del views, v                                 # (the loop variable held the last view)
+    assert sys.getrefcount(block) == before
+    with pytest.raises(ValueError):                              # a block smaller than the plan
+        _fastpack.views(plan, block[:8].copy())
+
+
+def test_native_round_calls_refuse_bad_arguments():
+    """fold_host / fedopt_host check K and their addresses before any call (no GPU needed)."""
+    from fedn_amd import _fastpack
+    fp = _fastpack.fold_plan([(0, 0, 0, 16)])
+    with pytest.raises(ValueError):
+        _fastpack.fold_host(fp, 1, 0, 0, 4096, 64, 0, 4096, [], [], 0)          # K = 0
+    with pytest.raises(ValueError):
+        _fastpack.fold_host(fp, 1, 0, 0, 4096, 64, 65, 4096, [0.0] * 65, [1.0] * 65, 0)   # K > 64
+    with pytest.raises(ValueError):
+        _fastpack.fold_host(fp, 1, 0, 0, 4096, 64, 2, 4096, [0.0], [1.0, 2.0], 0)  # n / N lengths
+    with pytest.raises(ValueError):
+        _fastpack.fold_plan([(0, 0, -1, 16)])
+    state = (0, -1, 4096, 1, 0, 1, 4096, 1)
+    with pytest.raises(ValueError):
+        _fastpack.fedopt_host(1, 0, 0, 0, 4096, 64, 1, 0, 0, 16, 4096, [1.0], [1.0], 0, state, 0, 1e-3, 0.9, 0.99,
+                              1e-4)                                                    # old = NULL
+    with pytest.raises(ValueError):
+        _fastpack.fedopt_host(1, 0, 0, 4096, 4096, 64, 0, 0, 0, 16, 4096, [], [], 0, state, 0, 1e-3, 0.9, 0.99,
+                              1e-4)                                                    # K = 0
+
+
+def test_poison_knob_is_off_by_default_and_ignores_host_tensors():
+    import torch
+
+    from fedn_amd import reuse
+    assert not reuse.enabled()
+    t = torch.empty(16)
+    assert reuse.watch(t) is t and reuse.stats()["watched"] == 0
+    reuse.set_enabled(True)
+    try:
+        assert reuse.watch(t) is t and reuse.stats()["watched"] == 0   # host tensors are not watched
+    finally:
+        reuse.set_enabled(False)
