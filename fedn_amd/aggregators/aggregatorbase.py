@@ -248,6 +248,14 @@ class AggregatorBase(ABC):
                     self._log_skip(e, traceback.format_exc())   # (fedavg.py:73-78): logged, still counted
         return len(skipped)
 
+    def _queued(self):
+        """Updates still in the queue (0 if the handler's queue cannot say): with the one being folded,
+        the round's size as the small-round paths see it (smallround.py)."""
+        try:
+            return self.update_handler.model_updates.qsize()
+        except Exception:  # noqa: BLE001
+            return 0
+
     def _begin_deletes(self):
         """The round's store deletes may run side by side (ingest.StagingUpdateHandler.begin_deletes)
         until :meth:`_finish_deletes`."""

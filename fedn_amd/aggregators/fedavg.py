@@ -95,7 +95,7 @@ class Aggregator(AggregatorBase):
         on one device with numpyhelper's arithmetic; None: the general pipeline."""
         if self.devices or os.environ.get("FEDN_AMD_DEVICES") or helper_kind(helper) == "androidhelper":
             return None
-        return self._small.round(first, self.device or default_device())
+        return self._small.round(first, self.device or default_device(), 1 + self._queued())
 
     def _general(self, helper):
         return lambda first: make_fedavg_pipeline(first, self.device, self.devices, helper, self._staging)

@@ -79,7 +79,7 @@ class Aggregator(AggregatorBase):
         if self.devices or self.sharded:
             return None
         dev = self.device or default_device()
-        r = self._small.round(model_old, model_next, dev, self._pipeline)
+        r = self._small.round(model_old, model_next, dev, self._pipeline, 1 + self._queued())
         if r is not None and self.sharded is None:
             self.sharded = False                 # what _pipeline decides for a one-device session
             self.state = FedOptState(self.fp32_state)

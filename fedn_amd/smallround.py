@@ -243,12 +243,15 @@ class SmallSessions:
         self._by_key = {}
         self._last = None
 
-    def round(self, first, device):
-        """A SmallRound for ``first`` on ``device``, or None (not a list of arrays, not eligible)."""
+    def round(self, first, device, k_hint=1):
+        """A SmallRound for ``first`` on ``device``, or None (not a list of arrays, not eligible, or
+        ``k_hint`` — the round's update count as far as the queue shows it — more than the arena holds:
+        those rounds go the general way from the start instead of replaying into it part-way)."""
         if type(first) is not list or not first:
             return None
         last = self._last
-        if last is not None and last.device == device and last.cap * last.stride <= _zero_copy_bytes():
+        if (last is not None and last.device == device and last.cap * last.stride <= _zero_copy_bytes()
+                and k_hint <= last.cap):
             r = SmallRound.start(last, first)
             if r is not None:
                 return r
@@ -260,7 +263,7 @@ class SmallSessions:
         s = self._by_key.get(key)
         if s is not None and s.layout is not layout:   # a recycled id (Layout.of's cache was cleared)
             s = None
-        if not eligible(layout):
+        if not eligible(layout, k_hint) or k_hint > 64:
             return None
         if s is None or s.cap * s.stride > _zero_copy_bytes():
             s = SmallSession(device, layout)
@@ -333,7 +336,7 @@ class SmallFedOptSession:
         for ent in pool:
             if sys.getrefcount(ent[0]) == 2:     # no array of an earlier round views it any more
                 return ent[0]
-        t = torch.empty(self.P * torch.empty((), dtype=sdt).element_size(), dtype=torch.uint8, pin_memory=True)
+        t = torch.empty(self.P * ops.numpy_dtype(sdt).itemsize, dtype=torch.uint8, pin_memory=True)
         ent = (t.numpy(), t)
         if len(pool) < _POOL:
             pool.append(ent)
@@ -504,12 +507,14 @@ class SmallFedOptSessions:
         self._by_key = {}
         self._last = None
 
-    def round(self, old_arrays, first, device, make_pipeline):
+    def round(self, old_arrays, first, device, make_pipeline, k_hint=1):
+        """A SmallFedOptRound, or None (see SmallSessions.round; ``k_hint``: the round's update count as
+        far as the queue shows it)."""
         if type(first) is not list or not first or type(old_arrays) is not list:
             return None
         last = self._last
         if (last is not None and last.device == device and last.cap * last.stride <= _zero_copy_bytes()
-                and last.layout is _layout_of(first)):
+                and k_hint <= last.cap and last.layout is _layout_of(first)):
             r = SmallFedOptRound.start(last, old_arrays, first, make_pipeline)
             if r is not None:
                 return r
@@ -517,7 +522,7 @@ class SmallFedOptSessions:
             layout, old_layout = Layout.of(first), Layout.of(old_arrays)
         except Exception:  # noqa: BLE001
             return None
-        if not fedopt_eligible(layout, old_layout):
+        if not fedopt_eligible(layout, old_layout) or k_hint > 64 or k_hint * layout.nbytes > _zero_copy_bytes():
             return None
         key = (str(device), id(layout), id(old_layout))
         s = self._by_key.get(key)

@@ -85,6 +85,8 @@ def test_small_round_is_the_oracle(K, dtype, monkeypatch):
         assert uh.model_updates.qsize() == 0 and not uh.store.models    # every folded update deleted
     if K <= min(cap, 64):
         assert seen == {"small": 3, "general": 0}
+    else:                                    # the queue showed a round larger than the arena
+        assert seen == {"small": 0, "general": 0}
     if K == 1:
         assert model[0] is updates[0][0][0]  # the first update itself (fedavg.py:65-66)
 
@@ -135,18 +137,24 @@ def test_other_dtype_or_shape_goes_general_in_fifo_order(monkeypatch):
     assert list(uh.store.models) != []               # the skipped update stays in storage (fedavg.py:71-78)
 
 
-def test_more_updates_than_the_arena_goes_general(monkeypatch):
+@pytest.mark.parametrize("queue_visible", [True, False])
+def test_more_updates_than_the_arena_goes_general(monkeypatch, queue_visible):
+    """A round the queue shows to be larger than the arena goes the general way from its first update;
+    one whose updates outgrow the arena unseen (they arrived during the round) is handed over part-way,
+    its admitted updates replayed in order."""
     from fedn_amd import staging
     monkeypatch.setattr(staging, "ZERO_COPY_BYTES", 3 * 210_688)      # a 3-update arena for mnist
     rng = np.random.default_rng(6)
     ups = _models(rng, MNIST, 7)
     uh, agg = _agg()
     seen = _spy(agg, monkeypatch)
+    if not queue_visible:
+        monkeypatch.setattr(agg, "_queued", lambda: 0)
     model, data = _round(uh, agg, ups)
     want, nr = ref.fedavg_combine(ups)
     assert data["nr_aggregated_models"] == nr == 7
     _same(model, want)
-    assert seen["general"] == 1
+    assert seen == ({"small": 0, "general": 0} if queue_visible else {"small": 0, "general": 1})
 
 
 def test_failed_launch_recovers_through_the_general_path(monkeypatch):
