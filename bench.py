@@ -42,6 +42,10 @@ Also measured in the same run:
                 bit-exact check of a sample against the oracle and ``access_pattern``: the same
                 loads and stores with the arithmetic cut to adds (probe kernel k_fedopt_mix), the
                 HBM ceiling of the kernel's own traffic pattern
+  configs0      (N = 1) BASELINE configs[0]: the mnist-pytorch model's K = 2 round through the
+                plug-ins' combine_models (FedAvg and FedAdam, the one-call small rounds of
+                fedn_amd/smallround.py), median µs per round, bit-exact, beside FEDn's own loop
+                restated around the oracle's numpy arithmetic (its cpu_baseline)
 """
 import argparse
 import hashlib
@@ -370,6 +374,85 @@ def side(fn):
         return fn()
     except Exception as e:  # noqa: BLE001
         return {"error": f"{type(e).__name__}: {e}"}
+
+
+def configs0_side(device, rounds=300, warm=30):
+    """BASELINE configs[0]'s round (examples/mnist-pytorch: 52,650 fp32 params in 6 tensors, K = 2 host
+    numpy updates) through the plug-ins' combine_models (the one-call small rounds, fedn_amd/smallround.py),
+    FedAvg and FedAdam, median µs per round including the stand-in update handler's submit of both
+    updates — beside FEDn's own loop restated around the oracle's numpy arithmetic over the same
+    handler (tools/bench_small.py: fedavg.py:45-83, fedopt.py:74-121), the CPU baseline of this field.
+    Every plug-in round is checked bit-exact against the oracle."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_small
+    from fedn_amd.aggregators import get_aggregator
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    from oracle import numpy_ref as ref  # the checker and the CPU baseline only
+
+    rng = np.random.default_rng(0)
+    base = [rng.standard_normal(s).astype(np.float32) for s in bench_small.MNIST]
+    cl = [[(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base] for _ in range(2)]
+    ns = [int(v) for v in rng.integers(1, 5001, 2)]
+
+    def med(fn):
+        for _ in range(warm):
+            fn()
+        ts = []
+        for _ in range(rounds):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[len(ts) // 2] * 1e6
+
+    out, box = {}, {}
+    with torch.cuda.device(device):
+        uh = MemoryUpdateHandler()
+        agg = get_aggregator("fedavg", uh)
+
+        def avg():
+            for u, n in zip(cl, ns):
+                uh.submit(u, n)
+            box["avg"], _ = agg.combine_models(helper=None)
+        out["fedavg_us"] = med(avg)
+        want, _ = ref.fedavg_combine(list(zip(cl, ns)))
+        out["fedavg_bit_exact"] = bench_small.same(box["avg"], want)
+        uh2 = MemoryUpdateHandler()
+        gid = uh2.put_global_model(base, "g0")
+        opt = get_aggregator("fedopt", uh2)
+        st = ref.FedOptState()
+
+        def fedadam():
+            for u, n in zip(cl, ns):
+                uh2.submit(u, n, model_id=gid)
+            box["opt"], _ = opt.combine_models(helper=None, parameters=bench_small.PARAMS)
+        fedadam()                           # round 1 (m / v None), then the steady state is timed
+        ref.fedopt_combine(st, list(zip(cl, ns)), base, bench_small.PARAMS)
+        out["fedadam_us"] = med(fedadam)
+        for _ in range(warm + rounds):      # the oracle's session over the same rounds
+            want_o, _ = ref.fedopt_combine(st, list(zip(cl, ns)), base, bench_small.PARAMS)
+        ok = bench_small.same(box["opt"], want_o)
+        out["fedadam_bit_exact"] = ok
+    uh3 = MemoryUpdateHandler()
+
+    def loop_avg():
+        for u, n in zip(cl, ns):
+            uh3.submit(u, n)
+        bench_small.fedn_loop_fedavg(uh3)
+    uh4 = MemoryUpdateHandler()
+    gid4 = uh4.put_global_model(base, "g0")
+    st4 = ref.FedOptState()
+
+    def loop_opt():
+        for u, n in zip(cl, ns):
+            uh4.submit(u, n, model_id=gid4)
+        bench_small.fedn_loop_fedopt(uh4, st4, bench_small.PARAMS)
+    out["cpu_baseline"] = {"fedavg_us": med(loop_avg), "fedadam_us": med(loop_opt), "unit": "us per round",
+                           "cores": 1, "kind": "port",
+                           "sample": "FEDn's combine_models loop restated (tools/bench_small.py) around "
+                                     "oracle/numpy_ref's numpyhelper arithmetic, the same handler and updates"}
+    out["unit"] = "us per round (median, incl. the handler's submit of both updates)"
+    out["config"] = "BASELINE configs[0]: mnist-pytorch (52,650 fp32 params, 6 tensors), 2 host numpy updates"
+    return out
 
 
 def fold_kernel_label(P, in_bytes, K, ran=None):
@@ -970,6 +1053,8 @@ def main():
         if rank == 0 and a.fedopt_params > 0:
             extra["fedopt"] = side(lambda: fedopt_side(a.fedopt_params, a.fedopt_clients, device,
                                                        pattern_probe=not a.no_side))
+        if rank == 0 and not a.no_side:
+            extra["configs0"] = side(lambda: configs0_side(device))
 
     if rank == 0:
         line = {
