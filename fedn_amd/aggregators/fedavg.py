@@ -59,16 +59,21 @@ def make_fedavg_pipeline(first, device=None, devices=None, helper=None, cache=No
 _HIP_SEEN = False      # torch.cuda.is_available() was True once in this process (it stays so)
 
 
+_DEVICES = {}          # torch.device per (FEDN_AMD_DEVICE, current device): built once, not per round
+
+
 def default_device():
     global _HIP_SEEN
-    dev = os.environ.get("FEDN_AMD_DEVICE")
-    if dev:
-        return torch.device(dev)
-    if not _HIP_SEEN:
+    env = os.environ.get("FEDN_AMD_DEVICE")
+    if not env and not _HIP_SEEN:
         if not torch.cuda.is_available():
             raise RuntimeError("fedn_amd aggregators need a HIP device (torch.cuda.is_available() is False)")
         _HIP_SEEN = True
-    return torch.device("cuda", torch.cuda.current_device())
+    key = env or torch.cuda.current_device()
+    dev = _DEVICES.get(key)
+    if dev is None:
+        dev = _DEVICES[key] = torch.device(env) if env else torch.device("cuda", key)
+    return dev
 
 
 class Aggregator(AggregatorBase):

@@ -7,7 +7,8 @@ hands the block to the next allocation on the WRITER's stream at once, and a new
 before the read. Whether that corrupts a round is a matter of timing, so a test can pass by luck.
 
 With the knob on, every buffer registered with :func:`watch` (the staging allocations of ingest.py,
-upload.py, staging.py, multidev.py, mixed.py) is watched: the moment its tensor is freed, a poison
+upload.py, staging.py, multidev.py, mixed.py) is watched: the moment its storage is freed (the tensor
+and every view of it dropped), a poison
 thread allocates blocks of the same size on the same stream until the allocator hands it that very
 block (or 0.3 ms pass) and fills it with 0xFF bytes — a NaN in every float dtype — on that stream. A
 buffer still read by an enqueued launch and not protected (held until the reader ran, or
@@ -27,7 +28,7 @@ ENABLED = os.environ.get("FEDN_AMD_POISON_REUSE", "") == "1"
 RETRY_S = 300e-6   # an unprotected block comes back at once; a protected one is safe whenever it does
 
 _q = queue.Queue()
-_stats = {"watched": 0, "poisoned": 0, "not_reissued": 0}
+_stats = {"watched": 0, "poisoned": 0, "not_reissued": 0, "poisoned_bytes": 0, "freed_bytes": 0}
 _lock = threading.Lock()
 _thread = None
 
@@ -49,8 +50,8 @@ def watch(t, stream=None):
         return t
     global _thread
     stream = stream if stream is not None else torch.cuda.current_stream(t.device)
-    nbytes = t.untyped_storage().nbytes()
-    weakref.finalize(t, _q.put, (t.untyped_storage().data_ptr(), nbytes, t.device, stream))
+    st = t.untyped_storage()           # its PyObject lives as long as the storage: views keep it too
+    weakref.finalize(st, _q.put, (st.data_ptr(), st.nbytes(), t.device, stream))
     with _lock:
         _stats["watched"] += 1
         if _thread is None:
@@ -74,15 +75,21 @@ def _poison(ptr, nbytes, device, stream):
     with torch.cuda.device(device), torch.cuda.stream(stream):
         while True:
             b = torch.empty(nbytes, dtype=torch.uint8, device=device)
-            if b.data_ptr() == ptr:
-                b.fill_(0xFF)            # on the writer's stream, as its next H2D would land
+            # the allocator may hand the block back merged with a free neighbour (a block split at
+            # another offset): whatever part of the freed range it returns is poisoned
+            lo, hi = max(ptr, b.data_ptr()), min(ptr + nbytes, b.data_ptr() + nbytes)
+            if lo < hi:
+                b[lo - b.data_ptr():hi - b.data_ptr()].fill_(0xFF)   # on the writer's stream, as its next H2D
                 with _lock:
                     _stats["poisoned"] += 1
+                    _stats["poisoned_bytes"] += hi - lo
+                    _stats["freed_bytes"] += nbytes
                 return
             held.append(b)
             if len(held) >= 64 or time.perf_counter() > deadline:
                 with _lock:
                     _stats["not_reissued"] += 1
+                    _stats["freed_bytes"] += nbytes
                 return
             if len(held) % 8 == 0:
                 held.clear()             # give the block time to come back (its free may still run)
