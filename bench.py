@@ -288,11 +288,12 @@ def fedopt_waves_side(a, devs, sample=1_000_000):
     outs = wf.round(ups, ns, old, params)
     t = time.perf_counter() - t0
     # per-kernel rooflines: the same round again with HIP events around every launch (round 1 of a
-    # session: FINAL reads old + pg, writes m / v / out; waves read 8 bf16 updates + f64 old and
-    # write the f64 pg workspace, later waves also read it)
+    # session: waves read 8 bf16 updates + f64 old and write the f64 pg workspace, later waves also
+    # read it; the last wave reads it and writes m / v / out instead, the server step fused)
     spans = {}
     WaveFedOpt(devs, P, wave=8).round(ups, ns, old, params, kernel_times=spans)
-    per_el = {"first": lambda k: 2 * k + 16, "mid": lambda k: 2 * k + 24, "final": lambda k: 40}
+    per_el = {"first": lambda k: 2 * k + 16, "mid": lambda k: 2 * k + 24, "final": lambda k: 40,
+              "mid_final": lambda k: 2 * k + 40, "first_final": lambda k: 2 * k + 32}
     kern = {}
     for kind, rows in spans.items():
         ms = sum(r[3] for r in rows) / len(rows)
@@ -303,10 +304,16 @@ def fedopt_waves_side(a, devs, sample=1_000_000):
                                    "frac": b / ms / 1e6 / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc},
                       "kernel": {"first": "k_fedopt_c<bf16, double, CF64, FIRST, !FINAL>",
                                  "mid": "k_fedopt_c<bf16, double, CF64, !FIRST, !FINAL>",
-                                 "final": "k_fedopt_c<bf16, double, CF64, !FIRST, FINAL> (K = 0 server step)"}[kind],
+                                 "final": "k_fedopt_c<bf16, double, CF64, !FIRST, FINAL> (K = 0 server step)",
+                                 "mid_final": "k_fedopt_c<bf16, double, CF64, !FIRST, FINAL> (last wave + server step)",
+                                 "first_final": "k_fedopt_c<bf16, double, CF64, FIRST, FINAL> (one wave)"}[kind],
                       "bytes_per_element": {"first": "2W + 16 (W bf16 updates, f64 old, f64 pg written)",
                                             "mid": "2W + 24 (W bf16 updates, f64 old, f64 pg read + written)",
-                                            "final": "40 (f64 old + pg read; f64 m / v / out written)"}[kind]}
+                                            "final": "40 (f64 old + pg read; f64 m / v / out written)",
+                                            "mid_final": "2W + 40 (W bf16 updates, f64 old + pg read; f64 m / v / "
+                                                         "out written)",
+                                            "first_final": "2W + 32 (W bf16 updates, f64 old read; f64 m / v / out "
+                                                           "written)"}[kind]}
     res = wf.gather(outs)
     S = min(sample, P)
     want, _ = ref.fedopt_combine(ref.FedOptState(), [([ups[k][:S].float().numpy()], n) for k, n in enumerate(ns)],

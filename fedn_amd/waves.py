@@ -8,9 +8,11 @@ flat buffer each, e.g. decoded by the streaming ingest) go to the devices W at a
 copies ONLY its parameter slice [lo_d, hi_d) of every update over its own PCIe link (one copy
 stream per device, two wave buffers: the H2D of wave i+1 overlaps the fold of wave i), folds the
 wave into its slice of the running pseudo-gradient (``fa_fedopt_step`` without FINAL keeps pg in
-HBM; FIRST on the first wave), and after the last wave runs the server step on its slice
-(K = 0, FINAL) with its slices of old / m / v resident. Every element sees the same client order
-and the same kernel, so the result is bit-identical for any device count and any wave size.
+HBM; FIRST on the first wave), and the last wave's launch also runs the server step on its slice
+(FINAL) with its slices of old / m / v resident, so pg makes no last HBM round trip and no K = 0
+launch follows (``fuse_final=False`` keeps the separate K = 0 FINAL launch, for A/B). Every element
+sees the same client order and the same kernel arithmetic, so the result is bit-identical for any
+device count, any wave size and either finish.
 """
 import numpy as np
 import torch
@@ -23,12 +25,13 @@ class WaveFedOpt:
     """One session's FedOpt state sliced over ``devices`` (a list; a device may repeat, e.g. on a
     one-GPU box), for P-element flat models whose updates stream from host memory."""
 
-    def __init__(self, devices, P, wave=8):
+    def __init__(self, devices, P, wave=8, fuse_final=True):
         self.devices = [torch.device(d) for d in devices]
         self.devices = [torch.device(d.type, torch.cuda.current_device()) if d.index is None else d
                         for d in self.devices]
         self.P = P
         self.wave = wave
+        self.fuse_final = fuse_final
         self.bounds = shard_bounds(P, len(self.devices))
         self.m = [None] * len(self.devices)
         self.v = [None] * len(self.devices)
@@ -41,8 +44,10 @@ class WaveFedOpt:
         tensor per device slice (``old[d]`` on device d, any dtype fa_fedopt_step takes).
         Returns the new model as per-device f64 slices; m / v stay on the devices.
         ``kernel_times``: a dict to receive, per launch kind ("first" wave, later "mid" waves, the
-        "final" server step), the list of (device, elements, clients, ms) of every launch (HIP
-        events on the launch stream) — bench.py's per-kernel rooflines."""
+        last wave with the server step fused, "mid_final" or "first_final" when it is the only one;
+        "final", the K = 0 server step, with ``fuse_final=False``), the list of (device, elements,
+        clients, ms) of every launch (HIP events on the launch stream) — bench.py's per-kernel
+        rooflines."""
         K = len(host_updates)
         if K == 0:
             raise ValueError("no updates")
@@ -65,14 +70,24 @@ class WaveFedOpt:
             with torch.cuda.device(dv):
                 n = hi - lo
                 pg_dt, m_dt = ops.fedopt_dtypes(upd_dt, old[d].dtype, None if self.m[d] is None else self.m[d].dtype)
-                slots = [[reuse.watch(torch.empty(n, dtype=upd_dt, device=dv)) for _ in range(W)] for _ in range(2)]
+                slots = [[reuse.watch(torch.empty(n, dtype=upd_dt, device=dv)) for _ in range(min(W, K))]
+                         for _ in range(2)]
                 ctx.append({"n": n, "slots": slots, "pg": torch.empty(n, dtype=pg_dt, device=dv), "m_dt": m_dt,
                             "loaded": [torch.cuda.Event() for _ in range(2)],
                             "used": [torch.cuda.Event() for _ in range(2)]})
         waves = (K + W - 1) // W
+        opt = dict(serveropt=params.get("serveropt", "adam"), learning_rate=params.get("learning_rate", 1e-3),
+                   beta1=params.get("beta1", 0.9), beta2=params.get("beta2", 0.99), tau=params.get("tau", 1e-4))
+        for d, dv in enumerate(self.devices):
+            c = ctx[d]
+            with torch.cuda.device(dv):
+                c["m_out"] = torch.empty(c["n"], dtype=c["m_dt"], device=dv)
+                c["v_out"] = self.v[d] if self.v[d] is not None else torch.empty(c["n"], dtype=torch.float64, device=dv)
+                c["out"] = torch.empty(c["n"], dtype=torch.float64, device=dv)
         for w in range(waves):                       # every device's wave w, then wave w + 1, ...
             b = w % 2
             ks = list(range(w * W, min(K, (w + 1) * W)))
+            last = self.fuse_final and w == waves - 1
             for d, dv in enumerate(self.devices):
                 lo, hi = self.bounds[d]
                 c = ctx[d]
@@ -87,26 +102,27 @@ class WaveFedOpt:
                         c["loaded"][b].record(self.copy[d])
                     self.compute[d].wait_event(c["loaded"][b])
                     ev = self._span(kernel_times, d)
-                    ops.fedopt_step(old[d], c["slots"][b][:len(ks)], [ns[k] for k in ks], [Ns[k] for k in ks],
-                                    first=(w == 0), final=False, pg=c["pg"], stream=self.compute[d])
-                    self._end(kernel_times, "first" if w == 0 else "mid", d, ev, c["n"], len(ks))
+                    if last:                                  # the last wave folds and steps in one launch
+                        ops.fedopt_step(old[d], c["slots"][b][:len(ks)], [ns[k] for k in ks], [Ns[k] for k in ks],
+                                        first=(w == 0), final=True, pg=c["pg"], m_in=self.m[d], m_out=c["m_out"],
+                                        v_in=self.v[d], v_out=c["v_out"], out=c["out"], stream=self.compute[d], **opt)
+                    else:
+                        ops.fedopt_step(old[d], c["slots"][b][:len(ks)], [ns[k] for k in ks], [Ns[k] for k in ks],
+                                        first=(w == 0), final=False, pg=c["pg"], stream=self.compute[d])
+                    self._end(kernel_times, ("first" if w == 0 else "mid") + ("_final" if last else ""), d, ev,
+                              c["n"], len(ks))
                     c["used"][b].record(self.compute[d])
         for d, dv in enumerate(self.devices):
             c = ctx[d]
             with torch.cuda.device(dv):
-                m_out = torch.empty(c["n"], dtype=c["m_dt"], device=dv)
-                v_out = self.v[d] if self.v[d] is not None else torch.empty(c["n"], dtype=torch.float64, device=dv)
-                out = torch.empty(c["n"], dtype=torch.float64, device=dv)
-                if c["n"]:
+                if c["n"] and not self.fuse_final:
                     ev = self._span(kernel_times, d)
-                    ops.fedopt_step(old[d], [], [], [], first=False, final=True, pg=c["pg"], m_in=self.m[d], m_out=m_out,
-                                    v_in=self.v[d], v_out=v_out, out=out, serveropt=params.get("serveropt", "adam"),
-                                    learning_rate=params.get("learning_rate", 1e-3), beta1=params.get("beta1", 0.9),
-                                    beta2=params.get("beta2", 0.99), tau=params.get("tau", 1e-4),
-                                    stream=self.compute[d], upd_dtype=upd_dt)
+                    ops.fedopt_step(old[d], [], [], [], first=False, final=True, pg=c["pg"], m_in=self.m[d],
+                                    m_out=c["m_out"], v_in=self.v[d], v_out=c["v_out"], out=c["out"],
+                                    stream=self.compute[d], upd_dtype=upd_dt, **opt)
                     self._end(kernel_times, "final", d, ev, c["n"], 0)
-                self.m[d], self.v[d] = m_out, v_out
-                outs.append(out)
+                self.m[d], self.v[d] = c["m_out"], c["v_out"]
+                outs.append(c["out"])
         for d, dv in enumerate(self.devices):
             torch.cuda.synchronize(dv)
         if kernel_times is not None:

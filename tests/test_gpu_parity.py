@@ -1306,18 +1306,21 @@ def test_staging_ingest_fortran_member_falls_back(ndev):
 
 
 # ------------------------------------------------------------------------- configs[4]: waves from host
-@pytest.mark.parametrize("ndev", [1, 2, 3])
-def test_fedopt_bf16_waves_two_rounds(ndev):
+@pytest.mark.parametrize("ndev,W,fuse", [(1, 8, True), (2, 8, True), (3, 8, True), (2, 8, False), (2, 16, True),
+                                          (2, 64, False), (1, 256, True)])
+def test_fedopt_bf16_waves_two_rounds(ndev, W, fuse):
     """BASELINE configs[4] shape at 1 M params: bf16 updates streamed from pinned host memory in
-    waves of 8 (FA_PG_FIRST wave, non-final waves, then a K = 0 FA_PG_FINAL server step), FedYogi,
-    K = 130 (two 64-client kernel tables per wave boundary crossing included), two rounds with m / v
-    carried, sliced over 1-3 devices: bit-exact to the oracle run on the exact f32 upcasts."""
+    waves of W (FA_PG_FIRST wave, non-final waves, the last wave with FA_PG_FINAL fused; or, with
+    ``fuse`` off, a separate K = 0 FA_PG_FINAL server step; W = 256 > K: one FIRST | FINAL wave),
+    FedYogi, K = 130 (a 2-update last wave at W = 8 / 16 / 64; two 64-client kernel tables in a
+    W = 256 wave), two rounds with m / v carried, sliced over 1-3 devices: bit-exact to the oracle
+    run on the exact f32 upcasts."""
     from fedn_amd.waves import WaveFedOpt
-    P, K, W = 1_000_003, 130, 8
+    P, K = 1_000_003, 130
     g = torch.Generator().manual_seed(55)
     old = torch.randn(P, generator=g).numpy()                  # round-1 global model, float32
     params = {"serveropt": "yogi", "learning_rate": 1e-2}
-    wf = WaveFedOpt([DEV] * ndev, P, wave=W)
+    wf = WaveFedOpt([DEV] * ndev, P, wave=W, fuse_final=fuse)
     state = ref.FedOptState()
     old_np = old
     for r in range(2):

@@ -105,7 +105,10 @@ X_SESSION = [
     ("pmcx_f32state", f"fedopt_adam_steady_f32state_k32_p{Q}", "k_fedopt_cw<float, float", Q * (4 * 32 + 24)),
     ("pmcx_waves", "fedyogi_wave_first_p1000000000_w8_bf16", (WAVE_BF16 + "true, false,",), 1_000_000_000 * (2 * 8 + 16)),
     ("pmcx_waves", "fedyogi_wave_mid_p1000000000_w8_bf16", (WAVE_BF16 + "false, false,",), 1_000_000_000 * (2 * 8 + 24)),
-    ("pmcx_waves", "fedyogi_wave_final_p1000000000_w8_bf16", (WAVE_BF16 + "false, true,",), 1_000_000_000 * 40),
+    ("pmcx_waves", "fedyogi_wave_final_p1000000000_w8_bf16", (WAVE_BF16 + "false, true,",), 1_000_000_000 * 40, (0, 3)),
+    # the fused last wave (8 bf16 updates, f64 old + pg read; f64 m / v / out written): dispatches 3..5
+    ("pmcx_waves", "fedyogi_wave_mid_final_p1000000000_w8_bf16", (WAVE_BF16 + "false, true,",),
+     1_000_000_000 * (2 * 8 + 40), (3, 6)),
 ]
 
 
@@ -160,8 +163,8 @@ def main():
                 record_rank(sys.argv[2], world)
         return
     if sys.argv[1] == "--x-session":
-        for sub, key, kernel, alg in X_SESSION:
-            record(os.path.join(sys.argv[2], sub), key, kernel, alg, session=sys.argv[2])
+        for sub, key, kernel, alg, *take in X_SESSION:
+            record(os.path.join(sys.argv[2], sub), key, kernel, alg, session=sys.argv[2], take=take[0] if take else None)
         return
     if sys.argv[1] == "--session":
         for sub, key, kernel, alg, *take in SESSION:

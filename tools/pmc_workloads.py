@@ -6,7 +6,9 @@ tools/pmc_traffic.py --x-session turns the passes into profiles/pmc_traffic.json
              k_fedopt_c<float, float, CF32, FIRST, FINAL> (the same instantiation as round 1)
   waves      configs[4]'s three wave kernels on one device (1 B bf16 params, waves of 8, FedYogi,
              round 1 of a session as bench.py's fedopt_waves times them): FIRST wave, a later wave,
-             the K = 0 FINAL server step — device-resident here (the PCIe copies are not measured)
+             the K = 0 FINAL server step, the last wave with FINAL fused (the same instantiation as
+             the K = 0 step: its dispatches come after those) — device-resident here (the PCIe copies
+             are not measured)
 """
 import argparse
 import os
@@ -54,6 +56,9 @@ def waves(steps):
     for _ in range(steps):
         ops.fedopt_step(old, [], [], [], first=False, final=True, pg=pg, m_out=m, v_out=v, out=out,
                         serveropt="yogi", upd_dtype=torch.bfloat16)
+    for _ in range(steps):     # the last wave with the server step fused (the same instantiation, K = 8)
+        ops.fedopt_step(old, ups, ns, [N + Ns[-1] for N in Ns], first=False, final=True, pg=pg, m_out=m, v_out=v,
+                        out=out, serveropt="yogi")
     torch.cuda.synchronize()
 
 
