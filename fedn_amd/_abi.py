@@ -29,7 +29,8 @@ FA_PG_FIRST, FA_PG_FINAL = 1, 2
  FA_TUNE_BLOCK, FA_TUNE_SUM_NOSTORE, FA_TUNE_NT_STORE, FA_TUNE_FASTDIV64, FA_TUNE_TILEMAP, FA_TUNE_OPT_NT,
  FA_TUNE_OPT_NOSTORE, FA_TUNE_OPT_STORE, FA_TUNE_OPT_COAL, FA_TUNE_NARROW, FA_TUNE_LDS, FA_TUNE_WPE, FA_TUNE_OPT_MV, FA_TUNE_AUTO_GEOM,
  FA_TUNE_OPT_MIX, FA_TUNE_OPT_BURST, FA_TUNE_OPT_G, FA_TUNE_OPT_WIN_PERIOD, FA_TUNE_OPT_WIN_W, FA_TUNE_OPT_WIN_MODE,
- FA_TUNE_AVG_WIN_PERIOD, FA_TUNE_AVG_WIN_W, FA_TUNE_AVG_WIN_MODE, FA_TUNE_OPT_WIN_PROD) = range(31)
+ FA_TUNE_AVG_WIN_PERIOD, FA_TUNE_AVG_WIN_W, FA_TUNE_AVG_WIN_MODE, FA_TUNE_OPT_WIN_PROD,
+ FA_TUNE_OPT_QUAD) = range(32)
 
 EXPORTS = {
     # name: (restype, argtypes)

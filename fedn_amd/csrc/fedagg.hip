@@ -1079,19 +1079,21 @@ __device__ __forceinline__ void fedopt_strip(const OptBuffers& b, const OptScala
 // owns the pairs {2L, 2L+1} + 128 j, j < NH, so every 8-byte stream (old, m, v, pg, out) moves one
 // contiguous 1 KiB per wave instruction (full 128-B lines, no half-line stores) and the client loads
 // are contiguous 512-B dwordx2 wave instructions. Whole wave tiles only.
+// H (probe builds only, FA_TUNE_OPT_QUAD): elements per lane per strip — 2 (the product: pairs) or 4
+// (quads at lane stride 4: 2-byte client loads become dwordx2, 8-byte streams two dwordx4 per strip).
 template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM = 0, int NH = 2,
-          int U = kUnroll / 2, bool WIN = false>
+          int U = kUnroll / 2, bool WIN = false, int H = 2>
 __device__ __forceinline__ void fedopt_strip_split(const OptBuffers& b, const OptScalars& s,
                                                    const ClientTable<typename PG::S>& tab, const int K,
                                                    const int64_t i0, const uint32_t period = 0,
                                                    const uint32_t win_w = 0) {
     using V = typename PG::V;
-    constexpr int H = 2, E = H * NH;
+    constexpr int E = H * NH;
     auto half = [](auto& a, int h) -> auto& {
         using T = std::remove_reference_t<decltype(a[0])>;
         return *reinterpret_cast<T(*)[H]>(&a[h * H]);
     };
-    auto at = [i0](int h) { return i0 + (int64_t)h * 128; };
+    auto at = [i0](int h) { return i0 + (int64_t)h * 64 * H; };
     OLD old[E];
 #pragma unroll
     for (int h = 0; h < NH; ++h) strip_load<OLD, H, false>(static_cast<const OLD*>(b.old) + at(h), half(old, h));
@@ -1428,6 +1430,26 @@ k_fedopt_cwp(const OptBuffers b, const OptScalars s, const ClientTable<typename 
 #endif
 
 #ifdef FEDAGG_PROBES
+// element-map probe (FA_TUNE_OPT_QUAD): k_fedopt_c's 512-element wave tiles with lane L owning the
+// quads {4L .. 4L+3} + 256 j, j < 2, instead of the pairs {2L, 2L+1} + 128 j, j < 4. Same elements
+// per lane, same arithmetic per element: bit-identical. 2-byte client loads widen from one dword to
+// one dwordx2 per strip; the 8-byte streams (old, pg, m, v, out) take two dwordx4 per strip.
+template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedopt_cq(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
+    const int64_t base = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 512;
+    const int lane = threadIdx.x & 63;
+    if (base + 512 <= P) {
+        fedopt_strip_split<Y, OLD, PG, FIRST, FINAL, NT, 1, 2, kUnroll / 2, false, 4>(b, s, tab, K, base + 4 * lane);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int64_t i0 = base + j * 256 + 4 * lane;
+            if (i0 < P) fedopt_strip<Y, OLD, PG, 4, FIRST, FINAL, NT, false, 1>(b, s, tab, K, P, i0);
+        }
+    }
+}
+
 template <typename Y, typename OLD, class PG, bool FIRST, bool FINAL, bool NT, int OSM, int NH, int U, int W>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W)))
 k_fedopt_c_w(const OptBuffers b, const OptScalars s, const ClientTable<typename PG::S> tab, const int K, const int64_t P) {
@@ -1948,7 +1970,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 #ifdef FEDAGG_PROBES
 struct FedAvgCfg {
     std::atomic<int> strips{4}, unroll{0}, lanetab{0}, grid_per_cu{0}, read_per_lane{16}, block_log{8},
-        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0}, opt_burst{0}, opt_g{0}, opt_win_period{0}, opt_win_w{0}, opt_win_mode{0}, avg_win_period{0}, avg_win_w{0}, avg_win_mode{0}, opt_win_prod{0};
+        sum_nostore{0}, nt_store{1}, nt{0}, tilemap{0}, fastdiv{1}, fastdiv64{1}, opt_nt{1}, opt_nostore{0}, opt_store{0}, opt_coal{2}, narrow{1}, lds_kib{0}, wpe{0}, opt_mv{0}, auto_geom{1}, opt_mix{0}, opt_burst{0}, opt_g{0}, opt_win_period{0}, opt_win_w{0}, opt_win_mode{0}, avg_win_period{0}, avg_win_w{0}, avg_win_mode{0}, opt_win_prod{0}, opt_quad{0};
 };
 FedAvgCfg g_cfg;
 int cfg_fastdiv() { return g_cfg.fastdiv.load(std::memory_order_relaxed); }
@@ -2364,6 +2386,16 @@ int launch_fedopt_one(const OptBuffers& b, const OptScalars& s, const ClientTabl
         // fp16 updates: one dword per pair)
         const dim3 g4((unsigned)((P + 4 * 512 - 1) / (4 * 512)));
 #ifdef FEDAGG_PROBES
+        if constexpr (std::is_same<Y, bf16>::value && std::is_same<OLD, double>::value && std::is_same<PG, CF64>::value) {
+            if (g_cfg.opt_quad) {                    // configs[4]'s wave kernels with the quad element map
+                g_kernel = "k_fedopt_cq";
+                if (first && final_) hipLaunchKernelGGL((k_fedopt_cq<Y, OLD, PG, true, true, NT>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+                else if (first) hipLaunchKernelGGL((k_fedopt_cq<Y, OLD, PG, true, false, NT>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+                else if (final_) hipLaunchKernelGGL((k_fedopt_cq<Y, OLD, PG, false, true, NT>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+                else hipLaunchKernelGGL((k_fedopt_cq<Y, OLD, PG, false, false, NT>), g4, dim3(kBlock), 0, st, b, s, tab, cnt, P);
+                return check_launch("fa_fedopt_step: kernel launch");
+            }
+        }
         const unsigned shm = (unsigned)g_cfg.lds_kib * 1024u;
         if constexpr (probe_combo) {
         if (first && final_ && g_cfg.opt_mv) {
@@ -3246,6 +3278,9 @@ int fa_tune(int knob, int value) {
             if (value < 0 || value > 3)
                 return fail(FA_EINVAL, "fa_tune: OPT_WIN_PROD 0 (pattern probe), 1 (k_fedopt_cw), 2 (k_fedopt_cgw), 3 (k_fedopt_cw2)");
             g_cfg.opt_win_prod = value;
+            return FA_OK;
+        case FA_TUNE_OPT_QUAD:
+            g_cfg.opt_quad = value ? 1 : 0;
             return FA_OK;
         case FA_TUNE_AVG_WIN_PERIOD:
             if (value != 0 && value != -1 && (value < 64 || value > (1 << 24)))

@@ -410,7 +410,8 @@ _KNOBS = {"strips": _abi.FA_TUNE_STRIPS, "unroll": _abi.FA_TUNE_UNROLL, "nt": _a
           "opt_g": _abi.FA_TUNE_OPT_G, "opt_win_period": _abi.FA_TUNE_OPT_WIN_PERIOD, "opt_win_w": _abi.FA_TUNE_OPT_WIN_W,
           "opt_win_mode": _abi.FA_TUNE_OPT_WIN_MODE, "avg_win_period": _abi.FA_TUNE_AVG_WIN_PERIOD,
           "avg_win_w": _abi.FA_TUNE_AVG_WIN_W, "avg_win_mode": _abi.FA_TUNE_AVG_WIN_MODE,
-          "opt_win_prod": _abi.FA_TUNE_OPT_WIN_PROD}
+          "opt_win_prod": _abi.FA_TUNE_OPT_WIN_PROD,
+          "opt_quad": _abi.FA_TUNE_OPT_QUAD}
 
 
 def tune(**knobs):

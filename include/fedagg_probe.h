@@ -96,7 +96,10 @@ enum fa_tune_knob { FA_TUNE_STRIPS = 0, FA_TUNE_UNROLL = 1, FA_TUNE_NT = 2, FA_T
                     FA_TUNE_AVG_WIN_MODE = 29,
                     FA_TUNE_OPT_WIN_PROD = 30 /* 1: OPT_WIN_PERIOD / _W apply to the product step (k_fedopt_cw,
                                                  bit-identical) instead of the pattern probe; OPT_WIN_PERIOD 0 =
-                                                 the product's own window (opt_store_window), -1 = none */ };
+                                                 the product's own window (opt_store_window), -1 = none */,
+                    FA_TUNE_OPT_QUAD = 31 /* FedOpt over bf16 updates, fp64 old, fp64 pg (configs[4]'s waves):
+                                             1 = k_fedopt_cq, lane L owning 4-element quads at lane stride 4
+                                             (dwordx2 client loads) instead of the product's pairs */ };
 int fa_tune(int knob, int value);
 int64_t fa_stream_read_blocks(int64_t bytes);
 int fa_stream_read(const void* src, int64_t bytes, void* sink, void* stream);
