@@ -67,7 +67,7 @@ def _entry_points():
 def eligible(layout, K_hint=2):
     """Whether a round over ``layout`` can take the one-call path: float16/32/64 tensors only (numpy's
     fold keeps their dtype, so the result block has the arena's layout), and at least two updates
-    (the first and one more) fit the arena."""
+    (the first and one more) fit the arena (a layout is never 0 bytes: groups are 256-B aligned)."""
     zc = _zero_copy_bytes()
     return (all(dt in _FOLDABLE for dt in layout.groups) and max(2, K_hint) * layout.nbytes <= zc
             and bool(_entry_points()))
@@ -349,10 +349,12 @@ class SmallFedOptSession:
         return self._fp.views(plan, block)
 
     def state_pair(self, m_dt, sdt, m_in, v_in):
-        """HBM buffers for the new m / v: a pair the state does not hold."""
+        """HBM buffers for the new m / v: a pair whose memory the state does not hold (compared by
+        address: the state may hold a view of a pair buffer rather than the buffer object)."""
         pairs = self.pairs.setdefault((m_dt, sdt), [])
+        held = {t.data_ptr() for t in (m_in, v_in) if t is not None and t.numel()}
         for m, v in pairs:
-            if m is not m_in and v is not v_in:
+            if m.data_ptr() not in held and v.data_ptr() not in held:
                 return m, v
         with torch.cuda.device(self.device):
             pair = (torch.empty(self.P, dtype=m_dt, device=self.device), torch.empty(self.P, dtype=sdt, device=self.device))

@@ -275,3 +275,37 @@ def test_fedopt_step_host_refuses_pageable_memory():
                                  m.data_ptr(), _abi.FA_F64, None, _abi.FA_F64, v.data_ptr(), out.ctypes.data,
                                  _abi.FA_F64, _abi.FA_ADAM, 1e-3, 0.9, 0.99, 1e-4, 256, None)
     assert rc == _abi.FA_EINVAL and b"page-locked" in lib.fa_last_error()
+
+
+@pytest.mark.parametrize("shapes", [[(0,), (3, 0)], [(0,), (64,), (0, 5), (10,)]], ids=["all_empty", "some_empty"])
+def test_empty_tensors_fedavg_and_fedopt(shapes, monkeypatch):
+    """Zero-size tensors through the one-call way: a model of only empty tensors (a 0-element fold, the
+    layout's 256-B minimum arena slot) and one with empty tensors among others, FedAvg and FedOpt, two
+    rounds each: the oracle's bits, shapes and dtypes."""
+    rng = np.random.default_rng(11)
+    seen = _spy(None, monkeypatch)
+    uh, agg = _agg()
+    for _ in range(2):
+        updates = _models(rng, shapes, 3)
+        model, data = _round(uh, agg, updates)
+        want, nr = ref.fedavg_combine(updates)
+        assert data["nr_aggregated_models"] == nr == 3
+        _same(model, want)
+    assert seen == {"small": 2, "general": 0}
+    oseen = _opt_spy(monkeypatch)
+    uh, agg = _opt_agg()
+    st = ref.FedOptState()
+    old = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    for r in range(2):
+        ups = _models(rng, shapes, 3)
+        gid = uh.put_global_model(old, f"g{r}")
+        for a, n in ups:
+            uh.submit(a, n, model_id=gid)
+        model, data = agg.combine_models(helper=None)
+        want, nr = ref.fedopt_combine(st, ups, old)
+        assert data["nr_aggregated_models"] == nr == 3
+        _same(model, want)
+        _same(agg.m, st.m)
+        _same(agg.v, st.v)
+        old = model
+    assert oseen == {"small": 2, "general": 0}
