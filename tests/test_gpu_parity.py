@@ -1337,6 +1337,37 @@ def test_fedopt_bf16_waves_two_rounds(ndev, W, fuse):
         old_np = want[0]
 
 
+@pytest.mark.parametrize("fuse", [True, False])
+@pytest.mark.parametrize("opt", ["adam", "adagrad"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+def test_fedopt_waves_dtypes_three_rounds(dtype, opt, fuse):
+    """The wave path for every client dtype the kernel takes (fp32 / fp16 / bf16 updates over a
+    float32 first global model, then the float64 models FEDn stores), Adam and AdaGrad, with and
+    without the server step fused into the last wave; waves of 4 over K = 19 (a 3-update last wave),
+    P = 100,003 (a ragged last tile), two slices, three rounds with m / v carried: the oracle's bits
+    on the exact f32 upcasts of the updates."""
+    from fedn_amd.waves import WaveFedOpt
+    P, K = 100_003, 19
+    g = torch.Generator().manual_seed(71)
+    old_np = torch.randn(P, generator=g).numpy()
+    params = {"serveropt": opt, "learning_rate": 1e-2}
+    wf = WaveFedOpt([DEV, DEV], P, wave=4, fuse_final=fuse)
+    state = ref.FedOptState()
+    for r in range(3):
+        base = torch.from_numpy(np.asarray(old_np, dtype=np.float32))
+        host = [(base + 0.01 * torch.randn(P, generator=g)).to(dtype).pin_memory() for _ in range(K)]
+        ns = [int(v) for v in np.random.default_rng(r + 7).integers(1, 5001, K)]
+        outs = wf.round(host, ns, wf.slices(torch.from_numpy(np.asarray(old_np))), params)
+        got = wf.gather(outs).numpy()
+        ups = [([h.float().numpy() if dtype == torch.bfloat16 else h.numpy()], n) for h, n in zip(host, ns)]
+        want, nr = ref.fedopt_combine(state, ups, [old_np], params)
+        assert nr == K
+        assert_lists_identical([got], want, f"round {r} {dtype} {opt} fuse={fuse}")
+        assert_lists_identical([wf.gather(wf.m).numpy()], state.m, f"round {r} m")
+        assert_lists_identical([wf.gather(wf.v).numpy()], state.v, f"round {r} v")
+        old_np = want[0]
+
+
 # ------------------------------------------------------------------------- N > 1 with the HIP kernel
 def _hip_gloo_worker(rank, world, port, P, K, q):
     import os
