@@ -186,6 +186,17 @@ def main():
     s = io.StringIO()
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(30)
     print(s.getvalue())
+    # the FedOpt plug-in's host work, by own time and by cumulative time
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(300):
+        plugin_opt()
+    pr.disable()
+    for key in ("tottime", "cumulative"):
+        s = io.StringIO()
+        pstats.Stats(pr, stream=s).sort_stats(key).print_stats(35)
+        print(f"# FedOpt plug-in, by {key}")
+        print(s.getvalue())
 
 
 if __name__ == "__main__":
