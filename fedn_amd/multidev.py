@@ -223,6 +223,10 @@ class _ShardedStaging:
                          for _ in range(self.nslots)]
             self.dslots = [[_DevSlot(self.dev_bytes[d], self.devices[d]) for _ in range(self.nslots)]
                            for d in range(len(self.devices))]
+            # fresh HBM from each compute stream's pool: its previous owners' queued work there runs
+            # before the copy streams' H2D overwrite it (staging._Pipeline.stage)
+            for d in range(len(self.devices)):
+                self.copy[d].wait_stream(self.compute[d])
 
     def _dev_view(self, d, slot, dt):
         lo, hi = self.bounds[dt][d]
@@ -716,6 +720,7 @@ class ShardedFedOptPipeline(_ShardedStaging):
                 lo, hi = self.bounds[dt][d]
                 per[dt] = torch.empty(hi - lo, dtype=ops.torch_dtype(odt), device=dv)
             self.old.append(per)
+            self.copy[d].wait_stream(self.compute[d])   # see _ensure_slots
         self.old_ready = set()
         self.streamer = HostStreamer()
         self.pg = [dict() for _ in self.devices]

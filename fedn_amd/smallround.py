@@ -279,9 +279,15 @@ class SmallSessions:
 class SmallFedOptSession:
     """The per-(device, update layout, global-model layout) resources of a FedOpt session's small rounds:
     a pinned block for the global model (packed on the round's first update, fedopt.py:89-90), the
-    updates' arena, admission plans for both, a stream, pinned result blocks per state dtype, and two
-    pairs of HBM buffers per (m, v) dtype the server step writes in turn — the pair the session's state
-    does not hold, so a step that fails leaves the state as the last round left it (fedopt.py:36-38)."""
+    updates' arena, admission plans for both, pinned result blocks per state dtype, and two pairs of HBM
+    buffers per (m, v) dtype the server step writes in turn — the pair the session's state does not
+    hold, so a step that fails leaves the state as the last round left it (fedopt.py:36-38).
+
+    Unlike FedAvg's one-call fold (host memory only), the step reads and writes HBM that torch's
+    streams also use — m / v from a general round or a regroup copy, and the pair buffers, which the
+    caching allocator hands out in the order of the device's current stream (a block freed there may
+    still have queued writes from its previous owner) — so it runs on that current stream, ordered
+    after them, never on a private one."""
 
     def __init__(self, device, layout, old_layout):
         fp, _, gstart, self._wait, self._fn = _entry_points()
@@ -300,9 +306,6 @@ class SmallFedOptSession:
         self.old_ptr = self.old.data_ptr()
         self.plan = self._plan(layout, self.dt)
         self.old_plan = self._plan(old_layout, self.odt)
-        with torch.cuda.device(self.device):
-            self.stream = torch.cuda.Stream(self.device)
-        self.stream_ptr = self.stream.cuda_stream
         self.out_plans = {}                  # state dtype -> views plan of the new model
         self.blocks = {}                     # state dtype -> [(uint8 numpy block, torch tensor)]
         self.pairs = {}                      # (m dtype, state dtype) -> [(m, v) HBM buffers]
@@ -452,8 +455,8 @@ class SmallFedOptRound:
         st = (ptr(m_in), _abi.FA_NONE if m_in is None else fa(m_in), ptr(m_out), fa(m_out), ptr(v_in),
               _abi.FA_F64 if v_in is None else fa(v_in), ptr(v_out), fa(sdt))
         ticket, self.ticket = self.ticket, None
-        fp, fn, wait, old, arena, stride, K, P, stream = (s._fp, s._fn, s._wait, s.old_ptr, s.arena_ptr, s.stride,
-                                                           len(self.ns), s.P, s.stream_ptr)
+        fp, fn, wait, old, arena, stride, K, P = s._fp, s._fn, s._wait, s.old_ptr, s.arena_ptr, s.stride, len(self.ns), s.P
+        stream = torch.cuda.current_stream(s.device).cuda_stream      # see SmallFedOptSession
         upd_fa, old_fa, out = fa(ops.torch_dtype(dt)), fa(old_t), block.ctypes.data
         args = (ops._OPTS[opt], float(params["learning_rate"]), float(params["beta1"]), float(params["beta2"]),
                 float(params["tau"]))

@@ -301,6 +301,10 @@ class _Pipeline:
         if s.used:
             s.h2d_done.synchronize()            # pinned bytes no longer read by the DMA
             self.copy.wait_event(s.consumed)    # device bytes no longer read by a fold
+        else:
+            # a fresh slot's HBM came from the compute stream's pool: its previous owner's queued work
+            # there must run before this stream's H2D overwrites it
+            self.copy.wait_stream(self.compute)
         self._copy_used = True
         tic = time.perf_counter()
         nb = self.layout.nbytes
@@ -1198,6 +1202,8 @@ class FedOptPipeline(_Pipeline):
         # chunk by chunk inside the server step's pipeline (H2D || step || D2H)
         self.old = {dt: torch.empty(layout.group_elems[dt], dtype=ops.torch_dtype(odt), device=self.device)
                     for dt, (odt, _) in self.old_host.items()}
+        if self.old:
+            self.copy.wait_stream(self.compute)  # their HBM's previous owners' queued work first (stage())
 
     def _pg_meta(self):
         """(shape, dtype) per tensor of the pseudo-gradient folded so far (fused layout)."""

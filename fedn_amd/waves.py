@@ -84,6 +84,9 @@ class WaveFedOpt:
                 c["m_out"] = torch.empty(c["n"], dtype=c["m_dt"], device=dv)
                 c["v_out"] = self.v[d] if self.v[d] is not None else torch.empty(c["n"], dtype=torch.float64, device=dv)
                 c["out"] = torch.empty(c["n"], dtype=torch.float64, device=dv)
+                # the slots' HBM came from the compute stream's pool: its previous owners' queued work
+                # there runs before the copy stream's first H2D overwrites it
+                self.copy[d].wait_stream(self.compute[d])
         for w in range(waves):                       # every device's wave w, then wave w + 1, ...
             b = w % 2
             ks = list(range(w * W, min(K, (w + 1) * W)))
