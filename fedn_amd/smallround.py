@@ -293,6 +293,7 @@ class SmallFedOptSession:
         fp, _, gstart, self._wait, self._fn = _entry_points()
         self._fp, self._gstart = fp, gstart
         self.device = torch.device(device)
+        self.dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self.layout, self.old_layout = layout, old_layout
         (self.dt,) = layout.groups
         (self.odt,) = old_layout.groups
@@ -456,7 +457,7 @@ class SmallFedOptRound:
               _abi.FA_F64 if v_in is None else fa(v_in), ptr(v_out), fa(sdt))
         ticket, self.ticket = self.ticket, None
         fp, fn, wait, old, arena, stride, K, P = s._fp, s._fn, s._wait, s.old_ptr, s.arena_ptr, s.stride, len(self.ns), s.P
-        stream = torch.cuda.current_stream(s.device).cuda_stream      # see SmallFedOptSession
+        stream = torch._C._cuda_getCurrentRawStream(s.dev_index)      # the current stream: see SmallFedOptSession
         upd_fa, old_fa, out = fa(ops.torch_dtype(dt)), fa(old_t), block.ctypes.data
         args = (ops._OPTS[opt], float(params["learning_rate"]), float(params["beta1"]), float(params["beta2"]),
                 float(params["tau"]))
