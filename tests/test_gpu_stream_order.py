@@ -31,15 +31,17 @@ def _gpu():
 
 
 def _busy_then_zero_fills(nbytes, count=16, folds=200):
-    """Queue ~tens of ms of folds on the current stream, then ``count`` blocks of ``nbytes`` zero-filled
-    behind them, and free the blocks (their fills still queued)."""
+    """Queue ~tens of ms of folds on the current stream, then ``count`` blocks of ``nbytes`` (an int or
+    a list of sizes, ``count`` of each) zero-filled behind them, and free the blocks (their fills still
+    queued)."""
     from fedn_amd import ops
     P = 50_000_000
     ups = [torch.ones(P, device=DEV) for _ in range(8)]
     agg = torch.empty(P, device=DEV)
     for _ in range(folds):
         ops.fedavg_fold(agg, ups, [1] * 8, list(range(1, 9)), init=True)
-    blocks = [torch.empty(nbytes, dtype=torch.uint8, device=DEV) for _ in range(count)]
+    sizes = nbytes if isinstance(nbytes, (list, tuple)) else [nbytes]
+    blocks = [torch.empty(nb, dtype=torch.uint8, device=DEV) for nb in sizes for _ in range(count)]
     for b in blocks:
         b.zero_()
     del blocks
@@ -104,4 +106,60 @@ def test_staging_slot_first_h2d_after_queued_work_on_its_block():
     want, nr = ref.fedavg_combine(ups)
     assert data["nr_aggregated_models"] == nr == 4
     _same(model, want, "model")
+    del keep
+
+
+def test_multidevice_slots_and_global_model_after_queued_work():
+    """The same for the pipelines sliced over several devices (multidev.py, two slices on this GPU):
+    FedAvg's per-device slots, then FedOpt's per-device global-model buffers."""
+    from fedn_amd.aggregators import fedavg, fedopt
+    from fedn_amd.layout import Layout
+    from fedn_amd.updatehandler import MemoryUpdateHandler
+    rng = np.random.default_rng(7)
+    shapes = [(1000, 2000), (2000,)]
+    base = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    ups = [([(b + 0.01 * rng.standard_normal(b.shape)).astype(np.float32) for b in base], int(n))
+           for n in rng.integers(1, 5001, 4)]
+    bounds, _, dev_bytes = Layout.of(ups[0][0]).shard_geometry(2)
+    old_bytes = sorted({(hi - lo) * 4 for lo, hi in bounds[np.dtype(np.float32)]})   # FedOpt's float32 global model
+    uh = MemoryUpdateHandler()
+    agg = fedavg.Aggregator(uh, devices=[DEV, DEV])
+    for a, n in ups:
+        uh.submit(a, n)
+    keep = _busy_then_zero_fills(sorted(set(dev_bytes)), count=8)
+    model, data = agg.combine_models(helper=None)
+    want, nr = ref.fedavg_combine(ups)
+    assert data["nr_aggregated_models"] == nr == 4
+    _same(model, want, "fedavg model")
+    del keep
+    uh = MemoryUpdateHandler()
+    agg = fedopt.Aggregator(uh, devices=[DEV, DEV])
+    gid = uh.put_global_model(base, "g0")
+    for a, n in ups:
+        uh.submit(a, n, model_id=gid)
+    keep = _busy_then_zero_fills(old_bytes + sorted(set(dev_bytes)), count=8)
+    model, data = agg.combine_models(helper=None)
+    st = ref.FedOptState()
+    want, nr = ref.fedopt_combine(st, ups, base)
+    assert data["nr_aggregated_models"] == nr == 4
+    _same(model, want, "fedopt model")
+    del keep
+
+
+def test_wave_slots_first_h2d_after_queued_work():
+    """configs[4]'s wave slots (allocated on the compute stream, first written by the copy stream)."""
+    from fedn_amd.waves import WaveFedOpt
+    P, K = 1_000_003, 12
+    g = torch.Generator().manual_seed(9)
+    base = torch.randn(P, generator=g)
+    host = [(base + 0.01 * torch.randn(P, generator=g)).to(torch.bfloat16).pin_memory() for _ in range(K)]
+    ns = [int(v) for v in np.random.default_rng(9).integers(1, 5001, K)]
+    wf = WaveFedOpt([DEV], P, wave=4)
+    old = wf.slices(base)
+    keep = _busy_then_zero_fills(P * 2, count=12)
+    outs = wf.round(host, ns, old, {"serveropt": "yogi"})
+    got = wf.gather(outs).numpy()
+    want, _ = ref.fedopt_combine(ref.FedOptState(), [([h.float().numpy()], n) for h, n in zip(host, ns)],
+                                 [base.numpy()], {"serveropt": "yogi"})
+    _same([got], want, "waves")
     del keep

@@ -36,10 +36,14 @@ def main():
     finally:
         torch._C._cuda_getCurrentRawStream = real
     out["slot_h2d_with_wait"] = run(t.test_staging_slot_first_h2d_after_queued_work_on_its_block)
+    out["multidev_with_wait"] = run(t.test_multidevice_slots_and_global_model_after_queued_work)
+    out["waves_with_wait"] = run(t.test_wave_slots_first_h2d_after_queued_work)
     real_wait = torch.cuda.Stream.wait_stream
     torch.cuda.Stream.wait_stream = lambda self, other: None                # no copy-stream wait
     try:
         out["slot_h2d_without_wait"] = run(t.test_staging_slot_first_h2d_after_queued_work_on_its_block)
+        out["multidev_without_wait"] = run(t.test_multidevice_slots_and_global_model_after_queued_work)
+        out["waves_without_wait"] = run(t.test_wave_slots_first_h2d_after_queued_work)
     finally:
         torch.cuda.Stream.wait_stream = real_wait
     torch.cuda.synchronize()
