@@ -26,6 +26,10 @@ import torch
 
 ENABLED = os.environ.get("FEDN_AMD_POISON_REUSE", "") == "1"
 RETRY_S = 300e-6   # an unprotected block comes back at once; a protected one is safe whenever it does
+# FEDN_AMD_POISON_HOLD=1: keep every same-size block the allocator offers first until the freed one comes
+# back (more of them are reached; the default returns them every 8 tries), at most HOLD_BYTES
+HOLD = os.environ.get("FEDN_AMD_POISON_HOLD", "") == "1"
+HOLD_BYTES = 8 << 30
 
 _q = queue.Queue()
 _stats = {"watched": 0, "poisoned": 0, "not_reissued": 0, "poisoned_bytes": 0, "freed_bytes": 0}
@@ -86,13 +90,14 @@ def _poison(ptr, nbytes, device, stream):
                     _stats["freed_bytes"] += nbytes
                 return
             held.append(b)
-            if len(held) >= 64 or time.perf_counter() > deadline:
+            if len(held) >= 64 or (HOLD and len(held) * nbytes > HOLD_BYTES) or time.perf_counter() > deadline:
                 with _lock:
                     _stats["not_reissued"] += 1
                     _stats["freed_bytes"] += nbytes
                 return
             if len(held) % 8 == 0:
-                held.clear()             # give the block time to come back (its free may still run)
+                if not HOLD:
+                    held.clear()         # give the block time to come back (its free may still run)
                 time.sleep(20e-6)
 
 

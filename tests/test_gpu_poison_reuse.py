@@ -23,7 +23,9 @@ def _knob():
     was = reuse.enabled()
     reuse.set_enabled(True)
     reuse.drain()                      # earlier tests' frees (a knob-on suite run) handled first
-    yield reuse
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()           # and their cached free blocks returned: no same-size block the
+    yield reuse                        # allocator could offer before the dropped one
     reuse.drain()
     reuse.set_enabled(was)
 
